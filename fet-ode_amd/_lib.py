@@ -1,0 +1,147 @@
+"""ctypes binding of libfetode.so (the C ABI in include/fetode.h).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950).  There is
+no fallback: if the library or a GPU is missing, every compute entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FETODE_LIB", os.path.join(_HERE, "libfetode.so"))
+
+FETODE_OK, FETODE_EINVAL, FETODE_EUNSUPPORTED, FETODE_EHIP = 0, 1, 2, 3
+EULER, MIDPOINT, RK4, RK4_CLASSIC = 0, 1, 2, 3
+
+_vp = ctypes.c_void_p
+_fp = ctypes.c_void_p  # device float* passed as raw address
+
+
+class KANLinearDesc(ctypes.Structure):
+    _fields_ = [
+        ("in_features", ctypes.c_int32), ("out_features", ctypes.c_int32),
+        ("grid_size", ctypes.c_int32), ("spline_order", ctypes.c_int32),
+        ("num_logistic", ctypes.c_int32), ("base_act", ctypes.c_int32),
+        ("grid", _fp), ("base_weight", _fp), ("spline_weight", _fp), ("spline_scaler", _fp),
+        ("logistic_a", _fp), ("logistic_b", _fp), ("logistic_weight", _fp),
+        ("logistic_scaler", _fp), ("scale_logistic", ctypes.c_float),
+    ]
+
+
+class FerroDesc(ctypes.Structure):
+    _fields_ = [
+        ("in_dim", ctypes.c_int32), ("out_dim", ctypes.c_int32), ("num_basis", ctypes.c_int32),
+        ("k", _fp), ("Ec", _fp), ("Ps", _fp), ("bias", _fp), ("coef", _fp),
+        ("gate_slope", ctypes.c_double), ("alpha", ctypes.c_double),
+        ("branch_sign", _fp), ("branch_sign_bstride", ctypes.c_int64),
+    ]
+
+
+class FieldDesc(ctypes.Structure):
+    _fields_ = [
+        ("n_layers", ctypes.c_int32),
+        ("kan", ctypes.POINTER(KANLinearDesc)),
+        ("ferro", ctypes.POINTER(FerroDesc)),
+    ]
+
+
+# exported symbol -> (restype, argtypes); mirrors include/fetode.h one to one
+SIGNATURES = {
+    "fetode_last_error": (ctypes.c_char_p, []),
+    "fetode_abi_version": (ctypes.c_int, []),
+    "fetode_plan_bytes": (ctypes.c_int64, [ctypes.POINTER(FieldDesc)]),
+    "fetode_plan_build": (ctypes.c_int, [ctypes.POINTER(FieldDesc), _vp, _vp]),
+    "fetode_state_width": (ctypes.c_int32, [ctypes.POINTER(FieldDesc)]),
+    "fetode_fused_supported": (ctypes.c_int, [ctypes.POINTER(FieldDesc)]),
+    "fetode_field_forward": (ctypes.c_int, [ctypes.POINTER(FieldDesc), _vp, _vp, ctypes.c_int64, _vp,
+                                            ctypes.c_uint32, _vp, _vp]),
+    "fetode_integrate_fixed": (ctypes.c_int, [ctypes.POINTER(FieldDesc), _vp, ctypes.c_int32, _vp,
+                                              ctypes.c_int64, _vp, ctypes.c_int32, _vp, _vp, _vp,
+                                              ctypes.c_int32, _vp, _vp, ctypes.c_uint32, _vp, _vp]),
+    "fetode_kanlinear_forward": (ctypes.c_int, [ctypes.POINTER(KANLinearDesc), _vp, ctypes.c_int64, _vp, _vp]),
+    "fetode_kanlinear_bsplines": (ctypes.c_int, [ctypes.POINTER(KANLinearDesc), _vp, ctypes.c_int64, _vp, _vp]),
+    "fetode_ferro_forward": (ctypes.c_int, [ctypes.POINTER(FerroDesc), _vp, ctypes.c_int64, _vp, ctypes.c_int32,
+                                            ctypes.c_int32, _vp, _vp, _vp, _vp]),
+    "fetode_rk_combine": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp,
+                                         ctypes.c_float, _vp, ctypes.c_int64, _vp]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+_load_error: Optional[str] = None
+
+
+class FetodeError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load libfetode.so (once).  Raises if it is absent: there is no CPU fallback."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FetodeError(f"libfetode.so not found at {LIB_PATH}; run __graft_entry__.build()")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.fetode_abi_version() != 1:
+        raise FetodeError("libfetode ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != FETODE_OK:
+        msg = load().fetode_last_error().decode(errors="replace")
+        if rc == FETODE_EINVAL:
+            raise ValueError(f"{what}: {msg}")
+        if rc == FETODE_EUNSUPPORTED:
+            raise NotImplementedError(f"{what}: {msg}")
+        raise FetodeError(f"{what}: {msg} (code {rc})")
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def require_gpu_tensor(x: torch.Tensor, what: str):
+    if not x.is_cuda:
+        raise RuntimeError(f"{what}: fet_ode_amd computes on the MI355X (HIP) only; got a {x.device} "
+                           "tensor. Move the module and inputs to 'cuda'.")
+    if x.dtype != torch.float32:
+        raise TypeError(f"{what}: expected float32, got {x.dtype}")
+
+
+def f32c(t: torch.Tensor) -> torch.Tensor:
+    """fp32 contiguous view/copy for passing to the ABI."""
+    return t.detach().to(torch.float32).contiguous()
+
+
+class FieldHandle:
+    """Keeps the ctypes descriptors (and the tensors they point to) alive for one call."""
+
+    def __init__(self, kan_descs: Sequence[KANLinearDesc], ferro_descs: Optional[Sequence[FerroDesc]],
+                 keep: List[torch.Tensor]):
+        n = len(kan_descs)
+        self._kan = (KANLinearDesc * n)(*kan_descs)
+        self._ferro = (FerroDesc * n)(*ferro_descs) if ferro_descs is not None else None
+        self.desc = FieldDesc(n, ctypes.cast(self._kan, ctypes.POINTER(KANLinearDesc)),
+                              ctypes.cast(self._ferro, ctypes.POINTER(FerroDesc)) if self._ferro is not None
+                              else ctypes.POINTER(FerroDesc)())
+        self.keep = keep
+
+    @property
+    def ref(self):
+        return ctypes.byref(self.desc)

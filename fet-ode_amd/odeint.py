@@ -1,0 +1,269 @@
+"""torchdiffeq-compatible ``odeint`` on the MI355X (drop-in for ``from torchdiffeq import odeint``).
+
+Reference call sites: train_kanfet_node_predprey.py:252,260 (default method => dopri5),
+predator_prey.py:142,149, train_ecg_kan_fet_nn_ode.py:558-565 (dopri5, rtol/atol).
+torchdiffeq itself is not vendored in the reference; the semantics follow its
+published algorithm (FixedGridODESolver.integrate, rk_common.rk4_alt_step_func,
+RKAdaptiveStepsizeODESolver + Dopri5Solver), including the call order of ``func`` — which
+matters because the hysteresis basis is stateful (ferro_class.py:409).
+
+Two execution paths, both HIP:
+  * fused: ``func`` is ``fet_ode_amd.autonomous(field)`` (or ``field.as_ode_func()``) for a
+    KAN / KANFET shape with a fused kernel and a fixed-grid method -> the whole solve is one
+    kernel launch (``fetode_integrate_fixed``).
+  * per-stage: any other callable -> ``func`` is called stage by stage exactly like
+    torchdiffeq, and the stage combines run as HIP kernels (``fetode_rk_combine``).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from .autograd_ops import build_plan, field_layers, make_handle, pack_state, unpack_state
+
+FIXED_METHODS = {"euler": _lib.EULER, "midpoint": _lib.MIDPOINT, "rk4": _lib.RK4,
+                 "rk4_classic": _lib.RK4_CLASSIC}
+SOLVERS = tuple(FIXED_METHODS) + ("dopri5",)
+
+
+# ---------------------------------------------------------------------------------------------
+# input checks (torchdiffeq misc._check_inputs)
+# ---------------------------------------------------------------------------------------------
+
+def _check_inputs(y0, t, method):
+    if not isinstance(y0, torch.Tensor):
+        raise NotImplementedError("tupled y0 is not on the hot path; pass a single tensor")
+    if not torch.is_floating_point(y0):
+        raise TypeError("`y0` must be a floating point Tensor but is a {}".format(y0.type()))
+    if method is None:
+        method = "dopri5"
+    if method not in SOLVERS:
+        raise ValueError('Invalid method "{}". Must be one of {}'.format(
+            method, '{"' + '", "'.join(SOLVERS) + '"}.'))
+    t = torch.as_tensor(t)
+    assert t.dim() == 1, "t must be one dimensional"
+    assert not t.requires_grad, "gradients w.r.t. t are not supported"
+    tc = t.detach().cpu()
+    if not torch.is_floating_point(tc):
+        tc = tc.to(torch.get_default_dtype())
+    reversed_ = len(tc) > 1 and bool(tc[0] > tc[1])
+    tp = -tc if reversed_ else tc
+    assert bool((tp[1:] > tp[:-1]).all()), "t must be strictly increasing or decreasing"
+    return method, tc, tp, reversed_
+
+
+# ---------------------------------------------------------------------------------------------
+# fixed-grid schedule (FixedGridODESolver.integrate), computed on the host in t's dtype
+# ---------------------------------------------------------------------------------------------
+
+class Schedule:
+    __slots__ = ("step_coef", "out_step", "out_mode", "out_slope", "n_steps", "T", "grid", "dev")
+
+    def __init__(self, tp: torch.Tensor, step_size, reversed_: bool):
+        if step_size is None:
+            grid = tp
+        else:
+            niters = torch.ceil((tp[-1] - tp[0]) / step_size + 1).item()
+            grid = torch.arange(0, niters, dtype=tp.dtype) * step_size + tp[0]
+            grid[-1] = tp[-1]
+        assert grid[0] == tp[0] and grid[-1] == tp[-1]
+        g = grid.numpy()
+        n = len(g) - 1
+        sign = -1.0 if reversed_ else 1.0
+        dt = (g[1:] - g[:-1])                     # time dtype arithmetic
+        coef = np.zeros((n, 4), dtype=np.float32)
+        coef[:, 0] = (sign * dt).astype(np.float32)
+        coef[:, 1] = (sign * (0.5 * dt)).astype(np.float32)
+        coef[:, 2] = (sign * (dt / 6.0)).astype(np.float32)
+        T = len(tp)
+        tt = tp.numpy()
+        out_step = np.zeros(T, dtype=np.int32)
+        out_mode = np.zeros(T, dtype=np.int32)
+        out_slope = np.zeros(T, dtype=np.float32)
+        j = 1
+        for s in range(n):
+            t0, t1 = g[s], g[s + 1]
+            while j < T and t1 >= tt[j]:
+                out_step[j] = s
+                if tt[j] == t0:
+                    out_mode[j] = 0
+                elif tt[j] == t1:
+                    out_mode[j] = 1
+                else:
+                    out_mode[j] = 2
+                    out_slope[j] = np.float32((tt[j] - t0) / (t1 - t0))
+                j += 1
+        self.step_coef, self.out_step, self.out_mode, self.out_slope = coef, out_step, out_mode, out_slope
+        self.n_steps, self.T, self.grid = n, T, g
+        self.dev: Dict[torch.device, Tuple[torch.Tensor, ...]] = {}
+
+    def device_arrays(self, device):
+        """One async H2D upload per device, cached."""
+        if device not in self.dev:
+            n, T = self.n_steps, self.T
+            buf = torch.empty(4 * n + 3 * T, dtype=torch.float32, pin_memory=True)
+            buf[:4 * n] = torch.from_numpy(self.step_coef.reshape(-1))
+            buf[4 * n:4 * n + T] = torch.from_numpy(self.out_step.view(np.float32))
+            buf[4 * n + T:4 * n + 2 * T] = torch.from_numpy(self.out_mode.view(np.float32))
+            buf[4 * n + 2 * T:] = torch.from_numpy(self.out_slope)
+            d = buf.to(device, non_blocking=True)
+            self.dev[device] = (d, d[:4 * n], d[4 * n:4 * n + T], d[4 * n + T:4 * n + 2 * T], d[4 * n + 2 * T:])
+        return self.dev[device]
+
+
+_SCHED_CACHE: Dict[tuple, Schedule] = {}
+
+
+def get_schedule(tp, step_size, reversed_) -> Schedule:
+    key = (tp.dtype, tuple(tp.tolist()), step_size, reversed_)
+    s = _SCHED_CACHE.get(key)
+    if s is None:
+        if len(_SCHED_CACHE) > 64:
+            _SCHED_CACHE.clear()
+        s = _SCHED_CACHE[key] = Schedule(tp, step_size, reversed_)
+    return s
+
+
+# ---------------------------------------------------------------------------------------------
+# fused path
+# ---------------------------------------------------------------------------------------------
+
+class _FusedFixedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, field, handle, method, y0, sched, *params):
+        dev = y0.device
+        B, D = y0.shape
+        lib = _lib.load()
+        plan = build_plan(field, handle, dev)
+        state, mask = pack_state(field, B, dev)
+        _, coef, ostep, omode, oslope = sched.device_arrays(dev)
+        sol = torch.empty(sched.T, B, D, device=dev, dtype=torch.float32)
+        _lib.check(lib.fetode_integrate_fixed(
+            handle.ref, plan.data_ptr(), method, y0.data_ptr(), B, coef.data_ptr(), sched.n_steps,
+            ostep.data_ptr(), omode.data_ptr(), oslope.data_ptr(), sched.T, sol.data_ptr(),
+            _lib.ptr(state), mask, None, _lib.stream_handle(dev)), "fetode_integrate_fixed")
+        if state is not None:
+            unpack_state(field, state)
+        return sol
+
+    @staticmethod
+    def backward(ctx, grad):
+        raise NotImplementedError("backward through the fused solve is not built yet")
+
+
+def fused_field(func):
+    """The KAN/KANFET module behind ``func`` if it was tagged by ``autonomous``."""
+    return getattr(func, "_fetode_field", None)
+
+
+def _try_fused(func, y0, sched, method_code):
+    field = fused_field(func)
+    if field is None or y0.dim() != 2:
+        return None
+    B = y0.shape[0]
+    handle = make_handle(field, B, y0.device)
+    if not _lib.load().fetode_fused_supported(handle.ref):
+        return None
+    params = [p for p in field.parameters()]
+    return _FusedFixedFn.apply(field, handle, method_code, y0.contiguous(), sched, *params)
+
+
+# ---------------------------------------------------------------------------------------------
+# per-stage path (any func)
+# ---------------------------------------------------------------------------------------------
+
+class _CombineFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, method, stage, dt, y, k1, k2, k3, k4):
+        out = torch.empty_like(y)
+        _lib.check(_lib.load().fetode_rk_combine(method, stage, y.data_ptr(), k1.data_ptr(), _lib.ptr(k2),
+                                                 _lib.ptr(k3), _lib.ptr(k4), dt, out.data_ptr(), y.numel(),
+                                                 _lib.stream_handle(y.device)), "fetode_rk_combine")
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        raise NotImplementedError("per-stage backward is not built yet")
+
+
+def _c(v):
+    return None if v is None else v.contiguous()
+
+
+def _combine(method, stage, dt, y, k1, k2=None, k3=None, k4=None):
+    return _CombineFn.apply(method, stage, float(dt), _c(y), _c(k1), _c(k2), _c(k3), _c(k4))
+
+
+def _per_stage_fixed(func, y0, sched: Schedule, method: str, tc_dtype, reversed_):
+    sol = torch.empty(sched.T, *y0.shape, dtype=y0.dtype, device=y0.device)
+    sol[0] = y0
+    y = y0
+    g = sched.grid
+    sign = -1.0 if reversed_ else 1.0
+
+    def tt(v):
+        return torch.tensor(sign * v, dtype=y0.dtype)
+
+    j = 1
+    for s in range(sched.n_steps):
+        dt, hh, h6 = (float(v) for v in sched.step_coef[s, :3])
+        t0, t1 = g[s], g[s + 1]
+        if method == "rk4":
+            k1 = func(tt(t0), y)
+            k2 = func(tt(t0 + (t1 - t0) / 3), _combine(_lib.RK4, 1, dt, y, k1))
+            k3 = func(tt(t0 + 2 * (t1 - t0) / 3), _combine(_lib.RK4, 2, dt, y, k1, k2))
+            k4 = func(tt(t1), _combine(_lib.RK4, 3, dt, y, k1, k2, k3))
+            y1 = _combine(_lib.RK4, 4, dt, y, k1, k2, k3, k4)
+        elif method == "euler":
+            y1 = _combine(_lib.EULER, 4, dt, y, func(tt(t0), y))
+        elif method == "midpoint":
+            k1 = func(tt(t0), y)
+            k2 = func(tt(t0 + 0.5 * (t1 - t0)), _combine(_lib.EULER, 4, hh, y, k1))
+            y1 = _combine(_lib.EULER, 4, dt, y, k2)
+        else:  # rk4_classic
+            k1 = func(tt(t0), y)
+            k2 = func(tt(t0 + 0.5 * (t1 - t0)), _combine(_lib.EULER, 4, hh, y, k1))
+            k3 = func(tt(t0 + 0.5 * (t1 - t0)), _combine(_lib.EULER, 4, hh, y, k2))
+            k4 = func(tt(t1), _combine(_lib.EULER, 4, dt, y, k3))
+            raise NotImplementedError("rk4_classic per-stage combine")  # fused path only for now
+        while j < sched.T and sched.out_step[j] == s:
+            m = sched.out_mode[j]
+            if m == 0:
+                sol[j] = y
+            elif m == 1:
+                sol[j] = y1
+            else:
+                sol[j] = y + float(sched.out_slope[j]) * (y1 - y)
+            j += 1
+        y = y1
+    return sol
+
+
+# ---------------------------------------------------------------------------------------------
+# public entry
+# ---------------------------------------------------------------------------------------------
+
+def odeint(func, y0, t, *, rtol=1e-7, atol=1e-9, method=None, options=None, event_fn=None):
+    """torchdiffeq.odeint(func, y0, t, *, rtol, atol, method, options, event_fn) on the GPU.
+
+    Returns a tensor of shape (len(t), *y0.shape).  ``method`` defaults to 'dopri5' like
+    torchdiffeq.  Supported: euler, midpoint, rk4 (3/8 rule), rk4_classic, dopri5.
+    """
+    if event_fn is not None:
+        raise NotImplementedError("event_fn is not on the hot path")
+    method, tc, tp, reversed_ = _check_inputs(y0, t, method)
+    _lib.require_gpu_tensor(y0, "odeint")
+    options = dict(options or {})
+    if method == "dopri5":
+        from .dopri5 import dopri5_solve
+        return dopri5_solve(func, y0, tc, tp, reversed_, rtol, atol, options)
+    sched = get_schedule(tp, options.pop("step_size", None), reversed_)
+    code = FIXED_METHODS[method]
+    out = _try_fused(func, y0, sched, code)
+    if out is not None:
+        return out
+    return _per_stage_fixed(func, y0, sched, method, tc.dtype, reversed_)

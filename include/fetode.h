@@ -1,0 +1,155 @@
+/*
+ * fetode.h — C ABI of libfetode.so, the MI355X (gfx950) hot path of the
+ * KAN-FET Neural-ODE integrator.
+ *
+ * The reference (sallywang147/FET-ODE) is pure Python; it has no FFI.  Its
+ * drop-in boundary on this path is the Python surface
+ *   torchdiffeq.odeint(func, y0, t, rtol, atol, method, options)
+ *       call sites: train_kanfet_node_predprey.py:252,260, predator_prey.py:142,149
+ *   efficientkan.KANLinear.forward / .b_splines   efficient_kan/efficientkan.py:117-182
+ *   ferro_class.FerroelectricBasis.forward          ferro_class.py:368-420
+ * Each entry point below replaces one of those; the Python package
+ * (fet-ode_amd/) binds them with ctypes (INTEGRATION.md shows the stub).
+ *
+ * Conventions
+ *   - every pointer marked (dev) is device memory on the current HIP device;
+ *     (host) pointers are host memory read synchronously before return.
+ *   - tensors are fp32, C-contiguous, shapes in comments.
+ *   - all work is enqueued on `stream` (a hipStream_t, may be NULL = default
+ *     stream); nothing is allocated and nothing synchronises the host.
+ *   - return 0 on success, otherwise a FETODE_E* code; fetode_last_error()
+ *     returns a thread-local message for the last failure.
+ */
+#ifndef FETODE_H_
+#define FETODE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FETODE_ABI_VERSION 1
+
+enum {
+  FETODE_OK = 0,
+  FETODE_EINVAL = 1,       /* bad shape / argument */
+  FETODE_EUNSUPPORTED = 2, /* no fused kernel for this field shape; use the per-stage path */
+  FETODE_EHIP = 3          /* HIP runtime error (message in fetode_last_error) */
+};
+
+/* integration methods (torchdiffeq names) */
+enum {
+  FETODE_EULER = 0,     /* fixed_grid.Euler */
+  FETODE_MIDPOINT = 1,  /* fixed_grid.Midpoint */
+  FETODE_RK4 = 2,       /* fixed_grid.RK4 -> rk_common.rk4_alt_step_func (3/8 rule) */
+  FETODE_RK4_CLASSIC = 3 /* classic 1/6 weights: train_ecg_kan_fet_nn_ode.py:693-705 */
+};
+
+/* One efficientkan.KANLinear (efficient_kan/efficientkan.py:27-90).  (dev) pointers. */
+typedef struct fetode_kanlinear {
+  int32_t in_features, out_features;
+  int32_t grid_size, spline_order;  /* grid has grid_size + 2*spline_order + 1 knots per input */
+  int32_t num_logistic;             /* logistic branch basis count; 0 = branch disabled */
+  int32_t base_act;                 /* 0 = SiLU (the only activation on the path) */
+  const float* grid;                /* (in, grid_size+2*spline_order+1) buffer :55-61 */
+  const float* base_weight;         /* (out, in) */
+  const float* spline_weight;       /* (out, in, grid_size+spline_order) */
+  const float* spline_scaler;       /* (out, in), NULL if enable_standalone_scale_spline=False */
+  const float* logistic_a;          /* (in, nb)  LogisticBasis.a :17 */
+  const float* logistic_b;          /* (in, nb)  LogisticBasis.b :18 */
+  const float* logistic_weight;     /* (out, in*nb) */
+  const float* logistic_scaler;     /* (out), NULL if enable_standalone_scale_logistic=False */
+  float scale_logistic;             /* :45 */
+} fetode_kanlinear_t;
+
+/* One ferro_class.FerroelectricBasis (ferro_class.py:329-424).  (dev) pointers. */
+typedef struct fetode_ferro {
+  int32_t in_dim, out_dim, num_basis;
+  const float *k, *Ec, *Ps, *bias, *coef; /* each (in, out, K) :358-362 */
+  double gate_slope, alpha;               /* :347 defaults 10.0, 0.8 (Python floats) */
+  /* branch_sign buffer (:366).  The reference never writes it after (re)initialising it to
+   * ones (:377-378), so NULL means "all ones" (fast path).  Otherwise a (Bs, in, out, K) tensor
+   * with batch stride branch_sign_bstride elements (0 = broadcast one slice). */
+  const float* branch_sign;
+  int64_t branch_sign_bstride;
+} fetode_ferro_t;
+
+/* A vector field: a stack of layers, layer l = kan[l](x) (+ ferro[l](x) when present).
+ * KANFET (build-defined): both present.  efficientkan.KAN: ferro == NULL.
+ * (host) arrays of n_layers descriptors. */
+typedef struct fetode_field {
+  int32_t n_layers;
+  const fetode_kanlinear_t* kan;  /* n_layers entries */
+  const fetode_ferro_t* ferro;    /* n_layers entries or NULL (no hysteresis layers) */
+} fetode_field_t;
+
+/* Hysteresis state of a field: for every Ferro layer l a compact prev_x of shape (B, in_l)
+ * (the reference stores x.expand(B,in,out,K), ferro_class.py:372,409 — constant over out,K).
+ * Concatenated per trajectory: state[b, off_l + i], row length = sum of in_l over Ferro layers.
+ * init_mask bit l set  =>  the reference's re-initialisation rule fires on the first call
+ * (prev_x := x, i.e. dx = 0, ferro_class.py:373-375); clear => use the stored prev_x. */
+
+const char* fetode_last_error(void);
+int fetode_abi_version(void);
+
+/* Size in bytes of the packed "plan" (pre-transformed parameters). */
+int64_t fetode_plan_bytes(const fetode_field_t* field);
+/* Build the plan from the parameters; enqueue on stream.  plan: (dev) fetode_plan_bytes bytes. */
+int fetode_plan_build(const fetode_field_t* field, void* plan, void* stream);
+
+/* Row length of the compact hysteresis state of `field` (sum of Ferro in_l). */
+int32_t fetode_state_width(const fetode_field_t* field);
+
+/* 1 if a fused (single-launch) integrator kernel exists for this field shape. */
+int fetode_fused_supported(const fetode_field_t* field);
+
+/* One stateful field evaluation out = field(x) — KANFET.forward / KAN.forward.
+ * x (B, in0), out (B, out_last), state (B, state_width) updated in place to x-per-layer. */
+int fetode_field_forward(const fetode_field_t* field, const void* plan, const float* x, int64_t B,
+                         float* state, uint32_t init_mask, float* out, void* stream);
+
+/* Fixed-grid integration in ONE launch (torchdiffeq FixedGridODESolver.integrate).
+ *   y0 (B, D) ; step_coef (dev) n_steps x 4 floats per step s, each formed in the time
+ *   dtype then rounded to fp32 as torch does for a 0-dim time tensor times an fp32 state:
+ *   [dt = grid[s+1]-grid[s], 0.5*dt, dt/6, 0] (0.5*dt: Midpoint / classic rk4; dt/6: classic rk4);
+ *   outputs j = 1..T-1: out_step[j] (dev int32) = step after which solution[j] is produced,
+ *   out_mode[j] (dev int32) 0: y(step start), 1: y(step end), 2: linear interp with out_slope[j];
+ *   solution (T, B, D): row 0 is written from y0.
+ *   state/init_mask as in fetode_field_forward (final state written back).
+ *   ckpt (dev, nullable): (n_steps, B, D + state_width) per-step start checkpoints for backward.
+ * Returns FETODE_EUNSUPPORTED when no fused kernel exists for this field shape. */
+int fetode_integrate_fixed(const fetode_field_t* field, const void* plan, int32_t method,
+                           const float* y0, int64_t B, const float* step_coef, int32_t n_steps,
+                           const int32_t* out_step, const int32_t* out_mode, const float* out_slope,
+                           int32_t T, float* solution, float* state, uint32_t init_mask,
+                           float* ckpt, void* stream);
+
+/* Standalone module kernels (generic widths). */
+/* KANLinear.forward (efficientkan.py:160-182): x (B,in) -> out (B,out). */
+int fetode_kanlinear_forward(const fetode_kanlinear_t* layer, const float* x, int64_t B, float* out,
+                             void* stream);
+/* KANLinear.b_splines (efficientkan.py:117-131): x (B,in) -> bases (B,in,grid_size+spline_order). */
+int fetode_kanlinear_bsplines(const fetode_kanlinear_t* layer, const float* x, int64_t B,
+                              float* bases, void* stream);
+/* FerroelectricBasis.forward (ferro_class.py:368-420).  prev (B,in) is read (ignored when
+ * reinit != 0, which applies the :373-375 rule dx = 0); after the kernel prev_out (nullable,
+ * may alias prev) receives x (:409).  basis (nullable): (B,in,out,K) activations (:417-418).
+ * accumulate != 0: out += ferro(x) (a KAN-FET layer adds it to the KANLinear output). */
+int fetode_ferro_forward(const fetode_ferro_t* layer, const float* x, int64_t B, const float* prev,
+                         int32_t reinit, int32_t accumulate, float* out, float* basis,
+                         float* prev_out, void* stream);
+
+/* Stage combines of the per-stage (generic func) path, exact torchdiffeq op order, n elements.
+ *   rk4 (3/8, rk_common.rk4_alt_step_func):
+ *     stage 1: out = y + (dt*k1)*(1/3)     stage 2: out = y + dt*(k2 - k1*(1/3))
+ *     stage 3: out = y + dt*(k1 - k2 + k3) stage 4: out = y + ((k1 + 3*(k2+k3)) + k4)*dt*0.125
+ *   euler: stage 4 form out = y + dt*k1.   k2..k4 may be NULL when unused. */
+int fetode_rk_combine(int32_t method, int32_t stage, const float* y, const float* k1,
+                      const float* k2, const float* k3, const float* k4, float dt, float* out,
+                      int64_t n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FETODE_H_ */

@@ -1,0 +1,582 @@
+"""CPU ORACLE — test infrastructure only.
+
+This module is a CPU restatement of the reference hot path, written in the
+reference's own eager-op order so that on CPU it reproduces the reference
+bit for bit (pinned by tests/golden, generated from the imported reference
+modules by tests/golden/make_golden.py).  Only tests/, __graft_entry__.smoke()
+and bench.py's ``cpu_baseline`` leg may import it, and only as the checker or
+the timed CPU baseline.  The product package (fet-ode_amd/) never imports it.
+
+Restated pieces (file:line relative to the reference snapshot):
+  * LogisticBasis.forward          efficient_kan/efficientkan.py:20-24
+  * KANLinear.b_splines            efficient_kan/efficientkan.py:117-131
+  * KANLinear.scaled_*_weight      efficient_kan/efficientkan.py:145-158
+  * KANLinear.forward              efficient_kan/efficientkan.py:160-182
+  * KAN.forward                    efficient_kan/efficientkan.py:274-279
+  * FerroelectricBasis.forward     ferro_class.py:368-420 (state rules :373-378, :409)
+  * FerroelectricBasis.reset_state ferro_class.py:422-424
+  * KANFET (build-defined): per layer KANLinear(x) + Ferro(x)
+  * torchdiffeq.odeint             third-party, NOT vendored / not installed,
+    no pinned version.  Restated from torchdiffeq's published
+    algorithm (torchdiffeq 0.2.x: _impl/odeint.py, misc.py, solvers.py,
+    fixed_grid.py, rk_common.py, dopri5.py, interp.py); call sites
+    train_kanfet_node_predprey.py:252,260, predator_prey.py:142,149,
+    train_ecg_kan_fet_nn_ode.py:558-565.  Parity for this part is pinned by
+    known-answer tests (tests/test_oracle_solver.py), not by reference
+    fixtures: "parity unpinned" w.r.t. a torchdiffeq binary.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+import torch
+import torch.nn.functional as F
+
+# ---------------------------------------------------------------------------
+# KANLinear (efficient_kan/efficientkan.py)
+# ---------------------------------------------------------------------------
+
+
+def make_grid(in_features: int, grid_size: int = 5, spline_order: int = 3,
+              grid_range=(-1, 1), dtype=torch.float32) -> torch.Tensor:
+    """Knot grid buffer, efficientkan.py:55-61."""
+    h = (grid_range[1] - grid_range[0]) / grid_size
+    g = (torch.arange(-spline_order, grid_size + spline_order + 1) * h + grid_range[0])
+    return g.expand(in_features, -1).contiguous().to(dtype)
+
+
+def logistic_basis(x: torch.Tensor, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """efficientkan.py:20-24 — 2/(1+exp(-a(x-b))), (B,in) -> (B,in,nb)."""
+    x = x.unsqueeze(-1)
+    return 2.0 / (1.0 + torch.exp(-a * (x - b)))
+
+
+def b_splines(x: torch.Tensor, grid: torch.Tensor, spline_order: int) -> torch.Tensor:
+    """efficientkan.py:117-131 — Cox-de Boor on the per-input knot grid."""
+    x = x.unsqueeze(-1)
+    bases = ((x >= grid[:, :-1]) & (x < grid[:, 1:])).to(x.dtype)
+    for k in range(1, spline_order + 1):
+        bases = (
+            (x - grid[:, : -(k + 1)]) / (grid[:, k:-1] - grid[:, : -(k + 1)]) * bases[:, :, :-1]
+        ) + (
+            (grid[:, k + 1:] - x) / (grid[:, k + 1:] - grid[:, 1:(-k)]) * bases[:, :, 1:]
+        )
+    return bases.contiguous()
+
+
+@dataclass
+class KANLinearParams:
+    """Parameter/buffer set of one KANLinear (names = reference state_dict keys)."""
+    grid: torch.Tensor                      # (in, G+2k+1) buffer
+    base_weight: torch.Tensor               # (out, in)
+    spline_weight: torch.Tensor             # (out, in, G+k)
+    spline_scaler: Optional[torch.Tensor]   # (out, in) or None
+    a: Optional[torch.Tensor] = None        # logistic_basis.a (in, nb)
+    b: Optional[torch.Tensor] = None        # logistic_basis.b (in, nb)
+    logistic_weight: Optional[torch.Tensor] = None   # (out, in*nb)
+    logistic_scaler: Optional[torch.Tensor] = None   # (out,)
+    spline_order: int = 3
+    scale_logistic: float = 1.0
+
+    @property
+    def in_features(self):
+        return self.base_weight.shape[1]
+
+    @property
+    def out_features(self):
+        return self.base_weight.shape[0]
+
+    @classmethod
+    def from_state_dict(cls, sd: Dict[str, torch.Tensor], prefix: str = "", spline_order=3,
+                        scale_logistic=1.0):
+        g = lambda k: sd.get(prefix + k)
+        return cls(grid=g("grid"), base_weight=g("base_weight"), spline_weight=g("spline_weight"),
+                   spline_scaler=g("spline_scaler"), a=g("logistic_basis.a"), b=g("logistic_basis.b"),
+                   logistic_weight=g("logistic_weight"), logistic_scaler=g("logistic_scaler"),
+                   spline_order=spline_order, scale_logistic=scale_logistic)
+
+    def to(self, dtype):
+        kw = {}
+        for f_ in ("grid", "base_weight", "spline_weight", "spline_scaler", "a", "b",
+                   "logistic_weight", "logistic_scaler"):
+            v = getattr(self, f_)
+            kw[f_] = None if v is None else v.detach().to(dtype)
+        return KANLinearParams(spline_order=self.spline_order, scale_logistic=self.scale_logistic, **kw)
+
+
+def scaled_spline_weight(p: KANLinearParams) -> torch.Tensor:
+    """efficientkan.py:145-147."""
+    return p.spline_weight * (p.spline_scaler.unsqueeze(-1) if p.spline_scaler is not None else 1.0)
+
+
+def scaled_logistic_weight(p: KANLinearParams) -> Optional[torch.Tensor]:
+    """efficientkan.py:149-158."""
+    if p.logistic_weight is None:
+        return None
+    w = p.logistic_weight
+    w = w * p.scale_logistic
+    if p.logistic_scaler is not None:
+        w = w * p.logistic_scaler.unsqueeze(-1)
+    return w
+
+
+def kanlinear_forward(x: torch.Tensor, p: KANLinearParams) -> torch.Tensor:
+    """efficientkan.py:160-182 (base_activation = SiLU)."""
+    in_f, out_f = p.in_features, p.out_features
+    assert x.size(-1) == in_f
+    original_shape = x.shape
+    x2d = x.reshape(-1, in_f)
+    base_output = F.linear(F.silu(x2d), p.base_weight)
+    spline_output = F.linear(
+        b_splines(x2d, p.grid, p.spline_order).view(x2d.size(0), -1),
+        scaled_spline_weight(p).view(out_f, -1),
+    )
+    out = base_output + spline_output
+    if p.logistic_weight is not None:
+        phi = logistic_basis(x2d, p.a, p.b)
+        phi_flat = phi.reshape(x2d.size(0), -1)
+        out = out + F.linear(phi_flat, scaled_logistic_weight(p))
+    return out.reshape(*original_shape[:-1], out_f)
+
+
+# ---------------------------------------------------------------------------
+# FerroelectricBasis (ferro_class.py:329-424)
+# ---------------------------------------------------------------------------
+
+
+@dataclass
+class FerroParams:
+    k: torch.Tensor      # (in, out, K)
+    Ec: torch.Tensor
+    Ps: torch.Tensor
+    bias: torch.Tensor
+    coef: torch.Tensor
+    gate_slope: float = 10.0
+    alpha: float = 0.8
+
+    @classmethod
+    def from_state_dict(cls, sd, prefix="", gate_slope=10.0, alpha=0.8):
+        return cls(*(sd[prefix + n] for n in ("k", "Ec", "Ps", "bias", "coef")),
+                   gate_slope=gate_slope, alpha=alpha)
+
+    def to(self, dtype):
+        return FerroParams(*(getattr(self, n).detach().to(dtype) for n in ("k", "Ec", "Ps", "bias", "coef")),
+                           gate_slope=self.gate_slope, alpha=self.alpha)
+
+
+class FerroState:
+    """The two state buffers of FerroelectricBasis (ferro_class.py:365-366)."""
+
+    def __init__(self, in_dim, out_dim, K, dtype=torch.float32):
+        self.prev_x = torch.zeros(1, in_dim, out_dim, K, dtype=dtype)
+        self.branch_sign = torch.ones(1, in_dim, out_dim, K, dtype=dtype)
+
+    def reset(self):
+        """ferro_class.py:422-424."""
+        self.prev_x.zero_()
+        self.branch_sign.fill_(1.0)
+
+    def clone(self):
+        s = FerroState.__new__(FerroState)
+        s.prev_x = self.prev_x.clone()
+        s.branch_sign = self.branch_sign.clone()
+        return s
+
+
+def ferro_forward(x: torch.Tensor, p: FerroParams, st: FerroState, return_activations=False):
+    """ferro_class.py:368-420; mutates ``st`` exactly as the module mutates its buffers."""
+    if x.dim() > 2:
+        x = x.view(x.shape[0], -1)
+    out_dim, K = p.k.shape[1], p.k.shape[2]
+    x_exp = x.unsqueeze(2).unsqueeze(3).expand(-1, -1, out_dim, K)
+    if st.prev_x.shape != x_exp.shape or st.prev_x.dtype != x_exp.dtype:       # :373-375
+        st.prev_x = x_exp.detach().clone()
+    if st.branch_sign.shape != x_exp.shape or st.branch_sign.dtype != x_exp.dtype:  # :377-378
+        st.branch_sign = torch.ones_like(x_exp).detach()
+    prev_x_snap = st.prev_x.detach().clone()
+    branch_snap = st.branch_sign.detach().clone()
+    dx = x_exp - prev_x_snap
+    is_moving_up = torch.sigmoid(p.gate_slope * dx)
+    crossed_pos_Ec = torch.sigmoid(p.gate_slope * (x_exp - p.Ec))
+    crossed_neg_Ec = torch.sigmoid(p.gate_slope * (-x_exp - p.Ec))
+    switch_to_upper = is_moving_up * crossed_pos_Ec
+    switch_to_lower = (1 - is_moving_up) * crossed_neg_Ec
+    target_sign = switch_to_upper * 1.0 + switch_to_lower * (-1.0) + \
+        (1 - switch_to_upper - switch_to_lower) * branch_snap
+    branch_mom = p.alpha * branch_snap + (1.0 - p.alpha) * target_sign
+    shifted_x = x_exp + p.Ec * branch_mom
+    basis = p.Ps * torch.tanh(p.k * shifted_x) + p.bias
+    st.prev_x.copy_(x_exp.detach())                                           # :409
+    weighted = basis * p.coef
+    output = weighted.sum(dim=(1, 3))
+    if return_activations:
+        return output, basis.detach(), p.coef.detach()
+    return output
+
+
+# ---------------------------------------------------------------------------
+# Composite vector fields
+# ---------------------------------------------------------------------------
+
+
+class KANRef:
+    """efficientkan.KAN (efficientkan.py:240-279) as a stateless field."""
+
+    def __init__(self, layers: List[KANLinearParams]):
+        self.layers = layers
+
+    def __call__(self, x):
+        for p in self.layers:
+            x = kanlinear_forward(x, p)
+        return x
+
+    def to(self, dtype):
+        return KANRef([p.to(dtype) for p in self.layers])
+
+
+class KANFETRef:
+    """KANFET, build-defined: layer(x) = KANLinear(x) + Ferro(x)."""
+
+    def __init__(self, kan: List[KANLinearParams], ferro: List[FerroParams], states=None):
+        assert len(kan) == len(ferro)
+        self.kan, self.ferro = kan, ferro
+        self.states = states or [FerroState(f.k.shape[0], f.k.shape[1], f.k.shape[2], f.k.dtype)
+                                 for f in ferro]
+
+    def __call__(self, x):
+        for kp, fp, st in zip(self.kan, self.ferro, self.states):
+            x = kanlinear_forward(x, kp) + ferro_forward(x, fp, st)
+        return x
+
+    def reset_state(self):
+        for s in self.states:
+            s.reset()
+
+    def to(self, dtype):
+        sts = []
+        for s in self.states:
+            c = s.clone()
+            c.prev_x = c.prev_x.to(dtype)
+            c.branch_sign = c.branch_sign.to(dtype)
+            sts.append(c)
+        return KANFETRef([p.to(dtype) for p in self.kan], [p.to(dtype) for p in self.ferro], sts)
+
+    @classmethod
+    def from_state_dict(cls, sd, n_layers, gate_slope=10.0, alpha=0.8):
+        kan = [KANLinearParams.from_state_dict(sd, f"layers.{l}.kan.") for l in range(n_layers)]
+        fer = [FerroParams.from_state_dict(sd, f"layers.{l}.ferro.", gate_slope, alpha)
+               for l in range(n_layers)]
+        return cls(kan, fer)
+
+
+# ---------------------------------------------------------------------------
+# torchdiffeq.odeint restated (third-party; see module docstring)
+# ---------------------------------------------------------------------------
+
+_ONE_THIRD = 1 / 3
+_TWO_THIRDS = 2 / 3
+
+# Dormand-Prince-Shampine tableau (torchdiffeq _impl/dopri5.py)
+DOPRI5_ALPHA = [1 / 5, 3 / 10, 4 / 5, 8 / 9, 1., 1.]
+DOPRI5_BETA = [
+    [1 / 5],
+    [3 / 40, 9 / 40],
+    [44 / 45, -56 / 15, 32 / 9],
+    [19372 / 6561, -25360 / 2187, 64448 / 6561, -212 / 729],
+    [9017 / 3168, -355 / 33, 46732 / 5247, 49 / 176, -5103 / 18656],
+    [35 / 384, 0, 500 / 1113, 125 / 192, -2187 / 6784, 11 / 84],
+]
+DOPRI5_C_SOL = [35 / 384, 0, 500 / 1113, 125 / 192, -2187 / 6784, 11 / 84, 0]
+DOPRI5_C_ERR = [
+    35 / 384 - 1951 / 21600, 0, 500 / 1113 - 22642 / 50085, 125 / 192 - 451 / 720,
+    -2187 / 6784 - -12231 / 42400, 11 / 84 - 649 / 6300, -1. / 60.,
+]
+DOPRI5_C_MID = [
+    6025192743 / 30085553152 / 2, 0, 51252292925 / 65400821598 / 2, -2691868925 / 45128329728 / 2,
+    187940372067 / 1594534317056 / 2, -1776094331 / 19743644256 / 2, 11237099 / 235043384 / 2,
+]
+
+
+def _as_time(t, y0):
+    t = torch.as_tensor(t)
+    if not torch.is_floating_point(t):
+        t = t.to(torch.get_default_dtype())
+    return t
+
+
+def _check_inputs(func, y0, t, method):
+    if not torch.is_floating_point(y0):
+        raise TypeError("`y0` must be a floating point Tensor but is a {}".format(y0.type()))
+    if method is None:
+        method = "dopri5"
+    if method not in ("euler", "midpoint", "rk4", "dopri5"):
+        raise ValueError('Invalid method "{}".'.format(method))
+    t = _as_time(t, y0)
+    assert t.dim() == 1, "t must be one dimensional"
+    reversed_ = len(t) > 1 and bool(t[0] > t[1])
+    if reversed_:
+        t = -t
+        base = func
+        func = lambda tt, yy: -base(-tt, yy)
+    assert (t[1:] > t[:-1]).all(), "t must be strictly increasing or decreasing"
+
+    def perturbed(tt, yy):
+        # _PerturbFunc: time is cast to the state's dtype before the user call.
+        return func(tt.to(yy.dtype) if torch.is_tensor(tt) else tt, yy)
+
+    return perturbed, t, method, reversed_
+
+
+def _fixed_grid(func, y0, t, step_fn, step_size=None):
+    """FixedGridODESolver.integrate (solvers.py) with linear interpolation."""
+    if step_size is None:
+        grid = t
+    else:
+        niters = torch.ceil((t[-1] - t[0]) / step_size + 1).item()
+        grid = torch.arange(0, niters, dtype=t.dtype) * step_size + t[0]
+        grid[-1] = t[-1]
+    solution = torch.empty(len(t), *y0.shape, dtype=y0.dtype)
+    solution[0] = y0
+    j = 1
+    y = y0
+    for t0, t1 in zip(grid[:-1], grid[1:]):
+        dt = t1 - t0
+        dy = step_fn(func, t0, dt, t1, y)
+        y1 = y + dy
+        while j < len(t) and t1 >= t[j]:
+            tj = t[j]
+            if tj == t0:
+                solution[j] = y
+            elif tj == t1:
+                solution[j] = y1
+            else:
+                slope = (tj - t0) / (t1 - t0)
+                solution[j] = y + slope * (y1 - y)
+            j += 1
+        y = y1
+    return solution
+
+
+def euler_step(func, t0, dt, t1, y0):
+    """fixed_grid.Euler._step_func."""
+    return dt * func(t0, y0)
+
+
+def midpoint_step(func, t0, dt, t1, y0):
+    """fixed_grid.Midpoint._step_func."""
+    half_dt = 0.5 * dt
+    f0 = func(t0, y0)
+    y_mid = y0 + f0 * half_dt
+    return dt * func(t0 + half_dt, y_mid)
+
+
+def rk4_alt_step(func, t0, dt, t1, y0):
+    """rk_common.rk4_alt_step_func — the 3/8-rule RK4 used by method='rk4'."""
+    k1 = func(t0, y0)
+    k2 = func(t0 + dt * _ONE_THIRD, y0 + dt * k1 * _ONE_THIRD)
+    k3 = func(t0 + dt * _TWO_THIRDS, y0 + dt * (k2 - k1 * _ONE_THIRD))
+    k4 = func(t1, y0 + dt * (k1 - k2 + k3))
+    return (k1 + 3 * (k2 + k3) + k4) * dt * 0.125
+
+
+def rk4_classic_step(func, t0, dt, t1, y0):
+    """Classic RK4 (train_ecg_kan_fet_nn_ode.py:693-705, train_kan_fet_ett.py:51-83)."""
+    k1 = func(t0, y0)
+    k2 = func(t0 + dt / 2, y0 + dt * k1 / 2)
+    k3 = func(t0 + dt / 2, y0 + dt * k2 / 2)
+    k4 = func(t0 + dt, y0 + dt * k3)
+    return dt * (k1 + 2 * k2 + 2 * k3 + k4) / 6
+
+
+def _rms_norm(x):
+    return x.abs().pow(2).mean().sqrt()
+
+
+@dataclass
+class Dopri5Trace:
+    attempts: List[tuple] = field(default_factory=list)   # (t0, dt, error_ratio, accepted)
+    nfev: int = 0
+    first_step: float = 0.0
+
+
+def _select_initial_step(func, t0, y0, order, rtol, atol, f0):
+    """misc._select_initial_step (Hairer, Norsett & Wanner II.4)."""
+    dtype = y0.dtype
+    scale = atol + torch.abs(y0) * rtol
+    d0 = _rms_norm(y0 / scale).abs()
+    d1 = _rms_norm(f0 / scale).abs()
+    if d0 < 1e-5 or d1 < 1e-5:
+        h0 = torch.tensor(1e-6, dtype=dtype)
+    else:
+        h0 = 0.01 * d0 / d1
+    h0 = h0.abs()
+    y1 = y0 + h0 * f0
+    f1 = func(t0 + h0, y1)
+    d2 = torch.abs(_rms_norm((f1 - f0) / scale) / h0)
+    if d1 <= 1e-15 and d2 <= 1e-15:
+        h1 = torch.max(torch.tensor(1e-6, dtype=dtype), h0 * 1e-3)
+    else:
+        h1 = (0.01 / max(d1, d2)) ** (1. / float(order + 1))
+    h1 = h1.abs()
+    return torch.min(100 * h0, h1).to(t0.dtype)
+
+
+def _interp_fit(y0, y1, y_mid, f0, f1, dt):
+    """interp._interp_fit — quartic through y0, y_mid, y1 with end slopes."""
+    a = 2 * dt * (f1 - f0) - 8 * (y1 + y0) + 16 * y_mid
+    b = dt * (5 * f0 - 3 * f1) + 18 * y0 + 14 * y1 - 32 * y_mid
+    c = dt * (f1 - 4 * f0) - 11 * y0 - 5 * y1 + 16 * y_mid
+    d = dt * f0
+    e = y0
+    return [e, d, c, b, a]
+
+
+def _interp_evaluate(coefficients, t0, t1, t):
+    """interp._interp_evaluate."""
+    assert (t0 <= t) & (t <= t1), "invalid interpolation"
+    x = (t - t0) / (t1 - t0)
+    x = x.to(coefficients[0].dtype)
+    total = coefficients[0] + x * coefficients[1]
+    x_power = x
+    for coefficient in coefficients[2:]:
+        x_power = x_power * x
+        total = total + x_power * coefficient
+    return total
+
+
+def _dopri5(func, y0, t, rtol, atol, trace: Optional[Dopri5Trace], max_num_steps=2 ** 31 - 1,
+            first_step=None):
+    """RKAdaptiveStepsizeODESolver + Dopri5Solver (rk_common.py / dopri5.py)."""
+    sdt = y0.dtype
+    tdt = torch.promote_types(torch.float64, sdt)
+    rtol_t = torch.as_tensor(rtol, dtype=tdt)
+    atol_t = torch.as_tensor(atol, dtype=tdt)
+    safety = torch.as_tensor(0.9, dtype=tdt)
+    ifactor = torch.as_tensor(10.0, dtype=tdt)
+    dfactor0 = torch.as_tensor(0.2, dtype=tdt)
+    alpha = torch.tensor(DOPRI5_ALPHA, dtype=torch.float64).to(sdt)
+    beta = [torch.tensor(b_, dtype=torch.float64).to(sdt) for b_ in DOPRI5_BETA]
+    c_err = torch.tensor(DOPRI5_C_ERR, dtype=torch.float64).to(sdt)
+    c_mid = torch.tensor(DOPRI5_C_MID, dtype=torch.float64).to(sdt)
+
+    t = t.to(tdt)
+    solution = torch.empty(len(t), *y0.shape, dtype=sdt)
+    solution[0] = y0
+    nf = [0]
+
+    def f(tt, yy):
+        nf[0] += 1
+        return func(tt, yy)
+
+    f0 = f(t[0], y0)
+    if first_step is None:
+        dt = _select_initial_step(f, t[0], y0, 4, rtol_t, atol_t, f0)
+    else:
+        dt = torch.as_tensor(first_step, dtype=tdt)
+    if trace is not None:
+        trace.first_step = float(dt)
+    # _RungeKuttaState(y1, f1, t0, t1, dt, interp_coeff)
+    st_y, st_f, st_t0, st_t1, st_dt, st_coeff = y0, f0, t[0], t[0], dt, [y0] * 5
+    for i in range(1, len(t)):
+        next_t = t[i]
+        n_steps = 0
+        while next_t > st_t1:
+            assert n_steps < max_num_steps, "max_num_steps exceeded"
+            # _adaptive_step
+            y0_, f0_, t0_, dt_ = st_y, st_f, st_t1, st_dt
+            t1_ = t0_ + dt_
+            assert t0_ + dt_ > t0_, "underflow in dt {}".format(dt_.item())
+            assert torch.isfinite(y0_).all(), "non-finite values in state `y`"
+            # _runge_kutta_step
+            t0c, dtc, t1c = t0_.to(sdt), dt_.to(sdt), t1_.to(sdt)
+            k = torch.empty(*f0_.shape, 7, dtype=sdt)
+            k[..., 0] = f0_
+            yi = None
+            for s, (alpha_i, beta_i) in enumerate(zip(alpha, beta)):
+                ti = t1c if alpha_i == 1. else t0c + alpha_i * dtc
+                yi = y0_ + k[..., :s + 1].matmul(beta_i * dtc).view_as(f0_)
+                k[..., s + 1] = f(ti, yi)
+            y1 = yi
+            f1 = k[..., -1]
+            y1_error = k.matmul(dtc * c_err)
+            error_tol = atol_t + rtol_t * torch.max(y0_.abs(), y1.abs())
+            error_ratio = _rms_norm(y1_error / error_tol)
+            accept = bool(error_ratio <= 1)
+            if trace is not None:
+                trace.attempts.append((float(t0_), float(dt_), float(error_ratio), accept))
+            if accept:
+                dtm = dt_.type_as(y0_)
+                y_mid = y0_ + k.matmul(dtm * c_mid).view_as(y0_)
+                coeff = _interp_fit(y0_, y1, y_mid, k[..., 0], k[..., -1], dtm)
+                st_y, st_f, st_t0, st_t1, st_coeff = y1, f1, t0_, t1_, coeff
+            else:
+                st_t0 = t0_
+            # _optimal_step_size
+            if error_ratio == 0:
+                dt_next = dt_ * ifactor
+            else:
+                dfactor = dfactor0 if error_ratio >= 1 else torch.ones((), dtype=tdt)
+                er = error_ratio.type_as(dt_)
+                exponent = torch.tensor(5, dtype=tdt).reciprocal()
+                factor = torch.min(ifactor, torch.max(safety / er ** exponent, dfactor))
+                dt_next = dt_ * factor
+            st_dt = dt_next.clamp(0, float("inf"))
+            n_steps += 1
+        solution[i] = _interp_evaluate(st_coeff, st_t0, st_t1, next_t)
+    if trace is not None:
+        trace.nfev = nf[0]
+    return solution
+
+
+def odeint(func: Callable, y0: torch.Tensor, t, *, rtol=1e-7, atol=1e-9, method=None,
+           options=None, trace: Optional[Dopri5Trace] = None, classic_rk4=False):
+    """torchdiffeq.odeint restated: euler / midpoint / rk4 (3/8) / dopri5."""
+    options = dict(options or {})
+    func, t, method, reversed_ = _check_inputs(func, y0, t, method)
+    if method == "dopri5":
+        sol = _dopri5(func, y0, t, rtol, atol, trace, first_step=options.get("first_step"))
+    else:
+        step = {"euler": euler_step, "midpoint": midpoint_step,
+                "rk4": rk4_classic_step if classic_rk4 else rk4_alt_step}[method]
+        sol = _fixed_grid(func, y0, t, step, options.get("step_size"))
+    return sol
+
+
+def rk4_with_states(field: "KANFETRef", y0: torch.Tensor, t: torch.Tensor):
+    """rk4 (3/8) on the grid t, recording (y_j, [compact prev_x per Ferro layer]) at every step
+    start — the teacher-forcing record used by the one-step parity tests."""
+    func, t, _, _ = _check_inputs(lambda tt, yy: field(yy), y0, t, "rk4")
+    recs = []
+    y = y0
+    sol = [y0]
+    for t0, t1 in zip(t[:-1], t[1:]):
+        recs.append((y.clone(), [st.prev_x[:, :, 0, 0].clone() for st in field.states]))
+        y = y + rk4_alt_step(func, t0, t1 - t0, t1, y)
+        sol.append(y)
+    return torch.stack(sol), recs
+
+
+# ---------------------------------------------------------------------------
+# Seeded synthetic workload — shared by tests and bench
+# ---------------------------------------------------------------------------
+
+def lv_y0(batch: int, seed: int = 0, dtype=torch.float32) -> torch.Tensor:
+    """y0 = 0.5 + 2.5 * U[0,1)^{B x 2} from torch.Generator().manual_seed(seed)."""
+    g = torch.Generator().manual_seed(seed)
+    return (0.5 + 2.5 * torch.rand(batch, 2, generator=g)).to(dtype)
+
+
+def lotka_volterra_truth(n_t=140, tf=14.0, x0=1.0, y0=1.0, alpha=1.5, beta=1.0, gamma=3.0,
+                         delta=1.0):
+    """train_kanfet_node_predprey.py:20-52 — LSODA ground truth (scipy)."""
+    import numpy as np
+    import scipy.integrate
+
+    def deriv(X, t, alpha, beta, delta, gamma):
+        x, y = X
+        return [alpha * x - beta * x * y, delta * x * y - gamma * y]
+
+    t = np.linspace(0, tf, n_t)
+    return t, scipy.integrate.odeint(deriv, np.array([x0, y0]), t, args=(alpha, beta, delta, gamma))
