@@ -1,0 +1,223 @@
+"""Benchmark: RK4 steps/s of the batch-4096, 2-state Lotka-Volterra KAN-FET Neural ODE.
+
+Workload (BASELINE.json configs[1]): KANFET([2,10,2], grid_size=5, K=10) as the
+vector field (train_kanfet_node_predprey.py:146), torch.manual_seed(0) weights, y0 = 0.5 +
+2.5*U[0,1)^(4096x2) (seed 0 + rank), t = linspace(0, 3.5, 35) float64 (t_learn, :155),
+method='rk4' (torchdiffeq 3/8 rule).  One bench "step" = one odeint solve = 34 RK4 steps of
+the whole batch, inputs resident in HBM.  value = RK4 batch-steps/s summed over ranks (weak
+scaling: every rank integrates its own 4096 trajectories; no collective on the forward path).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run.
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+import fet_ode_amd as F  # noqa: E402
+from fet_ode_amd import _lib  # noqa: E402
+from fet_ode_amd.autograd_ops import build_plan, make_handle, pack_state  # noqa: E402
+from fet_ode_amd.odeint import get_schedule  # noqa: E402
+
+B = 4096
+T = 35
+STEPS_PER_SOLVE = T - 1
+METRIC = "RK4 steps/sec, batch-4096 2-state LV KAN-FET NODE @1/2/4/8 GPU; traj MSE vs ref"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3       # MI355X_MICROARCH.md: FP32 vector (= f32 MFMA) peak
+PARAM_FLOATS = 3052 + 144      # trainable params + grid buffers of KANFET [2,10,2]
+STATE_IN = 2 + 10              # sum of Ferro in_l
+
+
+def alg_bytes_per_step(b):
+    """y read+write (16 B) + compact prev_x r/w per Ferro layer (8*sum in_l) per
+    trajectory, + parameters once:  112*B + 12784."""
+    return b * (16 + 8 * STATE_IN) + 4 * PARAM_FLOATS
+
+
+ALG_FLOPS_PER_TRAJ_STEP = 50_000   # ~50k flops (+5.8k transcendentals) per RK4 step
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def make_problem(rank, dev):
+    torch.manual_seed(0)
+    model = F.KANFET([2, 10, 2], grid_size=5)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    model = model.to(dev)
+    g = torch.Generator().manual_seed(rank)
+    y0 = (0.5 + 2.5 * torch.rand(B, 2, generator=g)).to(torch.float32)
+    t = torch.tensor(np.linspace(0, 3.5, T))
+    return model, sd, y0, t
+
+
+def kernel_time_ms(model, y0d, t, reps=20):
+    """Average duration of the fused integrate launch alone (HIP events on its stream)."""
+    dev = y0d.device
+    lib = _lib.load()
+    sched = get_schedule(t.to(torch.float64) if t.dtype == torch.float64 else t, None, False)
+    handle = make_handle(model, B, dev)
+    plan = build_plan(model, handle, dev)
+    state, mask = pack_state(model, B, dev)
+    _, coef, ostep, omode, oslope = sched.device_arrays(dev)
+    sol = torch.empty(sched.T, B, 2, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    h = stream.cuda_stream
+
+    def launch():
+        _lib.check(lib.fetode_integrate_fixed(handle.ref, plan.data_ptr(), _lib.RK4, y0d.data_ptr(), B,
+                                              coef.data_ptr(), sched.n_steps, ostep.data_ptr(),
+                                              omode.data_ptr(), oslope.data_ptr(), sched.T, sol.data_ptr(),
+                                              state.data_ptr(), mask, None, h), "integrate")
+    for _ in range(3):
+        launch()
+    torch.cuda.synchronize(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2 * reps)]
+    for r in range(reps):
+        ev[2 * r].record(stream)
+        launch()
+        ev[2 * r + 1].record(stream)
+    torch.cuda.synchronize(dev)
+    return float(np.mean([ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(reps)]))
+
+
+def pmc_traffic_per_launch():
+    """HBM bytes per fused launch from the newest committed rocprofv3 PMC summary, corrected as
+    MI355X_MICROARCH.md §HBM prescribes (FETCH_SIZE x2 on gfx950; WRITE_SIZE as is; KiB units)."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_traffic*.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], REPO)
+
+
+def cpu_baseline(sd, y0, t, seconds):
+    """The CPU oracle (restatement of the reference, reference op order) on this host's cores."""
+    from oracle import torch_ref as O
+    cores = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(cores)
+    ref = O.KANFETRef.from_state_dict(sd, 2)
+    f = lambda tt, yy: ref(yy)
+    with torch.no_grad():
+        O.odeint(f, y0, t[:2], method="rk4")           # warm-up (1 step)
+        ref = O.KANFETRef.from_state_dict(sd, 2)        # fresh state for the timed solve
+        f = lambda tt, yy: ref(yy)
+        t0 = time.perf_counter()
+        sol = O.odeint(f, y0, t, method="rk4")          # one full 34-step solve of the batch
+        el = time.perf_counter() - t0
+        n_solves = 1
+        while time.perf_counter() - t0 < seconds and n_solves < 20:
+            ref2 = O.KANFETRef.from_state_dict(sd, 2)
+            O.odeint(lambda tt, yy: ref2(yy), y0, t, method="rk4")
+            n_solves += 1
+        el = time.perf_counter() - t0
+    return {"value": n_solves * STEPS_PER_SOLVE / el, "unit": "RK4 steps/s (batch 4096)", "cores": cores,
+            "kind": "port",
+            "sample": f"{n_solves} full solve(s) of the bench workload (B=4096, 34 rk4 steps) with "
+                      f"oracle/torch_ref.py (reference op order, torch CPU fp32), {el:.1f} s"}, sol
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    model, sd, y0, t = make_problem(rank, dev)
+    y0d = y0.to(dev)
+    func = F.autonomous(model)
+
+    def solve():
+        return F.odeint(func, y0d, t, method="rk4")
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            solve()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            sol = solve()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = tt.item()
+        k_ms = kernel_time_ms(model, y0d, t)
+    ms_per_step = el / args.steps * 1e3
+    value = world * args.steps * STEPS_PER_SOLVE / el
+
+    if rank == 0:
+        bytes_launch = alg_bytes_per_step(B) * STEPS_PER_SOLVE
+        achieved = bytes_launch / (k_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic_per_launch()
+        flops_launch = ALG_FLOPS_PER_TRAJ_STEP * B * STEPS_PER_SOLVE
+        tflops = flops_launch / (k_ms * 1e-3) / 1e12
+        out = {
+            "metric": METRIC, "value": value, "unit": "RK4 steps/s (batch-4096 steps, summed over GPUs)",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (seeded y0, torch.manual_seed(0) weights; no dataset)",
+            "config": {"workload": "LV KAN-FET NODE: KANFET[2,10,2] G=5 k=3 nb=10 K=10, rk4 (3/8), "
+                                   "B=4096 per GPU, t=linspace(0,3.5,35) -> 34 steps per solve",
+                       "batch_per_gpu": B, "global_batch": B * world, "rk4_steps_per_solve": STEPS_PER_SOLVE,
+                       "parallelism": f"trajectory-sharded x{world} (no collective)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "fused_integrate_kernel<2,10,2,10,10,3,12,true,32>",
+                         "kernel_ms": k_ms, "alg_bytes_per_launch": bytes_launch,
+                         "traffic_source": traffic_src,
+                         "valu": {"achieved_tflops": tflops, "peak_tflops": FP32_PEAK_TFLOPS,
+                                  "frac": tflops / FP32_PEAK_TFLOPS,
+                                  "alg_flops_per_launch": flops_launch}},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            cb, ref_sol = cpu_baseline(sd, y0, t, args.cpu_seconds)
+            out["cpu_baseline"] = cb
+            fresh = F.KANFET([2, 10, 2], grid_size=5)
+            fresh.load_state_dict(sd)          # fresh hysteresis state, as the CPU solve had
+            with torch.no_grad():
+                sol = F.odeint(F.autonomous(fresh.to(dev)), y0d, t, method="rk4")
+            g = sol.cpu().double()
+            r = ref_sol.double()
+            out["parity"] = {
+                "traj_mse_vs_cpu_ref": ((g - r) ** 2).mean().item(),
+                "max_slice_rel_vs_cpu_ref": ((g - r).reshape(T, -1).norm(dim=1)
+                                             / r.reshape(T, -1).norm(dim=1)).max().item(),
+                "note": "KAN-FET is ill-conditioned in fp32 (the CPU reference's own fp32 vs fp64 "
+                        "per-slice error reaches ~6e-3 on this workload); see DESIGN.md §5",
+            }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -2,7 +2,7 @@
 # one GPU call: tests, smoke, quick bench; stops after any crash/timeout (status >1)
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 600 python -m pytest tests -q -m gpu > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc" | tee -a gpurun_out/pytest_gpu.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
