@@ -1,0 +1,58 @@
+// fetode_common.h — shared host/device declarations of libfetode (plan layout, errors).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fetode.h"
+#include "fetode_device.h"
+
+namespace fetode {
+
+int set_err(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+
+#define HIP_CHECK_RET(expr)                                                                        \
+  do {                                                                                             \
+    hipError_t e_ = (expr);                                                                        \
+    if (e_ != hipSuccess)                                                                          \
+      return ::fetode::set_err(FETODE_EHIP, "%s: %s", #expr, hipGetErrorString(e_));              \
+  } while (0)
+
+#define LAUNCH_CHECK()                                                                             \
+  do {                                                                                             \
+    hipError_t e_ = hipGetLastError();                                                             \
+    if (e_ != hipSuccess)                                                                          \
+      return ::fetode::set_err(FETODE_EHIP, "kernel launch: %s", hipGetErrorString(e_));           \
+  } while (0)
+
+inline int nblk(int64_t n, int t) { return (int)((n + t - 1) / t); }
+
+// Packed per-layer "plan" (parameters pre-transformed once per solve).
+// All offsets are in floats from the start of the plan buffer.
+struct LayerPlan {
+  int in, out, K, NB, SO, NG, NI, NFL;  // NI = NG-1 knot intervals, NFL = 1 + NB LDS features/input
+  int64_t base;
+  int64_t fe_GEc;   // (out, in*K)  gate_slope*log2e*Ec            (Ferro element order o, i, k)
+  int64_t fe_k2;    // (out, in*K)  2*log2e*k
+  int64_t fe_k2Ec;  // (out, in*K)  2*log2e*k*Ec
+  int64_t fe_CPs2;  // (out, in*K)  coef*Ps
+  int64_t fconst;   // (out)        sum_{i,k} coef*bias
+  int64_t kw;       // (out, in*NFL) SiLU weight, 2*scaled logistic weights
+  int64_t lg;       // (in*NB, 2)   (-a*log2e, a*b*log2e)
+  int64_t knots;    // (in, NG)
+  int64_t rh;       // (in, NI)     1/(g[m+1]-g[m])
+  int64_t sp;       // (out, in, NI+1, 4) spline contribution as a cubic in u per interval
+  int64_t flag;     // 1 word: max |gate_slope*log2e*Ec| (float bits) -> factored-exp guard
+  int64_t end;
+  float gsl2e;      // gate_slope*log2e
+  float wc;         // -2*(1-alpha)
+};
+
+void layer_plan(const fetode_kanlinear_t& kl, const fetode_ferro_t* fl, int64_t base, LayerPlan* p);
+int validate_field(const fetode_field_t* f);
+
+// The factored gate exp(gs(x+Ec)) = exp(gs x) * exp(gs Ec) is used only when
+// |gs*log2e*Ec| <= kFactorLimit everywhere in the layer: then exp(gs x) overflowing /
+// underflowing can only happen where the fp32 sigmoid is already saturated at 0 / 1.
+constexpr float kFactorLimit = 60.0f;
+
+}  // namespace fetode

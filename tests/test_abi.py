@@ -62,9 +62,11 @@ def test_host_queries_without_gpu():
     h = _lv_field(F)
     assert lib.fetode_state_width(h.ref) == 12
     nb = lib.fetode_plan_bytes(h.ref)
-    # per layer: 4*in*out*K + out + out*in*19 + 2*in*10 + in*12 + in*3*11, padded to 4 floats
+    # per layer (fetode_common.h LayerPlan): 4*in*out*K + out + out*in*(1+nb) + 2*in*nb
+    # + in*12 knots + in*11 spans, pad to 4; + out*in*12*4 spline table + 1 flag, pad to 4
     def lp(i, o):
-        n = 4 * i * o * 10 + o + o * i * 19 + 2 * i * 10 + i * 12 + i * 3 * 11
+        n = 4 * i * o * 10 + o + o * i * 11 + 2 * i * 10 + i * 12 + i * 11
+        n = (n + 3) // 4 * 4 + o * i * 12 * 4 + 1
         return (n + 3) // 4 * 4
     assert nb == 4 * (lp(2, 10) + lp(10, 2))
     assert lib.fetode_fused_supported(h.ref) == 1
