@@ -41,6 +41,15 @@ class FerroDesc(ctypes.Structure):
     ]
 
 
+class KANLinearGrad(ctypes.Structure):
+    _fields_ = [(n, _fp) for n in ("base_weight", "spline_weight", "spline_scaler", "logistic_a",
+                                   "logistic_b", "logistic_weight", "logistic_scaler")]
+
+
+class FerroGrad(ctypes.Structure):
+    _fields_ = [(n, _fp) for n in ("k", "Ec", "Ps", "bias", "coef")]
+
+
 class FieldDesc(ctypes.Structure):
     _fields_ = [
         ("n_layers", ctypes.c_int32),
@@ -68,6 +77,12 @@ SIGNATURES = {
                                             ctypes.c_int32, _vp, _vp, _vp, _vp]),
     "fetode_rk_combine": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp,
                                          ctypes.c_float, _vp, ctypes.c_int64, _vp]),
+    "fetode_axpby": (ctypes.c_int, [ctypes.c_int64, ctypes.c_float, _vp, ctypes.c_float, _vp, _vp, _vp]),
+    "fetode_kanlinear_backward_workspace": (ctypes.c_int64, [ctypes.POINTER(KANLinearDesc)]),
+    "fetode_kanlinear_backward": (ctypes.c_int, [ctypes.POINTER(KANLinearDesc), _vp, ctypes.c_int64, _vp, _vp,
+                                                 ctypes.POINTER(KANLinearGrad), _vp, ctypes.c_int32, _vp]),
+    "fetode_ferro_backward": (ctypes.c_int, [ctypes.POINTER(FerroDesc), _vp, ctypes.c_int64, _vp, ctypes.c_int32,
+                                             _vp, _vp, ctypes.POINTER(FerroGrad), ctypes.c_int32, _vp]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -1,12 +1,13 @@
 """Dispatch from the drop-in modules to libfetode, with autograd wrappers.
 
 Everything here runs HIP kernels through the C ABI; there is no CPU or torch-eager
-fallback for the forward maths.  Hysteresis state updates happen exactly once per
-forward call, in call order (ferro_class.py:409), whether or not autograd records.
+fallback for the forward or backward maths.  Hysteresis state updates happen exactly once
+per forward call, in call order (ferro_class.py:409), whether or not autograd records; the
+state is a detached snapshot in the reference (:381-382), so it carries no gradient.
 """
 from __future__ import annotations
 
-from typing import Optional
+from typing import List, Optional
 
 import torch
 
@@ -15,6 +16,19 @@ from . import _lib
 
 def _stream(x):
     return _lib.stream_handle(x.device)
+
+
+def axpby(a: float, x: torch.Tensor, b: float = 0.0, y: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """a*x + b*y on the GPU (HIP)."""
+    x = x.contiguous()
+    out = torch.empty_like(x)
+    _lib.check(_lib.load().fetode_axpby(x.numel(), float(a), x.data_ptr(), float(b), _lib.ptr(
+        None if y is None else y.contiguous()), out.data_ptr(), _stream(x)), "fetode_axpby")
+    return out
+
+
+def grad_enabled_for(*tensors) -> bool:
+    return torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in tensors)
 
 
 # ---------------------------------------------------------------------------------------------
@@ -40,6 +54,19 @@ def build_plan(owner, handle: _lib.FieldHandle, device) -> torch.Tensor:
 # KANLinear
 # ---------------------------------------------------------------------------------------------
 
+KAN_PARAM_NAMES = ("base_weight", "spline_weight", "spline_scaler", "logistic_a", "logistic_b",
+                   "logistic_weight", "logistic_scaler")
+
+
+def kan_params(mod) -> List[Optional[torch.Tensor]]:
+    lg = mod.enable_logistic_basis
+    return [mod.base_weight, mod.spline_weight,
+            mod.spline_scaler if mod.enable_standalone_scale_spline else None,
+            mod.logistic_basis.a if lg else None, mod.logistic_basis.b if lg else None,
+            mod.logistic_weight if lg else None,
+            mod.logistic_scaler if lg and mod.enable_standalone_scale_logistic else None]
+
+
 class _KANLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, mod, x, *params):
@@ -49,21 +76,53 @@ class _KANLinearFn(torch.autograd.Function):
         out = torch.empty(x.shape[0], mod.out_features, device=x.device, dtype=torch.float32)
         _lib.check(_lib.load().fetode_kanlinear_forward(_lib.ctypes.byref(d), xc.data_ptr(), x.shape[0],
                                                         out.data_ptr(), _stream(x)), "KANLinear.forward")
+        ctx.mod = mod
+        ctx.save_for_backward(xc)
         return out
 
     @staticmethod
     def backward(ctx, grad):
-        raise NotImplementedError("KANLinear backward: use the fused odeint path")
+        (xc,) = ctx.saved_tensors
+        mod = ctx.mod
+        gx, grads = kan_backward(mod, xc, grad, ctx.needs_input_grad[1], ctx.needs_input_grad[2:])
+        return (None, gx, *grads)
+
+
+def kan_backward(mod, xc, grad, want_x, want_params, gx_accum=None):
+    """HIP VJP of KANLinear: returns (gx, [grad per KAN_PARAM_NAMES or None])."""
+    lib = _lib.load()
+    keep = []
+    d = mod.desc(keep)
+    g = _lib.f32c(grad)
+    B = xc.shape[0]
+    gx = None
+    if want_x:
+        gx = torch.empty_like(xc) if gx_accum is None else gx_accum
+    params = kan_params(mod)
+    grads = [torch.zeros_like(p) if (p is not None and w) else None for p, w in zip(params, want_params)]
+    any_param = any(t is not None for t in grads)
+    gstruct = _lib.KANLinearGrad(*[_lib.ptr(t) for t in grads]) if any_param else None
+    ws = None
+    if any_param:
+        nb = lib.fetode_kanlinear_backward_workspace(_lib.ctypes.byref(d))
+        ws = torch.empty(max(1, nb // 4), device=xc.device, dtype=torch.float32)
+    _lib.check(lib.fetode_kanlinear_backward(
+        _lib.ctypes.byref(d), xc.data_ptr(), B, g.data_ptr(), _lib.ptr(gx),
+        _lib.ctypes.byref(gstruct) if any_param else None, _lib.ptr(ws),
+        int(gx_accum is not None), _stream(xc)), "KANLinear backward")
+    return gx, grads
 
 
 def kanlinear_apply(mod, x2d):
-    params = [p for p in mod.parameters()]
-    return _KANLinearFn.apply(mod, x2d, *params)
+    return _KANLinearFn.apply(mod, x2d, *kan_params(mod))
 
 
 # ---------------------------------------------------------------------------------------------
 # FerroelectricBasis
 # ---------------------------------------------------------------------------------------------
+
+FERRO_PARAM_NAMES = ("k", "Ec", "Ps", "bias", "coef")
+
 
 class _FerroFn(torch.autograd.Function):
     @staticmethod
@@ -73,7 +132,7 @@ class _FerroFn(torch.autograd.Function):
         xc = _lib.f32c(x)
         B = x.shape[0]
         if accumulate_into is not None:
-            out = accumulate_into.clone()
+            out = accumulate_into.detach().clone()
         else:
             out = torch.empty(B, mod.out_dim, device=x.device, dtype=torch.float32)
         basis = (torch.empty(B, mod.in_dim, mod.out_dim, mod.num_basis, device=x.device, dtype=torch.float32)
@@ -85,15 +144,41 @@ class _FerroFn(torch.autograd.Function):
             "FerroelectricBasis.forward")
         if basis is not None:
             ctx.mark_non_differentiable(basis)
+        ctx.mod, ctx.reinit, ctx.bsign = mod, reinit, bsign
+        # the module's prev_x is overwritten right after this call: keep the snapshot
+        ctx.save_for_backward(xc, None if prev is None else prev.detach().clone())
         return out, basis
 
     @staticmethod
     def backward(ctx, grad, gbasis):
-        raise NotImplementedError("FerroelectricBasis backward: use the fused odeint path")
+        xc, prev = ctx.saved_tensors
+        gx, grads = ferro_backward(ctx.mod, xc, prev, ctx.reinit, ctx.bsign, grad, ctx.needs_input_grad[1],
+                                   ctx.needs_input_grad[6:])
+        gacc = grad if ctx.needs_input_grad[5] else None
+        return (None, gx, None, None, None, gacc, *grads)
+
+
+def ferro_backward(mod, xc, prev, reinit, bsign, grad, want_x, want_params, gx_accum=None):
+    lib = _lib.load()
+    keep = []
+    d = mod.desc(keep, bsign)
+    g = _lib.f32c(grad)
+    gx = None
+    if want_x:
+        gx = torch.empty_like(xc) if gx_accum is None else gx_accum
+    params = [getattr(mod, n) for n in FERRO_PARAM_NAMES]
+    grads = [torch.zeros_like(p) if w else None for p, w in zip(params, want_params)]
+    any_param = any(t is not None for t in grads)
+    gstruct = _lib.FerroGrad(*[_lib.ptr(t) for t in grads]) if any_param else None
+    _lib.check(lib.fetode_ferro_backward(
+        _lib.ctypes.byref(d), xc.data_ptr(), xc.shape[0], _lib.ptr(prev), int(reinit), g.data_ptr(),
+        _lib.ptr(gx), _lib.ctypes.byref(gstruct) if any_param else None, int(gx_accum is not None),
+        _stream(xc)), "FerroelectricBasis backward")
+    return gx, grads
 
 
 def ferro_apply(mod, x, reinit: bool, bsign, want_basis: bool, accumulate_into=None):
-    params = [mod.k, mod.Ec, mod.Ps, mod.bias, mod.coef]
+    params = [getattr(mod, n) for n in FERRO_PARAM_NAMES]
     out, basis = _FerroFn.apply(mod, x, reinit, bsign, want_basis, accumulate_into, *params)
     return out, basis
 
@@ -113,8 +198,8 @@ def field_layers(model):
     return out
 
 
-def make_handle(model, B: int, device) -> tuple:
-    """Descriptor of the field + the per-layer explicit branch_sign tensors (None = ones)."""
+def make_handle(model, B: int, device) -> _lib.FieldHandle:
+    """Descriptor of the field (+ explicit branch_sign tensors; None = ones)."""
     keep = []
     layers = field_layers(model)
     kan = [k.desc(keep) for k, _ in layers]
@@ -155,52 +240,46 @@ def unpack_state(model, state: torch.Tensor):
             f._bsign = None
 
 
-class _FieldEvalFn(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, model, handle, x, state, mask, *params):
-        plan = build_plan(model, handle, x.device)
-        out = torch.empty(x.shape[0], field_layers(model)[-1][0].out_features, device=x.device,
-                          dtype=torch.float32)
-        _lib.check(_lib.load().fetode_field_forward(handle.ref, plan.data_ptr(), x.data_ptr(), x.shape[0],
-                                                    _lib.ptr(state), mask, out.data_ptr(), _stream(x)),
-                   "field forward")
-        return out
-
-    @staticmethod
-    def backward(ctx, grad):
-        raise NotImplementedError("field backward: use the fused odeint path")
+def _fused_eval(model, handle, x):
+    B = x.shape[0]
+    plan = build_plan(model, handle, x.device)
+    state, mask = pack_state(model, B, x.device)
+    out = torch.empty(B, field_layers(model)[-1][0].out_features, device=x.device, dtype=torch.float32)
+    _lib.check(_lib.load().fetode_field_forward(handle.ref, plan.data_ptr(), x.data_ptr(), B, _lib.ptr(state),
+                                                mask, out.data_ptr(), _stream(x)), "field forward")
+    if state is not None:
+        unpack_state(model, state)
+    return out
 
 
 def field_apply(model, x: torch.Tensor) -> torch.Tensor:
-    """KAN.forward / KANFET.forward: one evaluation, fused single-launch when the shape has a
-    fused kernel, otherwise one HIP kernel per KANLinear / Ferro layer."""
+    """KAN.forward / KANFET.forward: one evaluation.  Inference on a shape with a fused kernel
+    is one launch; otherwise (other widths, or autograd recording) one HIP kernel per
+    KANLinear / Ferro layer, each with its HIP backward."""
     in0 = field_layers(model)[0][0].in_features
     lead = x.shape[:-1]
-    x2 = x.reshape(-1, in0) if model.has_ferro is False else x
     if model.has_ferro and x.dim() != 2:
         raise ValueError("KANFET expects x of shape (B, in_features)")
+    x2 = x.reshape(-1, in0)
     _lib.require_gpu_tensor(x2, type(model).__name__ + ".forward")
-    x2 = x2.contiguous()
     B = x2.shape[0]
-    handle = make_handle(model, B, x2.device)
-    lib = _lib.load()
-    if lib.fetode_fused_supported(handle.ref):
-        state, mask = pack_state(model, B, x2.device)
-        params = [p for p in model.parameters()]
-        out = _FieldEvalFn.apply(model, handle, x2, state, mask, *params)
-        if state is not None:
-            unpack_state(model, state)
-    else:
-        h = x2
-        for kan, fer in field_layers(model):
-            y = kanlinear_apply(kan, h)
-            if fer is not None:
-                reinit = fer._needs_reinit(h)
-                bsign = fer._branch_sign_for(h)
-                y, _ = ferro_apply(fer, h, reinit, bsign, False, accumulate_into=y)
-                fer._commit_state(h, reinit)
-            h = y
-        out = h
+    params = list(model.parameters())
+    if not grad_enabled_for(x2, *params):
+        x2 = x2.contiguous()
+        handle = make_handle(model, B, x2.device)
+        if _lib.load().fetode_fused_supported(handle.ref):
+            out = _fused_eval(model, handle, x2)
+            return out.reshape(*lead, out.shape[-1]) if not model.has_ferro else out
+    h = x2
+    for kan, fer in field_layers(model):
+        y = kanlinear_apply(kan, h)
+        if fer is not None:
+            reinit = fer._needs_reinit(h)
+            bsign = fer._branch_sign_for(h)
+            y, _ = ferro_apply(fer, h, reinit, bsign, False, accumulate_into=y)
+            fer._commit_state(h, reinit)
+        h = y
+    out = h
     if not model.has_ferro:
         out = out.reshape(*lead, out.shape[-1])
     return out

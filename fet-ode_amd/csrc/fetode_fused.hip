@@ -24,6 +24,12 @@
 
 using namespace fetode;
 
+#ifdef FETODE_ISA_MARKERS
+#define FETODE_MARK(s) asm volatile("; MARK " s ::: "memory")
+#else
+#define FETODE_MARK(s)
+#endif
+
 namespace {
 
 template <int IN_, int OUT_, int K_, int NB_, int NG_, int LPT_>
@@ -286,18 +292,23 @@ __global__ __launch_bounds__(NT) void fused_integrate_kernel(FusedArgs a) {
     constexpr bool F_ = decltype(fact_tag)::value;
     if (own) T.x0[d] = xin;
     __syncthreads();
+    FETODE_MARK("A0");
     phase_A<S0, FERRO>(T.x0, T.L0, s_w0, R0, a.P0, lane, re0);
     re0 = false;
     __syncthreads();
+    FETODE_MARK("B0");
     const float v0 = phase_B<S0, FERRO, F_>(T.L0, s_sp0, R0, a.P0.gsl2e);
     if (R0.active && R0.c == 0) T.h[R0.o] = v0 + s_w0.cst[R0.o];
     __syncthreads();
+    FETODE_MARK("A1");
     phase_A<S1, FERRO>(T.h, T.L1, s_w1, R1, a.P1, lane, re1);
     re1 = false;
     __syncthreads();
+    FETODE_MARK("B1");
     const float v1 = phase_B<S1, FERRO, F_>(T.L1, s_sp1, R1, a.P1.gsl2e);
     if (R1.active && R1.c == 0) T.kout[R1.o] = v1 + s_w1.cst[R1.o];
     __syncthreads();
+    FETODE_MARK("END");
     return own ? T.kout[d] : 0.f;
   };
   auto eval = [&](float xin) __attribute__((always_inline)) -> float {
@@ -371,15 +382,21 @@ struct FusedEntry {
   int in0, h, out, K, NB, NG;
   bool ferro;
   fused_fn fn;
-  int nt;
+  int nt, lpt;
 };
-#define FUSED(IN0, H, OUT, K, NB, NG, FE, NT) \
-  {IN0, H, OUT, K, NB, NG, FE, fused_integrate_kernel<IN0, H, OUT, K, NB, NG, FE, 32, NT>, NT}
+#define FUSED(IN0, H, OUT, K, NB, NG, FE, LPT, NT) \
+  {IN0, H, OUT, K, NB, NG, FE, fused_integrate_kernel<IN0, H, OUT, K, NB, NG, FE, LPT, NT>, NT, LPT}
 const FusedEntry kFused[] = {
-    FUSED(2, 10, 2, 10, 10, 12, true, 256),  // LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146)
-    FUSED(2, 10, 2, 10, 10, 12, true, 64),
-    FUSED(2, 10, 2, 1, 10, 12, false, 256),  // LV KAN [2,10,2] (predator_prey.py:101)
-    FUSED(2, 10, 2, 1, 10, 12, false, 64),
+    // LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146)
+    FUSED(2, 10, 2, 10, 10, 12, true, 32, 64),
+    FUSED(2, 10, 2, 10, 10, 12, true, 32, 256),
+    FUSED(2, 10, 2, 10, 10, 12, true, 64, 64),
+    FUSED(2, 10, 2, 10, 10, 12, true, 64, 256),
+    // LV KAN [2,10,2] (predator_prey.py:101)
+    FUSED(2, 10, 2, 1, 10, 12, false, 32, 64),
+    FUSED(2, 10, 2, 1, 10, 12, false, 32, 256),
+    FUSED(2, 10, 2, 1, 10, 12, false, 64, 64),
+    FUSED(2, 10, 2, 1, 10, 12, false, 64, 256),
 };
 
 // workgroup size: 64 threads (one wave, 2 trajectories; its barriers cost almost nothing)
@@ -390,6 +407,14 @@ int preferred_nt() {
     return e ? atoi(e) : 64;
   }();
   return nt;
+}
+// lanes per trajectory: 32 (2 trajectories per wave) unless FETODE_FUSED_LPT says otherwise
+int preferred_lpt() {
+  static int v = [] {
+    const char* e = getenv("FETODE_FUSED_LPT");
+    return e ? atoi(e) : 32;
+  }();
+  return v;
 }
 
 const FusedEntry* find_fused(const fetode_field_t* f) {
@@ -403,7 +428,7 @@ const FusedEntry* find_fused(const fetode_field_t* f) {
     if (e.in0 != k0.in_features || e.h != k0.out_features || e.out != k1.out_features) continue;
     if (e.NB != k0.num_logistic || e.NG != NG) continue;
     if (e.ferro != (f->ferro != nullptr)) continue;
-    if (e.nt != preferred_nt()) continue;
+    if (e.nt != preferred_nt() || e.lpt != preferred_lpt()) continue;
     if (f->ferro) {
       if (f->ferro[0].num_basis != e.K || f->ferro[1].num_basis != e.K) continue;
       if (f->ferro[0].branch_sign || f->ferro[1].branch_sign) continue;  // general sign: generic path
@@ -418,7 +443,7 @@ int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
   if (!e) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
   layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
   layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
-  const int tpb = e->nt / 32;
+  const int tpb = e->nt / e->lpt;
   hipLaunchKernelGGL(e->fn, dim3(nblk(a.B, tpb)), dim3(e->nt), 0, (hipStream_t)stream, a);
   LAUNCH_CHECK();
   return FETODE_OK;

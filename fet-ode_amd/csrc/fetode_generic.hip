@@ -107,7 +107,21 @@ __global__ void rk_combine_kernel(int method, int stage, const float* __restrict
   out[t] = r;
 }
 
+__global__ void axpby_kernel(int64_t n, float a, const float* __restrict__ x, float b, const float* __restrict__ y,
+                             float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) out[t] = y ? a * x[t] + b * y[t] : a * x[t];
+}
+
 extern "C" {
+
+int fetode_axpby(int64_t n, float a, const float* x, float b, const float* y, float* out, void* stream) {
+  if (n <= 0) return FETODE_OK;
+  if (!x || !out) return set_err(FETODE_EINVAL, "null pointer");
+  hipLaunchKernelGGL(axpby_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, n, a, x, b, y, out);
+  LAUNCH_CHECK();
+  return FETODE_OK;
+}
 
 int fetode_kanlinear_forward(const fetode_kanlinear_t* kl, const float* x, int64_t B, float* out,
                              void* stream) {

@@ -1,0 +1,415 @@
+// fetode_grad.hip — vector-Jacobian products of KANLinear and FerroelectricBasis (any widths).
+//
+// These are the backward counterparts of the reference's autograd through
+//   efficientkan.KANLinear.forward  (efficient_kan/efficientkan.py:160-182)
+//   ferro_class.FerroelectricBasis.forward (ferro_class.py:368-420)
+// used by the per-stage path (any func) and by the backward of the fused solve
+// (train_kanfet_node_predprey.py:254-257: loss.backward() through every RK stage).
+// The hysteresis state is a detached snapshot in the reference (:381-382), so no gradient
+// flows through prev_x.  Parameter gradients are reduced over the batch inside one
+// workgroup per parameter group (fixed order, no atomics): results are run-to-run identical.
+#include <cstring>
+
+#include "fetode_common.h"
+
+using namespace fetode;
+
+namespace {
+
+constexpr int RB = 256;  // reduction block
+
+__device__ __forceinline__ float sigm(float z) { return 1.0f / (1.0f + expf(-z)); }
+
+template <int N>
+__device__ __forceinline__ void block_sum(float (&v)[N], float* red /* RB*N */) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < N; ++q) red[q * RB + t] = v[q];
+  __syncthreads();
+  for (int s = RB / 2; s > 0; s >>= 1) {
+    if (t < s) {
+#pragma unroll
+      for (int q = 0; q < N; ++q) red[q * RB + t] += red[q * RB + t + s];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < N; ++q) v[q] = red[q * RB];
+}
+
+__device__ __forceinline__ void put(float* dst, float v, int accumulate) {
+  if (dst) *dst = accumulate ? *dst + v : v;
+}
+
+// B-spline values and x-derivatives of the SO+1 bases that are non-zero at x (reference
+// recursion with divisions; derivative = sum over the recursion of the (x-g)/d factors, i.e.
+// SO*(B_{j,SO-1}/(g_{j+SO}-g_j) - B_{j+1,SO-1}/(g_{j+SO+1}-g_{j+1}))).  Returns m (or -1 if
+// x is outside the grid; -2 if x is not finite -> NaN everywhere, as the reference's autograd).
+template <int SO>
+__device__ int bspline_vals_derivs(float x, int NG, const float* __restrict__ g, float* val, float* der) {
+#pragma unroll
+  for (int r = 0; r <= SO; ++r) val[r] = der[r] = 0.f;
+  if (!__builtin_isfinite(x)) {
+    for (int r = 0; r <= SO; ++r) val[r] = der[r] = __builtin_nanf("");
+    return -2;
+  }
+  int m = -1;
+  for (int j = 0; j < NG; ++j) m += (x >= g[j]) ? 1 : 0;
+  if (m < 0 || m > NG - 2) return -1;
+  float N[SO + 2];
+#pragma unroll
+  for (int r = 0; r < SO + 2; ++r) N[r] = 0.f;
+  N[SO] = 1.f;
+  float P[SO + 2];  // level SO-1
+#pragma unroll
+  for (int r = 0; r < SO + 2; ++r) P[r] = 0.f;
+#pragma unroll
+  for (int k = 1; k <= SO; ++k) {
+    if (k == SO) {
+#pragma unroll
+      for (int r = 0; r < SO + 2; ++r) P[r] = N[r];
+    }
+    float M[SO + 2];
+#pragma unroll
+    for (int r = 0; r < SO + 2; ++r) M[r] = 0.f;
+#pragma unroll
+    for (int r = SO - k; r <= SO; ++r) {
+      const int j = m - SO + r;
+      if (j >= 0 && j <= NG - 2 - k) {
+        M[r] = ((x - g[j]) / (g[j + k] - g[j])) * N[r] + ((g[j + k + 1] - x) / (g[j + k + 1] - g[j + 1])) * N[r + 1];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < SO + 2; ++r) N[r] = M[r];
+  }
+#pragma unroll
+  for (int r = 0; r <= SO; ++r) {
+    const int j = m - SO + r;
+    val[r] = N[r];
+    if (j >= 0 && j <= NG - 2 - SO) {
+      const float a = P[r] / (g[j + SO] - g[j]);
+      const float b = (r + 1 <= SO) ? P[r + 1] / (g[j + SO + 1] - g[j + 1]) : 0.f;
+      der[r] = SO * (a - b);
+    }
+  }
+  return m;
+}
+
+// ------------------------------------------------------------------------------------------
+// KANLinear
+// ------------------------------------------------------------------------------------------
+
+// gx[b,i] (+)= sum_o g[b,o] d out[b,o] / d x[b,i]
+template <int SO>
+__global__ void kan_gx_kernel(fetode_kanlinear_t kl, const float* __restrict__ x, const float* __restrict__ g,
+                              int64_t B, float* __restrict__ gx, int accumulate) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int in = kl.in_features, out = kl.out_features, NB = kl.num_logistic;
+  const int NG = kl.grid_size + 2 * SO + 1, NS = kl.grid_size + SO;
+  if (t >= B * in) return;
+  const int64_t b = t / in;
+  const int i = t % in;
+  const float xv = x[t];
+  const float sg = sigm(xv);
+  const float dsilu = sg * (1.0f + xv * (1.0f - sg));
+  float val[SO + 1], der[SO + 1];
+  const int m = bspline_vals_derivs<SO>(xv, NG, kl.grid + (int64_t)i * NG, val, der);
+  float acc = 0.f;
+  for (int o = 0; o < out; ++o) {
+    const float go = g[b * out + o];
+    float d = kl.base_weight[o * in + i] * dsilu;
+    const float sc = kl.spline_scaler ? kl.spline_scaler[o * in + i] : 1.0f;
+    const float* sw = kl.spline_weight + ((int64_t)o * in + i) * NS;
+    if (m >= 0) {
+      for (int r = 0; r <= SO; ++r) {
+        const int j = m - SO + r;
+        if (j >= 0 && j < NS) d += (sw[j] * sc) * der[r];
+      }
+    } else if (m == -2) {
+      d = __builtin_nanf("");
+    }
+    if (NB > 0) {
+      const float ls = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
+      for (int j = 0; j < NB; ++j) {
+        const float a = kl.logistic_a[i * NB + j], bb = kl.logistic_b[i * NB + j];
+        const float s = sigm(a * (xv - bb));
+        const float w = (kl.logistic_weight[(int64_t)o * in * NB + i * NB + j] * kl.scale_logistic) * ls;
+        d += w * (2.0f * s * (1.0f - s) * a);
+      }
+    }
+    acc += go * d;
+  }
+  gx[t] = accumulate ? gx[t] + acc : acc;
+}
+
+// one block per (o, i, f): f = 0 base weight, 1..NS scaled spline weight c = f-1, NS+1.. W' (logistic)
+template <int SO>
+__global__ void kan_gw_kernel(fetode_kanlinear_t kl, const float* __restrict__ x, const float* __restrict__ g,
+                              int64_t B, float* __restrict__ d_scaled /* (out,in,NS) scratch */,
+                              float* __restrict__ d_wl /* (out,in*NB) scratch */, fetode_kanlinear_grad_t gr,
+                              int accumulate) {
+  __shared__ float red[RB];
+  const int in = kl.in_features, out = kl.out_features, NB = kl.num_logistic;
+  const int NG = kl.grid_size + 2 * SO + 1, NS = kl.grid_size + SO, NF = 1 + NS + NB;
+  const int blk = blockIdx.x;
+  const int o = blk / (in * NF), r = blk % (in * NF), i = r / NF, f = r % NF;
+  float s[1] = {0.f};
+  for (int64_t b = threadIdx.x; b < B; b += RB) {
+    const float xv = x[b * in + i], go = g[b * out + o];
+    float v;
+    if (f == 0) {
+      v = xv * sigm(xv);
+    } else if (f <= NS) {
+      float val[SO + 1], der[SO + 1];
+      const int m = bspline_vals_derivs<SO>(xv, NG, kl.grid + (int64_t)i * NG, val, der);
+      const int c = f - 1;
+      v = 0.f;
+      if (m == -2) v = __builtin_nanf("");
+#pragma unroll
+      for (int rr = 0; rr <= SO; ++rr)
+        if (m >= 0 && m - SO + rr == c) v = val[rr];
+    } else {
+      const int j = f - 1 - NS;
+      v = 2.0f / (1.0f + expf(-kl.logistic_a[i * NB + j] * (xv - kl.logistic_b[i * NB + j])));
+    }
+    s[0] += go * v;
+  }
+  block_sum(s, red);
+  if (threadIdx.x == 0) {
+    if (f == 0) put(gr.base_weight ? gr.base_weight + o * in + i : nullptr, s[0], accumulate);
+    else if (f <= NS) d_scaled[((int64_t)o * in + i) * NS + (f - 1)] = s[0];
+    else d_wl[(int64_t)o * in * NB + i * NB + (f - 1 - NS)] = s[0];
+  }
+}
+
+// chain rule of the scaled weights: spline_weight, spline_scaler, logistic_weight, logistic_scaler
+__global__ void kan_scale_grads_kernel(fetode_kanlinear_t kl, const float* __restrict__ d_scaled,
+                                       const float* __restrict__ d_wl, fetode_kanlinear_grad_t gr, int accumulate) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int in = kl.in_features, out = kl.out_features, NB = kl.num_logistic;
+  const int NS = kl.grid_size + kl.spline_order;
+  if (t < out * in) {
+    const int o = t / in, i = t % in;
+    const float sc = kl.spline_scaler ? kl.spline_scaler[t] : 1.0f;
+    float dsc = 0.f;
+    for (int c = 0; c < NS; ++c) {
+      const float ds = d_scaled[(int64_t)t * NS + c];
+      put(gr.spline_weight ? gr.spline_weight + (int64_t)t * NS + c : nullptr, ds * sc, accumulate);
+      dsc += ds * kl.spline_weight[(int64_t)t * NS + c];
+    }
+    if (kl.spline_scaler) put(gr.spline_scaler ? gr.spline_scaler + t : nullptr, dsc, accumulate);
+    (void)o;
+    (void)i;
+  }
+  if (NB > 0 && t < out) {
+    const float ls = kl.logistic_scaler ? kl.logistic_scaler[t] : 1.0f;
+    float dls = 0.f;
+    for (int q = 0; q < in * NB; ++q) {
+      const float dw = d_wl[(int64_t)t * in * NB + q];
+      const float lw = kl.logistic_weight[(int64_t)t * in * NB + q];
+      put(gr.logistic_weight ? gr.logistic_weight + (int64_t)t * in * NB + q : nullptr,
+          (dw * ls) * kl.scale_logistic, accumulate);
+      dls += dw * (lw * kl.scale_logistic);
+    }
+    if (kl.logistic_scaler) put(gr.logistic_scaler ? gr.logistic_scaler + t : nullptr, dls, accumulate);
+  }
+}
+
+// logistic basis parameters a, b: one block per (i, j)
+__global__ void kan_gab_kernel(fetode_kanlinear_t kl, const float* __restrict__ x, const float* __restrict__ g,
+                               int64_t B, fetode_kanlinear_grad_t gr, int accumulate) {
+  __shared__ float red[2 * RB];
+  const int in = kl.in_features, out = kl.out_features, NB = kl.num_logistic;
+  const int i = blockIdx.x / NB, j = blockIdx.x % NB;
+  const float a = kl.logistic_a[i * NB + j], bb = kl.logistic_b[i * NB + j];
+  float s[2] = {0.f, 0.f};
+  for (int64_t b = threadIdx.x; b < B; b += RB) {
+    const float xv = x[b * in + i];
+    float gphi = 0.f;
+    for (int o = 0; o < out; ++o) {
+      const float ls = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
+      gphi += g[b * out + o] * ((kl.logistic_weight[(int64_t)o * in * NB + i * NB + j] * kl.scale_logistic) * ls);
+    }
+    const float sg = sigm(a * (xv - bb));
+    const float dz = gphi * 2.0f * sg * (1.0f - sg);
+    s[0] += dz * (xv - bb);
+    s[1] += dz * (-a);
+  }
+  block_sum(s, red);
+  if (threadIdx.x == 0) {
+    put(gr.logistic_a ? gr.logistic_a + i * NB + j : nullptr, s[0], accumulate);
+    put(gr.logistic_b ? gr.logistic_b + i * NB + j : nullptr, s[1], accumulate);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// FerroelectricBasis (general branch_sign), reference formula differentiated by hand
+// ------------------------------------------------------------------------------------------
+struct FerroPoint {  // forward values of one (b, i, o, k) element
+  float th, m, u, cp, cn, bs, P;
+};
+
+__device__ __forceinline__ FerroPoint ferro_point(const fetode_ferro_t& fl, float xv, float pv, int e, int64_t b) {
+  FerroPoint q;
+  const float gs = (float)fl.gate_slope, al = (float)fl.alpha, oma = (float)(1.0 - fl.alpha);
+  const float Ec = fl.Ec[e];
+  q.bs = fl.branch_sign ? fl.branch_sign[b * fl.branch_sign_bstride + e] : 1.0f;
+  q.u = sigm(gs * (xv - pv));
+  q.cp = sigm(gs * (xv - Ec));
+  q.cn = sigm(gs * (-xv - Ec));
+  const float su = q.u * q.cp, sl = (1.0f - q.u) * q.cn;
+  const float tgt = (su * 1.0f + sl * (-1.0f)) + ((1.0f - su) - sl) * q.bs;
+  q.m = al * q.bs + oma * tgt;
+  q.th = tanhf(fl.k[e] * (xv + Ec * q.m));
+  q.P = fl.Ps[e] * q.th + fl.bias[e];
+  return q;
+}
+
+// given g on the element output (g_out[b,o]), contributions to dx and to the 5 parameters
+__device__ __forceinline__ void ferro_point_vjp(const fetode_ferro_t& fl, const FerroPoint& q, float xv, int e,
+                                                float go, float* gx, float* gk, float* gEc, float* gPs,
+                                                float* gbias, float* gcoef) {
+  const float gs = (float)fl.gate_slope, oma = (float)(1.0 - fl.alpha);
+  const float Ec = fl.Ec[e], kk = fl.k[e], Ps = fl.Ps[e], co = fl.coef[e];
+  *gcoef = go * q.P;
+  const float gP = go * co;
+  *gPs = gP * q.th;
+  *gbias = gP;
+  const float gz = gP * Ps * (1.0f - q.th * q.th);
+  const float sh = xv + Ec * q.m;
+  *gk = gz * sh;
+  const float gsh = gz * kk;
+  const float gm = gsh * Ec;
+  const float gt = gm * oma;
+  const float gsu = gt * (1.0f - q.bs), gsl = gt * (-1.0f - q.bs);
+  const float gu = gsu * q.cp - gsl * q.cn;
+  const float gcp = gsu * q.u, gcn = gsl * (1.0f - q.u);
+  const float dcp = gs * q.cp * (1.0f - q.cp), dcn = gs * q.cn * (1.0f - q.cn), du = gs * q.u * (1.0f - q.u);
+  *gx = gsh + gu * du + gcp * dcp - gcn * dcn;
+  *gEc = gsh * q.m - gcp * dcp - gcn * dcn;
+}
+
+__global__ void ferro_gx_kernel(fetode_ferro_t fl, const float* __restrict__ x, const float* __restrict__ prev,
+                                int reinit, const float* __restrict__ g, int64_t B, float* __restrict__ gx,
+                                int accumulate) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int in = fl.in_dim, out = fl.out_dim, K = fl.num_basis;
+  if (t >= B * in) return;
+  const int64_t b = t / in;
+  const int i = t % in;
+  const float xv = x[t], pv = reinit ? xv : prev[t];
+  float acc = 0.f;
+  for (int o = 0; o < out; ++o) {
+    const float go = g[b * out + o];
+    for (int k = 0; k < K; ++k) {
+      const int e = (i * out + o) * K + k;
+      const FerroPoint q = ferro_point(fl, xv, pv, e, b);
+      float dx, d1, d2, d3, d4, d5;
+      ferro_point_vjp(fl, q, xv, e, go, &dx, &d1, &d2, &d3, &d4, &d5);
+      acc += dx;
+    }
+  }
+  gx[t] = accumulate ? gx[t] + acc : acc;
+}
+
+// one block per element (i, o, k)
+__global__ void ferro_gp_kernel(fetode_ferro_t fl, const float* __restrict__ x, const float* __restrict__ prev,
+                                int reinit, const float* __restrict__ g, int64_t B, fetode_ferro_grad_t gr,
+                                int accumulate) {
+  __shared__ float red[5 * RB];
+  const int in = fl.in_dim, out = fl.out_dim, K = fl.num_basis;
+  const int e = blockIdx.x;
+  const int i = e / (out * K), o = (e / K) % out;
+  float s[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int64_t b = threadIdx.x; b < B; b += RB) {
+    const float xv = x[b * in + i], pv = reinit ? xv : prev[b * in + i];
+    const FerroPoint q = ferro_point(fl, xv, pv, e, b);
+    float dx, gk, gEc, gPs, gb, gc;
+    ferro_point_vjp(fl, q, xv, e, g[b * out + o], &dx, &gk, &gEc, &gPs, &gb, &gc);
+    s[0] += gk;
+    s[1] += gEc;
+    s[2] += gPs;
+    s[3] += gb;
+    s[4] += gc;
+  }
+  block_sum(s, red);
+  if (threadIdx.x == 0) {
+    put(gr.k ? gr.k + e : nullptr, s[0], accumulate);
+    put(gr.Ec ? gr.Ec + e : nullptr, s[1], accumulate);
+    put(gr.Ps ? gr.Ps + e : nullptr, s[2], accumulate);
+    put(gr.bias ? gr.bias + e : nullptr, s[3], accumulate);
+    put(gr.coef ? gr.coef + e : nullptr, s[4], accumulate);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t fetode_kanlinear_backward_workspace(const fetode_kanlinear_t* kl) {
+  if (!kl) return -1;
+  const int NS = kl->grid_size + kl->spline_order;
+  return (int64_t)sizeof(float) * kl->out_features * kl->in_features * (NS + kl->num_logistic);
+}
+
+int fetode_kanlinear_backward(const fetode_kanlinear_t* kl, const float* x, int64_t B, const float* g,
+                              float* gx, const fetode_kanlinear_grad_t* grads, void* workspace,
+                              int32_t accumulate, void* stream) {
+  fetode_field_t f{1, kl, nullptr};
+  int rc = validate_field(&f);
+  if (rc) return rc;
+  if (B <= 0) return FETODE_OK;
+  if (!x || !g) return set_err(FETODE_EINVAL, "null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const int in = kl->in_features, out = kl->out_features, NB = kl->num_logistic, SO = kl->spline_order;
+  const int NS = kl->grid_size + SO;
+  if (gx) {
+    const int64_t n = B * in;
+#define KGX(S) hipLaunchKernelGGL(kan_gx_kernel<S>, dim3(nblk(n, 256)), dim3(256), 0, s, *kl, x, g, B, gx, accumulate)
+    if (SO == 1) KGX(1); else if (SO == 2) KGX(2); else KGX(3);
+#undef KGX
+    LAUNCH_CHECK();
+  }
+  if (grads) {
+    if (!workspace) return set_err(FETODE_EINVAL, "kanlinear backward: workspace required for parameter grads");
+    float* d_scaled = (float*)workspace;
+    float* d_wl = d_scaled + (int64_t)out * in * NS;
+    const int nblocks = out * in * (1 + NS + NB);
+#define KGW(S) hipLaunchKernelGGL(kan_gw_kernel<S>, dim3(nblocks), dim3(RB), 0, s, *kl, x, g, B, d_scaled, d_wl, *grads, accumulate)
+    if (SO == 1) KGW(1); else if (SO == 2) KGW(2); else KGW(3);
+#undef KGW
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(kan_scale_grads_kernel, dim3(nblk((int64_t)out * in, 128)), dim3(128), 0, s, *kl, d_scaled,
+                       d_wl, *grads, accumulate);
+    LAUNCH_CHECK();
+    if (NB > 0) {
+      hipLaunchKernelGGL(kan_gab_kernel, dim3(in * NB), dim3(RB), 0, s, *kl, x, g, B, *grads, accumulate);
+      LAUNCH_CHECK();
+    }
+  }
+  return FETODE_OK;
+}
+
+int fetode_ferro_backward(const fetode_ferro_t* fl, const float* x, int64_t B, const float* prev, int32_t reinit,
+                          const float* g, float* gx, const fetode_ferro_grad_t* grads, int32_t accumulate,
+                          void* stream) {
+  if (!fl || fl->in_dim <= 0 || fl->out_dim <= 0 || fl->num_basis <= 0)
+    return set_err(FETODE_EINVAL, "ferro: bad dims");
+  if (B <= 0) return FETODE_OK;
+  if (!x || !g || (!reinit && !prev)) return set_err(FETODE_EINVAL, "null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  if (gx) {
+    const int64_t n = B * fl->in_dim;
+    hipLaunchKernelGGL(ferro_gx_kernel, dim3(nblk(n, 256)), dim3(256), 0, s, *fl, x, prev, reinit, g, B, gx,
+                       accumulate);
+    LAUNCH_CHECK();
+  }
+  if (grads) {
+    hipLaunchKernelGGL(ferro_gp_kernel, dim3(fl->in_dim * fl->out_dim * fl->num_basis), dim3(RB), 0, s, *fl, x,
+                       prev, reinit, g, B, *grads, accumulate);
+    LAUNCH_CHECK();
+  }
+  return FETODE_OK;
+}
+
+}  // extern "C"

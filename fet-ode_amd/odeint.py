@@ -23,7 +23,8 @@ import numpy as np
 import torch
 
 from . import _lib
-from .autograd_ops import build_plan, field_layers, make_handle, pack_state, unpack_state
+from .autograd_ops import (axpby, build_plan, field_layers, grad_enabled_for, make_handle, pack_state,
+                           unpack_state)
 
 FIXED_METHODS = {"euler": _lib.EULER, "midpoint": _lib.MIDPOINT, "rk4": _lib.RK4,
                  "rk4_classic": _lib.RK4_CLASSIC}
@@ -164,6 +165,8 @@ def _try_fused(func, y0, sched, method_code):
     field = fused_field(func)
     if field is None or y0.dim() != 2:
         return None
+    if grad_enabled_for(y0, *field.parameters()):
+        return None   # training: per-stage path, every stage differentiable through HIP VJPs
     B = y0.shape[0]
     handle = make_handle(field, B, y0.device)
     if not _lib.load().fetode_fused_supported(handle.ref):
@@ -176,6 +179,22 @@ def _try_fused(func, y0, sched, method_code):
 # per-stage path (any func)
 # ---------------------------------------------------------------------------------------------
 
+_THIRD = float(np.float32(1.0) / np.float32(3.0))
+
+
+def _combine_coefs(method, stage, dt):
+    """d out / d (k1..k4) of each stage combine (d out / d y = 1)."""
+    if method == _lib.RK4:
+        if stage == 1:
+            return [dt * _THIRD]
+        if stage == 2:
+            return [-dt * _THIRD, dt]
+        if stage == 3:
+            return [dt, -dt, dt]
+        return [dt * 0.125, 3 * dt * 0.125, 3 * dt * 0.125, dt * 0.125]
+    return [dt]
+
+
 class _CombineFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, method, stage, dt, y, k1, k2, k3, k4):
@@ -183,11 +202,15 @@ class _CombineFn(torch.autograd.Function):
         _lib.check(_lib.load().fetode_rk_combine(method, stage, y.data_ptr(), k1.data_ptr(), _lib.ptr(k2),
                                                  _lib.ptr(k3), _lib.ptr(k4), dt, out.data_ptr(), y.numel(),
                                                  _lib.stream_handle(y.device)), "fetode_rk_combine")
+        ctx.method, ctx.stage, ctx.dt = method, stage, dt
         return out
 
     @staticmethod
     def backward(ctx, grad):
-        raise NotImplementedError("per-stage backward is not built yet")
+        cs = _combine_coefs(ctx.method, ctx.stage, ctx.dt)
+        gks = [axpby(c, grad) if ctx.needs_input_grad[4 + i] else None for i, c in enumerate(cs)]
+        gks += [None] * (4 - len(gks))
+        return (None, None, None, grad if ctx.needs_input_grad[3] else None, *gks)
 
 
 def _c(v):

@@ -149,6 +149,35 @@ int fetode_rk_combine(int32_t method, int32_t stage, const float* y, const float
                       const float* k2, const float* k3, const float* k4, float dt, float* out,
                       int64_t n, void* stream);
 
+/* out = a*x + b*y  (y nullable -> out = a*x), n elements: adjoints of the stage combines. */
+int fetode_axpby(int64_t n, float a, const float* x, float b, const float* y, float* out, void* stream);
+
+/* ---- backward (vector-Jacobian products) -------------------------------------------------
+ * Gradients of the reference's autograd through KANLinear.forward (efficientkan.py:160-182)
+ * and FerroelectricBasis.forward (ferro_class.py:368-420; prev_x is a detached snapshot,
+ * :381-382, so it receives no gradient).  Gradient buffers are (dev) pointers shaped like the
+ * parameters; NULL members are skipped.  accumulate != 0: grad += result, else grad = result.
+ * Parameter gradients are reduced over the batch in a fixed order (no atomics). */
+typedef struct fetode_kanlinear_grad {
+  float *base_weight, *spline_weight, *spline_scaler, *logistic_a, *logistic_b, *logistic_weight,
+      *logistic_scaler;
+} fetode_kanlinear_grad_t;
+
+typedef struct fetode_ferro_grad {
+  float *k, *Ec, *Ps, *bias, *coef;
+} fetode_ferro_grad_t;
+
+/* Workspace bytes needed by fetode_kanlinear_backward when grads != NULL. */
+int64_t fetode_kanlinear_backward_workspace(const fetode_kanlinear_t* layer);
+/* g (B,out) -> gx (B,in) (nullable) and parameter grads (nullable). */
+int fetode_kanlinear_backward(const fetode_kanlinear_t* layer, const float* x, int64_t B, const float* g,
+                              float* gx, const fetode_kanlinear_grad_t* grads, void* workspace,
+                              int32_t accumulate, void* stream);
+/* prev/reinit exactly as the forward call that is being differentiated used them. */
+int fetode_ferro_backward(const fetode_ferro_t* layer, const float* x, int64_t B, const float* prev,
+                          int32_t reinit, const float* g, float* gx, const fetode_ferro_grad_t* grads,
+                          int32_t accumulate, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
