@@ -78,6 +78,13 @@ SIGNATURES = {
     "fetode_rk_combine": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, _vp, _vp, _vp, _vp, _vp,
                                          ctypes.c_float, _vp, ctypes.c_int64, _vp]),
     "fetode_axpby": (ctypes.c_int, [ctypes.c_int64, ctypes.c_float, _vp, ctypes.c_float, _vp, _vp, _vp]),
+    "fetode_lincomb": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_float), ctypes.c_int32,
+                                      _vp, ctypes.c_int64, _vp]),
+    "fetode_scaled_rms": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_int64,
+                                         _vp, _vp]),
+    "fetode_interp_fit": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_float),
+                                         ctypes.c_float, _vp, ctypes.c_int64, _vp]),
+    "fetode_interp_eval": (ctypes.c_int, [_vp, ctypes.c_float, _vp, ctypes.c_int64, _vp]),
     "fetode_kanlinear_backward_workspace": (ctypes.c_int64, [ctypes.POINTER(KANLinearDesc)]),
     "fetode_kanlinear_backward": (ctypes.c_int, [ctypes.POINTER(KANLinearDesc), _vp, ctypes.c_int64, _vp, _vp,
                                                  ctypes.POINTER(KANLinearGrad), _vp, ctypes.c_int32, _vp]),

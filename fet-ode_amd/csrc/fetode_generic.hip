@@ -101,6 +101,9 @@ __global__ void rk_combine_kernel(int method, int stage, const float* __restrict
     else if (stage == 2) r = yv + dt * (k2[t] - k1[t] * third);
     else if (stage == 3) r = yv + dt * ((k1[t] - k2[t]) + k3[t]);
     else r = yv + (((k1[t] + 3.0f * (k2[t] + k3[t])) + k4[t]) * dt) * 0.125f;
+  } else if (method == FETODE_RK4_CLASSIC && stage == 4) {
+    // train_kan_fet_ett.py:76: z + (h/6) * (k1 + 2*k2 + 2*k3 + k4), dt = fp32(h/6)
+    r = yv + dt * (((k1[t] + 2.0f * k2[t]) + 2.0f * k3[t]) + k4[t]);
   } else {
     r = yv + dt * k1[t];
   }
@@ -180,7 +183,8 @@ int fetode_rk_combine(int32_t method, int32_t stage, const float* y, const float
                       const float* k3, const float* k4, float dt, float* out, int64_t n, void* stream) {
   if (n <= 0) return FETODE_OK;
   if (!y || !k1 || !out) return set_err(FETODE_EINVAL, "null pointer");
-  if (method == FETODE_RK4 && ((stage >= 2 && !k2) || (stage >= 3 && !k3) || (stage >= 4 && !k4)))
+  if ((method == FETODE_RK4 && ((stage >= 2 && !k2) || (stage >= 3 && !k3) || (stage >= 4 && !k4))) ||
+      (method == FETODE_RK4_CLASSIC && stage == 4 && (!k2 || !k3 || !k4)))
     return set_err(FETODE_EINVAL, "rk4 stage %d: missing k", stage);
   hipLaunchKernelGGL(rk_combine_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, method,
                      stage, y, k1, k2, k3, k4, dt, out, n);

@@ -1,0 +1,198 @@
+"""Dormand–Prince 5(4) — torchdiffeq's default ``odeint`` method — on the GPU.
+
+Reference call sites: every ``odeint`` without ``method`` (train_kanfet_node_predprey.py:252,260;
+predator_prey.py:142,149) and the ECG NODEs (train_ecg_kan_fet_nn_ode.py:558-565, :1034-1041,
+rtol/atol 1e-2/1e-3 at :1196-1197).  The control flow restates torchdiffeq's
+RKAdaptiveStepsizeODESolver + Dopri5Solver: f0 = func(t0, y0); one more call in
+_select_initial_step; 6 calls per attempt (FSAL), rejected attempts included — the call order
+matters for the stateful hysteresis basis (SURVEY §7.3 hard part 2).  Error ratio = RMS norm of
+err / (atol + rtol*max(|y0|,|y1|)) over the whole batch; accept if <= 1; step factor
+min(10, max(0.9*ratio^-1/5, 0.2 on reject / 1 on accept)); quartic dense output.
+
+All vector arithmetic runs in HIP kernels (fetode_lincomb, fetode_scaled_rms,
+fetode_interp_fit/eval); the accept/reject decision reads one fp32 scalar per attempt back
+to the host, as torchdiffeq does (`if accept_step:` on a 0-dim tensor).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from .autograd_ops import axpby
+
+# torchdiffeq _impl/dopri5.py tableau (float64), rounded to the state dtype like
+# RKAdaptiveStepsizeODESolver.__init__ does (tableau.to(dtype=y0.dtype))
+_A = [1 / 5, 3 / 10, 4 / 5, 8 / 9, 1., 1.]
+_BETA = [
+    [1 / 5],
+    [3 / 40, 9 / 40],
+    [44 / 45, -56 / 15, 32 / 9],
+    [19372 / 6561, -25360 / 2187, 64448 / 6561, -212 / 729],
+    [9017 / 3168, -355 / 33, 46732 / 5247, 49 / 176, -5103 / 18656],
+    [35 / 384, 0, 500 / 1113, 125 / 192, -2187 / 6784, 11 / 84],
+]
+_C_ERR = [35 / 384 - 1951 / 21600, 0, 500 / 1113 - 22642 / 50085, 125 / 192 - 451 / 720,
+          -2187 / 6784 - -12231 / 42400, 11 / 84 - 649 / 6300, -1. / 60.]
+_C_MID = [6025192743 / 30085553152 / 2, 0, 51252292925 / 65400821598 / 2, -2691868925 / 45128329728 / 2,
+          187940372067 / 1594534317056 / 2, -1776094331 / 19743644256 / 2, 11237099 / 235043384 / 2]
+
+A32 = np.array(_A, dtype=np.float64).astype(np.float32)
+BETA32 = [np.array(b, dtype=np.float64).astype(np.float32) for b in _BETA]
+CERR32 = np.array(_C_ERR, dtype=np.float64).astype(np.float32)
+CMID32 = np.array(_C_MID, dtype=np.float64).astype(np.float32)
+ORDER = 5
+
+
+def _cfloat(arr):
+    a = np.ascontiguousarray(arr, dtype=np.float32)
+    return a, a.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_float))
+
+
+class _Dopri5:
+    def __init__(self, func, y0, rtol, atol, options, reversed_):
+        unsupported = [k for k in ("step_t", "jump_t", "norm", "perturb") if options.get(k) is not None]
+        if unsupported:
+            raise NotImplementedError(f"dopri5 options not supported: {unsupported}")
+        self.lib = _lib.load()
+        self.func_user = func
+        self.sign = -1.0 if reversed_ else 1.0
+        self.y0 = y0.contiguous()
+        self.n = self.y0.numel()
+        self.dev = y0.device
+        self.stream = _lib.stream_handle(self.dev)
+        self.rtol, self.atol = float(rtol), float(atol)
+        self.first_step = options.get("first_step")
+        self.safety = float(options.get("safety", 0.9))
+        self.ifactor = float(options.get("ifactor", 10.0))
+        self.dfactor = float(options.get("dfactor", 0.2))
+        self.min_step = float(options.get("min_step", 0.0))
+        self.max_step = float(options.get("max_step", math.inf))
+        self.max_num_steps = int(options.get("max_num_steps", 2 ** 31 - 1))
+        self.k = torch.empty(7, self.n, device=self.dev, dtype=torch.float32)
+        self.scal = torch.empty(2, device=self.dev, dtype=torch.float32)
+        self.nfev = 0
+        self.attempts = []   # (t0, dt, error_ratio, accepted) like the oracle's Dopri5Trace
+
+    # func with torchdiffeq's _PerturbFunc (t cast to the state dtype) and _ReverseFunc
+    def f(self, t: float, y: torch.Tensor) -> torch.Tensor:
+        self.nfev += 1
+        tt = torch.tensor(self.sign * t, dtype=torch.float64).to(y.dtype)
+        out = self.func_user(tt, y.view_as(self.y0))
+        if torch.is_grad_enabled() and out.requires_grad:
+            raise NotImplementedError("backpropagation through the GPU dopri5 solver is not built yet; "
+                                      "use method='rk4' for training, or torch.no_grad() for inference")
+        _lib.require_gpu_tensor(out, "odeint func output")
+        out = out.reshape(-1)
+        if self.sign < 0:
+            out = axpby(-1.0, out)
+        return out.contiguous()
+
+    def lincomb(self, y0, coefs, out=None):
+        c, cp = _cfloat(coefs)
+        out = torch.empty(self.n, device=self.dev, dtype=torch.float32) if out is None else out
+        _lib.check(self.lib.fetode_lincomb(_lib.ptr(y0), self.k.data_ptr(), self.n, cp, len(c), out.data_ptr(),
+                                           self.n, self.stream), "fetode_lincomb")
+        return out
+
+    def rms(self, a, sub, y0, y1, check_finite=False) -> float:
+        _lib.check(self.lib.fetode_scaled_rms(a.data_ptr(), _lib.ptr(sub), y0.data_ptr(), _lib.ptr(y1),
+                                              self.rtol, self.atol, self.n, self.scal.data_ptr(), self.stream),
+                   "fetode_scaled_rms")
+        r, bad = self.scal.tolist()           # one device->host read per call
+        if check_finite and bad:
+            raise AssertionError("non-finite values in state `y`")
+        return np.float32(r)
+
+    def select_initial_step(self, t0: float, y0, f0) -> float:
+        """misc._select_initial_step in fp32 (the state dtype), returned as float64."""
+        f32 = np.float32
+        d0 = abs(self.rms(y0, None, y0, None))
+        d1 = abs(self.rms(f0, None, y0, None))
+        if d0 < 1e-5 or d1 < 1e-5:
+            h0 = f32(1e-6)
+        else:
+            h0 = f32(f32(0.01) * d0) / d1
+        h0 = abs(f32(h0))
+        self.k[0].copy_(f0)
+        y1 = self.lincomb(y0, [h0])
+        f1 = self.f(t0 + float(h0), y1)
+        d2 = abs(f32(self.rms(f1, f0, y0, None)) / h0)
+        if d1 <= 1e-15 and d2 <= 1e-15:
+            h1 = max(f32(1e-6), f32(h0 * f32(1e-3)))
+        else:
+            h1 = f32(np.power(f32(0.01) / max(d1, d2), f32(1.0 / float(ORDER - 1 + 1))))
+        return float(min(f32(100 * h0), abs(h1)))
+
+    def integrate(self, tp: torch.Tensor) -> torch.Tensor:
+        t = tp.to(torch.float64).tolist()
+        T = len(t)
+        sol = torch.empty(T, *self.y0.shape, device=self.dev, dtype=torch.float32)
+        sol[0] = self.y0
+        y = self.y0.reshape(-1).clone()
+        f0 = self.f(t[0], y)
+        dt = float(self.first_step) if self.first_step is not None else self.select_initial_step(t[0], y, f0)
+        t0_state, t1_state = t[0], t[0]
+        coeffs = None
+        for i in range(1, T):
+            next_t = t[i]
+            n_steps = 0
+            while next_t > t1_state:
+                assert n_steps < self.max_num_steps, "max_num_steps exceeded"
+                t0 = t1_state
+                assert t0 + dt > t0, "underflow in dt {}".format(dt)
+                dt32 = np.float32(dt)
+                t1 = t0 + dt
+                # _runge_kutta_step
+                self.k[0].copy_(f0)
+                yi = None
+                for s in range(6):
+                    ti = t1 if A32[s] == 1.0 else float(np.float32(t0) + A32[s] * dt32)
+                    yi = self.lincomb(y, BETA32[s] * dt32)
+                    self.k[s + 1].copy_(self.f(ti, yi))
+                y1 = yi
+                err = self.lincomb(None, CERR32 * dt32)
+                ratio = self.rms(err, None, y, y1, check_finite=True)
+                accept = bool(ratio <= 1)
+                self.attempts.append((t0, dt, float(ratio), accept))
+                if accept:
+                    coeffs = torch.empty(5, self.n, device=self.dev, dtype=torch.float32)
+                    _, mp = _cfloat(CMID32 * dt32)
+                    _lib.check(self.lib.fetode_interp_fit(y.data_ptr(), y1.data_ptr(), self.k.data_ptr(), self.n,
+                                                          mp, dt32, coeffs.data_ptr(), self.n, self.stream),
+                               "fetode_interp_fit")
+                    y = y1
+                    f0 = self.k[6].clone()
+                    t0_state, t1_state = t0, t1
+                else:
+                    t0_state = t0
+                dt = self.optimal_step(dt, ratio)
+                n_steps += 1
+            x = np.float32((next_t - t0_state) / (t1_state - t0_state))
+            out = sol[i].view(-1)
+            _lib.check(self.lib.fetode_interp_eval(coeffs.data_ptr(), x, out.data_ptr(), self.n, self.stream),
+                       "fetode_interp_eval")
+        return sol
+
+    def optimal_step(self, dt: float, ratio) -> float:
+        """rk_common._optimal_step_size in float64."""
+        r = float(ratio)
+        if r == 0:
+            nxt = dt * self.ifactor
+        else:
+            dfac = 1.0 if r < 1 else self.dfactor
+            if math.isnan(r):
+                factor = math.nan
+            else:
+                factor = min(self.ifactor, max(self.safety / r ** (1.0 / ORDER), dfac))
+            nxt = dt * factor
+        return min(max(nxt, self.min_step), self.max_step) if not math.isnan(nxt) else nxt
+
+
+def dopri5_solve(func, y0, tc, tp, reversed_, rtol, atol, options):
+    solver = _Dopri5(func, y0, rtol, atol, options, reversed_)
+    sol = solver.integrate(tp)
+    dopri5_solve.last = solver   # exposes nfev / attempts for tests and tooling
+    return sol

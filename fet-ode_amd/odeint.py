@@ -192,6 +192,8 @@ def _combine_coefs(method, stage, dt):
         if stage == 3:
             return [dt, -dt, dt]
         return [dt * 0.125, 3 * dt * 0.125, 3 * dt * 0.125, dt * 0.125]
+    if method == _lib.RK4_CLASSIC and stage == 4:
+        return [dt, 2 * dt, 2 * dt, dt]
     return [dt]
 
 
@@ -252,7 +254,7 @@ def _per_stage_fixed(func, y0, sched: Schedule, method: str, tc_dtype, reversed_
             k2 = func(tt(t0 + 0.5 * (t1 - t0)), _combine(_lib.EULER, 4, hh, y, k1))
             k3 = func(tt(t0 + 0.5 * (t1 - t0)), _combine(_lib.EULER, 4, hh, y, k2))
             k4 = func(tt(t1), _combine(_lib.EULER, 4, dt, y, k3))
-            raise NotImplementedError("rk4_classic per-stage combine")  # fused path only for now
+            y1 = _combine(_lib.RK4_CLASSIC, 4, h6, y, k1, k2, k3, k4)
         while j < sched.T and sched.out_step[j] == s:
             m = sched.out_mode[j]
             if m == 0:

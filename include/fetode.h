@@ -144,13 +144,31 @@ int fetode_ferro_forward(const fetode_ferro_t* layer, const float* x, int64_t B,
  *   rk4 (3/8, rk_common.rk4_alt_step_func):
  *     stage 1: out = y + (dt*k1)*(1/3)     stage 2: out = y + dt*(k2 - k1*(1/3))
  *     stage 3: out = y + dt*(k1 - k2 + k3) stage 4: out = y + ((k1 + 3*(k2+k3)) + k4)*dt*0.125
- *   euler: stage 4 form out = y + dt*k1.   k2..k4 may be NULL when unused. */
+ *   rk4_classic stage 4: out = y + dt*(((k1 + 2*k2) + 2*k3) + k4) with dt = fp32(h/6);
+ *   any other (method, stage): out = y + dt*k1 (Euler / Midpoint / classic-rk4 stage inputs).
+ *   k2..k4 may be NULL when unused. */
 int fetode_rk_combine(int32_t method, int32_t stage, const float* y, const float* k1,
                       const float* k2, const float* k3, const float* k4, float dt, float* out,
                       int64_t n, void* stream);
 
 /* out = a*x + b*y  (y nullable -> out = a*x), n elements: adjoints of the stage combines. */
 int fetode_axpby(int64_t n, float a, const float* x, float b, const float* y, float* out, void* stream);
+
+/* ---- dopri5 pieces (torchdiffeq Dopri5Solver; train_ecg_kan_fet_nn_ode.py:558-565) ---------
+ * k: (m, n) stage derivatives with row stride kstride; c: (host) m <= 8 fp32 coefficients.   */
+/* out = (y0 ? y0 : 0) + sum_{j<m} k[j]*c[j]  — rk_common._runge_kutta_step stage inputs/error */
+int fetode_lincomb(const float* y0, const float* k, int64_t kstride, const float* c, int32_t m,
+                   float* out, int64_t n, void* stream);
+/* out[0] (dev) = sqrt(mean(((a - sub) / (atol + rtol*max(|y0|,|y1|)))^2)) — misc._rms_norm of the
+ * scaled error (sub, y1 nullable: _select_initial_step's scale = atol + |y0|*rtol);
+ * out[1] = 1 if y0 holds a non-finite value (torchdiffeq's per-step assertion), else 0. */
+int fetode_scaled_rms(const float* a, const float* sub, const float* y0, const float* y1,
+                      double rtol, double atol, int64_t n, float* out, void* stream);
+/* interp._interp_fit: coeffs (5, n) = [e, d, c, b, a]; y_mid = y0 + k . mid_dt (7 host floats). */
+int fetode_interp_fit(const float* y0, const float* y1, const float* k, int64_t kstride,
+                      const float* mid_dt, float dt, float* coeffs, int64_t n, void* stream);
+/* interp._interp_evaluate at fractional position x in [0, 1]. */
+int fetode_interp_eval(const float* coeffs, float x, float* out, int64_t n, void* stream);
 
 /* ---- backward (vector-Jacobian products) -------------------------------------------------
  * Gradients of the reference's autograd through KANLinear.forward (efficientkan.py:160-182)

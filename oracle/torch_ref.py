@@ -311,7 +311,7 @@ def _check_inputs(func, y0, t, method):
         raise TypeError("`y0` must be a floating point Tensor but is a {}".format(y0.type()))
     if method is None:
         method = "dopri5"
-    if method not in ("euler", "midpoint", "rk4", "dopri5"):
+    if method not in ("euler", "midpoint", "rk4", "rk4_classic", "dopri5"):
         raise ValueError('Invalid method "{}".'.format(method))
     t = _as_time(t, y0)
     assert t.dim() == 1, "t must be one dimensional"
@@ -382,12 +382,13 @@ def rk4_alt_step(func, t0, dt, t1, y0):
 
 
 def rk4_classic_step(func, t0, dt, t1, y0):
-    """Classic RK4 (train_ecg_kan_fet_nn_ode.py:693-705, train_kan_fet_ett.py:51-83)."""
+    """Classic RK4, op order of integrate_rk4 (train_ecg_kan_fet_nn_ode.py:693-705) and
+    odeint_rk4 (train_kan_fet_ett.py:51-83, one substep per interval)."""
     k1 = func(t0, y0)
-    k2 = func(t0 + dt / 2, y0 + dt * k1 / 2)
-    k3 = func(t0 + dt / 2, y0 + dt * k2 / 2)
+    k2 = func(t0 + 0.5 * dt, y0 + 0.5 * dt * k1)
+    k3 = func(t0 + 0.5 * dt, y0 + 0.5 * dt * k2)
     k4 = func(t0 + dt, y0 + dt * k3)
-    return dt * (k1 + 2 * k2 + 2 * k3 + k4) / 6
+    return (dt / 6.0) * (k1 + 2 * k2 + 2 * k3 + k4)
 
 
 def _rms_norm(x):
@@ -538,7 +539,7 @@ def odeint(func: Callable, y0: torch.Tensor, t, *, rtol=1e-7, atol=1e-9, method=
     if method == "dopri5":
         sol = _dopri5(func, y0, t, rtol, atol, trace, first_step=options.get("first_step"))
     else:
-        step = {"euler": euler_step, "midpoint": midpoint_step,
+        step = {"euler": euler_step, "midpoint": midpoint_step, "rk4_classic": rk4_classic_step,
                 "rk4": rk4_classic_step if classic_rk4 else rk4_alt_step}[method]
         sol = _fixed_grid(func, y0, t, step, options.get("step_size"))
     return sol

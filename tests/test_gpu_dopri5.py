@@ -1,0 +1,141 @@
+"""GPU dopri5 (torchdiffeq's default method) vs the oracle restatement and its golden trace."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_sd, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def lv_field(t, X):
+    """train_kanfet_node_predprey.py:41-47 with alpha, beta, gamma, delta = 1.5, 1, 3, 1."""
+    x, y = X[..., 0], X[..., 1]
+    return torch.stack([1.5 * x - x * y, x * y - 3.0 * y], -1)
+
+
+@pytest.mark.parametrize("first_step", [None, 0.1])
+def test_dopri5_lv_vs_oracle_and_lsoda(dev, first_step):
+    """Adaptive control in fp32: when an attempt's error ratio is itself at rounding level
+    (the automatically selected first step gives ~2e-5), GPU and CPU summation orders can pick
+    different next steps, so only the accuracy is compared; with first_step=0.1 every ratio is
+    well above rounding noise and the attempt sequences must coincide."""
+    import fet_ode_amd as F
+    from oracle import torch_ref as O
+    g = load_golden("lv_lsoda")
+    t = torch.from_numpy(g["t"]).float()
+    y0 = torch.tensor([[1.0, 1.0]])
+    opts = None if first_step is None else {"first_step": first_step}
+    with torch.no_grad():
+        gpu = F.odeint(lv_field, y0.to(dev), t, rtol=1e-3, atol=1e-5, options=opts).cpu()
+    tr = O.Dopri5Trace()
+    cpu = O.odeint(lv_field, y0, t, rtol=1e-3, atol=1e-5, trace=tr, options=opts)
+    solver = F.dopri5.dopri5_solve.last
+    assert solver.nfev == 2 + 6 * len(solver.attempts) - (1 if first_step else 0)
+    if first_step is not None:
+        # identical control decisions until fp32 noise in the ratios (~1e-4 rel) compounds
+        n = 20
+        assert [a[3] for a in solver.attempts[:n]] == [a[3] for a in tr.attempts[:n]]
+        np.testing.assert_allclose([a[1] for a in solver.attempts[:n]], [a[1] for a in tr.attempts[:n]],
+                                   rtol=1e-3)
+    assert abs(len(solver.attempts) - len(tr.attempts)) <= 0.1 * len(tr.attempts)
+    # as accurate as the reference CPU solve, against the LSODA truth
+    truth = torch.from_numpy(g["soln"])
+    e_gpu = (gpu[:, 0].double() - truth).abs().max().item()
+    e_cpu = (cpu[:, 0].double() - truth).abs().max().item()
+    assert e_gpu <= 2 * e_cpu + 1e-3, (e_gpu, e_cpu)
+
+
+def test_dopri5_kanfet_trace(dev):
+    """Golden trace (tests/golden/dopri5_kanfet.npz): same attempt sequence (accept/reject
+    pattern and step sizes) and the same dense output as the reference modules + restated
+    solver.  Each attempt makes 6 stateful hysteresis calls, rejected ones included."""
+    import fet_ode_amd as F
+    g = load_golden("dopri5_kanfet")
+    m = F.KANFET([2, 10, 2], grid_size=5)
+    m.load_state_dict(golden_sd(g))
+    m = m.to(dev)
+    with torch.no_grad():
+        sol = F.odeint(lambda tt, yy: m(yy), torch.from_numpy(g["y0"]).to(dev), torch.from_numpy(g["t"]),
+                       rtol=1e-3, atol=1e-4).cpu()
+    solver = F.dopri5.dopri5_solve.last
+    att = np.array([[a[0], a[1], a[2], float(a[3])] for a in solver.attempts])
+    exp = g["attempts"]
+    assert att.shape == exp.shape, (att.shape, exp.shape)
+    np.testing.assert_array_equal(att[:, 3], exp[:, 3])
+    np.testing.assert_allclose(att[:, 1], exp[:, 1], rtol=1e-3)   # dt ~ ratio^-1/5
+    np.testing.assert_allclose(att[:, 2], exp[:, 2], rtol=1e-2, atol=1e-6)  # ill-conditioned field
+    assert solver.nfev == int(g["nfev"])
+    ref = torch.from_numpy(g["sol"])
+    assert ((sol - ref).norm(dim=(1, 2)) / ref.norm(dim=(1, 2))).max() < 1e-4
+
+
+def test_dopri5_kan_strict(dev):
+    import fet_ode_amd as F
+    from oracle import torch_ref as O
+    g = load_golden("traj_kan")
+    sd = golden_sd(g)
+    m = F.KAN([2, 10, 2], grid_size=5)
+    m.load_state_dict(sd)
+    m = m.to(dev)
+    ref = O.KANRef([O.KANLinearParams.from_state_dict(sd, f"layers.{l}.") for l in range(2)])
+    y0 = torch.from_numpy(g["y0_B64"])
+    t = torch.tensor([0.0, 0.5, 1.0, 2.0])
+    with torch.no_grad():
+        gpu = F.odeint(F.autonomous(m), y0.to(dev), t, rtol=1e-5, atol=1e-7).cpu()
+        cpu = O.odeint(lambda tt, yy: ref(yy), y0, t, rtol=1e-5, atol=1e-7)
+    assert ((gpu - cpu).norm(dim=(1, 2)) / cpu.norm(dim=(1, 2))).max() < 1e-5
+
+
+@pytest.mark.parametrize("method", ["rk4", "dopri5", "euler", "midpoint"])
+def test_reversed_time(dev, method):
+    """torchdiffeq integrates decreasing t by negating time and the field (_ReverseFunc)."""
+    import fet_ode_amd as F
+    from oracle import torch_ref as O
+    y0 = torch.tensor([[1.0, 1.0], [2.0, 0.5]])
+    t = torch.linspace(2.0, 0.0, 9)
+    with torch.no_grad():
+        gpu = F.odeint(lv_field, y0.to(dev), t, method=method).cpu()
+    cpu = O.odeint(lv_field, y0, t, method=method)
+    assert (gpu - cpu).abs().max() < 1e-4 * cpu.abs().max()
+
+
+def test_fused_reversed_and_step_size(dev):
+    """Fused single-launch path: decreasing t and options={'step_size'} with linear interpolation."""
+    import fet_ode_amd as F
+    from oracle import torch_ref as O
+    g = load_golden("traj_kan")
+    sd = golden_sd(g)
+    m = F.KAN([2, 10, 2], grid_size=5)
+    m.load_state_dict(sd)
+    m = m.to(dev)
+    ref = O.KANRef([O.KANLinearParams.from_state_dict(sd, f"layers.{l}.") for l in range(2)])
+    y0 = torch.from_numpy(g["y0_B64"])
+    for t, opts in ((torch.linspace(1.0, 0.0, 6), None), (torch.tensor([0.0, 0.13, 0.5, 0.77]), {"step_size": 0.1})):
+        for method in ("rk4", "euler", "midpoint"):
+            with torch.no_grad():
+                gpu = F.odeint(F.autonomous(m), y0.to(dev), t, method=method, options=opts).cpu()
+            cpu = O.odeint(lambda tt, yy: ref(yy), y0, t, method=method, options=opts)
+            err = ((gpu - cpu).norm(dim=(1, 2)) / cpu.norm(dim=(1, 2))).max()
+            assert err < 1e-5, (method, opts, err)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_rk4_classic_fused_and_per_stage(dev, fused):
+    """method='rk4_classic' = the reference's own fixed-step RK4 helpers
+    (train_ecg_kan_fet_nn_ode.py:693-705, train_kan_fet_ett.py:51-83)."""
+    import fet_ode_amd as F
+    from oracle import torch_ref as O
+    g = load_golden("traj_kan")
+    sd = golden_sd(g)
+    m = F.KAN([2, 10, 2], grid_size=5)
+    m.load_state_dict(sd)
+    m = m.to(dev)
+    ref = O.KANRef([O.KANLinearParams.from_state_dict(sd, f"layers.{l}.") for l in range(2)])
+    y0 = torch.from_numpy(g["y0_B64"])
+    t = torch.from_numpy(g["t35"])
+    func = F.autonomous(m) if fused else (lambda tt, yy: m(yy))
+    with torch.no_grad():
+        gpu = F.odeint(func, y0.to(dev), t, method="rk4_classic").cpu()
+    cpu = O.odeint(lambda tt, yy: ref(yy), y0, t, method="rk4_classic")
+    assert ((gpu - cpu).norm(dim=(1, 2)) / cpu.norm(dim=(1, 2))).max() < 1e-5

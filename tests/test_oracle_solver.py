@@ -101,3 +101,23 @@ def test_input_errors():
         O.odeint(lambda t, y: y, torch.ones(2), torch.tensor([0.0, 1.0]), method="nope")
     with pytest.raises(AssertionError):
         O.odeint(lambda t, y: y, torch.ones(2), torch.tensor([0.0, 1.0, 0.5]))
+
+
+def test_classic_rk4_is_option_of_fixed_grid():
+    """method='rk4_classic' (fet_ode_amd extension) reproduces odeint_rk4 of
+    train_kan_fet_ett.py:51-83 with n_substeps=1."""
+    f = lambda t, y: torch.sin(y) - 0.3 * y
+    y0 = torch.tensor([0.4, -1.2], dtype=torch.float64)
+    t = torch.linspace(0, 2, 9, dtype=torch.float64)
+    a = O.odeint(f, y0, t, method="rk4", classic_rk4=True)
+    z = y0
+    out = [z]
+    for i in range(len(t) - 1):
+        h = t[i + 1] - t[i]
+        k1 = f(t[i], z)
+        k2 = f(t[i] + 0.5 * h, z + 0.5 * h * k1)
+        k3 = f(t[i] + 0.5 * h, z + 0.5 * h * k2)
+        k4 = f(t[i] + h, z + h * k3)
+        z = z + (h / 6.0) * (k1 + 2 * k2 + 2 * k3 + k4)
+        out.append(z)
+    assert torch.allclose(a, torch.stack(out), atol=1e-14)
