@@ -1,0 +1,82 @@
+"""Trajectory-sharded data parallelism over the GPUs of one node.
+
+The reference runs one process on one device and never communicates.  Here the
+batch of trajectories is split into contiguous blocks, one per rank (one process per GPU,
+``torch.distributed`` with the "nccl" backend = RCCL over xGMI).  The forward solve needs no
+communication: every trajectory and its hysteresis state (ferro_class.py:373-378, per sample)
+live on one rank.  Training adds ONE all-reduce per iteration: all parameter gradients
+flattened into a single fp32 bucket (12.2 KB for KANFET [2,10,2]) — a latency-bound message
+on xGMI, so one fused bucket and no pipelining.
+
+Caveat kept from the reference semantics: a fresh FerroelectricBasis re-initialises prev_x
+(dx = 0) on its first call unless the batch is 1 (ferro_class.py:373-375).  Sharding a global
+batch B > 1 into shards of size 1 would flip that rule, so ``shard_bounds`` refuses it.
+"""
+from __future__ import annotations
+
+from typing import Iterable, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def world() -> Tuple[int, int]:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def shard_bounds(global_batch: int, rank: int, world_size: int) -> Tuple[int, int]:
+    """Contiguous [lo, hi) block of the global batch for ``rank`` (sizes differ by at most 1)."""
+    if world_size < 1 or not 0 <= rank < world_size:
+        raise ValueError("bad rank/world")
+    base, rem = divmod(global_batch, world_size)
+    lo = rank * base + min(rank, rem)
+    hi = lo + base + (1 if rank < rem else 0)
+    if global_batch > 1 and (hi - lo) == 1:
+        raise ValueError("a shard of 1 trajectory would flip FerroelectricBasis' first-call rule "
+                         "(ferro_class.py:373-375); use fewer ranks or a larger batch")
+    if hi <= lo:
+        raise ValueError("more ranks than trajectories")
+    return lo, hi
+
+
+def shard(x: torch.Tensor, rank: Optional[int] = None, world_size: Optional[int] = None, dim: int = 0):
+    r, w = world()
+    rank = r if rank is None else rank
+    world_size = w if world_size is None else world_size
+    lo, hi = shard_bounds(x.shape[dim], rank, world_size)
+    return x.narrow(dim, lo, hi - lo)
+
+
+def broadcast_parameters(module: torch.nn.Module, src: int = 0) -> None:
+    """Identical initial weights on every rank (one flat broadcast)."""
+    _, w = world()
+    if w == 1:
+        return
+    ps = [p.data for p in module.parameters()]
+    flat = torch._utils._flatten_dense_tensors(ps)
+    dist.broadcast(flat, src)
+    for p, f in zip(ps, torch._utils._unflatten_dense_tensors(flat, ps)):
+        p.copy_(f)
+
+
+def allreduce_gradients(params: Iterable[torch.nn.Parameter], average: bool = True,
+                        weights: Optional[float] = None) -> None:
+    """Sum (or average) the gradients of ``params`` over ranks in ONE flat all-reduce.
+
+    ``weights``: this rank's share of the global batch (e.g. B_local / B_global) when the loss
+    is a per-rank mean over unequal shards; the result is then the global-mean gradient.
+    """
+    _, w = world()
+    grads: List[torch.Tensor] = [p.grad for p in params if p.grad is not None]
+    if w == 1 or not grads:
+        return
+    flat = torch._utils._flatten_dense_tensors(grads)
+    if weights is not None:
+        flat.mul_(weights)
+    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+    if weights is None and average:
+        flat.div_(w)
+    for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+        g.copy_(f)
