@@ -377,6 +377,313 @@ __global__ __launch_bounds__(NT) void fused_integrate_kernel(FusedArgs a) {
   }
 }
 
+
+// =============================================================================================
+// v3: merged phases, DPP reductions — D = 2 state, depth-2 field, hidden width H <= 10.
+//
+// One wave = 2 trajectories (32 lanes each = 2 rows of 16).  Per evaluation:
+//   (1) RK combine on every lane of row d (state dim d lives, replicated, in row d), then the
+//       layer-0 features of input d on row d: logistic (d, j) on lane c = j < NB, SiLU / knot
+//       interval / hysteresis gate on lane c = NB (its prev_x[d] lives in that lane's register);
+//   (2) sync; layer-0 edges: lane (o, c), o < H in groups of 3 lanes, 5 groups per row; each
+//       group reduces with DPP row shifts and ends with h_o on all 3 lanes, then computes the
+//       layer-1 features of input o (logistic j = c + 3r; SiLU / interval / gate on c = 0);
+//   (3) sync; layer-1 edges: lane (o = row, c) over the 16 lanes of the row; DPP row_ror
+//       reduction leaves k_o on every lane of row o — exactly where the combine needs it.
+// =============================================================================================
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF,
+                                                               false));
+}
+// sum over the 16 lanes of a row, result on every lane of the row
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp<0x128>(v);  // row_ror:8
+  v += dpp<0x124>(v);  // row_ror:4
+  v += dpp<0x122>(v);  // row_ror:2
+  v += dpp<0x121>(v);  // row_ror:1
+  return v;
+}
+// sum over lanes 3k, 3k+1, 3k+2 of a row (k < 5), result on all three
+__device__ __forceinline__ float group3_sum(float v, int c) {
+  const float s0 = v + dpp<0x101>(v) + dpp<0x102>(v);  // row_shl:1, row_shl:2 -> valid at c == 0
+  const float b1 = dpp<0x111>(s0);                      // row_shr:1 -> lane 3k+1 gets s0[3k]
+  const float b2 = dpp<0x112>(s0);                      // row_shr:2 -> lane 3k+2 gets s0[3k]
+  return c == 0 ? s0 : (c == 1 ? b1 : b2);
+}
+
+template <int IN, int NFL>
+struct V3Lds {            // per-trajectory features of one layer's inputs
+  float F[IN * NFL];      // SiLU, logistic
+  float G[IN * 4];        // x, w, exp(gs x), u
+  int M[IN];              // knot interval (NI row = zero)
+};
+
+template <int NG, bool FERRO>
+__device__ __forceinline__ void v3_misc(float x, float& prev, bool reinit, const float* __restrict__ knots,
+                                        const float* __restrict__ rh, float gsl2e, float wc, float* F, float* G,
+                                        int* M) {
+  constexpr int NI = NG - 1;
+  F[0] = silu(x);
+  int m = -1;
+#pragma unroll
+  for (int j = 0; j < NG; ++j) m += (x >= knots[j]) ? 1 : 0;
+  float u;
+  if (!__builtin_isfinite(x)) {
+    m = NI;
+    u = __builtin_nanf("");
+  } else if (m < 0 || m >= NI) {
+    m = NI;
+    u = 0.f;
+  } else {
+    u = (x - knots[m]) * rh[m];
+  }
+  *M = m;
+  G[3] = u;
+  if constexpr (FERRO) {
+    const float pv = reinit ? x : prev;
+    const float up = rcp(1.0f + ex2(-gsl2e * (x - pv)));
+    G[0] = x;
+    G[1] = wc * (1.0f - up);
+    G[2] = ex2(gsl2e * x);
+    prev = x;  // ferro_class.py:409
+  }
+}
+
+template <int IN, int NFL, int NI, int K, int C, int EPL, int FPL, int SPL, bool FERRO, bool FACT>
+__device__ __forceinline__ float v3_edges(const V3Lds<IN, NFL>& L, const float* __restrict__ sp, int o, int c,
+                                          bool act, const float* ep, const float* k2, const float* k2Ec,
+                                          const float* cps, const float* fw, float gsl2e) {
+  float acc = 0.f;
+  if constexpr (FERRO) {
+#pragma unroll
+    for (int r = 0; r < EPL; ++r) {
+      const int p = c + C * r;
+      const int i = (p < IN * K ? p : 0) / K;   // padded elements carry zero weight
+      const float x = L.G[4 * i], w = L.G[4 * i + 1];
+      float s;
+      if constexpr (FACT) s = rcp(1.0f + L.G[4 * i + 2] * ep[r]);
+      else s = rcp(1.0f + ex2(ffma(gsl2e, x, ep[r])));
+      const float m = ffma(w, s, 1.0f);
+      const float z = ffma(k2Ec[r], m, k2[r] * x);
+      const float th = ffma(-2.0f, rcp(1.0f + ex2(z)), 1.0f);
+      acc = ffma(cps[r], th, acc);
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < FPL; ++f) {
+    const int q = c + C * f;
+    acc = ffma(fw[f], L.F[q < IN * NFL ? q : 0], acc);
+  }
+#pragma unroll
+  for (int r = 0; r < SPL; ++r) {
+    const int i = c + C * r;
+    if (i < IN) {
+      const float u = L.G[4 * i + 3];
+      const float4 cf = *reinterpret_cast<const float4*>(&sp[((o * IN + i) * (NI + 1) + L.M[i]) * 4]);
+      acc += ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
+    }
+  }
+  return act ? acc : 0.f;
+}
+
+template <int H, int K_, int NB, int NG, bool FERRO>
+__global__ __launch_bounds__(64) void fused3_kernel(FusedArgs a) {
+  constexpr int D = 2, NI = NG - 1, NFL = 1 + NB, K = FERRO ? K_ : 0;
+  static_assert(H <= 10 && NB <= 15 && NB >= 1, "v3 layout: H <= 10 groups of 3, NB logistic lanes + 1");
+  // layer 0 (2 -> H): groups of C0 = 3 lanes
+  constexpr int C0 = 3, EPL0 = K > 0 ? (D * K + C0 - 1) / C0 : 0, FPL0 = (D * NFL + C0 - 1) / C0;
+  constexpr int SPL0 = (D + C0 - 1) / C0;
+  // layer 1 (H -> 2): the 16 lanes of a row
+  constexpr int C1 = 16, EPL1 = K > 0 ? (H * K + C1 - 1) / C1 : 0, FPL1 = (H * NFL + C1 - 1) / C1;
+  constexpr int SPL1 = (H + C1 - 1) / C1;
+  constexpr int LJ1 = (NB + C0 - 1) / C0;  // layer-1 logistic jobs per group lane
+  constexpr int SPT0 = H * D * (NI + 1) * 4, SPT1 = D * H * (NI + 1) * 4;
+
+  __shared__ __attribute__((aligned(16))) float s_sp0[SPT0];
+  __shared__ __attribute__((aligned(16))) float s_sp1[SPT1];
+  __shared__ float s_kn0[D * NG], s_rh0[D * NI], s_kn1[H * NG], s_rh1[H * NI], s_c0[H], s_c1[D];
+  __shared__ V3Lds<D, NFL> s_L0[2];
+  __shared__ V3Lds<H, NFL> s_L1[2];
+
+  const int tid = threadIdx.x;
+  const int g = tid >> 5, lane = tid & 31, row = lane >> 4, c1 = lane & 15;
+  const int64_t b = (int64_t)blockIdx.x * 2 + g;
+  const bool valid = b < a.B;
+  V3Lds<D, NFL>& L0 = s_L0[g];
+  V3Lds<H, NFL>& L1 = s_L1[g];
+
+  for (int i = tid; i < SPT0; i += 64) s_sp0[i] = a.plan[a.P0.sp + i];
+  for (int i = tid; i < SPT1; i += 64) s_sp1[i] = a.plan[a.P1.sp + i];
+  for (int i = tid; i < D * NG; i += 64) s_kn0[i] = a.plan[a.P0.knots + i];
+  for (int i = tid; i < H * NG; i += 64) s_kn1[i] = a.plan[a.P1.knots + i];
+  for (int i = tid; i < D * NI; i += 64) s_rh0[i] = a.plan[a.P0.rh + i];
+  for (int i = tid; i < H * NI; i += 64) s_rh1[i] = a.plan[a.P1.rh + i];
+  for (int i = tid; i < H; i += 64) s_c0[i] = a.plan[a.P0.fconst + i];
+  for (int i = tid; i < D; i += 64) s_c1[i] = a.plan[a.P1.fconst + i];
+
+  const bool fact = FERRO && a.plan[a.P0.flag] <= kFactorLimit && a.plan[a.P1.flag] <= kFactorLimit;
+
+  // ---- layer-0 edge lane (o0, cc0) ----
+  const int q = lane - 16 * row;
+  const int o0 = row * 5 + q / 3, cc0 = q % 3;
+  const bool act0 = q < 15 && o0 < H;
+  const int o0c = act0 ? o0 : 0;
+  float ep0[EPL0 > 0 ? EPL0 : 1], k20[EPL0 > 0 ? EPL0 : 1], kE0[EPL0 > 0 ? EPL0 : 1], cp0[EPL0 > 0 ? EPL0 : 1];
+  float fw0[FPL0];
+#pragma unroll
+  for (int r = 0; r < EPL0; ++r) {
+    const int p = cc0 + C0 * r;
+    const bool ok = act0 && p < D * K;
+    const int64_t idx = (int64_t)o0c * (D * K) + (ok ? p : 0);
+    const float gec = ok ? a.plan[a.P0.fe_GEc + idx] : 0.f;
+    ep0[r] = fact ? ex2(gec) : gec;
+    k20[r] = ok ? a.plan[a.P0.fe_k2 + idx] : 0.f;
+    kE0[r] = ok ? a.plan[a.P0.fe_k2Ec + idx] : 0.f;
+    cp0[r] = ok ? a.plan[a.P0.fe_CPs2 + idx] : 0.f;
+  }
+#pragma unroll
+  for (int f = 0; f < FPL0; ++f) {
+    const int qq = cc0 + C0 * f;
+    fw0[f] = (act0 && qq < D * NFL) ? a.plan[a.P0.kw + (int64_t)o0c * (D * NFL) + qq] : 0.f;
+  }
+  // ---- layer-1 edge lane (row, c1) ----
+  float ep1[EPL1 > 0 ? EPL1 : 1], k21[EPL1 > 0 ? EPL1 : 1], kE1[EPL1 > 0 ? EPL1 : 1], cp1[EPL1 > 0 ? EPL1 : 1];
+  float fw1[FPL1];
+#pragma unroll
+  for (int r = 0; r < EPL1; ++r) {
+    const int p = c1 + C1 * r;
+    const bool ok = p < H * K;
+    const int64_t idx = (int64_t)row * (H * K) + (ok ? p : 0);
+    const float gec = ok ? a.plan[a.P1.fe_GEc + idx] : 0.f;
+    ep1[r] = fact ? ex2(gec) : gec;
+    k21[r] = ok ? a.plan[a.P1.fe_k2 + idx] : 0.f;
+    kE1[r] = ok ? a.plan[a.P1.fe_k2Ec + idx] : 0.f;
+    cp1[r] = ok ? a.plan[a.P1.fe_CPs2 + idx] : 0.f;
+  }
+#pragma unroll
+  for (int f = 0; f < FPL1; ++f) {
+    const int qq = c1 + C1 * f;
+    fw1[f] = qq < H * NFL ? a.plan[a.P1.kw + (int64_t)row * (H * NFL) + qq] : 0.f;
+  }
+  // ---- feature jobs ----
+  // layer-0 features of input d = row: logistic j = c1 (< NB), misc on c1 == NB
+  const bool xlog = c1 < NB;
+  const float xna = xlog ? a.plan[a.P0.lg + 2 * (row * NB + c1)] : 0.f;
+  const float xab = xlog ? a.plan[a.P0.lg + 2 * (row * NB + c1) + 1] : 0.f;
+  const bool xmisc = c1 == NB;
+  // layer-1 features of input o0: logistic j = cc0 + 3r, misc on cc0 == 0
+  float hna[LJ1], hab[LJ1];
+#pragma unroll
+  for (int r = 0; r < LJ1; ++r) {
+    const int j = cc0 + C0 * r;
+    const bool ok = act0 && j < NB;
+    hna[r] = ok ? a.plan[a.P1.lg + 2 * (o0c * NB + j)] : 0.f;
+    hab[r] = ok ? a.plan[a.P1.lg + 2 * (o0c * NB + j) + 1] : 0.f;
+  }
+  const bool hmisc = act0 && cc0 == 0;
+
+  constexpr int SW = FERRO ? D + H : 0;
+  float prev0 = 0.f, prev1 = 0.f;  // prev_x of input `row` (xmisc lane) / of input o0 (hmisc lane)
+  if (FERRO && valid) {
+    if (xmisc) prev0 = a.state[b * SW + row];
+    if (hmisc) prev1 = a.state[b * SW + D + o0];
+  }
+  bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
+
+  float y = valid ? a.y0[b * D + row] : 0.f;   // state dim `row`, replicated over the row
+  if (!a.single_eval && valid && c1 == 0) a.solution[b * D + row] = y;
+  __syncthreads();  // tables staged
+
+  auto eval_body = [&](float xin, auto fact_tag) __attribute__((always_inline)) -> float {
+    constexpr bool F_ = decltype(fact_tag)::value;
+    // (1) layer-0 features of input `row`
+    if (xlog) L0.F[row * NFL + 1 + c1] = rcp(1.0f + ex2(ffma(xna, xin, xab)));
+    if (xmisc)
+      v3_misc<NG, FERRO>(xin, prev0, re0, &s_kn0[row * NG], &s_rh0[row * NI], a.P0.gsl2e, a.P0.wc,
+                         &L0.F[row * NFL], &L0.G[4 * row], &L0.M[row]);
+    re0 = false;
+    __syncthreads();
+    // (2) layer-0 edges -> h_o on the group, then layer-1 features of input o
+    float h = v3_edges<D, NFL, NI, K, C0, EPL0, FPL0, SPL0, FERRO, F_>(L0, s_sp0, o0c, cc0, act0, ep0, k20, kE0,
+                                                                       cp0, fw0, a.P0.gsl2e);
+    h = group3_sum(h, cc0) + s_c0[o0c];
+#pragma unroll
+    for (int r = 0; r < LJ1; ++r) {
+      const int j = cc0 + C0 * r;
+      if (act0 && j < NB) L1.F[o0 * NFL + 1 + j] = rcp(1.0f + ex2(ffma(hna[r], h, hab[r])));
+    }
+    if (hmisc)
+      v3_misc<NG, FERRO>(h, prev1, re1, &s_kn1[o0 * NG], &s_rh1[o0 * NI], a.P1.gsl2e, a.P1.wc, &L1.F[o0 * NFL],
+                         &L1.G[4 * o0], &L1.M[o0]);
+    re1 = false;
+    __syncthreads();
+    // (3) layer-1 edges -> k_row on every lane of the row
+    const float v = v3_edges<H, NFL, NI, K, C1, EPL1, FPL1, SPL1, FERRO, F_>(L1, s_sp1, row, c1, true, ep1, k21,
+                                                                             kE1, cp1, fw1, a.P1.gsl2e);
+    return row_sum16(v) + s_c1[row];
+  };
+  auto eval = [&](float xin) __attribute__((always_inline)) -> float {
+    if (fact) return eval_body(xin, std::integral_constant<bool, true>{});
+    return eval_body(xin, std::integral_constant<bool, false>{});
+  };
+
+  if (a.single_eval) {
+    const float f = eval(y);
+    if (valid && c1 == 0) a.eval_out[b * D + row] = f;
+  } else {
+    const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4
+                   : a.method == FETODE_MIDPOINT ? 2 : 1;
+    const float third = 1.0f / 3.0f;
+    int jj = 1;
+    for (int s = 0; s < a.n_steps; ++s) {
+      const float dt = a.step_coef[4 * s + 0], hh = a.step_coef[4 * s + 1], h6 = a.step_coef[4 * s + 2];
+      if (a.ckpt && valid) {
+        float* ck = a.ckpt + ((int64_t)s * a.B + b) * (D + SW);
+        if (c1 == 0) ck[row] = y;
+        if (FERRO && xmisc) ck[D + row] = prev0;
+        if (FERRO && hmisc) ck[D + D + o0] = prev1;
+      }
+      float k1 = 0.f, k2 = 0.f, k3 = 0.f, k4 = 0.f;
+      for (int st = 0; st < ns; ++st) {
+        float xin = y;
+        if (a.method == FETODE_RK4) {
+          if (st == 1) xin = y + (dt * k1) * third;
+          else if (st == 2) xin = y + dt * (k2 - k1 * third);
+          else if (st == 3) xin = y + dt * ((k1 - k2) + k3);
+        } else if (a.method == FETODE_RK4_CLASSIC) {
+          if (st == 1) xin = y + hh * k1;
+          else if (st == 2) xin = y + hh * k2;
+          else if (st == 3) xin = y + dt * k3;
+        } else if (a.method == FETODE_MIDPOINT) {
+          if (st == 1) xin = y + k1 * hh;
+        }
+        const float kk = eval(xin);
+        if (st == 0) k1 = kk;
+        else if (st == 1) k2 = kk;
+        else if (st == 2) k3 = kk;
+        else k4 = kk;
+      }
+      float y1;
+      if (a.method == FETODE_RK4) y1 = y + (((k1 + 3.0f * (k2 + k3)) + k4) * dt) * 0.125f;
+      else if (a.method == FETODE_RK4_CLASSIC) y1 = y + h6 * (((k1 + 2.0f * k2) + 2.0f * k3) + k4);
+      else if (a.method == FETODE_MIDPOINT) y1 = y + dt * k2;
+      else y1 = y + dt * k1;
+      while (jj < a.T && a.out_step[jj] == s) {
+        const int mode = a.out_mode[jj];
+        const float vv = mode == 0 ? y : (mode == 1 ? y1 : y + a.out_slope[jj] * (y1 - y));
+        if (valid && c1 == 0) a.solution[((int64_t)jj * a.B + b) * D + row] = vv;
+        ++jj;
+      }
+      y = y1;
+    }
+  }
+  if (FERRO && valid) {
+    if (xmisc) a.state[b * SW + row] = prev0;
+    if (hmisc) a.state[b * SW + D + o0] = prev1;
+  }
+}
+
 typedef void (*fused_fn)(FusedArgs);
 struct FusedEntry {
   int in0, h, out, K, NB, NG;
@@ -387,7 +694,10 @@ struct FusedEntry {
 #define FUSED(IN0, H, OUT, K, NB, NG, FE, LPT, NT) \
   {IN0, H, OUT, K, NB, NG, FE, fused_integrate_kernel<IN0, H, OUT, K, NB, NG, FE, LPT, NT>, NT, LPT}
 const FusedEntry kFused[] = {
-    // LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146)
+    // v3 (default): LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146) and LV KAN
+    {2, 10, 2, 10, 10, 12, true, fused3_kernel<10, 10, 10, 12, true>, 64, 3},
+    {2, 10, 2, 1, 10, 12, false, fused3_kernel<10, 1, 10, 12, false>, 64, 3},
+    // v2 (FETODE_FUSED_LPT=32|64, FETODE_FUSED_NT=64|256)
     FUSED(2, 10, 2, 10, 10, 12, true, 32, 64),
     FUSED(2, 10, 2, 10, 10, 12, true, 32, 256),
     FUSED(2, 10, 2, 10, 10, 12, true, 64, 64),
@@ -408,11 +718,11 @@ int preferred_nt() {
   }();
   return nt;
 }
-// lanes per trajectory: 32 (2 trajectories per wave) unless FETODE_FUSED_LPT says otherwise
+// kernel variant: 3 = v3 (merged phases, default); FETODE_FUSED_LPT=32|64 selects a v2 variant
 int preferred_lpt() {
   static int v = [] {
     const char* e = getenv("FETODE_FUSED_LPT");
-    return e ? atoi(e) : 32;
+    return e ? atoi(e) : 3;
   }();
   return v;
 }
@@ -443,7 +753,7 @@ int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
   if (!e) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
   layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
   layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
-  const int tpb = e->nt / e->lpt;
+  const int tpb = e->lpt == 3 ? 2 : e->nt / e->lpt;
   hipLaunchKernelGGL(e->fn, dim3(nblk(a.B, tpb)), dim3(e->nt), 0, (hipStream_t)stream, a);
   LAUNCH_CHECK();
   return FETODE_OK;
