@@ -198,8 +198,30 @@ def field_layers(model):
     return out
 
 
+def _handle_key(model, B, device):
+    """Identity of every tensor the descriptor points at, or None when a tensor would be
+    converted (non-fp32 / non-contiguous) — the converted copy could go stale silently."""
+    key = [B, str(device)]
+    for k, f in field_layers(model):
+        ts = [k.grid, *[p for p in kan_params(k) if p is not None]]
+        if f is not None:
+            ts += [getattr(f, n) for n in FERRO_PARAM_NAMES]
+            if f._bsign is not None:
+                ts.append(f._bsign)
+        for t in ts:
+            if t.dtype != torch.float32 or not t.is_contiguous():
+                return None
+            key += [t.data_ptr(), t._version, t.shape[0]]
+    return tuple(key)
+
+
 def make_handle(model, B: int, device) -> _lib.FieldHandle:
-    """Descriptor of the field (+ explicit branch_sign tensors; None = ones)."""
+    """Descriptor of the field (+ explicit branch_sign tensors; None = ones), cached on the model
+    while no parameter has been replaced or modified in place (tensor version counters)."""
+    key = _handle_key(model, B, device)
+    cached = getattr(model, "_fetode_handle", None)
+    if key is not None and cached is not None and cached[0] == key:
+        return cached[1]
     keep = []
     layers = field_layers(model)
     kan = [k.desc(keep) for k, _ in layers]
@@ -211,32 +233,49 @@ def make_handle(model, B: int, device) -> _lib.FieldHandle:
             if b is not None and (b.shape[0] != B or b.device != device):
                 b = None
             ferro.append(f.desc(keep, b))
-    return _lib.FieldHandle(kan, ferro, keep)
+    h = _lib.FieldHandle(kan, ferro, keep)
+    model._fetode_handle = (key, h)
+    return h
+
+
+def _state_views(buf, model, B):
+    views, off = [], 0
+    for _, f in field_layers(model):
+        views.append(buf[B * off:B * (off + f.in_dim)].view(B, f.in_dim))
+        off += f.in_dim
+    return views
 
 
 def pack_state(model, B: int, device):
-    """Concatenate the compact prev_x of every Ferro layer into (B, W); init-mask bits for the
-    layers whose stored state does not match the batch (ferro_class.py:373-375 rule)."""
+    """The fused kernels read/write the hysteresis state of all Ferro layers in one buffer laid
+    out as contiguous (B, in_l) blocks (include/fetode.h).  Each layer's compact prev_x IS a view
+    of that buffer between calls, so packing costs nothing in steady state.  Returns the buffer
+    and the init-mask bits of the layers whose stored state does not match the batch
+    (ferro_class.py:373-375 re-initialisation rule)."""
     layers = field_layers(model)
     if layers[0][1] is None:
         return None, 0
-    cols, mask = [], 0
-    for l, (_, f) in enumerate(layers):
+    W = sum(f.in_dim for _, f in layers)
+    buf = getattr(model, "_fetode_state", None)
+    if buf is None or buf.numel() != B * W or buf.device != device:
+        buf = torch.zeros(B * W, device=device, dtype=torch.float32)
+        model._fetode_state = buf
+    mask = 0
+    for l, ((_, f), v) in enumerate(zip(layers, _state_views(buf, model, B))):
         p = f._prev
         if p.shape[0] != B or p.device != device or p.dtype != torch.float32:
             mask |= 1 << l
-            cols.append(torch.zeros(B, f.in_dim, device=device, dtype=torch.float32))
-        else:
-            cols.append(p)
-    return torch.cat(cols, dim=1).contiguous(), mask
+        elif p.data_ptr() != v.data_ptr():
+            v.copy_(p)
+        f._prev = v
+    return buf, mask
 
 
 def unpack_state(model, state: torch.Tensor):
-    off = 0
-    for _, f in field_layers(model):
-        f._prev = state[:, off:off + f.in_dim].contiguous()
-        off += f.in_dim
-        if f._bsign is not None and f._bsign.shape[0] != state.shape[0]:
+    B = state.numel() // sum(f.in_dim for _, f in field_layers(model))
+    for (_, f), v in zip(field_layers(model), _state_views(state, model, B)):
+        f._prev = v
+        if f._bsign is not None and f._bsign.shape[0] != B:
             f._bsign = None
 
 

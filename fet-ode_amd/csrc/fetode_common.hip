@@ -130,9 +130,8 @@ __device__ void spline_interval_poly(const fetode_kanlinear_t& kl, const LayerPl
   dst[3] = (float)(9.0 * (-v[0] + 3.0 * v[1] - 3.0 * v[2] + v[3]) / 2.0);
 }
 
-__global__ void plan_build_kernel(LayerPlan P, fetode_kanlinear_t kl, fetode_ferro_t fl, int has_ferro,
-                                  float* __restrict__ plan) {
-  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ void plan_build_layer(const LayerPlan& P, const fetode_kanlinear_t& kl, const fetode_ferro_t& fl,
+                                 int has_ferro, float* __restrict__ plan, int tid) {
   const int in = P.in, out = P.out, K = P.K, NB = P.NB, NG = P.NG, NI = P.NI, NFL = P.NFL;
   const float l2 = FETODE_LOG2E;
   if (has_ferro) {
@@ -143,20 +142,10 @@ __global__ void plan_build_kernel(LayerPlan P, fetode_kanlinear_t kl, fetode_fer
       const float kk = fl.k[src], Ec = fl.Ec[src], Ps = fl.Ps[src], co = fl.coef[src];
       const float gec = P.gsl2e * Ec;
       plan[P.fe_GEc + tid] = gec;
-      atomicMax((unsigned int*)&plan[P.flag], __float_as_uint(fabsf(gec)));
       const float k2 = 2.0f * l2 * kk;
       plan[P.fe_k2 + tid] = k2;
       plan[P.fe_k2Ec + tid] = k2 * Ec;
       plan[P.fe_CPs2 + tid] = co * Ps;
-    }
-    if (tid < out) {
-      float s = 0.f;
-      for (int i = 0; i < in; ++i)
-        for (int k = 0; k < K; ++k) {
-          const int src = (i * out + tid) * K + k;
-          s += fl.coef[src] * fl.bias[src];
-        }
-      plan[P.fconst + tid] = s;
     }
   } else if (tid < out) {
     plan[P.fconst + tid] = 0.f;
@@ -193,6 +182,72 @@ __global__ void plan_build_kernel(LayerPlan P, fetode_kanlinear_t kl, fetode_fer
   }
 }
 
+constexpr int kPlanMaxLayers = 8;
+constexpr int kPlanBlock = 128;
+struct PlanBatch {
+  int n_layers;
+  int blk_begin[kPlanMaxLayers + 1];  // item blocks of layer l: [blk_begin[l], blk_begin[l+1])
+  LayerPlan P[kPlanMaxLayers];
+  fetode_kanlinear_t kl[kPlanMaxLayers];
+  fetode_ferro_t fl[kPlanMaxLayers];
+  int has_ferro[kPlanMaxLayers];
+};
+
+__device__ inline float wave_sum(float v) {
+  for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m, 64);
+  return v;
+}
+__device__ inline float wave_max(float v) {
+  for (int m = 32; m > 0; m >>= 1) v = fmaxf(v, __shfl_xor(v, m, 64));
+  return v;
+}
+
+// One launch for every layer: item blocks, then one tail block per Ferro layer that computes
+// the per-output constant sum_{i,k} coef*bias (one wave per output, fixed order) and the
+// factored-exp guard word max |gate_slope*log2e*Ec| — no atomics, no memset, deterministic.
+__global__ __launch_bounds__(kPlanBlock) void plan_build_kernel(PlanBatch pb, float* __restrict__ plan) {
+  constexpr int kWaves = kPlanBlock / 64;
+  __shared__ float red[kWaves];
+  const int blk = blockIdx.x;
+  const int nitem = pb.blk_begin[pb.n_layers];
+  if (blk < nitem) {
+    int l = 0;
+    while (blk >= pb.blk_begin[l + 1]) ++l;
+    plan_build_layer(pb.P[l], pb.kl[l], pb.fl[l], pb.has_ferro[l], plan,
+                     (blk - pb.blk_begin[l]) * kPlanBlock + threadIdx.x);
+    return;
+  }
+  const int l = blk - nitem;
+  const LayerPlan& P = pb.P[l];
+  if (!pb.has_ferro[l]) {
+    if (threadIdx.x == 0) plan[P.flag] = 0.f;
+    return;
+  }
+  const fetode_ferro_t& fl = pb.fl[l];
+  const int wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+  const int NIK = P.in * P.K;
+  for (int o = wave; o < P.out; o += kWaves) {
+    float s = 0.f;
+    for (int p = lane; p < NIK; p += 64) {
+      const int i = p / P.K, k = p % P.K;
+      const int src = (i * P.out + o) * P.K + k;
+      s += fl.coef[src] * fl.bias[src];
+    }
+    s = wave_sum(s);
+    if (lane == 0) plan[P.fconst + o] = s;
+  }
+  const int NE = P.in * P.out * P.K;
+  float mx = 0.f;
+  for (int e = threadIdx.x; e < NE; e += kPlanBlock) mx = fmaxf(mx, fabsf(P.gsl2e * fl.Ec[e]));
+  mx = wave_max(mx);
+  if (lane == 0) red[wave] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < kWaves; ++w) mx = fmaxf(mx, red[w]);
+    plan[P.flag] = mx;
+  }
+}
+
 }  // namespace fetode
 
 using namespace fetode;
@@ -225,20 +280,30 @@ int fetode_plan_build(const fetode_field_t* f, void* plan, void* stream) {
   if (rc) return rc;
   if (!plan) return set_err(FETODE_EINVAL, "plan is NULL");
   int64_t base = 0;
-  for (int l = 0; l < f->n_layers; ++l) {
-    LayerPlan p;
-    const fetode_ferro_t* fl = f->ferro ? &f->ferro[l] : nullptr;
-    layer_plan(f->kan[l], fl, base, &p);
-    HIP_CHECK_RET(hipMemsetAsync((float*)plan + p.flag, 0, sizeof(float), (hipStream_t)stream));
-    const int64_t n = std::max<int64_t>({(int64_t)p.out * p.in * std::max(p.K, 1), (int64_t)p.out * p.in * p.NFL,
-                                         (int64_t)p.in * p.NG, (int64_t)p.in * std::max(p.NB, 1),
-                                         (int64_t)p.out * p.in * (p.NI + 1), (int64_t)p.out});
-    fetode_ferro_t dummy;
-    memset(&dummy, 0, sizeof(dummy));
-    hipLaunchKernelGGL(plan_build_kernel, dim3(nblk(n, 128)), dim3(128), 0, (hipStream_t)stream, p,
-                       f->kan[l], fl ? *fl : dummy, fl ? 1 : 0, (float*)plan);
+  for (int l0 = 0; l0 < f->n_layers; l0 += kPlanMaxLayers) {
+    PlanBatch pb;
+    memset(&pb, 0, sizeof(pb));
+    pb.n_layers = std::min(kPlanMaxLayers, f->n_layers - l0);
+    int blocks = 0;
+    for (int j = 0; j < pb.n_layers; ++j) {
+      const int l = l0 + j;
+      const fetode_ferro_t* fl = f->ferro ? &f->ferro[l] : nullptr;
+      LayerPlan& p = pb.P[j];
+      layer_plan(f->kan[l], fl, base, &p);
+      base = p.end;
+      pb.kl[j] = f->kan[l];
+      if (fl) pb.fl[j] = *fl;
+      pb.has_ferro[j] = fl ? 1 : 0;
+      const int64_t n = std::max<int64_t>({(int64_t)p.out * p.in * std::max(p.K, 1), (int64_t)p.out * p.in * p.NFL,
+                                           (int64_t)p.in * p.NG, (int64_t)p.in * std::max(p.NB, 1),
+                                           (int64_t)p.out * p.in * (p.NI + 1), (int64_t)p.out});
+      pb.blk_begin[j] = blocks;
+      blocks += nblk(n, kPlanBlock);
+    }
+    pb.blk_begin[pb.n_layers] = blocks;
+    hipLaunchKernelGGL(plan_build_kernel, dim3(blocks + pb.n_layers), dim3(kPlanBlock), 0, (hipStream_t)stream, pb,
+                       (float*)plan);
     LAUNCH_CHECK();
-    base = p.end;
   }
   return FETODE_OK;
 }

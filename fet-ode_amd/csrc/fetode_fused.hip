@@ -278,8 +278,8 @@ __global__ __launch_bounds__(NT) void fused_integrate_kernel(FusedArgs a) {
 
   constexpr int SW = FERRO ? IN0 + H : 0;  // state width
   if (FERRO) {
-    for (int i = lane; i < IN0; i += LPT) T.L0.prev[i] = valid ? a.state[b * SW + i] : 0.f;
-    for (int i = lane; i < H; i += LPT) T.L1.prev[i] = valid ? a.state[b * SW + IN0 + i] : 0.f;
+    for (int i = lane; i < IN0; i += LPT) T.L0.prev[i] = valid ? a.state[b * IN0 + i] : 0.f;
+    for (int i = lane; i < H; i += LPT) T.L1.prev[i] = valid ? a.state[a.B * IN0 + b * H + i] : 0.f;
   }
   bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
 
@@ -372,8 +372,8 @@ __global__ __launch_bounds__(NT) void fused_integrate_kernel(FusedArgs a) {
     }
   }
   if (FERRO && valid) {
-    for (int i = lane; i < IN0; i += LPT) a.state[b * SW + i] = T.L0.prev[i];
-    for (int i = lane; i < H; i += LPT) a.state[b * SW + IN0 + i] = T.L1.prev[i];
+    for (int i = lane; i < IN0; i += LPT) a.state[b * IN0 + i] = T.L0.prev[i];
+    for (int i = lane; i < H; i += LPT) a.state[a.B * IN0 + b * H + i] = T.L1.prev[i];
   }
 }
 
@@ -586,8 +586,8 @@ __global__ __launch_bounds__(64) void fused3_kernel(FusedArgs a) {
   constexpr int SW = FERRO ? D + H : 0;
   float prev0 = 0.f, prev1 = 0.f;  // prev_x of input `row` (xmisc lane) / of input o0 (hmisc lane)
   if (FERRO && valid) {
-    if (xmisc) prev0 = a.state[b * SW + row];
-    if (hmisc) prev1 = a.state[b * SW + D + o0];
+    if (xmisc) prev0 = a.state[b * D + row];
+    if (hmisc) prev1 = a.state[a.B * D + b * H + o0];
   }
   bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
 
@@ -597,6 +597,7 @@ __global__ __launch_bounds__(64) void fused3_kernel(FusedArgs a) {
 
   auto eval_body = [&](float xin, auto fact_tag) __attribute__((always_inline)) -> float {
     constexpr bool F_ = decltype(fact_tag)::value;
+    FETODE_MARK("X_FEAT");
     // (1) layer-0 features of input `row`
     if (xlog) L0.F[row * NFL + 1 + c1] = rcp(1.0f + ex2(ffma(xna, xin, xab)));
     if (xmisc)
@@ -604,10 +605,12 @@ __global__ __launch_bounds__(64) void fused3_kernel(FusedArgs a) {
                          &L0.F[row * NFL], &L0.G[4 * row], &L0.M[row]);
     re0 = false;
     __syncthreads();
+    FETODE_MARK("EDGES0");
     // (2) layer-0 edges -> h_o on the group, then layer-1 features of input o
     float h = v3_edges<D, NFL, NI, K, C0, EPL0, FPL0, SPL0, FERRO, F_>(L0, s_sp0, o0c, cc0, act0, ep0, k20, kE0,
                                                                        cp0, fw0, a.P0.gsl2e);
     h = group3_sum(h, cc0) + s_c0[o0c];
+    FETODE_MARK("H_FEAT");
 #pragma unroll
     for (int r = 0; r < LJ1; ++r) {
       const int j = cc0 + C0 * r;
@@ -618,10 +621,13 @@ __global__ __launch_bounds__(64) void fused3_kernel(FusedArgs a) {
                          &L1.G[4 * o0], &L1.M[o0]);
     re1 = false;
     __syncthreads();
+    FETODE_MARK("EDGES1");
     // (3) layer-1 edges -> k_row on every lane of the row
     const float v = v3_edges<H, NFL, NI, K, C1, EPL1, FPL1, SPL1, FERRO, F_>(L1, s_sp1, row, c1, true, ep1, k21,
                                                                              kE1, cp1, fw1, a.P1.gsl2e);
-    return row_sum16(v) + s_c1[row];
+    const float kr = row_sum16(v) + s_c1[row];
+    FETODE_MARK("END");
+    return kr;
   };
   auto eval = [&](float xin) __attribute__((always_inline)) -> float {
     if (fact) return eval_body(xin, std::integral_constant<bool, true>{});
@@ -679,8 +685,8 @@ __global__ __launch_bounds__(64) void fused3_kernel(FusedArgs a) {
     }
   }
   if (FERRO && valid) {
-    if (xmisc) a.state[b * SW + row] = prev0;
-    if (hmisc) a.state[b * SW + D + o0] = prev1;
+    if (xmisc) a.state[b * D + row] = prev0;
+    if (hmisc) a.state[a.B * D + b * H + o0] = prev1;
   }
 }
 

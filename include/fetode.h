@@ -86,7 +86,9 @@ typedef struct fetode_field {
 
 /* Hysteresis state of a field: for every Ferro layer l a compact prev_x of shape (B, in_l)
  * (the reference stores x.expand(B,in,out,K), ferro_class.py:372,409 — constant over out,K).
- * Concatenated per trajectory: state[b, off_l + i], row length = sum of in_l over Ferro layers.
+ * Layout: one contiguous (B, in_l) block per Ferro layer, blocks concatenated in layer order:
+ * element (l, b, i) at state[B*off_l + b*in_l + i], off_l = sum of in over earlier Ferro layers
+ * (so every layer's prev_x is itself a contiguous (B, in_l) tensor); total B*state_width.
  * init_mask bit l set  =>  the reference's re-initialisation rule fires on the first call
  * (prev_x := x, i.e. dx = 0, ferro_class.py:373-375); clear => use the stored prev_x. */
 
@@ -105,7 +107,7 @@ int32_t fetode_state_width(const fetode_field_t* field);
 int fetode_fused_supported(const fetode_field_t* field);
 
 /* One stateful field evaluation out = field(x) — KANFET.forward / KAN.forward.
- * x (B, in0), out (B, out_last), state (B, state_width) updated in place to x-per-layer. */
+ * x (B, in0), out (B, out_last), state (B*state_width, layout above) updated in place. */
 int fetode_field_forward(const fetode_field_t* field, const void* plan, const float* x, int64_t B,
                          float* state, uint32_t init_mask, float* out, void* stream);
 

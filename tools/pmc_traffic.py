@@ -13,14 +13,14 @@ import os
 import sys
 from collections import defaultdict
 
-KERNEL = "fused_integrate_kernel"
+KERNEL = os.environ.get("FETODE_PMC_KERNEL", "fused")
 
 
 def counters(d):
     vals = defaultdict(list)
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if KERNEL in row.get("Kernel_Name", ""):
+            if KERNEL in row.get("Kernel_Name", "") and "plan_build" not in row.get("Kernel_Name", ""):
                 vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
 
