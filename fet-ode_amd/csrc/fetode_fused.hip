@@ -24,6 +24,38 @@
 
 using namespace fetode;
 
+// In-kernel phase timing for the v4 kernel (diagnostic build only: make stamps).  Each wave
+// accumulates s_memtime deltas per phase; the stamp waits for LDS (lgkmcnt(0)), so a stamped
+// run attributes time, it does not reproduce the unstamped schedule exactly.
+#ifdef FETODE_STAMPS
+__device__ unsigned long long* g_fetode_stamps;
+__device__ __forceinline__ unsigned long long stamp_now() {
+  unsigned long long t;
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  __builtin_amdgcn_sched_barrier(0);
+  return t;
+}
+#define STAMP_DECL            \
+  unsigned long long st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}; \
+  unsigned long long st_last = stamp_now();
+#define STAMP(p)                                  \
+  do {                                            \
+    const unsigned long long st_t = stamp_now();  \
+    st_acc[p] += st_t - st_last;                  \
+    st_last = st_t;                               \
+  } while (0)
+#define STAMP_FLUSH()                                                                \
+  do {                                                                               \
+    if (threadIdx.x == 0 && g_fetode_stamps)                                         \
+      for (int p_ = 0; p_ < 8; ++p_) g_fetode_stamps[blockIdx.x * 8 + p_] = st_acc[p_]; \
+  } while (0)
+#else
+#define STAMP_DECL
+#define STAMP(p)
+#define STAMP_FLUSH()
+#endif
+
 #ifdef FETODE_ISA_MARKERS
 #define FETODE_MARK(s) asm volatile("; MARK " s ::: "memory")
 #else
@@ -690,17 +722,564 @@ __global__ __launch_bounds__(64) void fused3_kernel(FusedArgs a) {
   }
 }
 
+// =============================================================================================
+// v4: packed-FP32 Ferro pairs, branch-free feature streams — same wave shape as v3.
+//
+// The field is VALU-issue bound: v3 spends ~320 VALU + ~60 transcendental
+// instructions per evaluation per wave.  v4 keeps v3's trajectory/row mapping and cuts the
+// VALU count:
+//   * a lane evaluates its Ferro elements two at a time, (i, k) and (i, k+1) of one input, in
+//     v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 (two fp32 lanes per instruction) with the
+//     input's x, gate factor and exp(gs x) broadcast from one ds_read_b128; only the
+//     transcendentals stay one per element;
+//   * feature weights are applied as packed FMAs over a contiguous 8-float LDS chunk;
+//   * every feature job (logistic j, SiLU, gate sigmoid, exp(gs x)) is the same
+//     sigmoid-of-affine instruction stream with per-lane constants, so the feature phases do
+//     not diverge; the knot interval is a per-lane compare + DPP row count instead of a
+//     12-step scan on one lane.
+// =============================================================================================
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 splat(float v) { return f2{v, v}; }
+__device__ __forceinline__ f2 ex2x2(f2 v) { return f2{ex2(v.x), ex2(v.y)}; }
+__device__ __forceinline__ f2 rcpx2(f2 v) { return f2{rcp(v.x), rcp(v.y)}; }
+
+template <int IN, int FLEN>
+struct V4Lds {
+  float F[FLEN];  // per input NFP floats: SiLU, logistic 0..NB-1 (2x folded into weights), zero pad
+  float4 G[IN];   // x, w = wc*(1-up), e = exp2(gs*log2e*x), u
+  int M[IN];      // knot interval (NI = zero table row)
+  float sink;     // target of idle feature jobs
+};
+
+// one Ferro element pair of one input: acc += cps * tanh(k (x - Ec m)) for both
+template <bool FACT>
+__device__ __forceinline__ f2 v4_pair(float4 g, f2 ep, f2 k2, f2 kE, f2 cp, f2 acc, float gsl2e) {
+  f2 s;
+  if constexpr (FACT) {
+    s = rcpx2(pfma(splat(g.z), ep, splat(1.0f)));               // sigma(gs(-x-Ec)), factored exp
+  } else {
+    s = rcpx2(ex2x2(pfma(splat(gsl2e), splat(g.x), ep)) + splat(1.0f));
+  }
+  const f2 m = pfma(splat(g.y), s, splat(1.0f));                  // 1 - 2(1-a)(1-u) sigma
+  const f2 z = pfma(kE, m, k2 * splat(g.x));                      // 2 log2e k (x - Ec m)
+  const f2 th = pfma(rcpx2(ex2x2(z) + splat(1.0f)), splat(-2.0f), splat(1.0f));
+  return pfma(cp, th, acc);
+}
+
+// the edge sum of one lane: NPL Ferro pairs, FPL feature weights, and (spl) the spline edge of
+// input `si` (sp_o = the layer's LDS cubic table at output o)
+template <int IN, int FLEN, int NI, int NPL, int FPL, bool FERRO, bool FACT>
+__device__ __forceinline__ float v4_edges(const V4Lds<IN, FLEN>& L, const float* sp_o, const int* gi, const f2* ep,
+                                          const f2* k2, const f2* kE, const f2* cp, const f2* fw, int fofs,
+                                          bool spl, int si, float gsl2e) {
+  // spline operands first (two dependent LDS reads), so their latency hides under the pairs
+  const float u = L.G[si].w;
+  const float4 cf = *reinterpret_cast<const float4*>(&sp_o[(si * (NI + 1) + L.M[si]) * 4]);
+  f2 acc = splat(0.0f);
+  if constexpr (FERRO) {
+#pragma unroll
+    for (int r = 0; r < NPL; ++r) acc = v4_pair<FACT>(L.G[gi[r]], ep[r], k2[r], kE[r], cp[r], acc, gsl2e);
+  }
+  const float4* Fp = reinterpret_cast<const float4*>(&L.F[fofs]);
+#pragma unroll
+  for (int f = 0; f < FPL / 4; ++f) {
+    const float4 v = Fp[f];
+    acc = pfma(fw[2 * f], f2{v.x, v.y}, acc);
+    acc = pfma(fw[2 * f + 1], f2{v.z, v.w}, acc);
+  }
+  const float sv = ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
+  return (acc.x + acc.y) + (spl ? sv : 0.0f);
+}
+
+// HOT = true: the rk4 (3/8) integrate path only, every stage inlined, outputs predicated;
+// HOT = false: single evaluations and every other method.
+template <int H, int K_, int NB, int NG, bool FERRO, bool HOT>
+__global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
+  constexpr int D = 2, NI = NG - 1, NFL = 1 + NB, NFP = (NFL + 1) & ~1, K = FERRO ? K_ : 0;
+  // feature jobs: logistic 0..NB-1, SiLU, [gate, exp(gs x)], then x / u / m stores
+  constexpr int J_SILU = NB, J_GATE = NB + 1, J_EXP = NB + 2, J_X = FERRO ? NB + 3 : NB + 1;
+  constexpr int J_M = J_X + 1;
+  static_assert(J_M < 16 && NG <= 16, "v4 layout: NB logistic + SiLU (+ gate, exp) + x, m jobs on a row of 16 lanes");
+  static_assert(H <= 10, "v4 layout: H <= 10 groups of 3 lanes");
+  static_assert(!FERRO || K % 2 == 0, "v4 pairs Ferro elements (i, k), (i, k+1)");
+  constexpr int KP = K / 2 > 0 ? K / 2 : 1;
+  // layer 0 (2 -> H): groups of 3 lanes; layer 1 (H -> 2): the 16 lanes of a row
+  constexpr int NPL0 = FERRO ? (D * KP + 2) / 3 : 0, NPL1 = FERRO ? (H * KP + 15) / 16 : 0;
+  constexpr int FPL0 = ((D * NFP + 2) / 3 + 3) & ~3, FPL1 = ((H * NFP + 15) / 16 + 3) & ~3;
+  constexpr int FLEN0 = (3 * FPL0 > D * NFP ? 3 * FPL0 : D * NFP);
+  constexpr int FLEN1 = (16 * FPL1 > H * NFP ? 16 * FPL1 : H * NFP);
+  constexpr int NJH = FERRO ? NB + 3 : NB + 1;      // sigmoid-stream jobs per hidden input
+  constexpr int RH = (NJH + 2) / 3;                  // rounds over the 3 lanes of a group
+  constexpr int KT = (NG + 2) / 3;                   // knots per group lane
+  static_assert(3 * KT >= NG, "knots per group lane");
+  constexpr int SPT0 = H * D * (NI + 1) * 4, SPT1 = D * H * (NI + 1) * 4;
+
+  __shared__ __attribute__((aligned(16))) float s_sp0[SPT0];
+  __shared__ __attribute__((aligned(16))) float s_sp1[SPT1];
+  __shared__ float s_c0[H], s_c1[D];
+  __shared__ __attribute__((aligned(16))) V4Lds<D, FLEN0> s_L0[2];
+  __shared__ __attribute__((aligned(16))) V4Lds<H, FLEN1> s_L1[2];
+
+  const int tid = threadIdx.x;
+  const int g = tid >> 5, lane = tid & 31, row = lane >> 4, c1 = lane & 15;
+  const int64_t b = (int64_t)blockIdx.x * 2 + g;
+  const bool valid = b < a.B;
+  V4Lds<D, FLEN0>& L0 = s_L0[g];
+  V4Lds<H, FLEN1>& L1 = s_L1[g];
+
+  for (int i = tid; i < SPT0; i += 64) s_sp0[i] = a.plan[a.P0.sp + i];
+  for (int i = tid; i < SPT1; i += 64) s_sp1[i] = a.plan[a.P1.sp + i];
+  for (int i = tid; i < H; i += 64) s_c0[i] = a.plan[a.P0.fconst + i];
+  for (int i = tid; i < D; i += 64) s_c1[i] = a.plan[a.P1.fconst + i];
+  for (int i = lane; i < FLEN0; i += 32) L0.F[i] = 0.f;  // pads stay zero (finite x zero weight)
+  for (int i = lane; i < FLEN1; i += 32) L1.F[i] = 0.f;
+
+  const bool fact = FERRO && a.plan[a.P0.flag] <= kFactorLimit && a.plan[a.P1.flag] <= kFactorLimit;
+  const float l2 = FETODE_LOG2E;
+
+  // ---- layer-0 edge lane: output o0 = 5 row + q/3, part cc0 ----
+  const int q = c1;
+  const int o0 = row * 5 + q / 3, cc0 = q % 3;
+  const bool act0 = q < 15 && o0 < H;
+  const int o0c = act0 ? o0 : 0;
+  f2 ep0[NPL0 > 0 ? NPL0 : 1], k20[NPL0 > 0 ? NPL0 : 1], kE0[NPL0 > 0 ? NPL0 : 1], cp0[NPL0 > 0 ? NPL0 : 1];
+  int gi0[NPL0 > 0 ? NPL0 : 1];
+#pragma unroll
+  for (int r = 0; r < NPL0; ++r) {
+    const int P = cc0 * NPL0 + r;
+    const bool ok = act0 && P < D * KP;
+    int i = ok ? P / KP : 0;
+    asm volatile("" : "+v"(i));  // keep in a VGPR (no per-evaluation rematerialisation)
+    gi0[r] = i;
+    float t[4][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t idx = (int64_t)o0c * (D * K) + i * K + (ok ? (P % KP) * 2 + h : 0);
+      const float gec = ok ? a.plan[a.P0.fe_GEc + idx] : 0.f;
+      t[0][h] = fact ? ex2(gec) : gec;
+      t[1][h] = ok ? a.plan[a.P0.fe_k2 + idx] : 0.f;
+      t[2][h] = ok ? a.plan[a.P0.fe_k2Ec + idx] : 0.f;
+      t[3][h] = ok ? a.plan[a.P0.fe_CPs2 + idx] : 0.f;
+    }
+    ep0[r] = f2{t[0][0], t[0][1]};
+    k20[r] = f2{t[1][0], t[1][1]};
+    kE0[r] = f2{t[2][0], t[2][1]};
+    cp0[r] = f2{t[3][0], t[3][1]};
+  }
+  f2 fw0[FPL0 / 2];
+#pragma unroll
+  for (int f = 0; f < FPL0; f += 2) {
+    float w[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int qq = cc0 * FPL0 + f + h, i = qq / NFP, ff = qq % NFP;
+      w[h] = (act0 && i < D && ff < NFL) ? a.plan[a.P0.kw + (int64_t)o0c * (D * NFL) + i * NFL + ff] : 0.f;
+    }
+    fw0[f / 2] = f2{w[0], w[1]};
+  }
+  // ---- layer-1 edge lane: output row, part c1 ----
+  f2 ep1[NPL1 > 0 ? NPL1 : 1], k21[NPL1 > 0 ? NPL1 : 1], kE1[NPL1 > 0 ? NPL1 : 1], cp1[NPL1 > 0 ? NPL1 : 1];
+  int gi1[NPL1 > 0 ? NPL1 : 1];
+#pragma unroll
+  for (int r = 0; r < NPL1; ++r) {
+    const int P = c1 * NPL1 + r;
+    const bool ok = P < H * KP;
+    int i = ok ? P / KP : 0;
+    asm volatile("" : "+v"(i));
+    gi1[r] = i;
+    float t[4][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t idx = (int64_t)row * (H * K) + i * K + (ok ? (P % KP) * 2 + h : 0);
+      const float gec = ok ? a.plan[a.P1.fe_GEc + idx] : 0.f;
+      t[0][h] = fact ? ex2(gec) : gec;
+      t[1][h] = ok ? a.plan[a.P1.fe_k2 + idx] : 0.f;
+      t[2][h] = ok ? a.plan[a.P1.fe_k2Ec + idx] : 0.f;
+      t[3][h] = ok ? a.plan[a.P1.fe_CPs2 + idx] : 0.f;
+    }
+    ep1[r] = f2{t[0][0], t[0][1]};
+    k21[r] = f2{t[1][0], t[1][1]};
+    kE1[r] = f2{t[2][0], t[2][1]};
+    cp1[r] = f2{t[3][0], t[3][1]};
+  }
+  f2 fw1[FPL1 / 2];
+#pragma unroll
+  for (int f = 0; f < FPL1; f += 2) {
+    float w[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int qq = c1 * FPL1 + f + h, i = qq / NFP, ff = qq % NFP;
+      w[h] = (i < H && ff < NFL) ? a.plan[a.P1.kw + (int64_t)row * (H * NFL) + i * NFL + ff] : 0.f;
+    }
+    fw1[f / 2] = f2{w[0], w[1]};
+  }
+
+  // ---- layer-0 feature stream: input d = row, job c1 ----
+  float xna, xab, xmul, xadd;
+  float* xdst;
+  {
+    const int j = c1;
+    xna = 0.f; xab = 0.f; xmul = 1.f; xadd = 0.f;
+    xdst = &L0.sink;
+    if (j < NB) {
+      xna = a.plan[a.P0.lg + 2 * (row * NB + j)];
+      xab = a.plan[a.P0.lg + 2 * (row * NB + j) + 1];
+      xdst = &L0.F[row * NFP + 1 + j];
+    } else if (j == J_SILU) {
+      xna = -l2;
+      xdst = &L0.F[row * NFP];
+    } else if (FERRO && j == J_GATE) {
+      xna = -a.P0.gsl2e; xmul = -a.P0.wc; xadd = a.P0.wc;
+      xdst = &L0.G[row].y;
+    } else if (FERRO && j == J_EXP) {
+      xna = a.P0.gsl2e;
+      xdst = &L0.G[row].z;
+    } else if (j == J_X) {
+      xdst = &L0.G[row].x;
+    } else if (j == J_M) {
+      xdst = reinterpret_cast<float*>(&L0.M[row]);
+    }
+  }
+  const bool x_silu = c1 == J_SILU, x_gate = FERRO && c1 == J_GATE, x_exp = FERRO && c1 == J_EXP;
+  const bool x_x = c1 == J_X, x_m = c1 == J_M;
+  // knot interval: lane c1 holds knot c1 (and 1/(knot c1+1 - knot c1)); the lane whose knot
+  // opens the interval writes u (no LDS round trip on the critical path)
+  const float xknot = c1 < NG ? a.plan[a.P0.knots + row * NG + c1] : __builtin_inff();
+  const float xrh = c1 < NI ? a.plan[a.P0.rh + row * NI + c1] : 0.f;
+
+  // ---- layer-1 feature stream: hidden input o0, jobs cc0 + 3r ----
+  float hna[RH], hab[RH], hmul[RH], hadd[RH];
+  float* hdst[RH];
+#pragma unroll
+  for (int r = 0; r < RH; ++r) {
+    const int j = cc0 + 3 * r;
+    hna[r] = 0.f; hab[r] = 0.f; hmul[r] = 1.f; hadd[r] = 0.f;
+    hdst[r] = &L1.sink;
+    if (!act0) continue;
+    if (j < NB) {
+      hna[r] = a.plan[a.P1.lg + 2 * (o0 * NB + j)];
+      hab[r] = a.plan[a.P1.lg + 2 * (o0 * NB + j) + 1];
+      hdst[r] = &L1.F[o0 * NFP + 1 + j];
+    } else if (j == J_SILU) {
+      hna[r] = -l2;
+      hdst[r] = &L1.F[o0 * NFP];
+    } else if (FERRO && j == J_GATE) {
+      hna[r] = -a.P1.gsl2e; hmul[r] = -a.P1.wc; hadd[r] = a.P1.wc;
+      hdst[r] = &L1.G[o0].y;
+    } else if (FERRO && j == J_EXP) {
+      hna[r] = a.P1.gsl2e;
+      hdst[r] = &L1.G[o0].z;
+    }
+  }
+  // knots of hidden input o0: lane cc0 holds knots KT cc0 .. KT cc0 + KT-1 and their 1/width
+  float hknot[KT], hrh[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    const int kk = KT * cc0 + t;
+    hknot[t] = (act0 && kk < NG) ? a.plan[a.P1.knots + o0 * NG + kk] : __builtin_inff();
+    hrh[t] = (act0 && kk < NI) ? a.plan[a.P1.rh + o0 * NI + kk] : 0.f;
+  }
+  constexpr int RG = J_GATE / 3, CG = J_GATE % 3;  // round / lane of the layer-1 gate job
+  constexpr int RS = J_SILU / 3, RE = J_EXP / 3;
+  const bool h_silu = cc0 == J_SILU % 3, h_gate = FERRO && cc0 == CG, h_exp = FERRO && cc0 == J_EXP % 3;
+
+  // hysteresis state: prev_x of input `row` on the layer-0 gate lane, of input o0 on the
+  // layer-1 gate lane (ferro_class.py:409); per-layer contiguous blocks (include/fetode.h)
+  float prev0 = 0.f, prev1 = 0.f;
+  if (FERRO && valid) {
+    if (x_gate) prev0 = a.state[b * D + row];
+    if (act0 && h_gate) prev1 = a.state[a.B * D + b * H + o0];
+  }
+  bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
+
+  float y = valid ? a.y0[b * D + row] : 0.f;   // state dim `row`, replicated over the row
+  if (!a.single_eval && valid && c1 == 0) a.solution[b * D + row] = y;
+  __syncthreads();  // tables staged
+
+  STAMP_DECL
+  const float c0o = s_c0[o0c], c1o = s_c1[row];  // per-output constants, held in registers
+  const float* sp0_o = &s_sp0[o0c * D * (NI + 1) * 4];
+  const float* sp1_o = &s_sp1[row * H * (NI + 1) * 4];
+  const int fofs0 = cc0 * FPL0, fofs1 = c1 * FPL1;
+  const bool spl0 = act0 && cc0 < D, spl1 = c1 < H;  // lanes owning a spline edge (input si)
+  const int si0 = spl0 ? cc0 : 0, si1 = spl1 ? c1 : 0;
+
+  auto eval_body = [&](float xin, auto fact_tag) __attribute__((always_inline)) -> float {
+    constexpr bool F_ = decltype(fact_tag)::value;
+    STAMP(6);
+    FETODE_MARK("X_FEAT");
+    {
+      // (1) layer-0 features of input `row`: one sigmoid-of-affine job per lane
+      const float pv = x_gate ? (re0 ? xin : prev0) : 0.f;
+      const float e = ex2(ffma(xna, xin - pv, xab));
+      const float sg = rcp(1.0f + e);
+      float val = ffma(sg, x_silu ? xin : xmul, xadd);
+      val = x_exp ? e : val;
+      val = x_x ? xin : val;
+      // knot interval: lanes c1 < NG compare against their knot, DPP row count
+      int cnt = xin >= xknot ? 1 : 0;
+      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x128, 0xF, 0xF, false);
+      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x124, 0xF, 0xF, false);
+      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x122, 0xF, 0xF, false);
+      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x121, 0xF, 0xF, false);
+      const int mm = cnt - 1;
+      const bool fin = __builtin_isfinite(xin);
+      const int mfix = ((unsigned)mm < (unsigned)NI && fin) ? mm : NI;
+      val = x_m ? __builtin_bit_cast(float, mfix) : val;
+      *xdst = val;
+      if (c1 == mfix) L0.G[row].w = c1 < NI ? (xin - xknot) * xrh : (fin ? 0.0f : __builtin_nanf(""));
+      if (FERRO) prev0 = xin;  // ferro_class.py:409 (meaningful on the gate lane)
+      re0 = false;
+    }
+    STAMP(0);
+    __syncthreads();
+    STAMP(0);
+    FETODE_MARK("EDGES0");
+    // (2) layer-0 edges -> h_o on the group of 3
+    float h = v4_edges<D, FLEN0, NI, NPL0, FPL0, FERRO, F_>(L0, sp0_o, gi0, ep0, k20, kE0, cp0, fw0, fofs0,
+                                                            spl0, si0, a.P0.gsl2e);
+    h = act0 ? h : 0.f;
+    h = group3_sum(h, cc0) + c0o;
+    STAMP(2);
+    FETODE_MARK("H_FEAT");
+    {
+      // layer-1 features of input o0: RH rounds of the sigmoid stream on the group's 3 lanes
+      const float pv = h_gate ? (re1 ? h : prev1) : 0.f;
+#pragma unroll
+      for (int r = 0; r < RH; ++r) {
+        const float hx = (FERRO && r == RG) ? h - pv : h;
+        const float e = ex2(ffma(hna[r], hx, hab[r]));
+        const float sg = rcp(1.0f + e);
+        float val;
+        if (r == RS || (FERRO && (r == RG || r == RE))) {
+          val = ffma(sg, (r == RS && h_silu) ? h : hmul[r], hadd[r]);
+          if (FERRO && r == RE) val = h_exp ? e : val;
+        } else {
+          val = sg;
+        }
+        *hdst[r] = val;
+      }
+      if (FERRO) prev1 = h;
+      re1 = false;
+      // knot interval of h: KT compares per lane, summed over the group
+      float cntf = 0.f;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) cntf += h >= hknot[t] ? 1.0f : 0.0f;
+      cntf = group3_sum(cntf, cc0);
+      const int mm = (int)cntf - 1;
+      const bool fin = __builtin_isfinite(h);
+      const int mfix = ((unsigned)mm < (unsigned)NI && fin) ? mm : NI;
+      const int tq = mfix % KT;
+      // register select chain; the empty asm keeps the compiler from turning it into an
+      // indexed load of hknot/hrh (which would put both arrays in scratch memory)
+      float knm = hknot[0], rhm = hrh[0];
+      asm volatile("" : "+v"(knm), "+v"(rhm));
+#pragma unroll
+      for (int t = 1; t < KT; ++t) {
+        knm = tq == t ? hknot[t] : knm;
+        rhm = tq == t ? hrh[t] : rhm;
+        asm volatile("" : "+v"(knm), "+v"(rhm));
+      }
+      if (act0 && cc0 == mfix / KT)
+        L1.G[o0].w = mfix < NI ? (h - knm) * rhm : (fin ? 0.0f : __builtin_nanf(""));
+      if (act0 && cc0 == 0) {
+        L1.G[o0].x = h;
+        L1.M[o0] = mfix;
+      }
+    }
+    STAMP(3);
+    __syncthreads();
+    STAMP(4);
+    FETODE_MARK("EDGES1");
+    // (3) layer-1 edges -> k_row on every lane of the row
+    const float v = v4_edges<H, FLEN1, NI, NPL1, FPL1, FERRO, F_>(L1, sp1_o, gi1, ep1, k21, kE1, cp1, fw1, fofs1,
+                                                                  spl1, si1, a.P1.gsl2e);
+    const float kr = row_sum16(v) + c1o;
+    STAMP(5);
+    FETODE_MARK("END");
+    return kr;
+  };
+  constexpr int SW = FERRO ? D + H : 0;
+  // the step / output schedule is staged through LDS in chunks: per-step global loads in the
+  // loop would wait (vmcnt) behind the solution stores of the previous step
+  constexpr int SCH = 32;
+  __shared__ float s_dt[SCH], s_hh[SCH], s_h6[SCH], s_oslope[SCH];
+  __shared__ int s_ostep[SCH], s_omode[SCH];
+  auto load_steps = [&](int s0) {
+    __syncthreads();
+    for (int i = tid; i < SCH && s0 + i < a.n_steps; i += 64) {
+      s_dt[i] = a.step_coef[4 * (s0 + i) + 0];
+      s_hh[i] = a.step_coef[4 * (s0 + i) + 1];
+      s_h6[i] = a.step_coef[4 * (s0 + i) + 2];
+    }
+    __syncthreads();
+  };
+  auto load_outs = [&](int j0) {
+    __syncthreads();
+    for (int i = tid; i < SCH; i += 64) {
+      const bool in = j0 + i < a.T;
+      s_ostep[i] = in ? a.out_step[j0 + i] : -1;
+      s_omode[i] = in ? a.out_mode[j0 + i] : 1;
+      s_oslope[i] = in ? a.out_slope[j0 + i] : 0.f;
+    }
+    __syncthreads();
+  };
+  auto ckpt_write = [&](int s) __attribute__((always_inline)) {
+    if (a.ckpt && valid) {
+      float* ck = a.ckpt + ((int64_t)s * a.B + b) * (D + SW);
+      if (c1 == 0) ck[row] = y;
+      if (FERRO && x_gate) ck[D + row] = prev0;
+      if (FERRO && act0 && h_gate) ck[D + D + o0] = prev1;
+    }
+  };
+  auto out_write = [&](int j, float v) __attribute__((always_inline)) {
+#ifndef FETODE_EXPERIMENT_NO_OUT
+    if (valid && c1 == 0) a.solution[((int64_t)j * a.B + b) * D + row] = v;
+#endif
+  };
+  using FT = std::integral_constant<bool, true>;
+  using FF = std::integral_constant<bool, false>;
+
+  if constexpr (HOT) {
+    // rk4 (torchdiffeq rk_common.rk4_alt_step_func op order); the step's first two output
+    // slots are read before its stages and consumed after them, with predicated stores
+    int sb = 0, jb = 1, jj = 1;
+    load_steps(0);
+    load_outs(1);
+    auto run = [&](auto fact_tag) __attribute__((always_inline)) {
+      const float third = 1.0f / 3.0f;
+      for (int s = 0; s < a.n_steps; ++s) {
+        if (s - sb == SCH) {
+          sb = s;
+          load_steps(s);
+        }
+        if (jj + 1 - jb >= SCH) {
+          jb = jj;
+          load_outs(jj);
+        }
+        const int sr = s - sb, jr = jj - jb;
+        const float dt = s_dt[sr];
+        const int os0 = s_ostep[jr], os1 = s_ostep[jr + 1], om0 = s_omode[jr];
+        const float osl0 = s_oslope[jr];
+        STAMP(7);
+        ckpt_write(s);
+        const float k1 = eval_body(y, fact_tag);
+        const float k2 = eval_body(y + (dt * k1) * third, fact_tag);
+        const float k3 = eval_body(y + dt * (k2 - k1 * third), fact_tag);
+        const float k4 = eval_body(y + dt * ((k1 - k2) + k3), fact_tag);
+        const float y1 = y + (((k1 + 3.0f * (k2 + k3)) + k4) * dt) * 0.125f;
+        if (os0 == s) {
+          // mode / slope as opaque VGPRs: VALU selects instead of scalar branches on the mode
+          int m0 = om0;
+          float sl0 = osl0;
+          asm volatile("" : "+v"(m0), "+v"(sl0));
+          out_write(jj, m0 == 0 ? y : (m0 == 1 ? y1 : y + sl0 * (y1 - y)));
+          ++jj;
+          if (os1 == s) {  // several outputs inside one step (step_size grids)
+            while (jj < a.T) {
+              if (jj - jb == SCH) {
+                jb = jj;
+                load_outs(jj);
+              }
+              if (s_ostep[jj - jb] != s) break;
+              const int mode = s_omode[jj - jb];
+              out_write(jj, mode == 0 ? y : (mode == 1 ? y1 : y + s_oslope[jj - jb] * (y1 - y)));
+              ++jj;
+            }
+          }
+        }
+        STAMP(1);
+        y = y1;
+      }
+    };
+    if (fact) run(FT{});
+    else run(FF{});
+  } else {
+    auto eval = [&](float xin) __attribute__((always_inline)) -> float {
+      if (fact) return eval_body(xin, FT{});
+      return eval_body(xin, FF{});
+    };
+    if (a.single_eval) {
+      const float f = eval(y);
+      if (valid && c1 == 0) a.eval_out[b * D + row] = f;
+    } else {
+      const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4
+                     : a.method == FETODE_MIDPOINT ? 2 : 1;
+      const float third = 1.0f / 3.0f;
+      int sb = 0, jb = 1, jj = 1;
+      load_steps(0);
+      load_outs(1);
+      for (int s = 0; s < a.n_steps; ++s) {
+        if (s - sb == SCH) {
+          sb = s;
+          load_steps(s);
+        }
+        const float dt = s_dt[s - sb], hh = s_hh[s - sb], h6 = s_h6[s - sb];
+        ckpt_write(s);
+        float k1 = 0.f, k2 = 0.f, k3 = 0.f, k4 = 0.f;
+        for (int st = 0; st < ns; ++st) {
+          float xin = y;
+          if (a.method == FETODE_RK4) {
+            if (st == 1) xin = y + (dt * k1) * third;
+            else if (st == 2) xin = y + dt * (k2 - k1 * third);
+            else if (st == 3) xin = y + dt * ((k1 - k2) + k3);
+          } else if (a.method == FETODE_RK4_CLASSIC) {
+            if (st == 1) xin = y + hh * k1;
+            else if (st == 2) xin = y + hh * k2;
+            else if (st == 3) xin = y + dt * k3;
+          } else if (a.method == FETODE_MIDPOINT) {
+            if (st == 1) xin = y + k1 * hh;
+          }
+          const float kk = eval(xin);
+          if (st == 0) k1 = kk;
+          else if (st == 1) k2 = kk;
+          else if (st == 2) k3 = kk;
+          else k4 = kk;
+        }
+        float y1;
+        if (a.method == FETODE_RK4) y1 = y + (((k1 + 3.0f * (k2 + k3)) + k4) * dt) * 0.125f;
+        else if (a.method == FETODE_RK4_CLASSIC) y1 = y + h6 * (((k1 + 2.0f * k2) + 2.0f * k3) + k4);
+        else if (a.method == FETODE_MIDPOINT) y1 = y + dt * k2;
+        else y1 = y + dt * k1;
+        while (jj < a.T) {
+          if (jj - jb == SCH) {
+            jb = jj;
+            load_outs(jj);
+          }
+          if (s_ostep[jj - jb] != s) break;
+          const int mode = s_omode[jj - jb];
+          out_write(jj, mode == 0 ? y : (mode == 1 ? y1 : y + s_oslope[jj - jb] * (y1 - y)));
+          ++jj;
+        }
+        y = y1;
+      }
+    }
+  }
+  if (FERRO && valid) {
+    if (x_gate) a.state[b * D + row] = prev0;
+    if (act0 && h_gate) a.state[a.B * D + b * H + o0] = prev1;
+  }
+  STAMP_FLUSH();
+}
+
 typedef void (*fused_fn)(FusedArgs);
 struct FusedEntry {
   int in0, h, out, K, NB, NG;
   bool ferro;
   fused_fn fn;
   int nt, lpt;
+  fused_fn fn_rk4 = nullptr;  // specialised rk4 integrate kernel, if any
 };
 #define FUSED(IN0, H, OUT, K, NB, NG, FE, LPT, NT) \
   {IN0, H, OUT, K, NB, NG, FE, fused_integrate_kernel<IN0, H, OUT, K, NB, NG, FE, LPT, NT>, NT, LPT}
 const FusedEntry kFused[] = {
-    // v3 (default): LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146) and LV KAN
+    // v4 (default): LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146) and LV KAN
+    {2, 10, 2, 10, 10, 12, true, fused4_kernel<10, 10, 10, 12, true, false>, 64, 4,
+     fused4_kernel<10, 10, 10, 12, true, true>},
+    {2, 10, 2, 1, 10, 12, false, fused4_kernel<10, 2, 10, 12, false, false>, 64, 4,
+     fused4_kernel<10, 2, 10, 12, false, true>},
+    // v3 (FETODE_FUSED_LPT=3)
     {2, 10, 2, 10, 10, 12, true, fused3_kernel<10, 10, 10, 12, true>, 64, 3},
     {2, 10, 2, 1, 10, 12, false, fused3_kernel<10, 1, 10, 12, false>, 64, 3},
     // v2 (FETODE_FUSED_LPT=32|64, FETODE_FUSED_NT=64|256)
@@ -724,11 +1303,11 @@ int preferred_nt() {
   }();
   return nt;
 }
-// kernel variant: 3 = v3 (merged phases, default); FETODE_FUSED_LPT=32|64 selects a v2 variant
+// kernel variant: 4 = v4 (packed pairs, default); FETODE_FUSED_LPT=3 selects v3, 32|64 a v2 variant
 int preferred_lpt() {
   static int v = [] {
     const char* e = getenv("FETODE_FUSED_LPT");
-    return e ? atoi(e) : 3;
+    return e ? atoi(e) : 4;
   }();
   return v;
 }
@@ -759,8 +1338,9 @@ int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
   if (!e) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
   layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
   layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
-  const int tpb = e->lpt == 3 ? 2 : e->nt / e->lpt;
-  hipLaunchKernelGGL(e->fn, dim3(nblk(a.B, tpb)), dim3(e->nt), 0, (hipStream_t)stream, a);
+  const int tpb = e->lpt <= 4 ? 2 : e->nt / e->lpt;
+  const fused_fn fn = (e->fn_rk4 && !a.single_eval && a.method == FETODE_RK4) ? e->fn_rk4 : e->fn;
+  hipLaunchKernelGGL(fn, dim3(nblk(a.B, tpb)), dim3(e->nt), 0, (hipStream_t)stream, a);
   LAUNCH_CHECK();
   return FETODE_OK;
 }
@@ -768,6 +1348,12 @@ int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
 }  // namespace
 
 extern "C" {
+
+#ifdef FETODE_STAMPS
+int fetode_debug_stamp_buffer(void* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_fetode_stamps), &p, sizeof(p)) == hipSuccess ? FETODE_OK : FETODE_EHIP;
+}
+#endif
 
 int fetode_fused_supported(const fetode_field_t* f) {
   if (validate_field(f) != FETODE_OK) return 0;

@@ -161,11 +161,44 @@ def test_fused_rk4_kanfet_one_step_parity(dev, B, tag):
     assert worst <= REL, worst
 
 
+def _error_stats(a, s64):
+    """Per-trajectory max-over-time relative error vs fp64: 25th percentile (the well-conditioned
+    majority), geomean, max, and how many
+    trajectories cross 1e-3 / 1e-2 (the fp32-diverging ones)."""
+    e = ((a.double() - s64).norm(dim=2) / s64.norm(dim=2).clamp_min(1e-6)).max(0).values
+    return {"p25": e.quantile(0.25).item(), "gmean": e.log().mean().exp().item(), "max": e.max().item(),
+            "n1e-3": int((e > 1e-3).sum()), "n1e-2": int((e > 1e-2).sum())}
+
+
+def fp32_error_envelope(sd, y0, t, s64, trials=6, seed=0):
+    """How far an fp32 solve of this model may land from fp64 by rounding alone.
+
+    KAN-FET trajectories are ill-conditioned in fp32 (the hysteresis gate amplifies
+    x - prev_x rounding).  Re-running the CPU fp32 oracle with every parameter moved by a
+    fraction of an ulp (an equally valid fp32 rounding of the same model), 4-7 of the 64
+    LV trajectories always end 1e-2..6e-2 away from fp64 and the rest stay near 3e-5 — so any
+    percentile near the 90th jumps between 1e-3 and 2e-2 from rounding alone.  The envelope
+    is the worst value of each statistic over the unperturbed run and `trials` perturbed runs
+    (tools/diag/acc_dist.py prints the distributions)."""
+    from oracle import torch_ref as O
+    env = None
+    gen = torch.Generator().manual_seed(seed)
+    for trial in range(trials + 1):
+        sdp = {k: (v * (1 + 6e-8 * torch.randn(v.shape, generator=gen)) if trial and v.dtype == torch.float32
+                   and "grid" not in k else v) for k, v in sd.items()}
+        r = O.KANFETRef.from_state_dict(sdp, 2)
+        with torch.no_grad():
+            st = _error_stats(O.odeint(lambda tt, yy: r(yy), y0, t, method="rk4"), s64)
+        env = st if env is None else {k: max(env[k], st[k]) for k in env}
+    return env
+
+
 @pytest.mark.parametrize("tag", ["t35", "t140"])
 def test_fused_rk4_kanfet_accuracy_parity(dev, tag):
-    """KAN-FET whole trajectories are ill-conditioned in fp32: the reference's own fp32 result
-    departs from fp64 by up to 1e-2 per slice (hysteresis gate on x - prev_x).  The GPU result
-    must be as accurate as the reference CPU fp32 odeint, measured against the fp64 oracle."""
+    """The GPU trajectory must be as accurate as the reference's CPU fp32 odeint, measured
+    against the fp64 oracle: typical error (25th percentile, geomean) within 2x of the fp32
+    rounding envelope, no more fp32-diverging trajectories than that envelope (+max(2, 15%)),
+    and no larger worst error (x1.5).  The committed reference fp32 run joins the envelope."""
     import fet_ode_amd as F
     from oracle import torch_ref as O
     g = load_golden("traj_kanfet")
@@ -175,18 +208,18 @@ def test_fused_rk4_kanfet_accuracy_parity(dev, tag):
     t = torch.from_numpy(g[tag])
     ref64 = O.KANFETRef.from_state_dict(sd, 2).to(torch.float64)
     s64 = O.odeint(lambda tt, yy: ref64(yy), y0.double(), t, method="rk4")
-    cpu32 = torch.from_numpy(g[f"sol_B{B}_{tag}"]).double()
     m = _kanfet_from(g, dev)
     with torch.no_grad():
         gpu = F.odeint(F.autonomous(m), y0.to(dev), t, method="rk4").cpu().double()
-
-    def per_traj(a):
-        return ((a - s64).norm(dim=2) / s64.norm(dim=2).clamp_min(1e-6)).max(0).values
-
-    ec, eg = per_traj(cpu32), per_traj(gpu)
-    for q in (0.5, 0.9):
-        assert eg.quantile(q) <= 4 * ec.quantile(q) + 1e-6, (q, eg.quantile(q).item(), ec.quantile(q).item())
     assert torch.isfinite(gpu).all()
+    eg = _error_stats(gpu, s64)
+    ec = _error_stats(torch.from_numpy(g[f"sol_B{B}_{tag}"]), s64)
+    env = {k: max(v, ec[k]) for k, v in fp32_error_envelope(sd, y0, t, s64).items()}
+    msg = (eg, env)
+    assert eg["p25"] <= 2 * env["p25"] and eg["gmean"] <= 2 * env["gmean"], msg
+    for k in ("n1e-2", "n1e-3"):
+        assert eg[k] <= env[k] + max(2, int(0.15 * env[k])), msg
+    assert eg["max"] <= 1.5 * env["max"], msg
     # final hysteresis state == last stage input of the last step, on the GPU trajectory
     assert m.layers[0].ferro.prev_x.shape == (B, 2, 10, 10)
 
