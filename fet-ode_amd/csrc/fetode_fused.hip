@@ -781,12 +781,19 @@ __device__ __forceinline__ float v4_edges(const V4Lds<IN, FLEN>& L, const float*
 #pragma unroll
     for (int r = 0; r < NPL; ++r) acc = v4_pair<FACT>(L.G[gi[r]], ep[r], k2[r], kE[r], cp[r], acc, gsl2e);
   }
-  const float4* Fp = reinterpret_cast<const float4*>(&L.F[fofs]);
+  if constexpr (FPL % 4 == 0) {  // chunk offsets are 16-byte aligned: ds_read_b128
+    const float4* Fp = reinterpret_cast<const float4*>(&L.F[fofs]);
 #pragma unroll
-  for (int f = 0; f < FPL / 4; ++f) {
-    const float4 v = Fp[f];
-    acc = pfma(fw[2 * f], f2{v.x, v.y}, acc);
-    acc = pfma(fw[2 * f + 1], f2{v.z, v.w}, acc);
+    for (int f = 0; f < FPL / 4; ++f) {
+      const float4 v = Fp[f];
+      acc = pfma(fw[2 * f], f2{v.x, v.y}, acc);
+      acc = pfma(fw[2 * f + 1], f2{v.z, v.w}, acc);
+    }
+  } else {  // 8-byte aligned chunks: ds_read_b64
+    static_assert(FPL % 2 == 0, "feature chunks are float pairs");
+    const f2* Fp = reinterpret_cast<const f2*>(&L.F[fofs]);
+#pragma unroll
+    for (int f = 0; f < FPL / 2; ++f) acc = pfma(fw[f], Fp[f], acc);
   }
   const float sv = ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
   return (acc.x + acc.y) + (spl ? sv : 0.0f);
@@ -1263,6 +1270,468 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
   STAMP_FLUSH();
 }
 
+// =============================================================================================
+// v5: one trajectory per wave — for batches that give v4 fewer than ~4 waves per SIMD.
+//
+// v4 is latency-bound at B = 4096 (2048 waves = 2 per SIMD: each wave stalls ~60% of an
+// evaluation on dependent LDS / DPP / transcendental chains).  v5 spreads one trajectory over
+// the 64 lanes, doubling the independent waves per SIMD and halving each wave's per-evaluation
+// instruction stream; a workgroup holds NW trajectories (one per wave) sharing the LDS tables,
+// and the waves never synchronise inside an evaluation (a wave's LDS traffic is in order).
+// Lane map, row = lane / 16:
+//   layer-0 features  input d on rows 2d, 2d+1 (row 2d writes), one job per lane as in v4;
+//   layer-0 edges     hidden output o on the quad 4o..4o+3 (quad_perm all-reduce);
+//   layer-1 features  input o on its quad, NJH jobs in rounds of 4;
+//   layer-1 edges     output d on rows 2d, 2d+1 (row_ror + permlane16_swap all-reduce), which
+//                     leaves k_d exactly where y_d lives for the stage combine.
+// =============================================================================================
+__device__ __forceinline__ float quad_sum(float v) {
+  v += dpp<0xB1>(v);  // quad_perm [1,0,3,2]
+  v += dpp<0x4E>(v);  // quad_perm [2,3,0,1]
+  return v;
+}
+// sum over the 32 lanes of rows {0,1} / {2,3}, result on every lane of the pair
+// (not v_permlane16_swap: this compiler reads its second result from the first result's
+// register, so r[0] + r[1] came out as 2*r[0].  ds_swizzle xor-16 goes through the LDS
+// crossbar without touching memory.)
+__device__ __forceinline__ float rowpair_sum(float v) {
+  v = row_sum16(v);
+  constexpr int kXor16 = (0x10 << 10) | 0x1F;  // bitmask mode: and 0x1F, or 0, xor 0x10
+  return v + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), kXor16));
+}
+// order this wave's LDS writes before its later reads.  The LDS executes one wave's requests
+// in issue order, so only the compiler has to be stopped from moving memory operations across
+// (a wavefront-scope fence does not constrain non-atomic accesses; a memory clobber does).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int H, int K_, int NB, int NG, bool FERRO, bool HOT, int NW>
+#ifndef FETODE_V5_WAVES
+#define FETODE_V5_WAVES 3  // waves per SIMD the register budget is cut for (4 spills today)
+#endif
+__global__ __launch_bounds__(64 * NW, FETODE_V5_WAVES) void fused5_kernel(FusedArgs a) {
+  constexpr int D = 2, NI = NG - 1, NFL = 1 + NB, NFP = (NFL + 1) & ~1, K = FERRO ? K_ : 0;
+  constexpr int J_SILU = NB, J_GATE = NB + 1, J_EXP = NB + 2, J_X = FERRO ? NB + 3 : NB + 1;
+  constexpr int J_M = J_X + 1;
+  static_assert(J_M < 16 && NG <= 16, "v5 layout: feature jobs of one input on a row of 16 lanes");
+  static_assert(4 * H <= 64, "v5 layout: H <= 16 quads");
+  static_assert(!FERRO || K % 2 == 0, "v5 pairs Ferro elements (i, k), (i, k+1)");
+  constexpr int KP = K / 2 > 0 ? K / 2 : 1;
+  constexpr int NPL0 = FERRO ? (D * KP + 3) / 4 : 0, NPL1 = FERRO ? (H * KP + 31) / 32 : 0;
+  constexpr int FPL0 = ((D * NFP + 3) / 4 + 1) & ~1, FPL1 = ((H * NFP + 31) / 32 + 1) & ~1;
+  constexpr int FLEN0 = (4 * FPL0 > D * NFP ? 4 * FPL0 : D * NFP);
+  constexpr int FLEN1 = (32 * FPL1 > H * NFP ? 32 * FPL1 : H * NFP);
+  constexpr int NJH = FERRO ? NB + 3 : NB + 1;   // sigmoid-stream jobs per hidden input
+  constexpr int RH = (NJH + 3) / 4;               // rounds over the 4 lanes of a quad
+  constexpr int KT = (NG + 3) / 4;                // knots per quad lane: q, q+4, q+8, ...
+  constexpr int SPT0 = H * D * (NI + 1) * 4, SPT1 = D * H * (NI + 1) * 4;
+  constexpr int SW = FERRO ? D + H : 0;
+
+  __shared__ __attribute__((aligned(16))) float s_sp0[SPT0];
+  __shared__ __attribute__((aligned(16))) float s_sp1[SPT1];
+  __shared__ __attribute__((aligned(16))) V4Lds<D, FLEN0> s_L0[NW];
+  __shared__ __attribute__((aligned(16))) V4Lds<H, FLEN1> s_L1[NW];
+
+  const int tid = threadIdx.x;
+  const int w = tid >> 6, l = tid & 63, row = l >> 4, c = l & 15;
+  const int64_t b = (int64_t)blockIdx.x * NW + w;
+  const bool valid = b < a.B;
+  V4Lds<D, FLEN0>& L0 = s_L0[w];
+  V4Lds<H, FLEN1>& L1 = s_L1[w];
+
+  for (int i = tid; i < SPT0; i += 64 * NW) s_sp0[i] = a.plan[a.P0.sp + i];
+  for (int i = tid; i < SPT1; i += 64 * NW) s_sp1[i] = a.plan[a.P1.sp + i];
+  for (int i = l; i < FLEN0; i += 64) L0.F[i] = 0.f;  // pads stay zero (finite x zero weight)
+  for (int i = l; i < FLEN1; i += 64) L1.F[i] = 0.f;
+
+  const bool fact = FERRO && a.plan[a.P0.flag] <= kFactorLimit && a.plan[a.P1.flag] <= kFactorLimit;
+  const float l2 = FETODE_LOG2E;
+
+  // ---- layer-0 edge lane: hidden output o0 = quad, part q ----
+  const int o0 = l >> 2, q = l & 3;
+  const bool act0 = o0 < H;
+  const int o0c = act0 ? o0 : 0;
+  f2 ep0[NPL0 > 0 ? NPL0 : 1], k20[NPL0 > 0 ? NPL0 : 1], kE0[NPL0 > 0 ? NPL0 : 1], cp0[NPL0 > 0 ? NPL0 : 1];
+  int gi0[NPL0 > 0 ? NPL0 : 1];
+  // ---- layer-1 edge lane: output d1 = rows {2 d1, 2 d1 + 1}, part c32 ----
+  const int d1 = l >> 5, c32 = l & 31;
+  f2 ep1[NPL1 > 0 ? NPL1 : 1], k21[NPL1 > 0 ? NPL1 : 1], kE1[NPL1 > 0 ? NPL1 : 1], cp1[NPL1 > 0 ? NPL1 : 1];
+  int gi1[NPL1 > 0 ? NPL1 : 1];
+  auto load_pairs = [&](const LayerPlan& P, int IN, int o, int part, int npl, bool act, f2* ep, f2* k2, f2* kE, f2* cp,
+                        int* gi) __attribute__((always_inline)) {
+    for (int r = 0; r < npl; ++r) {
+      const int Pi = part * npl + r;
+      const bool ok = act && Pi < IN * KP;
+      int i = ok ? Pi / KP : 0;
+      float t[4][2];
+      for (int h = 0; h < 2; ++h) {
+        const int64_t idx = (int64_t)o * (IN * K) + i * K + (ok ? (Pi % KP) * 2 + h : 0);
+        const float gec = ok ? a.plan[P.fe_GEc + idx] : 0.f;
+        t[0][h] = fact ? ex2(gec) : gec;
+        t[1][h] = ok ? a.plan[P.fe_k2 + idx] : 0.f;
+        t[2][h] = ok ? a.plan[P.fe_k2Ec + idx] : 0.f;
+        t[3][h] = ok ? a.plan[P.fe_CPs2 + idx] : 0.f;
+      }
+      asm volatile("" : "+v"(i));  // keep in a VGPR (no per-evaluation rematerialisation)
+      gi[r] = i;
+      ep[r] = f2{t[0][0], t[0][1]};
+      k2[r] = f2{t[1][0], t[1][1]};
+      kE[r] = f2{t[2][0], t[2][1]};
+      cp[r] = f2{t[3][0], t[3][1]};
+    }
+  };
+  if constexpr (FERRO) {
+    load_pairs(a.P0, D, o0c, q, NPL0, act0, ep0, k20, kE0, cp0, gi0);
+    load_pairs(a.P1, H, d1, c32, NPL1, true, ep1, k21, kE1, cp1, gi1);
+  }
+  f2 fw0[FPL0 / 2], fw1[FPL1 / 2];
+#pragma unroll
+  for (int f = 0; f < FPL0; f += 2) {
+    float wv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int qq = q * FPL0 + f + h, i = qq / NFP, ff = qq % NFP;
+      wv[h] = (act0 && i < D && ff < NFL) ? a.plan[a.P0.kw + (int64_t)o0c * (D * NFL) + i * NFL + ff] : 0.f;
+    }
+    fw0[f / 2] = f2{wv[0], wv[1]};
+  }
+#pragma unroll
+  for (int f = 0; f < FPL1; f += 2) {
+    float wv[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int qq = c32 * FPL1 + f + h, i = qq / NFP, ff = qq % NFP;
+      wv[h] = (i < H && ff < NFL) ? a.plan[a.P1.kw + (int64_t)d1 * (H * NFL) + i * NFL + ff] : 0.f;
+    }
+    fw1[f / 2] = f2{wv[0], wv[1]};
+  }
+
+  // ---- layer-0 feature stream: input dx = row / 2, job c (row 2 dx writes) ----
+  const int dx = row >> 1;
+  const bool xw = (row & 1) == 0;
+  float xna = 0.f, xab = 0.f, xmul = 1.f, xadd = 0.f;
+  float* xdst = &L0.sink;
+  if (xw) {
+    if (c < NB) {
+      xna = a.plan[a.P0.lg + 2 * (dx * NB + c)];
+      xab = a.plan[a.P0.lg + 2 * (dx * NB + c) + 1];
+      xdst = &L0.F[dx * NFP + 1 + c];
+    } else if (c == J_SILU) {
+      xdst = &L0.F[dx * NFP];
+    } else if (FERRO && c == J_GATE) {
+      xdst = &L0.G[dx].y;
+    } else if (FERRO && c == J_EXP) {
+      xdst = &L0.G[dx].z;
+    } else if (c == J_X) {
+      xdst = &L0.G[dx].x;
+    } else if (c == J_M) {
+      xdst = reinterpret_cast<float*>(&L0.M[dx]);
+    }
+  }
+  if (c == J_SILU) xna = -l2;
+  if (FERRO && c == J_GATE) {
+    xna = -a.P0.gsl2e;
+    xmul = -a.P0.wc;
+    xadd = a.P0.wc;
+  }
+  if (FERRO && c == J_EXP) xna = a.P0.gsl2e;
+  const bool x_silu = c == J_SILU, x_gate = FERRO && c == J_GATE, x_exp = FERRO && c == J_EXP;
+  const bool x_x = c == J_X, x_m = c == J_M;
+  const float xknot = c < NG ? a.plan[a.P0.knots + dx * NG + c] : __builtin_inff();
+  const float xrh = c < NI ? a.plan[a.P0.rh + dx * NI + c] : 0.f;
+
+  // ---- layer-1 feature stream: hidden input o0 on its quad, jobs q + 4r ----
+  float hna[RH], hab[RH], hmul[RH], hadd[RH];
+  float* hdst[RH];
+#pragma unroll
+  for (int r = 0; r < RH; ++r) {
+    const int j = q + 4 * r;
+    hna[r] = 0.f; hab[r] = 0.f; hmul[r] = 1.f; hadd[r] = 0.f;
+    hdst[r] = &L1.sink;
+    if (!act0) continue;
+    if (j < NB) {
+      hna[r] = a.plan[a.P1.lg + 2 * (o0 * NB + j)];
+      hab[r] = a.plan[a.P1.lg + 2 * (o0 * NB + j) + 1];
+      hdst[r] = &L1.F[o0 * NFP + 1 + j];
+    } else if (j == J_SILU) {
+      hna[r] = -l2;
+      hdst[r] = &L1.F[o0 * NFP];
+    } else if (FERRO && j == J_GATE) {
+      hna[r] = -a.P1.gsl2e; hmul[r] = -a.P1.wc; hadd[r] = a.P1.wc;
+      hdst[r] = &L1.G[o0].y;
+    } else if (FERRO && j == J_EXP) {
+      hna[r] = a.P1.gsl2e;
+      hdst[r] = &L1.G[o0].z;
+    }
+  }
+  float hknot[KT], hrh[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {
+    const int kk = q + 4 * t;
+    hknot[t] = (act0 && kk < NG) ? a.plan[a.P1.knots + o0 * NG + kk] : __builtin_inff();
+    hrh[t] = (act0 && kk < NI) ? a.plan[a.P1.rh + o0 * NI + kk] : 0.f;
+  }
+  constexpr int RG = J_GATE / 4, RS = J_SILU / 4, RE = J_EXP / 4;
+  const bool h_silu = q == J_SILU % 4, h_gate = FERRO && q == J_GATE % 4, h_exp = FERRO && q == J_EXP % 4;
+
+  // hysteresis state (per-layer contiguous blocks, include/fetode.h): prev_x of input dx on the
+  // layer-0 gate lane of row 2 dx, of hidden input o0 on its quad's gate lane
+  const bool own0 = FERRO && xw && x_gate, own1 = FERRO && act0 && h_gate;
+  float prev0 = 0.f, prev1 = 0.f;
+  if (valid) {
+    if (own0) prev0 = a.state[b * D + dx];
+    if (own1) prev1 = a.state[a.B * D + b * H + o0];
+  }
+  bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
+
+  float y = valid ? a.y0[b * D + dx] : 0.f;  // state dim dx, replicated over rows 2dx, 2dx+1
+  const bool yw = valid && (l & 31) == 0;   // the lane that writes y_dx
+  if (!a.single_eval && yw) a.solution[b * D + dx] = y;
+  __syncthreads();  // tables staged
+  const float c0o = a.plan[a.P0.fconst + o0c], c1o = a.plan[a.P1.fconst + d1];
+
+  const float* sp0_o = &s_sp0[o0c * D * (NI + 1) * 4];
+  const float* sp1_o = &s_sp1[d1 * H * (NI + 1) * 4];
+  const int fofs0 = q * FPL0, fofs1 = c32 * FPL1;
+  const bool spl0 = act0 && q < D, spl1 = c32 < H;
+  const int si0 = spl0 ? q : 0, si1 = spl1 ? c32 : 0;
+
+  auto eval_body = [&](float xin, auto fact_tag) __attribute__((always_inline)) -> float {
+    constexpr bool F_ = decltype(fact_tag)::value;
+    FETODE_MARK("X_FEAT");
+    {
+      const float pv = x_gate ? (re0 ? xin : prev0) : 0.f;
+      const float e = ex2(ffma(xna, xin - pv, xab));
+      const float sg = rcp(1.0f + e);
+      float val = ffma(sg, x_silu ? xin : xmul, xadd);
+      val = x_exp ? e : val;
+      val = x_x ? xin : val;
+      int cnt = xin >= xknot ? 1 : 0;
+      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x128, 0xF, 0xF, false);
+      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x124, 0xF, 0xF, false);
+      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x122, 0xF, 0xF, false);
+      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x121, 0xF, 0xF, false);
+      const int mm = cnt - 1;
+      const bool fin = __builtin_isfinite(xin);
+      const int mfix = ((unsigned)mm < (unsigned)NI && fin) ? mm : NI;
+      val = x_m ? __builtin_bit_cast(float, mfix) : val;
+      *xdst = val;
+      if (xw && c == mfix) L0.G[dx].w = c < NI ? (xin - xknot) * xrh : (fin ? 0.0f : __builtin_nanf(""));
+      if (FERRO) prev0 = xin;  // ferro_class.py:409
+      re0 = false;
+    }
+    wave_lds_sync();
+    FETODE_MARK("EDGES0");
+    float h = v4_edges<D, FLEN0, NI, NPL0, FPL0, FERRO, F_>(L0, sp0_o, gi0, ep0, k20, kE0, cp0, fw0, fofs0, spl0, si0,
+                                                            a.P0.gsl2e);
+    h = quad_sum(act0 ? h : 0.f) + c0o;
+    FETODE_MARK("H_FEAT");
+    {
+      const float pv = h_gate ? (re1 ? h : prev1) : 0.f;
+#pragma unroll
+      for (int r = 0; r < RH; ++r) {
+        const float hx = (FERRO && r == RG) ? h - pv : h;
+        const float e = ex2(ffma(hna[r], hx, hab[r]));
+        const float sg = rcp(1.0f + e);
+        float val;
+        if (r == RS || (FERRO && (r == RG || r == RE))) {
+          val = ffma(sg, (r == RS && h_silu) ? h : hmul[r], hadd[r]);
+          if (FERRO && r == RE) val = h_exp ? e : val;
+        } else {
+          val = sg;
+        }
+        *hdst[r] = val;
+      }
+      if (FERRO) prev1 = h;
+      re1 = false;
+      float cntf = 0.f;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) cntf += h >= hknot[t] ? 1.0f : 0.0f;
+      cntf = quad_sum(cntf);
+      const int mm = (int)cntf - 1;
+      const bool fin = __builtin_isfinite(h);
+      const int mfix = ((unsigned)mm < (unsigned)NI && fin) ? mm : NI;
+      const int tq = mfix >> 2;
+      // register select chain; the empty asm keeps it from becoming an indexed (scratch) load
+      float knm = hknot[0], rhm = hrh[0];
+      asm volatile("" : "+v"(knm), "+v"(rhm));
+#pragma unroll
+      for (int t = 1; t < KT; ++t) {
+        knm = tq == t ? hknot[t] : knm;
+        rhm = tq == t ? hrh[t] : rhm;
+        asm volatile("" : "+v"(knm), "+v"(rhm));
+      }
+      if (act0 && q == (mfix & 3)) L1.G[o0].w = mfix < NI ? (h - knm) * rhm : (fin ? 0.0f : __builtin_nanf(""));
+      if (act0 && q == 0) {
+        L1.G[o0].x = h;
+        L1.M[o0] = mfix;
+      }
+    }
+    wave_lds_sync();
+    FETODE_MARK("EDGES1");
+    const float v = v4_edges<H, FLEN1, NI, NPL1, FPL1, FERRO, F_>(L1, sp1_o, gi1, ep1, k21, kE1, cp1, fw1, fofs1, spl1,
+                                                                  si1, a.P1.gsl2e);
+    const float kr = rowpair_sum(v) + c1o;
+    FETODE_MARK("END");
+    wave_lds_sync();  // the next evaluation overwrites the feature blocks these reads used
+    return kr;
+  };
+
+  // the step / output schedule staged through LDS in chunks (shared by the NW waves)
+  constexpr int SCH = 32;
+  __shared__ float s_dt[SCH], s_hh[SCH], s_h6[SCH], s_oslope[SCH];
+  __shared__ int s_ostep[SCH], s_omode[SCH];
+  auto load_steps = [&](int s0) {
+    __syncthreads();
+    for (int i = tid; i < SCH && s0 + i < a.n_steps; i += 64 * NW) {
+      s_dt[i] = a.step_coef[4 * (s0 + i) + 0];
+      s_hh[i] = a.step_coef[4 * (s0 + i) + 1];
+      s_h6[i] = a.step_coef[4 * (s0 + i) + 2];
+    }
+    __syncthreads();
+  };
+  auto load_outs = [&](int j0) {
+    __syncthreads();
+    for (int i = tid; i < SCH; i += 64 * NW) {
+      const bool in = j0 + i < a.T;
+      s_ostep[i] = in ? a.out_step[j0 + i] : -1;
+      s_omode[i] = in ? a.out_mode[j0 + i] : 1;
+      s_oslope[i] = in ? a.out_slope[j0 + i] : 0.f;
+    }
+    __syncthreads();
+  };
+  auto ckpt_write = [&](int s) __attribute__((always_inline)) {
+    if (a.ckpt && valid) {
+      float* ck = a.ckpt + ((int64_t)s * a.B + b) * (D + SW);
+      if ((l & 31) == 0) ck[dx] = y;
+      if (own0) ck[D + dx] = prev0;
+      if (own1) ck[D + D + o0] = prev1;
+    }
+  };
+  auto out_write = [&](int j, float v) __attribute__((always_inline)) {
+    if (yw) a.solution[((int64_t)j * a.B + b) * D + dx] = v;
+  };
+  using FT = std::integral_constant<bool, true>;
+  using FF = std::integral_constant<bool, false>;
+
+  if constexpr (HOT) {
+    int sb = 0, jb = 1, jj = 1;
+    load_steps(0);
+    load_outs(1);
+    auto run = [&](auto fact_tag) __attribute__((always_inline)) {
+      const float third = 1.0f / 3.0f;
+      for (int s = 0; s < a.n_steps; ++s) {
+        if (s - sb == SCH) {
+          sb = s;
+          load_steps(s);
+        }
+        if (jj + 1 - jb >= SCH) {
+          jb = jj;
+          load_outs(jj);
+        }
+        const int sr = s - sb, jr = jj - jb;
+        const float dt = s_dt[sr];
+        const int os0 = s_ostep[jr], os1 = s_ostep[jr + 1], om0 = s_omode[jr];
+        const float osl0 = s_oslope[jr];
+        ckpt_write(s);
+        const float k1 = eval_body(y, fact_tag);
+        const float k2 = eval_body(y + (dt * k1) * third, fact_tag);
+        const float k3 = eval_body(y + dt * (k2 - k1 * third), fact_tag);
+        const float k4 = eval_body(y + dt * ((k1 - k2) + k3), fact_tag);
+        const float y1 = y + (((k1 + 3.0f * (k2 + k3)) + k4) * dt) * 0.125f;
+        if (os0 == s) {
+          int m0 = om0;
+          float sl0 = osl0;
+          asm volatile("" : "+v"(m0), "+v"(sl0));
+          out_write(jj, m0 == 0 ? y : (m0 == 1 ? y1 : y + sl0 * (y1 - y)));
+          ++jj;
+          if (os1 == s) {
+            while (jj < a.T) {
+              if (jj - jb == SCH) {
+                jb = jj;
+                load_outs(jj);
+              }
+              if (s_ostep[jj - jb] != s) break;
+              const int mode = s_omode[jj - jb];
+              out_write(jj, mode == 0 ? y : (mode == 1 ? y1 : y + s_oslope[jj - jb] * (y1 - y)));
+              ++jj;
+            }
+          }
+        }
+        y = y1;
+      }
+    };
+    if (fact) run(FT{});
+    else run(FF{});
+  } else {
+    auto eval = [&](float xin) __attribute__((always_inline)) -> float {
+      if (fact) return eval_body(xin, FT{});
+      return eval_body(xin, FF{});
+    };
+    if (a.single_eval) {
+      const float f = eval(y);
+      if (yw) a.eval_out[b * D + dx] = f;
+    } else {
+      const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4
+                     : a.method == FETODE_MIDPOINT ? 2 : 1;
+      const float third = 1.0f / 3.0f;
+      int sb = 0, jb = 1, jj = 1;
+      load_steps(0);
+      load_outs(1);
+      for (int s = 0; s < a.n_steps; ++s) {
+        if (s - sb == SCH) {
+          sb = s;
+          load_steps(s);
+        }
+        const float dt = s_dt[s - sb], hh = s_hh[s - sb], h6 = s_h6[s - sb];
+        ckpt_write(s);
+        float k1 = 0.f, k2 = 0.f, k3 = 0.f, k4 = 0.f;
+        for (int st = 0; st < ns; ++st) {
+          float xin = y;
+          if (a.method == FETODE_RK4) {
+            if (st == 1) xin = y + (dt * k1) * third;
+            else if (st == 2) xin = y + dt * (k2 - k1 * third);
+            else if (st == 3) xin = y + dt * ((k1 - k2) + k3);
+          } else if (a.method == FETODE_RK4_CLASSIC) {
+            if (st == 1) xin = y + hh * k1;
+            else if (st == 2) xin = y + hh * k2;
+            else if (st == 3) xin = y + dt * k3;
+          } else if (a.method == FETODE_MIDPOINT) {
+            if (st == 1) xin = y + k1 * hh;
+          }
+          const float kk = eval(xin);
+          if (st == 0) k1 = kk;
+          else if (st == 1) k2 = kk;
+          else if (st == 2) k3 = kk;
+          else k4 = kk;
+        }
+        float y1;
+        if (a.method == FETODE_RK4) y1 = y + (((k1 + 3.0f * (k2 + k3)) + k4) * dt) * 0.125f;
+        else if (a.method == FETODE_RK4_CLASSIC) y1 = y + h6 * (((k1 + 2.0f * k2) + 2.0f * k3) + k4);
+        else if (a.method == FETODE_MIDPOINT) y1 = y + dt * k2;
+        else y1 = y + dt * k1;
+        while (jj < a.T) {
+          if (jj - jb == SCH) {
+            jb = jj;
+            load_outs(jj);
+          }
+          if (s_ostep[jj - jb] != s) break;
+          const int mode = s_omode[jj - jb];
+          out_write(jj, mode == 0 ? y : (mode == 1 ? y1 : y + s_oslope[jj - jb] * (y1 - y)));
+          ++jj;
+        }
+        y = y1;
+      }
+    }
+  }
+  if (valid) {
+    if (own0) a.state[b * D + dx] = prev0;
+    if (own1) a.state[a.B * D + b * H + o0] = prev1;
+  }
+}
+
 typedef void (*fused_fn)(FusedArgs);
 struct FusedEntry {
   int in0, h, out, K, NB, NG;
@@ -1279,6 +1748,11 @@ const FusedEntry kFused[] = {
      fused4_kernel<10, 10, 10, 12, true, true>},
     {2, 10, 2, 1, 10, 12, false, fused4_kernel<10, 2, 10, 12, false, false>, 64, 4,
      fused4_kernel<10, 2, 10, 12, false, true>},
+    // v5: one trajectory per wave (small batches; FETODE_FUSED_LPT=5 forces it)
+    {2, 10, 2, 10, 10, 12, true, fused5_kernel<10, 10, 10, 12, true, false, 2>, 128, 5,
+     fused5_kernel<10, 10, 10, 12, true, true, 2>},
+    {2, 10, 2, 1, 10, 12, false, fused5_kernel<10, 2, 10, 12, false, false, 2>, 128, 5,
+     fused5_kernel<10, 2, 10, 12, false, true, 2>},
     // v3 (FETODE_FUSED_LPT=3)
     {2, 10, 2, 10, 10, 12, true, fused3_kernel<10, 10, 10, 12, true>, 64, 3},
     {2, 10, 2, 1, 10, 12, false, fused3_kernel<10, 1, 10, 12, false>, 64, 3},
@@ -1294,36 +1768,39 @@ const FusedEntry kFused[] = {
     FUSED(2, 10, 2, 1, 10, 12, false, 64, 256),
 };
 
-// workgroup size: 64 threads (one wave, 2 trajectories; its barriers cost almost nothing)
-// unless FETODE_FUSED_NT says otherwise (measured: 64 >= 256 at B=4096 and 1.11x at B=65536)
-int preferred_nt() {
-  static int nt = [] {
-    const char* e = getenv("FETODE_FUSED_NT");
-    return e ? atoi(e) : 64;
-  }();
-  return nt;
+// Kernel variant.  Default: v4 at every batch — measured, v5 (one trajectory per wave) is not
+// faster even where it has twice the waves: a wave's evaluation is bound by its dependent
+// chain (~0.17 ms per 34-step solve for one wave alone, v4 and v5 alike), and v5 needs 146+
+// VGPRs (3 waves/SIMD).  kV5MaxBatch keeps the switch for when that changes.
+// FETODE_FUSED_LPT=5|4|3 forces v5 / v4 / v3, 32|64 a v2 variant (with FETODE_FUSED_NT=64|256
+// its workgroup size).
+constexpr int64_t kV5MaxBatch = 0;
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
 }
-// kernel variant: 4 = v4 (packed pairs, default); FETODE_FUSED_LPT=3 selects v3, 32|64 a v2 variant
-int preferred_lpt() {
-  static int v = [] {
-    const char* e = getenv("FETODE_FUSED_LPT");
-    return e ? atoi(e) : 4;
-  }();
+int forced_lpt() {
+  static int v = env_int("FETODE_FUSED_LPT", 0);
   return v;
 }
+int preferred_nt() {
+  static int nt = env_int("FETODE_FUSED_NT", 64);
+  return nt;
+}
 
-const FusedEntry* find_fused(const fetode_field_t* f) {
+const FusedEntry* find_fused(const fetode_field_t* f, int64_t B) {
   if (f->n_layers != 2) return nullptr;
   const fetode_kanlinear_t &k0 = f->kan[0], &k1 = f->kan[1];
   if (k0.grid_size != k1.grid_size || k0.spline_order != k1.spline_order ||
       k0.num_logistic != k1.num_logistic)
     return nullptr;
   const int NG = k0.grid_size + 2 * k0.spline_order + 1;
+  const int want = forced_lpt() ? forced_lpt() : (B <= kV5MaxBatch ? 5 : 4);
   for (const FusedEntry& e : kFused) {
     if (e.in0 != k0.in_features || e.h != k0.out_features || e.out != k1.out_features) continue;
     if (e.NB != k0.num_logistic || e.NG != NG) continue;
     if (e.ferro != (f->ferro != nullptr)) continue;
-    if (e.nt != preferred_nt() || e.lpt != preferred_lpt()) continue;
+    if (e.lpt != want || (e.lpt >= 32 && e.nt != preferred_nt())) continue;
     if (f->ferro) {
       if (f->ferro[0].num_basis != e.K || f->ferro[1].num_basis != e.K) continue;
       if (f->ferro[0].branch_sign || f->ferro[1].branch_sign) continue;  // general sign: generic path
@@ -1334,11 +1811,12 @@ const FusedEntry* find_fused(const fetode_field_t* f) {
 }
 
 int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
-  const FusedEntry* e = find_fused(f);
+  const FusedEntry* e = find_fused(f, a.B);
   if (!e) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
   layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
   layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
-  const int tpb = e->lpt <= 4 ? 2 : e->nt / e->lpt;
+  // trajectories per workgroup: v3/v4 two per wave (one wave), v5 one per wave, v2 nt/lpt
+  const int tpb = e->lpt == 5 ? e->nt / 64 : (e->lpt <= 4 ? 2 : e->nt / e->lpt);
   const fused_fn fn = (e->fn_rk4 && !a.single_eval && a.method == FETODE_RK4) ? e->fn_rk4 : e->fn;
   hipLaunchKernelGGL(fn, dim3(nblk(a.B, tpb)), dim3(e->nt), 0, (hipStream_t)stream, a);
   LAUNCH_CHECK();
@@ -1357,7 +1835,7 @@ int fetode_debug_stamp_buffer(void* p) {
 
 int fetode_fused_supported(const fetode_field_t* f) {
   if (validate_field(f) != FETODE_OK) return 0;
-  return find_fused(f) != nullptr;
+  return find_fused(f, 1) != nullptr;
 }
 
 int fetode_field_forward(const fetode_field_t* f, const void* plan, const float* x, int64_t B,

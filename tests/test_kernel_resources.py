@@ -1,0 +1,63 @@
+"""Static checks of the built gfx950 code objects: no kernel of libfetode spills to scratch.
+
+A register spill turns into per-lane global-memory traffic inside the integrator's inner loop
+(a compiler select-to-lookup transform once put two knot arrays in scratch and cost ~15 % of
+the v4 kernel).  The metadata is read from the offload bundles embedded in libfetode.so with
+llvm-readelf; the test needs no GPU."""
+import os
+import re
+import struct
+import subprocess
+
+import pytest
+
+from conftest import REPO
+
+LIB = os.path.join(REPO, "fet-ode_amd", "libfetode.so")
+READELF = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+
+
+def gfx950_code_objects(path):
+    data = open(path, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    pos = data.find(magic)
+    while pos >= 0:
+        n = struct.unpack_from("<Q", data, pos + 24)[0]
+        p = pos + 32
+        for _ in range(n):
+            off, size, tl = struct.unpack_from("<QQQ", data, p)
+            p += 24
+            triple = data[p:p + tl].decode()
+            p += tl
+            if "gfx950" in triple and size:
+                yield data[pos + off:pos + off + size]
+        pos = data.find(magic, pos + 1)
+
+
+def kernel_metadata(path, tmp_path):
+    kernels = {}
+    for k, blob in enumerate(gfx950_code_objects(path)):
+        f = tmp_path / f"co{k}.elf"
+        f.write_bytes(blob)
+        notes = subprocess.run([READELF, "--notes", str(f)], capture_output=True, text=True, check=True).stdout
+        cur = None
+        for line in notes.splitlines():
+            m = re.match(r"\s+\.name:\s+(\S+)", line)
+            if m:
+                cur = kernels.setdefault(m.group(1), {})
+                continue
+            m = re.match(r"\s+\.(private_segment_fixed_size|vgpr_count|vgpr_spill_count|sgpr_spill_count):\s+(\d+)",
+                         line)
+            if m and cur is not None:
+                cur[m.group(1)] = int(m.group(2))
+    return kernels
+
+
+@pytest.mark.skipif(not (os.path.exists(LIB) and os.path.exists(READELF)), reason="libfetode.so / llvm-readelf")
+def test_no_kernel_uses_scratch(tmp_path):
+    ks = kernel_metadata(LIB, tmp_path)
+    fused = [n for n in ks if "fused" in n]
+    assert len(fused) >= 8, sorted(ks)
+    bad = {n: v for n, v in ks.items()
+           if v.get("private_segment_fixed_size", 0) or v.get("vgpr_spill_count", 0) or v.get("sgpr_spill_count", 0)}
+    assert not bad, bad
