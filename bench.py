@@ -191,7 +191,7 @@ def main():
                        "parallelism": f"trajectory-sharded x{world} (no collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "fused3_kernel<10,10,10,12,true> (v3)",
+                         "kernel": "fused4_kernel<10,10,10,12,true,true> (v4 rk4 path)",
                          "kernel_ms": k_ms, "alg_bytes_per_launch": bytes_launch,
                          "traffic_source": traffic_src,
                          "valu": {"achieved_tflops": tflops, "peak_tflops": FP32_PEAK_TFLOPS,

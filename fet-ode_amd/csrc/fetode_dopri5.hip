@@ -22,10 +22,12 @@ __global__ void lincomb_kernel(const float* __restrict__ y0, const float* __rest
   out[t] = y0 ? y0[t] + acc : acc;
 }
 
-// sqrt(mean(((a - sub) / (atol + rtol * max(|y0|, |y1|)))^2)), one workgroup, fp64 accumulation
+// sum(((a - sub) / (atol + rtol * max(|y0|, |y1|)))^2), one workgroup, fp64 accumulation;
+// RMS = true writes sqrt(sum / n) as fp32 (misc._rms_norm), false the raw fp64 sum
+template <bool RMS>
 __global__ void scaled_rms_kernel(const float* __restrict__ a, const float* __restrict__ sub,
                                   const float* __restrict__ y0, const float* __restrict__ y1, float rtol,
-                                  float atol, int64_t n, float* __restrict__ out) {
+                                  float atol, int64_t n, void* __restrict__ out_) {
   __shared__ double red[1024];
   __shared__ int bad;
   if (threadIdx.x == 0) bad = 0;
@@ -48,8 +50,15 @@ __global__ void scaled_rms_kernel(const float* __restrict__ a, const float* __re
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    out[0] = sqrtf((float)(red[0] / (double)n));
-    out[1] = bad ? 1.0f : 0.0f;  // torchdiffeq asserts torch.isfinite(y0).all() every step
+    if constexpr (RMS) {
+      float* out = static_cast<float*>(out_);
+      out[0] = sqrtf((float)(red[0] / (double)n));
+      out[1] = bad ? 1.0f : 0.0f;  // torchdiffeq asserts torch.isfinite(y0).all() every step
+    } else {
+      double* out = static_cast<double*>(out_);
+      out[0] = red[0];
+      out[1] = bad ? 1.0 : 0.0;
+    }
   }
 }
 
@@ -105,8 +114,20 @@ int fetode_lincomb(const float* y0, const float* k, int64_t kstride, const float
 int fetode_scaled_rms(const float* a, const float* sub, const float* y0, const float* y1, double rtol, double atol,
                       int64_t n, float* out, void* stream) {
   if (n <= 0 || !a || !y0 || !out) return set_err(FETODE_EINVAL, "scaled_rms: bad arguments");
-  hipLaunchKernelGGL(scaled_rms_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, a, sub, y0, y1, (float)rtol,
-                     (float)atol, n, out);
+  hipLaunchKernelGGL(scaled_rms_kernel<true>, dim3(1), dim3(1024), 0, (hipStream_t)stream, a, sub, y0, y1,
+                     (float)rtol, (float)atol, n, (void*)out);
+  LAUNCH_CHECK();
+  return FETODE_OK;
+}
+
+int fetode_scaled_sumsq(const float* a, const float* sub, const float* y0, const float* y1, double rtol, double atol,
+                        int64_t n, double* out, void* stream) {
+  if (n < 0 || !out || (n > 0 && (!a || !y0))) return set_err(FETODE_EINVAL, "scaled_sumsq: bad arguments");
+  if (n == 0) return hipMemsetAsync(out, 0, 2 * sizeof(double), (hipStream_t)stream) == hipSuccess
+                         ? FETODE_OK
+                         : set_err(FETODE_EHIP, "scaled_sumsq: memset failed");
+  hipLaunchKernelGGL(scaled_rms_kernel<false>, dim3(1), dim3(1024), 0, (hipStream_t)stream, a, sub, y0, y1,
+                     (float)rtol, (float)atol, n, (void*)out);
   LAUNCH_CHECK();
   return FETODE_OK;
 }

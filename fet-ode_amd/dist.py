@@ -8,6 +8,11 @@ live on one rank.  Training adds ONE all-reduce per iteration: all parameter gra
 flattened into a single fp32 bucket (12.2 KB for KANFET [2,10,2]) — a latency-bound message
 on xGMI, so one fused bucket and no pipelining.
 
+Adaptive solves (dopri5) shard too, with one exchange: the error ratio torchdiffeq tests is the
+RMS over the WHOLE batch, so ``odeint_sharded`` all-reduces two fp64 words (sum of squares,
+non-finite flag) per norm — 6 per attempt-free step selection, 1 per attempt — and every rank
+takes the step sequence a single device would take on the global batch (SURVEY §8e caveat 2).
+
 Caveat kept from the reference semantics: a fresh FerroelectricBasis re-initialises prev_x
 (dx = 0) on its first call unless the batch is 1 (ferro_class.py:373-375).  Sharding a global
 batch B > 1 into shards of size 1 would flip that rule, so ``shard_bounds`` refuses it.
@@ -80,3 +85,15 @@ def allreduce_gradients(params: Iterable[torch.nn.Parameter], average: bool = Tr
         flat.div_(w)
     for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
         g.copy_(f)
+
+
+def odeint_sharded(func, y0_local: torch.Tensor, t: torch.Tensor, *, rtol=1e-7, atol=1e-9, method=None,
+                   options: Optional[dict] = None, group=None):
+    """odeint over this rank's shard of a trajectory-sharded batch.  Fixed-grid methods need no
+    communication; adaptive ones use the global-batch error norm (all ranks, same steps)."""
+    from .odeint import odeint
+    opts = dict(options or {})
+    _, w = world()
+    if w > 1 and (method is None or method == "dopri5"):
+        opts["norm_group"] = "world" if group is None else group
+    return odeint(func, y0_local, t, rtol=rtol, atol=atol, method=method, options=opts)

@@ -57,6 +57,9 @@ class _Dopri5:
         if unsupported:
             raise NotImplementedError(f"dopri5 options not supported: {unsupported}")
         self.lib = _lib.load()
+        # trajectory-sharded solve (dist.odeint_sharded): every error norm is the RMS over the
+        # global batch, so all ranks take the same steps as one device would
+        self.group = options.get("norm_group")
         self.func_user = func
         self.sign = -1.0 if reversed_ else 1.0
         self.y0 = y0.contiguous()
@@ -73,6 +76,20 @@ class _Dopri5:
         self.max_num_steps = int(options.get("max_num_steps", 2 ** 31 - 1))
         self.k = torch.empty(7, self.n, device=self.dev, dtype=torch.float32)
         self.scal = torch.empty(2, device=self.dev, dtype=torch.float32)
+        self.n_global = self.n
+        if self.group is not None:
+            import torch.distributed as dist
+            self.group = None if self.group == "world" else self.group
+            self.dist = dist
+            self.scal64 = torch.empty(2, device=self.dev, dtype=torch.float64)
+            self.cpu_reduce = dist.get_backend(self.group) != "nccl"
+            cnt = torch.tensor([float(self.n)], dtype=torch.float64,
+                               device="cpu" if self.cpu_reduce else self.dev)
+            dist.all_reduce(cnt, group=self.group)
+            self.n_global = int(cnt.item())
+            self.distributed = True
+        else:
+            self.distributed = False
         self.nfev = 0
         self.attempts = []   # (t0, dt, error_ratio, accepted) like the oracle's Dopri5Trace
 
@@ -98,10 +115,21 @@ class _Dopri5:
         return out
 
     def rms(self, a, sub, y0, y1, check_finite=False) -> float:
-        _lib.check(self.lib.fetode_scaled_rms(a.data_ptr(), _lib.ptr(sub), y0.data_ptr(), _lib.ptr(y1),
-                                              self.rtol, self.atol, self.n, self.scal.data_ptr(), self.stream),
-                   "fetode_scaled_rms")
-        r, bad = self.scal.tolist()           # one device->host read per call
+        if self.distributed:
+            # local sum of squares -> all-reduce (sum, non-finite count) -> global RMS, rounded
+            # like the single-device kernel: sqrtf((float)(sum / n))
+            _lib.check(self.lib.fetode_scaled_sumsq(a.data_ptr(), _lib.ptr(sub), y0.data_ptr(), _lib.ptr(y1),
+                                                    self.rtol, self.atol, self.n, self.scal64.data_ptr(),
+                                                    self.stream), "fetode_scaled_sumsq")
+            t = self.scal64.cpu() if self.cpu_reduce else self.scal64
+            self.dist.all_reduce(t, group=self.group)
+            ssum, bad = t.tolist()
+            r = np.sqrt(np.float32(ssum / self.n_global))
+        else:
+            _lib.check(self.lib.fetode_scaled_rms(a.data_ptr(), _lib.ptr(sub), y0.data_ptr(), _lib.ptr(y1),
+                                                  self.rtol, self.atol, self.n, self.scal.data_ptr(), self.stream),
+                       "fetode_scaled_rms")
+            r, bad = self.scal.tolist()           # one device->host read per call
         if check_finite and bad:
             raise AssertionError("non-finite values in state `y`")
         return np.float32(r)

@@ -1,7 +1,9 @@
 #!/bin/bash
-# PMC counter passes on the bench command (one counter group per pass; no tracing domains)
+# One measurement round on the GPU box: rocprofv3 PMC passes (one counter group per pass, no
+# tracing domains), the kernel-trace stats, then the contract bench.  The HBM-traffic summary
+# is written before the bench runs so the bench line cites this round's counters.
 cd "$(dirname "$0")/.."
-R=${ROUND:-r01v3}
+R=${ROUND:-r01_v4}
 O=gpurun_out
 mkdir -p $O
 export TMPDIR=/tmp
@@ -12,7 +14,8 @@ step pmc_b timeout -k 10 400 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_
 step pmc_fetch timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$R -o run --output-format csv -- $B
 step pmc_write timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_$R -o run --output-format csv -- $B
 step prof_stats timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$R -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline
+python tools/pmc_traffic.py $O/pmc_fetch_$R $O/pmc_write_$R $O/pmc_a_$R $O/pmc_b_$R --out $O/${R}_pmc_traffic.json > $O/pmc_traffic.log 2>&1 || exit 3
+mkdir -p profiles && cp $O/${R}_pmc_traffic.json profiles/${R}_pmc_traffic.json
 step bench timeout -k 10 400 python bench.py
 tail -1 $O/bench.log > $O/bench_$R.json
-python tools/pmc_traffic.py $O/pmc_fetch_$R $O/pmc_write_$R $O/pmc_a_$R $O/pmc_b_$R --out $O/${R}_pmc_traffic.json | tail -30
 cat $O/bench_$R.json
