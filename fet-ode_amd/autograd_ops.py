@@ -7,6 +7,8 @@ state is a detached snapshot in the reference (:381-382), so it carries no gradi
 """
 from __future__ import annotations
 
+import os
+
 from typing import List, Optional
 
 import torch
@@ -35,7 +37,19 @@ def grad_enabled_for(*tensors) -> bool:
 # plans (pre-transformed parameters, one small kernel per call)
 # ---------------------------------------------------------------------------------------------
 
+_PLAN_CACHE = os.environ.get("FETODE_NO_PLAN_CACHE", "0") != "1"
+
+
 def build_plan(owner, handle: _lib.FieldHandle, device) -> torch.Tensor:
+    """The pre-transformed parameters of the field (fetode_plan_build).  Rebuilt whenever the
+    descriptor is: make_handle keeps a descriptor only while every parameter tensor is the same
+    storage at the same version counter, i.e. until anything writes a parameter through autograd-
+    visible ops (optimizer steps, load_state_dict, in-place updates).  Writes through `.data`
+    bypass version counters; call `owner._fetode_handle = None` after those (or set
+    FETODE_NO_PLAN_CACHE=1 to rebuild on every solve)."""
+    plan = getattr(owner, "_fetode_plan", None)
+    if _PLAN_CACHE and plan is not None and getattr(owner, "_fetode_plan_for", None) is handle:
+        return plan
     lib = _lib.load()
     nbytes = lib.fetode_plan_bytes(handle.ref)
     if nbytes < 0:
@@ -47,6 +61,7 @@ def build_plan(owner, handle: _lib.FieldHandle, device) -> torch.Tensor:
         owner._fetode_plan = plan
     _lib.check(lib.fetode_plan_build(handle.ref, plan.data_ptr(), _lib.stream_handle(device)),
                "fetode_plan_build")
+    owner._fetode_plan_for = handle
     return plan
 
 

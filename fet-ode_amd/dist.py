@@ -59,11 +59,12 @@ def broadcast_parameters(module: torch.nn.Module, src: int = 0) -> None:
     _, w = world()
     if w == 1:
         return
-    ps = [p.data for p in module.parameters()]
-    flat = torch._utils._flatten_dense_tensors(ps)
-    dist.broadcast(flat, src)
-    for p, f in zip(ps, torch._utils._unflatten_dense_tensors(flat, ps)):
-        p.copy_(f)
+    ps = list(module.parameters())
+    with torch.no_grad():
+        flat = torch._utils._flatten_dense_tensors([p.detach() for p in ps])
+        dist.broadcast(flat, src)
+        for p, f in zip(ps, torch._utils._unflatten_dense_tensors(flat, ps)):
+            p.copy_(f)   # through the Parameter: bumps its version, so cached plans rebuild
 
 
 def allreduce_gradients(params: Iterable[torch.nn.Parameter], average: bool = True,

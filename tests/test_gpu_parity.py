@@ -268,3 +268,36 @@ def test_state_carries_over_between_solves(dev):
     with torch.no_grad():
         c = F.odeint(F.autonomous(fresh), y0.to(dev), t2, method="rk4").cpu()
     assert slice_rel_err(c, e) > 1e-3   # the carried state matters
+
+
+def test_plan_cache_follows_parameter_updates(dev):
+    """The pre-transformed plan is reused across solves only while no parameter changed: an
+    in-place update (optimizer-style) or load_state_dict must show up in the next solve."""
+    import fet_ode_amd as F
+    g = load_golden("traj_kanfet")
+    y0 = torch.from_numpy(g["y0_B64"]).to(dev)
+    t = torch.from_numpy(g["t35"])[:5]
+
+    def warm():
+        mm = _kanfet_from(g, dev)
+        F.odeint(F.autonomous(mm), y0, t, method="rk4")   # builds and caches the plan
+        return mm
+
+    def solve(mm):
+        mm.reset_state()
+        return F.odeint(F.autonomous(mm), y0, t, method="rk4").cpu()
+
+    with torch.no_grad():
+        m = warm()
+        for layer in m.layers:
+            layer.kan.base_weight.mul_(1.5)
+            layer.ferro.coef.add_(0.01)
+        a = solve(m)
+        fresh = warm()
+        for lf, lm in zip(fresh.layers, m.layers):
+            lf.kan.base_weight.copy_(lm.kan.base_weight)
+            lf.ferro.coef.copy_(lm.ferro.coef)
+        assert torch.equal(a, solve(fresh))
+        m.load_state_dict(golden_sd(g))      # replaces weights AND the hysteresis buffers
+        c = solve(m)
+        assert torch.equal(c, solve(_kanfet_from(g, dev))) and not torch.equal(a, c)
