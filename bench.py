@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--train-iters", type=int, default=5, help="0 skips the training-rate line")
     return ap.parse_args()
 
 
@@ -108,6 +109,44 @@ def pmc_traffic_per_launch():
     return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], REPO)
 
 
+def train_rate(model, y0d, t, iters, warmup, world):
+    """One training iteration = forward rk4 solve with autograd + backward through every stage
+    (HIP VJPs) + gradient all-reduce (RCCL when world > 1) + Adam."""
+    import fet_ode_amd.dist as D
+    dev = y0d.device
+    func = F.autonomous(model)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    target = torch.zeros(T, y0d.shape[0], 2, device=dev)
+
+    def it():
+        opt.zero_grad(set_to_none=True)
+        sol = F.odeint(func, y0d, t, method="rk4")
+        loss = (sol - target).square().mean()
+        loss.backward()
+        D.allreduce_gradients(list(model.parameters()))
+        opt.step()
+
+    for _ in range(warmup):
+        it()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        it()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        torch.distributed.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([el], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+        el = tt.item()
+    return {"value": world * iters * STEPS_PER_SOLVE / el, "unit": "RK4 steps/s trained (fwd+bwd+allreduce+Adam)",
+            "ms_per_iter": el / iters * 1e3, "iters": iters,
+            "path": "per-stage HIP kernels + HIP VJPs (fused backward not built yet)"}
+
+
 def cpu_baseline(sd, y0, t, seconds):
     """The CPU oracle (restatement of the reference, reference op order) on this host's cores."""
     from oracle import torch_ref as O
@@ -132,6 +171,29 @@ def cpu_baseline(sd, y0, t, seconds):
             "kind": "port",
             "sample": f"{n_solves} full solve(s) of the bench workload (B=4096, 34 rk4 steps) with "
                       f"oracle/torch_ref.py (reference op order, torch CPU fp32), {el:.1f} s"}, sol
+
+
+def cpu_train_baseline(sd, y0, t, seconds, sample_b=512):
+    """The CPU oracle's training iteration (fwd with autograd + bwd) on a bounded sample of the
+    bench workload: the first `sample_b` trajectories, rate scaled to batch-4096 steps (the CPU
+    cost is linear in the batch at these sizes).  The Adam update (3 052 parameters) is left out."""
+    from oracle import torch_ref as O
+    cores = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(cores)
+    y0 = y0[:sample_b]
+    target = torch.zeros(T, y0.shape[0], 2)
+    n, t0 = 0, time.perf_counter()
+    while n < 1 or (time.perf_counter() - t0 < seconds and n < 10):
+        ps = {k: v.clone().requires_grad_(v.is_floating_point() and "grid" not in k) for k, v in sd.items()}
+        ref = O.KANFETRef.from_state_dict(ps, 2)
+        sol = O.odeint(lambda tt, yy: ref(yy), y0, t, method="rk4")
+        (sol - target).square().mean().backward()
+        n += 1
+    el = time.perf_counter() - t0
+    return {"value": n * STEPS_PER_SOLVE / el * sample_b / B, "unit": "RK4 steps/s trained (fwd+bwd, batch 4096)",
+            "cores": cores, "kind": "port",
+            "sample": f"{n} fwd+bwd iteration(s) of {sample_b} of the 4096 bench trajectories (34 rk4 steps) with "
+                      f"oracle/torch_ref.py autograd (torch CPU fp32), {el:.1f} s; rate scaled by {sample_b}/{B}"}
 
 
 def main():
@@ -171,6 +233,7 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             el = tt.item()
         k_ms = kernel_time_ms(model, y0d, t)
+    train = train_rate(model, y0d, t, args.train_iters, 2, world) if args.train_iters > 0 else None
     ms_per_step = el / args.steps * 1e3
     value = world * args.steps * STEPS_PER_SOLVE / el
 
@@ -198,9 +261,13 @@ def main():
                                   "frac": tflops / FP32_PEAK_TFLOPS,
                                   "alg_flops_per_launch": flops_launch}},
         }
+        if train is not None:
+            out["train"] = train
         if world == 1 and not args.no_cpu_baseline:
             cb, ref_sol = cpu_baseline(sd, y0, t, args.cpu_seconds)
             out["cpu_baseline"] = cb
+            if train is not None:
+                out["train"]["cpu_baseline"] = cpu_train_baseline(sd, y0, t, args.cpu_seconds)
             fresh = F.KANFET([2, 10, 2], grid_size=5)
             fresh.load_state_dict(sd)          # fresh hysteresis state, as the CPU solve had
             with torch.no_grad():
