@@ -12,8 +12,8 @@ from . import _lib
 from . import efficientkan, ferro_class
 from .efficientkan import KAN, KANFET, KANFETLayer, KANLinear, LogisticBasis, ODEFunc, autonomous
 from .ferro_class import FerroelectricBasis
-from .odeint import SOLVERS, odeint
+from .odeint import SOLVERS, odeint, set_fused_training
 
-__all__ = ["odeint", "SOLVERS", "KAN", "KANFET", "KANFETLayer", "KANLinear", "LogisticBasis",
+__all__ = ["odeint", "SOLVERS", "set_fused_training", "KAN", "KANFET", "KANFETLayer", "KANLinear", "LogisticBasis",
            "FerroelectricBasis", "ODEFunc", "autonomous", "efficientkan", "ferro_class"]
 __version__ = "0.1.0"

@@ -92,6 +92,13 @@ SIGNATURES = {
                                                  ctypes.POINTER(KANLinearGrad), _vp, ctypes.c_int32, _vp]),
     "fetode_ferro_backward": (ctypes.c_int, [ctypes.POINTER(FerroDesc), _vp, ctypes.c_int64, _vp, ctypes.c_int32,
                                              _vp, _vp, ctypes.POINTER(FerroGrad), ctypes.c_int32, _vp]),
+    "fetode_fused_backward_supported": (ctypes.c_int, [ctypes.POINTER(FieldDesc)]),
+    "fetode_integrate_fixed_backward_workspace": (ctypes.c_int64, [ctypes.POINTER(FieldDesc), ctypes.c_int64]),
+    "fetode_integrate_fixed_backward": (ctypes.c_int, [ctypes.POINTER(FieldDesc), _vp, ctypes.c_int32, ctypes.c_int64,
+                                                       _vp, ctypes.c_int32, _vp, _vp, _vp, ctypes.c_int32,
+                                                       _vp, _vp, _vp, ctypes.c_uint32, _vp,
+                                                       ctypes.POINTER(KANLinearGrad), ctypes.POINTER(FerroGrad),
+                                                       _vp, _vp]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

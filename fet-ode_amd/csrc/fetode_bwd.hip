@@ -1,0 +1,737 @@
+// fetode_bwd.hip — the reverse sweep of the single-launch fixed-grid integrator (training).
+//
+// What it replaces: loss.backward() through torchdiffeq's fixed-grid solve of a KAN / KAN-FET
+// field (train_kanfet_node_predprey.py:254-257), i.e. reverse-mode autograd through every stage
+// evaluation (KANLinear.forward efficientkan.py:160-182, FerroelectricBasis.forward
+// ferro_class.py:368-420 whose prev_x / branch_sign snapshots are detached, :381-382), the
+// rk_common.rk4_alt_step_func stage combines and FixedGridODESolver's output interpolation.
+//
+// Data flow.  The forward kernel (fetode_fused.hip) records the two layer inputs of every
+// evaluation on a "tape" (n_evals, B, D + H); the hysteresis input of evaluation ev is the tape
+// row of ev - 1 (ferro_class.py:409), or the state before the solve for ev = 0.  So the sweep
+// recomputes nothing but per-input features: one wave owns one trajectory and walks its
+// evaluations backwards, carrying the adjoints of y and of the stage derivatives k_j.
+//
+// Per evaluation (layer 1 then layer 0, lanes = jobs):
+//   features   per input: SiLU, SiLU', dense B-spline bases, knot interval/coordinate, the
+//              hysteresis gate u = sigmoid(gs(x - prev)); per (input, basis): the logistic sigmoid
+//   Ferro      per element (i, o, k): the element's forward quantities and its VJP; parameter
+//              gradients are accumulated in three per-element sums A, C, E (see below)
+//   KAN edges  per (o, i): base + spline-coefficient sums, d/dx via the plan's cubic tables
+//   logistic   per (i, j): the logistic-weight sums and the a / b gradients
+//   d out/d x  per-job contributions land in an LDS table and are summed per input in a fixed
+//              order (segmented sum + xor shuffles): run-to-run deterministic, no atomics.
+// The gradient sums live in VGPRs for the whole sweep (each lane owns fixed slots), are written
+// once per block to a partial buffer, reduced over blocks in a fixed order (fp64), and turned
+// into parameter gradients by one small kernel:
+//   Ferro e = (i,o,k):  A = sum g_o th,  C = sum g_o (1-th^2) sh,  E = sum g_o (1-th^2)(m + Ec dm/dEc),
+//                       G_o = sum g_o   ->  dk = coef Ps C, dEc = coef Ps k E, dPs = coef A,
+//                       dbias = coef G_o, dcoef = Ps A + bias G_o
+//   KAN (o,i):          base = sum g_o SiLU(x_i), spline_c = sum g_o B_c(x_i)
+//   logistic (o,i,j):   sum g_o sigmoid_ij;  a_ij, b_ij directly.
+#include <cstring>
+
+#include "fetode_common.h"
+
+using namespace fetode;
+
+namespace {
+
+constexpr int kSO = 3;  // spline order of the fused kernels (efficientkan default)
+
+constexpr int pow2_floor(int v) {
+  int p = 1;
+  while (p * 2 <= v) p *= 2;
+  return p;
+}
+
+// Layout of one layer's gradient sums in a partial row (host and device agree on it).
+struct AccLayout {
+  int E, NE, NL, NS, NTM;
+  int oA, oC, oE, oG, oBase, oSpl, oLw, oLa, oLb, n;
+};
+__host__ __device__ constexpr AccLayout acc_layout(int in, int out, int K, int NB, int NS, bool ferro) {
+  AccLayout L{};
+  L.E = ferro ? in * out * K : 0;
+  L.NE = in * out;
+  L.NL = in * NB;
+  L.NS = NS;
+  L.NTM = (ferro ? out * K : 0) + out + NB;
+  L.oA = 0;
+  L.oC = L.E;
+  L.oE = 2 * L.E;
+  L.oG = 3 * L.E;
+  L.oBase = L.oG + (ferro ? out : 0);
+  L.oSpl = L.oBase + L.NE;
+  L.oLw = L.oSpl + L.NE * NS;
+  L.oLa = L.oLw + out * L.NL;
+  L.oLb = L.oLa + L.NL;
+  L.n = L.oLb + L.NL;
+  return L;
+}
+
+template <int IN_, int OUT_, int K_, int NB_, int NG_, bool FERRO_>
+struct BL {  // compile-time shape of one layer
+  static constexpr int IN = IN_, OUT = OUT_, K = FERRO_ ? K_ : 0, NB = NB_, NG = NG_;
+  static constexpr bool FERRO = FERRO_;
+  static constexpr int NI = NG - 1, NS = NG - 1 - kSO, NFL = 1 + NB;
+  static constexpr AccLayout AL = acc_layout(IN, OUT, K, NB, NS, FERRO);
+  static constexpr int E = AL.E, NE = AL.NE, NL = AL.NL, NTM = AL.NTM;
+  static constexpr int RF = (E + 63) / 64, RE = (NE + 63) / 64, RL = (NL + 63) / 64;
+  static constexpr int RF1 = RF > 0 ? RF : 1, RL1 = RL > 0 ? RL : 1;
+  static constexpr int LPI = pow2_floor(64 / IN);  // lanes per input in the d/dx segmented sum
+  static_assert(IN <= 64 && OUT <= 64, "layer widths up to 64");
+  static_assert(NS >= 1, "grid too small for cubic splines");
+};
+
+template <class L>
+struct BTab {  // per-block LDS copy of one layer's shared tables (staged once per launch)
+  float4 sp[L::OUT * L::IN * (L::NI + 1)];  // spline edge (o, i) as a cubic in u per interval
+  float knots[L::IN * L::NG];
+  float rk[L::IN * kSO * (L::NG - 1)];      // 1/(g[j+k]-g[j]) at [i][(k-1)(NG-1)+j]
+  float lg[L::NL > 0 ? 2 * L::NL : 1];      // (-a log2e, a b log2e)
+  float kw[L::OUT * L::IN * L::NFL];        // SiLU weight, 2 * scaled logistic weights
+  float pa[L::NL > 0 ? L::NL : 1], pb[L::NL > 0 ? L::NL : 1];
+  float4 fe[L::E > 0 ? L::E : 1];           // Ferro element (i,o,k): k, Ec, coef*Ps*k
+
+  __device__ void stage(const fetode_kanlinear_t& kl, const fetode_ferro_t& fl, const float* __restrict__ plan,
+                        const LayerPlan& P, int tid, int nt) {
+    for (int e = tid; e < L::E; e += nt) fe[e] = make_float4(fl.k[e], fl.Ec[e], (fl.coef[e] * fl.Ps[e]) * fl.k[e], 0.f);
+    const float4* src = reinterpret_cast<const float4*>(plan + P.sp);
+    for (int q = tid; q < L::OUT * L::IN * (L::NI + 1); q += nt) sp[q] = src[q];
+    for (int q = tid; q < L::IN * L::NG; q += nt) knots[q] = plan[P.knots + q];
+    for (int q = tid; q < L::IN * kSO * (L::NG - 1); q += nt) {
+      const int i = q / (kSO * (L::NG - 1)), r = q % (kSO * (L::NG - 1));
+      const int k = r / (L::NG - 1) + 1, j = r % (L::NG - 1);
+      const float* g = plan + P.knots + i * L::NG;
+      rk[q] = j + k < L::NG ? 1.0f / (g[j + k] - g[j]) : 0.f;
+    }
+    for (int q = tid; q < 2 * L::NL; q += nt) lg[q] = plan[P.lg + q];
+    for (int q = tid; q < L::OUT * L::IN * L::NFL; q += nt) kw[q] = plan[P.kw + q];
+    for (int q = tid; q < L::NL; q += nt) {
+      pa[q] = kl.logistic_a[q];
+      pb[q] = kl.logistic_b[q];
+    }
+  }
+};
+
+template <class L>
+struct BFeat {  // per-wave LDS features of one layer's input
+  float x[L::IN], pv[L::IN], silu[L::IN], dsilu[L::IN], u[L::IN], up[L::IN];
+  int m[L::IN];
+  float bd[L::IN * L::NS];
+  float sg[L::NL > 0 ? L::NL : 1];
+  float gout[L::OUT];
+  float gin[L::IN];
+};
+
+template <class L>
+struct BReg {  // per-lane register slice of one layer: gradient sums + the Ferro parameters
+  float A[L::RF1], C[L::RF1], Ev[L::RF1];
+  float G;
+  float base[L::RE], spl[L::RE][L::NS];
+  float lw[L::RL1][L::OUT], la[L::RL1], lb[L::RL1];
+
+  __device__ void zero() {
+#pragma unroll
+    for (int r = 0; r < L::RF1; ++r) A[r] = C[r] = Ev[r] = 0.f;
+    G = 0.f;
+#pragma unroll
+    for (int r = 0; r < L::RE; ++r) {
+      base[r] = 0.f;
+#pragma unroll
+      for (int c = 0; c < L::NS; ++c) spl[r][c] = 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < L::RL1; ++r) {
+      la[r] = lb[r] = 0.f;
+#pragma unroll
+      for (int o = 0; o < L::OUT; ++o) lw[r][o] = 0.f;
+    }
+  }
+
+  __device__ void store(float* __restrict__ part, int lane) const {
+    constexpr AccLayout AL = L::AL;
+#pragma unroll
+    for (int r = 0; r < L::RF; ++r) {
+      const int e = lane + 64 * r;
+      if (e < L::E) {
+        part[AL.oA + e] = A[r];
+        part[AL.oC + e] = C[r];
+        part[AL.oE + e] = Ev[r];
+      }
+    }
+    if (L::FERRO && lane < L::OUT) part[AL.oG + lane] = G;
+#pragma unroll
+    for (int r = 0; r < L::RE; ++r) {
+      const int q = lane + 64 * r;
+      if (q < L::NE) {
+        part[AL.oBase + q] = base[r];
+#pragma unroll
+        for (int c = 0; c < L::NS; ++c) part[AL.oSpl + q * L::NS + c] = spl[r][c];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < L::RL; ++r) {
+      const int q = lane + 64 * r;
+      if (q < L::NL) {
+#pragma unroll
+        for (int o = 0; o < L::OUT; ++o) part[AL.oLw + o * L::NL + q] = lw[r][o];
+        part[AL.oLa + q] = la[r];
+        part[AL.oLb + q] = lb[r];
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ float sigm_l2(float zl) { return rcp(1.0f + ex2(zl)); }  // 1/(1+2^zl)
+
+// the lanes of one wave exchange data through that wave's private LDS region only: a wave-level
+// barrier (LDS ops complete + no reordering) replaces the workgroup barrier
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// per-input features of input i of a layer (one lane)
+template <class L>
+__device__ __forceinline__ void feat_input(BFeat<L>& F, const BTab<L>& Tb, int i, float gsl2e, int z) {
+  const float x = F.x[i];
+  const float sx = sigm_l2(-x * FETODE_LOG2E);
+  F.silu[i] = x * sx;
+  F.dsilu[i] = sx * ffma(x, 1.0f - sx, 1.0f);
+  const float* g = &Tb.knots[i * L::NG + z];
+  const float* rk = &Tb.rk[i * kSO * (L::NG - 1) + z];
+  int m = -1;
+#pragma unroll
+  for (int j = 0; j < L::NG; ++j) m += (x >= g[j]) ? 1 : 0;
+  float u;
+  if (!__builtin_isfinite(x)) {
+    m = L::NI;
+    u = __builtin_nanf("");
+  } else if (m < 0 || m >= L::NI) {
+    m = L::NI;
+    u = 0.f;
+  } else {
+    u = (x - g[m]) * rk[m];  // level-1 reciprocal = 1/(g[m+1]-g[m])
+  }
+  F.m[i] = m;
+  F.u[i] = u;
+  float* bd = &F.bd[i * L::NS];
+  bspline_local<kSO>(x, L::NG, g, rk, [&](int c, float v) { bd[c] = v; });
+  if constexpr (L::FERRO) F.up[i] = sigm_l2(-gsl2e * (x - F.pv[i]));
+}
+
+// the VJP jobs of one layer for one evaluation: gradient sums into R, d out/d x contributions
+// into cb[i * NTM + t]
+template <class L>
+__device__ __forceinline__ void layer_jobs(const BFeat<L>& F, const BTab<L>& Tb, BReg<L>& R, float* __restrict__ cb,
+                                           float gsl2e, float wc, float gs, int lane, int z) {
+  if constexpr (L::FERRO) {
+#pragma unroll
+    for (int r = 0; r < L::RF; ++r) {
+      const int e = lane + 64 * r;
+      if (e < L::E) {
+        const int i = e / (L::OUT * L::K), ok_ = e % (L::OUT * L::K);
+        const int o = ok_ / L::K;
+        const float x = F.x[i], up = F.up[i], go = F.gout[o];
+        const float4 pe = Tb.fe[e + z];
+        const float kk = pe.x, Ec = pe.y;
+        const float cn = sigm_l2(gsl2e * (x + Ec));           // sigmoid(gs(-x - Ec))
+        const float omu = 1.0f - up;
+        const float mm = ffma(wc, omu * cn, 1.0f);            // branch_mom with branch_sign = 1
+        const float sh = ffma(Ec, mm, x);                     // shifted_x
+        const float th = ffma(-2.0f, sigm_l2(2.0f * FETODE_LOG2E * kk * sh), 1.0f);  // tanh(k sh)
+        const float q = go * ffma(-th, th, 1.0f);
+        R.A[r] = ffma(go, th, R.A[r]);
+        R.C[r] = ffma(q, sh, R.C[r]);
+        const float dcn = gs * cn * (1.0f - cn), du = gs * up * omu;
+        const float dmdEc = -wc * omu * dcn;
+        R.Ev[r] = ffma(q, ffma(Ec, dmdEc, mm), R.Ev[r]);
+        const float dmdx = -wc * ffma(du, cn, omu * dcn);
+        cb[i * L::NTM + ok_] = q * pe.z * ffma(Ec, dmdx, 1.0f);
+      }
+    }
+    if (lane < L::OUT) R.G += F.gout[lane];
+  }
+#pragma unroll
+  for (int r = 0; r < L::RE; ++r) {
+    const int q = lane + 64 * r;
+    if (q < L::NE) {
+      const int o = q / L::IN, i = q % L::IN;
+      const float go = F.gout[o];
+      R.base[r] = ffma(go, F.silu[i], R.base[r]);
+#pragma unroll
+      for (int c = 0; c < L::NS; ++c) R.spl[r][c] = ffma(go, F.bd[i * L::NS + c], R.spl[r][c]);
+      const int m = F.m[i];
+      const float u = F.u[i];
+      float dsdx;
+      if (m < L::NI) {
+        const float4 cf = Tb.sp[q * (L::NI + 1) + m + z];  // (o, i, interval), q = o*IN + i
+        dsdx = ffma(u, ffma(3.0f * u, cf.w, 2.0f * cf.z), cf.y) * Tb.rk[i * kSO * (L::NG - 1) + m + z];
+      } else {
+        dsdx = u * 0.0f;  // 0 outside the grid, NaN for non-finite inputs (the reference's NaN bases)
+      }
+      const float wb = Tb.kw[o * (L::IN * L::NFL) + i * L::NFL + z];
+      cb[i * L::NTM + L::OUT * L::K + o] = go * ffma(wb, F.dsilu[i], dsdx);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < L::RL; ++r) {
+    const int q = lane + 64 * r;
+    if (q < L::NL) {
+      const int i = q / L::NB, j = q % L::NB;
+      const float s = F.sg[q], ds = s * (1.0f - s), x = F.x[i];
+      float S = 0.f;
+#pragma unroll
+      for (int o = 0; o < L::OUT; ++o) {
+        const float go = F.gout[o];
+        S = ffma(go, Tb.kw[o * (L::IN * L::NFL) + i * L::NFL + 1 + j + z], S);
+        R.lw[r][o] = ffma(go, s, R.lw[r][o]);
+      }
+      const float T = S * ds;  // kw holds 2 * scaled logistic weight: d(2 sigmoid) folded in
+      const float pa = Tb.pa[q + z];
+      R.la[r] = ffma(T, x - Tb.pb[q + z], R.la[r]);
+      R.lb[r] = ffma(-T, pa, R.lb[r]);
+      cb[i * L::NTM + L::OUT * L::K + L::OUT + j] = T * pa;
+    }
+  }
+}
+
+// gin[i] = sum_t cb[i * NTM + t], fixed order: LPI lanes per input, strided partial sums, xor tree
+template <class L>
+__device__ __forceinline__ void reduce_gin(const float* __restrict__ cb, float* gin, int lane) {
+  constexpr int LPI = L::LPI;
+  const int i = lane / LPI, sub = lane % LPI;
+  float s = 0.f;
+  if (i < L::IN) {
+#pragma unroll
+    for (int t = sub; t < L::NTM; t += LPI) s += cb[i * L::NTM + t];
+  }
+#pragma unroll
+  for (int k = LPI / 2; k >= 1; k >>= 1) s += __shfl_xor(s, k);
+  if (i < L::IN && sub == 0) gin[i] = s;
+}
+
+struct BwdArgs {
+  const float* plan;
+  LayerPlan P0, P1;
+  fetode_kanlinear_t k0, k1;
+  fetode_ferro_t f0, f1;
+  int32_t method;
+  int64_t B;
+  const float* step_coef;
+  int32_t n_steps;
+  const int32_t* out_step;
+  const int32_t* out_mode;
+  const float* out_slope;
+  int32_t T;
+  const float* gsol;    // (T, B, D)
+  const float* tape;    // (n_evals, B, D + H)
+  const float* state0;  // hysteresis state before the solve (include/fetode.h layout)
+  uint32_t init_mask;
+  float* gy0;           // (B, D) or null
+  float* part;          // (gridDim.x * kTPB, nacc)
+  int32_t nacc;
+};
+
+// stage-combine coefficients of one step in the forward's fp32 arithmetic (odeint.py
+// _combine_coefs): y1 = y + sum_j bc[j] k_j,  X_st = y + sum_{j<st} ac[st][j] k_j
+__device__ __forceinline__ void step_coefs(int method, float dt, float hh, float h6, float bc[4], float ac[4][3]) {
+  const float third = 1.0f / 3.0f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    bc[i] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) ac[i][j] = 0.f;
+  }
+  if (method == FETODE_RK4) {  // rk_common.rk4_alt_step_func (3/8 rule)
+    bc[0] = dt * 0.125f;
+    bc[1] = 3.0f * dt * 0.125f;
+    bc[2] = 3.0f * dt * 0.125f;
+    bc[3] = dt * 0.125f;
+    ac[1][0] = dt * third;
+    ac[2][0] = -dt * third;
+    ac[2][1] = dt;
+    ac[3][0] = dt;
+    ac[3][1] = -dt;
+    ac[3][2] = dt;
+  } else if (method == FETODE_RK4_CLASSIC) {  // train_kan_fet_ett.py:72-75
+    bc[0] = h6;
+    bc[1] = 2.0f * h6;
+    bc[2] = 2.0f * h6;
+    bc[3] = h6;
+    ac[1][0] = hh;
+    ac[2][1] = hh;
+    ac[3][2] = dt;
+  } else if (method == FETODE_MIDPOINT) {
+    bc[1] = dt;
+    ac[1][0] = hh;
+  } else {
+    bc[0] = dt;
+  }
+}
+
+constexpr int kTPB = 4;  // trajectories (waves) per workgroup, sharing one copy of the tables
+
+template <int D, int H, int K, int NB, int NG, bool FERRO>
+__global__ __launch_bounds__(64 * kTPB) void fixed_bwd_kernel(BwdArgs a) {
+  using L0 = BL<D, H, K, NB, NG, FERRO>;
+  using L1 = BL<H, D, K, NB, NG, FERRO>;
+  constexpr int W = D + H;
+  constexpr int CB = L0::IN * L0::NTM > L1::IN * L1::NTM ? L0::IN * L0::NTM : L1::IN * L1::NTM;
+  __shared__ BTab<L0> T0;
+  __shared__ BTab<L1> T1;
+  __shared__ BFeat<L0> sF0[kTPB];
+  __shared__ BFeat<L1> sF1[kTPB];
+  __shared__ float s_cb[kTPB][CB];
+  __shared__ float s_ak[kTPB][4][D], s_ay[kTPB][D], s_ac[kTPB][4][3];
+
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  T0.stage(a.k0, a.f0, a.plan, a.P0, threadIdx.x, 64 * kTPB);
+  T1.stage(a.k1, a.f1, a.plan, a.P1, threadIdx.x, 64 * kTPB);
+  BReg<L0> R0;
+  BReg<L1> R1;
+  R0.zero();
+  R1.zero();
+  __syncthreads();  // tables staged; from here on every wave syncs only with itself
+
+  BFeat<L0>& F0 = sF0[wid];
+  BFeat<L1>& F1 = sF1[wid];
+  float* cb = s_cb[wid];
+  float(&ak)[4][D] = s_ak[wid];
+  float(&ay)[D] = s_ay[wid];
+  float(&acs)[4][3] = s_ac[wid];
+  const float gs0 = (float)a.f0.gate_slope, gs1 = (float)a.f1.gate_slope;
+  const float gl0 = a.P0.gsl2e, gl1 = a.P1.gsl2e, wc0 = a.P0.wc, wc1 = a.P1.wc;
+  const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4 : a.method == FETODE_MIDPOINT ? 2 : 1;
+  const int64_t tstride = a.B * W;
+  const int n_ev = a.n_steps * ns;
+
+  for (int64_t b = (int64_t)blockIdx.x * kTPB + wid; b < a.B; b += (int64_t)gridDim.x * kTPB) {
+    // the hysteresis input of evaluation ev is the layer input of ev - 1 (ferro_class.py:409)
+    auto tape_at = [&](int ev) -> float {
+      if (lane >= W) return 0.f;
+      if (ev >= 0) return a.tape[(int64_t)ev * tstride + b * W + lane];
+      const float v = a.tape[b * W + lane];  // before evaluation 0: the stored state / reinit rule
+      if (lane < D) return (a.init_mask & 1u) ? v : (FERRO ? a.state0[b * D + lane] : 0.f);
+      return (a.init_mask & 2u) ? v : (FERRO ? a.state0[a.B * D + b * H + (lane - D)] : 0.f);
+    };
+    float cur = tape_at(n_ev - 1), prv = tape_at(n_ev - 2);
+    float ay1 = 0.f;  // adjoint of y at the end of the current step (lanes d < D)
+    int jj = a.T - 1;
+    for (int s = a.n_steps - 1; s >= 0; --s) {
+      float bc[4], ac[4][3];
+      step_coefs(a.method, a.step_coef[4 * s], a.step_coef[4 * s + 1], a.step_coef[4 * s + 2], bc, ac);
+      // outputs produced in this step (FixedGridODESolver: y at step start, end, or interpolated)
+      float ay0x = 0.f;
+      for (; jj >= 1 && a.out_step[jj] == s; --jj) {
+        if (lane < D) {
+          const float g = a.gsol[((int64_t)jj * a.B + b) * D + lane];
+          const int mode = a.out_mode[jj];
+          if (mode == 0) {
+            ay0x += g;
+          } else if (mode == 1) {
+            ay1 += g;
+          } else {
+            const float sl = a.out_slope[jj];
+            ay1 = ffma(sl, g, ay1);
+            ay0x = ffma(1.0f - sl, g, ay0x);
+          }
+        }
+      }
+      if (lane < D) {
+        for (int j = 0; j < ns; ++j) ak[j][lane] = bc[j] * ay1;
+        ay[lane] = ay1 + ay0x;
+      }
+      if (lane == 0) {  // through LDS: the stage index below is a runtime value
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) acs[i][j] = ac[i][j];
+      }
+      for (int st = ns - 1; st >= 0; --st) {
+        const int ev = s * ns + st;
+        // table reads are re-issued every evaluation (an opaque zero offset stops the compiler
+        // from hoisting ~100 loop-invariant LDS values into VGPRs, which halves occupancy)
+        int z = 0;
+        asm volatile("" : "+s"(z));
+        const float nxt = tape_at(ev - 2);  // prefetch: consumed by the next evaluation
+        if (lane < D) {
+          F0.x[lane] = cur;
+          F0.pv[lane] = prv;
+          F1.gout[lane] = ak[st][lane];
+        } else if (lane < W) {
+          F1.x[lane - D] = cur;
+          F1.pv[lane - D] = prv;
+        }
+        wsync();
+        // features of both layers' inputs
+        if (lane < D) feat_input<L0>(F0, T0, lane, gl0, z);
+        else if (lane < W) feat_input<L1>(F1, T1, lane - D, gl1, z);
+        for (int q = lane; q < L0::NL + L1::NL; q += 64) {
+          if (q < L0::NL) {
+            F0.sg[q] = sigm_l2(ffma(T0.lg[2 * q + z], F0.x[q / NB], T0.lg[2 * q + 1 + z]));
+          } else {
+            const int qq = q - L0::NL;
+            F1.sg[qq] = sigm_l2(ffma(T1.lg[2 * qq + z], F1.x[qq / NB], T1.lg[2 * qq + 1 + z]));
+          }
+        }
+        wsync();
+        layer_jobs<L1>(F1, T1, R1, cb, gl1, wc1, gs1, lane, z);
+        wsync();
+        reduce_gin<L1>(cb, F0.gout, lane);  // d loss / d h = layer-0 output adjoint
+        wsync();
+        layer_jobs<L0>(F0, T0, R0, cb, gl0, wc0, gs0, lane, z);
+        wsync();
+        reduce_gin<L0>(cb, F0.gin, lane);
+        wsync();
+        if (lane < D) {
+          const float ax = F0.gin[lane];
+          ay[lane] += ax;
+          for (int j = 0; j < st; ++j) ak[j][lane] = ffma(acs[st][j], ax, ak[j][lane]);
+        }
+        wsync();
+        cur = prv;
+        prv = nxt;
+      }
+      ay1 = lane < D ? ay[lane] : 0.f;
+    }
+    if (lane < D && a.gy0) a.gy0[b * D + lane] = ay1 + a.gsol[b * D + lane];  // solution[0] = y0
+    wsync();
+  }
+  float* part = a.part + ((int64_t)blockIdx.x * kTPB + wid) * a.nacc;
+  R0.store(part, lane);
+  R1.store(part + L0::AL.n, lane);
+}
+
+// partial rows -> chunk sums (fp64), fixed order
+__global__ void part_reduce_kernel(const float* __restrict__ part, int64_t nrows, int nacc, int64_t per,
+                                   double* __restrict__ out) {
+  const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= nacc) return;
+  const int64_t r0 = (int64_t)blockIdx.y * per, r1 = r0 + per < nrows ? r0 + per : nrows;
+  double s = 0.0;
+  for (int64_t r = r0; r < r1; ++r) s += part[r * nacc + slot];
+  out[(int64_t)blockIdx.y * nacc + slot] = s;
+}
+
+__global__ void chunk_sum_kernel(const double* __restrict__ ch, int nch, int nacc, double* __restrict__ S) {
+  const int slot = blockIdx.x * blockDim.x + threadIdx.x;
+  if (slot >= nacc) return;
+  double s = 0.0;
+  for (int c = 0; c < nch; ++c) s += ch[(int64_t)c * nacc + slot];
+  S[slot] = s;
+}
+
+struct ApplyLayer {
+  fetode_kanlinear_t kl;
+  fetode_ferro_t fl;
+  int has_ferro;
+  AccLayout AL;
+  fetode_kanlinear_grad_t kg;
+  fetode_ferro_grad_t fg;
+};
+
+__device__ __forceinline__ void put(float* p, int64_t i, double v) {
+  if (p) p[i] = (float)v;
+}
+
+// gradient sums of one layer -> parameter gradients (reference parameter layouts)
+__global__ void grad_apply_kernel(const double* __restrict__ S, ApplyLayer L) {
+  const AccLayout& A = L.AL;
+  const int in = L.kl.in_features, out = L.kl.out_features, NS = A.NS;
+  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < A.E) {  // Ferro element e = (i, o, k)
+    const int K = L.fl.num_basis, o = (t / K) % out;
+    const double co = L.fl.coef[t], Ps = L.fl.Ps[t], kk = L.fl.k[t], bi = L.fl.bias[t];
+    const double sA = S[A.oA + t], sC = S[A.oC + t], sE = S[A.oE + t], sG = S[A.oG + o];
+    put(L.fg.k, t, co * Ps * sC);
+    put(L.fg.Ec, t, co * Ps * kk * sE);
+    put(L.fg.Ps, t, co * sA);
+    put(L.fg.bias, t, co * sG);
+    put(L.fg.coef, t, Ps * sA + bi * sG);
+    return;
+  }
+  t -= A.E;
+  if (t < A.NE) {  // KAN edge (o, i)
+    put(L.kg.base_weight, t, S[A.oBase + t]);
+    const double ss = L.kl.spline_scaler ? (double)L.kl.spline_scaler[t] : 1.0;
+    double gsc = 0.0;
+    for (int c = 0; c < NS; ++c) {
+      const double d = S[A.oSpl + t * NS + c];
+      put(L.kg.spline_weight, (int64_t)t * NS + c, d * ss);
+      gsc += d * (double)L.kl.spline_weight[(int64_t)t * NS + c];
+    }
+    if (L.kl.spline_scaler) put(L.kg.spline_scaler, t, gsc);
+    return;
+  }
+  t -= A.NE;
+  if (A.NL == 0) return;
+  const double sl = L.kl.scale_logistic;
+  if (t < out * A.NL) {  // logistic weight (o, i*NB + j); the basis is 2 sigmoid
+    const int o = t / A.NL;
+    const double ls = L.kl.logistic_scaler ? (double)L.kl.logistic_scaler[o] : 1.0;
+    put(L.kg.logistic_weight, t, 2.0 * S[A.oLw + t] * sl * ls);
+    return;
+  }
+  t -= out * A.NL;
+  if (t < A.NL) {
+    put(L.kg.logistic_a, t, S[A.oLa + t]);
+    put(L.kg.logistic_b, t, S[A.oLb + t]);
+    return;
+  }
+  t -= A.NL;
+  if (t < out && L.kl.logistic_scaler) {
+    double g = 0.0;
+    for (int q = 0; q < A.NL; ++q)
+      g += 2.0 * S[A.oLw + t * A.NL + q] * (double)L.kl.logistic_weight[(int64_t)t * A.NL + q] * sl;
+    put(L.kg.logistic_scaler, t, g);
+  }
+  (void)in;
+}
+
+typedef void (*bwd_fn)(BwdArgs);
+struct BwdEntry {
+  int D, H, K, NB, NG;
+  bool ferro;
+  bwd_fn fn;
+};
+const BwdEntry kBwd[] = {
+    {2, 10, 10, 10, 12, true, fixed_bwd_kernel<2, 10, 10, 10, 12, true>},   // LV KAN-FET [2,10,2]
+    {2, 10, 0, 10, 12, false, fixed_bwd_kernel<2, 10, 1, 10, 12, false>},   // LV KAN [2,10,2]
+};
+
+const BwdEntry* find_bwd(const fetode_field_t* f) {
+  if (f->n_layers != 2) return nullptr;
+  const fetode_kanlinear_t &k0 = f->kan[0], &k1 = f->kan[1];
+  if (k0.spline_order != kSO || k1.spline_order != kSO || k0.grid_size != k1.grid_size ||
+      k0.num_logistic != k1.num_logistic || k0.in_features != k1.out_features)
+    return nullptr;
+  const int NG = k0.grid_size + 2 * kSO + 1;
+  for (const BwdEntry& e : kBwd) {
+    if (e.D != k0.in_features || e.H != k0.out_features || e.NB != k0.num_logistic || e.NG != NG) continue;
+    if (e.ferro != (f->ferro != nullptr)) continue;
+    if (f->ferro) {
+      if (f->ferro[0].num_basis != e.K || f->ferro[1].num_basis != e.K) continue;
+      if (f->ferro[0].branch_sign || f->ferro[1].branch_sign) continue;
+    }
+    return &e;
+  }
+  return nullptr;
+}
+
+constexpr int64_t kMaxBwdRows = 8192;  // partial rows (one per wave)
+constexpr int kChunks = 64;
+// one partial row per wave: the grid's waves, a multiple of kTPB
+int64_t bwd_rows(int64_t B) {
+  const int64_t w = B < kMaxBwdRows ? B : kMaxBwdRows;
+  return (w + kTPB - 1) / kTPB * kTPB;
+}
+
+void layouts(const fetode_field_t* f, AccLayout* L0, AccLayout* L1) {
+  const int NS = f->kan[0].grid_size + kSO;
+  const int K = f->ferro ? f->ferro[0].num_basis : 0;
+  const bool fe = f->ferro != nullptr;
+  *L0 = acc_layout(f->kan[0].in_features, f->kan[0].out_features, K, f->kan[0].num_logistic, NS, fe);
+  *L1 = acc_layout(f->kan[1].in_features, f->kan[1].out_features, K, f->kan[1].num_logistic, NS, fe);
+}
+
+}  // namespace
+
+extern "C" {
+
+int fetode_fused_backward_supported(const fetode_field_t* f) {
+  if (validate_field(f) != FETODE_OK) return 0;
+  return find_bwd(f) != nullptr;
+}
+
+int64_t fetode_integrate_fixed_backward_workspace(const fetode_field_t* f, int64_t B) {
+  if (validate_field(f) != FETODE_OK || !find_bwd(f) || B <= 0) return -1;
+  AccLayout L0, L1;
+  layouts(f, &L0, &L1);
+  const int64_t nacc = L0.n + L1.n;
+  const int64_t nrow = bwd_rows(B);
+  const int64_t nch = nrow < kChunks ? nrow : kChunks;
+  return (int64_t)sizeof(double) * nacc * (nch + 1) + (int64_t)sizeof(float) * nrow * nacc;
+}
+
+int fetode_integrate_fixed_backward(const fetode_field_t* f, const void* plan, int32_t method, int64_t B,
+                                    const float* step_coef, int32_t n_steps, const int32_t* out_step,
+                                    const int32_t* out_mode, const float* out_slope, int32_t T,
+                                    const float* grad_solution, const float* tape, const float* state0,
+                                    uint32_t init_mask, float* grad_y0, const fetode_kanlinear_grad_t* kan_grads,
+                                    const fetode_ferro_grad_t* ferro_grads, void* workspace, void* stream) {
+  int rc = validate_field(f);
+  if (rc) return rc;
+  const BwdEntry* e = find_bwd(f);
+  if (!e) return set_err(FETODE_EUNSUPPORTED, "no fused backward kernel for this field shape");
+  if (method < FETODE_EULER || method > FETODE_RK4_CLASSIC) return set_err(FETODE_EINVAL, "unknown method %d", method);
+  if (B <= 0 || T <= 0) return FETODE_OK;
+  if (!plan || !grad_solution || !workspace || (n_steps > 0 && (!tape || !step_coef || !out_step || !out_mode ||
+                                                                 !out_slope)) ||
+      (f->ferro && !state0 && (init_mask & 3u) != 3u))
+    return set_err(FETODE_EINVAL, "null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  AccLayout AL0, AL1;
+  layouts(f, &AL0, &AL1);
+  const int nacc = AL0.n + AL1.n;
+  const int64_t nrow = bwd_rows(B);
+  const int64_t nch = nrow < kChunks ? nrow : kChunks;
+  double* S = (double*)workspace;
+  double* chunks = S + nacc;
+  float* part = (float*)(chunks + nch * nacc);
+
+  BwdArgs a;
+  memset(&a, 0, sizeof(a));
+  a.plan = (const float*)plan;
+  layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
+  layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
+  a.k0 = f->kan[0];
+  a.k1 = f->kan[1];
+  if (f->ferro) {
+    a.f0 = f->ferro[0];
+    a.f1 = f->ferro[1];
+  }
+  a.method = method;
+  a.B = B;
+  a.step_coef = step_coef;
+  a.n_steps = n_steps;
+  a.out_step = out_step;
+  a.out_mode = out_mode;
+  a.out_slope = out_slope;
+  a.T = T;
+  a.gsol = grad_solution;
+  a.tape = tape;
+  a.state0 = state0;
+  a.init_mask = f->ferro ? init_mask : 3u;
+  a.gy0 = grad_y0;
+  a.part = part;
+  a.nacc = nacc;
+  hipLaunchKernelGGL(e->fn, dim3((unsigned)(nrow / kTPB)), dim3(64 * kTPB), 0, s, a);
+  LAUNCH_CHECK();
+  const int64_t per = (nrow + nch - 1) / nch;
+  hipLaunchKernelGGL(part_reduce_kernel, dim3(nblk(nacc, 64), (unsigned)nch), dim3(64), 0, s, part, nrow, nacc, per,
+                     chunks);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(chunk_sum_kernel, dim3(nblk(nacc, 64)), dim3(64), 0, s, chunks, (int)nch, nacc, S);
+  LAUNCH_CHECK();
+  if (!kan_grads && !ferro_grads) return FETODE_OK;
+  for (int l = 0; l < 2; ++l) {
+    ApplyLayer L;
+    memset(&L, 0, sizeof(L));
+    L.kl = f->kan[l];
+    if (f->ferro) L.fl = f->ferro[l];
+    L.has_ferro = f->ferro != nullptr;
+    L.AL = l == 0 ? AL0 : AL1;
+    if (kan_grads) L.kg = kan_grads[l];
+    if (ferro_grads && f->ferro) L.fg = ferro_grads[l];
+    const int n = L.AL.E + L.AL.NE + L.kl.out_features * L.AL.NL + L.AL.NL + L.kl.out_features;
+    hipLaunchKernelGGL(grad_apply_kernel, dim3(nblk(n, 64)), dim3(64), 0, s, S + (l == 0 ? 0 : AL0.n), L);
+    LAUNCH_CHECK();
+  }
+  return FETODE_OK;
+}
+
+}  // extern "C"

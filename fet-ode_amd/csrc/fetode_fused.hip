@@ -258,7 +258,7 @@ struct FusedArgs {
   float* solution;
   float* state;
   uint32_t init_mask;
-  float* ckpt;
+  float* tape;            // (n_evals, B, D+H) layer inputs of every evaluation (training), or null
   int32_t single_eval;  // 1: eval_out = field(y0) once (fetode_field_forward)
   float* eval_out;
 };
@@ -308,7 +308,6 @@ __global__ __launch_bounds__(NT) void fused_integrate_kernel(FusedArgs a) {
   R0.load(a.plan, a.P0, lane, fact);
   R1.load(a.plan, a.P1, lane, fact);
 
-  constexpr int SW = FERRO ? IN0 + H : 0;  // state width
   if (FERRO) {
     for (int i = lane; i < IN0; i += LPT) T.L0.prev[i] = valid ? a.state[b * IN0 + i] : 0.f;
     for (int i = lane; i < H; i += LPT) T.L1.prev[i] = valid ? a.state[a.B * IN0 + b * H + i] : 0.f;
@@ -358,15 +357,6 @@ __global__ __launch_bounds__(NT) void fused_integrate_kernel(FusedArgs a) {
     int jj = 1;
     for (int s = 0; s < a.n_steps; ++s) {
       const float dt = a.step_coef[4 * s + 0], hh = a.step_coef[4 * s + 1], h6 = a.step_coef[4 * s + 2];
-      if (a.ckpt && valid) {  // prev[i] is written and read by the same lane (i % LPT)
-        const int64_t W = D + SW;
-        float* ck = a.ckpt + ((int64_t)s * a.B + b) * W;
-        if (own) ck[d] = y;
-        if (FERRO) {
-          for (int i = lane; i < IN0; i += LPT) ck[D + i] = T.L0.prev[i];
-          for (int i = lane; i < H; i += LPT) ck[D + IN0 + i] = T.L1.prev[i];
-        }
-      }
       float k1 = 0.f, k2 = 0.f, k3 = 0.f, k4 = 0.f;
       for (int st = 0; st < ns; ++st) {
         float xin = y;
@@ -615,7 +605,6 @@ __global__ __launch_bounds__(64) void fused3_kernel(FusedArgs a) {
   }
   const bool hmisc = act0 && cc0 == 0;
 
-  constexpr int SW = FERRO ? D + H : 0;
   float prev0 = 0.f, prev1 = 0.f;  // prev_x of input `row` (xmisc lane) / of input o0 (hmisc lane)
   if (FERRO && valid) {
     if (xmisc) prev0 = a.state[b * D + row];
@@ -676,12 +665,6 @@ __global__ __launch_bounds__(64) void fused3_kernel(FusedArgs a) {
     int jj = 1;
     for (int s = 0; s < a.n_steps; ++s) {
       const float dt = a.step_coef[4 * s + 0], hh = a.step_coef[4 * s + 1], h6 = a.step_coef[4 * s + 2];
-      if (a.ckpt && valid) {
-        float* ck = a.ckpt + ((int64_t)s * a.B + b) * (D + SW);
-        if (c1 == 0) ck[row] = y;
-        if (FERRO && xmisc) ck[D + row] = prev0;
-        if (FERRO && hmisc) ck[D + D + o0] = prev1;
-      }
       float k1 = 0.f, k2 = 0.f, k3 = 0.f, k4 = 0.f;
       for (int st = 0; st < ns; ++st) {
         float xin = y;
@@ -1012,10 +995,15 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
   const bool spl0 = act0 && cc0 < D, spl1 = c1 < H;  // lanes owning a spline edge (input si)
   const int si0 = spl0 ? cc0 : 0, si1 = spl1 ? c1 : 0;
 
+  // training tape: the two layer inputs of evaluation `ev` at tape[(ev B + b)(D + H) + c]
+  const bool taping = a.tape != nullptr;  // uniform: the inference path skips every tape op
+  float* tape_b = taping ? a.tape + (valid ? b : 0) * (D + H) : nullptr;
+  const int64_t tape_stride = a.B * (D + H);
   auto eval_body = [&](float xin, auto fact_tag) __attribute__((always_inline)) -> float {
     constexpr bool F_ = decltype(fact_tag)::value;
     STAMP(6);
     FETODE_MARK("X_FEAT");
+    if (taping && valid && c1 == 0) tape_b[row] = xin;
     {
       // (1) layer-0 features of input `row`: one sigmoid-of-affine job per lane
       const float pv = x_gate ? (re0 ? xin : prev0) : 0.f;
@@ -1093,8 +1081,10 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
       if (act0 && cc0 == 0) {
         L1.G[o0].x = h;
         L1.M[o0] = mfix;
+        if (taping && valid) tape_b[D + o0] = h;
       }
     }
+    if (taping) tape_b += tape_stride;
     STAMP(3);
     __syncthreads();
     STAMP(4);
@@ -1107,7 +1097,6 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
     FETODE_MARK("END");
     return kr;
   };
-  constexpr int SW = FERRO ? D + H : 0;
   // the step / output schedule is staged through LDS in chunks: per-step global loads in the
   // loop would wait (vmcnt) behind the solution stores of the previous step
   constexpr int SCH = 32;
@@ -1132,14 +1121,7 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
     }
     __syncthreads();
   };
-  auto ckpt_write = [&](int s) __attribute__((always_inline)) {
-    if (a.ckpt && valid) {
-      float* ck = a.ckpt + ((int64_t)s * a.B + b) * (D + SW);
-      if (c1 == 0) ck[row] = y;
-      if (FERRO && x_gate) ck[D + row] = prev0;
-      if (FERRO && act0 && h_gate) ck[D + D + o0] = prev1;
-    }
-  };
+
   auto out_write = [&](int j, float v) __attribute__((always_inline)) {
 #ifndef FETODE_EXPERIMENT_NO_OUT
     if (valid && c1 == 0) a.solution[((int64_t)j * a.B + b) * D + row] = v;
@@ -1170,7 +1152,6 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
         const int os0 = s_ostep[jr], os1 = s_ostep[jr + 1], om0 = s_omode[jr];
         const float osl0 = s_oslope[jr];
         STAMP(7);
-        ckpt_write(s);
         const float k1 = eval_body(y, fact_tag);
         const float k2 = eval_body(y + (dt * k1) * third, fact_tag);
         const float k3 = eval_body(y + dt * (k2 - k1 * third), fact_tag);
@@ -1223,7 +1204,6 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
           load_steps(s);
         }
         const float dt = s_dt[s - sb], hh = s_hh[s - sb], h6 = s_h6[s - sb];
-        ckpt_write(s);
         float k1 = 0.f, k2 = 0.f, k3 = 0.f, k4 = 0.f;
         for (int st = 0; st < ns; ++st) {
           float xin = y;
@@ -1327,7 +1307,6 @@ __global__ __launch_bounds__(64 * NW, FETODE_V5_WAVES) void fused5_kernel(FusedA
   constexpr int RH = (NJH + 3) / 4;               // rounds over the 4 lanes of a quad
   constexpr int KT = (NG + 3) / 4;                // knots per quad lane: q, q+4, q+8, ...
   constexpr int SPT0 = H * D * (NI + 1) * 4, SPT1 = D * H * (NI + 1) * 4;
-  constexpr int SW = FERRO ? D + H : 0;
 
   __shared__ __attribute__((aligned(16))) float s_sp0[SPT0];
   __shared__ __attribute__((aligned(16))) float s_sp1[SPT1];
@@ -1602,14 +1581,7 @@ __global__ __launch_bounds__(64 * NW, FETODE_V5_WAVES) void fused5_kernel(FusedA
     }
     __syncthreads();
   };
-  auto ckpt_write = [&](int s) __attribute__((always_inline)) {
-    if (a.ckpt && valid) {
-      float* ck = a.ckpt + ((int64_t)s * a.B + b) * (D + SW);
-      if ((l & 31) == 0) ck[dx] = y;
-      if (own0) ck[D + dx] = prev0;
-      if (own1) ck[D + D + o0] = prev1;
-    }
-  };
+
   auto out_write = [&](int j, float v) __attribute__((always_inline)) {
     if (yw) a.solution[((int64_t)j * a.B + b) * D + dx] = v;
   };
@@ -1635,7 +1607,6 @@ __global__ __launch_bounds__(64 * NW, FETODE_V5_WAVES) void fused5_kernel(FusedA
         const float dt = s_dt[sr];
         const int os0 = s_ostep[jr], os1 = s_ostep[jr + 1], om0 = s_omode[jr];
         const float osl0 = s_oslope[jr];
-        ckpt_write(s);
         const float k1 = eval_body(y, fact_tag);
         const float k2 = eval_body(y + (dt * k1) * third, fact_tag);
         const float k3 = eval_body(y + dt * (k2 - k1 * third), fact_tag);
@@ -1686,7 +1657,6 @@ __global__ __launch_bounds__(64 * NW, FETODE_V5_WAVES) void fused5_kernel(FusedA
           load_steps(s);
         }
         const float dt = s_dt[s - sb], hh = s_hh[s - sb], h6 = s_h6[s - sb];
-        ckpt_write(s);
         float k1 = 0.f, k2 = 0.f, k3 = 0.f, k4 = 0.f;
         for (int st = 0; st < ns; ++st) {
           float xin = y;
@@ -1816,6 +1786,7 @@ int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
   layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
   layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
   // trajectories per workgroup: v3/v4 two per wave (one wave), v5 one per wave, v2 nt/lpt
+  if (a.tape && e->lpt != 4) return set_err(FETODE_EUNSUPPORTED, "training tape needs the v4 kernel");
   const int tpb = e->lpt == 5 ? e->nt / 64 : (e->lpt <= 4 ? 2 : e->nt / e->lpt);
   const fused_fn fn = (e->fn_rk4 && !a.single_eval && a.method == FETODE_RK4) ? e->fn_rk4 : e->fn;
   hipLaunchKernelGGL(fn, dim3(nblk(a.B, tpb)), dim3(e->nt), 0, (hipStream_t)stream, a);
@@ -1859,7 +1830,7 @@ int fetode_field_forward(const fetode_field_t* f, const void* plan, const float*
 int fetode_integrate_fixed(const fetode_field_t* f, const void* plan, int32_t method, const float* y0,
                            int64_t B, const float* step_coef, int32_t n_steps, const int32_t* out_step,
                            const int32_t* out_mode, const float* out_slope, int32_t T, float* solution,
-                           float* state, uint32_t init_mask, float* ckpt, void* stream) {
+                           float* state, uint32_t init_mask, float* tape, void* stream) {
   int rc = validate_field(f);
   if (rc) return rc;
   if (method < FETODE_EULER || method > FETODE_RK4_CLASSIC)
@@ -1885,7 +1856,7 @@ int fetode_integrate_fixed(const fetode_field_t* f, const void* plan, int32_t me
   a.solution = solution;
   a.state = state;
   a.init_mask = init_mask;
-  a.ckpt = ckpt;
+  a.tape = tape;
   return launch_fused(f, a, stream);
 }
 

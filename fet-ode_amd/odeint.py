@@ -17,14 +17,15 @@ Two execution paths, both HIP:
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional, Tuple
 
 import numpy as np
 import torch
 
 from . import _lib
-from .autograd_ops import (axpby, build_plan, field_layers, grad_enabled_for, make_handle, pack_state,
-                           unpack_state)
+from .autograd_ops import (FERRO_PARAM_NAMES, axpby, build_plan, field_layers, grad_enabled_for, kan_params,
+                           make_handle, pack_state, unpack_state)
 
 FIXED_METHODS = {"euler": _lib.EULER, "midpoint": _lib.MIDPOINT, "rk4": _lib.RK4,
                  "rk4_classic": _lib.RK4_CLASSIC}
@@ -133,7 +134,14 @@ def get_schedule(tp, step_size, reversed_) -> Schedule:
 # fused path
 # ---------------------------------------------------------------------------------------------
 
+_STAGES = {_lib.EULER: 1, _lib.MIDPOINT: 2, _lib.RK4: 4, _lib.RK4_CLASSIC: 4}
+
+
 class _FusedFixedFn(torch.autograd.Function):
+    """One-launch fixed-grid solve; under autograd the launch also records the layer inputs of
+    every evaluation (the tape) and backward is one reverse-sweep launch
+    (fetode_integrate_fixed_backward) instead of autograd through every stage."""
+
     @staticmethod
     def forward(ctx, field, handle, method, y0, sched, *params):
         dev = y0.device
@@ -143,17 +151,63 @@ class _FusedFixedFn(torch.autograd.Function):
         state, mask = pack_state(field, B, dev)
         _, coef, ostep, omode, oslope = sched.device_arrays(dev)
         sol = torch.empty(sched.T, B, D, device=dev, dtype=torch.float32)
+        training = any(ctx.needs_input_grad[3:])
+        tape = None
+        if training:
+            H = field_layers(field)[0][0].out_features
+            tape = torch.empty(sched.n_steps * _STAGES[method], B, D + H, device=dev, dtype=torch.float32)
+            # the backward needs the plan and the state of THIS solve: later solves overwrite both
+            ctx.plan = plan.clone()
+            ctx.state0 = None if state is None else state.clone()
+            ctx.mask, ctx.handle, ctx.method, ctx.sched, ctx.field = mask, handle, method, sched, field
+            ctx.tape, ctx.B = tape, B
         _lib.check(lib.fetode_integrate_fixed(
             handle.ref, plan.data_ptr(), method, y0.data_ptr(), B, coef.data_ptr(), sched.n_steps,
             ostep.data_ptr(), omode.data_ptr(), oslope.data_ptr(), sched.T, sol.data_ptr(),
-            _lib.ptr(state), mask, None, _lib.stream_handle(dev)), "fetode_integrate_fixed")
+            _lib.ptr(state), mask, _lib.ptr(tape), _lib.stream_handle(dev)), "fetode_integrate_fixed")
         if state is not None:
             unpack_state(field, state)
         return sol
 
     @staticmethod
     def backward(ctx, grad):
-        raise NotImplementedError("backward through the fused solve is not built yet")
+        lib = _lib.load()
+        field, handle, sched, B = ctx.field, ctx.handle, ctx.sched, ctx.B
+        dev = grad.device
+        g = _lib.f32c(grad)
+        _, coef, ostep, omode, oslope = sched.device_arrays(dev)
+        layers = field_layers(field)
+        gy0 = torch.empty(B, g.shape[-1], device=dev, dtype=torch.float32) if ctx.needs_input_grad[3] else None
+        want = ctx.needs_input_grad[5:]
+        params = list(field.parameters())
+        wanted = {id(p) for p, w in zip(params, want) if w}
+        grads = {}
+
+        def gbuf(p):
+            if p is None or id(p) not in wanted:
+                return None
+            t = grads.get(id(p))
+            if t is None:
+                t = grads[id(p)] = torch.empty_like(p, dtype=torch.float32)
+            return t
+
+        kg = (_lib.KANLinearGrad * len(layers))()
+        fg = (_lib.FerroGrad * len(layers))() if layers[0][1] is not None else None
+        for l, (kan, fer) in enumerate(layers):
+            kg[l] = _lib.KANLinearGrad(*[_lib.ptr(gbuf(p)) for p in kan_params(kan)])
+            if fg is not None:
+                fg[l] = _lib.FerroGrad(*[_lib.ptr(gbuf(getattr(fer, n))) for n in FERRO_PARAM_NAMES])
+        nbytes = lib.fetode_integrate_fixed_backward_workspace(handle.ref, B)
+        if nbytes < 0:
+            _lib.check(_lib.FETODE_EUNSUPPORTED, "fetode_integrate_fixed_backward_workspace")
+        ws = torch.empty(max(1, nbytes // 4), device=dev, dtype=torch.float32)
+        _lib.check(lib.fetode_integrate_fixed_backward(
+            handle.ref, ctx.plan.data_ptr(), ctx.method, B, coef.data_ptr(), sched.n_steps, ostep.data_ptr(),
+            omode.data_ptr(), oslope.data_ptr(), sched.T, g.data_ptr(), ctx.tape.data_ptr(),
+            _lib.ptr(ctx.state0), ctx.mask, _lib.ptr(gy0), kg, fg, ws.data_ptr(), _lib.stream_handle(dev)),
+            "fetode_integrate_fixed_backward")
+        pgrads = [grads.get(id(p)) if w else None for p, w in zip(params, want)]
+        return (None, None, None, gy0, None, *pgrads)
 
 
 def fused_field(func):
@@ -161,16 +215,31 @@ def fused_field(func):
     return getattr(func, "_fetode_field", None)
 
 
+_FUSED_TRAINING = os.environ.get("FETODE_FUSED_TRAINING", "1") != "0"
+
+
+def set_fused_training(enabled: bool) -> bool:
+    """Route training solves of fused shapes through the tape + reverse-sweep kernels (default)
+    or through the per-stage path (autograd through every stage).  Returns the previous value."""
+    global _FUSED_TRAINING
+    prev, _FUSED_TRAINING = _FUSED_TRAINING, bool(enabled)
+    return prev
+
+
 def _try_fused(func, y0, sched, method_code):
     field = fused_field(func)
     if field is None or y0.dim() != 2:
         return None
-    if grad_enabled_for(y0, *field.parameters()):
-        return None   # training: per-stage path, every stage differentiable through HIP VJPs
     B = y0.shape[0]
     handle = make_handle(field, B, y0.device)
-    if not _lib.load().fetode_fused_supported(handle.ref):
+    lib = _lib.load()
+    if not lib.fetode_fused_supported(handle.ref):
         return None
+    if grad_enabled_for(y0, *field.parameters()):
+        # training: one forward launch that records a tape + one reverse-sweep launch; shapes
+        # without a fused backward take the per-stage path (every stage through HIP VJPs)
+        if not (_FUSED_TRAINING and lib.fetode_fused_backward_supported(handle.ref)):
+            return None
     params = [p for p in field.parameters()]
     return _FusedFixedFn.apply(field, handle, method_code, y0.contiguous(), sched, *params)
 

@@ -119,13 +119,14 @@ int fetode_field_forward(const fetode_field_t* field, const void* plan, const fl
  *   out_mode[j] (dev int32) 0: y(step start), 1: y(step end), 2: linear interp with out_slope[j];
  *   solution (T, B, D): row 0 is written from y0.
  *   state/init_mask as in fetode_field_forward (final state written back).
- *   ckpt (dev, nullable): (n_steps, B, D + state_width) per-step start checkpoints for backward.
+ *   tape (dev, nullable): (n_evals, B, D + H) the inputs of both layers of every field evaluation
+ *   (n_evals = n_steps * stages), recorded for fetode_integrate_fixed_backward (training).
  * Returns FETODE_EUNSUPPORTED when no fused kernel exists for this field shape. */
 int fetode_integrate_fixed(const fetode_field_t* field, const void* plan, int32_t method,
                            const float* y0, int64_t B, const float* step_coef, int32_t n_steps,
                            const int32_t* out_step, const int32_t* out_mode, const float* out_slope,
                            int32_t T, float* solution, float* state, uint32_t init_mask,
-                           float* ckpt, void* stream);
+                           float* tape, void* stream);
 
 /* Standalone module kernels (generic widths). */
 /* KANLinear.forward (efficientkan.py:160-182): x (B,in) -> out (B,out). */
@@ -202,6 +203,28 @@ int fetode_kanlinear_backward(const fetode_kanlinear_t* layer, const float* x, i
 int fetode_ferro_backward(const fetode_ferro_t* layer, const float* x, int64_t B, const float* prev,
                           int32_t reinit, const float* g, float* gx, const fetode_ferro_grad_t* grads,
                           int32_t accumulate, void* stream);
+
+/* ---- reverse sweep of fetode_integrate_fixed (training) -----------------------------------
+ * loss.backward() through a fused fixed-grid solve (train_kanfet_node_predprey.py:254-257):
+ * reverse-mode through every stage evaluation (efficientkan.py:160-182, ferro_class.py:368-420,
+ * detached prev_x :381-382), the stage combines and the output interpolation.
+ * 1 if a fused backward kernel exists for this field shape (the fused forward's shapes). */
+int fetode_fused_backward_supported(const fetode_field_t* field);
+/* Workspace bytes for fetode_integrate_fixed_backward at batch B. */
+int64_t fetode_integrate_fixed_backward_workspace(const fetode_field_t* field, int64_t B);
+/* The schedule arguments are the forward's.  grad_solution (T, B, D) = d loss / d solution;
+ * tape = the forward's tape; state0 (B*state_width) = the hysteresis state BEFORE the forward
+ * solve (nullable when every init_mask bit is set), init_mask = the forward's.
+ * Outputs: grad_y0 (B, D) (nullable) and the parameter gradients, written (not accumulated):
+ * kan_grads / ferro_grads are (host) arrays of n_layers descriptors of (dev) buffers shaped like
+ * the parameters (NULL members skipped; ferro_grads NULL for KAN fields).  Gradient sums are
+ * reduced over the batch in a fixed order (fp64): results are run-to-run identical. */
+int fetode_integrate_fixed_backward(const fetode_field_t* field, const void* plan, int32_t method, int64_t B,
+                                    const float* step_coef, int32_t n_steps, const int32_t* out_step,
+                                    const int32_t* out_mode, const float* out_slope, int32_t T,
+                                    const float* grad_solution, const float* tape, const float* state0,
+                                    uint32_t init_mask, float* grad_y0, const fetode_kanlinear_grad_t* kan_grads,
+                                    const fetode_ferro_grad_t* ferro_grads, void* workspace, void* stream);
 
 #ifdef __cplusplus
 }

@@ -58,6 +58,8 @@ def test_no_kernel_uses_scratch(tmp_path):
     ks = kernel_metadata(LIB, tmp_path)
     fused = [n for n in ks if "fused" in n]
     assert len(fused) >= 8, sorted(ks)
+    # SGPR spills without a private segment land in VGPR lanes (v_writelane / v_readlane), not in
+    # memory; VGPR spills and any private segment are per-lane scratch traffic.
     bad = {n: v for n, v in ks.items()
-           if v.get("private_segment_fixed_size", 0) or v.get("vgpr_spill_count", 0) or v.get("sgpr_spill_count", 0)}
+           if v.get("private_segment_fixed_size", 0) or v.get("vgpr_spill_count", 0)}
     assert not bad, bad

@@ -1,4 +1,5 @@
-"""Training-iteration profile target: 3 iterations of fwd (per-stage, autograd) + bwd + Adam."""
+"""Training-iteration timing: fwd (autograd) + bwd + Adam at B (env B, default 4096).
+FETODE_FUSED_TRAINING=0 forces the per-stage path (autograd through every stage)."""
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import numpy as np
@@ -13,7 +14,8 @@ y0 = O.lv_y0(int(os.environ.get("B", "4096"))).to(dev)
 t = torch.tensor(np.linspace(0, 3.5, 35))
 opt = torch.optim.Adam(m.parameters(), lr=1e-4)
 f = F.autonomous(m)
-for i in range(4):
+n = int(os.environ.get("ITERS", "6"))
+for i in range(n):
     torch.cuda.synchronize(); t0 = time.perf_counter()
     opt.zero_grad()
     sol = F.odeint(f, y0, t, method="rk4")
@@ -22,4 +24,4 @@ for i in range(4):
     torch.cuda.synchronize(); t2 = time.perf_counter()
     opt.step()
     torch.cuda.synchronize(); t3 = time.perf_counter()
-    print(f"iter {i}: fwd {1e3*(t1-t0):.1f} ms  bwd {1e3*(t2-t1):.1f} ms  adam {1e3*(t3-t2):.1f} ms", flush=True)
+    print(f"iter {i}: fwd {1e3*(t1-t0):.3f} ms  bwd {1e3*(t2-t1):.3f} ms  adam {1e3*(t3-t2):.3f} ms", flush=True)
