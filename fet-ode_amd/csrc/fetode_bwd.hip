@@ -84,12 +84,68 @@ struct BL {  // compile-time shape of one layer
   static_assert(NS >= 1, "grid too small for cubic splines");
 };
 
+// Per-block LDS tables of the whole field.  Per-INPUT tables are laid out over the combined input
+// index t in [0, W): t < D are layer-0 inputs, t >= D layer-1 inputs (same knot count), so the
+// feature phase is one code path for both layers.
+template <int W, int NG, int NB>
+struct BInTab {
+  static constexpr int NI = NG - 1;
+  float4 bp[W * NI * 4];  // basis B_{m-3+r} on interval m as a cubic in u: [t][m][r] (power basis)
+  float knots[W * NG];
+  float rh[W * NI];       // 1/(g[m+1] - g[m])
+  float lg[NB > 0 ? 2 * W * NB : 1];  // (-a log2e, a b log2e) per (t, j)
+
+  __device__ void stage(const float* __restrict__ plan, const LayerPlan& P0, const LayerPlan& P1, int D, int tid,
+                        int nt) {
+    for (int q = tid; q < W * NG; q += nt) {
+      const int t = q / NG, j = q % NG;
+      knots[q] = t < D ? plan[P0.knots + t * NG + j] : plan[P1.knots + (t - D) * NG + j];
+    }
+    for (int q = tid; q < W * NI; q += nt) {
+      const int t = q / NI, m = q % NI;
+      rh[q] = t < D ? plan[P0.rh + t * NI + m] : plan[P1.rh + (t - D) * NI + m];
+    }
+    for (int q = tid; q < 2 * W * NB; q += nt)
+      lg[q] = q < 2 * D * NB ? plan[P0.lg + q] : plan[P1.lg + (q - 2 * D * NB)];
+    // basis polynomials: Cox-de Boor (efficientkan.py:117-131) restricted to interval m, in
+    // fp64 at u = 0, 1/3, 2/3, 1, converted to the power basis (exact for cubics)
+    for (int q = tid; q < W * NI; q += nt) {
+      const int t = q / NI, m = q % NI;
+      const float* g = t < D ? plan + P0.knots + t * NG : plan + P1.knots + (t - D) * NG;
+      const double h = (double)g[m + 1] - g[m];
+      double v[4][kSO + 2];
+      for (int s = 0; s < 4; ++s) {
+        const double x = g[m] + h * (s / 3.0);
+        double* N = v[s];
+        for (int r = 0; r < kSO + 2; ++r) N[r] = 0.0;
+        N[kSO] = 1.0;
+        for (int k = 1; k <= kSO; ++k) {
+          double M[kSO + 2];
+          for (int r = 0; r < kSO + 2; ++r) M[r] = 0.0;
+          for (int r = kSO - k; r <= kSO; ++r) {
+            const int j = m - kSO + r;
+            if (j >= 0 && j <= NG - 2 - k) {
+              const double left = (x - g[j]) / ((double)g[j + k] - g[j]) * N[r];
+              const double right = ((double)g[j + k + 1] - x) / ((double)g[j + k + 1] - g[j + 1]) * N[r + 1];
+              M[r] = left + right;
+            }
+          }
+          for (int r = 0; r < kSO + 2; ++r) N[r] = M[r];
+        }
+      }
+      for (int r = 0; r <= kSO; ++r) {
+        const double a0 = v[0][r], a1 = v[1][r], a2 = v[2][r], a3 = v[3][r];
+        bp[q * 4 + r] = make_float4((float)a0, (float)((-11.0 * a0 + 18.0 * a1 - 9.0 * a2 + 2.0 * a3) / 2.0),
+                                    (float)(9.0 * (2.0 * a0 - 5.0 * a1 + 4.0 * a2 - a3) / 2.0),
+                                    (float)(9.0 * (-a0 + 3.0 * a1 - 3.0 * a2 + a3) / 2.0));
+      }
+    }
+  }
+};
+
 template <class L>
-struct BTab {  // per-block LDS copy of one layer's shared tables (staged once per launch)
+struct BTab {  // per-block LDS copy of one layer's edge tables
   float4 sp[L::OUT * L::IN * (L::NI + 1)];  // spline edge (o, i) as a cubic in u per interval
-  float knots[L::IN * L::NG];
-  float rk[L::IN * kSO * (L::NG - 1)];      // 1/(g[j+k]-g[j]) at [i][(k-1)(NG-1)+j]
-  float lg[L::NL > 0 ? 2 * L::NL : 1];      // (-a log2e, a b log2e)
   float kw[L::OUT * L::IN * L::NFL];        // SiLU weight, 2 * scaled logistic weights
   float pa[L::NL > 0 ? L::NL : 1], pb[L::NL > 0 ? L::NL : 1];
   float4 fe[L::E > 0 ? L::E : 1];           // Ferro element (i,o,k): k, Ec, coef*Ps*k
@@ -99,14 +155,6 @@ struct BTab {  // per-block LDS copy of one layer's shared tables (staged once p
     for (int e = tid; e < L::E; e += nt) fe[e] = make_float4(fl.k[e], fl.Ec[e], (fl.coef[e] * fl.Ps[e]) * fl.k[e], 0.f);
     const float4* src = reinterpret_cast<const float4*>(plan + P.sp);
     for (int q = tid; q < L::OUT * L::IN * (L::NI + 1); q += nt) sp[q] = src[q];
-    for (int q = tid; q < L::IN * L::NG; q += nt) knots[q] = plan[P.knots + q];
-    for (int q = tid; q < L::IN * kSO * (L::NG - 1); q += nt) {
-      const int i = q / (kSO * (L::NG - 1)), r = q % (kSO * (L::NG - 1));
-      const int k = r / (L::NG - 1) + 1, j = r % (L::NG - 1);
-      const float* g = plan + P.knots + i * L::NG;
-      rk[q] = j + k < L::NG ? 1.0f / (g[j + k] - g[j]) : 0.f;
-    }
-    for (int q = tid; q < 2 * L::NL; q += nt) lg[q] = plan[P.lg + q];
     for (int q = tid; q < L::OUT * L::IN * L::NFL; q += nt) kw[q] = plan[P.kw + q];
     for (int q = tid; q < L::NL; q += nt) {
       pa[q] = kl.logistic_a[q];
@@ -115,18 +163,16 @@ struct BTab {  // per-block LDS copy of one layer's shared tables (staged once p
   }
 };
 
-template <class L>
-struct BFeat {  // per-wave LDS features of one layer's input
-  float x[L::IN], pv[L::IN], silu[L::IN], dsilu[L::IN], u[L::IN], up[L::IN];
-  int m[L::IN];
-  float bd[L::IN * L::NS];
-  float sg[L::NL > 0 ? L::NL : 1];
-  float gout[L::OUT];
-  float gin[L::IN];
+template <int W, int NS, int NB>
+struct BFeat {  // per-wave LDS features of both layers' inputs, combined index t
+  float x[W], pv[W], silu[W], dsilu[W], u[W], up[W];
+  int m[W];
+  float bd[W * NS];
+  float sg[NB > 0 ? W * NB : 1];
 };
 
 template <class L>
-struct BReg {  // per-lane register slice of one layer: gradient sums + the Ferro parameters
+struct BReg {  // per-lane register slice of one layer: its gradient sums
   float A[L::RF1], C[L::RF1], Ev[L::RF1];
   float G;
   float base[L::RE], spl[L::RE][L::NS];
@@ -186,47 +232,68 @@ struct BReg {  // per-lane register slice of one layer: gradient sums + the Ferr
 
 __device__ __forceinline__ float sigm_l2(float zl) { return rcp(1.0f + ex2(zl)); }  // 1/(1+2^zl)
 
-// the lanes of one wave exchange data through that wave's private LDS region only: a wave-level
-// barrier (LDS ops complete + no reordering) replaces the workgroup barrier
-__device__ __forceinline__ void wsync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+// The lanes of one wave exchange data only through that wave's private LDS region.  DS
+// instructions of one wave execute in issue order, so a compiler barrier plus a wait for the
+// wave's own LDS traffic replaces the workgroup barrier (global loads in flight — the tape
+// prefetch — are not waited for).
+__device__ __forceinline__ void wsync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// sum over aligned groups of G lanes (G a power of two <= 32), result on every lane of the group
+template <int G>
+__device__ __forceinline__ float group_sum(float v) {
+  if constexpr (G >= 2) v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  if constexpr (G >= 4) v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  if constexpr (G == 8) v += __shfl_xor(v, 4);
+  if constexpr (G >= 16) {  // row_ror 4 then 8: every lane of the 16-lane row holds the row sum
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x124, 0xF, 0xF, false));
+    v += __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), 0x128, 0xF, 0xF, false));
+  }
+  if constexpr (G >= 32) v += __shfl_xor(v, 16);
+  static_assert(G <= 32, "group up to 32 lanes");
+  return v;
 }
 
-// per-input features of input i of a layer (one lane)
-template <class L>
-__device__ __forceinline__ void feat_input(BFeat<L>& F, const BTab<L>& Tb, int i, float gsl2e, int z) {
-  const float x = F.x[i];
+// features of combined input t (one lane): SiLU, SiLU', knot interval, u, dense bases, gate
+template <int W, int NG, int NB>
+__device__ __forceinline__ void feat_input(BFeat<W, NG - 1 - kSO, NB>& F, const BInTab<W, NG, NB>& Tb, int t,
+                                           float gsl2e, int z) {
+  constexpr int NI = NG - 1, NS = NG - 1 - kSO;
+  const float x = F.x[t];
   const float sx = sigm_l2(-x * FETODE_LOG2E);
-  F.silu[i] = x * sx;
-  F.dsilu[i] = sx * ffma(x, 1.0f - sx, 1.0f);
-  const float* g = &Tb.knots[i * L::NG + z];
-  const float* rk = &Tb.rk[i * kSO * (L::NG - 1) + z];
+  F.silu[t] = x * sx;
+  F.dsilu[t] = sx * ffma(x, 1.0f - sx, 1.0f);
+  const float* g = &Tb.knots[t * NG + z];
   int m = -1;
 #pragma unroll
-  for (int j = 0; j < L::NG; ++j) m += (x >= g[j]) ? 1 : 0;
-  float u;
-  if (!__builtin_isfinite(x)) {
-    m = L::NI;
-    u = __builtin_nanf("");
-  } else if (m < 0 || m >= L::NI) {
-    m = L::NI;
-    u = 0.f;
-  } else {
-    u = (x - g[m]) * rk[m];  // level-1 reciprocal = 1/(g[m+1]-g[m])
+  for (int j = 0; j < NG; ++j) m += (x >= g[j]) ? 1 : 0;
+  const bool fin = __builtin_isfinite(x);
+  const bool in = fin && m >= 0 && m < NI;
+  const int mc = in ? m : 0;
+  const float u = in ? (x - g[mc]) * Tb.rh[t * NI + mc + z] : (fin ? 0.f : __builtin_nanf(""));
+  F.m[t] = in ? m : NI;
+  F.u[t] = u;
+  float* bd = &F.bd[t * NS];
+  // non-finite x: NaN bases like the reference's (x - g)/d * 0; outside the grid: all zero
+  const float fill = fin ? 0.f : __builtin_nanf("");
+#pragma unroll
+  for (int c = 0; c < NS; ++c) bd[c] = fill;
+  if (in) {
+    const float4* bp = &Tb.bp[(t * NI + mc) * 4 + z];
+#pragma unroll
+    for (int r = 0; r <= kSO; ++r) {
+      const int c = mc - kSO + r;
+      const float4 p = bp[r];
+      if (c >= 0 && c < NS) bd[c] = ffma(ffma(ffma(p.w, u, p.z), u, p.y), u, p.x);
+    }
   }
-  F.m[i] = m;
-  F.u[i] = u;
-  float* bd = &F.bd[i * L::NS];
-  bspline_local<kSO>(x, L::NG, g, rk, [&](int c, float v) { bd[c] = v; });
-  if constexpr (L::FERRO) F.up[i] = sigm_l2(-gsl2e * (x - F.pv[i]));
+  F.up[t] = sigm_l2(-gsl2e * (x - F.pv[t]));
 }
 
-// the VJP jobs of one layer for one evaluation: gradient sums into R, d out/d x contributions
-// into cb[i * NTM + t]
-template <class L>
-__device__ __forceinline__ void layer_jobs(const BFeat<L>& F, const BTab<L>& Tb, BReg<L>& R, float* __restrict__ cb,
+// the VJP jobs of one layer (inputs at combined offset TB) for one evaluation: gradient sums into
+// R, d out/d x contributions into cb[i * NTM + t]
+template <class L, int TB, class FT>
+__device__ __forceinline__ void layer_jobs(const FT& F, const float* __restrict__ gout, const BTab<L>& Tb,
+                                           const float* __restrict__ rhs, BReg<L>& R, float* __restrict__ cb,
                                            float gsl2e, float wc, float gs, int lane, int z) {
   if constexpr (L::FERRO) {
 #pragma unroll
@@ -235,7 +302,7 @@ __device__ __forceinline__ void layer_jobs(const BFeat<L>& F, const BTab<L>& Tb,
       if (e < L::E) {
         const int i = e / (L::OUT * L::K), ok_ = e % (L::OUT * L::K);
         const int o = ok_ / L::K;
-        const float x = F.x[i], up = F.up[i], go = F.gout[o];
+        const float x = F.x[TB + i], up = F.up[TB + i], go = gout[o];
         const float4 pe = Tb.fe[e + z];
         const float kk = pe.x, Ec = pe.y;
         const float cn = sigm_l2(gsl2e * (x + Ec));           // sigmoid(gs(-x - Ec))
@@ -253,28 +320,28 @@ __device__ __forceinline__ void layer_jobs(const BFeat<L>& F, const BTab<L>& Tb,
         cb[i * L::NTM + ok_] = q * pe.z * ffma(Ec, dmdx, 1.0f);
       }
     }
-    if (lane < L::OUT) R.G += F.gout[lane];
+    if (lane < L::OUT) R.G += gout[lane];
   }
 #pragma unroll
   for (int r = 0; r < L::RE; ++r) {
     const int q = lane + 64 * r;
     if (q < L::NE) {
       const int o = q / L::IN, i = q % L::IN;
-      const float go = F.gout[o];
-      R.base[r] = ffma(go, F.silu[i], R.base[r]);
+      const float go = gout[o];
+      R.base[r] = ffma(go, F.silu[TB + i], R.base[r]);
 #pragma unroll
-      for (int c = 0; c < L::NS; ++c) R.spl[r][c] = ffma(go, F.bd[i * L::NS + c], R.spl[r][c]);
-      const int m = F.m[i];
-      const float u = F.u[i];
+      for (int c = 0; c < L::NS; ++c) R.spl[r][c] = ffma(go, F.bd[(TB + i) * L::NS + c], R.spl[r][c]);
+      const int m = F.m[TB + i];
+      const float u = F.u[TB + i];
       float dsdx;
       if (m < L::NI) {
         const float4 cf = Tb.sp[q * (L::NI + 1) + m + z];  // (o, i, interval), q = o*IN + i
-        dsdx = ffma(u, ffma(3.0f * u, cf.w, 2.0f * cf.z), cf.y) * Tb.rk[i * kSO * (L::NG - 1) + m + z];
+        dsdx = ffma(u, ffma(3.0f * u, cf.w, 2.0f * cf.z), cf.y) * rhs[(TB + i) * L::NI + m + z];
       } else {
         dsdx = u * 0.0f;  // 0 outside the grid, NaN for non-finite inputs (the reference's NaN bases)
       }
       const float wb = Tb.kw[o * (L::IN * L::NFL) + i * L::NFL + z];
-      cb[i * L::NTM + L::OUT * L::K + o] = go * ffma(wb, F.dsilu[i], dsdx);
+      cb[i * L::NTM + L::OUT * L::K + o] = go * ffma(wb, F.dsilu[TB + i], dsdx);
     }
   }
 #pragma unroll
@@ -282,11 +349,11 @@ __device__ __forceinline__ void layer_jobs(const BFeat<L>& F, const BTab<L>& Tb,
     const int q = lane + 64 * r;
     if (q < L::NL) {
       const int i = q / L::NB, j = q % L::NB;
-      const float s = F.sg[q], ds = s * (1.0f - s), x = F.x[i];
+      const float s = F.sg[TB * L::NB + q], ds = s * (1.0f - s), x = F.x[TB + i];
       float S = 0.f;
 #pragma unroll
       for (int o = 0; o < L::OUT; ++o) {
-        const float go = F.gout[o];
+        const float go = gout[o];
         S = ffma(go, Tb.kw[o * (L::IN * L::NFL) + i * L::NFL + 1 + j + z], S);
         R.lw[r][o] = ffma(go, s, R.lw[r][o]);
       }
@@ -299,18 +366,17 @@ __device__ __forceinline__ void layer_jobs(const BFeat<L>& F, const BTab<L>& Tb,
   }
 }
 
-// gin[i] = sum_t cb[i * NTM + t], fixed order: LPI lanes per input, strided partial sums, xor tree
+// gin[i] = sum_t cb[i * NTM + t], fixed order: LPI lanes per input, strided partial sums, DPP tree
 template <class L>
 __device__ __forceinline__ void reduce_gin(const float* __restrict__ cb, float* gin, int lane) {
-  constexpr int LPI = L::LPI;
+  constexpr int LPI = L::LPI > 32 ? 32 : L::LPI;
   const int i = lane / LPI, sub = lane % LPI;
   float s = 0.f;
   if (i < L::IN) {
 #pragma unroll
     for (int t = sub; t < L::NTM; t += LPI) s += cb[i * L::NTM + t];
   }
-#pragma unroll
-  for (int k = LPI / 2; k >= 1; k >>= 1) s += __shfl_xor(s, k);
+  s = group_sum<LPI>(s);
   if (i < L::IN && sub == 0) gin[i] = s;
 }
 
@@ -379,16 +445,19 @@ template <int D, int H, int K, int NB, int NG, bool FERRO>
 __global__ __launch_bounds__(64 * kTPB) void fixed_bwd_kernel(BwdArgs a) {
   using L0 = BL<D, H, K, NB, NG, FERRO>;
   using L1 = BL<H, D, K, NB, NG, FERRO>;
-  constexpr int W = D + H;
+  constexpr int W = D + H, NI = NG - 1, NS = NG - 1 - kSO;
   constexpr int CB = L0::IN * L0::NTM > L1::IN * L1::NTM ? L0::IN * L0::NTM : L1::IN * L1::NTM;
+  static_assert(W <= 64, "one lane per input");
+  __shared__ BInTab<W, NG, NB> TI;
   __shared__ BTab<L0> T0;
   __shared__ BTab<L1> T1;
-  __shared__ BFeat<L0> sF0[kTPB];
-  __shared__ BFeat<L1> sF1[kTPB];
+  __shared__ BFeat<W, NS, NB> sF[kTPB];
   __shared__ float s_cb[kTPB][CB];
+  __shared__ float s_g1[kTPB][D], s_g0[kTPB][H], s_gx[kTPB][D];
   __shared__ float s_ak[kTPB][4][D], s_ay[kTPB][D], s_ac[kTPB][4][3];
 
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  TI.stage(a.plan, a.P0, a.P1, D, threadIdx.x, 64 * kTPB);
   T0.stage(a.k0, a.f0, a.plan, a.P0, threadIdx.x, 64 * kTPB);
   T1.stage(a.k1, a.f1, a.plan, a.P1, threadIdx.x, 64 * kTPB);
   BReg<L0> R0;
@@ -397,14 +466,17 @@ __global__ __launch_bounds__(64 * kTPB) void fixed_bwd_kernel(BwdArgs a) {
   R1.zero();
   __syncthreads();  // tables staged; from here on every wave syncs only with itself
 
-  BFeat<L0>& F0 = sF0[wid];
-  BFeat<L1>& F1 = sF1[wid];
+  BFeat<W, NS, NB>& F = sF[wid];
   float* cb = s_cb[wid];
+  float* g1 = s_g1[wid];  // layer-1 output adjoint = d loss / d k_stage
+  float* g0 = s_g0[wid];  // layer-0 output adjoint = d loss / d h
+  float* gx = s_gx[wid];
   float(&ak)[4][D] = s_ak[wid];
   float(&ay)[D] = s_ay[wid];
   float(&acs)[4][3] = s_ac[wid];
   const float gs0 = (float)a.f0.gate_slope, gs1 = (float)a.f1.gate_slope;
   const float gl0 = a.P0.gsl2e, gl1 = a.P1.gsl2e, wc0 = a.P0.wc, wc1 = a.P1.wc;
+  const float glane = lane < D ? gl0 : gl1;  // the feature lane's layer
   const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4 : a.method == FETODE_MIDPOINT ? 2 : 1;
   const int64_t tstride = a.B * W;
   const int n_ev = a.n_steps * ns;
@@ -458,37 +530,28 @@ __global__ __launch_bounds__(64 * kTPB) void fixed_bwd_kernel(BwdArgs a) {
         int z = 0;
         asm volatile("" : "+s"(z));
         const float nxt = tape_at(ev - 2);  // prefetch: consumed by the next evaluation
-        if (lane < D) {
-          F0.x[lane] = cur;
-          F0.pv[lane] = prv;
-          F1.gout[lane] = ak[st][lane];
-        } else if (lane < W) {
-          F1.x[lane - D] = cur;
-          F1.pv[lane - D] = prv;
+        if (lane < W) {
+          F.x[lane] = cur;
+          F.pv[lane] = prv;
         }
+        if (lane < D) g1[lane] = ak[st][lane];
         wsync();
-        // features of both layers' inputs
-        if (lane < D) feat_input<L0>(F0, T0, lane, gl0, z);
-        else if (lane < W) feat_input<L1>(F1, T1, lane - D, gl1, z);
-        for (int q = lane; q < L0::NL + L1::NL; q += 64) {
-          if (q < L0::NL) {
-            F0.sg[q] = sigm_l2(ffma(T0.lg[2 * q + z], F0.x[q / NB], T0.lg[2 * q + 1 + z]));
-          } else {
-            const int qq = q - L0::NL;
-            F1.sg[qq] = sigm_l2(ffma(T1.lg[2 * qq + z], F1.x[qq / NB], T1.lg[2 * qq + 1 + z]));
-          }
-        }
+        // features of both layers' inputs: one code path over the combined input index
+        if (lane < W) feat_input<W, NG, NB>(F, TI, lane, glane, z);
+#pragma unroll
+        for (int q = lane; q < W * NB; q += 64)
+          F.sg[q] = sigm_l2(ffma(TI.lg[2 * q + z], F.x[q / NB], TI.lg[2 * q + 1 + z]));
         wsync();
-        layer_jobs<L1>(F1, T1, R1, cb, gl1, wc1, gs1, lane, z);
+        layer_jobs<L1, D>(F, g1, T1, TI.rh, R1, cb, gl1, wc1, gs1, lane, z);
         wsync();
-        reduce_gin<L1>(cb, F0.gout, lane);  // d loss / d h = layer-0 output adjoint
+        reduce_gin<L1>(cb, g0, lane);  // d loss / d h
         wsync();
-        layer_jobs<L0>(F0, T0, R0, cb, gl0, wc0, gs0, lane, z);
+        layer_jobs<L0, 0>(F, g0, T0, TI.rh, R0, cb, gl0, wc0, gs0, lane, z);
         wsync();
-        reduce_gin<L0>(cb, F0.gin, lane);
+        reduce_gin<L0>(cb, gx, lane);
         wsync();
         if (lane < D) {
-          const float ax = F0.gin[lane];
+          const float ax = gx[lane];
           ay[lane] += ax;
           for (int j = 0; j < st; ++j) ak[j][lane] = ffma(acs[st][j], ax, ak[j][lane]);
         }
