@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--train-iters", type=int, default=5, help="0 skips the training-rate line")
+    ap.add_argument("--train-iters", type=int, default=20, help="0 skips the training-rate line")
     return ap.parse_args()
 
 
@@ -110,12 +110,17 @@ def pmc_traffic_per_launch():
 
 
 def train_rate(model, y0d, t, iters, warmup, world):
-    """One training iteration = forward rk4 solve with autograd + backward through every stage
-    (HIP VJPs) + gradient all-reduce (RCCL when world > 1) + Adam."""
+    """One training iteration = forward rk4 solve with autograd (one launch that also records the
+    layer inputs of every evaluation) + backward (one reverse-sweep launch + fixed-order gradient
+    reduction) + gradient all-reduce (RCCL when world > 1) + Adam.  Adam runs as
+    torch's fused multi-tensor kernel (same update rule as the reference's torch.optim.Adam)."""
     import fet_ode_amd.dist as D
     dev = y0d.device
     func = F.autonomous(model)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    try:
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=True)
+    except (RuntimeError, TypeError):
+        opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     target = torch.zeros(T, y0d.shape[0], 2, device=dev)
 
     def it():
@@ -144,7 +149,7 @@ def train_rate(model, y0d, t, iters, warmup, world):
         el = tt.item()
     return {"value": world * iters * STEPS_PER_SOLVE / el, "unit": "RK4 steps/s trained (fwd+bwd+allreduce+Adam)",
             "ms_per_iter": el / iters * 1e3, "iters": iters,
-            "path": "per-stage HIP kernels + HIP VJPs (fused backward not built yet)"}
+            "path": "fused: fetode_integrate_fixed with tape + fetode_integrate_fixed_backward (one launch each)"}
 
 
 def cpu_baseline(sd, y0, t, seconds):

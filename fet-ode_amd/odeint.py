@@ -143,7 +143,7 @@ class _FusedFixedFn(torch.autograd.Function):
     (fetode_integrate_fixed_backward) instead of autograd through every stage."""
 
     @staticmethod
-    def forward(ctx, field, handle, method, y0, sched, *params):
+    def forward(ctx, field, handle, method, y0, sched, training, *params):
         dev = y0.device
         B, D = y0.shape
         lib = _lib.load()
@@ -151,8 +151,7 @@ class _FusedFixedFn(torch.autograd.Function):
         state, mask = pack_state(field, B, dev)
         _, coef, ostep, omode, oslope = sched.device_arrays(dev)
         sol = torch.empty(sched.T, B, D, device=dev, dtype=torch.float32)
-        training = any(ctx.needs_input_grad[3:])
-        tape = None
+        tape = None  # the caller's flag: needs_input_grad follows requires_grad even under no_grad
         if training:
             H = field_layers(field)[0][0].out_features
             tape = torch.empty(sched.n_steps * _STAGES[method], B, D + H, device=dev, dtype=torch.float32)
@@ -178,7 +177,7 @@ class _FusedFixedFn(torch.autograd.Function):
         _, coef, ostep, omode, oslope = sched.device_arrays(dev)
         layers = field_layers(field)
         gy0 = torch.empty(B, g.shape[-1], device=dev, dtype=torch.float32) if ctx.needs_input_grad[3] else None
-        want = ctx.needs_input_grad[5:]
+        want = ctx.needs_input_grad[6:]
         params = list(field.parameters())
         wanted = {id(p) for p, w in zip(params, want) if w}
         grads = {}
@@ -207,7 +206,7 @@ class _FusedFixedFn(torch.autograd.Function):
             _lib.ptr(ctx.state0), ctx.mask, _lib.ptr(gy0), kg, fg, ws.data_ptr(), _lib.stream_handle(dev)),
             "fetode_integrate_fixed_backward")
         pgrads = [grads.get(id(p)) if w else None for p, w in zip(params, want)]
-        return (None, None, None, gy0, None, *pgrads)
+        return (None, None, None, gy0, None, None, *pgrads)
 
 
 def fused_field(func):
@@ -235,13 +234,14 @@ def _try_fused(func, y0, sched, method_code):
     lib = _lib.load()
     if not lib.fetode_fused_supported(handle.ref):
         return None
-    if grad_enabled_for(y0, *field.parameters()):
+    params = [p for p in field.parameters()]
+    training = grad_enabled_for(y0, *params)
+    if training:
         # training: one forward launch that records a tape + one reverse-sweep launch; shapes
         # without a fused backward take the per-stage path (every stage through HIP VJPs)
         if not (_FUSED_TRAINING and lib.fetode_fused_backward_supported(handle.ref)):
             return None
-    params = [p for p in field.parameters()]
-    return _FusedFixedFn.apply(field, handle, method_code, y0.contiguous(), sched, *params)
+    return _FusedFixedFn.apply(field, handle, method_code, y0.contiguous(), sched, training, *params)
 
 
 # ---------------------------------------------------------------------------------------------
