@@ -4,16 +4,18 @@ Drop-in surface of the reference hot path (sallywang147/FET-ODE):
   * ``odeint``               — torchdiffeq.odeint (euler, midpoint, rk4, dopri5)
   * ``efficientkan``         — LogisticBasis, KANLinear, KAN (+ KANFET)
   * ``ferro_class``          — FerroelectricBasis
+  * ``ecg``                  — the ECG KAN-FET NODE (hysteretic LogisticBasis, KANFeatureMixer,
+                               No_MLP_KANODEFunc, KanFet_NODE; train_ecg_kan_fet_nn_ode.py)
   * ``autonomous(field)``    — calDeriv-style func(t, y) = field(y) that odeint integrates in a
                                single fused HIP launch
 All compute runs in libfetode.so (HIP, gfx950) through the C ABI of include/fetode.h.
 """
 from . import _lib
-from . import efficientkan, ferro_class
+from . import ecg, efficientkan, ferro_class
 from .efficientkan import KAN, KANFET, KANFETLayer, KANLinear, LogisticBasis, ODEFunc, autonomous
 from .ferro_class import FerroelectricBasis
 from .odeint import SOLVERS, odeint, set_fused_training
 
 __all__ = ["odeint", "SOLVERS", "set_fused_training", "KAN", "KANFET", "KANFETLayer", "KANLinear", "LogisticBasis",
-           "FerroelectricBasis", "ODEFunc", "autonomous", "efficientkan", "ferro_class"]
+           "FerroelectricBasis", "ODEFunc", "autonomous", "ecg", "efficientkan", "ferro_class"]
 __version__ = "0.1.0"

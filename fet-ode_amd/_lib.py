@@ -50,6 +50,12 @@ class FerroGrad(ctypes.Structure):
     _fields_ = [(n, _fp) for n in ("k", "Ec", "Ps", "bias", "coef")]
 
 
+class HLogisticDesc(ctypes.Structure):
+    _fields_ = [("in_dim", ctypes.c_int32), ("num_basis", ctypes.c_int32),
+                ("k", _fp), ("Ec", _fp), ("Ps", _fp), ("bias", _fp),
+                ("gate_slope", ctypes.c_double), ("breaking_point", ctypes.c_double)]
+
+
 class FieldDesc(ctypes.Structure):
     _fields_ = [
         ("n_layers", ctypes.c_int32),
@@ -99,6 +105,13 @@ SIGNATURES = {
                                                        _vp, _vp, _vp, ctypes.c_uint32, _vp,
                                                        ctypes.POINTER(KANLinearGrad), ctypes.POINTER(FerroGrad),
                                                        _vp, _vp]),
+    "fetode_hlogistic_mixer_forward": (ctypes.c_int, [ctypes.POINTER(HLogisticDesc), _vp, ctypes.c_int64, _vp,
+                                                      ctypes.c_int32, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp,
+                                                      _vp, _vp]),
+    "fetode_hlogistic_mixer_backward_workspace": (ctypes.c_int64, [ctypes.POINTER(HLogisticDesc), ctypes.c_int64]),
+    "fetode_hlogistic_mixer_backward": (ctypes.c_int, [ctypes.POINTER(HLogisticDesc), _vp, ctypes.c_int64, _vp,
+                                                       ctypes.c_int32, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp, _vp,
+                                                       _vp, _vp, _vp, _vp, _vp, _vp]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

@@ -445,7 +445,7 @@ template <int D, int H, int K, int NB, int NG, bool FERRO>
 __global__ __launch_bounds__(64 * kTPB) void fixed_bwd_kernel(BwdArgs a) {
   using L0 = BL<D, H, K, NB, NG, FERRO>;
   using L1 = BL<H, D, K, NB, NG, FERRO>;
-  constexpr int W = D + H, NI = NG - 1, NS = NG - 1 - kSO;
+  constexpr int W = D + H, NS = NG - 1 - kSO;
   constexpr int CB = L0::IN * L0::NTM > L1::IN * L1::NTM ? L0::IN * L0::NTM : L1::IN * L1::NTM;
   static_assert(W <= 64, "one lane per input");
   __shared__ BInTab<W, NG, NB> TI;

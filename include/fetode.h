@@ -226,6 +226,37 @@ int fetode_integrate_fixed_backward(const fetode_field_t* field, const void* pla
                                     uint32_t init_mask, float* grad_y0, const fetode_kanlinear_grad_t* kan_grads,
                                     const fetode_ferro_grad_t* ferro_grads, void* workspace, void* stream);
 
+/* ---- ECG KAN-FET NODE field (BASELINE configs[2]) -----------------------
+ * The hysteretic LogisticBasis of train_ecg_kan_fet_nn_ode.py:54-133 (hard branch switch:
+ * branch_state = sigmoid(gate_slope (x - prev_x)) > breaking_point; prev_x remembers the LAST
+ * batch row of the previous call, :131-132).  (dev) pointers. */
+typedef struct fetode_hlogistic {
+  int32_t in_dim, num_basis;
+  const float *k, *Ec, *Ps, *bias;  /* (in, nb) :84-88 (coef :88 is unused by forward) */
+  double gate_slope, breaking_point; /* :71,74 defaults 5.0, 0.5 */
+} fetode_hlogistic_t;
+
+/* KANFeatureMixer (:408-421): phi = act(basis(x)) flattened (B, in*nb), act = sigmoid when
+ * act_sigmoid != 0 else identity; with w != NULL also the Linear head of No_MLP_KANODEFunc
+ * (:483-509): out = phi w^T + bias, w (n_out, in*nb), bias (n_out) nullable.
+ * x (B, in); prev (in*nb) = prev_x as read by this call; phi (B, in*nb) nullable when w != NULL;
+ * branch (B, in*nb) nullable = the rebound branch_state buffer (:119); prev_out (in*nb) nullable
+ * receives x[B-1] broadcast over the bases, written by a second launch on the same stream (may
+ * alias prev). */
+int fetode_hlogistic_mixer_forward(const fetode_hlogistic_t* layer, const float* x, int64_t B, const float* prev,
+                                   int32_t act_sigmoid, const float* w, const float* bias, int32_t n_out,
+                                   float* phi, float* out, float* branch, float* prev_out, void* stream);
+/* Workspace bytes of fetode_hlogistic_mixer_backward (the head's input gradient). */
+int64_t fetode_hlogistic_mixer_backward_workspace(const fetode_hlogistic_t* layer, int64_t B);
+/* VJP of the mixer (+ head).  x, prev, phi, w: as in (and produced by) the forward being
+ * differentiated; g (B, n_out) with a head, else (B, in*nb).  Outputs (nullable, written):
+ * gx (B, in), gw (n_out, in*nb), gbias_head (n_out), gk/gEc/gPs/gbias (in, nb).  Batch reductions
+ * in a fixed order (no atomics). */
+int fetode_hlogistic_mixer_backward(const fetode_hlogistic_t* layer, const float* x, int64_t B, const float* prev,
+                                    int32_t act_sigmoid, const float* phi, const float* w, int32_t n_out,
+                                    const float* g, float* gx, float* gw, float* gbias_head, float* gk, float* gEc,
+                                    float* gPs, float* gbias, void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
