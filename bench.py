@@ -53,6 +53,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-ecg", action="store_true", help="skip the ECG dopri5 (configs[2]) line")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--train-iters", type=int, default=20, help="0 skips the training-rate line")
     return ap.parse_args()
@@ -150,6 +151,49 @@ def train_rate(model, y0d, t, iters, warmup, world):
     return {"value": world * iters * STEPS_PER_SOLVE / el, "unit": "RK4 steps/s trained (fwd+bwd+allreduce+Adam)",
             "ms_per_iter": el / iters * 1e3, "iters": iters,
             "path": "fused: fetode_integrate_fixed with tape + fetode_integrate_fixed_backward (one launch each)"}
+
+
+def ecg_rate(dev, reps=10, cpu_seconds=5.0, with_cpu=True):
+    """BASELINE configs[2] (train_ecg_kan_fet_nn_ode.py:512-572): KanFet_NODE.eval() forward on a
+    batch of 200 synthetic ECG200-shaped series (T = 96; the dataset is not in the image), latent
+    64, 10 bases, dopri5 rtol 1e-3 / atol 1e-4 on [0, 1].  The field (hysteretic mixer + Linear
+    head) is one HIP launch per evaluation; dopri5's accept/reject is host-driven (one scalar
+    read per attempt, as torchdiffeq's `if accept_step`)."""
+    from fet_ode_amd import ecg
+    from oracle import ecg_ref as E
+    torch.manual_seed(0)
+    m = ecg.KanFet_NODE(T=96, num_classes=2, latent_dim=64, num_basis=10, rtol=1e-3, atol=1e-4)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.to(dev).eval()
+    x = E.ecg_x(200, seed=1)
+    xd = x.to(dev)
+    with torch.no_grad():
+        for _ in range(2):
+            m(xd)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            m(xd)
+        torch.cuda.synchronize(dev)
+        el = (time.perf_counter() - t0) / reps
+    s = m.last_solve
+    out = {"value": 1.0 / el, "unit": "KanFet_NODE forward solves/s (B=200, dopri5)", "ms_per_solve": el * 1e3,
+           "nfev": s.nfev, "attempts": len(s.attempts), "field_evals_per_s": s.nfev / el,
+           "workload": "KanFet_NODE(T=96, 2 classes, latent 64, nb 10), dopri5 rtol 1e-3 atol 1e-4, t=[0,1], "
+                       "B=200 synthetic series, eval mode"}
+    if with_cpu:
+        cores = min(16, os.cpu_count() or 1)
+        torch.set_num_threads(cores)
+        n, t0 = 0, time.perf_counter()
+        with torch.no_grad():
+            while n < 1 or (time.perf_counter() - t0 < cpu_seconds and n < 20):
+                E.ECGNodeRef({k: v.clone() for k, v in sd.items()}, rtol=1e-3, atol=1e-4)(x)
+                n += 1
+        cel = (time.perf_counter() - t0) / n
+        out["cpu_baseline"] = {"value": 1.0 / cel, "unit": out["unit"], "cores": cores, "kind": "port",
+                               "sample": f"{n} full forward(s) of the same workload with oracle/ecg_ref.py "
+                                         f"(reference op order, torch CPU fp32), {cel * n:.1f} s"}
+    return out
 
 
 def cpu_baseline(sd, y0, t, seconds):
@@ -268,6 +312,8 @@ def main():
         }
         if train is not None:
             out["train"] = train
+        if world == 1 and not args.no_ecg:
+            out["ecg"] = ecg_rate(dev, with_cpu=not args.no_cpu_baseline)
         if world == 1 and not args.no_cpu_baseline:
             cb, ref_sol = cpu_baseline(sd, y0, t, args.cpu_seconds)
             out["cpu_baseline"] = cb
