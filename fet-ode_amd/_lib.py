@@ -109,6 +109,11 @@ SIGNATURES = {
                                                       ctypes.c_int32, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp,
                                                       _vp, _vp]),
     "fetode_hlogistic_mixer_backward_workspace": (ctypes.c_int64, [ctypes.POINTER(HLogisticDesc), ctypes.c_int64]),
+    "fetode_ecg_dopri5": (ctypes.c_int, [ctypes.POINTER(HLogisticDesc), _vp, _vp, ctypes.c_int32, _vp, _vp,
+                                         ctypes.c_int64, _vp, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+                                         ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_float), _vp, _vp,
+                                         _vp, _vp, _vp, _vp, ctypes.c_int32, _vp]),
+    "fetode_ecg_dopri5_workspace": (ctypes.c_int64, [ctypes.c_int64]),
     "fetode_hlogistic_mixer_backward": (ctypes.c_int, [ctypes.POINTER(HLogisticDesc), _vp, ctypes.c_int64, _vp,
                                                        ctypes.c_int32, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp, _vp,
                                                        _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -260,3 +260,365 @@ int fetode_hlogistic_mixer_backward(const fetode_hlogistic_t* layer, const float
 }
 
 }  // extern "C"
+
+// =============================================================================================
+// Device-resident dopri5 for the ECG field: the whole torchdiffeq solve —
+// f0, _select_initial_step, 6 evaluations per attempt (FSAL), the global RMS error norm,
+// accept/reject, _optimal_step_size, _interp_fit / _interp_evaluate — in ONE cooperative launch,
+// with the same fp32/fp64 arithmetic as the host-driven path (dopri5.py + the kernels above).
+//
+// A workgroup owns kDR batch rows and, as a SHADOW row, the batch's last row: the hysteresis
+// memory every evaluation reads is the last row's previous input (:131-132), so each workgroup
+// evaluates that row itself and no evaluation needs data from another workgroup.  Only the
+// error norms (one per attempt, three in the initial-step selection) are global: per-workgroup
+// fp64 partial sums, a grid barrier, and the same fixed-order sum in every workgroup — so every
+// workgroup takes the same accept/reject decisions and the same dt sequence.
+// =============================================================================================
+namespace {
+
+constexpr int kDR = 3;                 // real rows per workgroup (+1 shadow)
+constexpr int kDT = 64 * (kDR + 1);    // one thread per (row, state dim): state dim <= 64
+
+struct DopriTab {
+  float beta[6][6];  // torchdiffeq Dopri5 tableau rounded to fp32 (tableau.to(y0.dtype))
+  float cerr[7];
+  float cmid[7];
+};
+
+struct EcgDopriArgs {
+  HL L;
+  const float* wT;  // (F, D) head weight, transposed
+  const float* bh;  // (D) head bias, nullable
+  int D, F;
+  const float* prev0;  // (F) prev_x before the solve
+  const float* y0;     // (B, D)
+  int64_t B;
+  const double* t;  // (T) strictly increasing
+  int T;
+  float rtol, atol;
+  double first_step;  // > 0: options["first_step"]; else _select_initial_step
+  double safety, ifactor, dfactor, min_step, max_step;
+  int max_steps;
+  DopriTab tab;
+  float* sol;         // (T, B, D)
+  float* prev_out;    // (F)
+  float* branch_out;  // (B, F) nullable: branch_state of the last evaluation
+  double* part;       // (2, gridDim.x, 2) double-buffered partial sums
+  unsigned* bar;      // 2 words, zeroed: arrival count, generation
+  int* stats;         // [nfev, attempts, status]
+  double* att;        // (max_att, 4): t0, dt, error ratio, accepted
+  int max_att;
+};
+
+__device__ void grid_barrier(unsigned* bar, unsigned nblk) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned* count = bar;
+    unsigned* gen = bar + 1;
+    const unsigned g = __hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned old = __hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == nblk - 1) {
+      __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ float fast_sigmoid(float z) { return rcp(1.0f + ex2(-z * FETODE_LOG2E)); }
+
+// misc._rms_norm over the WHOLE batch of sum_v (per-thread fp64 squares, real elements only):
+// workgroup tree -> partial slot -> grid barrier -> the same fixed-order sum in every workgroup
+struct GlobalNorm {
+  double* red;  // LDS, kDT doubles
+  int* bad_lds;
+  double* tot;  // LDS, 2 doubles
+  __device__ void run(const EcgDopriArgs& a, double v, int bad, int phase, int nvals, double* out_sum, int* out_bad) {
+    const int tid = threadIdx.x;
+    red[tid] = v;
+    if (tid == 0) *bad_lds = 0;
+    __syncthreads();
+    if (bad) atomicOr(bad_lds, 1);
+    for (int w = kDT / 2; w > 0; w >>= 1) {
+      if (tid < w) red[tid] += red[tid + w];
+      __syncthreads();
+    }
+    double* slot = a.part + ((int64_t)(phase & 1) * gridDim.x + blockIdx.x) * 2;
+    if (tid == 0) {
+      __hip_atomic_store(&slot[0], red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&slot[1], (double)*bad_lds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    grid_barrier(a.bar, gridDim.x);
+    double s = 0.0, fb = 0.0;
+    for (int g = tid; g < (int)gridDim.x; g += kDT) {
+      const double* o = a.part + ((int64_t)(phase & 1) * gridDim.x + g) * 2;
+      s += __hip_atomic_load(&o[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      fb += __hip_atomic_load(&o[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    red[tid] = s;
+    __syncthreads();
+    for (int w = kDT / 2; w > 0; w >>= 1) {
+      if (tid < w) red[tid] += red[tid + w];
+      __syncthreads();
+    }
+    if (tid == 0) tot[0] = red[0];
+    red[tid] = fb;
+    __syncthreads();
+    for (int w = kDT / 2; w > 0; w >>= 1) {
+      if (tid < w) red[tid] += red[tid + w];
+      __syncthreads();
+    }
+    if (tid == 0) tot[1] = red[0];
+    __syncthreads();
+    *out_sum = tot[0];
+    *out_bad = tot[1] != 0.0;
+    (void)nvals;
+  }
+};
+
+__global__ __launch_bounds__(kDT) void ecg_dopri5_kernel(EcgDopriArgs a) {
+  extern __shared__ float s_dyn[];  // phi (kDR+1) * F | prev F | prevold F
+  __shared__ float xs[kDR + 1][64];
+  __shared__ double red[kDT];
+  __shared__ double tot[2];
+  __shared__ int bad_lds;
+  const int tid = threadIdx.x, r = tid / 64, d = tid % 64;
+  const int D = a.D, F = a.F, nb = a.L.nb;
+  float* phi = s_dyn;
+  float* prev = phi + (kDR + 1) * F;
+  float* prevold = prev + F;
+  const bool dval = d < D;
+  int64_t b = r < kDR ? (int64_t)blockIdx.x * kDR + r : a.B - 1;  // row kDR: the shadow last row
+  const bool real = r < kDR && b < a.B && dval;
+  if (b >= a.B) b = a.B - 1;  // padding rows mirror the last row; never stored or counted
+  const int64_t BD = a.B * D;
+  const double n_el = (double)BD;
+  GlobalNorm gn{red, &bad_lds, tot};
+  int phase = 0, nfev = 0, status = 0, n_att = 0;
+
+  for (int q = tid; q < F; q += kDT) prev[q] = a.prev0[q];
+  __syncthreads();
+
+  // one field evaluation of this thread's element; all threads of the workgroup take part
+  auto eval = [&](float xv) -> float {
+    if (dval) xs[r][d] = xv;
+    __syncthreads();
+    for (int idx = tid; idx < (kDR + 1) * F; idx += kDT) {
+      const int r2 = idx / F, q = idx - r2 * F, i = q / nb;
+      const float x = xs[r2][i];
+      const float kq = a.L.k[q], Ec = a.L.Ec[q], Ps = a.L.Ps[q];
+      const float su = fast_sigmoid(kq * (x - Ec)), sd = fast_sigmoid(kq * (x + Ec));
+      const float up = Ps * su * 2.0f - Ps, down = Ps * sd * 2.0f - Ps;
+      const float bs = ref_sigmoid(a.L.gs * (x - prev[q])) > a.L.bp ? 1.0f : 0.0f;
+      phi[idx] = fast_sigmoid(bs * up + (1.0f - bs) * down + a.L.bias[q]);
+    }
+    __syncthreads();
+    for (int q = tid; q < F; q += kDT) {  // :131-132, the shadow row's input
+      prevold[q] = prev[q];
+      prev[q] = xs[kDR][q / nb];
+    }
+    float acc = 0.f;
+    if (dval) {
+      const float* ph = phi + r * F;
+      for (int q = 0; q < F; ++q) acc = __builtin_fmaf(ph[q], a.wT[(int64_t)q * D + d], acc);
+      acc += a.bh ? a.bh[d] : 0.f;
+    }
+    __syncthreads();
+    ++nfev;
+    return acc;
+  };
+
+  float y = dval ? a.y0[b * D + d] : 0.f;
+  if (real) a.sol[b * D + d] = y;
+  float f0 = eval(y);
+  double dt;
+  if (a.first_step > 0.0) {
+    dt = a.first_step;
+  } else {  // misc._select_initial_step in fp32 (dopri5.py select_initial_step)
+    const float scale = a.atol + a.rtol * fabsf(y);
+    double s;
+    int bad;
+    const float q0 = y / scale, q1 = f0 / scale;
+    gn.run(a, real ? (double)q0 * q0 : 0.0, 0, phase++, 0, &s, &bad);
+    const float d0 = fabsf(sqrtf((float)(s / n_el)));
+    gn.run(a, real ? (double)q1 * q1 : 0.0, 0, phase++, 0, &s, &bad);
+    const float d1 = fabsf(sqrtf((float)(s / n_el)));
+    float h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : (0.01f * d0) / d1;
+    h0 = fabsf(h0);
+    const float f1 = eval(y + f0 * h0);
+    const float q2 = (f1 - f0) / scale;
+    gn.run(a, real ? (double)q2 * q2 : 0.0, 0, phase++, 0, &s, &bad);
+    const float d2 = fabsf(sqrtf((float)(s / n_el)) / h0);
+    float h1;
+    if (d1 <= 1e-15f && d2 <= 1e-15f) h1 = fmaxf(1e-6f, h0 * 1e-3f);
+    else h1 = powf(0.01f / fmaxf(d1, d2), 0.2f);
+    dt = (double)fminf(100.0f * h0, fabsf(h1));
+  }
+
+  float co[5] = {y, 0.f, 0.f, 0.f, 0.f};
+  double t0s = a.t[0], t1s = a.t[0];
+  for (int i = 1; i < a.T && status == 0; ++i) {
+    const double next_t = a.t[i];
+    int n_steps = 0;
+    while (next_t > t1s) {
+      if (n_steps >= a.max_steps) { status = 3; break; }
+      const double t0 = t1s;
+      if (!(t0 + dt > t0)) { status = 2; break; }
+      const float dt32 = (float)dt;
+      const double t1 = t0 + dt;
+      float k[7];
+      k[0] = f0;
+      float yi = y;
+#pragma unroll
+      for (int s = 0; s < 6; ++s) {  // rk_common._runge_kutta_step via fetode_lincomb's op order
+        float acc = k[0] * (a.tab.beta[s][0] * dt32);
+#pragma unroll
+        for (int j = 1; j <= s; ++j) acc = acc + k[j] * (a.tab.beta[s][j] * dt32);
+        yi = y + acc;
+        k[s + 1] = eval(yi);
+      }
+      const float y1 = yi;
+      float err = k[0] * (a.tab.cerr[0] * dt32);
+#pragma unroll
+      for (int j = 1; j < 7; ++j) err = err + k[j] * (a.tab.cerr[j] * dt32);
+      const float tol = a.atol + a.rtol * fmaxf(fabsf(y), fabsf(y1));
+      const float qe = err / tol;
+      double s;
+      int bad;
+      gn.run(a, real ? (double)qe * qe : 0.0, real && !__builtin_isfinite(y), phase++, 0, &s, &bad);
+      if (bad) { status = 1; break; }
+      const float ratio = sqrtf((float)(s / n_el));
+      const bool accept = ratio <= 1.0f;
+      if (blockIdx.x == 0 && tid == 0 && n_att < a.max_att) {
+        double* o = a.att + (int64_t)n_att * 4;
+        o[0] = t0;
+        o[1] = dt;
+        o[2] = (double)ratio;
+        o[3] = accept ? 1.0 : 0.0;
+      }
+      ++n_att;
+      if (accept) {  // interp._interp_fit (fetode_interp_fit's op order)
+        float acc = k[0] * (a.tab.cmid[0] * dt32);
+#pragma unroll
+        for (int j = 1; j < 7; ++j) acc = acc + k[j] * (a.tab.cmid[j] * dt32);
+        const float ym = y + acc, fa = k[0], fb = k[6];
+        co[4] = ((2.0f * dt32) * (fb - fa) - 8.0f * (y1 + y)) + 16.0f * ym;
+        co[3] = ((dt32 * (5.0f * fa - 3.0f * fb) + 18.0f * y) + 14.0f * y1) - 32.0f * ym;
+        co[2] = ((dt32 * (fb - 4.0f * fa) - 11.0f * y) - 5.0f * y1) + 16.0f * ym;
+        co[1] = dt32 * fa;
+        co[0] = y;
+        y = y1;
+        f0 = k[6];
+        t0s = t0;
+        t1s = t1;
+      } else {
+        t0s = t0;
+      }
+      // rk_common._optimal_step_size in fp64 (dopri5.py optimal_step)
+      const double rr = (double)ratio;
+      double nxt;
+      if (rr == 0.0) {
+        nxt = dt * a.ifactor;
+      } else {
+        const double dfac = rr < 1.0 ? 1.0 : a.dfactor;
+        const double factor = __builtin_isnan(rr) ? rr : fmin(a.ifactor, fmax(a.safety / pow(rr, 1.0 / 5.0), dfac));
+        nxt = dt * factor;
+      }
+      dt = __builtin_isnan(nxt) ? nxt : fmin(fmax(nxt, a.min_step), a.max_step);
+      ++n_steps;
+    }
+    if (status) break;
+    const float x = (float)((next_t - t0s) / (t1s - t0s));  // interp._interp_evaluate
+    float total = co[0] + x * co[1];
+    float xp = x;
+#pragma unroll
+    for (int j = 2; j < 5; ++j) {
+      xp = xp * x;
+      total = total + xp * co[j];
+    }
+    if (real) a.sol[(int64_t)i * BD + b * D + d] = total;
+  }
+  // module state after the solve: prev_x = the last evaluation's last-row input; branch_state of
+  // that evaluation for this workgroup's rows
+  if (blockIdx.x == 0)
+    for (int q = tid; q < F; q += kDT) a.prev_out[q] = prev[q];
+  if (a.branch_out) {
+    for (int idx = tid; idx < kDR * F; idx += kDT) {
+      const int r2 = idx / F, q = idx - r2 * F;
+      const int64_t b2 = (int64_t)blockIdx.x * kDR + r2;
+      if (b2 < a.B)
+        a.branch_out[b2 * F + q] = ref_sigmoid(a.L.gs * (xs[r2][q / nb] - prevold[q])) > a.L.bp ? 1.0f : 0.0f;
+    }
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    a.stats[0] = nfev;
+    a.stats[1] = n_att;
+    a.stats[2] = status;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int fetode_ecg_dopri5(const fetode_hlogistic_t* layer, const float* wT, const float* bias, int32_t D,
+                      const float* prev, const float* y0, int64_t B, const double* t, int32_t T, double rtol,
+                      double atol, const double* opts, const float* tableau, float* solution, float* prev_out,
+                      float* branch_out, void* workspace, int32_t* stats, double* attempts, int32_t max_attempts,
+                      void* stream) {
+  int rc = check_layer(layer);
+  if (rc) return rc;
+  if (B <= 0 || T <= 0) return FETODE_OK;
+  if (!wT || !prev || !y0 || !t || !opts || !tableau || !solution || !prev_out || !workspace || !stats)
+    return set_err(FETODE_EINVAL, "ecg dopri5: null pointer");
+  if (D != layer->in_dim || D > 64) return set_err(FETODE_EINVAL, "ecg dopri5: state dim %d (must equal in_dim, <= 64)", D);
+  EcgDopriArgs a;
+  memset(&a, 0, sizeof(a));
+  a.L = to_dev(layer);
+  a.wT = wT;
+  a.bh = bias;
+  a.D = D;
+  a.F = a.L.in * a.L.nb;
+  a.prev0 = prev;
+  a.y0 = y0;
+  a.B = B;
+  a.t = t;
+  a.T = T;
+  a.rtol = (float)rtol;
+  a.atol = (float)atol;
+  a.first_step = opts[0];
+  a.safety = opts[1];
+  a.ifactor = opts[2];
+  a.dfactor = opts[3];
+  a.min_step = opts[4];
+  a.max_step = opts[5];
+  a.max_steps = opts[6] > 2e9 ? 2000000000 : (int)opts[6];
+  memcpy(&a.tab, tableau, sizeof(DopriTab));
+  a.sol = solution;
+  a.prev_out = prev_out;
+  a.branch_out = branch_out;
+  const int64_t grid = (B + kDR - 1) / kDR;
+  if (grid > 1024) return set_err(FETODE_EUNSUPPORTED, "ecg dopri5: batch %lld too large for one cooperative grid", (long long)B);
+  a.bar = (unsigned*)workspace;
+  a.part = (double*)((char*)workspace + 64);
+  a.stats = stats;
+  a.att = attempts;
+  a.max_att = attempts ? max_attempts : 0;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_CHECK_RET(hipMemsetAsync(workspace, 0, 64, s));
+  const size_t lds = sizeof(float) * ((kDR + 1) * a.F + 2 * a.F);
+  if (lds > 48 * 1024) return set_err(FETODE_EINVAL, "ecg dopri5: in*num_basis=%d too large", a.F);
+  void* args[] = {&a};
+  HIP_CHECK_RET(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(ecg_dopri5_kernel), dim3((unsigned)grid),
+                                           dim3(kDT), args, (unsigned)lds, s));
+  return FETODE_OK;
+}
+
+int64_t fetode_ecg_dopri5_workspace(int64_t B) {
+  const int64_t grid = (B + kDR - 1) / kDR;
+  return 64 + (int64_t)sizeof(double) * 2 * 2 * grid;
+}
+
+}  // extern "C"

@@ -219,7 +219,114 @@ class _Dopri5:
         return min(max(nxt, self.min_step), self.max_step) if not math.isnan(nxt) else nxt
 
 
+_TABLEAU = np.concatenate([np.concatenate([b, np.zeros(6 - len(b), np.float32)]) for b in BETA32]
+                          + [CERR32, CMID32]).astype(np.float32)
+_RESIDENT_OPTS = {"first_step", "safety", "ifactor", "dfactor", "min_step", "max_step", "max_num_steps"}
+_MAX_TRACE = 4096
+
+
+class ResidentSolve:
+    """nfev / attempts of a device-resident solve, read back from the device lazily."""
+
+    def __init__(self, stats, attempts):
+        self._stats, self._att = stats, attempts
+        self._host = None
+
+    def _load(self):
+        if self._host is None:
+            st = self._stats.tolist()
+            n = min(st[1], _MAX_TRACE)
+            att = [(a[0], a[1], a[2], bool(a[3])) for a in self._att[:n].tolist()]
+            self._host = (st[0], att, st[2])
+        return self._host
+
+    @property
+    def nfev(self):
+        return self._load()[0]
+
+    @property
+    def attempts(self):
+        return self._load()[1]
+
+
+def _try_ecg_resident(func, y0, tp, reversed_, rtol, atol, options):
+    """The whole solve in one launch when `func` is the ECG field (No_MLP_KANODEFunc with the
+    sigmoid mixer), nothing needs gradients, and the options are the scalar ones."""
+    from .ecg import No_MLP_KANODEFunc
+    import torch.nn as nn
+    if not isinstance(func, No_MLP_KANODEFunc) or reversed_ or y0.dim() != 2:
+        return None
+    if not isinstance(func.feat.act, nn.Sigmoid) or set(options) - _RESIDENT_OPTS:
+        return None
+    if not (isinstance(rtol, (int, float)) and isinstance(atol, (int, float))):
+        return None
+    basis = func.feat.basis
+    B, D = y0.shape
+    if D != basis.in_dim or D > 64 or B > 3072 or func.proj.out_features != D or basis.use_noise:
+        return None
+    if torch.is_grad_enabled() and (y0.requires_grad or any(p.requires_grad for p in func.parameters())):
+        return None
+    lib = _lib.load()
+    dev = y0.device
+    keep = []
+    d = basis.desc(keep)
+    w = func.proj.weight
+    key = (w.data_ptr(), w._version)
+    cached = getattr(func, "_fetode_wT", None)
+    if cached is None or cached[0] != key:
+        cached = (key, w.detach().t().contiguous().float())
+        func._fetode_wT = cached
+    wT = cached[1]
+    bias = _lib.f32c(func.proj.bias) if func.proj.bias is not None else None
+    prev = basis._prev_for(dev)
+    yc = _lib.f32c(y0)
+    t_dev = tp.to(torch.float64).to(dev)
+    T = t_dev.numel()
+    sol = torch.empty(T, B, D, device=dev, dtype=torch.float32)
+    prev_out = torch.empty_like(prev)
+    branch = torch.empty(B, basis.in_dim, basis.num_basis, device=dev, dtype=torch.float32)
+    ws = torch.empty(max(1, lib.fetode_ecg_dopri5_workspace(B) // 4), device=dev, dtype=torch.float32)
+    stats = torch.zeros(3, device=dev, dtype=torch.int32)
+    att = torch.empty(_MAX_TRACE, 4, device=dev, dtype=torch.float64)
+    fs = options.get("first_step")
+    opts = np.array([float(fs) if fs is not None else 0.0, float(options.get("safety", 0.9)),
+                     float(options.get("ifactor", 10.0)), float(options.get("dfactor", 0.2)),
+                     float(options.get("min_step", 0.0)), float(options.get("max_step", math.inf)),
+                     float(options.get("max_num_steps", 2 ** 31 - 1))], dtype=np.float64)
+    _lib.check(lib.fetode_ecg_dopri5(
+        _lib.ctypes.byref(d), wT.data_ptr(), _lib.ptr(bias), D, prev.data_ptr(), yc.data_ptr(), B, t_dev.data_ptr(),
+        T, float(rtol), float(atol), opts.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_double)),
+        _TABLEAU.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_float)), sol.data_ptr(), prev_out.data_ptr(),
+        branch.data_ptr(), ws.data_ptr(), stats.data_ptr(), att.data_ptr(), _MAX_TRACE,
+        _lib.stream_handle(dev)), "fetode_ecg_dopri5")
+    prev.copy_(prev_out)
+    basis.branch_state = branch
+    status = int(stats[2].item())   # one read per solve: torchdiffeq's assertions
+    if status == 1:
+        raise AssertionError("non-finite values in state `y`")
+    if status == 2:
+        raise AssertionError("underflow in dt")
+    if status == 3:
+        raise AssertionError("max_num_steps exceeded")
+    dopri5_solve.last = ResidentSolve(stats, att)
+    return sol
+
+
+_RESIDENT = True
+
+
+def set_resident_dopri5(enabled: bool) -> bool:
+    """Device-resident dopri5 for fields that have one (default) or the host-driven loop."""
+    global _RESIDENT
+    prev, _RESIDENT = _RESIDENT, bool(enabled)
+    return prev
+
+
 def dopri5_solve(func, y0, tc, tp, reversed_, rtol, atol, options):
+    if _RESIDENT:
+        sol = _try_ecg_resident(func, y0, tp, reversed_, rtol, atol, options)
+        if sol is not None:
+            return sol
     solver = _Dopri5(func, y0, rtol, atol, options, reversed_)
     sol = solver.integrate(tp)
     dopri5_solve.last = solver   # exposes nfev / attempts for tests and tooling

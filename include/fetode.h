@@ -257,6 +257,29 @@ int fetode_hlogistic_mixer_backward(const fetode_hlogistic_t* layer, const float
                                     const float* g, float* gx, float* gw, float* gbias_head, float* gk, float* gEc,
                                     float* gPs, float* gbias, void* workspace, void* stream);
 
+/* The whole dopri5 solve of dh/dt = No_MLP_KANODEFunc(h) (train_ecg_kan_fet_nn_ode.py:558-565 with
+ * the field :483-509) in ONE cooperative launch: f0, misc._select_initial_step (unless
+ * opts[0] = first_step > 0), 6 evaluations per attempt incl. rejected ones (the hysteresis memory
+ * sees every call, :131-132), the global RMS error norm, accept/reject, _optimal_step_size,
+ * _interp_fit/_interp_evaluate at every output time — the arithmetic of the host-driven path
+ * (fetode_lincomb / fetode_scaled_rms / fetode_interp_*) on the device.
+ *   layer/wT (in*nb, D) transposed head weight /bias (D, nullable), D = in_dim <= 64;
+ *   prev (in*nb) prev_x before the solve; y0 (B, D); t (dev, fp64, T) strictly increasing;
+ *   opts (host, 7 doubles): first_step (<= 0: select), safety, ifactor, dfactor, min_step,
+ *   max_step, max_num_steps; tableau (host, 50 floats): beta[6][6], c_err[7], c_mid[7] in fp32;
+ *   solution (T, B, D); prev_out (in*nb, must not alias prev) = prev_x after the solve;
+ *   branch_out (B, in*nb, nullable) = branch_state of the last evaluation;
+ *   workspace: fetode_ecg_dopri5_workspace(B) bytes; stats (dev, 3 ints) = nfev, attempts,
+ *   status (0 ok, 1 non-finite state, 2 dt underflow, 3 max_num_steps);
+ *   attempts (dev, nullable) (max_attempts, 4) doubles: t0, dt, error ratio, accepted.
+ * FETODE_EUNSUPPORTED when B needs more than one cooperative grid (B > 3072). */
+int fetode_ecg_dopri5(const fetode_hlogistic_t* layer, const float* wT, const float* bias, int32_t D,
+                      const float* prev, const float* y0, int64_t B, const double* t, int32_t T, double rtol,
+                      double atol, const double* opts, const float* tableau, float* solution, float* prev_out,
+                      float* branch_out, void* workspace, int32_t* stats, double* attempts, int32_t max_attempts,
+                      void* stream);
+int64_t fetode_ecg_dopri5_workspace(int64_t B);
+
 #ifdef __cplusplus
 }
 #endif

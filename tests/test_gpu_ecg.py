@@ -150,3 +150,58 @@ def test_training_through_fixed_grid(dev):
         close(p.grad, ps[n].grad, 1e-4, n)
     with pytest.raises(NotImplementedError):
         F.odeint(f, hg, t, method="dopri5").sum().backward()
+
+
+@pytest.mark.parametrize("B,latent,nb,opts", [(200, 64, 10, None), (37, 64, 10, {"first_step": 0.05}),
+                                             (16, 1, 12, None), (3, 5, 4, {"first_step": 0.3})])
+def test_resident_dopri5_matches_host_driven(dev, B, latent, nb, opts):
+    """The one-launch device-resident dopri5 (fetode_ecg_dopri5) against the host-driven dopri5
+    (HIP field kernel per call, host accept/reject): identical attempt sequence and nfev, solution
+    and the module state it leaves (prev_x, branch_state) equal to fp32 rounding."""
+    import fet_ode_amd as F
+    from fet_ode_amd import dopri5 as D5
+    from fet_ode_amd import ecg
+    from oracle import ecg_ref as E
+    torch.manual_seed(B + latent)
+    f = ecg.No_MLP_KANODEFunc(latent_dim=latent, num_basis=nb)
+    sd = {k: v.clone() for k, v in f.state_dict().items()}
+    h0 = (torch.randn(B, latent, generator=torch.Generator().manual_seed(9)) * 2).to(dev)
+    t = torch.tensor([0.0, 0.3, 1.0], dtype=torch.float64)
+    out = {}
+    for resident in (True, False):
+        m = ecg.No_MLP_KANODEFunc(latent_dim=latent, num_basis=nb)
+        m.load_state_dict(sd)
+        m = m.to(dev)
+        prev = D5.set_resident_dopri5(resident)
+        try:
+            with torch.no_grad():
+                sol = F.odeint(m, h0, t, method="dopri5", rtol=1e-3, atol=1e-4, options=opts)
+        finally:
+            D5.set_resident_dopri5(prev)
+        last = D5.dopri5_solve.last
+        assert isinstance(last, D5.ResidentSolve) == resident
+        out[resident] = (sol.cpu(), last.nfev, last.attempts, m.feat.basis.prev_x.cpu(),
+                         m.feat.basis.branch_state.cpu())
+    (s1, n1, a1, p1, b1), (s2, n2, a2, p2, b2) = out[True], out[False]
+    assert n1 == n2 and len(a1) == len(a2)
+    assert [a[3] for a in a1] == [a[3] for a in a2]
+    np.testing.assert_allclose([a[1] for a in a1], [a[1] for a in a2], rtol=1e-5)
+    close(s1, s2, 1e-5, "solution")
+    close(p1, p2, 1e-5, "prev_x")
+    assert (b1 != b2).float().mean().item() < 1e-3   # branch flips only where dx rounds across 0
+    # and against the CPU oracle
+    ref = E.ECGFieldRef.from_state_dict(sd)
+    from oracle import torch_ref as O
+    se = O.odeint(ref, h0.cpu(), t, method="dopri5", rtol=1e-3, atol=1e-4, options=opts)
+    close(s1, se, 1e-5, "solution vs oracle")
+
+
+def test_resident_dopri5_nonfinite_raises(dev):
+    import fet_ode_amd as F
+    from fet_ode_amd import ecg
+    torch.manual_seed(1)
+    m = ecg.No_MLP_KANODEFunc(latent_dim=8, num_basis=4).to(dev)
+    h0 = torch.randn(6, 8, device=dev)
+    h0[3, 2] = float("nan")
+    with torch.no_grad(), pytest.raises(AssertionError):
+        F.odeint(m, h0, torch.tensor([0.0, 1.0]), method="dopri5", options={"first_step": 0.1})
