@@ -13,6 +13,7 @@
 // and the parameter gradients reduced over the batch by one thread per parameter in a fixed order
 // (no atomics, run-to-run identical).  branch_state is a comparison: no gradient flows through it,
 // nor through the detached prev_x (:119-132).
+#include <algorithm>
 #include <cstring>
 
 #include "fetode_common.h"
@@ -31,6 +32,13 @@ struct HL {  // device copy of fetode_hlogistic_t
 };
 
 __device__ __forceinline__ float ref_sigmoid(float z) { return 1.0f / (1.0f + expf(-z)); }
+
+// The head's fp32 summation order, shared by every kernel that evaluates it: q in [0, F) splits
+// into kHeadParts consecutive parts of head_part(F) (a multiple of 4) indices; each part is an FMA
+// chain from 0 in increasing q, and the parts add left to right.  The resident dopri5 gives each
+// part to its own wave.
+constexpr int kHeadParts = 8;
+__host__ __device__ __forceinline__ int head_part(int F) { return (((F + 3) & ~3) + 4 * kHeadParts - 1) / (4 * kHeadParts) * 4; }
 
 // the reference's up / down / gate for element (i, j) at input x (train_ecg_kan_fet_nn_ode.py:110-121)
 struct HPoint {
@@ -73,9 +81,15 @@ __global__ __launch_bounds__(kThreads) void mixer_fwd_kernel(HL L, const float* 
     const int r = t / n_out, o = t % n_out;
     const float* wr = w + (int64_t)o * F;
     const float* ph = s_phi + r * F;
-    float acc = 0.f;
-    for (int q = 0; q < F; ++q) acc = __builtin_fmaf(ph[q], wr[q], acc);
-    out[(b0 + r) * n_out + o] = acc + (bvec ? bvec[o] : 0.f);
+    const int PS = head_part(F);
+    float tot = 0.f;
+    for (int p = 0; p < kHeadParts; ++p) {
+      float acc = 0.f;
+      const int q1 = min(F, (p + 1) * PS);
+      for (int q = p * PS; q < q1; ++q) acc = __builtin_fmaf(ph[q], wr[q], acc);
+      tot = p == 0 ? acc : tot + acc;
+    }
+    out[(b0 + r) * n_out + o] = tot + (bvec ? bvec[o] : 0.f);
   }
 }
 
@@ -267,17 +281,24 @@ int fetode_hlogistic_mixer_backward(const fetode_hlogistic_t* layer, const float
 // accept/reject, _optimal_step_size, _interp_fit / _interp_evaluate — in ONE cooperative launch,
 // with the same fp32/fp64 arithmetic as the host-driven path (dopri5.py + the kernels above).
 //
-// A workgroup owns kDR batch rows and, as a SHADOW row, the batch's last row: the hysteresis
+// A workgroup owns R-1 batch rows and, as a SHADOW row, the batch's last row: the hysteresis
 // memory every evaluation reads is the last row's previous input (:131-132), so each workgroup
 // evaluates that row itself and no evaluation needs data from another workgroup.  Only the
 // error norms (one per attempt, three in the initial-step selection) are global: per-workgroup
 // fp64 partial sums, a grid barrier, and the same fixed-order sum in every workgroup — so every
 // workgroup takes the same accept/reject decisions and the same dt sequence.
+//
+// Everything an evaluation reads stays on chip for the whole solve.  The head weight W^T (F x D,
+// 160 KB at latent 64) is split: its first QL rows sit in LDS as float4 groups [q/4][d] (all the
+// LDS phi leaves), the remaining <= kTail rows in registers of the threads that own output d.
+// The head is then one fp32 FMA chain over q per (row, output) — the mixer kernel's order — fed
+// by ds_read_b128 instead of L2 round trips.  The feature parameters (k, Ec, Ps, bias) and the
+// hysteresis memory prev_x live in registers of the thread that owns input-basis index q.
 // =============================================================================================
 namespace {
 
-constexpr int kDR = 3;                 // real rows per workgroup (+1 shadow)
-constexpr int kDT = 64 * (kDR + 1);    // one thread per (row, state dim): state dim <= 64
+constexpr int kMaxF = 768;          // in * num_basis (in <= 64, num_basis <= 12)
+constexpr int kLdsBytes = 163840;   // gfx950: one workgroup may declare all 160 KiB
 
 struct DopriTab {
   float beta[6][6];  // torchdiffeq Dopri5 tableau rounded to fp32 (tableau.to(y0.dtype))
@@ -290,6 +311,9 @@ struct EcgDopriArgs {
   const float* wT;  // (F, D) head weight, transposed
   const float* bh;  // (D) head bias, nullable
   int D, F;
+  int Fp;              // F rounded up to 4 (phi rows are zero-padded)
+  int PS;              // head_part(F): q indices per head part
+  int QL;              // head-weight rows per part kept in LDS (multiple of 4); the rest in registers
   const float* prev0;  // (F) prev_x before the solve
   const float* y0;     // (B, D)
   int64_t B;
@@ -327,107 +351,189 @@ __device__ void grid_barrier(unsigned* bar, unsigned nblk) {
   __syncthreads();
 }
 
-__device__ __forceinline__ float fast_sigmoid(float z) { return rcp(1.0f + ex2(-z * FETODE_LOG2E)); }
-
-// misc._rms_norm over the WHOLE batch of sum_v (per-thread fp64 squares, real elements only):
-// workgroup tree -> partial slot -> grid barrier -> the same fixed-order sum in every workgroup
-struct GlobalNorm {
-  double* red;  // LDS, kDT doubles
-  int* bad_lds;
-  double* tot;  // LDS, 2 doubles
-  __device__ void run(const EcgDopriArgs& a, double v, int bad, int phase, int nvals, double* out_sum, int* out_bad) {
-    const int tid = threadIdx.x;
-    red[tid] = v;
-    if (tid == 0) *bad_lds = 0;
-    __syncthreads();
-    if (bad) atomicOr(bad_lds, 1);
-    for (int w = kDT / 2; w > 0; w >>= 1) {
-      if (tid < w) red[tid] += red[tid + w];
-      __syncthreads();
-    }
-    double* slot = a.part + ((int64_t)(phase & 1) * gridDim.x + blockIdx.x) * 2;
-    if (tid == 0) {
-      __hip_atomic_store(&slot[0], red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&slot[1], (double)*bad_lds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    grid_barrier(a.bar, gridDim.x);
-    double s = 0.0, fb = 0.0;
-    for (int g = tid; g < (int)gridDim.x; g += kDT) {
-      const double* o = a.part + ((int64_t)(phase & 1) * gridDim.x + g) * 2;
-      s += __hip_atomic_load(&o[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      fb += __hip_atomic_load(&o[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    red[tid] = s;
-    __syncthreads();
-    for (int w = kDT / 2; w > 0; w >>= 1) {
-      if (tid < w) red[tid] += red[tid + w];
-      __syncthreads();
-    }
-    if (tid == 0) tot[0] = red[0];
-    red[tid] = fb;
-    __syncthreads();
-    for (int w = kDT / 2; w > 0; w >>= 1) {
-      if (tid < w) red[tid] += red[tid + w];
-      __syncthreads();
-    }
-    if (tid == 0) tot[1] = red[0];
-    __syncthreads();
-    *out_sum = tot[0];
-    *out_bad = tot[1] != 0.0;
-    (void)nvals;
-  }
-};
-
-__global__ __launch_bounds__(kDT) void ecg_dopri5_kernel(EcgDopriArgs a) {
-  extern __shared__ float s_dyn[];  // phi (kDR+1) * F | prev F | prevold F
-  __shared__ float xs[kDR + 1][64];
-  __shared__ double red[kDT];
+// NT = 512 threads, R rows per workgroup (R-1 real + the shadow).  Solver thread (r, d) = tid for
+// tid < 64 R carries state element d of row r.  Head: wave p (of kHeadParts) owns q-part p and
+// forms all R rows' partial sums for output d = lane; W^T rows of the part sit in LDS (the first
+// QLp of each part) and registers (the rest, <= TAIL).  Features: thread tid owns input-basis
+// index q = tid + j * NT for all R rows.
+constexpr int kResThreads = 64 * kHeadParts;
+template <int R, int TAIL>
+__global__ __launch_bounds__(kResThreads) void ecg_dopri5_kernel(EcgDopriArgs a) {
+  constexpr int NT = kResThreads, NR = R - 1, FQ = (kMaxF + NT - 1) / NT;
+  extern __shared__ float4 s_dyn4[];  // W^T [part][QLp/4][D] float4 | phi (R, Fp), later partials
+  __shared__ float xs[R][64];
+  __shared__ double red[NT / 64][2];
   __shared__ double tot[2];
-  __shared__ int bad_lds;
-  const int tid = threadIdx.x, r = tid / 64, d = tid % 64;
-  const int D = a.D, F = a.F, nb = a.L.nb;
-  float* phi = s_dyn;
-  float* prev = phi + (kDR + 1) * F;
-  float* prevold = prev + F;
-  const bool dval = d < D;
-  int64_t b = r < kDR ? (int64_t)blockIdx.x * kDR + r : a.B - 1;  // row kDR: the shadow last row
-  const bool real = r < kDR && b < a.B && dval;
+  const int tid = threadIdx.x, lane = tid % 64, wv = tid / 64;
+  const int r = wv, d = lane;  // solver view (rows r < R)
+  const int D = a.D, F = a.F, Fp = a.Fp, PS = a.PS, QLp = a.QL, G = a.QL / 4;
+  float* phi = reinterpret_cast<float*>(s_dyn4 + (int64_t)kHeadParts * G * D);
+  const bool solver = tid < 64 * R;
+  const bool dval = solver && d < D;
+  int64_t b = r < NR ? (int64_t)blockIdx.x * NR + r : a.B - 1;  // row NR: the shadow last row
+  const bool real = r < NR && b < a.B && dval;
   if (b >= a.B) b = a.B - 1;  // padding rows mirror the last row; never stored or counted
   const int64_t BD = a.B * D;
   const double n_el = (double)BD;
-  GlobalNorm gn{red, &bad_lds, tot};
   int phase = 0, nfev = 0, status = 0, n_att = 0;
 
-  for (int q = tid; q < F; q += kDT) prev[q] = a.prev0[q];
+  // misc._rms_norm numerators over the WHOLE batch, two at once (per-thread fp64 terms, real
+  // elements only): wave sums -> workgroup sum in wave order -> partial slot -> grid barrier ->
+  // the same fixed-order sum of the slots in every workgroup
+  auto global_sum2 = [&](double v0, double v1, double& s0, double& s1) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      v0 += __shfl_xor(v0, o);
+      v1 += __shfl_xor(v1, o);
+    }
+    if (lane == 0) {
+      red[wv][0] = v0;
+      red[wv][1] = v1;
+    }
+    __syncthreads();
+    double* slot = a.part + ((int64_t)(phase & 1) * gridDim.x + blockIdx.x) * 2;
+    if (tid == 0) {
+      double w0 = red[0][0], w1 = red[0][1];
+      for (int w = 1; w < NT / 64; ++w) {
+        w0 += red[w][0];
+        w1 += red[w][1];
+      }
+      __hip_atomic_store(&slot[0], w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&slot[1], w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    grid_barrier(a.bar, gridDim.x);
+    if (wv == 0) {  // one wave sums the slots: lane-strided then a fixed butterfly
+      double u0 = 0.0, u1 = 0.0;
+      for (int g = lane; g < (int)gridDim.x; g += 64) {
+        const double* o = a.part + ((int64_t)(phase & 1) * gridDim.x + g) * 2;
+        u0 += __hip_atomic_load(&o[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        u1 += __hip_atomic_load(&o[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        u0 += __shfl_xor(u0, o);
+        u1 += __shfl_xor(u1, o);
+      }
+      if (lane == 0) {
+        tot[0] = u0;
+        tot[1] = u1;
+      }
+    }
+    __syncthreads();
+    s0 = tot[0];
+    s1 = tot[1];
+    ++phase;
+  };
+
+  // stage the head weight once; zero phi's padding
+  const int qp0 = wv * PS;  // this wave's head part
+  for (int idx = tid; idx < kHeadParts * G * D; idx += NT) {
+    const int pg = idx / D, dd = idx - pg * D, p = pg / G, g = pg - p * G;
+    const int q = p * PS + 4 * g;
+    const int qe = min(F, (p + 1) * PS);
+    float4 v;
+    v.x = q + 0 < qe ? a.wT[(int64_t)(q + 0) * D + dd] : 0.f;
+    v.y = q + 1 < qe ? a.wT[(int64_t)(q + 1) * D + dd] : 0.f;
+    v.z = q + 2 < qe ? a.wT[(int64_t)(q + 2) * D + dd] : 0.f;
+    v.w = q + 3 < qe ? a.wT[(int64_t)(q + 3) * D + dd] : 0.f;
+    s_dyn4[idx] = v;
+  }
+  for (int idx = tid; idx < R * Fp; idx += NT) phi[idx] = 0.f;
+  const int qend = min(F, qp0 + PS);
+  float wt[TAIL];
+#pragma unroll
+  for (int j = 0; j < TAIL; ++j) {
+    const int q = qp0 + QLp + j;
+    wt[j] = (d < D && q < qend) ? a.wT[(int64_t)q * D + d] : 0.f;
+  }
+  const int ntail = max(0, min(PS, Fp - qp0) - QLp);  // this part's register rows (multiple of 4)
+  const float bhd = (dval && a.bh) ? a.bh[d] : 0.f;
+  float fk[FQ], fE[FQ], fP[FQ], fb[FQ], pv[FQ], pvo[FQ];
+  int fi[FQ];
+#pragma unroll
+  for (int j = 0; j < FQ; ++j) {
+    const int q = tid + j * NT;
+    const bool own = q < F;
+    fk[j] = own ? a.L.k[q] : 0.f;
+    fE[j] = own ? a.L.Ec[q] : 0.f;
+    fP[j] = own ? a.L.Ps[q] : 0.f;
+    fb[j] = own ? a.L.bias[q] : 0.f;
+    fi[j] = own ? q / a.L.nb : 0;
+    pv[j] = own ? a.prev0[q] : 0.f;
+    pvo[j] = pv[j];
+  }
+  const float gs = a.L.gs, bp = a.L.bp;
   __syncthreads();
 
-  // one field evaluation of this thread's element; all threads of the workgroup take part
+  // one field evaluation of the solver thread's element; every thread of the workgroup takes part
   auto eval = [&](float xv) -> float {
     if (dval) xs[r][d] = xv;
     __syncthreads();
-    for (int idx = tid; idx < (kDR + 1) * F; idx += kDT) {
-      const int r2 = idx / F, q = idx - r2 * F, i = q / nb;
-      const float x = xs[r2][i];
-      const float kq = a.L.k[q], Ec = a.L.Ec[q], Ps = a.L.Ps[q];
-      const float su = fast_sigmoid(kq * (x - Ec)), sd = fast_sigmoid(kq * (x + Ec));
-      const float up = Ps * su * 2.0f - Ps, down = Ps * sd * 2.0f - Ps;
-      const float bs = ref_sigmoid(a.L.gs * (x - prev[q])) > a.L.bp ? 1.0f : 0.0f;
-      phi[idx] = fast_sigmoid(bs * up + (1.0f - bs) * down + a.L.bias[q]);
+#pragma unroll
+    for (int j = 0; j < FQ; ++j) {
+      const int q = tid + j * NT;
+      if (q < F) {
+        const float k = fk[j], Ec = fE[j], Ps = fP[j], pq = pv[j];
+#pragma unroll 2
+        for (int r2 = 0; r2 < R; ++r2) {  // hpoint's op order (train_ecg_kan_fet_nn_ode.py:110-121)
+          const float x = xs[r2][fi[j]];
+          const float su = 1.0f / (1.0f + expf(-k * (x - Ec)));
+          const float sd = 1.0f / (1.0f + expf(-k * (x + Ec)));
+          const float up = Ps * su * 2.0f - Ps;
+          const float down = Ps * sd * 2.0f - Ps;
+          const float bs = ref_sigmoid(gs * (x - pq)) > bp ? 1.0f : 0.0f;
+          phi[r2 * Fp + q] = ref_sigmoid(bs * up + (1.0f - bs) * down + fb[j]);
+        }
+        pvo[j] = pq;  // :131-132, the shadow row's input becomes prev_x
+        pv[j] = xs[NR][fi[j]];
+      }
     }
     __syncthreads();
-    for (int q = tid; q < F; q += kDT) {  // :131-132, the shadow row's input
-      prevold[q] = prev[q];
-      prev[q] = xs[kDR][q / nb];
+    // this wave's part of every row's head sum
+    float acc[R];
+#pragma unroll
+    for (int r2 = 0; r2 < R; ++r2) acc[r2] = 0.f;
+    const float4* W4 = s_dyn4 + (int64_t)wv * G * D + d;
+    const float* ph0 = phi + qp0;
+#pragma unroll 1
+    for (int g = 0; g < G; ++g) {
+      const float4 w = W4[g * D];
+#pragma unroll
+      for (int r2 = 0; r2 < R; ++r2) {
+        const float4 p = *reinterpret_cast<const float4*>(ph0 + r2 * Fp + 4 * g);
+        acc[r2] = __builtin_fmaf(p.x, w.x, acc[r2]);
+        acc[r2] = __builtin_fmaf(p.y, w.y, acc[r2]);
+        acc[r2] = __builtin_fmaf(p.z, w.z, acc[r2]);
+        acc[r2] = __builtin_fmaf(p.w, w.w, acc[r2]);
+      }
     }
-    float acc = 0.f;
+#pragma unroll
+    for (int j = 0; j < TAIL; j += 4) {
+      if (j < ntail) {
+#pragma unroll
+        for (int r2 = 0; r2 < R; ++r2) {
+          const float4 p = *reinterpret_cast<const float4*>(ph0 + r2 * Fp + QLp + j);
+          acc[r2] = __builtin_fmaf(p.x, wt[j], acc[r2]);
+          acc[r2] = __builtin_fmaf(p.y, wt[j + 1], acc[r2]);
+          acc[r2] = __builtin_fmaf(p.z, wt[j + 2], acc[r2]);
+          acc[r2] = __builtin_fmaf(p.w, wt[j + 3], acc[r2]);
+        }
+      }
+    }
+    __syncthreads();  // every wave has read phi: its space takes the partials
+#pragma unroll
+    for (int r2 = 0; r2 < R; ++r2) phi[(wv * R + r2) * 64 + d] = acc[r2];
+    __syncthreads();
+    float out = 0.f;
     if (dval) {
-      const float* ph = phi + r * F;
-      for (int q = 0; q < F; ++q) acc = __builtin_fmaf(ph[q], a.wT[(int64_t)q * D + d], acc);
-      acc += a.bh ? a.bh[d] : 0.f;
+      out = phi[r * 64 + d];
+#pragma unroll
+      for (int p = 1; p < kHeadParts; ++p) out = out + phi[(p * R + r) * 64 + d];
+      out = out + bhd;
     }
-    __syncthreads();
+    // no trailing barrier: the next evaluation writes xs, then waits before phi is rewritten
     ++nfev;
-    return acc;
+    return out;
   };
 
   float y = dval ? a.y0[b * D + d] : 0.f;
@@ -439,17 +545,16 @@ __global__ __launch_bounds__(kDT) void ecg_dopri5_kernel(EcgDopriArgs a) {
   } else {  // misc._select_initial_step in fp32 (dopri5.py select_initial_step)
     const float scale = a.atol + a.rtol * fabsf(y);
     double s;
-    int bad;
     const float q0 = y / scale, q1 = f0 / scale;
-    gn.run(a, real ? (double)q0 * q0 : 0.0, 0, phase++, 0, &s, &bad);
+    double s1;
+    global_sum2(real ? (double)q0 * q0 : 0.0, real ? (double)q1 * q1 : 0.0, s, s1);
     const float d0 = fabsf(sqrtf((float)(s / n_el)));
-    gn.run(a, real ? (double)q1 * q1 : 0.0, 0, phase++, 0, &s, &bad);
-    const float d1 = fabsf(sqrtf((float)(s / n_el)));
+    const float d1 = fabsf(sqrtf((float)(s1 / n_el)));
     float h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : (0.01f * d0) / d1;
     h0 = fabsf(h0);
     const float f1 = eval(y + f0 * h0);
     const float q2 = (f1 - f0) / scale;
-    gn.run(a, real ? (double)q2 * q2 : 0.0, 0, phase++, 0, &s, &bad);
+    global_sum2(real ? (double)q2 * q2 : 0.0, 0.0, s, s1);
     const float d2 = fabsf(sqrtf((float)(s / n_el)) / h0);
     float h1;
     if (d1 <= 1e-15f && d2 <= 1e-15f) h1 = fmaxf(1e-6f, h0 * 1e-3f);
@@ -468,27 +573,31 @@ __global__ __launch_bounds__(kDT) void ecg_dopri5_kernel(EcgDopriArgs a) {
       if (!(t0 + dt > t0)) { status = 2; break; }
       const float dt32 = (float)dt;
       const double t1 = t0 + dt;
-      float k[7];
-      k[0] = f0;
-      float yi = y;
+      // rk_common._runge_kutta_step via fetode_lincomb's op order, accumulated as the stages
+      // arrive: A[i] is stage s+1+i's sum k0*b0 + k1*b1 + ... (the same left-to-right sums), so
+      // the stage loop keeps one copy of the evaluation and no indexed register array
+      float A[6];
 #pragma unroll
-      for (int s = 0; s < 6; ++s) {  // rk_common._runge_kutta_step via fetode_lincomb's op order
-        float acc = k[0] * (a.tab.beta[s][0] * dt32);
+      for (int i = 0; i < 6; ++i) A[i] = f0 * (a.tab.beta[i][0] * dt32);
+      float err = f0 * (a.tab.cerr[0] * dt32);
+      float mid = f0 * (a.tab.cmid[0] * dt32);
+      float yi = y, kn = f0;
+#pragma unroll 1
+      for (int s = 0; s < 6; ++s) {
+        yi = y + A[0];
+        kn = eval(yi);
+        const int j = s + 1;
 #pragma unroll
-        for (int j = 1; j <= s; ++j) acc = acc + k[j] * (a.tab.beta[s][j] * dt32);
-        yi = y + acc;
-        k[s + 1] = eval(yi);
+        for (int i = 0; i < 5; ++i) A[i] = (j + i <= 5) ? A[i + 1] + kn * (a.tab.beta[j + i][j] * dt32) : 0.f;
+        err = err + kn * (a.tab.cerr[j] * dt32);
+        mid = mid + kn * (a.tab.cmid[j] * dt32);
       }
       const float y1 = yi;
-      float err = k[0] * (a.tab.cerr[0] * dt32);
-#pragma unroll
-      for (int j = 1; j < 7; ++j) err = err + k[j] * (a.tab.cerr[j] * dt32);
       const float tol = a.atol + a.rtol * fmaxf(fabsf(y), fabsf(y1));
       const float qe = err / tol;
-      double s;
-      int bad;
-      gn.run(a, real ? (double)qe * qe : 0.0, real && !__builtin_isfinite(y), phase++, 0, &s, &bad);
-      if (bad) { status = 1; break; }
+      double s, nbad;
+      global_sum2(real ? (double)qe * qe : 0.0, (real && !__builtin_isfinite(y)) ? 1.0 : 0.0, s, nbad);
+      if (nbad != 0.0) { status = 1; break; }
       const float ratio = sqrtf((float)(s / n_el));
       const bool accept = ratio <= 1.0f;
       if (blockIdx.x == 0 && tid == 0 && n_att < a.max_att) {
@@ -500,17 +609,14 @@ __global__ __launch_bounds__(kDT) void ecg_dopri5_kernel(EcgDopriArgs a) {
       }
       ++n_att;
       if (accept) {  // interp._interp_fit (fetode_interp_fit's op order)
-        float acc = k[0] * (a.tab.cmid[0] * dt32);
-#pragma unroll
-        for (int j = 1; j < 7; ++j) acc = acc + k[j] * (a.tab.cmid[j] * dt32);
-        const float ym = y + acc, fa = k[0], fb = k[6];
-        co[4] = ((2.0f * dt32) * (fb - fa) - 8.0f * (y1 + y)) + 16.0f * ym;
-        co[3] = ((dt32 * (5.0f * fa - 3.0f * fb) + 18.0f * y) + 14.0f * y1) - 32.0f * ym;
-        co[2] = ((dt32 * (fb - 4.0f * fa) - 11.0f * y) - 5.0f * y1) + 16.0f * ym;
+        const float ym = y + mid, fa = f0, fb6 = kn;
+        co[4] = ((2.0f * dt32) * (fb6 - fa) - 8.0f * (y1 + y)) + 16.0f * ym;
+        co[3] = ((dt32 * (5.0f * fa - 3.0f * fb6) + 18.0f * y) + 14.0f * y1) - 32.0f * ym;
+        co[2] = ((dt32 * (fb6 - 4.0f * fa) - 11.0f * y) - 5.0f * y1) + 16.0f * ym;
         co[1] = dt32 * fa;
         co[0] = y;
         y = y1;
-        f0 = k[6];
+        f0 = kn;
         t0s = t0;
         t1s = t1;
       } else {
@@ -541,15 +647,17 @@ __global__ __launch_bounds__(kDT) void ecg_dopri5_kernel(EcgDopriArgs a) {
     if (real) a.sol[(int64_t)i * BD + b * D + d] = total;
   }
   // module state after the solve: prev_x = the last evaluation's last-row input; branch_state of
-  // that evaluation for this workgroup's rows
-  if (blockIdx.x == 0)
-    for (int q = tid; q < F; q += kDT) a.prev_out[q] = prev[q];
-  if (a.branch_out) {
-    for (int idx = tid; idx < kDR * F; idx += kDT) {
-      const int r2 = idx / F, q = idx - r2 * F;
-      const int64_t b2 = (int64_t)blockIdx.x * kDR + r2;
-      if (b2 < a.B)
-        a.branch_out[b2 * F + q] = ref_sigmoid(a.L.gs * (xs[r2][q / nb] - prevold[q])) > a.L.bp ? 1.0f : 0.0f;
+  // that evaluation for this workgroup's rows (xs still holds its inputs)
+#pragma unroll
+  for (int j = 0; j < FQ; ++j) {
+    const int q = tid + j * NT;
+    if (q >= F) continue;
+    if (blockIdx.x == 0) a.prev_out[q] = pv[j];
+    if (a.branch_out) {
+      for (int r2 = 0; r2 < NR; ++r2) {
+        const int64_t b2 = (int64_t)blockIdx.x * NR + r2;
+        if (b2 < a.B) a.branch_out[b2 * F + q] = ref_sigmoid(gs * (xs[r2][fi[j]] - pvo[j])) > bp ? 1.0f : 0.0f;
+      }
     }
   }
   if (blockIdx.x == 0 && tid == 0) {
@@ -558,6 +666,16 @@ __global__ __launch_bounds__(kDT) void ecg_dopri5_kernel(EcgDopriArgs a) {
     a.stats[2] = status;
   }
 }
+
+// one instantiation of the resident kernel: rows per workgroup and the register tail per part
+struct EcgVariant {
+  const void* fn;
+  int rows, tail;
+};
+const EcgVariant kEcgVariants[] = {
+    {reinterpret_cast<const void*>(ecg_dopri5_kernel<4, 16>), 4, 16},
+    {reinterpret_cast<const void*>(ecg_dopri5_kernel<8, 24>), 8, 24},
+};
 
 }  // namespace
 
@@ -574,13 +692,16 @@ int fetode_ecg_dopri5(const fetode_hlogistic_t* layer, const float* wT, const fl
   if (!wT || !prev || !y0 || !t || !opts || !tableau || !solution || !prev_out || !workspace || !stats)
     return set_err(FETODE_EINVAL, "ecg dopri5: null pointer");
   if (D != layer->in_dim || D > 64) return set_err(FETODE_EINVAL, "ecg dopri5: state dim %d (must equal in_dim, <= 64)", D);
+  const int F = layer->in_dim * layer->num_basis;
+  if (F > kMaxF) return set_err(FETODE_EUNSUPPORTED, "ecg dopri5: in*num_basis=%d > %d", F, kMaxF);
   EcgDopriArgs a;
   memset(&a, 0, sizeof(a));
   a.L = to_dev(layer);
   a.wT = wT;
   a.bh = bias;
   a.D = D;
-  a.F = a.L.in * a.L.nb;
+  a.F = F;
+  a.Fp = (F + 3) & ~3;
   a.prev0 = prev;
   a.y0 = y0;
   a.B = B;
@@ -599,25 +720,45 @@ int fetode_ecg_dopri5(const fetode_hlogistic_t* layer, const float* wT, const fl
   a.sol = solution;
   a.prev_out = prev_out;
   a.branch_out = branch_out;
-  const int64_t grid = (B + kDR - 1) / kDR;
-  if (grid > 1024) return set_err(FETODE_EUNSUPPORTED, "ecg dopri5: batch %lld too large for one cooperative grid", (long long)B);
   a.bar = (unsigned*)workspace;
   a.part = (double*)((char*)workspace + 64);
   a.stats = stats;
   a.att = attempts;
   a.max_att = attempts ? max_attempts : 0;
-  hipStream_t s = (hipStream_t)stream;
-  HIP_CHECK_RET(hipMemsetAsync(workspace, 0, 64, s));
-  const size_t lds = sizeof(float) * ((kDR + 1) * a.F + 2 * a.F);
-  if (lds > 48 * 1024) return set_err(FETODE_EINVAL, "ecg dopri5: in*num_basis=%d too large", a.F);
-  void* args[] = {&a};
-  HIP_CHECK_RET(hipLaunchCooperativeKernel(reinterpret_cast<const void*>(ecg_dopri5_kernel), dim3((unsigned)grid),
-                                           dim3(kDT), args, (unsigned)lds, s));
-  return FETODE_OK;
+  int dev = 0, n_cu = 0;
+  HIP_CHECK_RET(hipGetDevice(&dev));
+  HIP_CHECK_RET(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  // the smallest workgroup whose grid is co-resident (one cooperative grid) and whose head
+  // weight fits LDS + its register tail
+  a.PS = head_part(F);
+  for (const EcgVariant& v : kEcgVariants) {
+    hipFuncAttributes fa;
+    HIP_CHECK_RET(hipFuncGetAttributes(&fa, v.fn));
+    // phi (R, Fp), reused for the (parts, R, 64) head partials
+    const int64_t phi_bytes = (int64_t)sizeof(float) * v.rows * std::max(a.Fp, 64 * kHeadParts);
+    const int64_t w_floats = (kLdsBytes - (int64_t)fa.sharedSizeBytes - phi_bytes) / (int64_t)sizeof(float);
+    if (w_floats < 0) continue;
+    const int QL = (int)std::min<int64_t>(a.PS, (w_floats / ((int64_t)kHeadParts * D)) & ~(int64_t)3);
+    if (a.PS - QL > v.tail) continue;
+    const size_t lds = (size_t)kHeadParts * QL * D * sizeof(float) + (size_t)phi_bytes;
+    HIP_CHECK_RET(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    int per_cu = 0;
+    HIP_CHECK_RET(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v.fn, kResThreads, lds));
+    const int64_t grid = (B + v.rows - 2) / (v.rows - 1);
+    if (per_cu <= 0 || grid > (int64_t)per_cu * n_cu) continue;
+    a.QL = QL;
+    hipStream_t s = (hipStream_t)stream;
+    HIP_CHECK_RET(hipMemsetAsync(workspace, 0, 64, s));
+    void* args[] = {&a};
+    HIP_CHECK_RET(hipLaunchCooperativeKernel(v.fn, dim3((unsigned)grid), dim3(kResThreads), args, (unsigned)lds, s));
+    return FETODE_OK;
+  }
+  return set_err(FETODE_EUNSUPPORTED, "ecg dopri5: batch %lld x in*num_basis %d does not fit one resident grid",
+                 (long long)B, F);
 }
 
 int64_t fetode_ecg_dopri5_workspace(int64_t B) {
-  const int64_t grid = (B + kDR - 1) / kDR;
+  const int64_t grid = (B + 2) / 3;  // the most workgroups any variant launches (3 real rows each)
   return 64 + (int64_t)sizeof(double) * 2 * 2 * grid;
 }
 

@@ -293,12 +293,15 @@ def _try_ecg_resident(func, y0, tp, reversed_, rtol, atol, options):
                      float(options.get("ifactor", 10.0)), float(options.get("dfactor", 0.2)),
                      float(options.get("min_step", 0.0)), float(options.get("max_step", math.inf)),
                      float(options.get("max_num_steps", 2 ** 31 - 1))], dtype=np.float64)
-    _lib.check(lib.fetode_ecg_dopri5(
+    rc = lib.fetode_ecg_dopri5(
         _lib.ctypes.byref(d), wT.data_ptr(), _lib.ptr(bias), D, prev.data_ptr(), yc.data_ptr(), B, t_dev.data_ptr(),
         T, float(rtol), float(atol), opts.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_double)),
         _TABLEAU.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_float)), sol.data_ptr(), prev_out.data_ptr(),
         branch.data_ptr(), ws.data_ptr(), stats.data_ptr(), att.data_ptr(), _MAX_TRACE,
-        _lib.stream_handle(dev)), "fetode_ecg_dopri5")
+        _lib.stream_handle(dev))
+    if rc == _lib.FETODE_EUNSUPPORTED:   # no resident grid for this batch / width: host-driven loop
+        return None
+    _lib.check(rc, "fetode_ecg_dopri5")
     prev.copy_(prev_out)
     basis.branch_state = branch
     status = int(stats[2].item())   # one read per solve: torchdiffeq's assertions
