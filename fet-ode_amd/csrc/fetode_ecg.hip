@@ -34,10 +34,12 @@ struct HL {  // device copy of fetode_hlogistic_t
 __device__ __forceinline__ float ref_sigmoid(float z) { return 1.0f / (1.0f + expf(-z)); }
 
 // The head's fp32 summation order, shared by every kernel that evaluates it: q in [0, F) splits
-// into kHeadParts consecutive parts of head_part(F) (a multiple of 4) indices; each part is an FMA
-// chain from 0 in increasing q, and the parts add left to right.  The resident dopri5 gives each
-// part to its own wave.
-constexpr int kHeadParts = 8;
+// into kHeadParts = 32 consecutive parts of head_part(F) (a multiple of 4) indices; each part P_p
+// is an FMA chain from 0 in increasing q; groups of four add as S_w = (P_4w + P_4w+1) +
+// (P_4w+2 + P_4w+3), and the eight S_w add left to right.  (The resident dopri5 gives each wave
+// one group, a quarter-wave per part, and combines a group with two lane shuffles.)
+constexpr int kHeadParts = 32;
+constexpr int kHeadGroups = kHeadParts / 4;
 __host__ __device__ __forceinline__ int head_part(int F) { return (((F + 3) & ~3) + 4 * kHeadParts - 1) / (4 * kHeadParts) * 4; }
 
 // the reference's up / down / gate for element (i, j) at input x (train_ecg_kan_fet_nn_ode.py:110-121)
@@ -83,11 +85,17 @@ __global__ __launch_bounds__(kThreads) void mixer_fwd_kernel(HL L, const float* 
     const float* ph = s_phi + r * F;
     const int PS = head_part(F);
     float tot = 0.f;
-    for (int p = 0; p < kHeadParts; ++p) {
-      float acc = 0.f;
-      const int q1 = min(F, (p + 1) * PS);
-      for (int q = p * PS; q < q1; ++q) acc = __builtin_fmaf(ph[q], wr[q], acc);
-      tot = p == 0 ? acc : tot + acc;
+    for (int w = 0; w < kHeadGroups; ++w) {
+      float P[4];
+      for (int c = 0; c < 4; ++c) {
+        const int p = 4 * w + c;
+        float acc = 0.f;
+        const int q1 = min(F, (p + 1) * PS);
+        for (int q = p * PS; q < q1; ++q) acc = __builtin_fmaf(ph[q], wr[q], acc);
+        P[c] = acc;
+      }
+      const float S = (P[0] + P[1]) + (P[2] + P[3]);
+      tot = w == 0 ? S : tot + S;
     }
     out[(b0 + r) * n_out + o] = tot + (bvec ? bvec[o] : 0.f);
   }
@@ -332,7 +340,27 @@ struct EcgDopriArgs {
   int* stats;         // [nfev, attempts, status]
   double* att;        // (max_att, 4): t0, dt, error ratio, accepted
   int max_att;
+  long long* stamps;  // debug (fetode_debug_ecg_stamps): workgroup 0's 100 MHz ticks per phase
 };
+
+// phase timer of workgroup 0 in the diagnostic build only (make stamps, tools/diag/ecg_time.py):
+// other, features, head, partials, norms in 100 MHz ticks; the kernel's s_memtime total
+#ifdef FETODE_STAMPS
+#define STAMP(i)                                               \
+  do {                                                         \
+    if (stamping) {                                            \
+      const long long now_ = __builtin_amdgcn_s_memrealtime(); \
+      st_acc[i] += now_ - st_last;                             \
+      st_last = now_;                                          \
+    }                                                          \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#endif
+
+__device__ __forceinline__ float fast_sigmoid(float z) { return rcp(1.0f + ex2(-z * FETODE_LOG2E)); }
 
 __device__ void grid_barrier(unsigned* bar, unsigned nblk) {
   __syncthreads();
@@ -352,22 +380,35 @@ __device__ void grid_barrier(unsigned* bar, unsigned nblk) {
 }
 
 // NT = 512 threads, R rows per workgroup (R-1 real + the shadow).  Solver thread (r, d) = tid for
-// tid < 64 R carries state element d of row r.  Head: wave p (of kHeadParts) owns q-part p and
-// forms all R rows' partial sums for output d = lane; W^T rows of the part sit in LDS (the first
-// QLp of each part) and registers (the rest, <= TAIL).  Features: thread tid owns input-basis
-// index q = tid + j * NT for all R rows.
-constexpr int kResThreads = 64 * kHeadParts;
+// tid < 64 R carries state element d of row r.
+// Features: the R * F (row, basis) elements of an evaluation are dealt round-robin to all threads
+// (<= EPT each); their parameters sit in LDS as float4 {k, Ec, Ps, bias}.  prev_x is constant over
+// the bases of one input after the first call (:131-132 expands the last row's x), so it is kept per
+// input, double-buffered by evaluation parity; the first evaluation reads the module's prev_x.
+// Head: wave w owns head group w = parts 4w..4w+3, a quarter-wave per part; lane l16 of a quarter
+// forms the part's sums for outputs l16 + 16c (c < 4) of every row.  The part's W^T rows sit in
+// LDS as [part][q/4][64] float4 (the first QL) and in registers (the rest, <= TAIL).  Two lane
+// shuffles combine the four parts of a group; the solver threads add the eight groups.
+constexpr int kResThreads = 512;
 template <int R, int TAIL>
 __global__ __launch_bounds__(kResThreads) void ecg_dopri5_kernel(EcgDopriArgs a) {
-  constexpr int NT = kResThreads, NR = R - 1, FQ = (kMaxF + NT - 1) / NT;
-  extern __shared__ float4 s_dyn4[];  // W^T [part][QLp/4][D] float4 | phi (R, Fp), later partials
+  constexpr int NT = kResThreads, NR = R - 1, EPT = (R * kMaxF + NT - 1) / NT;
+  constexpr int FU = R <= 4 ? EPT : 2;  // feature-loop unroll (R = 8: registers)
+  static_assert(NT / 64 == kHeadGroups, "one head group per wave");
+  static_assert(R % 4 == 0, "the head runs four rows at a time");
+  // dynamic LDS: W^T [kHeadParts][QL/4][64] float4 | prm [F] float4 | pv0 [Fp] | phi (R, Fp) | hs
+  extern __shared__ float4 s_dyn4[];
   __shared__ float xs[R][64];
+  __shared__ float pvx[2][64];
   __shared__ double red[NT / 64][2];
   __shared__ double tot[2];
   const int tid = threadIdx.x, lane = tid % 64, wv = tid / 64;
   const int r = wv, d = lane;  // solver view (rows r < R)
-  const int D = a.D, F = a.F, Fp = a.Fp, PS = a.PS, QLp = a.QL, G = a.QL / 4;
-  float* phi = reinterpret_cast<float*>(s_dyn4 + (int64_t)kHeadParts * G * D);
+  const int D = a.D, F = a.F, Fp = a.Fp, PS = a.PS, QL = a.QL, G = a.QL / 4, nb = a.L.nb;
+  float4* prm = s_dyn4 + (int64_t)kHeadParts * G * 64;
+  float* pv0 = reinterpret_cast<float*>(prm + F);  // the module's prev_x before the solve (F)
+  float* phi = pv0 + Fp;                            // (R, Fp)
+  float* hs = phi + R * Fp;                          // (kHeadGroups, R, 64) group sums
   const bool solver = tid < 64 * R;
   const bool dval = solver && d < D;
   int64_t b = r < NR ? (int64_t)blockIdx.x * NR + r : a.B - 1;  // row NR: the shadow last row
@@ -376,11 +417,17 @@ __global__ __launch_bounds__(kResThreads) void ecg_dopri5_kernel(EcgDopriArgs a)
   const int64_t BD = a.B * D;
   const double n_el = (double)BD;
   int phase = 0, nfev = 0, status = 0, n_att = 0;
+#ifdef FETODE_STAMPS
+  const bool stamping = a.stamps != nullptr && blockIdx.x == 0 && tid == 0;
+  long long st_acc[5] = {0, 0, 0, 0, 0}, st_last = stamping ? __builtin_amdgcn_s_memrealtime() : 0;
+  const long long st_clk0 = stamping ? __builtin_amdgcn_s_memtime() : 0, st_rt0 = st_last;
+#endif
 
   // misc._rms_norm numerators over the WHOLE batch, two at once (per-thread fp64 terms, real
   // elements only): wave sums -> workgroup sum in wave order -> partial slot -> grid barrier ->
   // the same fixed-order sum of the slots in every workgroup
   auto global_sum2 = [&](double v0, double v1, double& s0, double& s1) {
+    STAMP(0);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       v0 += __shfl_xor(v0, o);
@@ -423,45 +470,44 @@ __global__ __launch_bounds__(kResThreads) void ecg_dopri5_kernel(EcgDopriArgs a)
     s0 = tot[0];
     s1 = tot[1];
     ++phase;
+    STAMP(4);
   };
 
-  // stage the head weight once; zero phi's padding
-  const int qp0 = wv * PS;  // this wave's head part
-  for (int idx = tid; idx < kHeadParts * G * D; idx += NT) {
-    const int pg = idx / D, dd = idx - pg * D, p = pg / G, g = pg - p * G;
-    const int q = p * PS + 4 * g;
-    const int qe = min(F, (p + 1) * PS);
-    float4 v;
-    v.x = q + 0 < qe ? a.wT[(int64_t)(q + 0) * D + dd] : 0.f;
-    v.y = q + 1 < qe ? a.wT[(int64_t)(q + 1) * D + dd] : 0.f;
-    v.z = q + 2 < qe ? a.wT[(int64_t)(q + 2) * D + dd] : 0.f;
-    v.w = q + 3 < qe ? a.wT[(int64_t)(q + 3) * D + dd] : 0.f;
+  // stage the head weight and the feature parameters; zero phi's padding
+  const int qtr = lane >> 4, l16 = lane & 15, part = 4 * wv + qtr;
+  const int qp0 = part * PS, qend = min(F, qp0 + PS);
+  for (int idx = tid; idx < kHeadParts * G * 64; idx += NT) {
+    const int pg = idx / 64, dd = idx - pg * 64, pp = pg / G, g = pg - pp * G;
+    const int q = pp * PS + 4 * g, qe = min(F, (pp + 1) * PS);
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (dd < D) {
+      v.x = q + 0 < qe ? a.wT[(int64_t)(q + 0) * D + dd] : 0.f;
+      v.y = q + 1 < qe ? a.wT[(int64_t)(q + 1) * D + dd] : 0.f;
+      v.z = q + 2 < qe ? a.wT[(int64_t)(q + 2) * D + dd] : 0.f;
+      v.w = q + 3 < qe ? a.wT[(int64_t)(q + 3) * D + dd] : 0.f;
+    }
     s_dyn4[idx] = v;
   }
+  for (int q = tid; q < F; q += NT) {
+    prm[q] = make_float4(a.L.k[q], a.L.Ec[q], a.L.Ps[q], a.L.bias[q]);
+    pv0[q] = a.prev0[q];
+  }
   for (int idx = tid; idx < R * Fp; idx += NT) phi[idx] = 0.f;
-  const int qend = min(F, qp0 + PS);
-  float wt[TAIL];
+  float wt[TAIL][4];
 #pragma unroll
-  for (int j = 0; j < TAIL; ++j) {
-    const int q = qp0 + QLp + j;
-    wt[j] = (d < D && q < qend) ? a.wT[(int64_t)q * D + d] : 0.f;
-  }
-  const int ntail = max(0, min(PS, Fp - qp0) - QLp);  // this part's register rows (multiple of 4)
+  for (int j = 0; j < TAIL; ++j)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int q = qp0 + QL + j, dd = l16 + 16 * c;
+      wt[j][c] = (dd < D && q < qend) ? a.wT[(int64_t)q * D + dd] : 0.f;
+    }
+  const int gcount = max(0, min(G, (qend - qp0 + 3) / 4));            // LDS groups of this part
+  const int ntail = max(0, min(TAIL, ((qend - qp0 + 3) & ~3) - QL));  // register rows of this part
   const float bhd = (dval && a.bh) ? a.bh[d] : 0.f;
-  float fk[FQ], fE[FQ], fP[FQ], fb[FQ], pv[FQ], pvo[FQ];
-  int fi[FQ];
-#pragma unroll
-  for (int j = 0; j < FQ; ++j) {
-    const int q = tid + j * NT;
-    const bool own = q < F;
-    fk[j] = own ? a.L.k[q] : 0.f;
-    fE[j] = own ? a.L.Ec[q] : 0.f;
-    fP[j] = own ? a.L.Ps[q] : 0.f;
-    fb[j] = own ? a.L.bias[q] : 0.f;
-    fi[j] = own ? q / a.L.nb : 0;
-    pv[j] = own ? a.prev0[q] : 0.f;
-    pvo[j] = pv[j];
-  }
+  // this thread's first element (row e0 / F, basis e0 % F), then every NT-th; i = q / nb by a
+  // 16-bit reciprocal (exact for q < 768, nb <= 64)
+  const int e_r0 = tid / F, e_q0 = tid - e_r0 * F;
+  const unsigned inv_nb = (65536u + (unsigned)nb - 1u) / (unsigned)nb;
   const float gs = a.L.gs, bp = a.L.bp;
   __syncthreads();
 
@@ -469,69 +515,102 @@ __global__ __launch_bounds__(kResThreads) void ecg_dopri5_kernel(EcgDopriArgs a)
   auto eval = [&](float xv) -> float {
     if (dval) xs[r][d] = xv;
     __syncthreads();
-#pragma unroll
-    for (int j = 0; j < FQ; ++j) {
-      const int q = tid + j * NT;
-      if (q < F) {
-        const float k = fk[j], Ec = fE[j], Ps = fP[j], pq = pv[j];
-#pragma unroll 2
-        for (int r2 = 0; r2 < R; ++r2) {  // hpoint's op order (train_ecg_kan_fet_nn_ode.py:110-121)
-          const float x = xs[r2][fi[j]];
-          const float su = 1.0f / (1.0f + expf(-k * (x - Ec)));
-          const float sd = 1.0f / (1.0f + expf(-k * (x + Ec)));
-          const float up = Ps * su * 2.0f - Ps;
-          const float down = Ps * sd * 2.0f - Ps;
-          const float bs = ref_sigmoid(gs * (x - pq)) > bp ? 1.0f : 0.0f;
-          phi[r2 * Fp + q] = ref_sigmoid(bs * up + (1.0f - bs) * down + fb[j]);
-        }
-        pvo[j] = pq;  // :131-132, the shadow row's input becomes prev_x
-        pv[j] = xs[NR][fi[j]];
+    STAMP(0);
+    const int n = nfev;
+    int q = e_q0, r2 = e_r0;
+#pragma unroll FU
+    for (int j = 0; j < EPT; ++j) {
+      if (r2 < R) {  // hpoint's op order (train_ecg_kan_fet_nn_ode.py:110-121)
+        const int i = (int)(((unsigned)q * inv_nb) >> 16);
+        const float x = xs[r2][i];
+        const float4 pr = prm[q];
+        const float pq = n == 0 ? pv0[q] : pvx[n & 1][i];
+        const float k = pr.x, Ec = pr.y, Ps = pr.z;
+        // the smooth logistics on v_exp / v_rcp (1-ulp class); the hard gate in the reference's
+        // rounding (expf, IEEE division), so it flips exactly where the mixer kernel's does
+        const float su = fast_sigmoid(k * (x - Ec));
+        const float sd = fast_sigmoid(k * (x + Ec));
+        const float up = Ps * su * 2.0f - Ps;
+        const float down = Ps * sd * 2.0f - Ps;
+        const float bs = ref_sigmoid(gs * (x - pq)) > bp ? 1.0f : 0.0f;
+        phi[r2 * Fp + q] = fast_sigmoid(bs * up + (1.0f - bs) * down + pr.w);
+      }
+      q += NT;
+      while (q >= F) {
+        q -= F;
+        ++r2;
       }
     }
     __syncthreads();
-    // this wave's part of every row's head sum
-    float acc[R];
-#pragma unroll
-    for (int r2 = 0; r2 < R; ++r2) acc[r2] = 0.f;
-    const float4* W4 = s_dyn4 + (int64_t)wv * G * D + d;
+    STAMP(1);
+    if (tid < D) pvx[(n + 1) & 1][tid] = xs[NR][tid];  // :131-132, the shadow row's input
+    // this quarter-wave's part of every row's head sums, outputs l16 + 16 c, four rows at a time
+    const float4* W4 = s_dyn4 + (int64_t)part * G * 64 + l16;
     const float* ph0 = phi + qp0;
-#pragma unroll 1
-    for (int g = 0; g < G; ++g) {
-      const float4 w = W4[g * D];
 #pragma unroll
-      for (int r2 = 0; r2 < R; ++r2) {
-        const float4 p = *reinterpret_cast<const float4*>(ph0 + r2 * Fp + 4 * g);
-        acc[r2] = __builtin_fmaf(p.x, w.x, acc[r2]);
-        acc[r2] = __builtin_fmaf(p.y, w.y, acc[r2]);
-        acc[r2] = __builtin_fmaf(p.z, w.z, acc[r2]);
-        acc[r2] = __builtin_fmaf(p.w, w.w, acc[r2]);
-      }
-    }
+    for (int rc = 0; rc < R; rc += 4) {
+      float acc[4][4];
 #pragma unroll
-    for (int j = 0; j < TAIL; j += 4) {
-      if (j < ntail) {
+      for (int r2 = 0; r2 < 4; ++r2)
 #pragma unroll
-        for (int r2 = 0; r2 < R; ++r2) {
-          const float4 p = *reinterpret_cast<const float4*>(ph0 + r2 * Fp + QLp + j);
-          acc[r2] = __builtin_fmaf(p.x, wt[j], acc[r2]);
-          acc[r2] = __builtin_fmaf(p.y, wt[j + 1], acc[r2]);
-          acc[r2] = __builtin_fmaf(p.z, wt[j + 2], acc[r2]);
-          acc[r2] = __builtin_fmaf(p.w, wt[j + 3], acc[r2]);
+        for (int c = 0; c < 4; ++c) acc[r2][c] = 0.f;
+#pragma unroll 2
+      for (int g = 0; g < gcount; ++g) {
+        float4 w[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) w[c] = W4[g * 64 + 16 * c];
+#pragma unroll
+        for (int r2 = 0; r2 < 4; ++r2) {
+          const float4 p = *reinterpret_cast<const float4*>(ph0 + (rc + r2) * Fp + 4 * g);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            acc[r2][c] = __builtin_fmaf(p.x, w[c].x, acc[r2][c]);
+            acc[r2][c] = __builtin_fmaf(p.y, w[c].y, acc[r2][c]);
+            acc[r2][c] = __builtin_fmaf(p.z, w[c].z, acc[r2][c]);
+            acc[r2][c] = __builtin_fmaf(p.w, w[c].w, acc[r2][c]);
+          }
         }
       }
-    }
-    __syncthreads();  // every wave has read phi: its space takes the partials
 #pragma unroll
-    for (int r2 = 0; r2 < R; ++r2) phi[(wv * R + r2) * 64 + d] = acc[r2];
+      for (int j = 0; j < TAIL; j += 4) {
+        if (j < ntail) {
+#pragma unroll
+          for (int r2 = 0; r2 < 4; ++r2) {
+            const float4 p = *reinterpret_cast<const float4*>(ph0 + (rc + r2) * Fp + QL + j);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              acc[r2][c] = __builtin_fmaf(p.x, wt[j][c], acc[r2][c]);
+              acc[r2][c] = __builtin_fmaf(p.y, wt[j + 1][c], acc[r2][c]);
+              acc[r2][c] = __builtin_fmaf(p.z, wt[j + 2][c], acc[r2][c]);
+              acc[r2][c] = __builtin_fmaf(p.w, wt[j + 3][c], acc[r2][c]);
+            }
+          }
+        }
+      }
+      // S_w = (P_4w + P_4w+1) + (P_4w+2 + P_4w+3): quarter 0 meets quarter 1, then the pairs meet
+#pragma unroll
+      for (int r2 = 0; r2 < 4; ++r2)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          acc[r2][c] = acc[r2][c] + __shfl_xor(acc[r2][c], 16);
+          acc[r2][c] = acc[r2][c] + __shfl_xor(acc[r2][c], 32);
+        }
+      if (qtr == 0)
+#pragma unroll
+        for (int r2 = 0; r2 < 4; ++r2)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) hs[(wv * R + rc + r2) * 64 + l16 + 16 * c] = acc[r2][c];
+    }
     __syncthreads();
+    STAMP(2);
     float out = 0.f;
     if (dval) {
-      out = phi[r * 64 + d];
+      out = hs[r * 64 + d];
 #pragma unroll
-      for (int p = 1; p < kHeadParts; ++p) out = out + phi[(p * R + r) * 64 + d];
+      for (int w = 1; w < kHeadGroups; ++w) out = out + hs[(w * R + r) * 64 + d];
       out = out + bhd;
     }
-    // no trailing barrier: the next evaluation writes xs, then waits before phi is rewritten
+    // no trailing barrier: the next evaluation writes xs, then waits before phi / hs are rewritten
     ++nfev;
     return out;
   };
@@ -648,15 +727,15 @@ __global__ __launch_bounds__(kResThreads) void ecg_dopri5_kernel(EcgDopriArgs a)
   }
   // module state after the solve: prev_x = the last evaluation's last-row input; branch_state of
   // that evaluation for this workgroup's rows (xs still holds its inputs)
-#pragma unroll
-  for (int j = 0; j < FQ; ++j) {
-    const int q = tid + j * NT;
-    if (q >= F) continue;
-    if (blockIdx.x == 0) a.prev_out[q] = pv[j];
+  const int nl = nfev - 1;  // the last evaluation
+  for (int q = tid; q < F; q += NT) {
+    const int i = q / nb;
+    if (blockIdx.x == 0) a.prev_out[q] = xs[NR][i];
     if (a.branch_out) {
+      const float pq = nl == 0 ? pv0[q] : pvx[nl & 1][i];
       for (int r2 = 0; r2 < NR; ++r2) {
         const int64_t b2 = (int64_t)blockIdx.x * NR + r2;
-        if (b2 < a.B) a.branch_out[b2 * F + q] = ref_sigmoid(gs * (xs[r2][fi[j]] - pvo[j])) > bp ? 1.0f : 0.0f;
+        if (b2 < a.B) a.branch_out[b2 * F + q] = ref_sigmoid(gs * (xs[r2][i] - pq)) > bp ? 1.0f : 0.0f;
       }
     }
   }
@@ -664,8 +743,17 @@ __global__ __launch_bounds__(kResThreads) void ecg_dopri5_kernel(EcgDopriArgs a)
     a.stats[0] = nfev;
     a.stats[1] = n_att;
     a.stats[2] = status;
+#ifdef FETODE_STAMPS
+    if (stamping) {
+      for (int i = 0; i < 5; ++i) a.stamps[i] += st_acc[i];
+      a.stamps[5] += __builtin_amdgcn_s_memtime() - st_clk0;
+      a.stamps[6] += __builtin_amdgcn_s_memrealtime() - st_rt0;
+    }
+#endif
   }
 }
+
+long long* g_ecg_stamps = nullptr;  // fetode_debug_ecg_stamps
 
 // one instantiation of the resident kernel: rows per workgroup and the register tail per part
 struct EcgVariant {
@@ -673,8 +761,8 @@ struct EcgVariant {
   int rows, tail;
 };
 const EcgVariant kEcgVariants[] = {
-    {reinterpret_cast<const void*>(ecg_dopri5_kernel<4, 16>), 4, 16},
-    {reinterpret_cast<const void*>(ecg_dopri5_kernel<8, 24>), 8, 24},
+    {reinterpret_cast<const void*>(ecg_dopri5_kernel<4, 8>), 4, 8},
+    {reinterpret_cast<const void*>(ecg_dopri5_kernel<8, 8>), 8, 8},
 };
 
 }  // namespace
@@ -725,6 +813,7 @@ int fetode_ecg_dopri5(const fetode_hlogistic_t* layer, const float* wT, const fl
   a.stats = stats;
   a.att = attempts;
   a.max_att = attempts ? max_attempts : 0;
+  a.stamps = g_ecg_stamps;
   int dev = 0, n_cu = 0;
   HIP_CHECK_RET(hipGetDevice(&dev));
   HIP_CHECK_RET(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
@@ -734,13 +823,14 @@ int fetode_ecg_dopri5(const fetode_hlogistic_t* layer, const float* wT, const fl
   for (const EcgVariant& v : kEcgVariants) {
     hipFuncAttributes fa;
     HIP_CHECK_RET(hipFuncGetAttributes(&fa, v.fn));
-    // phi (R, Fp), reused for the (parts, R, 64) head partials
-    const int64_t phi_bytes = (int64_t)sizeof(float) * v.rows * std::max(a.Fp, 64 * kHeadParts);
-    const int64_t w_floats = (kLdsBytes - (int64_t)fa.sharedSizeBytes - phi_bytes) / (int64_t)sizeof(float);
+    // phi (R, Fp) + the (groups, R, 64) head sums; feature parameters; W^T in the rest
+    const int64_t phi_bytes = (int64_t)sizeof(float) * v.rows * (a.Fp + 64 * kHeadGroups);
+    const int64_t prm_bytes = (int64_t)sizeof(float) * (4 * F + a.Fp);  // + prev_x before the solve
+    const int64_t w_floats = (kLdsBytes - (int64_t)fa.sharedSizeBytes - phi_bytes - prm_bytes) / (int64_t)sizeof(float);
     if (w_floats < 0) continue;
-    const int QL = (int)std::min<int64_t>(a.PS, (w_floats / ((int64_t)kHeadParts * D)) & ~(int64_t)3);
+    const int QL = (int)std::min<int64_t>(a.PS, (w_floats / ((int64_t)kHeadParts * 64)) & ~(int64_t)3);
     if (a.PS - QL > v.tail) continue;
-    const size_t lds = (size_t)kHeadParts * QL * D * sizeof(float) + (size_t)phi_bytes;
+    const size_t lds = (size_t)kHeadParts * QL * 64 * sizeof(float) + (size_t)(prm_bytes + phi_bytes);
     HIP_CHECK_RET(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     int per_cu = 0;
     HIP_CHECK_RET(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v.fn, kResThreads, lds));
@@ -756,6 +846,10 @@ int fetode_ecg_dopri5(const fetode_hlogistic_t* layer, const float* wT, const fl
   return set_err(FETODE_EUNSUPPORTED, "ecg dopri5: batch %lld x in*num_basis %d does not fit one resident grid",
                  (long long)B, F);
 }
+
+#ifdef FETODE_STAMPS
+void fetode_debug_ecg_stamps(void* p) { g_ecg_stamps = (long long*)p; }
+#endif
 
 int64_t fetode_ecg_dopri5_workspace(int64_t B) {
   const int64_t grid = (B + 2) / 3;  // the most workgroups any variant launches (3 real rows each)
