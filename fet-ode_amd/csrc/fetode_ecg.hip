@@ -336,7 +336,7 @@ struct EcgDopriArgs {
   float* prev_out;    // (F)
   float* branch_out;  // (B, F) nullable: branch_state of the last evaluation
   double* part;       // (2, gridDim.x, 2) double-buffered partial sums
-  unsigned* bar;      // 2 words, zeroed: arrival count, generation
+  unsigned* bar;      // kBarWords, zeroed: per-XCD and top arrival counters, generation
   int* stats;         // [nfev, attempts, status]
   double* att;        // (max_att, 4): t0, dt, error ratio, accepted
   int max_att;
@@ -362,19 +362,31 @@ struct EcgDopriArgs {
 
 __device__ __forceinline__ float fast_sigmoid(float z) { return rcp(1.0f + ex2(-z * FETODE_LOG2E)); }
 
+// Grid barrier, XCD-hierarchical (MI355X_MICROARCH.md "barrier-xcd"): workgroup i runs on XCD
+// i % 8, so each XCD's workgroups arrive on their own counter (256 B apart); the last arriver of an
+// XCD arrives on the top counter, the last of those bumps the generation every workgroup polls.
+// Release before arriving, acquire after: the partial slots written before the barrier are
+// visible after it.  Counters reset themselves; the words are zeroed once per launch.
+constexpr int kBarWords = 64 * 10;  // 8 XCD counters, top counter, generation (256 B each)
 __device__ void grid_barrier(unsigned* bar, unsigned nblk) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned* count = bar;
-    unsigned* gen = bar + 1;
-    const unsigned g = __hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned old = __hip_atomic_fetch_add(count, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == nblk - 1) {
-      __hip_atomic_store(count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      while (__hip_atomic_load(gen, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == g) __builtin_amdgcn_s_sleep(2);
+    const unsigned x = blockIdx.x & 7u;
+    const unsigned nx = (nblk + 7u - x) / 8u, nxcd = nblk < 8u ? nblk : 8u;
+    unsigned* cnt = bar + 64 * x;
+    unsigned* top = bar + 64 * 8;
+    unsigned* gen = bar + 64 * 9;
+    const unsigned g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nx - 1u) {
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nxcd - 1u) {
+        __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
+    while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
 }
@@ -809,7 +821,7 @@ int fetode_ecg_dopri5(const fetode_hlogistic_t* layer, const float* wT, const fl
   a.prev_out = prev_out;
   a.branch_out = branch_out;
   a.bar = (unsigned*)workspace;
-  a.part = (double*)((char*)workspace + 64);
+  a.part = (double*)((char*)workspace + sizeof(unsigned) * kBarWords);
   a.stats = stats;
   a.att = attempts;
   a.max_att = attempts ? max_attempts : 0;
@@ -838,7 +850,7 @@ int fetode_ecg_dopri5(const fetode_hlogistic_t* layer, const float* wT, const fl
     if (per_cu <= 0 || grid > (int64_t)per_cu * n_cu) continue;
     a.QL = QL;
     hipStream_t s = (hipStream_t)stream;
-    HIP_CHECK_RET(hipMemsetAsync(workspace, 0, 64, s));
+    HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kBarWords, s));
     void* args[] = {&a};
     HIP_CHECK_RET(hipLaunchCooperativeKernel(v.fn, dim3((unsigned)grid), dim3(kResThreads), args, (unsigned)lds, s));
     return FETODE_OK;
@@ -853,7 +865,7 @@ void fetode_debug_ecg_stamps(void* p) { g_ecg_stamps = (long long*)p; }
 
 int64_t fetode_ecg_dopri5_workspace(int64_t B) {
   const int64_t grid = (B + 2) / 3;  // the most workgroups any variant launches (3 real rows each)
-  return 64 + (int64_t)sizeof(double) * 2 * 2 * grid;
+  return (int64_t)sizeof(unsigned) * kBarWords + (int64_t)sizeof(double) * 2 * 2 * grid;
 }
 
 }  // extern "C"
