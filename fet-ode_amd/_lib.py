@@ -114,6 +114,12 @@ SIGNATURES = {
                                          ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_float), _vp, _vp,
                                          _vp, _vp, _vp, _vp, ctypes.c_int32, _vp]),
     "fetode_ecg_dopri5_workspace": (ctypes.c_int64, [ctypes.c_int64]),
+    "fetode_tanh_bound": (ctypes.c_int, [ctypes.c_int64, ctypes.c_float, _vp, _vp, _vp, _vp]),
+    "fetode_tanh_bound_backward": (ctypes.c_int, [ctypes.c_int64, ctypes.c_float, _vp, _vp, _vp, _vp]),
+    "fetode_tanh": (ctypes.c_int, [ctypes.c_int64, _vp, _vp, _vp]),
+    "fetode_tanh_backward": (ctypes.c_int, [ctypes.c_int64, _vp, _vp, _vp, _vp]),
+    "fetode_nan_clamp": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_float] * 5 + [_vp, _vp, _vp]),
+    "fetode_nan_clamp_backward": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_float] * 5 + [_vp, _vp, _vp, _vp]),
     "fetode_hlogistic_mixer_backward": (ctypes.c_int, [ctypes.POINTER(HLogisticDesc), _vp, ctypes.c_int64, _vp,
                                                        ctypes.c_int32, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp, _vp,
                                                        _vp, _vp, _vp, _vp, _vp, _vp]),

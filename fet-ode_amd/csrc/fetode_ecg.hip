@@ -826,28 +826,48 @@ int fetode_ecg_dopri5(const fetode_hlogistic_t* layer, const float* wT, const fl
   a.att = attempts;
   a.max_att = attempts ? max_attempts : 0;
   a.stamps = g_ecg_stamps;
-  int dev = 0, n_cu = 0;
+  // per-variant launch facts, queried once (static LDS, the dynamic-LDS cap) and per LDS size
+  // (occupancy): the launch path does no runtime queries on repeat calls
+  static int n_cu_of[64] = {0};
+  static struct {
+    int static_lds = -1;
+    size_t lds = 0;
+    int per_cu = 0;
+  } vstate[sizeof(kEcgVariants) / sizeof(kEcgVariants[0])];
+  int dev = 0;
   HIP_CHECK_RET(hipGetDevice(&dev));
-  HIP_CHECK_RET(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  if (dev < 0 || dev >= 64) return set_err(FETODE_EINVAL, "ecg dopri5: device %d", dev);
+  if (!n_cu_of[dev]) HIP_CHECK_RET(hipDeviceGetAttribute(&n_cu_of[dev], hipDeviceAttributeMultiprocessorCount, dev));
+  const int n_cu = n_cu_of[dev];
+  a.PS = head_part(F);
   // the smallest workgroup whose grid is co-resident (one cooperative grid) and whose head
   // weight fits LDS + its register tail
-  a.PS = head_part(F);
-  for (const EcgVariant& v : kEcgVariants) {
-    hipFuncAttributes fa;
-    HIP_CHECK_RET(hipFuncGetAttributes(&fa, v.fn));
+  for (size_t vi = 0; vi < sizeof(kEcgVariants) / sizeof(kEcgVariants[0]); ++vi) {
+    const EcgVariant& v = kEcgVariants[vi];
+    auto& vs = vstate[vi];
+    if (vs.static_lds < 0) {
+      hipFuncAttributes fa;
+      HIP_CHECK_RET(hipFuncGetAttributes(&fa, v.fn));
+      HIP_CHECK_RET(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        kLdsBytes - (int)fa.sharedSizeBytes));
+      vs.static_lds = (int)fa.sharedSizeBytes;
+    }
     // phi (R, Fp) + the (groups, R, 64) head sums; feature parameters; W^T in the rest
     const int64_t phi_bytes = (int64_t)sizeof(float) * v.rows * (a.Fp + 64 * kHeadGroups);
     const int64_t prm_bytes = (int64_t)sizeof(float) * (4 * F + a.Fp);  // + prev_x before the solve
-    const int64_t w_floats = (kLdsBytes - (int64_t)fa.sharedSizeBytes - phi_bytes - prm_bytes) / (int64_t)sizeof(float);
+    const int64_t w_floats = (kLdsBytes - (int64_t)vs.static_lds - phi_bytes - prm_bytes) / (int64_t)sizeof(float);
     if (w_floats < 0) continue;
     const int QL = (int)std::min<int64_t>(a.PS, (w_floats / ((int64_t)kHeadParts * 64)) & ~(int64_t)3);
     if (a.PS - QL > v.tail) continue;
     const size_t lds = (size_t)kHeadParts * QL * 64 * sizeof(float) + (size_t)(prm_bytes + phi_bytes);
-    HIP_CHECK_RET(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    int per_cu = 0;
-    HIP_CHECK_RET(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v.fn, kResThreads, lds));
+    if (vs.lds != lds) {
+      int per_cu = 0;
+      HIP_CHECK_RET(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v.fn, kResThreads, lds));
+      vs.lds = lds;
+      vs.per_cu = per_cu;
+    }
     const int64_t grid = (B + v.rows - 2) / (v.rows - 1);
-    if (per_cu <= 0 || grid > (int64_t)per_cu * n_cu) continue;
+    if (vs.per_cu <= 0 || grid > (int64_t)vs.per_cu * n_cu) continue;
     a.QL = QL;
     hipStream_t s = (hipStream_t)stream;
     HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kBarWords, s));

@@ -9,6 +9,11 @@ Reference: train_ecg_kan_fet_nn_ode.py
   * No_MLP_KANODEFunc      :483-509  dh/dt = Linear(KANFeatureMixer(h))   (the dopri5 field)
   * KanFet_NODE            :512-572  encoder Linear -> odeint(dopri5, [0, 1]) -> dropout ->
                                     KANFeatureMixer -> Linear
+Reference: train_ecg.py (the FerroElectricNet field)
+  * KANFetODEFunc          :986-1013  h_bound tanh(h / h_bound) -> FerroelectricBasis(latent ->
+                                    hidden, K) -> tanh -> FerroelectricBasis(hidden -> latent, K)
+                                    -> nan_to_num -> clamp(-50, 50)
+  * KanFet_MLP_NODE        :1017-1059 per-row batch-1 solves, classifier of the last row
 
 Same constructor arguments, parameter names / shapes / init RNG order, buffers (prev_x (1, in,
 nb); branch_state, rebound to (B, in, nb) by every call like the reference) and error types.
@@ -24,6 +29,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
+from .ferro_class import FerroelectricBasis
 from .odeint import odeint
 
 _PARAMS = ("k", "Ec", "Ps", "bias")
@@ -215,7 +221,9 @@ class KanFet_NODE(nn.Module):
     def forward(self, x):
         _lib.require_gpu_tensor(x, "KanFet_NODE.forward")
         h0 = self.encoder(x)
-        t_eval = torch.tensor([0.0, 1.0], device=x.device, dtype=x.dtype)
+        # the reference builds t on x's device; odeint reads the grid on the host, so it is built
+        # there (same values and dtype, no device round trip)
+        t_eval = torch.tensor([0.0, 1.0], dtype=x.dtype)
         h_traj = odeint(self.odefunc, h0, t_eval, method=self.solver, rtol=self.rtol, atol=self.atol)
         if self.solver == "dopri5":
             from .dopri5 import dopri5_solve
@@ -224,3 +232,138 @@ class KanFet_NODE(nn.Module):
         hT = self.dropout(hT)
         feat = self.cls_feat(hT)
         return self.cls(feat)
+
+
+# ---------------------------------------------------------------------------------------------
+# The FerroElectricNet field of train_ecg.py: FerroelectricBasis layers (HIP, fetode_ferro_*)
+# joined by HIP elementwise stages (fetode_ferronet.hip) with HIP VJPs
+# ---------------------------------------------------------------------------------------------
+
+class _TanhBoundFn(torch.autograd.Function):
+    """h_bound * tanh(h / h_bound) (train_ecg.py:1002)."""
+
+    @staticmethod
+    def forward(ctx, x, hb, training):
+        lib = _lib.load()
+        xc = _lib.f32c(x)
+        out = torch.empty_like(xc)
+        t = torch.empty_like(xc) if training else None
+        _lib.check(lib.fetode_tanh_bound(xc.numel(), float(hb), xc.data_ptr(), out.data_ptr(), _lib.ptr(t),
+                                         _stream(xc)), "KANFetODEFunc h_bound")
+        if training:
+            ctx.save_for_backward(t)
+            ctx.hb = hb
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (t,) = ctx.saved_tensors
+        gc = _lib.f32c(g)
+        gx = torch.empty_like(gc)
+        _lib.check(_lib.load().fetode_tanh_bound_backward(gc.numel(), float(ctx.hb), gc.data_ptr(), t.data_ptr(),
+                                                          gx.data_ptr(), _stream(gc)), "KANFetODEFunc h_bound backward")
+        return gx, None, None
+
+
+class _TanhFn(torch.autograd.Function):
+    """nn.Tanh between the Ferro layers (:1004)."""
+
+    @staticmethod
+    def forward(ctx, x, training):
+        xc = _lib.f32c(x)
+        out = torch.empty_like(xc)
+        _lib.check(_lib.load().fetode_tanh(xc.numel(), xc.data_ptr(), out.data_ptr(), _stream(xc)), "tanh")
+        if training:
+            ctx.save_for_backward(out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (y,) = ctx.saved_tensors
+        gc = _lib.f32c(g)
+        gx = torch.empty_like(gc)
+        _lib.check(_lib.load().fetode_tanh_backward(gc.numel(), gc.data_ptr(), y.data_ptr(), gx.data_ptr(),
+                                                    _stream(gc)), "tanh backward")
+        return gx, None
+
+
+_NAN_CLAMP = (0.0, 1e3, -1e3, -50.0, 50.0)   # nan_to_num(nan, posinf, neginf), clamp(lo, hi): :1008-1011
+
+
+class _NanClampFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, training):
+        xc = _lib.f32c(x)
+        out = torch.empty_like(xc)
+        _lib.check(_lib.load().fetode_nan_clamp(xc.numel(), *_NAN_CLAMP, xc.data_ptr(), out.data_ptr(), _stream(xc)),
+                   "nan_to_num / clamp")
+        if training:
+            ctx.save_for_backward(xc)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        gc = _lib.f32c(g)
+        gx = torch.empty_like(gc)
+        _lib.check(_lib.load().fetode_nan_clamp_backward(gc.numel(), *_NAN_CLAMP, gc.data_ptr(), x.data_ptr(),
+                                                         gx.data_ptr(), _stream(gc)), "nan_to_num / clamp backward")
+        return gx, None
+
+
+def _grad_on(x):
+    return torch.is_grad_enabled() and x.requires_grad
+
+
+class KANFetODEFunc(nn.Module):
+    """train_ecg.py:986-1013 (compare_noise_ecg.py:1561-1588): the FerroElectricNet ODE field.
+    fc1 / fc2 are the drop-in FerroelectricBasis (same RNG order, buffers and state rules)."""
+
+    def __init__(self, latent_dim: int, hidden_dim: int, num_basis: int, h_bound: float = 1.0):
+        super().__init__()
+        self.h_bound = h_bound
+        self.fc1 = FerroelectricBasis(latent_dim, hidden_dim, num_basis)
+        self.act = nn.Tanh()
+        self.fc2 = FerroelectricBasis(hidden_dim, latent_dim, num_basis)
+
+    def forward(self, t, h):
+        if h.dim() == 1:
+            h = h.unsqueeze(0)
+        _lib.require_gpu_tensor(h, "KANFetODEFunc.forward")
+        h = _TanhBoundFn.apply(h, float(self.h_bound), _grad_on(h))
+        z = self.fc1(h)
+        z = _TanhFn.apply(z, _grad_on(z)) if isinstance(self.act, nn.Tanh) else self.act(z)
+        dh = self.fc2(z)
+        return _NanClampFn.apply(dh, _grad_on(dh))
+
+
+class KanFet_MLP_NODE(nn.Module):
+    """train_ecg.py:1017-1059, as the reference runs it: every row is solved on its own with batch
+    1 (the Ferro state carries from row to row) and the classifier of the LAST row's h(1) is
+    returned, shape (1, num_classes)."""
+
+    def __init__(self, T: int, num_classes: int, latent_dim: int = 64, num_basis: int = 10,
+                 ode_hidden: int = 128, dropout: float = 0.1, solver: str = "dopri5", rtol: float = 1e-3,
+                 atol: float = 1e-4):
+        super().__init__()
+        self.T = T
+        self.num_classes = num_classes
+        self.latent_dim = latent_dim
+        self.solver = solver
+        self.rtol = rtol
+        self.atol = atol
+        self.encoder = nn.Linear(T, latent_dim)
+        self.odefunc = KANFetODEFunc(latent_dim=latent_dim, hidden_dim=ode_hidden, num_basis=num_basis)
+        self.dropout = nn.Dropout(dropout)
+        self.cls = nn.Linear(latent_dim, num_classes)
+
+    def forward(self, x):
+        _lib.require_gpu_tensor(x, "KanFet_MLP_NODE.forward")
+        h0 = self.encoder(x)
+        t = torch.tensor([0.0, 1.0], dtype=x.dtype)   # host grid: same values as the reference's
+        for b in range(x.size(0)):
+            xb = x[b:b + 1]
+            h0 = self.encoder(xb)
+            hT = odeint(self.odefunc, h0, t, method=self.solver, rtol=self.rtol, atol=self.atol)[-1]
+            hT = self.dropout(hT)
+        return self.cls(hT)

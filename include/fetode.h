@@ -267,18 +267,37 @@ int fetode_hlogistic_mixer_backward(const fetode_hlogistic_t* layer, const float
  *   prev (in*nb) prev_x before the solve; y0 (B, D); t (dev, fp64, T) strictly increasing;
  *   opts (host, 7 doubles): first_step (<= 0: select), safety, ifactor, dfactor, min_step,
  *   max_step, max_num_steps; tableau (host, 50 floats): beta[6][6], c_err[7], c_mid[7] in fp32;
- *   solution (T, B, D); prev_out (in*nb, must not alias prev) = prev_x after the solve;
+ *   solution (T, B, D); prev_out (in*nb, may alias prev: prev is read before the first
+ *   evaluation, prev_out written after the last) = prev_x after the solve;
  *   branch_out (B, in*nb, nullable) = branch_state of the last evaluation;
  *   workspace: fetode_ecg_dopri5_workspace(B) bytes; stats (dev, 3 ints) = nfev, attempts,
  *   status (0 ok, 1 non-finite state, 2 dt underflow, 3 max_num_steps);
  *   attempts (dev, nullable) (max_attempts, 4) doubles: t0, dt, error ratio, accepted.
- * FETODE_EUNSUPPORTED when B needs more than one cooperative grid (B > 3072). */
+ * FETODE_EUNSUPPORTED when B or in*nb need more than one co-resident grid (B > 7 * 256 at
+ * in*nb = 640 on MI355X: 3 rows + a shadow row per 512-thread workgroup up to B = 768, 7 + 1
+ * beyond); the caller then takes the host-driven loop. */
 int fetode_ecg_dopri5(const fetode_hlogistic_t* layer, const float* wT, const float* bias, int32_t D,
                       const float* prev, const float* y0, int64_t B, const double* t, int32_t T, double rtol,
                       double atol, const double* opts, const float* tableau, float* solution, float* prev_out,
                       float* branch_out, void* workspace, int32_t* stats, double* attempts, int32_t max_attempts,
                       void* stream);
 int64_t fetode_ecg_dopri5_workspace(int64_t B);
+
+/* Elementwise stages of the ECG FerroElectricNet field KANFetODEFunc (train_ecg.py:986-1013; the
+ * two FerroelectricBasis layers are fetode_ferro_forward / _backward), in torch's op order:
+ *   fetode_tanh_bound: out = h_bound * tanh(x / h_bound) (:1002); t_out (nullable) keeps the tanh
+ *   for the backward, gx = ((g * h_bound) * (1 - t^2)) / h_bound;
+ *   fetode_tanh: nn.Tanh between the layers (:1004), gx = g * (1 - y^2);
+ *   fetode_nan_clamp: clamp(nan_to_num(x, nan, posinf, neginf), lo, hi) (:1008-1011),
+ *   gx = g where x is finite and lo <= nan_to_num(x) <= hi, else 0. */
+int fetode_tanh_bound(int64_t n, float h_bound, const float* x, float* out, float* t_out, void* stream);
+int fetode_tanh_bound_backward(int64_t n, float h_bound, const float* g, const float* t, float* gx, void* stream);
+int fetode_tanh(int64_t n, const float* x, float* out, void* stream);
+int fetode_tanh_backward(int64_t n, const float* g, const float* y, float* gx, void* stream);
+int fetode_nan_clamp(int64_t n, float nan, float posinf, float neginf, float lo, float hi, const float* x, float* out,
+                     void* stream);
+int fetode_nan_clamp_backward(int64_t n, float nan, float posinf, float neginf, float lo, float hi, const float* g,
+                              const float* x, float* gx, void* stream);
 
 #ifdef __cplusplus
 }

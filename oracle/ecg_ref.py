@@ -116,6 +116,61 @@ class ECGNodeRef:
         return F.linear(feat, self.cls_w, self.cls_b)
 
 
+def _ferro_from_sd(sd, prefix):
+    p = O.FerroParams.from_state_dict(sd, prefix)
+    st = O.FerroState(*p.k.shape, dtype=p.k.dtype)
+    if prefix + "prev_x" in sd:
+        st.prev_x = sd[prefix + "prev_x"].clone()
+    if prefix + "branch_sign" in sd:
+        st.branch_sign = sd[prefix + "branch_sign"].clone()
+    return p, st
+
+
+class FerroNetFieldRef:
+    """KANFetODEFunc (train_ecg.py:986-1013; the same class at compare_noise_ecg.py:1561-1588):
+    h_bound * tanh(h / h_bound) -> FerroelectricBasis(latent -> hidden) -> tanh ->
+    FerroelectricBasis(hidden -> latent) -> nan_to_num(0, 1e3, -1e3) -> clamp(-50, 50)."""
+
+    def __init__(self, p1, st1, p2, st2, h_bound=1.0):
+        self.p1, self.st1, self.p2, self.st2, self.h_bound = p1, st1, p2, st2, h_bound
+
+    @classmethod
+    def from_state_dict(cls, sd, prefix="", h_bound=1.0):
+        p1, st1 = _ferro_from_sd(sd, prefix + "fc1.")
+        p2, st2 = _ferro_from_sd(sd, prefix + "fc2.")
+        return cls(p1, st1, p2, st2, h_bound)
+
+    def __call__(self, t, h):
+        if h.dim() == 1:
+            h = h.unsqueeze(0)
+        h = self.h_bound * torch.tanh(h / self.h_bound)
+        z = O.ferro_forward(h, self.p1, self.st1)
+        z = torch.tanh(z)
+        dh = O.ferro_forward(z, self.p2, self.st2)
+        dh = torch.nan_to_num(dh, nan=0.0, posinf=1e3, neginf=-1e3)
+        return torch.clamp(dh, -50.0, 50.0)
+
+
+class FerroNetNodeRef:
+    """KanFet_MLP_NODE.forward (train_ecg.py:1043-1059) in eval mode: the reference solves each row
+    on its own (batch 1, so the Ferro state carries from row to row) and returns the classifier
+    of the LAST row's h(1) only, shape (1, num_classes)."""
+
+    def __init__(self, sd, solver="dopri5", rtol=1e-3, atol=1e-4, h_bound=1.0):
+        self.enc_w, self.enc_b = sd["encoder.weight"], sd["encoder.bias"]
+        self.field = FerroNetFieldRef.from_state_dict(sd, "odefunc.", h_bound)
+        self.cls_w, self.cls_b = sd["cls.weight"], sd["cls.bias"]
+        self.solver, self.rtol, self.atol = solver, rtol, atol
+
+    def __call__(self, x):
+        h0 = F.linear(x, self.enc_w, self.enc_b)   # :1044, unused like the reference's
+        t = torch.tensor([0.0, 1.0], dtype=x.dtype)
+        for b in range(x.size(0)):
+            h0 = F.linear(x[b:b + 1], self.enc_w, self.enc_b)
+            hT = O.odeint(self.field, h0, t, method=self.solver, rtol=self.rtol, atol=self.atol)[-1]
+        return F.linear(hT, self.cls_w, self.cls_b)
+
+
 def ecg_x(batch: int, T: int = 96, seed: int = 0, dtype=torch.float32) -> torch.Tensor:
     """Synthetic ECG200-shaped series (the dataset is not in the image): a seeded sum of two
     sinusoids + noise per row, z-normalised like the UCR files (T = 96)."""

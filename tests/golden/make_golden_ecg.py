@@ -1,4 +1,5 @@
-"""Generate tests/golden/ecg_*.npz from the REFERENCE's ECG KAN-FET NODE classes.
+"""Generate tests/golden/ecg_*.npz from the REFERENCE's ECG KAN-FET NODE classes (and the
+FerroElectricNet field of train_ecg.py).
 
 Run in the survey/build container (needs /root/reference; never on the GPU box):
 
@@ -41,6 +42,23 @@ def reference_classes():
     assert [n.name for n in body] == list(CLASSES), [n.name for n in body]
     ns = {"torch": torch, "nn": nn, "F": F, "odeint": O.odeint}
     exec(compile(ast.Module(body=body, type_ignores=[]), "train_ecg_kan_fet_nn_ode.py", "exec"), ns)
+    return ns
+
+
+FERRONET_CLASSES = ("KANFetODEFunc", "KanFet_MLP_NODE")
+
+
+def ferronet_classes():
+    """train_ecg.py:986-1059 (KANFetODEFunc, KanFet_MLP_NODE) the same way; their
+    FerroelectricBasis is the reference's own ferro_class module (importable here)."""
+    sys.path.insert(0, REF)
+    import ferro_class  # noqa: E402  (the reference module)
+    src = open(os.path.join(REF, "train_ecg.py")).read()
+    tree = ast.parse(src)
+    body = [n for n in tree.body if isinstance(n, ast.ClassDef) and n.name in FERRONET_CLASSES]
+    assert [n.name for n in body] == list(FERRONET_CLASSES), [n.name for n in body]
+    ns = {"torch": torch, "nn": nn, "F": F, "odeint": O.odeint, "FerroelectricBasis": ferro_class.FerroelectricBasis}
+    exec(compile(ast.Module(body=body, type_ignores=[]), "train_ecg.py", "exec"), ns)
     return ns
 
 
@@ -127,8 +145,76 @@ def node_case(R, latent, nb, rtol, atol, B, seed):
     return out
 
 
+def ferronet_field_case(R):
+    out = {}
+    g = torch.Generator().manual_seed(21)
+    t = torch.tensor(0.0)
+    # batch calls (the B > 1 first-call rule dx = 0), then a carried-state call with gradients
+    torch.manual_seed(11)
+    f = R["KANFetODEFunc"](latent_dim=8, hidden_dim=16, num_basis=12)
+    out.update(sd_np(f, "sd_a/"))
+    ref = E.FerroNetFieldRef.from_state_dict({k: v.clone() for k, v in f.state_dict().items()})
+    h1 = torch.randn(4, 8, generator=g) * 1.5
+    h2 = (h1 + 0.1 * torch.randn(4, 8, generator=g)).requires_grad_(True)
+    y1 = f(t, h1)
+    same(y1, ref(t, h1), "ferronet call 1")
+    y2 = f(t, h2)
+    same(y2, ref(t, h2.detach()), "ferronet call 2")
+    w = torch.randn(4, 8, generator=g)
+    (y2 * w).sum().backward()
+    out.update({"a/h1": h1.numpy(), "a/h2": h2.detach().numpy(), "a/y1": y1.detach().numpy(),
+                "a/y2": y2.detach().numpy(), "a/w": w.numpy(), "a/grad/h": h2.grad.numpy()})
+    for n, prm in f.named_parameters():
+        out["a/grad/" + n] = prm.grad.numpy()
+    # batch-1 calls (fresh buffers keep their (1, in, out, K) zeros: dx = x), incl. a 1-D h
+    torch.manual_seed(12)
+    f = R["KANFetODEFunc"](latent_dim=8, hidden_dim=16, num_basis=12)
+    out.update(sd_np(f, "sd_b/"))
+    ref = E.FerroNetFieldRef.from_state_dict({k: v.clone() for k, v in f.state_dict().items()})
+    for c in range(3):
+        h = torch.randn(8, generator=g) * 1.5 if c == 1 else torch.randn(1, 8, generator=g) * 1.5
+        y = f(t, h)
+        same(y, ref(t, h), f"ferronet b1 call {c}")
+        out[f"b/h{c}"], out[f"b/y{c}"] = h.numpy(), y.detach().numpy()
+    # saturating field: coef x 8 drives fc2 past the +-50 clamp; gradients stop there
+    torch.manual_seed(13)
+    f = R["KANFetODEFunc"](latent_dim=8, hidden_dim=16, num_basis=12)
+    with torch.no_grad():
+        f.fc2.coef.mul_(8.0)
+    out.update(sd_np(f, "sd_c/"))
+    ref = E.FerroNetFieldRef.from_state_dict({k: v.clone() for k, v in f.state_dict().items()})
+    h = (torch.randn(5, 8, generator=g) * 2).requires_grad_(True)
+    y = f(t, h)
+    same(y, ref(t, h.detach()), "ferronet saturating call")
+    assert bool((y.abs() == 50).any()), "clamp not exercised"
+    w = torch.randn(5, 8, generator=g)
+    (y * w).sum().backward()
+    out.update({"c/h": h.detach().numpy(), "c/y": y.detach().numpy(), "c/w": w.numpy(), "c/grad/h": h.grad.numpy()})
+    for n, prm in f.named_parameters():
+        out["c/grad/" + n] = prm.grad.numpy()
+    return out
+
+
+def ferronet_node_case(R, solver, B, seed, rtol=1e-3, atol=1e-4):
+    torch.manual_seed(seed)
+    m = R["KanFet_MLP_NODE"](T=96, num_classes=2, latent_dim=8, num_basis=12, ode_hidden=16, dropout=0.1,
+                             solver=solver, rtol=rtol, atol=atol)
+    m.eval()
+    out = sd_np(m)
+    ref = E.FerroNetNodeRef({k: v.clone() for k, v in m.state_dict().items()}, solver=solver, rtol=rtol, atol=atol)
+    x = E.ecg_x(B, seed=seed)
+    with torch.no_grad():
+        logits = m(x)
+        lo = ref(x)
+    same(logits, lo, f"ferronet node {solver}")
+    out.update({"x": x.numpy(), "logits": logits.numpy(), "rtol": np.array(rtol), "atol": np.array(atol),
+                "fc1_prev_x": m.odefunc.fc1.prev_x.numpy().copy(), "fc2_prev_x": m.odefunc.fc2.prev_x.numpy().copy()})
+    return out
+
+
 def main():
     R = reference_classes()
+    RF = ferronet_classes()
     cases = {
         "ecg_hlogistic": hlogistic_case(R),
         "ecg_field": field_case(R),
@@ -136,6 +222,11 @@ def main():
         # (latent 1, nb 12, rtol 1e-2 atol 1e-3, :1181-1198)
         "ecg_node64": node_case(R, 64, 10, 1e-3, 1e-4, 16, 7),
         "ecg_node1": node_case(R, 1, 12, 1e-2, 1e-3, 16, 8),
+        # the FerroElectricNet field (train_ecg.py:986-1013) and its NODE (:1017-1059): __main__
+        # runs it with euler (:1365); dopri5 is the class default
+        "ecg_ferronet_field": ferronet_field_case(RF),
+        "ecg_ferronet_euler": ferronet_node_case(RF, "euler", 3, 31),
+        "ecg_ferronet_dopri5": ferronet_node_case(RF, "dopri5", 2, 32),
     }
     for name, d in cases.items():
         np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)

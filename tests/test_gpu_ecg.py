@@ -236,3 +236,133 @@ def test_resident_dopri5_nonfinite_raises(dev):
     h0[3, 2] = float("nan")
     with torch.no_grad(), pytest.raises(AssertionError):
         F.odeint(m, h0, torch.tensor([0.0, 1.0]), method="dopri5", options={"first_step": 0.1})
+
+
+# ---------------------------------------------------------------------------------------------
+# The FerroElectricNet field of train_ecg.py (KANFetODEFunc)
+# ---------------------------------------------------------------------------------------------
+
+def _ferronet(sd, latent, hidden, K, dev):
+    from fet_ode_amd import ecg
+    f = ecg.KANFetODEFunc(latent_dim=latent, hidden_dim=hidden, num_basis=K)
+    f.load_state_dict(sd)
+    return f.to(dev)
+
+
+def test_ferronet_field_calls_and_grads(dev):
+    """KANFetODEFunc vs the reference class (fixture): batch calls (B > 1 first-call rule), a
+    carried-state call with every parameter gradient, batch-1 calls incl. a 1-D h, and a field
+    that saturates the +-50 clamp (clamped outputs pass no gradient)."""
+    g = load_golden("ecg_ferronet_field")
+    t = torch.tensor(0.0)
+    f = _ferronet(golden_sd(g, "sd_a/"), 8, 16, 12, dev)
+    with torch.no_grad():
+        close(f(t, torch.from_numpy(g["a/h1"]).to(dev)), torch.from_numpy(g["a/y1"]), 1e-5, "a/y1")
+    h2 = torch.from_numpy(g["a/h2"]).to(dev).requires_grad_(True)
+    y2 = f(t, h2)
+    close(y2, torch.from_numpy(g["a/y2"]), 1e-5, "a/y2")
+    (y2 * torch.from_numpy(g["a/w"]).to(dev)).sum().backward()
+    close(h2.grad, torch.from_numpy(g["a/grad/h"]), 1e-4, "a/grad/h")
+    for n, p in f.named_parameters():
+        close(p.grad, torch.from_numpy(g["a/grad/" + n]), 2e-4, "a/grad/" + n)
+    f = _ferronet(golden_sd(g, "sd_b/"), 8, 16, 12, dev)
+    with torch.no_grad():
+        for c in range(3):
+            y = f(t, torch.from_numpy(g[f"b/h{c}"]).to(dev))
+            assert y.shape == (1, 8)
+            close(y, torch.from_numpy(g[f"b/y{c}"]), 1e-5, f"b/y{c}")
+    f = _ferronet(golden_sd(g, "sd_c/"), 8, 16, 12, dev)
+    h = torch.from_numpy(g["c/h"]).to(dev).requires_grad_(True)
+    y = f(t, h)
+    yc = torch.from_numpy(g["c/y"])
+    close(y, yc, 1e-5, "c/y")
+    assert torch.equal(y.detach().cpu().abs() == 50, yc.abs() == 50)
+    (y * torch.from_numpy(g["c/w"]).to(dev)).sum().backward()
+    close(h.grad, torch.from_numpy(g["c/grad/h"]), 1e-4, "c/grad/h")
+    for n, p in f.named_parameters():
+        close(p.grad, torch.from_numpy(g["c/grad/" + n]), 2e-4, "c/grad/" + n)
+
+
+@pytest.mark.parametrize("name,solver", [("ecg_ferronet_euler", "euler"), ("ecg_ferronet_dopri5", "dopri5")])
+def test_ferronet_node_vs_reference(dev, name, solver):
+    """KanFet_MLP_NODE.eval(): per-row batch-1 solves with the Ferro state carried across rows,
+    the last row's logits and both layers' prev_x after the forward."""
+    from fet_ode_amd import ecg
+    g = load_golden(name)
+    m = ecg.KanFet_MLP_NODE(T=96, num_classes=2, latent_dim=8, num_basis=12, ode_hidden=16, solver=solver,
+                            rtol=float(g["rtol"]), atol=float(g["atol"]))
+    m.load_state_dict(golden_sd(g))
+    m = m.to(dev).eval()
+    with torch.no_grad():
+        lo = m(torch.from_numpy(g["x"]).to(dev))
+    assert lo.shape == (1, 2)
+    # bound: 1e-5 relative, or 4x the reference's own fp32-vs-fp64 spread (the oracle in fp64 on
+    # the same weights): error-controlled dopri5 steps through the hysteresis amplify rounding
+    # (fc1 prev_x: 1.9e-5 between the reference's fp32 and fp64 runs of this case)
+    from oracle import ecg_ref as E
+    r64 = E.FerroNetNodeRef({k: v.double() for k, v in golden_sd(g).items()}, solver=solver,
+                            rtol=float(g["rtol"]), atol=float(g["atol"]))
+    with torch.no_grad():
+        l64 = r64(torch.from_numpy(g["x"]).double())
+    for got, key, e64 in ((lo, "logits", l64), (m.odefunc.fc1.prev_x, "fc1_prev_x", r64.field.st1.prev_x),
+                          (m.odefunc.fc2.prev_x, "fc2_prev_x", r64.field.st2.prev_x)):
+        exp = torch.from_numpy(g[key])
+        spread = (exp.double() - e64).abs().max().item() / (exp.abs().max().item() + 1e-12)
+        close(got, exp, max(1e-5, 4.0 * spread), f"{name} {key}")
+
+
+def _envelope_close(got, e32, e64, name, floor=1e-5, k=4.0):
+    """|got - fp64| <= k * |fp32 reference - fp64| + floor * scale, elementwise maximum: the GPU
+    must be as accurate as the reference's own fp32 arithmetic, within a factor k."""
+    got, e32, e64 = got.detach().double().cpu(), e32.detach().double().cpu(), e64.detach().double().cpu()
+    scale = e64.abs().max().item() + 1e-12
+    spread = (e32 - e64).abs().max().item()
+    err = (got - e64).abs().max().item()
+    assert err <= k * spread + floor * scale, f"{name}: |gpu-fp64|={err:.3e} fp32 spread={spread:.3e} scale={scale:.3e}"
+
+
+def test_ferronet_production_width_vs_oracle(dev):
+    """The train_ecg.py __main__ widths (latent 64, hidden 128, K = 12): a batch-200 euler solve on
+    [0, 0.5, 1] (stateful field calls through the solver) and the gradients of a loss on a batch-32
+    call, against the oracle in fp64 with the reference's own fp32 error as the yardstick (sums of
+    768 / 1536 Ferro terms of size ~3: the CPU fp32 run is 9e-4 from fp64 on a scale of 53)."""
+    from fet_ode_amd import ecg
+    import fet_ode_amd as F
+    from oracle import ecg_ref as E
+    from oracle import torch_ref as O
+    torch.manual_seed(41)
+    f = ecg.KANFetODEFunc(latent_dim=64, hidden_dim=128, num_basis=12)
+    sd = {k: v.clone() for k, v in f.state_dict().items()}
+    f = f.to(dev)
+    gen = torch.Generator().manual_seed(42)
+    h0 = torch.randn(200, 64, generator=gen)
+    t = torch.tensor([0.0, 0.5, 1.0])
+    r32 = E.FerroNetFieldRef.from_state_dict({k: v.clone() for k, v in sd.items()})
+    r64 = E.FerroNetFieldRef.from_state_dict({k: v.double() for k, v in sd.items()})
+    with torch.no_grad():
+        sol = F.odeint(f, h0.to(dev), t, method="euler")
+        s32 = O.odeint(r32, h0, t, method="euler")
+        s64 = O.odeint(r64, h0.double(), t.double(), method="euler")
+    _envelope_close(sol, s32, s64, "euler solution")
+    _envelope_close(f.fc1.prev_x[:, :, :1, :1], r32.st1.prev_x[:, :, :1, :1], r64.st1.prev_x[:, :, :1, :1],
+                    "fc1 prev_x")
+    # gradients on a fresh batch-32 module pair (first call: dx = 0)
+    f = ecg.KANFetODEFunc(latent_dim=64, hidden_dim=128, num_basis=12)
+    f.load_state_dict(sd)
+    f = f.to(dev)
+    h1 = torch.randn(32, 64, generator=gen)
+    w = torch.randn(32, 64, generator=gen)
+    hd = h1.to(dev).requires_grad_(True)
+    (f(torch.tensor(0.0), hd) * w.to(dev)).sum().backward()
+    grads = {}
+    for dt in (torch.float32, torch.float64):
+        ps = {k: v.detach().to(dt).clone().requires_grad_("prev_x" not in k and "branch_sign" not in k)
+              for k, v in sd.items()}
+        hh = h1.detach().to(dt).clone().requires_grad_(True)
+        (E.FerroNetFieldRef.from_state_dict(ps)(torch.tensor(0.0), hh) * w.to(dt)).sum().backward()
+        grads[dt] = {"h": hh.grad, **{k: v.grad for k, v in ps.items() if v.grad is not None}}
+    _envelope_close(hd.grad, grads[torch.float32]["h"], grads[torch.float64]["h"], "grad h")
+    missing = [n for n, p in f.named_parameters() if p.grad is None or n not in grads[torch.float64]]
+    assert not missing, (missing, sorted(grads[torch.float64]))
+    for n, p in f.named_parameters():
+        _envelope_close(p.grad, grads[torch.float32][n], grads[torch.float64][n], "grad " + n)
