@@ -368,6 +368,9 @@ __device__ __forceinline__ float fast_sigmoid(float z) { return rcp(1.0f + ex2(-
 // Release before arriving, acquire after: the partial slots written before the barrier are
 // visible after it.  Counters reset themselves; the words are zeroed once per launch.
 constexpr int kBarWords = 64 * 10;  // 8 XCD counters, top counter, generation (256 B each)
+// Every spin is bounded (MI355X_MICROARCH.md: a stranded workgroup must not hang the device): after
+// 2^20 polls (about a second) the barrier gives up and raises word 64*9+1, which the host reports.
+constexpr unsigned kSpinLimit = 1u << 20;
 __device__ void grid_barrier(unsigned* bar, unsigned nblk) {
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -385,7 +388,14 @@ __device__ void grid_barrier(unsigned* bar, unsigned nblk) {
         __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) __builtin_amdgcn_s_sleep(1);
+    unsigned spins = 0;
+    while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins == kSpinLimit) {
+        __hip_atomic_store(gen + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   __syncthreads();
@@ -754,7 +764,7 @@ __global__ __launch_bounds__(kResThreads) void ecg_dopri5_kernel(EcgDopriArgs a)
   if (blockIdx.x == 0 && tid == 0) {
     a.stats[0] = nfev;
     a.stats[1] = n_att;
-    a.stats[2] = status;
+    a.stats[2] = __hip_atomic_load(a.bar + 64 * 9 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 4 : status;
 #ifdef FETODE_STAMPS
     if (stamping) {
       for (int i = 0; i < 5; ++i) a.stamps[i] += st_acc[i];
@@ -848,8 +858,6 @@ int fetode_ecg_dopri5(const fetode_hlogistic_t* layer, const float* wT, const fl
     if (vs.static_lds < 0) {
       hipFuncAttributes fa;
       HIP_CHECK_RET(hipFuncGetAttributes(&fa, v.fn));
-      HIP_CHECK_RET(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        kLdsBytes - (int)fa.sharedSizeBytes));
       vs.static_lds = (int)fa.sharedSizeBytes;
     }
     // phi (R, Fp) + the (groups, R, 64) head sums; feature parameters; W^T in the rest
@@ -861,13 +869,16 @@ int fetode_ecg_dopri5(const fetode_hlogistic_t* layer, const float* wT, const fl
     if (a.PS - QL > v.tail) continue;
     const size_t lds = (size_t)kHeadParts * QL * 64 * sizeof(float) + (size_t)(prm_bytes + phi_bytes);
     if (vs.lds != lds) {
+      HIP_CHECK_RET(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
       int per_cu = 0;
       HIP_CHECK_RET(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, v.fn, kResThreads, lds));
       vs.lds = lds;
       vs.per_cu = per_cu;
     }
     const int64_t grid = (B + v.rows - 2) / (v.rows - 1);
-    if (vs.per_cu <= 0 || grid > (int64_t)vs.per_cu * n_cu) continue;
+    // one workgroup per CU below the API's answer when it admits several (it can be one too high)
+    const int per_cu = vs.per_cu > 1 ? vs.per_cu - 1 : vs.per_cu;
+    if (per_cu <= 0 || grid > (int64_t)per_cu * n_cu) continue;
     a.QL = QL;
     hipStream_t s = (hipStream_t)stream;
     HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kBarWords, s));

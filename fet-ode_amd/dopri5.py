@@ -15,6 +15,7 @@ to the host, as torchdiffeq does (`if accept_step:` on a 0-dim tensor).
 """
 from __future__ import annotations
 
+import atexit
 import math
 
 import numpy as np
@@ -250,6 +251,9 @@ class ResidentSolve:
 
 
 _T_DEV = {}   # (device, time grid) -> the grid as a device fp64 tensor
+# dropped at interpreter exit, before module teardown: device memory freed after the runtime's
+# (or a profiler's) own exit handlers have run crashes the process
+atexit.register(_T_DEV.clear)
 
 
 def _try_ecg_resident(func, y0, tp, reversed_, rtol, atol, options):
@@ -317,6 +321,9 @@ def _try_ecg_resident(func, y0, tp, reversed_, rtol, atol, options):
         raise AssertionError("underflow in dt")
     if status == 3:
         raise AssertionError("max_num_steps exceeded")
+    if status == 4:
+        raise RuntimeError("fetode_ecg_dopri5: a grid barrier timed out (workgroups not co-resident); "
+                           "the solution is invalid")
     dopri5_solve.last = ResidentSolve(stats, att)
     return sol
 

@@ -271,7 +271,8 @@ int fetode_hlogistic_mixer_backward(const fetode_hlogistic_t* layer, const float
  *   evaluation, prev_out written after the last) = prev_x after the solve;
  *   branch_out (B, in*nb, nullable) = branch_state of the last evaluation;
  *   workspace: fetode_ecg_dopri5_workspace(B) bytes; stats (dev, 3 ints) = nfev, attempts,
- *   status (0 ok, 1 non-finite state, 2 dt underflow, 3 max_num_steps);
+ *   status (0 ok, 1 non-finite state, 2 dt underflow, 3 max_num_steps, 4 a grid barrier timed
+ *   out: the grid was not co-resident and the outputs are invalid);
  *   attempts (dev, nullable) (max_attempts, 4) doubles: t0, dt, error ratio, accepted.
  * FETODE_EUNSUPPORTED when B or in*nb need more than one co-resident grid (B > 7 * 256 at
  * in*nb = 640 on MI355X: 3 rows + a shadow row per 512-thread workgroup up to B = 768, 7 + 1
