@@ -100,8 +100,9 @@ class _Dopri5:
         tt = torch.tensor(self.sign * t, dtype=torch.float64).to(y.dtype)
         out = self.func_user(tt, y.view_as(self.y0))
         if torch.is_grad_enabled() and out.requires_grad:
-            raise NotImplementedError("backpropagation through the GPU dopri5 solver is not built yet; "
-                                      "use method='rk4' for training, or torch.no_grad() for inference")
+            raise RuntimeError("the field's output requires grad but the solve was started without "
+                               "autograd (a module without trainable parameters closing over trainable "
+                               "tensors?); run it with torch.enable_grad()")
         _lib.require_gpu_tensor(out, "odeint func output")
         out = out.reshape(-1)
         if self.sign < 0:
@@ -338,11 +339,147 @@ def set_resident_dopri5(enabled: bool) -> bool:
     return prev
 
 
+class _Dopri5Grad:
+    """dopri5 with torchdiffeq's direct backpropagation (no adjoint): the solve is recorded by
+    autograd through every stage of every attempt, the RMS error ratios and the adaptive step
+    sizes (rk_common._optimal_step_size and misc._select_initial_step are tensor expressions in
+    torchdiffeq, so d(loss)/d(theta) includes d(dt)/d(theta)).  Same control flow and call order
+    as _Dopri5; the field's own HIP VJP serves each evaluation, the O(B*D) stage algebra is torch
+    on the device, and t / dt are float64 device tensors like torchdiffeq's."""
+
+    def __init__(self, func, y0, rtol, atol, options, reversed_):
+        unsupported = [k for k in ("step_t", "jump_t", "norm", "perturb", "norm_group") if options.get(k) is not None]
+        if unsupported:
+            raise NotImplementedError(f"dopri5 options not supported with autograd: {unsupported}")
+        self.func_user, self.sign, self.y0 = func, (-1.0 if reversed_ else 1.0), y0
+        self.dev, self.sdt = y0.device, y0.dtype
+        f64 = dict(dtype=torch.float64, device=self.dev)
+        self.rtol, self.atol = torch.as_tensor(rtol, **f64), torch.as_tensor(atol, **f64)
+        self.first_step = options.get("first_step")
+        self.safety = torch.as_tensor(options.get("safety", 0.9), **f64)
+        self.ifactor = torch.as_tensor(options.get("ifactor", 10.0), **f64)
+        self.dfactor = torch.as_tensor(options.get("dfactor", 0.2), **f64)
+        self.min_step = float(options.get("min_step", 0.0))
+        self.max_step = float(options.get("max_step", math.inf))
+        self.max_num_steps = int(options.get("max_num_steps", 2 ** 31 - 1))
+        sd = dict(dtype=self.sdt, device=self.dev)
+        self.alpha = [float(a) for a in A32]
+        self.alpha_t = torch.as_tensor(np.asarray(_A, dtype=np.float64), dtype=torch.float64).to(**sd)
+        self.beta = [torch.as_tensor(np.asarray(b, dtype=np.float64)).to(**sd) for b in _BETA]
+        self.c_err = torch.as_tensor(np.asarray(_C_ERR, dtype=np.float64)).to(**sd)
+        self.c_mid = torch.as_tensor(np.asarray(_C_MID, dtype=np.float64)).to(**sd)
+        self.nfev = 0
+        self.attempts = []
+
+    def f(self, t, y):
+        """_PerturbFunc (t cast to the state dtype) + _ReverseFunc (-f(-t, y))."""
+        self.nfev += 1
+        out = self.func_user((self.sign * t).to(y.dtype), y)
+        _lib.require_gpu_tensor(out, "odeint func output")
+        return -out if self.sign < 0 else out
+
+    @staticmethod
+    def rms(x):
+        return x.abs().pow(2).mean().sqrt()
+
+    def select_initial_step(self, t0, y0, f0):
+        scale = self.atol + torch.abs(y0) * self.rtol
+        d0, d1 = self.rms(y0 / scale).abs(), self.rms(f0 / scale).abs()
+        if d0 < 1e-5 or d1 < 1e-5:
+            h0 = torch.tensor(1e-6, dtype=self.sdt, device=self.dev)
+        else:
+            h0 = 0.01 * d0 / d1
+        h0 = h0.abs()
+        f1 = self.f(t0 + h0, y0 + h0 * f0)
+        d2 = torch.abs(self.rms((f1 - f0) / scale) / h0)
+        if d1 <= 1e-15 and d2 <= 1e-15:
+            h1 = torch.max(torch.tensor(1e-6, dtype=self.sdt, device=self.dev), h0 * 1e-3)
+        else:
+            h1 = (0.01 / max(d1, d2)) ** (1. / float(ORDER))
+        return torch.min(100 * h0, h1.abs()).to(torch.float64)
+
+    def step(self, y0, f0, t0, dt):
+        """One attempt (rk_common._runge_kutta_step): y1, f1, the error estimate and k."""
+        t0c, dtc, t1c = t0.to(self.sdt), dt.to(self.sdt), (t0 + dt).to(self.sdt)
+        ks = [f0]
+        yi = None
+        for s in range(6):
+            ti = t1c if self.alpha[s] == 1.0 else t0c + self.alpha_t[s] * dtc
+            yi = y0 + torch.stack(ks, dim=-1).matmul(self.beta[s] * dtc).view_as(f0)
+            ks.append(self.f(ti, yi))
+        k = torch.stack(ks, dim=-1)
+        return yi, ks[-1], k.matmul(dtc * self.c_err), k
+
+    def optimal_step(self, dt, ratio):
+        if ratio == 0:
+            return dt * self.ifactor
+        dfactor = self.dfactor if ratio >= 1 else torch.ones((), dtype=torch.float64, device=self.dev)
+        er = ratio.type_as(dt)
+        factor = torch.min(self.ifactor, torch.max(self.safety / er ** (1.0 / ORDER), dfactor))
+        return dt * factor
+
+    def integrate(self, tp):
+        t = tp.to(device=self.dev, dtype=torch.float64)
+        y = self.y0
+        sol = [y]
+        f0 = self.f(t[0], y)
+        dt = (torch.as_tensor(float(self.first_step), dtype=torch.float64, device=self.dev)
+              if self.first_step is not None else self.select_initial_step(t[0], y, f0))
+        t0s = t1s = t[0]
+        coeff = [y] * 5
+        for i in range(1, len(t)):
+            n_steps = 0
+            while t[i] > t1s:
+                assert n_steps < self.max_num_steps, "max_num_steps exceeded"
+                t0 = t1s
+                assert t0 + dt > t0, "underflow in dt {}".format(dt.item())
+                assert torch.isfinite(y).all(), "non-finite values in state `y`"
+                y1, f1, err, k = self.step(y, f0, t0, dt)
+                tol = self.atol + self.rtol * torch.max(y.abs(), y1.abs())
+                ratio = self.rms(err / tol)
+                accept = bool(ratio <= 1)
+                self.attempts.append((float(t0.detach()), float(dt.detach()), float(ratio.detach()), accept))
+                if accept:
+                    dtm = dt.type_as(y)
+                    ym = y + k.matmul(dtm * self.c_mid).view_as(y)
+                    fa, fb = k[..., 0], k[..., -1]
+                    coeff = [y, dtm * fa, dtm * (fb - 4 * fa) - 11 * y - 5 * y1 + 16 * ym,
+                             dtm * (5 * fa - 3 * fb) + 18 * y + 14 * y1 - 32 * ym,
+                             2 * dtm * (fb - fa) - 8 * (y1 + y) + 16 * ym]
+                    y, f0, t0s, t1s = y1, f1, t0, t0 + dt
+                else:
+                    t0s = t0
+                dt = self.optimal_step(dt, ratio).clamp(self.min_step, self.max_step)
+                n_steps += 1
+            x = ((t[i] - t0s) / (t1s - t0s)).to(self.sdt)   # interp._interp_evaluate
+            total, xp = coeff[0] + x * coeff[1], x
+            for c in coeff[2:]:
+                xp = xp * x
+                total = total + xp * c
+            sol.append(total)
+        return torch.stack(sol)
+
+
+def _needs_grad(func, y0) -> bool:
+    if not torch.is_grad_enabled():
+        return False
+    if y0.requires_grad:
+        return True
+    if isinstance(func, torch.nn.Module):
+        return any(p.requires_grad for p in func.parameters())
+    return True   # a plain callable may close over trainable tensors
+
+
 def dopri5_solve(func, y0, tc, tp, reversed_, rtol, atol, options):
     if _RESIDENT:
         sol = _try_ecg_resident(func, y0, tp, reversed_, rtol, atol, options)
         if sol is not None:
             return sol
+    if _needs_grad(func, y0):
+        solver = _Dopri5Grad(func, y0, rtol, atol, options, reversed_)
+        sol = solver.integrate(tp)
+        dopri5_solve.last = solver
+        return sol
     solver = _Dopri5(func, y0, rtol, atol, options, reversed_)
     sol = solver.integrate(tp)
     dopri5_solve.last = solver   # exposes nfev / attempts for tests and tooling

@@ -447,6 +447,21 @@ def _interp_evaluate(coefficients, t0, t1, t):
     return total
 
 
+class _UncheckedAssign(torch.autograd.Function):
+    """rk_common._UncheckedAssign: writes a stage into the scratch tensor k without bumping its
+    version, so autograd can differentiate through the slices the earlier stages read."""
+
+    @staticmethod
+    def forward(ctx, scratch, value, index):
+        ctx.index = index
+        scratch.data[index] = value
+        return scratch
+
+    @staticmethod
+    def backward(ctx, grad_scratch):
+        return grad_scratch, grad_scratch[ctx.index], None
+
+
 def _dopri5(func, y0, t, rtol, atol, trace: Optional[Dopri5Trace], max_num_steps=2 ** 31 - 1,
             first_step=None):
     """RKAdaptiveStepsizeODESolver + Dopri5Solver (rk_common.py / dopri5.py)."""
@@ -477,7 +492,7 @@ def _dopri5(func, y0, t, rtol, atol, trace: Optional[Dopri5Trace], max_num_steps
     else:
         dt = torch.as_tensor(first_step, dtype=tdt)
     if trace is not None:
-        trace.first_step = float(dt)
+        trace.first_step = float(dt.detach())
     # _RungeKuttaState(y1, f1, t0, t1, dt, interp_coeff)
     st_y, st_f, st_t0, st_t1, st_dt, st_coeff = y0, f0, t[0], t[0], dt, [y0] * 5
     for i in range(1, len(t)):
@@ -493,12 +508,12 @@ def _dopri5(func, y0, t, rtol, atol, trace: Optional[Dopri5Trace], max_num_steps
             # _runge_kutta_step
             t0c, dtc, t1c = t0_.to(sdt), dt_.to(sdt), t1_.to(sdt)
             k = torch.empty(*f0_.shape, 7, dtype=sdt)
-            k[..., 0] = f0_
+            k = _UncheckedAssign.apply(k, f0_, (..., 0))
             yi = None
             for s, (alpha_i, beta_i) in enumerate(zip(alpha, beta)):
                 ti = t1c if alpha_i == 1. else t0c + alpha_i * dtc
                 yi = y0_ + k[..., :s + 1].matmul(beta_i * dtc).view_as(f0_)
-                k[..., s + 1] = f(ti, yi)
+                k = _UncheckedAssign.apply(k, f(ti, yi), (..., s + 1))
             y1 = yi
             f1 = k[..., -1]
             y1_error = k.matmul(dtc * c_err)
@@ -506,7 +521,7 @@ def _dopri5(func, y0, t, rtol, atol, trace: Optional[Dopri5Trace], max_num_steps
             error_ratio = _rms_norm(y1_error / error_tol)
             accept = bool(error_ratio <= 1)
             if trace is not None:
-                trace.attempts.append((float(t0_), float(dt_), float(error_ratio), accept))
+                trace.attempts.append((float(t0_.detach()), float(dt_.detach()), float(error_ratio.detach()), accept))
             if accept:
                 dtm = dt_.type_as(y0_)
                 y_mid = y0_ + k.matmul(dtm * c_mid).view_as(y0_)

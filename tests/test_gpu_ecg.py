@@ -133,7 +133,7 @@ def test_node_dopri5_batch200_vs_oracle(dev):
 
 def test_training_through_fixed_grid(dev):
     """The field's HIP VJP under a fixed-grid solve (rk4): gradients of every parameter match the
-    oracle's autograd (dopri5 backprop is not provided: odeint raises)."""
+    oracle's autograd (dopri5: test_training_through_dopri5_vs_oracle_autograd)."""
     from fet_ode_amd import ecg
     import fet_ode_amd as F
     from oracle import ecg_ref as E
@@ -158,8 +158,6 @@ def test_training_through_fixed_grid(dev):
             assert p.grad is None
             continue
         close(p.grad, ps[n].grad, 1e-4, n)
-    with pytest.raises(NotImplementedError):
-        F.odeint(f, hg, t, method="dopri5").sum().backward()
 
 
 # rel: latent 1 (the __main__ config, :1181-1198) moves the last row by tiny amounts between
@@ -366,3 +364,37 @@ def test_ferronet_production_width_vs_oracle(dev):
     assert not missing, (missing, sorted(grads[torch.float64]))
     for n, p in f.named_parameters():
         _envelope_close(p.grad, grads[torch.float32][n], grads[torch.float64][n], "grad " + n)
+
+
+def test_training_through_dopri5_vs_oracle_autograd(dev):
+    """train_ecg_kan_fet_nn_ode.py trains KanFet_NODE through dopri5: cross-entropy on the logits,
+    loss.backward() through the host-driven GPU dopri5 (the resident solver is inference-only)
+    with the mixer's HIP VJP, against the oracle's autograd — same attempts, every parameter
+    gradient within 1e-3 relative (hysteresis gates are piecewise constant: no gradient flows
+    through them in either)."""
+    from fet_ode_amd import ecg
+    from fet_ode_amd import dopri5 as D5
+    from oracle import ecg_ref as E
+    g = load_golden("ecg_node64")
+    sd = golden_sd(g)
+    m = ecg.KanFet_NODE(T=96, num_classes=2, latent_dim=64, num_basis=10, rtol=1e-3, atol=1e-4)
+    m.load_state_dict(sd)
+    m = m.to(dev).eval()
+    x = torch.from_numpy(g["x"])
+    y = torch.arange(x.shape[0]) % 2
+    loss = torch.nn.functional.cross_entropy(m(x.to(dev)), y.to(dev))
+    loss.backward()
+    assert isinstance(D5.dopri5_solve.last, D5._Dopri5Grad)
+    ps = {k: v.clone().requires_grad_(v.dtype.is_floating_point and "prev_x" not in k and "branch_state" not in k)
+          for k, v in sd.items()}
+    ref = E.ECGNodeRef(ps, rtol=1e-3, atol=1e-4)
+    lref = torch.nn.functional.cross_entropy(ref(x), y)
+    lref.backward()
+    assert len(D5.dopri5_solve.last.attempts) == len(ref.trace.attempts)
+    assert abs(loss.item() - lref.item()) <= 1e-5 * abs(lref.item())
+    for n, p in m.named_parameters():
+        exp = ps[n].grad
+        if exp is None:
+            assert p.grad is None or float(p.grad.abs().max()) == 0.0, n
+            continue
+        close(p.grad, exp, 1e-3, "grad " + n)

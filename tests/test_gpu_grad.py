@@ -318,3 +318,52 @@ def test_fused_backward_deterministic(dev):
         out.append([p.grad.clone() for p in m.parameters()])
     for a, b in zip(*out):
         assert torch.equal(a, b)
+
+
+def test_training_grads_through_dopri5_kan(dev):
+    """predator_prey.py:139-145 trains through torchodeint's default dopri5: loss.backward()
+    through the GPU dopri5 (every stage of every attempt, the error ratios and the step sizes,
+    as torchdiffeq's direct backprop) against the oracle's autograd through the same solve.
+    The gradient through the step-size control is ill-conditioned in fp32 (the oracle's own fp32
+    and fp64 gradients differ by up to 9 % on the spline scalers here), so the bound is the fp64
+    oracle with 4x the oracle's own fp32 error, plus 1e-4 relative."""
+    import fet_ode_amd as F
+    from fet_ode_amd import dopri5 as D5
+    from oracle import torch_ref as O
+    g = load_golden("traj_kan")
+    sd = golden_sd(g)
+    t = torch.from_numpy(g["t35"])[:12]
+    y0 = torch.tensor([[1.0, 1.0], [0.7, 1.9]])
+    target = torch.from_numpy(load_golden("lv_lsoda")["soln"][:12]).float()
+    m = F.KAN([2, 10, 2], grid_size=5)
+    m.load_state_dict(sd)
+    m = m.to(dev)
+    y0g = y0.clone().to(dev).requires_grad_(True)
+    pred = F.odeint(lambda tt, yy: m(yy), y0g, t, rtol=1e-5, atol=1e-7)
+    assert isinstance(D5.dopri5_solve.last, D5._Dopri5Grad)
+    loss = torch.mean(torch.square(pred[:, 0, :] - target.to(dev)))
+    loss.backward()
+    ref = {}
+    for dt in (torch.float32, torch.float64):
+        ps = {k: v.clone().to(dt).requires_grad_(k.split(".")[-1] != "grid") for k, v in sd.items()}
+        kan = O.KANRef([O.KANLinearParams.from_state_dict(ps, f"layers.{l}.") for l in range(2)])
+        y0c = y0.clone().to(dt).requires_grad_(True)
+        tr = O.Dopri5Trace()
+        pr = O.odeint(lambda tt, yy: kan(yy), y0c, t, rtol=1e-5, atol=1e-7, trace=tr)
+        lref = torch.mean(torch.square(pr[:, 0, :] - target.to(dt)))
+        lref.backward()
+        ref[dt] = (lref.detach(), y0c.grad, {k: v.grad for k, v in ps.items() if v.grad is not None}, tr)
+    last = D5.dopri5_solve.last
+    tr = ref[torch.float32][3]
+    assert len(last.attempts) == len(tr.attempts) and [a[3] for a in last.attempts] == [a[3] for a in tr.attempts]
+
+    def env(got, e32, e64, name):
+        got, e32, e64 = got.detach().double().cpu(), e32.double(), e64.double()
+        scale = e64.abs().max().item() + 1e-12
+        err, spread = (got - e64).abs().max().item(), (e32 - e64).abs().max().item()
+        assert err <= 4 * spread + 1e-4 * scale, f"{name}: |gpu-fp64|={err:.3e} fp32 spread={spread:.3e} scale={scale:.3e}"
+
+    env(loss, ref[torch.float32][0], ref[torch.float64][0], "loss")
+    env(y0g.grad, ref[torch.float32][1], ref[torch.float64][1], "y0")
+    for n, p in m.named_parameters():
+        env(p.grad, ref[torch.float32][2][n], ref[torch.float64][2][n], n)
