@@ -120,6 +120,11 @@ SIGNATURES = {
     "fetode_tanh_backward": (ctypes.c_int, [ctypes.c_int64, _vp, _vp, _vp, _vp]),
     "fetode_nan_clamp": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_float] * 5 + [_vp, _vp, _vp]),
     "fetode_nan_clamp_backward": (ctypes.c_int, [ctypes.c_int64] + [ctypes.c_float] * 5 + [_vp, _vp, _vp, _vp]),
+    "fetode_kuramoto_forward": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                               ctypes.c_float, _vp, _vp, _vp, _vp, _vp]),
+    "fetode_kuramoto_backward_workspace": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
+    "fetode_kuramoto_backward": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                ctypes.c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "fetode_hlogistic_mixer_backward": (ctypes.c_int, [ctypes.POINTER(HLogisticDesc), _vp, ctypes.c_int64, _vp,
                                                        ctypes.c_int32, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp, _vp,
                                                        _vp, _vp, _vp, _vp, _vp, _vp]),

@@ -300,6 +300,20 @@ int fetode_nan_clamp(int64_t n, float nan, float posinf, float neginf, float lo,
 int fetode_nan_clamp_backward(int64_t n, float nan, float posinf, float neginf, float lo, float hi, const float* g,
                               const float* x, float* gx, void* stream);
 
+/* Kuramoto2D.forward (mnist_kuramoto_kan.py:179-199): x (B, H*W) pixels in [0, 1] -> feat (B, 2*H*W)
+ * = [cos(theta) | sin(theta)] after `steps` Euler steps of theta += dt (omega + K coupling);
+ * K (1 float) and omega (H*W) are device pointers; H*W <= 3072.  tape (nullable,
+ * (B, steps + 1, H*W)) records theta_0..theta_steps for the backward.
+ * fetode_kuramoto_backward: from the tape and gfeat (B, 2*H*W), gx (nullable, (B, H*W)), gK
+ * (nullable, 1 float) and gomega (nullable, H*W), reduced over the batch in a fixed order;
+ * workspace: fetode_kuramoto_backward_workspace(B, H, W) bytes when gK or gomega is wanted. */
+int fetode_kuramoto_forward(const float* x, int64_t B, int32_t H, int32_t W, int32_t steps, float dt, const float* K,
+                            const float* omega, float* feat, float* tape, void* stream);
+int64_t fetode_kuramoto_backward_workspace(int64_t B, int32_t H, int32_t W);
+int fetode_kuramoto_backward(int64_t B, int32_t H, int32_t W, int32_t steps, float dt, const float* K,
+                             const float* tape, const float* gfeat, float* gx, float* gK, float* gomega,
+                             void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

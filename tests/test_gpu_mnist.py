@@ -1,0 +1,87 @@
+"""GPU parity of the MNIST Kuramoto + KANLinear classifier (mnist_kuramoto_kan.py; SURVEY §8f
+rank 3) against fixtures made from the reference classes and the CPU oracle (oracle/mnist_ref.py)."""
+import pytest
+import torch
+
+from conftest import golden_sd, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def close(got, exp, rel, name):
+    got, exp = got.detach().double().cpu(), exp.detach().double().cpu()
+    scale = exp.abs().max().item() + 1e-12
+    err = (got - exp).abs().max().item()
+    assert err <= rel * scale, f"{name}: max|diff|={err:.3e} scale={scale:.3e}"
+
+
+def test_head_forward_and_grads(dev):
+    """KANLinear(288 -> 10, 8 logistic bases, logistic bias): inputs in and outside the grid incl.
+    a knot and both grid ends; every parameter gradient against the reference's autograd."""
+    from fet_ode_amd import mnist
+    g = load_golden("mnist_head")
+    m = mnist.KANLinear(288, 10, num_basis=8)
+    m.load_state_dict(golden_sd(g))
+    m = m.to(dev)
+    x = torch.from_numpy(g["x"]).to(dev).requires_grad_(True)
+    y = m(x)
+    close(y, torch.from_numpy(g["y"]), 1e-5, "y")
+    (y * torch.from_numpy(g["w"]).to(dev)).sum().backward()
+    close(x.grad, torch.from_numpy(g["grad/x"]), 1e-4, "grad x")
+    for n, p in m.named_parameters():
+        close(p.grad, torch.from_numpy(g["grad/" + n]), 2e-4, "grad " + n)
+
+
+def test_kuramoto_forward_and_grads(dev):
+    """Kuramoto2D(12 x 12, 10 steps, random omega, K = 0.7): features and d/dx, d/dK, d/domega."""
+    from fet_ode_amd import mnist
+    g = load_golden("mnist_kuramoto")
+    m = mnist.Kuramoto2D(H=12, W=12, steps=10, dt=0.15)
+    m.load_state_dict(golden_sd(g))
+    m = m.to(dev)
+    x = torch.from_numpy(g["x"]).to(dev).requires_grad_(True)
+    y = m(x)
+    close(y, torch.from_numpy(g["y"]), 1e-5, "features")
+    (y * torch.from_numpy(g["w"]).to(dev)).sum().backward()
+    close(x.grad, torch.from_numpy(g["grad/x"]), 1e-4, "grad x")
+    close(m.K.grad, torch.from_numpy(g["grad/K"]), 1e-4, "grad K")
+    close(m.omega.grad, torch.from_numpy(g["grad/omega"]), 1e-4, "grad omega")
+
+
+def test_classifier_training_step(dev):
+    """KuramotoKANClassifier: logits and the cross-entropy gradients of every parameter."""
+    from fet_ode_amd import mnist
+    g = load_golden("mnist_classifier")
+    m = mnist.KuramotoKANClassifier(H=12, W=12, num_classes=10, kuramoto_steps=10, num_basis=8)
+    m.load_state_dict(golden_sd(g))
+    m = m.to(dev)
+    logits = m(torch.from_numpy(g["x"]).to(dev))
+    close(logits, torch.from_numpy(g["logits"]), 1e-5, "logits")
+    torch.nn.functional.cross_entropy(logits, torch.from_numpy(g["labels"]).to(dev)).backward()
+    for n, p in m.named_parameters():
+        close(p.grad, torch.from_numpy(g["grad/" + n]), 2e-4, "grad " + n)
+
+
+def test_production_size_vs_oracle(dev):
+    """28 x 28 images, KANLinear(1568 -> 10): batch-64 logits and gradients against the CPU oracle
+    (and its autograd) on the same seeded weights and synthetic images."""
+    from fet_ode_amd import mnist
+    from oracle import mnist_ref as M
+    torch.manual_seed(61)
+    m = mnist.KuramotoKANClassifier()
+    with torch.no_grad():
+        m.osc.omega.normal_(0, 0.3)
+        m.head.logistic_bias.normal_(0, 0.1)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    x = M.mnist_x(64, seed=62)
+    y = torch.arange(64) % 10
+    logits = m(x.to(dev))
+    torch.nn.functional.cross_entropy(logits, y.to(dev)).backward()
+    ps = {k: v.clone().requires_grad_(k not in ("osc.neighbor_kernel", "head.grid")) for k, v in sd.items()}
+    ref = M.ClassifierRef(ps)
+    lr = ref(x)
+    close(logits, lr, 1e-5, "logits")
+    torch.nn.functional.cross_entropy(lr, y).backward()
+    for n, p in m.named_parameters():
+        close(p.grad, ps[n].grad, 5e-4, "grad " + n)
