@@ -54,6 +54,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ecg", action="store_true", help="skip the ECG dopri5 (configs[2]) line")
+    ap.add_argument("--no-mnist", action="store_true", help="skip the MNIST Kuramoto + KANLinear line")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--train-iters", type=int, default=20, help="0 skips the training-rate line")
     return ap.parse_args()
@@ -156,9 +157,8 @@ def train_rate(model, y0d, t, iters, warmup, world):
 def ecg_rate(dev, reps=10, cpu_seconds=5.0, with_cpu=True):
     """BASELINE configs[2] (train_ecg_kan_fet_nn_ode.py:512-572): KanFet_NODE.eval() forward on a
     batch of 200 synthetic ECG200-shaped series (T = 96; the dataset is not in the image), latent
-    64, 10 bases, dopri5 rtol 1e-3 / atol 1e-4 on [0, 1].  The field (hysteretic mixer + Linear
-    head) is one HIP launch per evaluation; dopri5's accept/reject is host-driven (one scalar
-    read per attempt, as torchdiffeq's `if accept_step`)."""
+    64, 10 bases, dopri5 rtol 1e-3 / atol 1e-4 on [0, 1].  Under no_grad the whole dopri5 solve is
+    one device-resident launch (fetode_ecg_dopri5); the encoder / classifier are one launch each."""
     from fet_ode_amd import ecg
     from oracle import ecg_ref as E
     torch.manual_seed(0)
@@ -193,6 +193,60 @@ def ecg_rate(dev, reps=10, cpu_seconds=5.0, with_cpu=True):
         out["cpu_baseline"] = {"value": 1.0 / cel, "unit": out["unit"], "cores": cores, "kind": "port",
                                "sample": f"{n} full forward(s) of the same workload with oracle/ecg_ref.py "
                                          f"(reference op order, torch CPU fp32), {cel * n:.1f} s"}
+    return out
+
+
+def mnist_rate(dev, batch=8192, reps=10, cpu_seconds=5.0, with_cpu=True):
+    """The MNIST config (mnist_kuramoto_kan.py:202-221): KuramotoKANClassifier on 28 x 28 synthetic
+    images (the dataset is not in the image), 10 Kuramoto steps, KANLinear(1568 -> 10, 8 logistic
+    bases).  Forward images/s under no_grad and training images/s (forward + cross-entropy +
+    backward of every parameter) on one GPU."""
+    from fet_ode_amd import mnist
+    from oracle import mnist_ref as M
+    torch.manual_seed(0)
+    m = mnist.KuramotoKANClassifier()
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    x = M.mnist_x(batch, seed=3)
+    xd = x.to(dev)
+    y = (torch.arange(batch) % 10).to(dev)
+
+    def timed(fn, n):
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / n
+
+    with torch.no_grad():
+        fwd = timed(lambda: m(xd), reps)
+
+    def train_step():
+        m.zero_grad(set_to_none=True)
+        torch.nn.functional.cross_entropy(m(xd), y).backward()
+
+    trn = timed(train_step, reps)
+    out = {"value": batch / fwd, "unit": "images/s forward (KuramotoKANClassifier 28x28, 1 GPU)",
+           "ms_per_batch": fwd * 1e3, "train_images_per_s": batch / trn, "train_ms_per_batch": trn * 1e3,
+           "workload": f"KuramotoKANClassifier(28x28, 10 Kuramoto steps, KANLinear 1568->10, nb 8), batch {batch}, "
+                       "synthetic images"}
+    if with_cpu:
+        cores = min(16, os.cpu_count() or 1)
+        torch.set_num_threads(cores)
+        ref = M.ClassifierRef(sd)
+        xs = x[:256]
+        n, t0 = 0, time.perf_counter()
+        with torch.no_grad():
+            while n < 1 or (time.perf_counter() - t0 < cpu_seconds and n < 20):
+                ref(xs)
+                n += 1
+        cel = (time.perf_counter() - t0) / n
+        out["cpu_baseline"] = {"value": 256 / cel, "unit": out["unit"].replace("1 GPU", "CPU"), "cores": cores,
+                               "kind": "port", "sample": f"{n} forward(s) of 256 of the images with "
+                                                         f"oracle/mnist_ref.py (torch CPU fp32), {cel * n:.1f} s"}
     return out
 
 
@@ -314,6 +368,8 @@ def main():
             out["train"] = train
         if world == 1 and not args.no_ecg:
             out["ecg"] = ecg_rate(dev, with_cpu=not args.no_cpu_baseline)
+        if world == 1 and not args.no_mnist:
+            out["mnist"] = mnist_rate(dev, with_cpu=not args.no_cpu_baseline)
         if world == 1 and not args.no_cpu_baseline:
             cb, ref_sol = cpu_baseline(sd, y0, t, args.cpu_seconds)
             out["cpu_baseline"] = cb
