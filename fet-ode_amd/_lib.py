@@ -123,6 +123,12 @@ SIGNATURES = {
     "fetode_kuramoto_forward": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                                ctypes.c_float, _vp, _vp, _vp, _vp, _vp]),
     "fetode_kuramoto_backward_workspace": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
+    "fetode_kanlinear_wide_supported": (ctypes.c_int, [ctypes.POINTER(KANLinearDesc)]),
+    "fetode_kanlinear_wide_pack_bytes": (ctypes.c_int64, [ctypes.POINTER(KANLinearDesc)]),
+    "fetode_kanlinear_wide_pack": (ctypes.c_int, [ctypes.POINTER(KANLinearDesc), _vp, _vp]),
+    "fetode_kanlinear_wide_workspace": (ctypes.c_int64, [ctypes.POINTER(KANLinearDesc), ctypes.c_int64]),
+    "fetode_kanlinear_wide_forward": (ctypes.c_int, [ctypes.POINTER(KANLinearDesc), _vp, _vp, _vp, ctypes.c_int64, _vp,
+                                                     _vp, _vp]),
     "fetode_kuramoto_backward": (ctypes.c_int, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                                 ctypes.c_float, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "fetode_hlogistic_mixer_backward": (ctypes.c_int, [ctypes.POINTER(HLogisticDesc), _vp, ctypes.c_int64, _vp,

@@ -155,6 +155,129 @@ __global__ void column_sum_kernel(const float* __restrict__ part, int64_t B, int
   out[j] = accumulate ? out[j] + (float)s : (float)s;
 }
 
+
+// =============================================================================================
+// Wide KANLinear head on MFMA (mnist_kuramoto_kan.py:127-142 at in = 1568, out = 10; SURVEY §8f
+// rank 3: "the only place MFMA is justified").  out[b, o] = sum_i sum_f feat_f(x[b, i]) Wp[i, f, o]
+// with the F = 1 + 8 + 8 features of one input — SiLU, the 8 cubic B-spline bases (4 nonzero),
+// the 8 logistic bases — computed ONCE per (row, input) (the generic kernel recomputes them per
+// output) and contracted on v_mfma_f32_16x16x4_f32: an exact f32 fma chain in k order.
+//   A (16 rows x 4 k): lane (r = l & 15, kq = l >> 4) holds feature f of input 4 g + kq of row r;
+//   B (4 k x 16 outputs): lane (kq, o) holds Wp[4 g + kq, f, o] (o >= out: 0), read from LDS;
+//   one MFMA per (input group g, feature f).
+// A 256-thread workgroup = 4 waves x 16 rows; the inputs are split over gridDim.y (split-K) into
+// fixed chunks whose packed weights (and knots, logistic a / b) are staged in LDS for all 64 rows.
+// Partials (S, B, 16) are added in split order by a second kernel with the logistic bias.
+// =============================================================================================
+constexpr int kWideCh = 32;            // inputs per staged chunk
+constexpr int kWideNS = 8, kWideNB = 8, kWideNG = 12;
+constexpr int kWideF = 1 + kWideNS + kWideNB;
+constexpr int kWideRows = 64;          // rows per workgroup (4 waves x 16)
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Wp[i][f][o16]: f = 0 base, 1 + c scaled spline, 1 + NS + j scaled logistic
+__global__ void wide_pack_kernel(fetode_kanlinear_t kl, float* __restrict__ wp) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int in = kl.in_features, outf = kl.out_features;
+  if (t >= (int64_t)in * kWideF * 16) return;
+  const int o = t % 16, f = (t / 16) % kWideF, i = (int)(t / (16 * kWideF));
+  float v = 0.f;
+  if (o < outf) {
+    if (f == 0) {
+      v = kl.base_weight[(int64_t)o * in + i];
+    } else if (f <= kWideNS) {
+      const float sc = kl.spline_scaler ? kl.spline_scaler[(int64_t)o * in + i] : 1.0f;
+      v = kl.spline_weight[((int64_t)o * in + i) * kWideNS + (f - 1)] * sc;
+    } else if (kl.num_logistic) {
+      const float lsc = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
+      v = (kl.logistic_weight[(int64_t)o * in * kWideNB + i * kWideNB + (f - 1 - kWideNS)] * kl.scale_logistic) * lsc;
+    }
+  }
+  wp[t] = v;
+}
+
+__global__ __launch_bounds__(256) void wide_fwd_kernel(fetode_kanlinear_t kl, const float* __restrict__ wp,
+                                                      const float* __restrict__ x, int64_t B, int nch,
+                                                      float* __restrict__ part) {
+  __shared__ float ws[kWideCh * kWideF * 16];   // packed weights of the chunk
+  __shared__ float xs[kWideRows][kWideCh + 1];  // the 64 rows' inputs of the chunk
+  __shared__ float gk[kWideCh][kWideNG];        // knots
+  __shared__ float lab[kWideCh][2 * kWideNB];   // logistic a | b
+  __shared__ float sbs[kWideNS][256];            // each lane's spline bases (runtime-indexed writes)
+  const int in = kl.in_features;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = lane & 15, kq = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * kWideRows;
+  const int S = gridDim.y, s = blockIdx.y;
+  const int c0 = s * nch / S, c1 = (s + 1) * nch / S;
+  const bool lg = kl.num_logistic != 0;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int c = c0; c < c1; ++c) {
+    const int i0 = c * kWideCh, ni = min(kWideCh, in - i0);
+    __syncthreads();
+    for (int t = tid; t < ni * kWideF * 16; t += 256) ws[t] = wp[(int64_t)i0 * kWideF * 16 + t];
+    for (int t = tid; t < kWideRows * kWideCh; t += 256) {
+      const int rr = t / kWideCh, ii = t - rr * kWideCh;
+      xs[rr][ii] = (row0 + rr < B && ii < ni) ? x[(row0 + rr) * in + i0 + ii] : 0.f;
+    }
+    for (int t = tid; t < ni * kWideNG; t += 256) gk[t / kWideNG][t % kWideNG] = kl.grid[(int64_t)i0 * kWideNG + t];
+    if (lg)
+      for (int t = tid; t < ni * kWideNB; t += 256) {
+        lab[t / kWideNB][t % kWideNB] = kl.logistic_a[(int64_t)i0 * kWideNB + t];
+        lab[t / kWideNB][kWideNB + t % kWideNB] = kl.logistic_b[(int64_t)i0 * kWideNB + t];
+      }
+    __syncthreads();
+    for (int g = 0; g < ni / 4; ++g) {
+      const int il = 4 * g + kq;
+      const float xi = xs[wv * 16 + r][il];
+      float feat[kWideF];
+      feat[0] = xi / (1.0f + expf(-xi));  // SiLU, efficientkan.py:166 / mnist :131
+      bspline_local_div<3>(xi, kWideNG, gk[il], [&](int cc, float v) { sbs[cc][tid] = v; });
+#pragma unroll
+      for (int k = 0; k < kWideNS; ++k) feat[1 + k] = sbs[k][tid];
+#pragma unroll
+      for (int j = 0; j < kWideNB; ++j)
+        feat[1 + kWideNS + j] = lg ? 2.0f / (1.0f + expf(-lab[il][j] * (xi - lab[il][kWideNB + j]))) : 0.f;
+      const float* wrow = ws + (il * kWideF) * 16 + r;   // lane (kq, o = r): Wp[i, f, o]
+#pragma unroll
+      for (int f = 0; f < kWideF; ++f) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(feat[f], wrow[f * 16], acc, 0, 0, 0);
+    }
+  }
+  // D: lane l holds rows 4 (l >> 4) + v, column l & 15
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int64_t row = row0 + wv * 16 + 4 * kq + v;
+    if (row < B) part[((int64_t)s * B + row) * 16 + r] = acc[v];
+  }
+}
+
+__global__ void wide_reduce_kernel(const float* __restrict__ part, int S, int64_t B, int outf,
+                                   const float* __restrict__ bias, float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= B * outf) return;
+  const int64_t b = t / outf;
+  const int o = t % outf;
+  float v = part[b * 16 + o];
+  for (int s = 1; s < S; ++s) v = v + part[((int64_t)s * B + b) * 16 + o];
+  out[t] = bias ? v + bias[o] : v;
+}
+
+int wide_supported(const fetode_kanlinear_t* kl) {
+  return kl && kl->spline_order == 3 && kl->grid_size == 5 && (kl->num_logistic == 0 || kl->num_logistic == kWideNB) &&
+         kl->out_features >= 1 && kl->out_features <= 16 && kl->in_features >= 4 && kl->in_features % 4 == 0 &&
+         kl->grid && kl->base_weight && kl->spline_weight && (kl->num_logistic == 0 ||
+         (kl->logistic_a && kl->logistic_b && kl->logistic_weight));
+}
+
+int wide_splits(const fetode_kanlinear_t* kl, int64_t B) {
+  const int nch = (kl->in_features + kWideCh - 1) / kWideCh;
+  const int64_t tiles = (B + kWideRows - 1) / kWideRows;
+  int64_t S = (2048 + tiles - 1) / tiles;   // aim at >= 2048 workgroups
+  if (S > nch) S = nch;
+  return (int)(S < 1 ? 1 : S);
+}
+
 }  // namespace
 
 extern "C" {
@@ -200,6 +323,46 @@ int fetode_kuramoto_backward(int64_t B, int32_t H, int32_t W, int32_t steps, flo
     hipLaunchKernelGGL(column_sum_kernel, dim3(1), dim3(256), 0, s, gK_part, B, 1, gK, 0);
     LAUNCH_CHECK();
   }
+  return FETODE_OK;
+}
+
+int fetode_kanlinear_wide_supported(const fetode_kanlinear_t* kl) { return wide_supported(kl); }
+
+int64_t fetode_kanlinear_wide_pack_bytes(const fetode_kanlinear_t* kl) {
+  return kl ? (int64_t)sizeof(float) * kl->in_features * kWideF * 16 : 0;
+}
+
+int fetode_kanlinear_wide_pack(const fetode_kanlinear_t* kl, float* wpack, void* stream) {
+  if (!wide_supported(kl)) return set_err(FETODE_EUNSUPPORTED, "kanlinear wide: unsupported layer");
+  if (!wpack) return set_err(FETODE_EINVAL, "kanlinear wide: null pack");
+  const int64_t n = (int64_t)kl->in_features * kWideF * 16;
+  hipLaunchKernelGGL(wide_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *kl, wpack);
+  LAUNCH_CHECK();
+  return FETODE_OK;
+}
+
+int64_t fetode_kanlinear_wide_workspace(const fetode_kanlinear_t* kl, int64_t B) {
+  if (!kl || B <= 0) return 0;
+  return (int64_t)sizeof(float) * wide_splits(kl, B) * B * 16;
+}
+
+int fetode_kanlinear_wide_forward(const fetode_kanlinear_t* kl, const float* wpack, const float* bias, const float* x,
+                                  int64_t B, float* out, void* workspace, void* stream) {
+  if (!wide_supported(kl)) return set_err(FETODE_EUNSUPPORTED, "kanlinear wide: unsupported layer");
+  if (B <= 0) return FETODE_OK;
+  if (!wpack || !x || !out || !workspace) return set_err(FETODE_EINVAL, "kanlinear wide: null pointer");
+  const int S = wide_splits(kl, B);
+  const int nch = (kl->in_features + kWideCh - 1) / kWideCh;
+  const int64_t tiles = (B + kWideRows - 1) / kWideRows;
+  if (tiles > 0x7fffffff) return set_err(FETODE_EINVAL, "kanlinear wide: batch too large");
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(wide_fwd_kernel, dim3((unsigned)tiles, (unsigned)S), dim3(256), 0, s, *kl, wpack, x, B, nch,
+                     (float*)workspace);
+  LAUNCH_CHECK();
+  const int64_t n = B * kl->out_features;
+  hipLaunchKernelGGL(wide_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)workspace, S, B,
+                     kl->out_features, bias, out);
+  LAUNCH_CHECK();
   return FETODE_OK;
 }
 

@@ -8,9 +8,9 @@
 
 Same constructor arguments, parameter / buffer names and shapes, init RNG order as the reference.
 Kuramoto2D is one HIP launch per forward (a workgroup per image, all steps in LDS) with a HIP VJP
-from a theta tape; KANLinear runs the HIP KANLinear kernels (fetode_kanlinear_forward / _backward:
-SiLU + B-spline + logistic per (row, output)); the logistic bias is the only torch op.  There is no
-CPU path: CPU tensors raise.
+from a theta tape; the KANLinear head's forward is the MFMA kernel (fetode_kanlinear_wide_forward:
+features once per (row, input), contraction on v_mfma_f32_16x16x4_f32, the logistic bias in its
+epilogue), its backward the HIP KANLinear VJP kernels.  There is no CPU path: CPU tensors raise.
 """
 from __future__ import annotations
 
@@ -20,7 +20,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .autograd_ops import kanlinear_apply
+from .autograd_ops import kan_backward, kan_params, kanlinear_apply
 
 
 def _stream(x):
@@ -143,15 +143,64 @@ class KANLinear(nn.Module):
             p(self.logistic_basis.a) if lg else None, p(self.logistic_basis.b) if lg else None,
             p(self.logistic_weight) if lg else None, None, 1.0)
 
+    def _wide_pack_for(self, d, keep):
+        """The weights in the MFMA head's layout, re-packed whenever a weight tensor changes."""
+        ws = [t for t in (self.base_weight, self.spline_weight, getattr(self, "spline_scaler", None),
+                          getattr(self, "logistic_weight", None)) if t is not None]
+        key = tuple((t.data_ptr(), t._version) for t in ws)
+        cached = getattr(self, "_wide_cache", None)
+        if cached is None or cached[0] != key:
+            lib = _lib.load()
+            wp = torch.empty(lib.fetode_kanlinear_wide_pack_bytes(_lib.ctypes.byref(d)) // 4, device=self.base_weight.device)
+            _lib.check(lib.fetode_kanlinear_wide_pack(_lib.ctypes.byref(d), wp.data_ptr(), _stream(wp)),
+                       "KANLinear wide pack")
+            cached = (key, wp)
+            self._wide_cache = cached
+        return cached[1]
+
     def forward(self, x: torch.Tensor):
         assert x.size(-1) == self.in_features
         orig = x.shape
         x2 = x.reshape(-1, self.in_features)
         _lib.require_gpu_tensor(x2, "KANLinear.forward")
-        out = kanlinear_apply(self, x2)
-        if self.use_logistic_basis:
-            out = out + self.logistic_bias
+        keep = []
+        if _lib.load().fetode_kanlinear_wide_supported(_lib.ctypes.byref(self.desc(keep))):
+            bias = self.logistic_bias if self.use_logistic_basis else None
+            out = _WideKANFn.apply(self, x2, bias, *kan_params(self))
+        else:
+            out = kanlinear_apply(self, x2)
+            if self.use_logistic_basis:
+                out = out + self.logistic_bias
         return out.reshape(*orig[:-1], self.out_features)
+
+
+class _WideKANFn(torch.autograd.Function):
+    """KANLinear + logistic bias, forward on the MFMA head kernel (fetode_kanlinear_wide_forward),
+    backward on the HIP KANLinear VJP kernels."""
+
+    @staticmethod
+    def forward(ctx, mod, x, bias, *params):
+        lib = _lib.load()
+        keep = []
+        d = mod.desc(keep)
+        xc = _lib.f32c(x)
+        B = xc.shape[0]
+        wp = mod._wide_pack_for(d, keep)
+        out = torch.empty(B, mod.out_features, device=x.device, dtype=torch.float32)
+        ws = torch.empty(max(1, lib.fetode_kanlinear_wide_workspace(_lib.ctypes.byref(d), B) // 4), device=x.device)
+        bc = _lib.f32c(bias) if bias is not None else None
+        _lib.check(lib.fetode_kanlinear_wide_forward(_lib.ctypes.byref(d), wp.data_ptr(), _lib.ptr(bc), xc.data_ptr(), B,
+                                                     out.data_ptr(), ws.data_ptr(), _stream(x)), "KANLinear.forward")
+        ctx.mod = mod
+        ctx.save_for_backward(xc)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        (xc,) = ctx.saved_tensors
+        gx, grads = kan_backward(ctx.mod, xc, grad, ctx.needs_input_grad[1], ctx.needs_input_grad[3:])
+        gb = grad.sum(0) if ctx.needs_input_grad[2] else None
+        return (None, gx, gb, *grads)
 
 
 class _KuramotoFn(torch.autograd.Function):

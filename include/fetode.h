@@ -314,6 +314,21 @@ int fetode_kuramoto_backward(int64_t B, int32_t H, int32_t W, int32_t steps, flo
                              const float* tape, const float* gfeat, float* gx, float* gK, float* gomega,
                              void* workspace, void* stream);
 
+/* Wide KANLinear forward on MFMA (the MNIST head, mnist_kuramoto_kan.py:127-142, KANLinear(1568 -> 10)):
+ * out (B, out) = SiLU / B-spline / logistic features of each input contracted with the weights on
+ * v_mfma_f32_16x16x4_f32, + bias (nullable: the MNIST logistic_bias).  Supported: grid_size 5,
+ * spline_order 3, num_logistic 0 or 8, out <= 16, in % 4 == 0 (fetode_kanlinear_wide_supported);
+ * otherwise FETODE_EUNSUPPORTED (fetode_kanlinear_forward serves every shape).  wpack
+ * (fetode_kanlinear_wide_pack_bytes) holds the weights in the MFMA layout, filled by
+ * fetode_kanlinear_wide_pack (re-pack after a weight update); workspace:
+ * fetode_kanlinear_wide_workspace(layer, B) bytes. */
+int fetode_kanlinear_wide_supported(const fetode_kanlinear_t* layer);
+int64_t fetode_kanlinear_wide_pack_bytes(const fetode_kanlinear_t* layer);
+int fetode_kanlinear_wide_pack(const fetode_kanlinear_t* layer, float* wpack, void* stream);
+int64_t fetode_kanlinear_wide_workspace(const fetode_kanlinear_t* layer, int64_t B);
+int fetode_kanlinear_wide_forward(const fetode_kanlinear_t* layer, const float* wpack, const float* bias, const float* x,
+                                  int64_t B, float* out, void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
