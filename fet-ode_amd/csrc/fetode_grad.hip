@@ -99,6 +99,7 @@ __device__ int bspline_vals_derivs(float x, int NG, const float* __restrict__ g,
 // KANLinear
 // ------------------------------------------------------------------------------------------
 
+constexpr int kMaxLogistic = 16;
 // gx[b,i] (+)= sum_o g[b,o] d out[b,o] / d x[b,i]
 template <int SO>
 __global__ void kan_gx_kernel(fetode_kanlinear_t kl, const float* __restrict__ x, const float* __restrict__ g,
@@ -114,6 +115,12 @@ __global__ void kan_gx_kernel(fetode_kanlinear_t kl, const float* __restrict__ x
   const float dsilu = sg * (1.0f + xv * (1.0f - sg));
   float val[SO + 1], der[SO + 1];
   const int m = bspline_vals_derivs<SO>(xv, NG, kl.grid + (int64_t)i * NG, val, der);
+  float dphi[kMaxLogistic];  // d phi_j / d x, once per (b, i) rather than per output
+  for (int j = 0; j < NB && j < kMaxLogistic; ++j) {
+    const float a = kl.logistic_a[i * NB + j], bb = kl.logistic_b[i * NB + j];
+    const float sj = sigm(a * (xv - bb));
+    dphi[j] = 2.0f * sj * (1.0f - sj) * a;
+  }
   float acc = 0.f;
   for (int o = 0; o < out; ++o) {
     const float go = g[b * out + o];
@@ -131,10 +138,16 @@ __global__ void kan_gx_kernel(fetode_kanlinear_t kl, const float* __restrict__ x
     if (NB > 0) {
       const float ls = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
       for (int j = 0; j < NB; ++j) {
-        const float a = kl.logistic_a[i * NB + j], bb = kl.logistic_b[i * NB + j];
-        const float s = sigm(a * (xv - bb));
         const float w = (kl.logistic_weight[(int64_t)o * in * NB + i * NB + j] * kl.scale_logistic) * ls;
-        d += w * (2.0f * s * (1.0f - s) * a);
+        float dj;
+        if (j < kMaxLogistic) {
+          dj = dphi[j];
+        } else {
+          const float a = kl.logistic_a[i * NB + j], bb = kl.logistic_b[i * NB + j];
+          const float sj = sigm(a * (xv - bb));
+          dj = 2.0f * sj * (1.0f - sj) * a;
+        }
+        d += w * dj;
       }
     }
     acc += go * d;
@@ -182,13 +195,228 @@ __global__ void kan_gw_kernel(fetode_kanlinear_t kl, const float* __restrict__ x
   }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Wide layers (the MNIST head, 1568 -> 10; fetode_kanlinear_wide_supported): the weight
+// gradients are one contraction over the batch, D[i, f, o] = sum_b feat_f(x[b, i]) g[b, o], on
+// v_mfma_f32_16x16x4_f32 — A = features (lane (f, row-quad)), B = g (lane (row-quad, o)) — with
+// the 17 features of each (row, input) computed once into LDS (the generic kan_gw_kernel computes
+// them per (o, i, f) block: 170x).  A workgroup owns 4 inputs and a quarter of the batch (64-row
+// chunks); the quarters add in a fixed order in wide_gw_reduce_kernel.
+// ------------------------------------------------------------------------------------------
+constexpr int kGwSplit = 4, kGwNS = 8, kGwNB = 8, kGwF = 1 + kGwNS + kGwNB, kGwNG = 12;
+typedef float gw_f32x4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void wide_gw_kernel(fetode_kanlinear_t kl, const float* __restrict__ x,
+                                                     const float* __restrict__ g, int64_t B,
+                                                     float* __restrict__ dpart) {
+  __shared__ float Fs[4][kGwF][64];
+  __shared__ float gs[64][16];
+  __shared__ float gk[4][kGwNG];
+  __shared__ float lab[4][2 * kGwNB];
+  __shared__ float sbs[kGwNS][256];
+  const int in = kl.in_features, out = kl.out_features;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int i0 = blockIdx.x * 4;
+  const int sp = blockIdx.y;
+  const int64_t nch = (B + 63) / 64;
+  const int64_t c0 = sp * nch / kGwSplit, c1 = (sp + 1) * nch / kGwSplit;
+  const bool lg = kl.num_logistic != 0;
+  if (tid < 4 * kGwNG) gk[tid / kGwNG][tid % kGwNG] = kl.grid[(int64_t)i0 * kGwNG + tid];
+  if (lg && tid < 4 * kGwNB) {
+    lab[tid / kGwNB][tid % kGwNB] = kl.logistic_a[(int64_t)i0 * kGwNB + tid];
+    lab[tid / kGwNB][kGwNB + tid % kGwNB] = kl.logistic_b[(int64_t)i0 * kGwNB + tid];
+  }
+  gw_f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  for (int64_t c = c0; c < c1; ++c) {
+    const int64_t b = c * 64 + lane;
+    __syncthreads();
+    {  // features of (row b, input i0 + wv)
+      const bool ok = b < B;
+      const float xv = ok ? x[b * in + i0 + wv] : 0.f;
+      Fs[wv][0][lane] = ok ? xv * sigm(xv) : 0.f;   // the reference's base branch SiLU(x)
+      bspline_local_div<3>(xv, kGwNG, gk[wv], [&](int cc, float v) { sbs[cc][tid] = v; });
+#pragma unroll
+      for (int k = 0; k < kGwNS; ++k) Fs[wv][1 + k][lane] = ok ? sbs[k][tid] : 0.f;
+#pragma unroll
+      for (int j = 0; j < kGwNB; ++j)
+        Fs[wv][1 + kGwNS + j][lane] =
+            (ok && lg) ? 2.0f / (1.0f + expf(-lab[wv][j] * (xv - lab[wv][kGwNB + j]))) : 0.f;
+    }
+    for (int t = tid; t < 64 * 16; t += 256) {
+      const int rr = t / 16, o = t % 16;
+      const int64_t bb = c * 64 + rr;
+      gs[rr][o] = (bb < B && o < out) ? g[bb * out + o] : 0.f;
+    }
+    __syncthreads();
+    const int m = lane & 15, kq = lane >> 4;
+#pragma unroll 4
+    for (int kt = 0; kt < 16; ++kt) {
+      const float bo = gs[4 * kt + kq][m];
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(Fs[wv][m][4 * kt + kq], bo, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(m == 0 ? Fs[wv][16][4 * kt + kq] : 0.f, bo, acc1, 0, 0, 0);
+    }
+  }
+  // D: lane holds rows (features) 4 (lane >> 4) + v, column (output) lane & 15
+  const int o = lane & 15, i = i0 + wv;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int f = 4 * (lane >> 4) + v;
+    dpart[(((int64_t)sp * in + i) * kGwF + f) * 16 + o] = acc0[v];
+    if (f == 0) dpart[(((int64_t)sp * in + i) * kGwF + 16) * 16 + o] = acc1[v];
+  }
+}
+
+
+// d x and d (logistic a, b) of a wide layer in one pass over the batch: per (row, input)
+// G_f = sum_o g[b, o] W_f[i, o] (the packed weights of 4 inputs staged in LDS, one input per
+// wave: broadcast reads), then d x = sum_f G_f d feat_f / d x and the logistic bases' a / b sums
+// (per-lane partials -> wave sum in a fixed order -> per-split slots -> wide_ab_reduce_kernel).
+__global__ __launch_bounds__(256) void wide_gxab_kernel(fetode_kanlinear_t kl, const float* __restrict__ x,
+                                                       const float* __restrict__ g, int64_t B, float* __restrict__ gx,
+                                                       float* __restrict__ abpart, int accumulate) {
+  __shared__ float wts[4][kGwF][16];
+  __shared__ float gs[64][17];
+  __shared__ float gk[4][kGwNG];
+  __shared__ float lab[4][2 * kGwNB];
+  __shared__ float red[4][64];
+  const int in = kl.in_features, out = kl.out_features;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int i0 = blockIdx.x * 4, i = i0 + wv;
+  const int sp = blockIdx.y;
+  const int64_t nch = (B + 63) / 64;
+  const int64_t c0 = sp * nch / kGwSplit, c1 = (sp + 1) * nch / kGwSplit;
+  const bool lg = kl.num_logistic != 0;
+  for (int t = tid; t < 4 * kGwF * 16; t += 256) {
+    const int ii = t / (kGwF * 16), f = (t / 16) % kGwF, o = t % 16;
+    const int iv = i0 + ii;
+    float v = 0.f;
+    if (o < out) {
+      if (f == 0) {
+        v = kl.base_weight[(int64_t)o * in + iv];
+      } else if (f <= kGwNS) {
+        const float sc = kl.spline_scaler ? kl.spline_scaler[(int64_t)o * in + iv] : 1.0f;
+        v = kl.spline_weight[((int64_t)o * in + iv) * kGwNS + (f - 1)] * sc;
+      } else if (lg) {
+        const float ls = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
+        v = (kl.logistic_weight[(int64_t)o * in * kGwNB + iv * kGwNB + (f - 1 - kGwNS)] * kl.scale_logistic) * ls;
+      }
+    }
+    wts[ii][f][o] = v;
+  }
+  if (tid < 4 * kGwNG) gk[tid / kGwNG][tid % kGwNG] = kl.grid[(int64_t)i0 * kGwNG + tid];
+  if (lg && tid < 4 * kGwNB) {
+    lab[tid / kGwNB][tid % kGwNB] = kl.logistic_a[(int64_t)i0 * kGwNB + tid];
+    lab[tid / kGwNB][kGwNB + tid % kGwNB] = kl.logistic_b[(int64_t)i0 * kGwNB + tid];
+  }
+  float ga[kGwNB], gb[kGwNB];
+#pragma unroll
+  for (int j = 0; j < kGwNB; ++j) ga[j] = gb[j] = 0.f;
+  for (int64_t c = c0; c < c1; ++c) {
+    __syncthreads();
+    for (int t = tid; t < 64 * 16; t += 256) {
+      const int rr = t / 16, o = t % 16;
+      const int64_t bb = c * 64 + rr;
+      gs[rr][o] = (bb < B && o < out) ? g[bb * out + o] : 0.f;
+    }
+    __syncthreads();
+    const int64_t b = c * 64 + lane;
+    if (b >= B) continue;
+    const float xv = x[b * in + i];
+    float go[16];
+#pragma unroll
+    for (int o = 0; o < 16; ++o) go[o] = gs[lane][o];
+    float G[kGwF];
+#pragma unroll
+    for (int f = 0; f < kGwF; ++f) {
+      float acc = 0.f;
+#pragma unroll
+      for (int o = 0; o < 16; ++o) acc = __builtin_fmaf(go[o], wts[wv][f][o], acc);
+      G[f] = acc;
+    }
+    const float sg = sigm(xv);
+    float d = G[0] * (sg * (1.0f + xv * (1.0f - sg)));
+    float val[4], der[4];
+    const int m = bspline_vals_derivs<3>(xv, kGwNG, gk[wv], val, der);
+    if (m >= 0) {
+#pragma unroll
+      for (int r = 0; r <= 3; ++r) {
+        const int cc = m - 3 + r;
+#pragma unroll
+        for (int k = 0; k < kGwNS; ++k)
+          if (k == cc) d += G[1 + k] * der[r];
+      }
+    } else if (m == -2) {
+      d = __builtin_nanf("");
+    }
+    if (lg) {
+#pragma unroll
+      for (int j = 0; j < kGwNB; ++j) {
+        const float a = lab[wv][j], bj = lab[wv][kGwNB + j];
+        const float sj = sigm(a * (xv - bj));
+        const float dz = G[1 + kGwNS + j] * (2.0f * sj * (1.0f - sj));
+        d += dz * a;
+        ga[j] += dz * (xv - bj);
+        gb[j] += dz * (-a);
+      }
+    }
+    if (gx) gx[b * in + i] = accumulate ? gx[b * in + i] + d : d;
+  }
+  if (abpart && lg) {
+#pragma unroll
+    for (int j = 0; j < kGwNB; ++j) {
+      float va = ga[j], vb = gb[j];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        va += __shfl_xor(va, o);
+        vb += __shfl_xor(vb, o);
+      }
+      if (lane == 0) {
+        abpart[(((int64_t)sp * in + i) * kGwNB + j) * 2 + 0] = va;
+        abpart[(((int64_t)sp * in + i) * kGwNB + j) * 2 + 1] = vb;
+      }
+    }
+  }
+  (void)red;
+}
+
+__global__ void wide_ab_reduce_kernel(fetode_kanlinear_t kl, const float* __restrict__ abpart, fetode_kanlinear_grad_t gr,
+                                      int accumulate) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int in = kl.in_features;
+  if (t >= in * kGwNB) return;
+  float va = abpart[(int64_t)t * 2], vb = abpart[(int64_t)t * 2 + 1];
+  for (int sp = 1; sp < kGwSplit; ++sp) {
+    va = va + abpart[((int64_t)sp * in * kGwNB + t) * 2];
+    vb = vb + abpart[((int64_t)sp * in * kGwNB + t) * 2 + 1];
+  }
+  put(gr.logistic_a ? gr.logistic_a + t : nullptr, va, accumulate);
+  put(gr.logistic_b ? gr.logistic_b + t : nullptr, vb, accumulate);
+}
+
+// the splits in order -> base-weight gradient, d_scaled (spline), d_wl (logistic) as kan_gw_kernel
+__global__ void wide_gw_reduce_kernel(fetode_kanlinear_t kl, const float* __restrict__ dpart, float* __restrict__ d_scaled,
+                                      float* __restrict__ d_wl, fetode_kanlinear_grad_t gr, int accumulate) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int in = kl.in_features, out = kl.out_features;
+  if (t >= (int64_t)out * in * kGwF) return;
+  const int f = (int)(t % kGwF);
+  const int64_t oi = t / kGwF;
+  const int o = (int)(oi / in), i = (int)(oi % in);
+  float v = dpart[(((int64_t)0 * in + i) * kGwF + f) * 16 + o];
+  for (int sp = 1; sp < kGwSplit; ++sp) v = v + dpart[(((int64_t)sp * in + i) * kGwF + f) * 16 + o];
+  if (f == 0) put(gr.base_weight ? gr.base_weight + (int64_t)o * in + i : nullptr, v, accumulate);
+  else if (f <= kGwNS) d_scaled[((int64_t)o * in + i) * kGwNS + (f - 1)] = v;
+  else if (kl.num_logistic) d_wl[(int64_t)o * in * kGwNB + i * kGwNB + (f - 1 - kGwNS)] = v;
+}
+
 // chain rule of the scaled weights: spline_weight, spline_scaler, logistic_weight, logistic_scaler
 __global__ void kan_scale_grads_kernel(fetode_kanlinear_t kl, const float* __restrict__ d_scaled,
                                        const float* __restrict__ d_wl, fetode_kanlinear_grad_t gr, int accumulate) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int in = kl.in_features, out = kl.out_features, NB = kl.num_logistic;
   const int NS = kl.grid_size + kl.spline_order;
-  if (t < out * in) {
+  if (t < (int64_t)out * in) {
     const int o = t / in, i = t % in;
     const float sc = kl.spline_scaler ? kl.spline_scaler[t] : 1.0f;
     float dsc = 0.f;
@@ -201,18 +429,23 @@ __global__ void kan_scale_grads_kernel(fetode_kanlinear_t kl, const float* __res
     (void)o;
     (void)i;
   }
-  if (NB > 0 && t < out) {
-    const float ls = kl.logistic_scaler ? kl.logistic_scaler[t] : 1.0f;
-    float dls = 0.f;
-    for (int q = 0; q < in * NB; ++q) {
-      const float dw = d_wl[(int64_t)t * in * NB + q];
-      const float lw = kl.logistic_weight[(int64_t)t * in * NB + q];
-      put(gr.logistic_weight ? gr.logistic_weight + (int64_t)t * in * NB + q : nullptr,
-          (dw * ls) * kl.scale_logistic, accumulate);
-      dls += dw * (lw * kl.scale_logistic);
-    }
-    if (kl.logistic_scaler) put(gr.logistic_scaler ? gr.logistic_scaler + t : nullptr, dls, accumulate);
+  if (NB > 0 && t < (int64_t)out * in * NB) {   // one thread per logistic weight
+    const int o = (int)(t / ((int64_t)in * NB));
+    const float ls = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
+    put(gr.logistic_weight ? gr.logistic_weight + t : nullptr, (d_wl[t] * ls) * kl.scale_logistic, accumulate);
   }
+}
+
+// d logistic_scaler[o] = sum_q dW'[o, q] (W[o, q] scale): a fixed-order sum per output
+__global__ void kan_scale_ls_kernel(fetode_kanlinear_t kl, const float* __restrict__ d_wl, fetode_kanlinear_grad_t gr,
+                                    int accumulate) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int in = kl.in_features, NB = kl.num_logistic;
+  if (t >= kl.out_features) return;
+  float dls = 0.f;
+  for (int q = 0; q < in * NB; ++q)
+    dls += d_wl[(int64_t)t * in * NB + q] * (kl.logistic_weight[(int64_t)t * in * NB + q] * kl.scale_logistic);
+  put(gr.logistic_scaler ? gr.logistic_scaler + t : nullptr, dls, accumulate);
 }
 
 // logistic basis parameters a, b: one block per (i, j)
@@ -349,7 +582,10 @@ extern "C" {
 int64_t fetode_kanlinear_backward_workspace(const fetode_kanlinear_t* kl) {
   if (!kl) return -1;
   const int NS = kl->grid_size + kl->spline_order;
-  return (int64_t)sizeof(float) * kl->out_features * kl->in_features * (NS + kl->num_logistic);
+  int64_t n = (int64_t)kl->out_features * kl->in_features * (NS + kl->num_logistic);
+  if (fetode_kanlinear_wide_supported(kl))   // MFMA partials + logistic a / b partials
+    n += (int64_t)kGwSplit * kl->in_features * (kGwF * 16 + 2 * kGwNB);
+  return (int64_t)sizeof(float) * n;
 }
 
 int fetode_kanlinear_backward(const fetode_kanlinear_t* kl, const float* x, int64_t B, const float* g,
@@ -363,7 +599,20 @@ int fetode_kanlinear_backward(const fetode_kanlinear_t* kl, const float* x, int6
   hipStream_t s = (hipStream_t)stream;
   const int in = kl->in_features, out = kl->out_features, NB = kl->num_logistic, SO = kl->spline_order;
   const int NS = kl->grid_size + SO;
-  if (gx) {
+  const bool wide = fetode_kanlinear_wide_supported(kl) && B >= 256;
+  if (wide && (gx || (grads && NB > 0))) {   // d x and d (a, b) in one pass over the batch
+    if (grads && !workspace) return set_err(FETODE_EINVAL, "kanlinear backward: workspace required for parameter grads");
+    float* abpart = (grads && NB > 0)
+                        ? (float*)workspace + (int64_t)out * in * (NS + NB) + (int64_t)kGwSplit * in * kGwF * 16
+                        : nullptr;
+    hipLaunchKernelGGL(wide_gxab_kernel, dim3(in / 4, kGwSplit), dim3(256), 0, s, *kl, x, g, B, gx, abpart, accumulate);
+    LAUNCH_CHECK();
+    if (abpart) {
+      hipLaunchKernelGGL(wide_ab_reduce_kernel, dim3(nblk((int64_t)in * NB, 256)), dim3(256), 0, s, *kl, abpart, *grads,
+                         accumulate);
+      LAUNCH_CHECK();
+    }
+  } else if (gx) {
     const int64_t n = B * in;
 #define KGX(S) hipLaunchKernelGGL(kan_gx_kernel<S>, dim3(nblk(n, 256)), dim3(256), 0, s, *kl, x, g, B, gx, accumulate)
     if (SO == 1) KGX(1); else if (SO == 2) KGX(2); else KGX(3);
@@ -374,15 +623,28 @@ int fetode_kanlinear_backward(const fetode_kanlinear_t* kl, const float* x, int6
     if (!workspace) return set_err(FETODE_EINVAL, "kanlinear backward: workspace required for parameter grads");
     float* d_scaled = (float*)workspace;
     float* d_wl = d_scaled + (int64_t)out * in * NS;
-    const int nblocks = out * in * (1 + NS + NB);
+    if (wide) {   // MFMA contraction over the batch
+      float* dpart = d_wl + (int64_t)out * in * NB;
+      hipLaunchKernelGGL(wide_gw_kernel, dim3(in / 4, kGwSplit), dim3(256), 0, s, *kl, x, g, B, dpart);
+      LAUNCH_CHECK();
+      hipLaunchKernelGGL(wide_gw_reduce_kernel, dim3(nblk((int64_t)out * in * kGwF, 256)), dim3(256), 0, s, *kl, dpart,
+                         d_scaled, d_wl, *grads, accumulate);
+      LAUNCH_CHECK();
+    } else {
+      const int nblocks = out * in * (1 + NS + NB);
 #define KGW(S) hipLaunchKernelGGL(kan_gw_kernel<S>, dim3(nblocks), dim3(RB), 0, s, *kl, x, g, B, d_scaled, d_wl, *grads, accumulate)
-    if (SO == 1) KGW(1); else if (SO == 2) KGW(2); else KGW(3);
+      if (SO == 1) KGW(1); else if (SO == 2) KGW(2); else KGW(3);
 #undef KGW
+      LAUNCH_CHECK();
+    }
+    hipLaunchKernelGGL(kan_scale_grads_kernel, dim3(nblk((int64_t)out * in * (NB > 1 ? NB : 1), 128)), dim3(128), 0, s,
+                       *kl, d_scaled, d_wl, *grads, accumulate);
     LAUNCH_CHECK();
-    hipLaunchKernelGGL(kan_scale_grads_kernel, dim3(nblk((int64_t)out * in, 128)), dim3(128), 0, s, *kl, d_scaled,
-                       d_wl, *grads, accumulate);
-    LAUNCH_CHECK();
-    if (NB > 0) {
+    if (NB > 0 && kl->logistic_scaler) {
+      hipLaunchKernelGGL(kan_scale_ls_kernel, dim3(nblk(out, 64)), dim3(64), 0, s, *kl, d_wl, *grads, accumulate);
+      LAUNCH_CHECK();
+    }
+    if (NB > 0 && !wide) {
       hipLaunchKernelGGL(kan_gab_kernel, dim3(in * NB), dim3(RB), 0, s, *kl, x, g, B, *grads, accumulate);
       LAUNCH_CHECK();
     }

@@ -145,14 +145,30 @@ __global__ __launch_bounds__(kKThreads) void kuramoto_bwd_kernel(int H, int W, i
   }
 }
 
-// out[j] (+)= sum_b part[b, j], b in increasing order in fp64: one thread per column
-__global__ void column_sum_kernel(const float* __restrict__ part, int64_t B, int n, float* __restrict__ out,
-                                  int accumulate) {
+// out[j] = sum_b part[b, j] in a fixed order, two levels: 64 row slices x 4 row phases per column
+// block (64 columns wide, coalesced), fp64 partials, then the 64 slices in order
+constexpr int kColSlices = 64;
+__global__ __launch_bounds__(256) void column_sum_part_kernel(const float* __restrict__ part, int64_t B, int n,
+                                                              double* __restrict__ mid) {
+  __shared__ double red[4][64];
+  const int c = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + c;
+  const int sl = blockIdx.y;
+  const int64_t b0 = sl * B / kColSlices, b1 = (sl + 1) * B / kColSlices;
+  double s = 0.0;
+  if (j < n)
+    for (int64_t b = b0 + ph; b < b1; b += 4) s += (double)part[b * n + j];
+  red[ph][c] = s;
+  __syncthreads();
+  if (ph == 0 && j < n) mid[(int64_t)sl * n + j] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+}
+
+__global__ void column_sum_final_kernel(const double* __restrict__ mid, int n, float* __restrict__ out) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   double s = 0.0;
-  for (int64_t b = 0; b < B; ++b) s += (double)part[b * n + j];
-  out[j] = accumulate ? out[j] + (float)s : (float)s;
+  for (int sl = 0; sl < kColSlices; ++sl) s += mid[(int64_t)sl * n + j];
+  out[j] = (float)s;
 }
 
 
@@ -296,7 +312,8 @@ int fetode_kuramoto_forward(const float* x, int64_t B, int32_t H, int32_t W, int
 }
 
 int64_t fetode_kuramoto_backward_workspace(int64_t B, int32_t H, int32_t W) {
-  return (int64_t)sizeof(float) * B * ((int64_t)H * W + 1);
+  // per-image partials (d omega, d K) + fp64 slice sums of both
+  return (int64_t)sizeof(float) * B * ((int64_t)H * W + 1) + (int64_t)sizeof(double) * kColSlices * ((int64_t)H * W + 1) + 16;
 }
 
 int fetode_kuramoto_backward(int64_t B, int32_t H, int32_t W, int32_t steps, float dt, const float* K,
@@ -315,12 +332,20 @@ int fetode_kuramoto_backward(int64_t B, int32_t H, int32_t W, int32_t steps, flo
   hipLaunchKernelGGL(kuramoto_bwd_kernel, dim3((unsigned)B), dim3(kKThreads), lds, s, H, W, steps, dt, K, tape, gfeat,
                      gx, gK_part, gom_part);
   LAUNCH_CHECK();
+  // fp64 slice sums, 8-byte aligned after the float partials
+  const int64_t fl = B * ((int64_t)HW + 1);
+  double* mid = (double*)((char*)workspace + ((sizeof(float) * fl + 15) & ~(size_t)15));
   if (gomega) {
-    hipLaunchKernelGGL(column_sum_kernel, dim3((HW + 255) / 256), dim3(256), 0, s, gom_part, B, HW, gomega, 0);
+    hipLaunchKernelGGL(column_sum_part_kernel, dim3((HW + 63) / 64, kColSlices), dim3(256), 0, s, gom_part, B, HW, mid);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(column_sum_final_kernel, dim3((HW + 255) / 256), dim3(256), 0, s, mid, HW, gomega);
     LAUNCH_CHECK();
   }
   if (gK) {
-    hipLaunchKernelGGL(column_sum_kernel, dim3(1), dim3(256), 0, s, gK_part, B, 1, gK, 0);
+    double* midk = mid + (int64_t)kColSlices * HW;
+    hipLaunchKernelGGL(column_sum_part_kernel, dim3(1, kColSlices), dim3(256), 0, s, gK_part, B, 1, midk);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(column_sum_final_kernel, dim3(1), dim3(256), 0, s, midk, 1, gK);
     LAUNCH_CHECK();
   }
   return FETODE_OK;
