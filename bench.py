@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ecg", action="store_true", help="skip the ECG dopri5 (configs[2]) line")
     ap.add_argument("--no-mnist", action="store_true", help="skip the MNIST Kuramoto + KANLinear line")
+    ap.add_argument("--no-ett", action="store_true", help="skip the ETT KAN-FET latent-ODE forecaster line")
+    ap.add_argument("--ett-batch", type=int, default=8192)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--train-iters", type=int, default=20, help="0 skips the training-rate line")
     return ap.parse_args()
@@ -250,6 +252,58 @@ def mnist_rate(dev, batch=8192, reps=10, cpu_seconds=5.0, with_cpu=True):
     return out
 
 
+def ett_rate(dev, batch=8192, reps=2, substeps=4, cpu_seconds=5.0, with_cpu=True):
+    """The ETT config (train_kan_fet_ett.py:155-197, BASELINE configs[3]): LatentNeuralODEForecaster
+    on 96 -> 96 windows of a 7-column synthetic ETTh1-shaped series (the dataset is not in the
+    image), latent 64, KAN-FET latent field [64, 128, 64] (K=10), odeint_rk4 with the reference
+    TrainConfig's rk4_substeps=4 over t_fut = 0..95.  Forward windows/s under no_grad on one GPU."""
+    from fet_ode_amd import ett
+    from oracle import ett_ref as E
+    from oracle import torch_ref as O
+    c = p = 96
+    torch.manual_seed(0)
+    m = ett.LatentNeuralODEForecaster(num_features=7, context_len=c, pred_len=p, latent_dim=64, solver="rk4")
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    g = torch.Generator().manual_seed(4)
+    series = torch.cumsum(torch.randn(batch + c + p, 7, generator=g), 0) * 0.05
+    ds = ett.EnergyWindowDataset(series, series[:, -1], c, p, device=dev)
+    xb, _ = ds.batch(torch.arange(batch, device=dev))
+    t_fut = torch.linspace(0.0, float(p - 1), steps=p, device=dev)
+    with torch.no_grad():
+        finite = bool(torch.isfinite(m(xb, t_fut, rk4_substeps=substeps)).all())
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            m(xb, t_fut, rk4_substeps=substeps)
+        torch.cuda.synchronize(dev)
+    fwd = (time.perf_counter() - t0) / reps
+    steps = (p - 1) * substeps
+    out = {"value": batch / fwd, "unit": "forecast windows/s forward (96->96, 1 GPU)", "ms_per_batch": fwd * 1e3,
+           "rk4_steps_per_s": batch * steps / fwd, "finite": finite,
+           "workload": f"LatentNeuralODEForecaster(7 features, 96->96, latent 64, KANFET[64,128,64] K=10), "
+                       f"odeint_rk4 x{substeps} substeps ({steps} steps), batch {batch}, synthetic series"}
+    if with_cpu:
+        cores = min(16, os.cpu_count() or 1)
+        torch.set_num_threads(cores)
+        field = O.KANFETRef.from_state_dict({k[len("dynamics.net."):]: v for k, v in sd.items()
+                                             if k.startswith("dynamics.net.")}, 2)
+        ref = E.ForecasterRef(sd, lambda tt, zz: field(zz))
+        xs = xb[:8].cpu()
+        tc = t_fut.cpu()
+        n, t0 = 0, time.perf_counter()
+        with torch.no_grad():
+            while n < 1 or (time.perf_counter() - t0 < cpu_seconds and n < 5):
+                field.reset_state()
+                ref(xs, tc, rk4_substeps=substeps)
+                n += 1
+        cel = (time.perf_counter() - t0) / n
+        out["cpu_baseline"] = {"value": 8 / cel, "unit": out["unit"].replace("1 GPU", "CPU"), "cores": cores,
+                               "kind": "port", "sample": f"{n} forward(s) of 8 of the windows with oracle/ett_ref.py "
+                                                         f"+ torch_ref.py (torch CPU fp32), {cel * n:.1f} s"}
+    return out
+
+
 def cpu_baseline(sd, y0, t, seconds):
     """The CPU oracle (restatement of the reference, reference op order) on this host's cores."""
     from oracle import torch_ref as O
@@ -370,6 +424,8 @@ def main():
             out["ecg"] = ecg_rate(dev, with_cpu=not args.no_cpu_baseline)
         if world == 1 and not args.no_mnist:
             out["mnist"] = mnist_rate(dev, with_cpu=not args.no_cpu_baseline)
+        if world == 1 and not args.no_ett:
+            out["ett"] = ett_rate(dev, batch=args.ett_batch, with_cpu=not args.no_cpu_baseline)
         if world == 1 and not args.no_cpu_baseline:
             cb, ref_sol = cpu_baseline(sd, y0, t, args.cpu_seconds)
             out["cpu_baseline"] = cb

@@ -63,7 +63,7 @@ def _check_inputs(y0, t, method):
 # ---------------------------------------------------------------------------------------------
 
 class Schedule:
-    __slots__ = ("step_coef", "out_step", "out_mode", "out_slope", "n_steps", "T", "grid", "dev")
+    __slots__ = ("step_coef", "out_step", "out_mode", "out_slope", "n_steps", "T", "grid", "dev", "h")
 
     def __init__(self, tp: torch.Tensor, step_size, reversed_: bool):
         if step_size is None:
@@ -100,8 +100,40 @@ class Schedule:
                     out_slope[j] = np.float32((tt[j] - t0) / (t1 - t0))
                 j += 1
         self.step_coef, self.out_step, self.out_mode, self.out_slope = coef, out_step, out_mode, out_slope
-        self.n_steps, self.T, self.grid = n, T, g
+        self.n_steps, self.T, self.grid, self.h = n, T, g, None
         self.dev: Dict[torch.device, Tuple[torch.Tensor, ...]] = {}
+
+    @classmethod
+    def substeps(cls, tp: torch.Tensor, n_sub: int) -> "Schedule":
+        """The grid of ``odeint_rk4(f, z0, t, n_substeps)`` (train_kan_fet_ett.py:51-83): per output
+        interval h = (t1 - t0) / n_substeps in t's dtype, substep times ti = ti + h accumulated from
+        t0, and every substep advanced with that same h; solution[j] = z after interval j."""
+        s = object.__new__(cls)
+        tt = tp.numpy()
+        T = len(tt)
+        grid, hs = [tt[0]], []
+        for i in range(T - 1):
+            t0, t1 = tt[i], tt[i + 1]
+            h = (t1 - t0) / tt.dtype.type(n_sub)
+            ti = t0
+            for k in range(n_sub):
+                hs.append(h)
+                ti = ti + h
+                grid.append(ti)
+        hs = np.asarray(hs, dtype=tt.dtype)
+        n = len(hs)
+        coef = np.zeros((n, 4), dtype=np.float32)
+        coef[:, 0] = hs.astype(np.float32)
+        coef[:, 1] = (0.5 * hs).astype(np.float32)
+        coef[:, 2] = (hs / 6.0).astype(np.float32)
+        out_step = np.zeros(T, dtype=np.int32)
+        out_mode = np.zeros(T, dtype=np.int32)
+        out_step[1:] = np.arange(1, T, dtype=np.int32) * n_sub - 1
+        out_mode[1:] = 1
+        s.step_coef, s.out_step, s.out_mode, s.out_slope = coef, out_step, out_mode, np.zeros(T, np.float32)
+        s.n_steps, s.T, s.grid, s.h = n, T, np.asarray(grid, dtype=tt.dtype), hs
+        s.dev = {}
+        return s
 
     def device_arrays(self, device):
         """One async H2D upload per device, cached."""
@@ -299,13 +331,14 @@ def _per_stage_fixed(func, y0, sched: Schedule, method: str, tc_dtype, reversed_
     g = sched.grid
     sign = -1.0 if reversed_ else 1.0
 
-    def tt(v):
-        return torch.tensor(sign * v, dtype=y0.dtype)
+    def tt(v):  # on y0's device, like torchdiffeq's t (fields may torch.cat it with the state)
+        return torch.tensor(sign * v, dtype=y0.dtype).to(y0.device, non_blocking=True)
 
     j = 1
     for s in range(sched.n_steps):
         dt, hh, h6 = (float(v) for v in sched.step_coef[s, :3])
         t0, t1 = g[s], g[s + 1]
+        hs = sched.h[s] if sched.h is not None else t1 - t0   # odeint_rk4: stage times ti + h / 2, ti + h
         if method == "rk4":
             k1 = func(tt(t0), y)
             k2 = func(tt(t0 + (t1 - t0) / 3), _combine(_lib.RK4, 1, dt, y, k1))
@@ -320,9 +353,9 @@ def _per_stage_fixed(func, y0, sched: Schedule, method: str, tc_dtype, reversed_
             y1 = _combine(_lib.EULER, 4, dt, y, k2)
         else:  # rk4_classic
             k1 = func(tt(t0), y)
-            k2 = func(tt(t0 + 0.5 * (t1 - t0)), _combine(_lib.EULER, 4, hh, y, k1))
-            k3 = func(tt(t0 + 0.5 * (t1 - t0)), _combine(_lib.EULER, 4, hh, y, k2))
-            k4 = func(tt(t1), _combine(_lib.EULER, 4, dt, y, k3))
+            k2 = func(tt(t0 + 0.5 * hs), _combine(_lib.EULER, 4, hh, y, k1))
+            k3 = func(tt(t0 + 0.5 * hs), _combine(_lib.EULER, 4, hh, y, k2))
+            k4 = func(tt(t0 + hs), _combine(_lib.EULER, 4, dt, y, k3))
             y1 = _combine(_lib.RK4_CLASSIC, 4, h6, y, k1, k2, k3, k4)
         while j < sched.T and sched.out_step[j] == s:
             m = sched.out_mode[j]
