@@ -6,16 +6,19 @@ Drop-in surface of the reference hot path (sallywang147/FET-ODE):
   * ``ferro_class``          — FerroelectricBasis
   * ``ecg``                  — the ECG KAN-FET NODE (hysteretic LogisticBasis, KANFeatureMixer,
                                No_MLP_KANODEFunc, KanFet_NODE; train_ecg_kan_fet_nn_ode.py)
+  * ``mnist``                — the MNIST Kuramoto + KANLinear classifier (mnist_kuramoto_kan.py)
+  * ``ett``                  — odeint_rk4, EnergyWindowDataset, the KAN-FET LatentNeuralODEForecaster
+                               (train_kan_fet_ett.py)
   * ``autonomous(field)``    — calDeriv-style func(t, y) = field(y) that odeint integrates in a
                                single fused HIP launch
 All compute runs in libfetode.so (HIP, gfx950) through the C ABI of include/fetode.h.
 """
 from . import _lib
-from . import ecg, efficientkan, ferro_class
+from . import ecg, efficientkan, ett, ferro_class, mnist
 from .efficientkan import KAN, KANFET, KANFETLayer, KANLinear, LogisticBasis, ODEFunc, autonomous
 from .ferro_class import FerroelectricBasis
 from .odeint import SOLVERS, odeint, set_fused_training
 
 __all__ = ["odeint", "SOLVERS", "set_fused_training", "KAN", "KANFET", "KANFETLayer", "KANLinear", "LogisticBasis",
-           "FerroelectricBasis", "ODEFunc", "autonomous", "ecg", "efficientkan", "ferro_class"]
+           "FerroelectricBasis", "ODEFunc", "autonomous", "ecg", "efficientkan", "ett", "ferro_class", "mnist"]
 __version__ = "0.1.0"

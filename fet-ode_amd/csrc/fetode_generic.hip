@@ -5,6 +5,8 @@
 //   rk_combine_kernel     torchdiffeq stage combines (exact op order)
 #include "fetode_common.h"
 
+#include <cstdlib>
+
 using namespace fetode;
 
 // ---------------------------------------------------------------------------------------------
@@ -91,6 +93,132 @@ __global__ void ferro_fwd_kernel(fetode_ferro_t fl, const float* __restrict__ x,
   out[t] = accumulate ? out[t] + acc : acc;
 }
 
+// KANLinear.forward for wide layers: a wave owns 64 rows (lane -> b) x kOB outputs, so the features
+// of (b, i) — SiLU, the cubic B-spline bases, the logistic bases — are computed once per wave and
+// reused for kOB outputs (the thread-per-(b, o) kernel recomputes them for every o), and every
+// weight read is wave-uniform (scalar loads).  Per output the accumulation order is the thread
+// kernel's (base, spline over c ascending incl. the zero bases, logistic over j), so the two agree
+// bit for bit.
+constexpr int kNBMax = 16;
+template <int SO, int G, int kOB>
+__global__ __launch_bounds__(256) void kanlinear_fwd_wave_kernel(fetode_kanlinear_t kl, const float* __restrict__ x,
+                                                                int64_t B, float* __restrict__ out) {
+  constexpr int NG = G + 2 * SO + 1, NS = G + SO;
+  const int in = kl.in_features, outf = kl.out_features, NB = kl.num_logistic;
+  const int lane = threadIdx.x & 63;
+  const int o0 = (blockIdx.y * 4 + (threadIdx.x >> 6)) * kOB;
+  if (o0 >= outf) return;
+  const int64_t b = (int64_t)blockIdx.x * 64 + lane;
+  const bool live = b < B;
+  const int no = min(kOB, outf - o0);
+  float base[kOB], spl[kOB], lgs[kOB], lsc[kOB];
+#pragma unroll
+  for (int q = 0; q < kOB; ++q) {
+    base[q] = spl[q] = lgs[q] = 0.f;
+    lsc[q] = (q < no && NB > 0 && kl.logistic_scaler) ? kl.logistic_scaler[o0 + q] : 1.0f;
+  }
+  for (int i = 0; i < in; ++i) {
+    const float xi = live ? x[b * in + i] : 0.f;
+    const float silu = xi / (1.0f + expf(-xi));
+    float S[NS];
+    bspline_local_div<SO>(xi, NG, kl.grid + (int64_t)i * NG, [&](int c, float v) {
+#pragma unroll
+      for (int cc = 0; cc < NS; ++cc)   // register select (no dynamically indexed private array)
+        if (cc == c) S[cc] = v;
+    });
+    float phi[kNBMax];
+#pragma unroll
+    for (int j = 0; j < kNBMax; ++j) {
+      if (j < NB) {
+        const float a = kl.logistic_a[i * NB + j], bb = kl.logistic_b[i * NB + j];
+        phi[j] = 2.0f / (1.0f + expf(-a * (xi - bb)));
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kOB; ++q) {
+      if (q >= no) break;
+      const int o = o0 + q;
+      base[q] += silu * kl.base_weight[o * in + i];
+      const float sc = kl.spline_scaler ? kl.spline_scaler[o * in + i] : 1.0f;
+      const float* sw = kl.spline_weight + ((int64_t)o * in + i) * NS;
+#pragma unroll
+      for (int c = 0; c < NS; ++c) spl[q] += S[c] * (sw[c] * sc);
+      const float* lw = kl.logistic_weight + (int64_t)o * in * NB + i * NB;
+#pragma unroll
+      for (int j = 0; j < kNBMax; ++j)
+        if (j < NB) lgs[q] += phi[j] * ((lw[j] * kl.scale_logistic) * lsc[q]);
+    }
+  }
+  if (!live) return;
+#pragma unroll
+  for (int q = 0; q < kOB; ++q) {
+    if (q >= no) break;
+    float r = base[q] + spl[q];
+    if (NB > 0) r = r + lgs[q];
+    out[b * outf + o0 + q] = r;
+  }
+}
+
+// FerroelectricBasis.forward for wide layers with the constant branch_sign (the reference never
+// updates it, ferro_class.py:377-378) and no activations output: a wave owns 64 rows (lane -> b)
+// and one output o, so every parameter read is wave-uniform (scalar loads); x and the hysteresis
+// gate of the (64 rows x in) tile are staged once per block in LDS ([i][row], conflict-free).  The
+// gate sigmoid(gate_slope (x - prev_x)) keeps the precise exp (it carries the fp32 conditioning of
+// the hysteresis); the two coercive sigmoids and tanh use v_exp_f32 / v_rcp_f32
+// (tanh z = 1 - 2 / (1 + e^{2z})), ~1 ulp each.  Two-level sum as the thread kernel.
+__global__ __launch_bounds__(256) void ferro_fwd_wide_kernel(fetode_ferro_t fl, const float* __restrict__ x, int64_t B,
+                                                            const float* __restrict__ prev, int reinit,
+                                                            int accumulate, float* __restrict__ out) {
+  extern __shared__ float sm[];
+  const int in = fl.in_dim, outd = fl.out_dim, K = fl.num_basis;
+  const float gs = (float)fl.gate_slope, al = (float)fl.alpha, oma = (float)(1.0 - fl.alpha);
+  float* xs = sm;
+  float* ups = sm + in * 64;
+  const int64_t b0 = (int64_t)blockIdx.x * 64;
+  for (int idx = threadIdx.x; idx < 64 * in; idx += 256) {
+    const int r = idx / in, i = idx - r * in;
+    const int64_t b = b0 + r;
+    float xv = 0.f, up = 0.f;
+    if (b < B) {
+      xv = x[b * in + i];
+      const float pv = reinit ? xv : prev[b * in + i];
+      up = 1.0f / (1.0f + expf(-(gs * (xv - pv))));
+    }
+    xs[i * 64 + r] = xv;
+    ups[i * 64 + r] = up;
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int o = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (o >= outd) return;
+  const int64_t b = b0 + lane;
+  float acc = 0.f;
+  for (int i = 0; i < in; ++i) {
+    const float xv = xs[i * 64 + lane], up = ups[i * 64 + lane];
+    const float omu = 1.0f - up;
+    const int e0 = (i * outd + o) * K;
+    float acc_i = 0.f;
+    for (int k = 0; k < K; ++k) {
+      const int e = e0 + k;
+      const float Ec = fl.Ec[e];
+      const float cp = __builtin_amdgcn_rcpf(1.0f + __expf(-(gs * (xv - Ec))));
+      const float cn = __builtin_amdgcn_rcpf(1.0f + __expf(-(gs * (-xv - Ec))));
+      const float su = up * cp, sl = omu * cn;
+      const float tgt = (su - sl) + ((1.0f - su) - sl);       // branch_sign = 1
+      const float mom = al + oma * tgt;
+      const float sh = xv + Ec * mom;
+      const float th = 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * (fl.k[e] * sh)));
+      const float bv = fl.Ps[e] * th + fl.bias[e];
+      acc_i += bv * fl.coef[e];
+    }
+    acc += acc_i;
+  }
+  if (b < B) {
+    const int64_t t = b * outd + o;
+    out[t] = accumulate ? out[t] + acc : acc;
+  }
+}
+
 __global__ void rk_combine_kernel(int method, int stage, const float* __restrict__ y,
                                   const float* __restrict__ k1, const float* __restrict__ k2,
                                   const float* __restrict__ k3, const float* __restrict__ k4, float dt,
@@ -137,6 +265,27 @@ int fetode_kanlinear_forward(const fetode_kanlinear_t* kl, const float* x, int64
   if (rc) return rc;
   if (B <= 0) return FETODE_OK;
   if (!x || !out) return set_err(FETODE_EINVAL, "null pointer");
+  if (kl->out_features >= 16 && kl->num_logistic <= kNBMax && kl->grid_size == 5 && kl->spline_order == 3) {
+    // outputs per wave: the largest of 8/4/2/1 that still gives >= 1024 workgroups (4 per CU); fewer
+    // outputs per wave recompute the features more often but fill the chip at small batches
+    static const int64_t min_blocks = [] {
+      const char* e = getenv("FETODE_WAVE_MIN_BLOCKS");  // tuning knob (default 1024, measured r01_s5)
+      return e ? (int64_t)atoll(e) : (int64_t)1024;
+    }();
+    const int64_t rb = (B + 63) / 64;
+    int ob = 8;
+    while (ob > 1 && rb * ((kl->out_features + 4 * ob - 1) / (4 * ob)) < min_blocks) ob >>= 1;
+    const dim3 grid((unsigned)rb, (unsigned)((kl->out_features + 4 * ob - 1) / (4 * ob)));
+    const hipStream_t st = (hipStream_t)stream;
+    switch (ob) {
+      case 8: hipLaunchKernelGGL((kanlinear_fwd_wave_kernel<3, 5, 8>), grid, dim3(256), 0, st, *kl, x, B, out); break;
+      case 4: hipLaunchKernelGGL((kanlinear_fwd_wave_kernel<3, 5, 4>), grid, dim3(256), 0, st, *kl, x, B, out); break;
+      case 2: hipLaunchKernelGGL((kanlinear_fwd_wave_kernel<3, 5, 2>), grid, dim3(256), 0, st, *kl, x, B, out); break;
+      default: hipLaunchKernelGGL((kanlinear_fwd_wave_kernel<3, 5, 1>), grid, dim3(256), 0, st, *kl, x, B, out); break;
+    }
+    LAUNCH_CHECK();
+    return FETODE_OK;
+  }
   const int64_t n = B * kl->out_features;
   switch (kl->spline_order) {
     case 1: hipLaunchKernelGGL(kanlinear_fwd_kernel<1>, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, *kl, x, B, out); break;
@@ -174,8 +323,14 @@ int fetode_ferro_forward(const fetode_ferro_t* fl, const float* x, int64_t B, co
   if (B <= 0) return FETODE_OK;
   if (!x || !out || (!reinit && !prev)) return set_err(FETODE_EINVAL, "null pointer");
   const int64_t n = B * fl->out_dim;
-  hipLaunchKernelGGL(ferro_fwd_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, *fl, x, B,
-                     prev, reinit, accumulate, out, basis);
+  if (fl->in_dim >= 32 && fl->in_dim <= 128 && !fl->branch_sign && !basis) {
+    const dim3 grid((unsigned)((B + 63) / 64), (unsigned)((fl->out_dim + 3) / 4));
+    hipLaunchKernelGGL(ferro_fwd_wide_kernel, grid, dim3(256), (size_t)fl->in_dim * 64 * 2 * sizeof(float),
+                       (hipStream_t)stream, *fl, x, B, prev, reinit, accumulate, out);
+  } else {
+    hipLaunchKernelGGL(ferro_fwd_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, *fl, x, B,
+                       prev, reinit, accumulate, out, basis);
+  }
   LAUNCH_CHECK();
   if (prev_out)
     HIP_CHECK_RET(hipMemcpyAsync(prev_out, x, sizeof(float) * B * fl->in_dim, hipMemcpyDeviceToDevice,
