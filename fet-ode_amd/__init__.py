@@ -14,11 +14,11 @@ Drop-in surface of the reference hot path (sallywang147/FET-ODE):
 All compute runs in libfetode.so (HIP, gfx950) through the C ABI of include/fetode.h.
 """
 from . import _lib
-from . import ecg, efficientkan, ett, ferro_class, mnist
+from . import ecg, efficientkan, ett, ferro_class, lv, mnist
 from .efficientkan import KAN, KANFET, KANFETLayer, KANLinear, LogisticBasis, ODEFunc, autonomous
 from .ferro_class import FerroelectricBasis
 from .odeint import SOLVERS, odeint, set_fused_training
 
 __all__ = ["odeint", "SOLVERS", "set_fused_training", "KAN", "KANFET", "KANFETLayer", "KANLinear", "LogisticBasis",
-           "FerroelectricBasis", "ODEFunc", "autonomous", "ecg", "efficientkan", "ett", "ferro_class", "mnist"]
+           "FerroelectricBasis", "ODEFunc", "autonomous", "ecg", "efficientkan", "ett", "ferro_class", "lv", "mnist"]
 __version__ = "0.1.0"
