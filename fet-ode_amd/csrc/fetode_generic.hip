@@ -161,59 +161,88 @@ __global__ __launch_bounds__(256) void kanlinear_fwd_wave_kernel(fetode_kanlinea
 
 // FerroelectricBasis.forward for wide layers with the constant branch_sign (the reference never
 // updates it, ferro_class.py:377-378) and no activations output: a wave owns 64 rows (lane -> b)
-// and one output o, so every parameter read is wave-uniform (scalar loads); x and the hysteresis
-// gate of the (64 rows x in) tile are staged once per block in LDS ([i][row], conflict-free).  The
-// gate sigmoid(gate_slope (x - prev_x)) keeps the precise exp (it carries the fp32 conditioning of
-// the hysteresis); the two coercive sigmoids and tanh use v_exp_f32 / v_rcp_f32
-// (tanh z = 1 - 2 / (1 + e^{2z})), ~1 ulp each.  Two-level sum as the thread kernel.
+// and one output o, so every parameter read is wave-uniform.  Inputs are walked in chunks of kFI:
+// per chunk the block stages x, the hysteresis gate and e^{-gs x}, e^{gs x} of its (64 rows x kFI)
+// tile in LDS ([i][row], conflict-free), and each wave stages P = e^{gs Ec} of its own output.
+// The two coercive sigmoids then need no exponential per basis element:
+//     sigma(gs (x - Ec)) = 1 / (1 + e^{-gs x} P),   sigma(gs (-x - Ec)) = 1 / (1 + e^{gs x} P)
+// (inputs with |gs x| > 80 take the direct form, so no 0 * inf can appear); tanh z =
+// 1 - 2 / (1 + e^{2z}) with v_exp_f32 / v_rcp_f32.  The gate sigmoid(gs (x - prev_x)) keeps the
+// precise exp (it carries the fp32 conditioning of the hysteresis).  Two-level sum as the thread
+// kernel (K bases of one input, then inputs).
+constexpr int kFI = 32, kFKMax = 16;
+template <int KT>  // KT > 0: the basis count as a compile-time constant (unrolled, batched scalar loads)
 __global__ __launch_bounds__(256) void ferro_fwd_wide_kernel(fetode_ferro_t fl, const float* __restrict__ x, int64_t B,
                                                             const float* __restrict__ prev, int reinit,
                                                             int accumulate, float* __restrict__ out) {
-  extern __shared__ float sm[];
-  const int in = fl.in_dim, outd = fl.out_dim, K = fl.num_basis;
+  __shared__ float xs[kFI * 64], ups[kFI * 64], e1s[kFI * 64], e2s[kFI * 64];
+  __shared__ float ps[4][kFI * kFKMax];
+  const int in = fl.in_dim, outd = fl.out_dim, K = KT > 0 ? KT : fl.num_basis;
   const float gs = (float)fl.gate_slope, al = (float)fl.alpha, oma = (float)(1.0 - fl.alpha);
-  float* xs = sm;
-  float* ups = sm + in * 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int o = blockIdx.y * 4 + w;
+  const bool ovalid = o < outd;
   const int64_t b0 = (int64_t)blockIdx.x * 64;
-  for (int idx = threadIdx.x; idx < 64 * in; idx += 256) {
-    const int r = idx / in, i = idx - r * in;
-    const int64_t b = b0 + r;
-    float xv = 0.f, up = 0.f;
-    if (b < B) {
-      xv = x[b * in + i];
-      const float pv = reinit ? xv : prev[b * in + i];
-      up = 1.0f / (1.0f + expf(-(gs * (xv - pv))));
-    }
-    xs[i * 64 + r] = xv;
-    ups[i * 64 + r] = up;
-  }
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int o = blockIdx.y * 4 + (threadIdx.x >> 6);
-  if (o >= outd) return;
   const int64_t b = b0 + lane;
   float acc = 0.f;
-  for (int i = 0; i < in; ++i) {
-    const float xv = xs[i * 64 + lane], up = ups[i * 64 + lane];
-    const float omu = 1.0f - up;
-    const int e0 = (i * outd + o) * K;
-    float acc_i = 0.f;
-    for (int k = 0; k < K; ++k) {
-      const int e = e0 + k;
-      const float Ec = fl.Ec[e];
-      const float cp = __builtin_amdgcn_rcpf(1.0f + __expf(-(gs * (xv - Ec))));
-      const float cn = __builtin_amdgcn_rcpf(1.0f + __expf(-(gs * (-xv - Ec))));
-      const float su = up * cp, sl = omu * cn;
-      const float tgt = (su - sl) + ((1.0f - su) - sl);       // branch_sign = 1
-      const float mom = al + oma * tgt;
-      const float sh = xv + Ec * mom;
-      const float th = 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * (fl.k[e] * sh)));
-      const float bv = fl.Ps[e] * th + fl.bias[e];
-      acc_i += bv * fl.coef[e];
+  for (int i0 = 0; i0 < in; i0 += kFI) {
+    const int ni = min(kFI, in - i0);
+    __syncthreads();  // the previous chunk is consumed
+    for (int idx = threadIdx.x; idx < 64 * ni; idx += 256) {
+      const int r = idx / ni, ii = idx - r * ni;
+      const int64_t bb = b0 + r;
+      float xv = 0.f, up = 0.f;
+      if (bb < B) {
+        xv = x[bb * in + i0 + ii];
+        const float pv = reinit ? xv : prev[bb * in + i0 + ii];
+        up = 1.0f / (1.0f + expf(-(gs * (xv - pv))));
+      }
+      const float gx = gs * xv;
+      xs[ii * 64 + r] = xv;
+      ups[ii * 64 + r] = up;
+      e1s[ii * 64 + r] = __expf(-gx);
+      e2s[ii * 64 + r] = __expf(gx);
     }
-    acc += acc_i;
+    if (ovalid)
+      for (int idx = lane; idx < ni * K; idx += 64) {
+        const int ii = idx / K, k = idx - ii * K;
+        ps[w][idx] = __expf(gs * fl.Ec[((i0 + ii) * outd + o) * K + k]);
+      }
+    __syncthreads();
+    if (!ovalid) continue;
+    for (int ii = 0; ii < ni; ++ii) {
+      const float xv = xs[ii * 64 + lane], up = ups[ii * 64 + lane];
+      const float e1 = e1s[ii * 64 + lane], e2 = e2s[ii * 64 + lane];
+      const bool direct = __any(fabsf(gs * xv) > 80.0f);   // wave-uniform: no divergent paths
+      const float omu = 1.0f - up;
+      const int e0 = ((i0 + ii) * outd + o) * K;
+      const float* P = &ps[w][ii * K];
+      float acc_i = 0.f;
+#pragma unroll
+      for (int k = 0; k < (KT > 0 ? KT : kFKMax); ++k) {
+        if (KT == 0 && k >= K) break;
+        const int e = e0 + k;
+        const float Ec = fl.Ec[e];
+        float cp, cn;
+        if (direct) {
+          cp = __builtin_amdgcn_rcpf(1.0f + __expf(-(gs * (xv - Ec))));
+          cn = __builtin_amdgcn_rcpf(1.0f + __expf(-(gs * (-xv - Ec))));
+        } else {
+          cp = __builtin_amdgcn_rcpf(1.0f + e1 * P[k]);
+          cn = __builtin_amdgcn_rcpf(1.0f + e2 * P[k]);
+        }
+        const float su = up * cp, sl = omu * cn;
+        const float tgt = (su - sl) + ((1.0f - su) - sl);       // branch_sign = 1
+        const float mom = al + oma * tgt;
+        const float sh = xv + Ec * mom;
+        const float th = 1.0f - 2.0f * __builtin_amdgcn_rcpf(1.0f + __expf(2.0f * (fl.k[e] * sh)));
+        const float bv = fl.Ps[e] * th + fl.bias[e];
+        acc_i += bv * fl.coef[e];
+      }
+      acc += acc_i;
+    }
   }
-  if (b < B) {
+  if (ovalid && b < B) {
     const int64_t t = b * outd + o;
     out[t] = accumulate ? out[t] + acc : acc;
   }
@@ -323,10 +352,15 @@ int fetode_ferro_forward(const fetode_ferro_t* fl, const float* x, int64_t B, co
   if (B <= 0) return FETODE_OK;
   if (!x || !out || (!reinit && !prev)) return set_err(FETODE_EINVAL, "null pointer");
   const int64_t n = B * fl->out_dim;
-  if (fl->in_dim >= 32 && fl->in_dim <= 128 && !fl->branch_sign && !basis) {
+  if (fl->in_dim >= 32 && fl->num_basis <= kFKMax && !fl->branch_sign && !basis) {
     const dim3 grid((unsigned)((B + 63) / 64), (unsigned)((fl->out_dim + 3) / 4));
-    hipLaunchKernelGGL(ferro_fwd_wide_kernel, grid, dim3(256), (size_t)fl->in_dim * 64 * 2 * sizeof(float),
-                       (hipStream_t)stream, *fl, x, B, prev, reinit, accumulate, out);
+    const hipStream_t st = (hipStream_t)stream;
+    if (fl->num_basis == 10)
+      hipLaunchKernelGGL(ferro_fwd_wide_kernel<10>, grid, dim3(256), 0, st, *fl, x, B, prev, reinit, accumulate, out);
+    else if (fl->num_basis == 12)
+      hipLaunchKernelGGL(ferro_fwd_wide_kernel<12>, grid, dim3(256), 0, st, *fl, x, B, prev, reinit, accumulate, out);
+    else
+      hipLaunchKernelGGL(ferro_fwd_wide_kernel<0>, grid, dim3(256), 0, st, *fl, x, B, prev, reinit, accumulate, out);
   } else {
     hipLaunchKernelGGL(ferro_fwd_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, *fl, x, B,
                        prev, reinit, accumulate, out, basis);
