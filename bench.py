@@ -2,10 +2,13 @@
 
 Workload (BASELINE.json configs[1]): KANFET([2,10,2], grid_size=5, K=10) as the
 vector field (train_kanfet_node_predprey.py:146), torch.manual_seed(0) weights, y0 = 0.5 +
-2.5*U[0,1)^(4096x2) (seed 0 + rank), t = linspace(0, 3.5, 35) float64 (t_learn, :155),
-method='rk4' (torchdiffeq 3/8 rule).  One bench "step" = one odeint solve = 34 RK4 steps of
-the whole batch, inputs resident in HBM.  value = RK4 batch-steps/s summed over ranks (weak
-scaling: every rank integrates its own 4096 trajectories; no collective on the forward path).
+2.5*U[0,1)^(4096x2), t = linspace(0, 3.5, 35) float64 (t_learn, :155), method='rk4' (torchdiffeq
+3/8 rule).  One bench "step" = one odeint solve = 34 RK4 steps of the batch, inputs resident in HBM.
+
+Scaling: --scaling strong (default, primary) splits the GLOBAL batch of 4096
+(seed 0) into contiguous per-rank blocks (fet_ode_amd.dist.shard_bounds): value = batch-4096 RK4
+steps/s of the whole job.  --scaling weak gives every rank its own 4096 trajectories (seed = rank):
+value = batch-4096 steps/s summed over ranks.  The forward path needs no collective either way.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run.
 Prints ONE JSON line on rank 0.
@@ -52,42 +55,58 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong: global batch 4096 split over ranks (primary); weak: 4096 per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ecg", action="store_true", help="skip the ECG dopri5 (configs[2]) line")
     ap.add_argument("--no-mnist", action="store_true", help="skip the MNIST Kuramoto + KANLinear line")
     ap.add_argument("--no-ett", action="store_true", help="skip the ETT KAN-FET latent-ODE forecaster line")
     ap.add_argument("--ett-batch", type=int, default=8192)
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-solves", type=int, default=3, help="CPU baseline: median over this many solves")
     ap.add_argument("--train-iters", type=int, default=20, help="0 skips the training-rate line")
     return ap.parse_args()
 
 
-def make_problem(rank, dev):
+def make_problem(rank, world, scaling, dev):
+    """Seed-0 weights on every rank; y0: strong = this rank's block of the seed-0 global batch,
+    weak = a full batch of its own (seed = rank)."""
+    import fet_ode_amd.dist as D
     torch.manual_seed(0)
     model = F.KANFET([2, 10, 2], grid_size=5)
     sd = {k: v.clone() for k, v in model.state_dict().items()}
     model = model.to(dev)
-    g = torch.Generator().manual_seed(rank)
-    y0 = (0.5 + 2.5 * torch.rand(B, 2, generator=g)).to(torch.float32)
+    if scaling == "strong":
+        y0g = lv_y0(B, 0)
+        lo, hi = D.shard_bounds(B, rank, world)
+        y0 = y0g[lo:hi].clone()
+    else:
+        y0g = y0 = lv_y0(B, rank)
     t = torch.tensor(np.linspace(0, 3.5, T))
-    return model, sd, y0, t
+    return model, sd, y0, y0g, t
+
+
+def lv_y0(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    return (0.5 + 2.5 * torch.rand(n, 2, generator=g)).to(torch.float32)
 
 
 def kernel_time_ms(model, y0d, t, reps=20):
-    """Average duration of the fused integrate launch alone (HIP events on its stream)."""
+    """Average duration of the fused integrate launch alone (HIP events on its stream) for the
+    batch y0d."""
     dev = y0d.device
+    Bl = y0d.shape[0]
     lib = _lib.load()
     sched = get_schedule(t.to(torch.float64) if t.dtype == torch.float64 else t, None, False)
-    handle = make_handle(model, B, dev)
+    handle = make_handle(model, Bl, dev)
     plan = build_plan(model, handle, dev)
-    state, mask = pack_state(model, B, dev)
+    state, mask = pack_state(model, Bl, dev)
     _, coef, ostep, omode, oslope = sched.device_arrays(dev)
-    sol = torch.empty(sched.T, B, 2, device=dev)
+    sol = torch.empty(sched.T, Bl, 2, device=dev)
     stream = torch.cuda.current_stream(dev)
     h = stream.cuda_stream
 
     def launch():
-        _lib.check(lib.fetode_integrate_fixed(handle.ref, plan.data_ptr(), _lib.RK4, y0d.data_ptr(), B,
+        _lib.check(lib.fetode_integrate_fixed(handle.ref, plan.data_ptr(), _lib.RK4, y0d.data_ptr(), Bl,
                                               coef.data_ptr(), sched.n_steps, ostep.data_ptr(),
                                               omode.data_ptr(), oslope.data_ptr(), sched.T, sol.data_ptr(),
                                               state.data_ptr(), mask, None, h), "integrate")
@@ -103,6 +122,23 @@ def kernel_time_ms(model, y0d, t, reps=20):
     return float(np.mean([ev[2 * r].elapsed_time(ev[2 * r + 1]) for r in range(reps)]))
 
 
+def solve_ms(model, y0d, t, reps=30):
+    """Host wall time of one whole odeint call (what a caller sees), median of `reps`."""
+    func = F.autonomous(model)
+    dev = y0d.device
+    with torch.no_grad():
+        for _ in range(3):
+            F.odeint(func, y0d, t, method="rk4")
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            F.odeint(func, y0d, t, method="rk4")
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)) * 1e3
+
+
 def pmc_traffic_per_launch():
     """HBM bytes per fused launch from the newest committed rocprofv3 PMC summary, corrected as
     MI355X_MICROARCH.md §HBM prescribes (FETCH_SIZE x2 on gfx950; WRITE_SIZE as is; KiB units)."""
@@ -113,7 +149,7 @@ def pmc_traffic_per_launch():
     return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], REPO)
 
 
-def train_rate(model, y0d, t, iters, warmup, world):
+def train_rate(model, y0d, t, iters, warmup, world, strong=True):
     """One training iteration = forward rk4 solve with autograd (one launch that also records the
     layer inputs of every evaluation) + backward (one reverse-sweep launch + fixed-order gradient
     reduction) + gradient all-reduce (RCCL when world > 1) + Adam.  Adam runs as
@@ -151,20 +187,23 @@ def train_rate(model, y0d, t, iters, warmup, world):
         tt = torch.tensor([el], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         el = tt.item()
-    return {"value": world * iters * STEPS_PER_SOLVE / el, "unit": "RK4 steps/s trained (fwd+bwd+allreduce+Adam)",
+    return {"value": (1 if strong else world) * iters * STEPS_PER_SOLVE / el,
+            "unit": "RK4 steps/s trained (fwd+bwd+allreduce+Adam) of the batch-4096 job",
             "ms_per_iter": el / iters * 1e3, "iters": iters,
             "path": "fused: fetode_integrate_fixed with tape + fetode_integrate_fixed_backward (one launch each)"}
 
 
-def ecg_rate(dev, reps=10, cpu_seconds=5.0, with_cpu=True):
+def ecg_rate(dev, reps=10, cpu_seconds=5.0, with_cpu=True, rtol=1e-3, atol=1e-4):
     """BASELINE configs[2] (train_ecg_kan_fet_nn_ode.py:512-572): KanFet_NODE.eval() forward on a
     batch of 200 synthetic ECG200-shaped series (T = 96; the dataset is not in the image), latent
-    64, 10 bases, dopri5 rtol 1e-3 / atol 1e-4 on [0, 1].  Under no_grad the whole dopri5 solve is
-    one device-resident launch (fetode_ecg_dopri5); the encoder / classifier are one launch each."""
+    64, 10 bases, dopri5 on [0, 1] at the class defaults rtol 1e-3 / atol 1e-4 (:512-530) or, for
+    the `rtol_1e-2` leg, the __main__'s rtol 1e-2 / atol 1e-3 (:1196-1197).  Under no_grad the whole
+    dopri5 solve is one device-resident launch (fetode_ecg_dopri5); the encoder / classifier are one
+    launch each."""
     from fet_ode_amd import ecg
     from oracle import ecg_ref as E
     torch.manual_seed(0)
-    m = ecg.KanFet_NODE(T=96, num_classes=2, latent_dim=64, num_basis=10, rtol=1e-3, atol=1e-4)
+    m = ecg.KanFet_NODE(T=96, num_classes=2, latent_dim=64, num_basis=10, rtol=rtol, atol=atol)
     sd = {k: v.clone() for k, v in m.state_dict().items()}
     m = m.to(dev).eval()
     x = E.ecg_x(200, seed=1)
@@ -181,15 +220,15 @@ def ecg_rate(dev, reps=10, cpu_seconds=5.0, with_cpu=True):
     s = m.last_solve
     out = {"value": 1.0 / el, "unit": "KanFet_NODE forward solves/s (B=200, dopri5)", "ms_per_solve": el * 1e3,
            "nfev": s.nfev, "attempts": len(s.attempts), "field_evals_per_s": s.nfev / el,
-           "workload": "KanFet_NODE(T=96, 2 classes, latent 64, nb 10), dopri5 rtol 1e-3 atol 1e-4, t=[0,1], "
-                       "B=200 synthetic series, eval mode"}
+           "workload": f"KanFet_NODE(T=96, 2 classes, latent 64, nb 10), dopri5 rtol {rtol:g} atol {atol:g}, "
+                       "t=[0,1], B=200 synthetic series, eval mode"}
     if with_cpu:
-        cores = min(16, os.cpu_count() or 1)
+        cores, _ = cpu_cores()
         torch.set_num_threads(cores)
         n, t0 = 0, time.perf_counter()
         with torch.no_grad():
             while n < 1 or (time.perf_counter() - t0 < cpu_seconds and n < 20):
-                E.ECGNodeRef({k: v.clone() for k, v in sd.items()}, rtol=1e-3, atol=1e-4)(x)
+                E.ECGNodeRef({k: v.clone() for k, v in sd.items()}, rtol=rtol, atol=atol)(x)
                 n += 1
         cel = (time.perf_counter() - t0) / n
         out["cpu_baseline"] = {"value": 1.0 / cel, "unit": out["unit"], "cores": cores, "kind": "port",
@@ -236,7 +275,7 @@ def mnist_rate(dev, batch=8192, reps=10, cpu_seconds=5.0, with_cpu=True):
            "workload": f"KuramotoKANClassifier(28x28, 10 Kuramoto steps, KANLinear 1568->10, nb 8), batch {batch}, "
                        "synthetic images"}
     if with_cpu:
-        cores = min(16, os.cpu_count() or 1)
+        cores, _ = cpu_cores()
         torch.set_num_threads(cores)
         ref = M.ClassifierRef(sd)
         xs = x[:256]
@@ -284,7 +323,7 @@ def ett_rate(dev, batch=8192, reps=2, substeps=4, cpu_seconds=5.0, with_cpu=True
            "workload": f"LatentNeuralODEForecaster(7 features, 96->96, latent 64, KANFET[64,128,64] K=10), "
                        f"odeint_rk4 x{substeps} substeps ({steps} steps), batch {batch}, synthetic series"}
     if with_cpu:
-        cores = min(16, os.cpu_count() or 1)
+        cores, _ = cpu_cores()
         torch.set_num_threads(cores)
         field = O.KANFETRef.from_state_dict({k[len("dynamics.net."):]: v for k, v in sd.items()
                                              if k.startswith("dynamics.net.")}, 2)
@@ -304,53 +343,96 @@ def ett_rate(dev, batch=8192, reps=2, substeps=4, cpu_seconds=5.0, with_cpu=True
     return out
 
 
-def cpu_baseline(sd, y0, t, seconds):
-    """The CPU oracle (restatement of the reference, reference op order) on this host's cores."""
-    from oracle import torch_ref as O
-    cores = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(cores)
-    ref = O.KANFETRef.from_state_dict(sd, 2)
-    f = lambda tt, yy: ref(yy)
-    with torch.no_grad():
-        O.odeint(f, y0, t[:2], method="rk4")           # warm-up (1 step)
-        ref = O.KANFETRef.from_state_dict(sd, 2)        # fresh state for the timed solve
-        f = lambda tt, yy: ref(yy)
+def cpu_cores():
+    """(threads used, physical cores of this host from lscpu).  The threads are the physical cores,
+    capped at the process's CPU share (OMP_NUM_THREADS; 16 per GPU on the GPU box)."""
+    phys = None
+    try:
+        import subprocess
+        out = subprocess.run(["lscpu", "-p=core,socket"], capture_output=True, text=True, timeout=10).stdout
+        phys = len({ln for ln in out.splitlines() if ln and not ln.startswith("#")})
+    except Exception:
+        pass
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16
+    return max(1, min(phys or share, share)), phys
+
+
+def _median_solves(fn, n):
+    ts = []
+    for _ in range(n):
         t0 = time.perf_counter()
-        sol = O.odeint(f, y0, t, method="rk4")          # one full 34-step solve of the batch
-        el = time.perf_counter() - t0
-        n_solves = 1
-        while time.perf_counter() - t0 < seconds and n_solves < 20:
-            ref2 = O.KANFETRef.from_state_dict(sd, 2)
-            O.odeint(lambda tt, yy: ref2(yy), y0, t, method="rk4")
-            n_solves += 1
-        el = time.perf_counter() - t0
-    return {"value": n_solves * STEPS_PER_SOLVE / el, "unit": "RK4 steps/s (batch 4096)", "cores": cores,
-            "kind": "port",
-            "sample": f"{n_solves} full solve(s) of the bench workload (B=4096, 34 rk4 steps) with "
-                      f"oracle/torch_ref.py (reference op order, torch CPU fp32), {el:.1f} s"}, sol
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), ts
 
 
-def cpu_train_baseline(sd, y0, t, seconds, sample_b=512):
-    """The CPU oracle's training iteration (fwd with autograd + bwd) on a bounded sample of the
-    bench workload: the first `sample_b` trajectories, rate scaled to batch-4096 steps (the CPU
-    cost is linear in the batch at these sizes).  The Adam update (3 052 parameters) is left out."""
+def cpu_baseline(sd, y0, t, n_solves):
+    """The CPU oracle (restatement of the reference, reference op order, verified bitwise against
+    the reference modules) on this host: the full bench workload (B = 4096, 34 rk4 steps), median
+    of `n_solves` fresh-state solves on the physical cores, plus one solve on 1 thread."""
     from oracle import torch_ref as O
-    cores = min(16, os.cpu_count() or 1)
+    cores, phys = cpu_cores()
+    sol = None
+
+    def solve():
+        nonlocal sol
+        ref = O.KANFETRef.from_state_dict(sd, 2)
+        sol = O.odeint(lambda tt, yy: ref(yy), y0, t, method="rk4")
+
+    with torch.no_grad():
+        torch.set_num_threads(cores)
+        O.odeint(lambda tt, yy: O.KANFETRef.from_state_dict(sd, 2)(yy), y0[:64], t[:2], method="rk4")  # warm-up
+        med, ts = _median_solves(solve, n_solves)
+        first = sol
+        torch.set_num_threads(1)
+        med1, ts1 = _median_solves(solve, 1)
+        torch.set_num_threads(cores)
+    return {"value": STEPS_PER_SOLVE / med, "unit": "RK4 steps/s (batch 4096)", "cores": cores,
+            "physical_cores": phys, "kind": "port",
+            "sample": f"median of {n_solves} full solves of the bench workload (B=4096, 34 rk4 steps) with "
+                      f"oracle/torch_ref.py (reference op order, torch CPU fp32) on {cores} threads: "
+                      + ", ".join(f"{x:.2f}" for x in ts) + " s",
+            "one_thread": {"value": STEPS_PER_SOLVE / med1, "cores": 1,
+                           "sample": f"1 full solve of the bench workload on 1 thread: {ts1[0]:.2f} s"}}, first
+
+
+def cpu_train_baseline(sd, y0, t, n_iters):
+    """The CPU oracle's training iteration (forward with autograd + backward of an MSE over the
+    whole (35, 4096, 2) trajectory) on the FULL bench batch, median of `n_iters`.  The Adam update
+    (3 052 parameters) is left out."""
+    from oracle import torch_ref as O
+    cores, phys = cpu_cores()
     torch.set_num_threads(cores)
-    y0 = y0[:sample_b]
     target = torch.zeros(T, y0.shape[0], 2)
-    n, t0 = 0, time.perf_counter()
-    while n < 1 or (time.perf_counter() - t0 < seconds and n < 10):
+
+    def it():
         ps = {k: v.clone().requires_grad_(v.is_floating_point() and "grid" not in k) for k, v in sd.items()}
         ref = O.KANFETRef.from_state_dict(ps, 2)
         sol = O.odeint(lambda tt, yy: ref(yy), y0, t, method="rk4")
         (sol - target).square().mean().backward()
-        n += 1
-    el = time.perf_counter() - t0
-    return {"value": n * STEPS_PER_SOLVE / el * sample_b / B, "unit": "RK4 steps/s trained (fwd+bwd, batch 4096)",
-            "cores": cores, "kind": "port",
-            "sample": f"{n} fwd+bwd iteration(s) of {sample_b} of the 4096 bench trajectories (34 rk4 steps) with "
-                      f"oracle/torch_ref.py autograd (torch CPU fp32), {el:.1f} s; rate scaled by {sample_b}/{B}"}
+
+    med, ts = _median_solves(it, n_iters)
+    return {"value": STEPS_PER_SOLVE / med, "unit": "RK4 steps/s trained (fwd+bwd, batch 4096)",
+            "cores": cores, "physical_cores": phys, "kind": "port",
+            "sample": f"median of {n_iters} fwd+bwd iterations of the full bench batch (B=4096, 34 rk4 steps) "
+                      f"with oracle/torch_ref.py autograd (torch CPU fp32): " + ", ".join(f"{x:.2f}" for x in ts) + " s"}
+
+
+def well_conditioned_stats(gpu, e32, e64, tol_ref=1e-5, tol_gpu=2e-5):
+    """tests/test_gpu_parity.py well_conditioned_parity: the trajectories the reference's fp32 solve
+    keeps within 1e-5 of fp64, and how the GPU does on them."""
+    def te(a, b):
+        a, b = a.double(), b.double()
+        return ((a - b).norm(dim=2) / b.norm(dim=2).clamp_min(1e-30)).max(0).values
+    well = te(e32, e64) <= tol_ref
+    g_ref = te(gpu, e32)
+    return {"oracle_fp32_well_frac": float(well.double().mean()),
+            "gpu_well_frac": float((te(gpu, e64) <= tol_ref).double().mean()),
+            "n_well": int(well.sum()),
+            "max_gpu_vs_oracle_fp32_on_well": float(g_ref[well].max()) if bool(well.any()) else 0.0,
+            "all_within_2e-5": bool((g_ref[well] <= tol_gpu).all()),
+            "criterion": "per trajectory, max over time of ||y_t - ref_t|| / ||ref_t||; 'well' = the reference "
+                         "fp32 solve within 1e-5 of fp64 (tests/test_gpu_parity.py)"}
 
 
 def main():
@@ -364,8 +446,10 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
-    model, sd, y0, t = make_problem(rank, dev)
+    strong = args.scaling == "strong"
+    model, sd, y0, y0g, t = make_problem(rank, world, args.scaling, dev)
     y0d = y0.to(dev)
+    Bl = y0d.shape[0]
     func = F.autonomous(model)
 
     def solve():
@@ -390,24 +474,29 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             el = tt.item()
         k_ms = kernel_time_ms(model, y0d, t)
-    train = train_rate(model, y0d, t, args.train_iters, 2, world) if args.train_iters > 0 else None
+    train = train_rate(model, y0d, t, args.train_iters, 2, world, strong) if args.train_iters > 0 else None
     ms_per_step = el / args.steps * 1e3
-    value = world * args.steps * STEPS_PER_SOLVE / el
+    # strong: every solve covers the global batch once; weak: each rank's solve is a batch of its own
+    value = (1 if strong else world) * args.steps * STEPS_PER_SOLVE / el
 
     if rank == 0:
-        bytes_launch = alg_bytes_per_step(B) * STEPS_PER_SOLVE
+        bytes_launch = alg_bytes_per_step(Bl) * STEPS_PER_SOLVE
         achieved = bytes_launch / (k_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic_per_launch()
-        flops_launch = ALG_FLOPS_PER_TRAJ_STEP * B * STEPS_PER_SOLVE
+        traffic, traffic_src = pmc_traffic_per_launch() if Bl == B else (None, None)
+        flops_launch = ALG_FLOPS_PER_TRAJ_STEP * Bl * STEPS_PER_SOLVE
         tflops = flops_launch / (k_ms * 1e-3) / 1e12
         out = {
-            "metric": METRIC, "value": value, "unit": "RK4 steps/s (batch-4096 steps, summed over GPUs)",
+            "metric": METRIC, "value": value,
+            "unit": "RK4 steps/s of the batch-4096 job" + (" (global batch split over GPUs)" if strong
+                                                          else " (4096 per GPU, summed over GPUs)"),
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (seeded y0, torch.manual_seed(0) weights; no dataset)",
             "config": {"workload": "LV KAN-FET NODE: KANFET[2,10,2] G=5 k=3 nb=10 K=10, rk4 (3/8), "
-                                   "B=4096 per GPU, t=linspace(0,3.5,35) -> 34 steps per solve",
-                       "batch_per_gpu": B, "global_batch": B * world, "rk4_steps_per_solve": STEPS_PER_SOLVE,
+                                   + (f"global B=4096 split {world} ways" if strong else "B=4096 per GPU")
+                                   + ", t=linspace(0,3.5,35) -> 34 steps per solve",
+                       "batch_per_gpu": Bl, "global_batch": B if strong else B * world,
+                       "rk4_steps_per_solve": STEPS_PER_SOLVE,
                        "parallelism": f"trajectory-sharded x{world} (no collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -418,31 +507,48 @@ def main():
                                   "frac": tflops / FP32_PEAK_TFLOPS,
                                   "alg_flops_per_launch": flops_launch}},
         }
+        if world == 1:
+            # strong-scaling proxy on one GPU: the per-GPU block of an 8-GPU strong-scaled job
+            y512 = y0d[:B // 8].contiguous()
+            kb = kernel_time_ms(model, y512, t)
+            out["strong_proxy_ms_b512"] = kb
+            out["strong_proxy"] = {"kernel_ms_b4096": k_ms, "kernel_ms_b512": kb, "ratio_b512_over_b4096": kb / k_ms,
+                                   "solve_ms_b4096": solve_ms(model, y0d, t), "solve_ms_b512": solve_ms(model, y512, t),
+                                   "note": "B=512 = the per-GPU block of the 8-GPU strong-scaled job; kernel by HIP "
+                                           "events, solve = host wall of one odeint call (median)"}
         if train is not None:
             out["train"] = train
         if world == 1 and not args.no_ecg:
             out["ecg"] = ecg_rate(dev, with_cpu=not args.no_cpu_baseline)
+            out["ecg"]["rtol_1e-2"] = ecg_rate(dev, with_cpu=False, rtol=1e-2, atol=1e-3)
         if world == 1 and not args.no_mnist:
             out["mnist"] = mnist_rate(dev, with_cpu=not args.no_cpu_baseline)
         if world == 1 and not args.no_ett:
             out["ett"] = ett_rate(dev, batch=args.ett_batch, with_cpu=not args.no_cpu_baseline)
         if world == 1 and not args.no_cpu_baseline:
-            cb, ref_sol = cpu_baseline(sd, y0, t, args.cpu_seconds)
+            cb, ref_sol = cpu_baseline(sd, y0, t, args.cpu_solves)
             out["cpu_baseline"] = cb
             if train is not None:
-                out["train"]["cpu_baseline"] = cpu_train_baseline(sd, y0, t, args.cpu_seconds)
+                out["train"]["cpu_baseline"] = cpu_train_baseline(sd, y0, t, args.cpu_solves)
             fresh = F.KANFET([2, 10, 2], grid_size=5)
             fresh.load_state_dict(sd)          # fresh hysteresis state, as the CPU solve had
             with torch.no_grad():
                 sol = F.odeint(F.autonomous(fresh.to(dev)), y0d, t, method="rk4")
+                from oracle import torch_ref as O
+                r64 = O.KANFETRef.from_state_dict(sd, 2).to(torch.float64)
+                e64 = O.odeint(lambda tt, yy: r64(yy), y0.double(), t, method="rk4")
             g = sol.cpu().double()
             r = ref_sol.double()
             out["parity"] = {
                 "traj_mse_vs_cpu_ref": ((g - r) ** 2).mean().item(),
                 "max_slice_rel_vs_cpu_ref": ((g - r).reshape(T, -1).norm(dim=1)
                                              / r.reshape(T, -1).norm(dim=1)).max().item(),
-                "note": "KAN-FET is ill-conditioned in fp32 (the CPU reference's own fp32 vs fp64 "
-                        "per-slice error reaches ~6e-3 on this workload); see DESIGN.md §5",
+                "cpu_ref_fp32_vs_fp64_max_slice_rel": ((r - e64).reshape(T, -1).norm(dim=1)
+                                                       / e64.reshape(T, -1).norm(dim=1)).max().item(),
+                "well_conditioned": well_conditioned_stats(g, r, e64),
+                "note": "KAN-FET is ill-conditioned in fp32: the CPU reference's own fp32 solve departs from "
+                        "fp64 by the per-slice error above; the 1e-5 bar is checked on the trajectories fp32 "
+                        "can meet it on (well_conditioned; DESIGN.md §2)",
             }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -369,9 +369,12 @@ __device__ __forceinline__ float fast_sigmoid(float z) { return rcp(1.0f + ex2(-
 // visible after it.  Counters reset themselves; the words are zeroed once per launch.
 constexpr int kBarWords = 64 * 10;  // 8 XCD counters, top counter, generation (256 B each)
 // Every spin is bounded (MI355X_MICROARCH.md: a stranded workgroup must not hang the device): after
-// 2^20 polls (about a second) the barrier gives up and raises word 64*9+1, which the host reports.
+// 2^20 polls (about a second) the barrier gives up and raises the abort word 64*9+1.  Once that word
+// is set every barrier returns at once (entering or spinning) and reports it: the solver then stops
+// (status 4) instead of running on with counters that were never reset.
 constexpr unsigned kSpinLimit = 1u << 20;
-__device__ void grid_barrier(unsigned* bar, unsigned nblk) {
+__device__ bool grid_barrier(unsigned* bar, unsigned nblk) {
+  __shared__ int s_abort;
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned x = blockIdx.x & 7u;
@@ -379,26 +382,37 @@ __device__ void grid_barrier(unsigned* bar, unsigned nblk) {
     unsigned* cnt = bar + 64 * x;
     unsigned* top = bar + 64 * 8;
     unsigned* gen = bar + 64 * 9;
-    const unsigned g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nx - 1u) {
-      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nxcd - 1u) {
-        __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned* abort_word = gen + 1;
+    int ab = __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (!ab) {
+      const unsigned g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nx - 1u) {
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nxcd - 1u) {
+          __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
       }
-    }
-    unsigned spins = 0;
-    while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
-      __builtin_amdgcn_s_sleep(1);
-      if (++spins == kSpinLimit) {
-        __hip_atomic_store(gen + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
+      unsigned spins = 0;
+      while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+        __builtin_amdgcn_s_sleep(1);
+        if (__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          ab = 1;
+          break;
+        }
+        if (++spins == kSpinLimit) {
+          __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ab = 1;
+          break;
+        }
       }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    s_abort = ab;
   }
   __syncthreads();
+  return s_abort != 0;
 }
 
 // NT = 512 threads, R rows per workgroup (R-1 real + the shadow).  Solver thread (r, d) = tid for
@@ -470,7 +484,7 @@ __global__ __launch_bounds__(kResThreads) void ecg_dopri5_kernel(EcgDopriArgs a)
       __hip_atomic_store(&slot[0], w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&slot[1], w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    grid_barrier(a.bar, gridDim.x);
+    if (grid_barrier(a.bar, gridDim.x)) status = 4;  // aborted: every loop below checks status
     if (wv == 0) {  // one wave sums the slots: lane-strided then a fixed butterfly
       double u0 = 0.0, u1 = 0.0;
       for (int g = lane; g < (int)gridDim.x; g += 64) {
@@ -656,7 +670,7 @@ __global__ __launch_bounds__(kResThreads) void ecg_dopri5_kernel(EcgDopriArgs a)
     const float f1 = eval(y + f0 * h0);
     const float q2 = (f1 - f0) / scale;
     global_sum2(real ? (double)q2 * q2 : 0.0, 0.0, s, s1);
-    const float d2 = fabsf(sqrtf((float)(s / n_el)) / h0);
+    const float d2 = fabsf(sqrtf((float)(s / n_el)) / h0);  // (status 4: the loop below is skipped)
     float h1;
     if (d1 <= 1e-15f && d2 <= 1e-15f) h1 = fmaxf(1e-6f, h0 * 1e-3f);
     else h1 = powf(0.01f / fmaxf(d1, d2), 0.2f);
@@ -698,6 +712,7 @@ __global__ __launch_bounds__(kResThreads) void ecg_dopri5_kernel(EcgDopriArgs a)
       const float qe = err / tol;
       double s, nbad;
       global_sum2(real ? (double)qe * qe : 0.0, (real && !__builtin_isfinite(y)) ? 1.0 : 0.0, s, nbad);
+      if (status) break;
       if (nbad != 0.0) { status = 1; break; }
       const float ratio = sqrtf((float)(s / n_el));
       const bool accept = ratio <= 1.0f;

@@ -1,20 +1,13 @@
-// fetode_fused.hip — the single-launch fixed-grid integrator of a depth-2 KAN / KAN-FET field.
+// fetode_fused.hip — the single-launch fixed-grid integrator of the depth-2 LV KAN / KAN-FET field.
 //
 // One launch integrates the whole t-grid (torchdiffeq FixedGridODESolver.integrate): every RK
 // stage evaluation of the field, the hysteresis state updates in exact call order
 // (ferro_class.py:409), the stage combines (rk_common.rk4_alt_step_func op order) and the
 // output writes.  Nothing but y0, the parameters and the outputs touch HBM.
 //
-// Mapping.  A trajectory is owned by a group of LPT = 32 lanes (2 per wave).
-// Per field evaluation and per layer:
-//   phase A  per-input features into LDS: logistic basis (one (i,j) job per lane), and per input
-//            SiLU, the knot interval m and local coordinate u of x, the hysteresis gate
-//            w = -2(1-alpha)(1-sigmoid(gs*(x-prev))) and exp(gs*x); prev_x <- x.
-//   phase B  lane (o, c) owns a fixed slice of the layer's (input, basis) Ferro elements and of
-//            its feature weights, kept in VGPRs for the whole solve; the spline edge (o, i) is a
-//            cubic in u per knot interval, read as one float4 from the LDS table; partial sums
-//            are reduced over the C lanes of an output with cross-lane shuffles.
-// The stage combine runs on lanes d < D, in registers.
+// Kernel: fused4_kernel — one wave = two trajectories, packed-FP32 Ferro pairs,
+// branch-free feature streams.  (Earlier variants v1-v3 and the one-trajectory-per-wave v5 were
+// measured slower and removed from the library; they are in the git history before round 2.)
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -64,185 +57,6 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 
 namespace {
 
-template <int IN_, int OUT_, int K_, int NB_, int NG_, int LPT_>
-struct LS {
-  static constexpr int IN = IN_, OUT = OUT_, K = K_, NB = NB_, NG = NG_, LPT = LPT_;
-  static constexpr int NI = NG - 1;           // knot intervals
-  static constexpr int NFL = 1 + NB;          // LDS features per input: SiLU + logistic
-  static constexpr int C = LPT / OUT;         // lanes (chunks) per output
-  static constexpr int NP = IN * K;           // Ferro (input, basis) pairs
-  static constexpr int NQ = IN * NFL;         // feature weights per output
-  static constexpr int EPL = K > 0 ? (NP + C - 1) / C : 0;
-  static constexpr int FPL = (NQ + C - 1) / C;
-  static constexpr int SPL = (IN + C - 1) / C;
-  static constexpr int LJ = NB > 0 ? (IN * NB + LPT - 1) / LPT : 0;
-  static constexpr int SPT = OUT * IN * (NI + 1) * 4;  // spline table floats
-  static_assert(C >= 1, "out_features must be <= lanes per trajectory");
-};
-
-template <class S>
-struct Regs {  // per-lane register-resident slice of one layer
-  float ep[S::EPL > 0 ? S::EPL : 1];    // exp2(GEc) (factored gate) or GEc
-  float k2[S::EPL > 0 ? S::EPL : 1], k2Ec[S::EPL > 0 ? S::EPL : 1], CPs2[S::EPL > 0 ? S::EPL : 1];
-  float fw[S::FPL];
-  float lna[S::LJ > 0 ? S::LJ : 1], lab[S::LJ > 0 ? S::LJ : 1];
-  int o, c;
-  bool active;
-
-  __device__ void load(const float* __restrict__ plan, const LayerPlan& P, int lane, bool factored) {
-    o = lane / S::C;
-    c = lane % S::C;
-    active = lane < S::C * S::OUT;
-    const int oo = active ? o : 0;
-#pragma unroll
-    for (int r = 0; r < S::EPL; ++r) {
-      const int p = c + S::C * r;
-      const bool ok = active && p < S::NP;
-      const int64_t idx = (int64_t)oo * S::NP + (ok ? p : 0);
-      const float gec = ok ? plan[P.fe_GEc + idx] : 0.f;
-      ep[r] = factored ? ex2(gec) : gec;
-      k2[r] = ok ? plan[P.fe_k2 + idx] : 0.f;
-      k2Ec[r] = ok ? plan[P.fe_k2Ec + idx] : 0.f;
-      CPs2[r] = ok ? plan[P.fe_CPs2 + idx] : 0.f;
-    }
-#pragma unroll
-    for (int f = 0; f < S::FPL; ++f) {
-      const int q = c + S::C * f;
-      const bool ok = active && q < S::NQ;
-      fw[f] = ok ? plan[P.kw + (int64_t)oo * S::NQ + q] : 0.f;
-    }
-#pragma unroll
-    for (int r = 0; r < S::LJ; ++r) {
-      const int job = lane + S::LPT * r;
-      const bool ok = job < S::IN * S::NB;
-      lna[r] = ok ? plan[P.lg + 2 * job] : 0.f;
-      lab[r] = ok ? plan[P.lg + 2 * job + 1] : 0.f;
-    }
-  }
-};
-
-template <class S>
-struct TrajLayer {        // per-trajectory LDS scratch of one layer
-  float F[S::IN * S::NFL];  // SiLU, logistic features
-  float G[S::IN * 4];       // x, w (gate factor), exp(gs x), u (spline coordinate)
-  int M[S::IN];             // knot interval (NI = outside / non-finite -> zero table row)
-  float prev[S::IN];        // compact prev_x
-};
-
-template <class S>
-struct WgLayer {          // per-workgroup LDS copy of the shared tables of one layer
-  float knots[S::IN * S::NG];
-  float rh[S::IN * S::NI];
-  float cst[S::OUT];
-};
-
-// sum over the C consecutive lanes of an output; valid on lane c == 0 (and on all for pow2 C)
-template <int C>
-__device__ __forceinline__ float group_sum(float v) {
-  if constexpr ((C & (C - 1)) == 0) {
-#pragma unroll
-    for (int k = C / 2; k >= 1; k >>= 1) v += __shfl_xor(v, k);
-    return v;
-  } else {
-    float s = v;
-#pragma unroll
-    for (int d = 1; d < C; ++d) s += __shfl_down(v, d);
-    return s;
-  }
-}
-
-template <class S, bool FERRO>
-__device__ __forceinline__ void phase_A(const float* xin, TrajLayer<S>& L, const WgLayer<S>& W, const Regs<S>& R,
-                                        const LayerPlan& P, int lane, bool reinit) {
-  // logistic basis phi'_{ij} = 1/(1+exp(-a(x-b)))  (efficientkan.py:24; the 2 is in the weights)
-#pragma unroll
-  for (int r = 0; r < S::LJ; ++r) {
-    const int job = lane + S::LPT * r;
-    if (job < S::IN * S::NB) {
-      const int i = job / S::NB, j = job % S::NB;
-      L.F[i * S::NFL + 1 + j] = rcp(1.0f + ex2(ffma(R.lna[r], xin[i], R.lab[r])));
-    }
-  }
-  for (int i = lane; i < S::IN; i += S::LPT) {
-    const float x = xin[i];
-    L.F[i * S::NFL] = silu(x);
-    // knot interval: half-open [g_m, g_{m+1}) as the order-0 indicator (efficientkan.py:122)
-    const float* g = &W.knots[i * S::NG];
-    int m = -1;
-#pragma unroll
-    for (int j = 0; j < S::NG; ++j) m += (x >= g[j]) ? 1 : 0;
-    float u;
-    if (!__builtin_isfinite(x)) {
-      m = S::NI;
-      u = __builtin_nanf("");  // the reference's bases are NaN for +-inf / NaN inputs
-    } else if (m < 0 || m >= S::NI) {
-      m = S::NI;               // zero row of the table: all bases vanish outside the grid
-      u = 0.f;
-    } else {
-      u = (x - g[m]) * W.rh[i * S::NI + m];
-    }
-    L.M[i] = m;
-    L.G[4 * i + 3] = u;
-    if constexpr (FERRO) {
-      const float pv = reinit ? x : L.prev[i];
-      const float dx = x - pv;
-      // is_moving_up = sigmoid(gate_slope*dx) (ferro_class.py:387); w = -2(1-alpha)(1-u)
-      const float up = rcp(1.0f + ex2(-P.gsl2e * dx));
-      L.G[4 * i + 0] = x;
-      L.G[4 * i + 1] = P.wc * (1.0f - up);
-      L.G[4 * i + 2] = ex2(P.gsl2e * x);
-      L.prev[i] = x;  // ferro_class.py:409
-    }
-  }
-}
-
-// returns the output value on lanes with c == 0 (garbage elsewhere)
-template <class S, bool FERRO, bool FACT>
-__device__ __forceinline__ float phase_B(const TrajLayer<S>& L, const float* __restrict__ sp_lds,
-                                         const Regs<S>& R, float gsl2e) {
-  float acc = 0.f;
-  if (R.active) {
-    if constexpr (FERRO) {
-      // Ferro element (ferro_class.py:384-414) with branch_sign == 1 (never written, F8):
-      //   sl = (1-u) sigmoid(gs(-x-Ec)),  m = alpha + (1-alpha)(1-2 sl) = 1 + w s
-      //   coef (Ps tanh(k(x+Ec m)) + bias), tanh(z) = 1 - 2/(1+exp(2z)); sum coef*bias is folded
-      //   into the output constant.  The centred term coef*Ps*tanh keeps partial sums as small
-      //   as the reference's (a folded coef*(Ps+bias) constant costs ~10x more rounding).
-#pragma unroll
-      for (int r = 0; r < S::EPL; ++r) {
-        const int p = R.c + S::C * r;
-        if (p < S::NP) {
-          const int i = p / S::K;
-          const float x = L.G[4 * i], w = L.G[4 * i + 1];
-          float s;
-          if constexpr (FACT) s = rcp(1.0f + L.G[4 * i + 2] * R.ep[r]);
-          else s = rcp(1.0f + ex2(ffma(gsl2e, x, R.ep[r])));
-          const float m = ffma(w, s, 1.0f);
-          const float z = ffma(R.k2Ec[r], m, R.k2[r] * x);
-          const float th = ffma(-2.0f, rcp(1.0f + ex2(z)), 1.0f);
-          acc = ffma(R.CPs2[r], th, acc);
-        }
-      }
-    }
-#pragma unroll
-    for (int f = 0; f < S::FPL; ++f) {
-      const int q = R.c + S::C * f;
-      if (q < S::NQ) acc = ffma(R.fw[f], L.F[q], acc);
-    }
-#pragma unroll
-    for (int r = 0; r < S::SPL; ++r) {
-      const int i = R.c + S::C * r;
-      if (i < S::IN) {
-        const float u = L.G[4 * i + 3];
-        const float4 cf = *reinterpret_cast<const float4*>(
-            &sp_lds[((R.o * S::IN + i) * (S::NI + 1) + L.M[i]) * 4]);
-        acc += ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
-      }
-    }
-  }
-  return group_sum<S::C>(acc);
-}
-
 struct FusedArgs {
   const float* plan;
   LayerPlan P0, P1;
@@ -263,156 +77,7 @@ struct FusedArgs {
   float* eval_out;
 };
 
-template <int IN0, int H, int OUT, int K, int NB, int NG, bool FERRO, int LPT, int NT>
-__global__ __launch_bounds__(NT) void fused_integrate_kernel(FusedArgs a) {
-  using S0 = LS<IN0, H, FERRO ? K : 0, NB, NG, LPT>;
-  using S1 = LS<H, OUT, FERRO ? K : 0, NB, NG, LPT>;
-  constexpr int TPB = NT / LPT;  // trajectories per block
-  constexpr int D = IN0;
-  static_assert(IN0 == OUT, "ODE field must map R^D -> R^D");
-  static_assert(D <= LPT && H <= LPT, "dims exceed lanes per trajectory");
-
-  struct Traj {
-    float x0[IN0];
-    float h[H];
-    float kout[OUT];
-    TrajLayer<S0> L0;
-    TrajLayer<S1> L1;
-  };
-  __shared__ __attribute__((aligned(16))) float s_sp0[S0::SPT];
-  __shared__ __attribute__((aligned(16))) float s_sp1[S1::SPT];
-  __shared__ WgLayer<S0> s_w0;
-  __shared__ WgLayer<S1> s_w1;
-  __shared__ Traj s_traj[TPB];
-
-  const int tid = threadIdx.x;
-  const int g = tid / LPT, lane = tid % LPT;
-  const int64_t b = (int64_t)blockIdx.x * TPB + g;
-  const bool valid = b < a.B;
-  Traj& T = s_traj[g];
-
-  // stage the shared tables
-  for (int i = tid; i < S0::SPT; i += NT) s_sp0[i] = a.plan[a.P0.sp + i];
-  for (int i = tid; i < S1::SPT; i += NT) s_sp1[i] = a.plan[a.P1.sp + i];
-  for (int i = tid; i < IN0 * NG; i += NT) s_w0.knots[i] = a.plan[a.P0.knots + i];
-  for (int i = tid; i < H * NG; i += NT) s_w1.knots[i] = a.plan[a.P1.knots + i];
-  for (int i = tid; i < IN0 * S0::NI; i += NT) s_w0.rh[i] = a.plan[a.P0.rh + i];
-  for (int i = tid; i < H * S1::NI; i += NT) s_w1.rh[i] = a.plan[a.P1.rh + i];
-  for (int i = tid; i < H; i += NT) s_w0.cst[i] = a.plan[a.P0.fconst + i];
-  for (int i = tid; i < OUT; i += NT) s_w1.cst[i] = a.plan[a.P1.fconst + i];
-
-  // factored gate exp only where it is exact in fp32 (fetode_common.h kFactorLimit)
-  const bool fact = FERRO && a.plan[a.P0.flag] <= kFactorLimit && a.plan[a.P1.flag] <= kFactorLimit;
-  Regs<S0> R0;
-  Regs<S1> R1;
-  R0.load(a.plan, a.P0, lane, fact);
-  R1.load(a.plan, a.P1, lane, fact);
-
-  if (FERRO) {
-    for (int i = lane; i < IN0; i += LPT) T.L0.prev[i] = valid ? a.state[b * IN0 + i] : 0.f;
-    for (int i = lane; i < H; i += LPT) T.L1.prev[i] = valid ? a.state[a.B * IN0 + b * H + i] : 0.f;
-  }
-  bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
-
-  const int d = lane;
-  const bool own = d < D;
-  float y = (own && valid) ? a.y0[b * D + d] : 0.f;
-  if (!a.single_eval && own && valid) a.solution[b * D + d] = y;  // solution[0] = y0
-
-  auto eval_body = [&](float xin, auto fact_tag) __attribute__((always_inline)) -> float {
-    constexpr bool F_ = decltype(fact_tag)::value;
-    if (own) T.x0[d] = xin;
-    __syncthreads();
-    FETODE_MARK("A0");
-    phase_A<S0, FERRO>(T.x0, T.L0, s_w0, R0, a.P0, lane, re0);
-    re0 = false;
-    __syncthreads();
-    FETODE_MARK("B0");
-    const float v0 = phase_B<S0, FERRO, F_>(T.L0, s_sp0, R0, a.P0.gsl2e);
-    if (R0.active && R0.c == 0) T.h[R0.o] = v0 + s_w0.cst[R0.o];
-    __syncthreads();
-    FETODE_MARK("A1");
-    phase_A<S1, FERRO>(T.h, T.L1, s_w1, R1, a.P1, lane, re1);
-    re1 = false;
-    __syncthreads();
-    FETODE_MARK("B1");
-    const float v1 = phase_B<S1, FERRO, F_>(T.L1, s_sp1, R1, a.P1.gsl2e);
-    if (R1.active && R1.c == 0) T.kout[R1.o] = v1 + s_w1.cst[R1.o];
-    __syncthreads();
-    FETODE_MARK("END");
-    return own ? T.kout[d] : 0.f;
-  };
-  auto eval = [&](float xin) __attribute__((always_inline)) -> float {
-    if (fact) return eval_body(xin, std::integral_constant<bool, true>{});
-    return eval_body(xin, std::integral_constant<bool, false>{});
-  };
-
-  if (a.single_eval) {
-    const float f = eval(y);
-    if (own && valid) a.eval_out[b * OUT + d] = f;
-  } else {
-    const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4
-                   : a.method == FETODE_MIDPOINT ? 2 : 1;
-    const float third = 1.0f / 3.0f;
-    int jj = 1;
-    for (int s = 0; s < a.n_steps; ++s) {
-      const float dt = a.step_coef[4 * s + 0], hh = a.step_coef[4 * s + 1], h6 = a.step_coef[4 * s + 2];
-      float k1 = 0.f, k2 = 0.f, k3 = 0.f, k4 = 0.f;
-      for (int st = 0; st < ns; ++st) {
-        float xin = y;
-        if (a.method == FETODE_RK4) {
-          // rk_common.rk4_alt_step_func, exact op order (3/8 rule)
-          if (st == 1) xin = y + (dt * k1) * third;
-          else if (st == 2) xin = y + dt * (k2 - k1 * third);
-          else if (st == 3) xin = y + dt * ((k1 - k2) + k3);
-        } else if (a.method == FETODE_RK4_CLASSIC) {
-          // train_kan_fet_ett.py:72-75 / train_ecg_kan_fet_nn_ode.py:699-702
-          if (st == 1) xin = y + hh * k1;
-          else if (st == 2) xin = y + hh * k2;
-          else if (st == 3) xin = y + dt * k3;
-        } else if (a.method == FETODE_MIDPOINT) {
-          if (st == 1) xin = y + k1 * hh;  // fixed_grid.Midpoint: y0 + f0 * half_dt
-        }
-        const float kk = eval(xin);
-        if (st == 0) k1 = kk;
-        else if (st == 1) k2 = kk;
-        else if (st == 2) k3 = kk;
-        else k4 = kk;
-      }
-      float y1;
-      if (a.method == FETODE_RK4) y1 = y + (((k1 + 3.0f * (k2 + k3)) + k4) * dt) * 0.125f;
-      else if (a.method == FETODE_RK4_CLASSIC) y1 = y + h6 * (((k1 + 2.0f * k2) + 2.0f * k3) + k4);
-      else if (a.method == FETODE_MIDPOINT) y1 = y + dt * k2;
-      else y1 = y + dt * k1;
-      while (jj < a.T && a.out_step[jj] == s) {
-        const int mode = a.out_mode[jj];
-        const float v = mode == 0 ? y : (mode == 1 ? y1 : y + a.out_slope[jj] * (y1 - y));
-        if (own && valid) a.solution[((int64_t)jj * a.B + b) * D + d] = v;
-        ++jj;
-      }
-      y = y1;
-    }
-  }
-  if (FERRO && valid) {
-    for (int i = lane; i < IN0; i += LPT) a.state[b * IN0 + i] = T.L0.prev[i];
-    for (int i = lane; i < H; i += LPT) a.state[a.B * IN0 + b * H + i] = T.L1.prev[i];
-  }
-}
-
-
-// =============================================================================================
-// v3: merged phases, DPP reductions — D = 2 state, depth-2 field, hidden width H <= 10.
-//
-// One wave = 2 trajectories (32 lanes each = 2 rows of 16).  Per evaluation:
-//   (1) RK combine on every lane of row d (state dim d lives, replicated, in row d), then the
-//       layer-0 features of input d on row d: logistic (d, j) on lane c = j < NB, SiLU / knot
-//       interval / hysteresis gate on lane c = NB (its prev_x[d] lives in that lane's register);
-//   (2) sync; layer-0 edges: lane (o, c), o < H in groups of 3 lanes, 5 groups per row; each
-//       group reduces with DPP row shifts and ends with h_o on all 3 lanes, then computes the
-//       layer-1 features of input o (logistic j = c + 3r; SiLU / interval / gate on c = 0);
-//   (3) sync; layer-1 edges: lane (o = row, c) over the 16 lanes of the row; DPP row_ror
-//       reduction leaves k_o on every lane of row o — exactly where the combine needs it.
-// =============================================================================================
+// ---- cross-lane helpers (DPP) -------------------------------------------------------------
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF,
@@ -432,277 +97,6 @@ __device__ __forceinline__ float group3_sum(float v, int c) {
   const float b1 = dpp<0x111>(s0);                      // row_shr:1 -> lane 3k+1 gets s0[3k]
   const float b2 = dpp<0x112>(s0);                      // row_shr:2 -> lane 3k+2 gets s0[3k]
   return c == 0 ? s0 : (c == 1 ? b1 : b2);
-}
-
-template <int IN, int NFL>
-struct V3Lds {            // per-trajectory features of one layer's inputs
-  float F[IN * NFL];      // SiLU, logistic
-  float G[IN * 4];        // x, w, exp(gs x), u
-  int M[IN];              // knot interval (NI row = zero)
-};
-
-template <int NG, bool FERRO>
-__device__ __forceinline__ void v3_misc(float x, float& prev, bool reinit, const float* __restrict__ knots,
-                                        const float* __restrict__ rh, float gsl2e, float wc, float* F, float* G,
-                                        int* M) {
-  constexpr int NI = NG - 1;
-  F[0] = silu(x);
-  int m = -1;
-#pragma unroll
-  for (int j = 0; j < NG; ++j) m += (x >= knots[j]) ? 1 : 0;
-  float u;
-  if (!__builtin_isfinite(x)) {
-    m = NI;
-    u = __builtin_nanf("");
-  } else if (m < 0 || m >= NI) {
-    m = NI;
-    u = 0.f;
-  } else {
-    u = (x - knots[m]) * rh[m];
-  }
-  *M = m;
-  G[3] = u;
-  if constexpr (FERRO) {
-    const float pv = reinit ? x : prev;
-    const float up = rcp(1.0f + ex2(-gsl2e * (x - pv)));
-    G[0] = x;
-    G[1] = wc * (1.0f - up);
-    G[2] = ex2(gsl2e * x);
-    prev = x;  // ferro_class.py:409
-  }
-}
-
-template <int IN, int NFL, int NI, int K, int C, int EPL, int FPL, int SPL, bool FERRO, bool FACT>
-__device__ __forceinline__ float v3_edges(const V3Lds<IN, NFL>& L, const float* __restrict__ sp, int o, int c,
-                                          bool act, const float* ep, const float* k2, const float* k2Ec,
-                                          const float* cps, const float* fw, float gsl2e) {
-  float acc = 0.f;
-  if constexpr (FERRO) {
-#pragma unroll
-    for (int r = 0; r < EPL; ++r) {
-      const int p = c + C * r;
-      const int i = (p < IN * K ? p : 0) / K;   // padded elements carry zero weight
-      const float x = L.G[4 * i], w = L.G[4 * i + 1];
-      float s;
-      if constexpr (FACT) s = rcp(1.0f + L.G[4 * i + 2] * ep[r]);
-      else s = rcp(1.0f + ex2(ffma(gsl2e, x, ep[r])));
-      const float m = ffma(w, s, 1.0f);
-      const float z = ffma(k2Ec[r], m, k2[r] * x);
-      const float th = ffma(-2.0f, rcp(1.0f + ex2(z)), 1.0f);
-      acc = ffma(cps[r], th, acc);
-    }
-  }
-#pragma unroll
-  for (int f = 0; f < FPL; ++f) {
-    const int q = c + C * f;
-    acc = ffma(fw[f], L.F[q < IN * NFL ? q : 0], acc);
-  }
-#pragma unroll
-  for (int r = 0; r < SPL; ++r) {
-    const int i = c + C * r;
-    if (i < IN) {
-      const float u = L.G[4 * i + 3];
-      const float4 cf = *reinterpret_cast<const float4*>(&sp[((o * IN + i) * (NI + 1) + L.M[i]) * 4]);
-      acc += ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
-    }
-  }
-  return act ? acc : 0.f;
-}
-
-template <int H, int K_, int NB, int NG, bool FERRO>
-__global__ __launch_bounds__(64) void fused3_kernel(FusedArgs a) {
-  constexpr int D = 2, NI = NG - 1, NFL = 1 + NB, K = FERRO ? K_ : 0;
-  static_assert(H <= 10 && NB <= 15 && NB >= 1, "v3 layout: H <= 10 groups of 3, NB logistic lanes + 1");
-  // layer 0 (2 -> H): groups of C0 = 3 lanes
-  constexpr int C0 = 3, EPL0 = K > 0 ? (D * K + C0 - 1) / C0 : 0, FPL0 = (D * NFL + C0 - 1) / C0;
-  constexpr int SPL0 = (D + C0 - 1) / C0;
-  // layer 1 (H -> 2): the 16 lanes of a row
-  constexpr int C1 = 16, EPL1 = K > 0 ? (H * K + C1 - 1) / C1 : 0, FPL1 = (H * NFL + C1 - 1) / C1;
-  constexpr int SPL1 = (H + C1 - 1) / C1;
-  constexpr int LJ1 = (NB + C0 - 1) / C0;  // layer-1 logistic jobs per group lane
-  constexpr int SPT0 = H * D * (NI + 1) * 4, SPT1 = D * H * (NI + 1) * 4;
-
-  __shared__ __attribute__((aligned(16))) float s_sp0[SPT0];
-  __shared__ __attribute__((aligned(16))) float s_sp1[SPT1];
-  __shared__ float s_kn0[D * NG], s_rh0[D * NI], s_kn1[H * NG], s_rh1[H * NI], s_c0[H], s_c1[D];
-  __shared__ V3Lds<D, NFL> s_L0[2];
-  __shared__ V3Lds<H, NFL> s_L1[2];
-
-  const int tid = threadIdx.x;
-  const int g = tid >> 5, lane = tid & 31, row = lane >> 4, c1 = lane & 15;
-  const int64_t b = (int64_t)blockIdx.x * 2 + g;
-  const bool valid = b < a.B;
-  V3Lds<D, NFL>& L0 = s_L0[g];
-  V3Lds<H, NFL>& L1 = s_L1[g];
-
-  for (int i = tid; i < SPT0; i += 64) s_sp0[i] = a.plan[a.P0.sp + i];
-  for (int i = tid; i < SPT1; i += 64) s_sp1[i] = a.plan[a.P1.sp + i];
-  for (int i = tid; i < D * NG; i += 64) s_kn0[i] = a.plan[a.P0.knots + i];
-  for (int i = tid; i < H * NG; i += 64) s_kn1[i] = a.plan[a.P1.knots + i];
-  for (int i = tid; i < D * NI; i += 64) s_rh0[i] = a.plan[a.P0.rh + i];
-  for (int i = tid; i < H * NI; i += 64) s_rh1[i] = a.plan[a.P1.rh + i];
-  for (int i = tid; i < H; i += 64) s_c0[i] = a.plan[a.P0.fconst + i];
-  for (int i = tid; i < D; i += 64) s_c1[i] = a.plan[a.P1.fconst + i];
-
-  const bool fact = FERRO && a.plan[a.P0.flag] <= kFactorLimit && a.plan[a.P1.flag] <= kFactorLimit;
-
-  // ---- layer-0 edge lane (o0, cc0) ----
-  const int q = lane - 16 * row;
-  const int o0 = row * 5 + q / 3, cc0 = q % 3;
-  const bool act0 = q < 15 && o0 < H;
-  const int o0c = act0 ? o0 : 0;
-  float ep0[EPL0 > 0 ? EPL0 : 1], k20[EPL0 > 0 ? EPL0 : 1], kE0[EPL0 > 0 ? EPL0 : 1], cp0[EPL0 > 0 ? EPL0 : 1];
-  float fw0[FPL0];
-#pragma unroll
-  for (int r = 0; r < EPL0; ++r) {
-    const int p = cc0 + C0 * r;
-    const bool ok = act0 && p < D * K;
-    const int64_t idx = (int64_t)o0c * (D * K) + (ok ? p : 0);
-    const float gec = ok ? a.plan[a.P0.fe_GEc + idx] : 0.f;
-    ep0[r] = fact ? ex2(gec) : gec;
-    k20[r] = ok ? a.plan[a.P0.fe_k2 + idx] : 0.f;
-    kE0[r] = ok ? a.plan[a.P0.fe_k2Ec + idx] : 0.f;
-    cp0[r] = ok ? a.plan[a.P0.fe_CPs2 + idx] : 0.f;
-  }
-#pragma unroll
-  for (int f = 0; f < FPL0; ++f) {
-    const int qq = cc0 + C0 * f;
-    fw0[f] = (act0 && qq < D * NFL) ? a.plan[a.P0.kw + (int64_t)o0c * (D * NFL) + qq] : 0.f;
-  }
-  // ---- layer-1 edge lane (row, c1) ----
-  float ep1[EPL1 > 0 ? EPL1 : 1], k21[EPL1 > 0 ? EPL1 : 1], kE1[EPL1 > 0 ? EPL1 : 1], cp1[EPL1 > 0 ? EPL1 : 1];
-  float fw1[FPL1];
-#pragma unroll
-  for (int r = 0; r < EPL1; ++r) {
-    const int p = c1 + C1 * r;
-    const bool ok = p < H * K;
-    const int64_t idx = (int64_t)row * (H * K) + (ok ? p : 0);
-    const float gec = ok ? a.plan[a.P1.fe_GEc + idx] : 0.f;
-    ep1[r] = fact ? ex2(gec) : gec;
-    k21[r] = ok ? a.plan[a.P1.fe_k2 + idx] : 0.f;
-    kE1[r] = ok ? a.plan[a.P1.fe_k2Ec + idx] : 0.f;
-    cp1[r] = ok ? a.plan[a.P1.fe_CPs2 + idx] : 0.f;
-  }
-#pragma unroll
-  for (int f = 0; f < FPL1; ++f) {
-    const int qq = c1 + C1 * f;
-    fw1[f] = qq < H * NFL ? a.plan[a.P1.kw + (int64_t)row * (H * NFL) + qq] : 0.f;
-  }
-  // ---- feature jobs ----
-  // layer-0 features of input d = row: logistic j = c1 (< NB), misc on c1 == NB
-  const bool xlog = c1 < NB;
-  const float xna = xlog ? a.plan[a.P0.lg + 2 * (row * NB + c1)] : 0.f;
-  const float xab = xlog ? a.plan[a.P0.lg + 2 * (row * NB + c1) + 1] : 0.f;
-  const bool xmisc = c1 == NB;
-  // layer-1 features of input o0: logistic j = cc0 + 3r, misc on cc0 == 0
-  float hna[LJ1], hab[LJ1];
-#pragma unroll
-  for (int r = 0; r < LJ1; ++r) {
-    const int j = cc0 + C0 * r;
-    const bool ok = act0 && j < NB;
-    hna[r] = ok ? a.plan[a.P1.lg + 2 * (o0c * NB + j)] : 0.f;
-    hab[r] = ok ? a.plan[a.P1.lg + 2 * (o0c * NB + j) + 1] : 0.f;
-  }
-  const bool hmisc = act0 && cc0 == 0;
-
-  float prev0 = 0.f, prev1 = 0.f;  // prev_x of input `row` (xmisc lane) / of input o0 (hmisc lane)
-  if (FERRO && valid) {
-    if (xmisc) prev0 = a.state[b * D + row];
-    if (hmisc) prev1 = a.state[a.B * D + b * H + o0];
-  }
-  bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
-
-  float y = valid ? a.y0[b * D + row] : 0.f;   // state dim `row`, replicated over the row
-  if (!a.single_eval && valid && c1 == 0) a.solution[b * D + row] = y;
-  __syncthreads();  // tables staged
-
-  auto eval_body = [&](float xin, auto fact_tag) __attribute__((always_inline)) -> float {
-    constexpr bool F_ = decltype(fact_tag)::value;
-    FETODE_MARK("X_FEAT");
-    // (1) layer-0 features of input `row`
-    if (xlog) L0.F[row * NFL + 1 + c1] = rcp(1.0f + ex2(ffma(xna, xin, xab)));
-    if (xmisc)
-      v3_misc<NG, FERRO>(xin, prev0, re0, &s_kn0[row * NG], &s_rh0[row * NI], a.P0.gsl2e, a.P0.wc,
-                         &L0.F[row * NFL], &L0.G[4 * row], &L0.M[row]);
-    re0 = false;
-    __syncthreads();
-    FETODE_MARK("EDGES0");
-    // (2) layer-0 edges -> h_o on the group, then layer-1 features of input o
-    float h = v3_edges<D, NFL, NI, K, C0, EPL0, FPL0, SPL0, FERRO, F_>(L0, s_sp0, o0c, cc0, act0, ep0, k20, kE0,
-                                                                       cp0, fw0, a.P0.gsl2e);
-    h = group3_sum(h, cc0) + s_c0[o0c];
-    FETODE_MARK("H_FEAT");
-#pragma unroll
-    for (int r = 0; r < LJ1; ++r) {
-      const int j = cc0 + C0 * r;
-      if (act0 && j < NB) L1.F[o0 * NFL + 1 + j] = rcp(1.0f + ex2(ffma(hna[r], h, hab[r])));
-    }
-    if (hmisc)
-      v3_misc<NG, FERRO>(h, prev1, re1, &s_kn1[o0 * NG], &s_rh1[o0 * NI], a.P1.gsl2e, a.P1.wc, &L1.F[o0 * NFL],
-                         &L1.G[4 * o0], &L1.M[o0]);
-    re1 = false;
-    __syncthreads();
-    FETODE_MARK("EDGES1");
-    // (3) layer-1 edges -> k_row on every lane of the row
-    const float v = v3_edges<H, NFL, NI, K, C1, EPL1, FPL1, SPL1, FERRO, F_>(L1, s_sp1, row, c1, true, ep1, k21,
-                                                                             kE1, cp1, fw1, a.P1.gsl2e);
-    const float kr = row_sum16(v) + s_c1[row];
-    FETODE_MARK("END");
-    return kr;
-  };
-  auto eval = [&](float xin) __attribute__((always_inline)) -> float {
-    if (fact) return eval_body(xin, std::integral_constant<bool, true>{});
-    return eval_body(xin, std::integral_constant<bool, false>{});
-  };
-
-  if (a.single_eval) {
-    const float f = eval(y);
-    if (valid && c1 == 0) a.eval_out[b * D + row] = f;
-  } else {
-    const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4
-                   : a.method == FETODE_MIDPOINT ? 2 : 1;
-    const float third = 1.0f / 3.0f;
-    int jj = 1;
-    for (int s = 0; s < a.n_steps; ++s) {
-      const float dt = a.step_coef[4 * s + 0], hh = a.step_coef[4 * s + 1], h6 = a.step_coef[4 * s + 2];
-      float k1 = 0.f, k2 = 0.f, k3 = 0.f, k4 = 0.f;
-      for (int st = 0; st < ns; ++st) {
-        float xin = y;
-        if (a.method == FETODE_RK4) {
-          if (st == 1) xin = y + (dt * k1) * third;
-          else if (st == 2) xin = y + dt * (k2 - k1 * third);
-          else if (st == 3) xin = y + dt * ((k1 - k2) + k3);
-        } else if (a.method == FETODE_RK4_CLASSIC) {
-          if (st == 1) xin = y + hh * k1;
-          else if (st == 2) xin = y + hh * k2;
-          else if (st == 3) xin = y + dt * k3;
-        } else if (a.method == FETODE_MIDPOINT) {
-          if (st == 1) xin = y + k1 * hh;
-        }
-        const float kk = eval(xin);
-        if (st == 0) k1 = kk;
-        else if (st == 1) k2 = kk;
-        else if (st == 2) k3 = kk;
-        else k4 = kk;
-      }
-      float y1;
-      if (a.method == FETODE_RK4) y1 = y + (((k1 + 3.0f * (k2 + k3)) + k4) * dt) * 0.125f;
-      else if (a.method == FETODE_RK4_CLASSIC) y1 = y + h6 * (((k1 + 2.0f * k2) + 2.0f * k3) + k4);
-      else if (a.method == FETODE_MIDPOINT) y1 = y + dt * k2;
-      else y1 = y + dt * k1;
-      while (jj < a.T && a.out_step[jj] == s) {
-        const int mode = a.out_mode[jj];
-        const float vv = mode == 0 ? y : (mode == 1 ? y1 : y + a.out_slope[jj] * (y1 - y));
-        if (valid && c1 == 0) a.solution[((int64_t)jj * a.B + b) * D + row] = vv;
-        ++jj;
-      }
-      y = y1;
-    }
-  }
-  if (FERRO && valid) {
-    if (xmisc) a.state[b * D + row] = prev0;
-    if (hmisc) a.state[a.B * D + b * H + o0] = prev1;
-  }
 }
 
 // =============================================================================================
@@ -1250,527 +644,31 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
   STAMP_FLUSH();
 }
 
-// =============================================================================================
-// v5: one trajectory per wave — for batches that give v4 fewer than ~4 waves per SIMD.
-//
-// v4 is latency-bound at B = 4096 (2048 waves = 2 per SIMD: each wave stalls ~60% of an
-// evaluation on dependent LDS / DPP / transcendental chains).  v5 spreads one trajectory over
-// the 64 lanes, doubling the independent waves per SIMD and halving each wave's per-evaluation
-// instruction stream; a workgroup holds NW trajectories (one per wave) sharing the LDS tables,
-// and the waves never synchronise inside an evaluation (a wave's LDS traffic is in order).
-// Lane map, row = lane / 16:
-//   layer-0 features  input d on rows 2d, 2d+1 (row 2d writes), one job per lane as in v4;
-//   layer-0 edges     hidden output o on the quad 4o..4o+3 (quad_perm all-reduce);
-//   layer-1 features  input o on its quad, NJH jobs in rounds of 4;
-//   layer-1 edges     output d on rows 2d, 2d+1 (row_ror + permlane16_swap all-reduce), which
-//                     leaves k_d exactly where y_d lives for the stage combine.
-// =============================================================================================
-__device__ __forceinline__ float quad_sum(float v) {
-  v += dpp<0xB1>(v);  // quad_perm [1,0,3,2]
-  v += dpp<0x4E>(v);  // quad_perm [2,3,0,1]
-  return v;
-}
-// sum over the 32 lanes of rows {0,1} / {2,3}, result on every lane of the pair
-// (not v_permlane16_swap: this compiler reads its second result from the first result's
-// register, so r[0] + r[1] came out as 2*r[0].  ds_swizzle xor-16 goes through the LDS
-// crossbar without touching memory.)
-__device__ __forceinline__ float rowpair_sum(float v) {
-  v = row_sum16(v);
-  constexpr int kXor16 = (0x10 << 10) | 0x1F;  // bitmask mode: and 0x1F, or 0, xor 0x10
-  return v + __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), kXor16));
-}
-// order this wave's LDS writes before its later reads.  The LDS executes one wave's requests
-// in issue order, so only the compiler has to be stopped from moving memory operations across
-// (a wavefront-scope fence does not constrain non-atomic accesses; a memory clobber does).
-__device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_wave_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <int H, int K_, int NB, int NG, bool FERRO, bool HOT, int NW>
-#ifndef FETODE_V5_WAVES
-#define FETODE_V5_WAVES 3  // waves per SIMD the register budget is cut for (4 spills today)
-#endif
-__global__ __launch_bounds__(64 * NW, FETODE_V5_WAVES) void fused5_kernel(FusedArgs a) {
-  constexpr int D = 2, NI = NG - 1, NFL = 1 + NB, NFP = (NFL + 1) & ~1, K = FERRO ? K_ : 0;
-  constexpr int J_SILU = NB, J_GATE = NB + 1, J_EXP = NB + 2, J_X = FERRO ? NB + 3 : NB + 1;
-  constexpr int J_M = J_X + 1;
-  static_assert(J_M < 16 && NG <= 16, "v5 layout: feature jobs of one input on a row of 16 lanes");
-  static_assert(4 * H <= 64, "v5 layout: H <= 16 quads");
-  static_assert(!FERRO || K % 2 == 0, "v5 pairs Ferro elements (i, k), (i, k+1)");
-  constexpr int KP = K / 2 > 0 ? K / 2 : 1;
-  constexpr int NPL0 = FERRO ? (D * KP + 3) / 4 : 0, NPL1 = FERRO ? (H * KP + 31) / 32 : 0;
-  constexpr int FPL0 = ((D * NFP + 3) / 4 + 1) & ~1, FPL1 = ((H * NFP + 31) / 32 + 1) & ~1;
-  constexpr int FLEN0 = (4 * FPL0 > D * NFP ? 4 * FPL0 : D * NFP);
-  constexpr int FLEN1 = (32 * FPL1 > H * NFP ? 32 * FPL1 : H * NFP);
-  constexpr int NJH = FERRO ? NB + 3 : NB + 1;   // sigmoid-stream jobs per hidden input
-  constexpr int RH = (NJH + 3) / 4;               // rounds over the 4 lanes of a quad
-  constexpr int KT = (NG + 3) / 4;                // knots per quad lane: q, q+4, q+8, ...
-  constexpr int SPT0 = H * D * (NI + 1) * 4, SPT1 = D * H * (NI + 1) * 4;
-
-  __shared__ __attribute__((aligned(16))) float s_sp0[SPT0];
-  __shared__ __attribute__((aligned(16))) float s_sp1[SPT1];
-  __shared__ __attribute__((aligned(16))) V4Lds<D, FLEN0> s_L0[NW];
-  __shared__ __attribute__((aligned(16))) V4Lds<H, FLEN1> s_L1[NW];
-
-  const int tid = threadIdx.x;
-  const int w = tid >> 6, l = tid & 63, row = l >> 4, c = l & 15;
-  const int64_t b = (int64_t)blockIdx.x * NW + w;
-  const bool valid = b < a.B;
-  V4Lds<D, FLEN0>& L0 = s_L0[w];
-  V4Lds<H, FLEN1>& L1 = s_L1[w];
-
-  for (int i = tid; i < SPT0; i += 64 * NW) s_sp0[i] = a.plan[a.P0.sp + i];
-  for (int i = tid; i < SPT1; i += 64 * NW) s_sp1[i] = a.plan[a.P1.sp + i];
-  for (int i = l; i < FLEN0; i += 64) L0.F[i] = 0.f;  // pads stay zero (finite x zero weight)
-  for (int i = l; i < FLEN1; i += 64) L1.F[i] = 0.f;
-
-  const bool fact = FERRO && a.plan[a.P0.flag] <= kFactorLimit && a.plan[a.P1.flag] <= kFactorLimit;
-  const float l2 = FETODE_LOG2E;
-
-  // ---- layer-0 edge lane: hidden output o0 = quad, part q ----
-  const int o0 = l >> 2, q = l & 3;
-  const bool act0 = o0 < H;
-  const int o0c = act0 ? o0 : 0;
-  f2 ep0[NPL0 > 0 ? NPL0 : 1], k20[NPL0 > 0 ? NPL0 : 1], kE0[NPL0 > 0 ? NPL0 : 1], cp0[NPL0 > 0 ? NPL0 : 1];
-  int gi0[NPL0 > 0 ? NPL0 : 1];
-  // ---- layer-1 edge lane: output d1 = rows {2 d1, 2 d1 + 1}, part c32 ----
-  const int d1 = l >> 5, c32 = l & 31;
-  f2 ep1[NPL1 > 0 ? NPL1 : 1], k21[NPL1 > 0 ? NPL1 : 1], kE1[NPL1 > 0 ? NPL1 : 1], cp1[NPL1 > 0 ? NPL1 : 1];
-  int gi1[NPL1 > 0 ? NPL1 : 1];
-  auto load_pairs = [&](const LayerPlan& P, int IN, int o, int part, int npl, bool act, f2* ep, f2* k2, f2* kE, f2* cp,
-                        int* gi) __attribute__((always_inline)) {
-    for (int r = 0; r < npl; ++r) {
-      const int Pi = part * npl + r;
-      const bool ok = act && Pi < IN * KP;
-      int i = ok ? Pi / KP : 0;
-      float t[4][2];
-      for (int h = 0; h < 2; ++h) {
-        const int64_t idx = (int64_t)o * (IN * K) + i * K + (ok ? (Pi % KP) * 2 + h : 0);
-        const float gec = ok ? a.plan[P.fe_GEc + idx] : 0.f;
-        t[0][h] = fact ? ex2(gec) : gec;
-        t[1][h] = ok ? a.plan[P.fe_k2 + idx] : 0.f;
-        t[2][h] = ok ? a.plan[P.fe_k2Ec + idx] : 0.f;
-        t[3][h] = ok ? a.plan[P.fe_CPs2 + idx] : 0.f;
-      }
-      asm volatile("" : "+v"(i));  // keep in a VGPR (no per-evaluation rematerialisation)
-      gi[r] = i;
-      ep[r] = f2{t[0][0], t[0][1]};
-      k2[r] = f2{t[1][0], t[1][1]};
-      kE[r] = f2{t[2][0], t[2][1]};
-      cp[r] = f2{t[3][0], t[3][1]};
-    }
-  };
-  if constexpr (FERRO) {
-    load_pairs(a.P0, D, o0c, q, NPL0, act0, ep0, k20, kE0, cp0, gi0);
-    load_pairs(a.P1, H, d1, c32, NPL1, true, ep1, k21, kE1, cp1, gi1);
-  }
-  f2 fw0[FPL0 / 2], fw1[FPL1 / 2];
-#pragma unroll
-  for (int f = 0; f < FPL0; f += 2) {
-    float wv[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int qq = q * FPL0 + f + h, i = qq / NFP, ff = qq % NFP;
-      wv[h] = (act0 && i < D && ff < NFL) ? a.plan[a.P0.kw + (int64_t)o0c * (D * NFL) + i * NFL + ff] : 0.f;
-    }
-    fw0[f / 2] = f2{wv[0], wv[1]};
-  }
-#pragma unroll
-  for (int f = 0; f < FPL1; f += 2) {
-    float wv[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int qq = c32 * FPL1 + f + h, i = qq / NFP, ff = qq % NFP;
-      wv[h] = (i < H && ff < NFL) ? a.plan[a.P1.kw + (int64_t)d1 * (H * NFL) + i * NFL + ff] : 0.f;
-    }
-    fw1[f / 2] = f2{wv[0], wv[1]};
-  }
-
-  // ---- layer-0 feature stream: input dx = row / 2, job c (row 2 dx writes) ----
-  const int dx = row >> 1;
-  const bool xw = (row & 1) == 0;
-  float xna = 0.f, xab = 0.f, xmul = 1.f, xadd = 0.f;
-  float* xdst = &L0.sink;
-  if (xw) {
-    if (c < NB) {
-      xna = a.plan[a.P0.lg + 2 * (dx * NB + c)];
-      xab = a.plan[a.P0.lg + 2 * (dx * NB + c) + 1];
-      xdst = &L0.F[dx * NFP + 1 + c];
-    } else if (c == J_SILU) {
-      xdst = &L0.F[dx * NFP];
-    } else if (FERRO && c == J_GATE) {
-      xdst = &L0.G[dx].y;
-    } else if (FERRO && c == J_EXP) {
-      xdst = &L0.G[dx].z;
-    } else if (c == J_X) {
-      xdst = &L0.G[dx].x;
-    } else if (c == J_M) {
-      xdst = reinterpret_cast<float*>(&L0.M[dx]);
-    }
-  }
-  if (c == J_SILU) xna = -l2;
-  if (FERRO && c == J_GATE) {
-    xna = -a.P0.gsl2e;
-    xmul = -a.P0.wc;
-    xadd = a.P0.wc;
-  }
-  if (FERRO && c == J_EXP) xna = a.P0.gsl2e;
-  const bool x_silu = c == J_SILU, x_gate = FERRO && c == J_GATE, x_exp = FERRO && c == J_EXP;
-  const bool x_x = c == J_X, x_m = c == J_M;
-  const float xknot = c < NG ? a.plan[a.P0.knots + dx * NG + c] : __builtin_inff();
-  const float xrh = c < NI ? a.plan[a.P0.rh + dx * NI + c] : 0.f;
-
-  // ---- layer-1 feature stream: hidden input o0 on its quad, jobs q + 4r ----
-  float hna[RH], hab[RH], hmul[RH], hadd[RH];
-  float* hdst[RH];
-#pragma unroll
-  for (int r = 0; r < RH; ++r) {
-    const int j = q + 4 * r;
-    hna[r] = 0.f; hab[r] = 0.f; hmul[r] = 1.f; hadd[r] = 0.f;
-    hdst[r] = &L1.sink;
-    if (!act0) continue;
-    if (j < NB) {
-      hna[r] = a.plan[a.P1.lg + 2 * (o0 * NB + j)];
-      hab[r] = a.plan[a.P1.lg + 2 * (o0 * NB + j) + 1];
-      hdst[r] = &L1.F[o0 * NFP + 1 + j];
-    } else if (j == J_SILU) {
-      hna[r] = -l2;
-      hdst[r] = &L1.F[o0 * NFP];
-    } else if (FERRO && j == J_GATE) {
-      hna[r] = -a.P1.gsl2e; hmul[r] = -a.P1.wc; hadd[r] = a.P1.wc;
-      hdst[r] = &L1.G[o0].y;
-    } else if (FERRO && j == J_EXP) {
-      hna[r] = a.P1.gsl2e;
-      hdst[r] = &L1.G[o0].z;
-    }
-  }
-  float hknot[KT], hrh[KT];
-#pragma unroll
-  for (int t = 0; t < KT; ++t) {
-    const int kk = q + 4 * t;
-    hknot[t] = (act0 && kk < NG) ? a.plan[a.P1.knots + o0 * NG + kk] : __builtin_inff();
-    hrh[t] = (act0 && kk < NI) ? a.plan[a.P1.rh + o0 * NI + kk] : 0.f;
-  }
-  constexpr int RG = J_GATE / 4, RS = J_SILU / 4, RE = J_EXP / 4;
-  const bool h_silu = q == J_SILU % 4, h_gate = FERRO && q == J_GATE % 4, h_exp = FERRO && q == J_EXP % 4;
-
-  // hysteresis state (per-layer contiguous blocks, include/fetode.h): prev_x of input dx on the
-  // layer-0 gate lane of row 2 dx, of hidden input o0 on its quad's gate lane
-  const bool own0 = FERRO && xw && x_gate, own1 = FERRO && act0 && h_gate;
-  float prev0 = 0.f, prev1 = 0.f;
-  if (valid) {
-    if (own0) prev0 = a.state[b * D + dx];
-    if (own1) prev1 = a.state[a.B * D + b * H + o0];
-  }
-  bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
-
-  float y = valid ? a.y0[b * D + dx] : 0.f;  // state dim dx, replicated over rows 2dx, 2dx+1
-  const bool yw = valid && (l & 31) == 0;   // the lane that writes y_dx
-  if (!a.single_eval && yw) a.solution[b * D + dx] = y;
-  __syncthreads();  // tables staged
-  const float c0o = a.plan[a.P0.fconst + o0c], c1o = a.plan[a.P1.fconst + d1];
-
-  const float* sp0_o = &s_sp0[o0c * D * (NI + 1) * 4];
-  const float* sp1_o = &s_sp1[d1 * H * (NI + 1) * 4];
-  const int fofs0 = q * FPL0, fofs1 = c32 * FPL1;
-  const bool spl0 = act0 && q < D, spl1 = c32 < H;
-  const int si0 = spl0 ? q : 0, si1 = spl1 ? c32 : 0;
-
-  auto eval_body = [&](float xin, auto fact_tag) __attribute__((always_inline)) -> float {
-    constexpr bool F_ = decltype(fact_tag)::value;
-    FETODE_MARK("X_FEAT");
-    {
-      const float pv = x_gate ? (re0 ? xin : prev0) : 0.f;
-      const float e = ex2(ffma(xna, xin - pv, xab));
-      const float sg = rcp(1.0f + e);
-      float val = ffma(sg, x_silu ? xin : xmul, xadd);
-      val = x_exp ? e : val;
-      val = x_x ? xin : val;
-      int cnt = xin >= xknot ? 1 : 0;
-      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x128, 0xF, 0xF, false);
-      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x124, 0xF, 0xF, false);
-      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x122, 0xF, 0xF, false);
-      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x121, 0xF, 0xF, false);
-      const int mm = cnt - 1;
-      const bool fin = __builtin_isfinite(xin);
-      const int mfix = ((unsigned)mm < (unsigned)NI && fin) ? mm : NI;
-      val = x_m ? __builtin_bit_cast(float, mfix) : val;
-      *xdst = val;
-      if (xw && c == mfix) L0.G[dx].w = c < NI ? (xin - xknot) * xrh : (fin ? 0.0f : __builtin_nanf(""));
-      if (FERRO) prev0 = xin;  // ferro_class.py:409
-      re0 = false;
-    }
-    wave_lds_sync();
-    FETODE_MARK("EDGES0");
-    float h = v4_edges<D, FLEN0, NI, NPL0, FPL0, FERRO, F_>(L0, sp0_o, gi0, ep0, k20, kE0, cp0, fw0, fofs0, spl0, si0,
-                                                            a.P0.gsl2e);
-    h = quad_sum(act0 ? h : 0.f) + c0o;
-    FETODE_MARK("H_FEAT");
-    {
-      const float pv = h_gate ? (re1 ? h : prev1) : 0.f;
-#pragma unroll
-      for (int r = 0; r < RH; ++r) {
-        const float hx = (FERRO && r == RG) ? h - pv : h;
-        const float e = ex2(ffma(hna[r], hx, hab[r]));
-        const float sg = rcp(1.0f + e);
-        float val;
-        if (r == RS || (FERRO && (r == RG || r == RE))) {
-          val = ffma(sg, (r == RS && h_silu) ? h : hmul[r], hadd[r]);
-          if (FERRO && r == RE) val = h_exp ? e : val;
-        } else {
-          val = sg;
-        }
-        *hdst[r] = val;
-      }
-      if (FERRO) prev1 = h;
-      re1 = false;
-      float cntf = 0.f;
-#pragma unroll
-      for (int t = 0; t < KT; ++t) cntf += h >= hknot[t] ? 1.0f : 0.0f;
-      cntf = quad_sum(cntf);
-      const int mm = (int)cntf - 1;
-      const bool fin = __builtin_isfinite(h);
-      const int mfix = ((unsigned)mm < (unsigned)NI && fin) ? mm : NI;
-      const int tq = mfix >> 2;
-      // register select chain; the empty asm keeps it from becoming an indexed (scratch) load
-      float knm = hknot[0], rhm = hrh[0];
-      asm volatile("" : "+v"(knm), "+v"(rhm));
-#pragma unroll
-      for (int t = 1; t < KT; ++t) {
-        knm = tq == t ? hknot[t] : knm;
-        rhm = tq == t ? hrh[t] : rhm;
-        asm volatile("" : "+v"(knm), "+v"(rhm));
-      }
-      if (act0 && q == (mfix & 3)) L1.G[o0].w = mfix < NI ? (h - knm) * rhm : (fin ? 0.0f : __builtin_nanf(""));
-      if (act0 && q == 0) {
-        L1.G[o0].x = h;
-        L1.M[o0] = mfix;
-      }
-    }
-    wave_lds_sync();
-    FETODE_MARK("EDGES1");
-    const float v = v4_edges<H, FLEN1, NI, NPL1, FPL1, FERRO, F_>(L1, sp1_o, gi1, ep1, k21, kE1, cp1, fw1, fofs1, spl1,
-                                                                  si1, a.P1.gsl2e);
-    const float kr = rowpair_sum(v) + c1o;
-    FETODE_MARK("END");
-    wave_lds_sync();  // the next evaluation overwrites the feature blocks these reads used
-    return kr;
-  };
-
-  // the step / output schedule staged through LDS in chunks (shared by the NW waves)
-  constexpr int SCH = 32;
-  __shared__ float s_dt[SCH], s_hh[SCH], s_h6[SCH], s_oslope[SCH];
-  __shared__ int s_ostep[SCH], s_omode[SCH];
-  auto load_steps = [&](int s0) {
-    __syncthreads();
-    for (int i = tid; i < SCH && s0 + i < a.n_steps; i += 64 * NW) {
-      s_dt[i] = a.step_coef[4 * (s0 + i) + 0];
-      s_hh[i] = a.step_coef[4 * (s0 + i) + 1];
-      s_h6[i] = a.step_coef[4 * (s0 + i) + 2];
-    }
-    __syncthreads();
-  };
-  auto load_outs = [&](int j0) {
-    __syncthreads();
-    for (int i = tid; i < SCH; i += 64 * NW) {
-      const bool in = j0 + i < a.T;
-      s_ostep[i] = in ? a.out_step[j0 + i] : -1;
-      s_omode[i] = in ? a.out_mode[j0 + i] : 1;
-      s_oslope[i] = in ? a.out_slope[j0 + i] : 0.f;
-    }
-    __syncthreads();
-  };
-
-  auto out_write = [&](int j, float v) __attribute__((always_inline)) {
-    if (yw) a.solution[((int64_t)j * a.B + b) * D + dx] = v;
-  };
-  using FT = std::integral_constant<bool, true>;
-  using FF = std::integral_constant<bool, false>;
-
-  if constexpr (HOT) {
-    int sb = 0, jb = 1, jj = 1;
-    load_steps(0);
-    load_outs(1);
-    auto run = [&](auto fact_tag) __attribute__((always_inline)) {
-      const float third = 1.0f / 3.0f;
-      for (int s = 0; s < a.n_steps; ++s) {
-        if (s - sb == SCH) {
-          sb = s;
-          load_steps(s);
-        }
-        if (jj + 1 - jb >= SCH) {
-          jb = jj;
-          load_outs(jj);
-        }
-        const int sr = s - sb, jr = jj - jb;
-        const float dt = s_dt[sr];
-        const int os0 = s_ostep[jr], os1 = s_ostep[jr + 1], om0 = s_omode[jr];
-        const float osl0 = s_oslope[jr];
-        const float k1 = eval_body(y, fact_tag);
-        const float k2 = eval_body(y + (dt * k1) * third, fact_tag);
-        const float k3 = eval_body(y + dt * (k2 - k1 * third), fact_tag);
-        const float k4 = eval_body(y + dt * ((k1 - k2) + k3), fact_tag);
-        const float y1 = y + (((k1 + 3.0f * (k2 + k3)) + k4) * dt) * 0.125f;
-        if (os0 == s) {
-          int m0 = om0;
-          float sl0 = osl0;
-          asm volatile("" : "+v"(m0), "+v"(sl0));
-          out_write(jj, m0 == 0 ? y : (m0 == 1 ? y1 : y + sl0 * (y1 - y)));
-          ++jj;
-          if (os1 == s) {
-            while (jj < a.T) {
-              if (jj - jb == SCH) {
-                jb = jj;
-                load_outs(jj);
-              }
-              if (s_ostep[jj - jb] != s) break;
-              const int mode = s_omode[jj - jb];
-              out_write(jj, mode == 0 ? y : (mode == 1 ? y1 : y + s_oslope[jj - jb] * (y1 - y)));
-              ++jj;
-            }
-          }
-        }
-        y = y1;
-      }
-    };
-    if (fact) run(FT{});
-    else run(FF{});
-  } else {
-    auto eval = [&](float xin) __attribute__((always_inline)) -> float {
-      if (fact) return eval_body(xin, FT{});
-      return eval_body(xin, FF{});
-    };
-    if (a.single_eval) {
-      const float f = eval(y);
-      if (yw) a.eval_out[b * D + dx] = f;
-    } else {
-      const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4
-                     : a.method == FETODE_MIDPOINT ? 2 : 1;
-      const float third = 1.0f / 3.0f;
-      int sb = 0, jb = 1, jj = 1;
-      load_steps(0);
-      load_outs(1);
-      for (int s = 0; s < a.n_steps; ++s) {
-        if (s - sb == SCH) {
-          sb = s;
-          load_steps(s);
-        }
-        const float dt = s_dt[s - sb], hh = s_hh[s - sb], h6 = s_h6[s - sb];
-        float k1 = 0.f, k2 = 0.f, k3 = 0.f, k4 = 0.f;
-        for (int st = 0; st < ns; ++st) {
-          float xin = y;
-          if (a.method == FETODE_RK4) {
-            if (st == 1) xin = y + (dt * k1) * third;
-            else if (st == 2) xin = y + dt * (k2 - k1 * third);
-            else if (st == 3) xin = y + dt * ((k1 - k2) + k3);
-          } else if (a.method == FETODE_RK4_CLASSIC) {
-            if (st == 1) xin = y + hh * k1;
-            else if (st == 2) xin = y + hh * k2;
-            else if (st == 3) xin = y + dt * k3;
-          } else if (a.method == FETODE_MIDPOINT) {
-            if (st == 1) xin = y + k1 * hh;
-          }
-          const float kk = eval(xin);
-          if (st == 0) k1 = kk;
-          else if (st == 1) k2 = kk;
-          else if (st == 2) k3 = kk;
-          else k4 = kk;
-        }
-        float y1;
-        if (a.method == FETODE_RK4) y1 = y + (((k1 + 3.0f * (k2 + k3)) + k4) * dt) * 0.125f;
-        else if (a.method == FETODE_RK4_CLASSIC) y1 = y + h6 * (((k1 + 2.0f * k2) + 2.0f * k3) + k4);
-        else if (a.method == FETODE_MIDPOINT) y1 = y + dt * k2;
-        else y1 = y + dt * k1;
-        while (jj < a.T) {
-          if (jj - jb == SCH) {
-            jb = jj;
-            load_outs(jj);
-          }
-          if (s_ostep[jj - jb] != s) break;
-          const int mode = s_omode[jj - jb];
-          out_write(jj, mode == 0 ? y : (mode == 1 ? y1 : y + s_oslope[jj - jb] * (y1 - y)));
-          ++jj;
-        }
-        y = y1;
-      }
-    }
-  }
-  if (valid) {
-    if (own0) a.state[b * D + dx] = prev0;
-    if (own1) a.state[a.B * D + b * H + o0] = prev1;
-  }
-}
-
 typedef void (*fused_fn)(FusedArgs);
 struct FusedEntry {
   int in0, h, out, K, NB, NG;
   bool ferro;
-  fused_fn fn;
-  int nt, lpt;
-  fused_fn fn_rk4 = nullptr;  // specialised rk4 integrate kernel, if any
+  fused_fn fn;      // single evaluations and every fixed-grid method
+  fused_fn fn_rk4;  // the rk4 (3/8) integrate path, all four stages inlined
 };
-#define FUSED(IN0, H, OUT, K, NB, NG, FE, LPT, NT) \
-  {IN0, H, OUT, K, NB, NG, FE, fused_integrate_kernel<IN0, H, OUT, K, NB, NG, FE, LPT, NT>, NT, LPT}
 const FusedEntry kFused[] = {
-    // v4 (default): LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146) and LV KAN
-    {2, 10, 2, 10, 10, 12, true, fused4_kernel<10, 10, 10, 12, true, false>, 64, 4,
-     fused4_kernel<10, 10, 10, 12, true, true>},
-    {2, 10, 2, 1, 10, 12, false, fused4_kernel<10, 2, 10, 12, false, false>, 64, 4,
-     fused4_kernel<10, 2, 10, 12, false, true>},
-    // v5: one trajectory per wave (small batches; FETODE_FUSED_LPT=5 forces it)
-    {2, 10, 2, 10, 10, 12, true, fused5_kernel<10, 10, 10, 12, true, false, 2>, 128, 5,
-     fused5_kernel<10, 10, 10, 12, true, true, 2>},
-    {2, 10, 2, 1, 10, 12, false, fused5_kernel<10, 2, 10, 12, false, false, 2>, 128, 5,
-     fused5_kernel<10, 2, 10, 12, false, true, 2>},
-    // v3 (FETODE_FUSED_LPT=3)
-    {2, 10, 2, 10, 10, 12, true, fused3_kernel<10, 10, 10, 12, true>, 64, 3},
-    {2, 10, 2, 1, 10, 12, false, fused3_kernel<10, 1, 10, 12, false>, 64, 3},
-    // v2 (FETODE_FUSED_LPT=32|64, FETODE_FUSED_NT=64|256)
-    FUSED(2, 10, 2, 10, 10, 12, true, 32, 64),
-    FUSED(2, 10, 2, 10, 10, 12, true, 32, 256),
-    FUSED(2, 10, 2, 10, 10, 12, true, 64, 64),
-    FUSED(2, 10, 2, 10, 10, 12, true, 64, 256),
+    // LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146)
+    {2, 10, 2, 10, 10, 12, true, fused4_kernel<10, 10, 10, 12, true, false>, fused4_kernel<10, 10, 10, 12, true, true>},
     // LV KAN [2,10,2] (predator_prey.py:101)
-    FUSED(2, 10, 2, 1, 10, 12, false, 32, 64),
-    FUSED(2, 10, 2, 1, 10, 12, false, 32, 256),
-    FUSED(2, 10, 2, 1, 10, 12, false, 64, 64),
-    FUSED(2, 10, 2, 1, 10, 12, false, 64, 256),
+    {2, 10, 2, 1, 10, 12, false, fused4_kernel<10, 2, 10, 12, false, false>, fused4_kernel<10, 2, 10, 12, false, true>},
 };
 
-// Kernel variant.  Default: v4 at every batch — measured, v5 (one trajectory per wave) is not
-// faster even where it has twice the waves: a wave's evaluation is bound by its dependent
-// chain (~0.17 ms per 34-step solve for one wave alone, v4 and v5 alike), and v5 needs 146+
-// VGPRs (3 waves/SIMD).  kV5MaxBatch keeps the switch for when that changes.
-// FETODE_FUSED_LPT=5|4|3 forces v5 / v4 / v3, 32|64 a v2 variant (with FETODE_FUSED_NT=64|256
-// its workgroup size).
-constexpr int64_t kV5MaxBatch = 0;
-int env_int(const char* name, int dflt) {
-  const char* e = getenv(name);
-  return e ? atoi(e) : dflt;
-}
-int forced_lpt() {
-  static int v = env_int("FETODE_FUSED_LPT", 0);
-  return v;
-}
-int preferred_nt() {
-  static int nt = env_int("FETODE_FUSED_NT", 64);
-  return nt;
-}
-
-const FusedEntry* find_fused(const fetode_field_t* f, int64_t B) {
+const FusedEntry* find_fused(const fetode_field_t* f) {
   if (f->n_layers != 2) return nullptr;
   const fetode_kanlinear_t &k0 = f->kan[0], &k1 = f->kan[1];
   if (k0.grid_size != k1.grid_size || k0.spline_order != k1.spline_order ||
       k0.num_logistic != k1.num_logistic)
     return nullptr;
   const int NG = k0.grid_size + 2 * k0.spline_order + 1;
-  const int want = forced_lpt() ? forced_lpt() : (B <= kV5MaxBatch ? 5 : 4);
   for (const FusedEntry& e : kFused) {
     if (e.in0 != k0.in_features || e.h != k0.out_features || e.out != k1.out_features) continue;
     if (e.NB != k0.num_logistic || e.NG != NG) continue;
     if (e.ferro != (f->ferro != nullptr)) continue;
-    if (e.lpt != want || (e.lpt >= 32 && e.nt != preferred_nt())) continue;
     if (f->ferro) {
       if (f->ferro[0].num_basis != e.K || f->ferro[1].num_basis != e.K) continue;
       if (f->ferro[0].branch_sign || f->ferro[1].branch_sign) continue;  // general sign: generic path
@@ -1781,15 +679,13 @@ const FusedEntry* find_fused(const fetode_field_t* f, int64_t B) {
 }
 
 int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
-  const FusedEntry* e = find_fused(f, a.B);
+  const FusedEntry* e = find_fused(f);
   if (!e) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
   layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
   layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
-  // trajectories per workgroup: v3/v4 two per wave (one wave), v5 one per wave, v2 nt/lpt
-  if (a.tape && e->lpt != 4) return set_err(FETODE_EUNSUPPORTED, "training tape needs the v4 kernel");
-  const int tpb = e->lpt == 5 ? e->nt / 64 : (e->lpt <= 4 ? 2 : e->nt / e->lpt);
-  const fused_fn fn = (e->fn_rk4 && !a.single_eval && a.method == FETODE_RK4) ? e->fn_rk4 : e->fn;
-  hipLaunchKernelGGL(fn, dim3(nblk(a.B, tpb)), dim3(e->nt), 0, (hipStream_t)stream, a);
+  // two trajectories per one-wave workgroup
+  const fused_fn fn = (!a.single_eval && a.method == FETODE_RK4) ? e->fn_rk4 : e->fn;
+  hipLaunchKernelGGL(fn, dim3(nblk(a.B, 2)), dim3(64), 0, (hipStream_t)stream, a);
   LAUNCH_CHECK();
   return FETODE_OK;
 }
@@ -1806,7 +702,7 @@ int fetode_debug_stamp_buffer(void* p) {
 
 int fetode_fused_supported(const fetode_field_t* f) {
   if (validate_field(f) != FETODE_OK) return 0;
-  return find_fused(f, 1) != nullptr;
+  return find_fused(f) != nullptr;
 }
 
 int fetode_field_forward(const fetode_field_t* f, const void* plan, const float* x, int64_t B,

@@ -166,7 +166,8 @@ __global__ __launch_bounds__(256) void kanlinear_fwd_wave_kernel(fetode_kanlinea
 // tile in LDS ([i][row], conflict-free), and each wave stages P = e^{gs Ec} of its own output.
 // The two coercive sigmoids then need no exponential per basis element:
 //     sigma(gs (x - Ec)) = 1 / (1 + e^{-gs x} P),   sigma(gs (-x - Ec)) = 1 / (1 + e^{gs x} P)
-// (inputs with |gs x| > 80 take the direct form, so no 0 * inf can appear); tanh z =
+// (inputs with |gs x| > 80 or parameters with |gs Ec| > 80 take the direct form, so no 0 * inf and
+// no overflowed factor can appear); tanh z =
 // 1 - 2 / (1 + e^{2z}) with v_exp_f32 / v_rcp_f32.  The gate sigmoid(gs (x - prev_x)) keeps the
 // precise exp (it carries the fp32 conditioning of the hysteresis).  Two-level sum as the thread
 // kernel (K bases of one input, then inputs).
@@ -203,17 +204,23 @@ __global__ __launch_bounds__(256) void ferro_fwd_wide_kernel(fetode_ferro_t fl, 
       e1s[ii * 64 + r] = __expf(-gx);
       e2s[ii * 64 + r] = __expf(gx);
     }
+    bool big_ec = false;  // some |gs Ec| > 80 in this chunk of output o: P would over/underflow
     if (ovalid)
       for (int idx = lane; idx < ni * K; idx += 64) {
         const int ii = idx / K, k = idx - ii * K;
-        ps[w][idx] = __expf(gs * fl.Ec[((i0 + ii) * outd + o) * K + k]);
+        const float gec = gs * fl.Ec[((i0 + ii) * outd + o) * K + k];
+        big_ec |= fabsf(gec) > 80.0f;
+        ps[w][idx] = __expf(gec);
       }
+    big_ec = __any(big_ec);
     __syncthreads();
     if (!ovalid) continue;
     for (int ii = 0; ii < ni; ++ii) {
       const float xv = xs[ii * 64 + lane], up = ups[ii * 64 + lane];
       const float e1 = e1s[ii * 64 + lane], e2 = e2s[ii * 64 + lane];
-      const bool direct = __any(fabsf(gs * xv) > 80.0f);   // wave-uniform: no divergent paths
+      // the product form needs both factors finite and non-zero: |gs x| <= 80 and |gs Ec| <= 80
+      // (then a product that overflows / underflows only does so where the sigmoid is saturated)
+      const bool direct = big_ec || __any(fabsf(gs * xv) > 80.0f);   // wave-uniform: no divergent paths
       const float omu = 1.0f - up;
       const int e0 = ((i0 + ii) * outd + o) * K;
       const float* P = &ps[w][ii * K];

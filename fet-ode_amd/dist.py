@@ -10,8 +10,10 @@ on xGMI, so one fused bucket and no pipelining.
 
 Adaptive solves (dopri5) shard too, with one exchange: the error ratio torchdiffeq tests is the
 RMS over the WHOLE batch, so ``odeint_sharded`` all-reduces two fp64 words (sum of squares,
-non-finite flag) per norm — 6 per attempt-free step selection, 1 per attempt — and every rank
+non-finite flag) per norm — 3 in the initial step selection, 1 per attempt — and every rank
 takes the step sequence a single device would take on the global batch (SURVEY §8e caveat 2).
+Under autograd the backward all-reduces those norms' adjoints too (the gradient through the
+adaptive step sizes has cross-rank terms).
 
 Caveat kept from the reference semantics: a fresh FerroelectricBasis re-initialises prev_x
 (dx = 0) on its first call unless the batch is 1 (ferro_class.py:373-375).  Sharding a global
@@ -81,7 +83,13 @@ def allreduce_gradients(params: Iterable[torch.nn.Parameter], average: bool = Tr
     flat = torch._utils._flatten_dense_tensors(grads)
     if weights is not None:
         flat.mul_(weights)
-    dist.all_reduce(flat, op=dist.ReduceOp.SUM)
+    # RCCL ("nccl") reduces device buffers in place; gloo (CPU tests, several ranks on one GPU)
+    # reduces a host copy
+    host = flat.is_cuda and dist.get_backend() != "nccl"
+    buf = flat.cpu() if host else flat
+    dist.all_reduce(buf, op=dist.ReduceOp.SUM)
+    if host:
+        flat.copy_(buf)
     if weights is None and average:
         flat.div_(w)
     for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
@@ -91,7 +99,13 @@ def allreduce_gradients(params: Iterable[torch.nn.Parameter], average: bool = Tr
 def odeint_sharded(func, y0_local: torch.Tensor, t: torch.Tensor, *, rtol=1e-7, atol=1e-9, method=None,
                    options: Optional[dict] = None, group=None):
     """odeint over this rank's shard of a trajectory-sharded batch.  Fixed-grid methods need no
-    communication; adaptive ones use the global-batch error norm (all ranks, same steps)."""
+    communication; adaptive ones use the global-batch error norm (all ranks, same steps).
+
+    Training through dopri5: the norm's gradient is all-reduced in the backward
+    (dopri5._NormAllReduce), so rank r's parameter gradient holds its trajectories' share of
+    every cross-rank term.  Write the loss as this shard's share of the GLOBAL loss (e.g.
+    ``sum_local / N_global`` for a global mean) and sum with ``allreduce_gradients(average=False)``;
+    for equal shards a per-rank mean with ``weights=B_local / B`` is the same thing."""
     from .odeint import odeint
     opts = dict(options or {})
     _, w = world()

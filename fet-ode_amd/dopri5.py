@@ -339,6 +339,30 @@ def set_resident_dopri5(enabled: bool) -> bool:
     return prev
 
 
+class _NormAllReduce(torch.autograd.Function):
+    """Sum of a small fp64 vector over the ranks of a trajectory-sharded solve, differentiable:
+    forward all-reduces the values, backward all-reduces their adjoints.  The error ratio of every
+    attempt (and the initial-step norms) is a function of the WHOLE batch, so d loss / d theta
+    through the step-size control has cross-rank terms: rank r's loss depends on dt, dt on every
+    rank's sum of squares.  All-reducing the adjoint of the global sum hands every rank the full
+    d loss_total / d S, and rank r then backpropagates it into its own trajectories; summing the
+    parameter gradients over ranks (dist.allreduce_gradients) gives the single-device gradient.
+    Every rank runs the same attempts, so the backward collectives pair up in the same order."""
+
+    @staticmethod
+    def forward(ctx, v, group, cpu):
+        ctx.group, ctx.cpu = group, cpu
+        t = v.detach().cpu() if cpu else v.detach().clone()
+        torch.distributed.all_reduce(t, group=group)
+        return t.to(v.device)
+
+    @staticmethod
+    def backward(ctx, g):
+        t = g.detach().cpu() if ctx.cpu else g.detach().clone()
+        torch.distributed.all_reduce(t, group=ctx.group)
+        return t.to(g.device), None, None
+
+
 class _Dopri5Grad:
     """dopri5 with torchdiffeq's direct backpropagation (no adjoint): the solve is recorded by
     autograd through every stage of every attempt, the RMS error ratios and the adaptive step
@@ -348,10 +372,22 @@ class _Dopri5Grad:
     on the device, and t / dt are float64 device tensors like torchdiffeq's."""
 
     def __init__(self, func, y0, rtol, atol, options, reversed_):
-        unsupported = [k for k in ("step_t", "jump_t", "norm", "perturb", "norm_group") if options.get(k) is not None]
+        unsupported = [k for k in ("step_t", "jump_t", "norm", "perturb") if options.get(k) is not None]
         if unsupported:
             raise NotImplementedError(f"dopri5 options not supported with autograd: {unsupported}")
         self.func_user, self.sign, self.y0 = func, (-1.0 if reversed_ else 1.0), y0
+        # trajectory-sharded solve (dist.odeint_sharded): norms over the global batch, see
+        # _NormAllReduce for the gradient through them
+        group = options.get("norm_group")
+        self.distributed = group is not None
+        if self.distributed:
+            import torch.distributed as dist
+            self.group = None if group == "world" else group
+            self.cpu_reduce = dist.get_backend(self.group) != "nccl"
+            cnt = torch.tensor([float(y0.numel())], dtype=torch.float64,
+                               device="cpu" if self.cpu_reduce else y0.device)
+            dist.all_reduce(cnt, group=self.group)
+            self.n_global = float(cnt.item())
         self.dev, self.sdt = y0.device, y0.dtype
         f64 = dict(dtype=torch.float64, device=self.dev)
         self.rtol, self.atol = torch.as_tensor(rtol, **f64), torch.as_tensor(atol, **f64)
@@ -378,9 +414,19 @@ class _Dopri5Grad:
         _lib.require_gpu_tensor(out, "odeint func output")
         return -out if self.sign < 0 else out
 
-    @staticmethod
-    def rms(x):
-        return x.abs().pow(2).mean().sqrt()
+    def rms(self, x, finite_of=None):
+        """misc._rms_norm; sharded: RMS over the global batch.  With ``finite_of`` also returns
+        whether that tensor is finite on every rank (one collective for both)."""
+        if not self.distributed:
+            r = x.abs().pow(2).mean().sqrt()
+            return r if finite_of is None else (r, bool(torch.isfinite(finite_of).all()))
+        bad = torch.zeros((), dtype=torch.float64, device=x.device)
+        if finite_of is not None:
+            bad = (~torch.isfinite(finite_of)).any().to(torch.float64)
+        v = _NormAllReduce.apply(torch.stack([x.abs().pow(2).sum().to(torch.float64), bad]), self.group,
+                                 self.cpu_reduce)
+        r = (v[0] / self.n_global).sqrt().to(x.dtype)
+        return r if finite_of is None else (r, bool(v[1] == 0))
 
     def select_initial_step(self, t0, y0, f0):
         scale = self.atol + torch.abs(y0) * self.rtol
@@ -433,10 +479,13 @@ class _Dopri5Grad:
                 assert n_steps < self.max_num_steps, "max_num_steps exceeded"
                 t0 = t1s
                 assert t0 + dt > t0, "underflow in dt {}".format(dt.item())
-                assert torch.isfinite(y).all(), "non-finite values in state `y`"
+                if not self.distributed:
+                    assert torch.isfinite(y).all(), "non-finite values in state `y`"
                 y1, f1, err, k = self.step(y, f0, t0, dt)
                 tol = self.atol + self.rtol * torch.max(y.abs(), y1.abs())
-                ratio = self.rms(err / tol)
+                # sharded: the finiteness of y on every rank travels with this attempt's norm
+                ratio, finite = self.rms(err / tol, finite_of=y)
+                assert finite, "non-finite values in state `y`"
                 accept = bool(ratio <= 1)
                 self.attempts.append((float(t0.detach()), float(dt.detach()), float(ratio.detach()), accept))
                 if accept:

@@ -19,7 +19,9 @@ Same constructor arguments, parameter names / shapes / init RNG order, buffers (
 nb); branch_state, rebound to (B, in, nb) by every call like the reference) and error types.
 The mixer (+ Linear head) is one HIP launch per call (fetode_hlogistic_mixer_forward) with a HIP
 VJP; the encoder / classifier Linear layers are plain library GEMMs (torch).  There is no CPU
-path.  Not provided: use_noise=True (random), backprop through dopri5 (odeint raises).
+path.  Not provided: use_noise=True (random).  Backprop through dopri5 works like torchdiffeq's
+direct backprop (dopri5._Dopri5Grad: every stage, error ratio and step size, with the mixer's HIP
+VJP per evaluation); the device-resident solve serves inference only.
 """
 from __future__ import annotations
 

@@ -91,11 +91,15 @@ class KANFET_ODE_WithHead(nn.Module):
         return f
 
 
-def train_epoch(model: nn.Module, prob: LVProblem, optimizer, method: str = "rk4",
+def train_epoch(model: nn.Module, prob: LVProblem, optimizer, method: Optional[str] = None,
                 head: Optional[nn.Module] = None) -> torch.Tensor:
     """One epoch of train_kanfet_node_predprey.py:248-256 (``model`` = the KANFET field) or of
     train_kanfet_mlp_node_predprey.py:254-268 (``model`` = KANFET_ODE_WithHead): zero_grad, solve on
-    t_learn, MSE of pred[:, 0, :] against the 35-point truth, backward, Adam step.  Returns the loss."""
+    t_learn, MSE of pred[:, 0, :] against the 35-point truth, backward, Adam step.  Returns the loss.
+
+    ``method=None`` is what the reference runs: ``torchodeint(calDeriv, X0, t_learn)`` without a
+    method, i.e. dopri5 at rtol 1e-7 / atol 1e-9 (:252).  ``method="rk4"`` is BASELINE configs[1]'s
+    fixed-step choice (one fused launch + one reverse-sweep launch)."""
     optimizer.zero_grad()
     if isinstance(model, KANFET_ODE_WithHead):
         pred = model.head(odeint(model.rhs, prob.X0, prob.t_learn, method=method))
@@ -110,8 +114,9 @@ def train_epoch(model: nn.Module, prob: LVProblem, optimizer, method: str = "rk4
 
 
 @torch.no_grad()
-def test_loss(model: nn.Module, prob: LVProblem, method: str = "rk4") -> torch.Tensor:
-    """The test MSE of :259-261 / :271-275 on points n_train.. of the 140-point horizon."""
+def test_loss(model: nn.Module, prob: LVProblem, method: Optional[str] = None) -> torch.Tensor:
+    """The test MSE of :259-261 / :271-275 on points n_train.. of the 140-point horizon (default
+    method: dopri5, as the reference's :260)."""
     if isinstance(model, KANFET_ODE_WithHead):
         pred = model.head(odeint(model.rhs, prob.X0, prob.t, method=method))
     else:

@@ -1,0 +1,119 @@
+"""MI355X parity at the PRODUCTION widths of BASELINE configs[3] (train_kan_fet_ett.py:136-197 with
+the KAN-FET latent field KANFET([64, 128, 64], K = 10)): the kernels the ETT workload runs —
+wide KANLinear (every outputs-per-wave variant the launcher picks by batch size), the wide Ferro
+forward (K = 10 / 12 templated and a generic K) and the whole field — against oracle/torch_ref.py.
+
+Edge cases the product-form coercive sigmoids must survive (ferro_class.py:390-391): rows with
+|gate_slope * x| > 80 mixed into a batch of normal rows, and parameters with |gate_slope * Ec| > 80
+(e^{gs Ec} would overflow / underflow in fp32)."""
+import pytest
+import torch
+
+import fet_ode_amd as F
+from fet_ode_amd import ett
+from oracle import ett_ref as E
+from oracle import torch_ref as O
+
+pytestmark = pytest.mark.gpu
+
+
+def row_rel(got, exp):
+    """max over rows of ||got_b - exp_b|| / ||exp_b||."""
+    got, exp = got.double().cpu(), exp.double().cpu()
+    return ((got - exp).norm(dim=-1) / exp.norm(dim=-1).clamp_min(1e-30)).max().item()
+
+
+def _x(B, n, seed, wild_rows=()):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(B, n, generator=g) * 6 - 3          # in and out of the [-2.2, 2.2) knot grid
+    for r in wild_rows:                                  # |gs x| > 80 (gs = 10): the direct-form rows
+        x[r] = torch.sign(torch.randn(n, generator=g)) * (8.2 + torch.rand(n, generator=g) * 3)
+    return x
+
+
+@pytest.mark.parametrize("i,o", [(64, 128), (128, 64)])
+@pytest.mark.parametrize("B", [300, 4096, 8192, 16384])
+def test_wide_kanlinear_forward(dev, i, o, B):
+    """KANLinear at ETT widths; B sweeps the launcher's outputs-per-wave choice (1/2/4/8)."""
+    torch.manual_seed(i + o)
+    m = F.KANLinear(i, o)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    x = _x(B, i, seed=B)
+    with torch.no_grad():
+        got = m(x.to(dev))
+    exp = O.kanlinear_forward(x, O.KANLinearParams.from_state_dict(sd))
+    assert row_rel(got, exp) <= 1e-5, row_rel(got, exp)
+
+
+def _ferro_with_edges(i, o, K, seed):
+    torch.manual_seed(seed)
+    m = F.FerroelectricBasis(i, o, K)
+    with torch.no_grad():                        # a trained Ec can leave [0.5, 2.5]: |gs Ec| > 80 and < 0
+        m.Ec[0, :, 0] = 9.5
+        m.Ec[1, :, 1] = -9.0
+        m.Ec[2, 3, :] = -0.3
+    return m
+
+
+@pytest.mark.parametrize("i,o,K", [(64, 128, 10), (128, 64, 10), (64, 128, 12), (48, 40, 7)])
+def test_wide_ferro_forward_sequence(dev, i, o, K):
+    """Three stateful calls (first-call rule dx = 0, then dx = x - prev_x) of a B = 300 batch with
+    wild rows; each against the fp32 oracle (1e-5 per row) and the fp64 oracle (within 4x the fp32
+    oracle's own error + 1e-6)."""
+    m = _ferro_with_edges(i, o, K, seed=i * o + K)
+    p = O.FerroParams(*(getattr(m, n).detach().clone() for n in ("k", "Ec", "Ps", "bias", "coef")))
+    st32, st64 = O.FerroState(i, o, K), O.FerroState(i, o, K, torch.float64)
+    p64 = p.to(torch.float64)
+    m = m.to(dev)
+    B = 300
+    for call in range(3):
+        x = _x(B, i, seed=100 * call + i, wild_rows=(5, 77, 140, 299)) * (1.0 + 0.05 * call)
+        with torch.no_grad():
+            got = m(x.to(dev))
+        e32 = O.ferro_forward(x, p, st32)
+        e64 = O.ferro_forward(x.double(), p64, st64)
+        assert torch.isfinite(got).all()
+        assert row_rel(got, e32) <= 1e-5, (call, row_rel(got, e32))
+        err = row_rel(got, e64)
+        assert err <= 4 * row_rel(e32, e64) + 1e-6, (call, err, row_rel(e32, e64))
+        assert torch.equal(m.prev_x[:, :, 0, 0].cpu(), x)
+
+
+def test_wide_kanfet_field_calls(dev):
+    """KANFET([64, 128, 64], K = 10) — the ETT latent field — two stateful evaluations."""
+    torch.manual_seed(5)
+    m = F.KANFET([64, 128, 64], grid_size=5, num_fet_basis=10)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    ref = O.KANFETRef.from_state_dict(sd, 2)
+    for call in range(2):
+        x = _x(300, 64, seed=11 + call, wild_rows=(0, 150) if call else ())
+        with torch.no_grad():
+            got = m(x.to(dev))
+        assert row_rel(got, ref(x)) <= 1e-5, (call, row_rel(got, ref(x)))
+
+
+def test_ett_field_through_odeint_rk4_production_width(dev):
+    """The config-4 latent ODE itself: ett.KANFETDynamics(64, hidden=128, K=10) through odeint_rk4
+    (classic RK4 with substeps, train_kan_fet_ett.py:51-83) at B = 256 against the oracle, with the
+    reference's own fp32 error as the yardstick (KAN-FET hysteresis is ill-conditioned in fp32)."""
+    torch.manual_seed(9)
+    dyn = ett.KANFETDynamics(64, hidden=128, num_fet_basis=10)
+    sd = {k: v.clone() for k, v in dyn.net.state_dict().items()}
+    dyn = dyn.to(dev)
+    g = torch.Generator().manual_seed(10)
+    z0 = torch.randn(256, 64, generator=g) * 0.8
+    t = torch.linspace(0.0, 0.25, steps=2)
+    with torch.no_grad():
+        got = ett.odeint_rk4(dyn, z0.to(dev), t.to(dev), n_substeps=2).cpu()
+    r32 = O.KANFETRef.from_state_dict(sd, 2)
+    r64 = O.KANFETRef.from_state_dict({k: v.double() for k, v in sd.items()}, 2)
+    e32 = E.odeint_rk4(lambda tt, zz: r32(zz), z0, t, n_substeps=2)
+    e64 = E.odeint_rk4(lambda tt, zz: r64(zz), z0.double(), t.double(), n_substeps=2)
+    assert got.shape == (2, 256, 64) and torch.isfinite(got).all()
+    spread = row_rel(e32[1], e64[1])
+    err = row_rel(got[1], e64[1])
+    assert err <= 4 * spread + 1e-5, (err, spread)
+    # the hysteresis state after the solve is the last stage input of each layer (ferro_class.py:409)
+    assert dyn.net.layers[0].ferro.prev_x.shape == (256, 64, 128, 10)

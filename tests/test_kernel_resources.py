@@ -57,7 +57,7 @@ def kernel_metadata(path, tmp_path):
 def test_no_kernel_uses_scratch(tmp_path):
     ks = kernel_metadata(LIB, tmp_path)
     fused = [n for n in ks if "fused" in n]
-    assert len(fused) >= 8, sorted(ks)
+    assert len(fused) >= 4, sorted(ks)   # fused4 x {KAN, KAN-FET} x {generic, rk4}
     # SGPR spills without a private segment land in VGPR lanes (v_writelane / v_readlane), not in
     # memory; VGPR spills and any private segment are per-lane scratch traffic.
     bad = {n: v for n, v in ks.items()

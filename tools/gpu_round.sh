@@ -1,13 +1,19 @@
 #!/bin/bash
-# one GPU call: tests, smoke, quick bench; stops after any crash/timeout (status >1)
+# GPU call: gpu suite (no -x: see every failure), smoke, default bench (the contract line), then
+# the rocprofv3 kernel-trace stats of a short bench.  Every step has its own time limit; a step
+# that crashes / times out (rc > 1) ends the call.
 cd "$(dirname "$0")/.."
-mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -q -m gpu > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc" | tee -a gpurun_out/pytest_gpu.log
-if [ $rc -gt 1 ]; then exit $rc; fi
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
-rc2=$?; echo "smoke rc=$rc2" | tee -a gpurun_out/smoke.log
-if [ $rc2 -gt 1 ]; then exit $rc2; fi
-timeout -k 10 300 python tools/quick_bench.py > gpurun_out/quick_bench.log 2>&1
-echo "bench rc=$?" | tee -a gpurun_out/quick_bench.log
-tail -5 gpurun_out/pytest_gpu.log; cat gpurun_out/smoke.log gpurun_out/quick_bench.log
+R=${ROUND:-r02}
+O=gpurun_out; mkdir -p $O
+export TMPDIR=/tmp
+step() { local name=$1; shift; "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; [ $rc -le 1 ] || exit $rc; return 0; }
+step pytest_gpu timeout -k 10 ${PYTEST_LIMIT:-900} python -u -m pytest tests -q -m gpu ${PYTEST_ARGS:-} --timeout 240 --timeout-method thread
+tail -25 $O/pytest_gpu.log
+[ -n "$NO_BENCH" ] && exit 0
+step smoke timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()"
+tail -1 $O/smoke.log
+step bench timeout -k 10 600 python bench.py
+tail -1 $O/bench.log > $O/bench_$R.json
+cat $O/bench_$R.json
+[ -n "$NO_PROF" ] && exit 0
+step prof_stats timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$R -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --ett-batch 1024 --train-iters 5
