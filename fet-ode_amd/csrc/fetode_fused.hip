@@ -75,6 +75,7 @@ struct FusedArgs {
   float* tape;            // (n_evals, B, D+H) layer inputs of every evaluation (training), or null
   int32_t single_eval;  // 1: eval_out = field(y0) once (fetode_field_forward)
   float* eval_out;
+  float factor_limit;   // kFactorLimit (FETODE_FACTOR_LIMIT=-1 disables the factored gate: diagnostics)
 };
 
 // ---- cross-lane helpers (DPP) -------------------------------------------------------------
@@ -219,7 +220,7 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
   for (int i = lane; i < FLEN0; i += 32) L0.F[i] = 0.f;  // pads stay zero (finite x zero weight)
   for (int i = lane; i < FLEN1; i += 32) L1.F[i] = 0.f;
 
-  const bool fact = FERRO && a.plan[a.P0.flag] <= kFactorLimit && a.plan[a.P1.flag] <= kFactorLimit;
+  const bool fact = FERRO && a.plan[a.P0.flag] <= a.factor_limit && a.plan[a.P1.flag] <= a.factor_limit;
   const float l2 = FETODE_LOG2E;
 
   // ---- layer-0 edge lane: output o0 = 5 row + q/3, part cc0 ----
@@ -644,19 +645,409 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
   STAMP_FLUSH();
 }
 
+// =============================================================================================
+// v6: one trajectory per 3-wave workgroup — the small-batch (strong-scaling) kernel.
+//
+// At B = 512 (an 8-GPU strong-scaled shard of the 4096 batch) v4 has 256 waves for 1024 SIMDs
+// and every wave walks the whole evaluation chain of two trajectories (~0.17 ms per solve, lone
+// wave).  v6 spreads ONE trajectory over 192 lanes so each lane's share of an evaluation is one
+// short stream: row r (16 lanes) of the workgroup is layer-0 output r AND layer-1 input r
+// (r < H = 10), so layer 0 -> layer 1 needs no exchange at all:
+//   layer 0  the layer inputs x_0, x_1 are known to every lane; lane c takes the feature jobs
+//            c and c + 16 of one sigmoid-of-affine stream (logistic, SiLU, gates, exp(gs x)),
+//            the gates / exps reach the Ferro lanes by DPP row_newbcast, lanes c < 10 take one
+//            packed Ferro pair (i, k..k+1) of output r, the lane whose knot opens x_i's interval
+//            takes the spline edge; a DPP row sum leaves h_r on the 16 lanes of row r;
+//   layer 1  row r evaluates the 13 feature jobs of h_r (one per lane), 10 Ferro pairs
+//            (output o, k..k+1) and the two spline edges of input r; row sums, a readlane sum
+//            over the wave's rows, and ONE workgroup barrier (per-wave partials in LDS, double-
+//            buffered by evaluation parity) give k on every lane.
+// The stage combines run redundantly on every lane in torchdiffeq's op order; thread 0 writes
+// the outputs.  Inference only (training tapes take v4).
+// =============================================================================================
+template <bool FERRO, bool HOT>
+__global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
+  constexpr int D = 2, H = 10, K = FERRO ? 10 : 0, KP = 5, NB = 10, NG = 12, NI = NG - 1, NFL = 1 + NB;
+  constexpr int SPT = H * D * (NI + 1) * 4;
+  __shared__ __attribute__((aligned(16))) float s_sp0[SPT];
+  __shared__ __attribute__((aligned(16))) float s_sp1[SPT];
+  __shared__ __attribute__((aligned(8))) f2 s_part[2][3];
+  constexpr int SCH = 32;
+  __shared__ float s_dt[SCH], s_hh[SCH], s_h6[SCH], s_oslope[SCH];
+  __shared__ int s_ostep[SCH], s_omode[SCH];
+
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = tid >> 4, c = tid & 15;
+  const bool act = r < H;
+  const int rr = act ? r : 0;
+  const int64_t b = blockIdx.x;
+  const float l2 = FETODE_LOG2E;
+  for (int i = tid; i < SPT; i += 192) {
+    s_sp0[i] = a.plan[a.P0.sp + i];
+    s_sp1[i] = a.plan[a.P1.sp + i];
+  }
+  const bool fact = FERRO && a.plan[a.P0.flag] <= a.factor_limit && a.plan[a.P1.flag] <= a.factor_limit;
+
+  // ---- layer 0, row rr = output o: one Ferro pair (input i0, bases 2kp, 2kp+1) on lanes c < 10
+  const int i0 = c >= KP ? 1 : 0;
+  f2 ep0 = splat(0.f), k20 = splat(0.f), kE0 = splat(0.f), cp0 = splat(0.f);
+  f2 ep1 = splat(0.f), k21 = splat(0.f), kE1 = splat(0.f), cp1 = splat(0.f);
+  const int o1 = c >= KP ? 1 : 0;  // layer-1 pair lanes: output o1, bases 2 (c % 5) ..
+  if constexpr (FERRO) {
+    const bool pj = act && c < 2 * KP;
+    float t0[4][2], t1[4][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t i0x = (int64_t)rr * (D * K) + i0 * K + (pj ? (c % KP) * 2 + h : 0);
+      const float g0 = pj ? a.plan[a.P0.fe_GEc + i0x] : 0.f;
+      t0[0][h] = fact ? ex2(g0) : g0;
+      t0[1][h] = pj ? a.plan[a.P0.fe_k2 + i0x] : 0.f;
+      t0[2][h] = pj ? a.plan[a.P0.fe_k2Ec + i0x] : 0.f;
+      t0[3][h] = pj ? a.plan[a.P0.fe_CPs2 + i0x] : 0.f;
+      const int64_t i1x = (int64_t)o1 * (H * K) + rr * K + (pj ? (c % KP) * 2 + h : 0);
+      const float g1 = pj ? a.plan[a.P1.fe_GEc + i1x] : 0.f;
+      t1[0][h] = fact ? ex2(g1) : g1;
+      t1[1][h] = pj ? a.plan[a.P1.fe_k2 + i1x] : 0.f;
+      t1[2][h] = pj ? a.plan[a.P1.fe_k2Ec + i1x] : 0.f;
+      t1[3][h] = pj ? a.plan[a.P1.fe_CPs2 + i1x] : 0.f;
+    }
+    ep0 = f2{t0[0][0], t0[0][1]}; k20 = f2{t0[1][0], t0[1][1]}; kE0 = f2{t0[2][0], t0[2][1]}; cp0 = f2{t0[3][0], t0[3][1]};
+    ep1 = f2{t1[0][0], t1[0][1]}; k21 = f2{t1[1][0], t1[1][1]}; kE1 = f2{t1[2][0], t1[2][1]}; cp1 = f2{t1[3][0], t1[3][1]};
+  }
+  // ---- layer 0 feature jobs q = c + 16 s:  logistic (0, j) | logistic (1, j) | SiLU_0, SiLU_1 |
+  //      gate_0, gate_1 | exp_0, exp_1  (the last four only with FERRO)
+  float fna[2], fab[2], fmul[2], fadd[2], fw[2];
+  int fx[2];
+  bool fsilu[2], fgate[2], fexp[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int q = c + 16 * s;
+    fna[s] = 0.f; fab[s] = 0.f; fmul[s] = 1.f; fadd[s] = 0.f; fw[s] = 0.f; fx[s] = 0;
+    fsilu[s] = fgate[s] = fexp[s] = false;
+    if (q < 2 * NB) {
+      const int i = q / NB, j = q % NB;
+      fx[s] = i;
+      fna[s] = a.plan[a.P0.lg + 2 * (i * NB + j)];
+      fab[s] = a.plan[a.P0.lg + 2 * (i * NB + j) + 1];
+      fw[s] = act ? a.plan[a.P0.kw + (int64_t)rr * (D * NFL) + i * NFL + 1 + j] : 0.f;
+    } else if (q < 2 * NB + 2) {
+      const int i = q - 2 * NB;
+      fx[s] = i;
+      fna[s] = -l2;
+      fsilu[s] = true;
+      fw[s] = act ? a.plan[a.P0.kw + (int64_t)rr * (D * NFL) + i * NFL] : 0.f;
+    } else if (FERRO && q < 2 * NB + 4) {
+      fx[s] = q - (2 * NB + 2);
+      fna[s] = -a.P0.gsl2e; fmul[s] = -a.P0.wc; fadd[s] = a.P0.wc;
+      fgate[s] = true;
+    } else if (FERRO && q < 2 * NB + 6) {
+      fx[s] = q - (2 * NB + 4);
+      fna[s] = a.P0.gsl2e;
+      fexp[s] = true;
+    }
+  }
+  // knots of the two layer-0 inputs on lanes c < NG (every row holds the same)
+  const float kn0 = c < NG ? a.plan[a.P0.knots + c] : __builtin_inff();
+  const float kn1 = c < NG ? a.plan[a.P0.knots + NG + c] : __builtin_inff();
+  const float rh0 = c < NI ? a.plan[a.P0.rh + c] : 0.f;
+  const float rh1 = c < NI ? a.plan[a.P0.rh + NI + c] : 0.f;
+  const float c0o = act ? a.plan[a.P0.fconst + rr] : 0.f;
+  const float* sp0_r = &s_sp0[rr * D * (NI + 1) * 4];
+
+  // ---- layer 1, row rr = input i: feature job c (logistic j = c < 10, SiLU, gate, exp)
+  float hna = 0.f, hab = 0.f, hmul = 1.f, hadd = 0.f, hw0 = 0.f, hw1 = 0.f;
+  bool hsilu = false, hgate = false, hexp = false;
+  if (act) {
+    if (c < NB) {
+      hna = a.plan[a.P1.lg + 2 * (rr * NB + c)];
+      hab = a.plan[a.P1.lg + 2 * (rr * NB + c) + 1];
+      hw0 = a.plan[a.P1.kw + (int64_t)0 * (H * NFL) + rr * NFL + 1 + c];
+      hw1 = a.plan[a.P1.kw + (int64_t)1 * (H * NFL) + rr * NFL + 1 + c];
+    } else if (c == NB) {
+      hna = -l2;
+      hsilu = true;
+      hw0 = a.plan[a.P1.kw + (int64_t)0 * (H * NFL) + rr * NFL];
+      hw1 = a.plan[a.P1.kw + (int64_t)1 * (H * NFL) + rr * NFL];
+    } else if (FERRO && c == NB + 1) {
+      hna = -a.P1.gsl2e; hmul = -a.P1.wc; hadd = a.P1.wc;
+      hgate = true;
+    } else if (FERRO && c == NB + 2) {
+      hna = a.P1.gsl2e;
+      hexp = true;
+    }
+  }
+  const float knh = (act && c < NG) ? a.plan[a.P1.knots + rr * NG + c] : __builtin_inff();
+  const float rhh = (act && c < NI) ? a.plan[a.P1.rh + rr * NI + c] : 0.f;
+  const float c1o0 = a.plan[a.P1.fconst + 0], c1o1 = a.plan[a.P1.fconst + 1];
+  const float* sp1_a = &s_sp1[(0 * H + rr) * (NI + 1) * 4];
+  const float* sp1_b = &s_sp1[(1 * H + rr) * (NI + 1) * 4];
+
+  // hysteresis state (ferro_class.py:409): both layer-0 inputs on every lane, input rr of layer 1
+  // on its row
+  float pv0a = 0.f, pv0b = 0.f, pv1 = 0.f;
+  if (FERRO) {
+    pv0a = a.state[b * D + 0];
+    pv0b = a.state[b * D + 1];
+    pv1 = a.state[a.B * D + b * H + rr];
+  }
+  bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
+  f2 y = f2{a.y0[b * D + 0], a.y0[b * D + 1]};
+  if (!a.single_eval && tid == 0) *reinterpret_cast<f2*>(&a.solution[b * D]) = y;
+  int par = 0;
+  __syncthreads();  // tables staged
+
+  auto eval_body = [&](f2 xin, auto fact_tag) __attribute__((always_inline)) -> f2 {
+    constexpr bool F_ = decltype(fact_tag)::value;
+    const float x0 = xin.x, x1 = xin.y;
+    // ---------------- layer 0 ----------------
+    float acc = 0.f;
+    float fv[2];
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const float x = fx[s] ? x1 : x0;
+      const float pv = fgate[s] ? (re0 ? x : (fx[s] ? pv0b : pv0a)) : 0.f;
+      const float e = ex2(ffma(fna[s], x - pv, fab[s]));
+      const float sg = rcp(1.0f + e);
+      float v = ffma(sg, fsilu[s] ? x : fmul[s], fadd[s]);
+      fv[s] = fexp[s] ? e : v;
+      acc = ffma(fw[s], fv[s], acc);
+    }
+    if constexpr (FERRO) {
+      // gate_i / exp_i of the two inputs: slot 1, lanes 6..9 of every row (row_newbcast)
+      const float g0 = dpp<0x156>(fv[1]), g1 = dpp<0x157>(fv[1]);
+      const float e0 = dpp<0x158>(fv[1]), e1 = dpp<0x159>(fv[1]);
+      const float4 gi = i0 ? make_float4(x1, g1, e1, 0.f) : make_float4(x0, g0, e0, 0.f);
+      const f2 pr = v4_pair<F_>(gi, ep0, k20, kE0, cp0, splat(0.0f), a.P0.gsl2e);
+      acc += pr.x + pr.y;
+      pv0a = x0;  // ferro_class.py:409
+      pv0b = x1;
+      re0 = false;
+    }
+    // spline edges (r, 0), (r, 1): the lane whose knot opens the interval (ballot count over a row)
+    {
+      const bool fin0 = __builtin_isfinite(x0), fin1 = __builtin_isfinite(x1);
+      int m0 = (int)__builtin_popcountll(__builtin_amdgcn_ballot_w64(x0 >= kn0) & 0xFFFFull) - 1;
+      int m1 = (int)__builtin_popcountll(__builtin_amdgcn_ballot_w64(x1 >= kn1) & 0xFFFFull) - 1;
+      m0 = ((unsigned)m0 < (unsigned)NI && fin0) ? m0 : NI;
+      m1 = ((unsigned)m1 < (unsigned)NI && fin1) ? m1 : NI;
+      if (c == m0) {
+        const float u = (x0 - kn0) * rh0;
+        const float4 cf = *reinterpret_cast<const float4*>(&sp0_r[(0 * (NI + 1) + m0) * 4]);
+        acc += ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
+      }
+      if (c == m1) {
+        const float u = (x1 - kn1) * rh1;
+        const float4 cf = *reinterpret_cast<const float4*>(&sp0_r[(1 * (NI + 1) + m1) * 4]);
+        acc += ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
+      }
+      if (c == 0 && !(fin0 && fin1)) acc += __builtin_nanf("");  // the reference's NaN bases
+    }
+    const float h = row_sum16(acc) + c0o;
+    // ---------------- layer 1 (input h = h_rr) ----------------
+    float acc0 = 0.f, acc1 = 0.f;
+    {
+      const float pv = hgate ? (re1 ? h : pv1) : 0.f;
+      const float e = ex2(ffma(hna, h - pv, hab));
+      const float sg = rcp(1.0f + e);
+      float v = ffma(sg, hsilu ? h : hmul, hadd);
+      v = hexp ? e : v;
+      acc0 = hw0 * v;
+      acc1 = hw1 * v;
+      if constexpr (FERRO) {
+        const float gt = dpp<0x15B>(v), ee = dpp<0x15C>(v);  // row_newbcast:11 / :12
+        const f2 pr = v4_pair<F_>(make_float4(h, gt, ee, 0.f), ep1, k21, kE1, cp1, splat(0.0f), a.P1.gsl2e);
+        const float ps = pr.x + pr.y;
+        acc0 += o1 ? 0.0f : ps;
+        acc1 += o1 ? ps : 0.0f;
+        pv1 = h;
+        re1 = false;
+      }
+    }
+    {
+      const bool fin = __builtin_isfinite(h);
+      const uint64_t bal = __builtin_amdgcn_ballot_w64(h >= knh);
+      int m = (int)__builtin_popcountll((bal >> (lane & 48)) & 0xFFFFull) - 1;
+      m = ((unsigned)m < (unsigned)NI && fin) ? m : NI;
+      if (c == m) {
+        const float u = (h - knh) * rhh;
+        const float4 ca = *reinterpret_cast<const float4*>(&sp1_a[m * 4]);
+        const float4 cb = *reinterpret_cast<const float4*>(&sp1_b[m * 4]);
+        acc0 += ffma(ffma(ffma(ca.w, u, ca.z), u, ca.y), u, ca.x);
+        acc1 += ffma(ffma(ffma(cb.w, u, cb.z), u, cb.y), u, cb.x);
+      }
+      if (c == 0 && !fin) {
+        acc0 += __builtin_nanf("");
+        acc1 += __builtin_nanf("");
+      }
+    }
+    acc0 = act ? acc0 : 0.0f;
+    acc1 = act ? acc1 : 0.0f;
+    const float v0 = row_sum16(acc0), v1 = row_sum16(acc1);
+    auto rl = [](float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); };
+    const float s0 = (rl(v0, 0) + rl(v0, 16)) + (rl(v0, 32) + rl(v0, 48));
+    const float s1 = (rl(v1, 0) + rl(v1, 16)) + (rl(v1, 32) + rl(v1, 48));
+    if (lane == 0) s_part[par][w] = f2{s0, s1};
+    __syncthreads();
+    const f2 p0 = s_part[par][0], p1 = s_part[par][1], p2 = s_part[par][2];
+    par ^= 1;
+    return f2{((p0.x + p1.x) + p2.x) + c1o0, ((p0.y + p1.y) + p2.y) + c1o1};
+  };
+
+  auto load_steps = [&](int s0) {
+    __syncthreads();
+    for (int i = tid; i < SCH && s0 + i < a.n_steps; i += 192) {
+      s_dt[i] = a.step_coef[4 * (s0 + i) + 0];
+      s_hh[i] = a.step_coef[4 * (s0 + i) + 1];
+      s_h6[i] = a.step_coef[4 * (s0 + i) + 2];
+    }
+    __syncthreads();
+  };
+  auto load_outs = [&](int j0) {
+    __syncthreads();
+    for (int i = tid; i < SCH; i += 192) {
+      const bool in = j0 + i < a.T;
+      s_ostep[i] = in ? a.out_step[j0 + i] : -1;
+      s_omode[i] = in ? a.out_mode[j0 + i] : 1;
+      s_oslope[i] = in ? a.out_slope[j0 + i] : 0.f;
+    }
+    __syncthreads();
+  };
+  auto out_write = [&](int j, f2 v) __attribute__((always_inline)) {
+    if (tid == 0) *reinterpret_cast<f2*>(&a.solution[((int64_t)j * a.B + b) * D]) = v;
+  };
+  auto interp = [](int mode, f2 y0v, f2 y1v, float sl) -> f2 {
+    return mode == 0 ? y0v : (mode == 1 ? y1v : y0v + splat(sl) * (y1v - y0v));
+  };
+  using FT = std::integral_constant<bool, true>;
+  using FF = std::integral_constant<bool, false>;
+
+  const f2 third = splat(1.0f / 3.0f);
+  if constexpr (HOT) {
+    int sb = 0, jb = 1, jj = 1;
+    load_steps(0);
+    load_outs(1);
+    auto run = [&](auto fact_tag) __attribute__((always_inline)) {
+      for (int s = 0; s < a.n_steps; ++s) {
+        if (s - sb == SCH) {
+          sb = s;
+          load_steps(s);
+        }
+        if (jj + 1 - jb >= SCH) {
+          jb = jj;
+          load_outs(jj);
+        }
+        const f2 dt = splat(s_dt[s - sb]);
+        const f2 k1 = eval_body(y, fact_tag);
+        const f2 k2 = eval_body(y + (dt * k1) * third, fact_tag);
+        const f2 k3 = eval_body(y + dt * (k2 - k1 * third), fact_tag);
+        const f2 k4 = eval_body(y + dt * ((k1 - k2) + k3), fact_tag);
+        const f2 y1 = y + (((k1 + splat(3.0f) * (k2 + k3)) + k4) * dt) * splat(0.125f);
+        while (jj < a.T) {
+          if (jj - jb == SCH) {
+            jb = jj;
+            load_outs(jj);
+          }
+          if (s_ostep[jj - jb] != s) break;
+          out_write(jj, interp(s_omode[jj - jb], y, y1, s_oslope[jj - jb]));
+          ++jj;
+        }
+        y = y1;
+      }
+    };
+    if (fact) run(FT{});
+    else run(FF{});
+  } else {
+    auto eval = [&](f2 xin) __attribute__((always_inline)) -> f2 {
+      if (fact) return eval_body(xin, FT{});
+      return eval_body(xin, FF{});
+    };
+    if (a.single_eval) {
+      const f2 f = eval(y);
+      if (tid == 0) *reinterpret_cast<f2*>(&a.eval_out[b * D]) = f;
+    } else {
+      const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4 : a.method == FETODE_MIDPOINT ? 2 : 1;
+      int sb = 0, jb = 1, jj = 1;
+      load_steps(0);
+      load_outs(1);
+      for (int s = 0; s < a.n_steps; ++s) {
+        if (s - sb == SCH) {
+          sb = s;
+          load_steps(s);
+        }
+        const f2 dt = splat(s_dt[s - sb]), hh = splat(s_hh[s - sb]), h6 = splat(s_h6[s - sb]);
+        f2 k1 = splat(0.f), k2 = splat(0.f), k3 = splat(0.f), k4 = splat(0.f);
+        for (int st = 0; st < ns; ++st) {
+          f2 xin = y;
+          if (a.method == FETODE_RK4) {
+            if (st == 1) xin = y + (dt * k1) * third;
+            else if (st == 2) xin = y + dt * (k2 - k1 * third);
+            else if (st == 3) xin = y + dt * ((k1 - k2) + k3);
+          } else if (a.method == FETODE_RK4_CLASSIC) {
+            if (st == 1) xin = y + hh * k1;
+            else if (st == 2) xin = y + hh * k2;
+            else if (st == 3) xin = y + dt * k3;
+          } else if (a.method == FETODE_MIDPOINT) {
+            if (st == 1) xin = y + k1 * hh;
+          }
+          const f2 kk = eval(xin);
+          if (st == 0) k1 = kk;
+          else if (st == 1) k2 = kk;
+          else if (st == 2) k3 = kk;
+          else k4 = kk;
+        }
+        f2 y1;
+        if (a.method == FETODE_RK4) y1 = y + (((k1 + splat(3.0f) * (k2 + k3)) + k4) * dt) * splat(0.125f);
+        else if (a.method == FETODE_RK4_CLASSIC) y1 = y + h6 * (((k1 + splat(2.0f) * k2) + splat(2.0f) * k3) + k4);
+        else if (a.method == FETODE_MIDPOINT) y1 = y + dt * k2;
+        else y1 = y + dt * k1;
+        while (jj < a.T) {
+          if (jj - jb == SCH) {
+            jb = jj;
+            load_outs(jj);
+          }
+          if (s_ostep[jj - jb] != s) break;
+          out_write(jj, interp(s_omode[jj - jb], y, y1, s_oslope[jj - jb]));
+          ++jj;
+        }
+        y = y1;
+      }
+    }
+  }
+  if (FERRO) {
+    if (tid == 0) {
+      a.state[b * D + 0] = pv0a;
+      a.state[b * D + 1] = pv0b;
+    }
+    if (act && c == 0) a.state[a.B * D + b * H + rr] = pv1;
+  }
+}
+
+
 typedef void (*fused_fn)(FusedArgs);
 struct FusedEntry {
   int in0, h, out, K, NB, NG;
   bool ferro;
-  fused_fn fn;      // single evaluations and every fixed-grid method
-  fused_fn fn_rk4;  // the rk4 (3/8) integrate path, all four stages inlined
+  fused_fn fn;        // v4: single evaluations and every fixed-grid method
+  fused_fn fn_rk4;    // v4: the rk4 (3/8) integrate path, all four stages inlined
+  fused_fn small;     // v6 (one trajectory per workgroup): generic
+  fused_fn small_rk4; // v6: rk4
 };
 const FusedEntry kFused[] = {
     // LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146)
-    {2, 10, 2, 10, 10, 12, true, fused4_kernel<10, 10, 10, 12, true, false>, fused4_kernel<10, 10, 10, 12, true, true>},
+    {2, 10, 2, 10, 10, 12, true, fused4_kernel<10, 10, 10, 12, true, false>, fused4_kernel<10, 10, 10, 12, true, true>,
+     small6_kernel<true, false>, small6_kernel<true, true>},
     // LV KAN [2,10,2] (predator_prey.py:101)
-    {2, 10, 2, 1, 10, 12, false, fused4_kernel<10, 2, 10, 12, false, false>, fused4_kernel<10, 2, 10, 12, false, true>},
+    {2, 10, 2, 1, 10, 12, false, fused4_kernel<10, 2, 10, 12, false, false>, fused4_kernel<10, 2, 10, 12, false, true>,
+     small6_kernel<false, false>, small6_kernel<false, true>},
 };
+
+// Batches up to kSmallMax take v6 (one trajectory per 3-wave workgroup, latency-bound chain split
+// over 160 lanes), larger ones v4 (two trajectories per wave, issue-bound); training tapes are v4
+// only.  FETODE_SMALL_MAX overrides the switch point (diagnostics / tuning).
+int64_t g_small_max = [] {
+  const char* e = getenv("FETODE_SMALL_MAX");
+  return e ? (int64_t)atoll(e) : (int64_t)2048;
+}();
+int64_t small_max() { return g_small_max; }
 
 const FusedEntry* find_fused(const fetode_field_t* f) {
   if (f->n_layers != 2) return nullptr;
@@ -683,9 +1074,17 @@ int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
   if (!e) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
   layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
   layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
-  // two trajectories per one-wave workgroup
-  const fused_fn fn = (!a.single_eval && a.method == FETODE_RK4) ? e->fn_rk4 : e->fn;
-  hipLaunchKernelGGL(fn, dim3(nblk(a.B, 2)), dim3(64), 0, (hipStream_t)stream, a);
+  static const float limit = [] {
+    const char* e = getenv("FETODE_FACTOR_LIMIT");
+    return e ? (float)atof(e) : kFactorLimit;
+  }();
+  a.factor_limit = limit;
+  const bool rk4 = !a.single_eval && a.method == FETODE_RK4;
+  if (!a.tape && a.B <= small_max()) {  // v6: one trajectory per 192-thread workgroup
+    hipLaunchKernelGGL(rk4 ? e->small_rk4 : e->small, dim3((unsigned)a.B), dim3(192), 0, (hipStream_t)stream, a);
+  } else {                              // v4: two trajectories per one-wave workgroup
+    hipLaunchKernelGGL(rk4 ? e->fn_rk4 : e->fn, dim3(nblk(a.B, 2)), dim3(64), 0, (hipStream_t)stream, a);
+  }
   LAUNCH_CHECK();
   return FETODE_OK;
 }
@@ -699,6 +1098,12 @@ int fetode_debug_stamp_buffer(void* p) {
   return hipMemcpyToSymbol(HIP_SYMBOL(g_fetode_stamps), &p, sizeof(p)) == hipSuccess ? FETODE_OK : FETODE_EHIP;
 }
 #endif
+
+int64_t fetode_fused_set_small_batch_max(int64_t b) {
+  const int64_t prev = g_small_max;
+  if (b >= 0) g_small_max = b;
+  return prev;
+}
 
 int fetode_fused_supported(const fetode_field_t* f) {
   if (validate_field(f) != FETODE_OK) return 0;

@@ -352,13 +352,13 @@ class _NormAllReduce(torch.autograd.Function):
     @staticmethod
     def forward(ctx, v, group, cpu):
         ctx.group, ctx.cpu = group, cpu
-        t = v.detach().cpu() if cpu else v.detach().clone()
+        t = v.detach().cpu().clone() if cpu else v.detach().clone()   # never reduce into v itself
         torch.distributed.all_reduce(t, group=group)
         return t.to(v.device)
 
     @staticmethod
     def backward(ctx, g):
-        t = g.detach().cpu() if ctx.cpu else g.detach().clone()
+        t = g.detach().cpu().clone() if ctx.cpu else g.detach().clone()
         torch.distributed.all_reduce(t, group=ctx.group)
         return t.to(g.device), None, None
 
@@ -371,11 +371,14 @@ class _Dopri5Grad:
     as _Dopri5; the field's own HIP VJP serves each evaluation, the O(B*D) stage algebra is torch
     on the device, and t / dt are float64 device tensors like torchdiffeq's."""
 
-    def __init__(self, func, y0, rtol, atol, options, reversed_):
+    def __init__(self, func, y0, rtol, atol, options, reversed_, check_device=True):
         unsupported = [k for k in ("step_t", "jump_t", "norm", "perturb") if options.get(k) is not None]
         if unsupported:
             raise NotImplementedError(f"dopri5 options not supported with autograd: {unsupported}")
         self.func_user, self.sign, self.y0 = func, (-1.0 if reversed_ else 1.0), y0
+        # the field's output must come from the HIP path; the CPU gloo tests of the sharded-norm
+        # logic drive this class with a plain torch field in fp64 (check_device=False)
+        self.check_device = check_device
         # trajectory-sharded solve (dist.odeint_sharded): norms over the global batch, see
         # _NormAllReduce for the gradient through them
         group = options.get("norm_group")
@@ -411,7 +414,8 @@ class _Dopri5Grad:
         """_PerturbFunc (t cast to the state dtype) + _ReverseFunc (-f(-t, y))."""
         self.nfev += 1
         out = self.func_user((self.sign * t).to(y.dtype), y)
-        _lib.require_gpu_tensor(out, "odeint func output")
+        if self.check_device:
+            _lib.require_gpu_tensor(out, "odeint func output")
         return -out if self.sign < 0 else out
 
     def rms(self, x, finite_of=None):

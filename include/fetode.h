@@ -106,6 +106,12 @@ int32_t fetode_state_width(const fetode_field_t* field);
 /* 1 if a fused (single-launch) integrator kernel exists for this field shape. */
 int fetode_fused_supported(const fetode_field_t* field);
 
+/* Kernel choice of the fused integrator: batches B <= this value (default 2048, env
+ * FETODE_SMALL_MAX) take the small-batch kernel (one trajectory per 3-wave workgroup: the
+ * strong-scaling shard size), larger ones and every training tape the two-trajectories-per-wave
+ * kernel.  Sets the value when b >= 0; returns the previous one.  Process-wide tuning knob. */
+int64_t fetode_fused_set_small_batch_max(int64_t b);
+
 /* One stateful field evaluation out = field(x) — KANFET.forward / KAN.forward.
  * x (B, in0), out (B, out_last), state (B*state_width, layout above) updated in place. */
 int fetode_field_forward(const fetode_field_t* field, const void* plan, const float* x, int64_t B,

@@ -69,3 +69,73 @@ def test_shard_bounds_rules():
     with pytest.raises(ValueError):
         D.shard_bounds(3, 2, 3)          # shard of 1 flips the ferro first-call rule
     assert D.shard_bounds(1, 0, 1) == (0, 1)
+
+
+# ---------------------------------------------------------------------------------------------
+# sharded dopri5 under autograd: the norm all-reduce and its backward (dopri5._NormAllReduce)
+# ---------------------------------------------------------------------------------------------
+
+def _field64():
+    torch.manual_seed(4)
+    W1 = torch.nn.Parameter(torch.randn(2, 16, dtype=torch.float64) * 0.7)
+    W2 = torch.nn.Parameter(torch.randn(16, 2, dtype=torch.float64) * 0.5)
+    b = torch.nn.Parameter(torch.randn(2, dtype=torch.float64) * 0.1)
+    return [W1, W2, b], (lambda tt, y: torch.tanh(y @ W1) @ W2 + b - 0.3 * y)
+
+
+def _y0_64():
+    return torch.linspace(-1.0, 1.5, 12, dtype=torch.float64).reshape(6, 2)
+
+
+def _sharded_grad(rank, world, sizes, group_opt):
+    from fet_ode_amd.dopri5 import _Dopri5Grad
+    ps, f = _field64()
+    y0g = _y0_64()
+    lo = sum(sizes[:rank])
+    y0 = y0g[lo:lo + sizes[rank]]
+    opts = {"norm_group": group_opt} if group_opt else {}
+    s = _Dopri5Grad(f, y0, 1e-6, 1e-8, opts, False, check_device=False)
+    sol = s.integrate(torch.tensor([0.0, 0.4, 1.0], dtype=torch.float64))
+    # this shard's share of the global mean loss (odeint_sharded docstring)
+    loss = (sol * sol.flip(-1)).sum() / (sol.shape[0] * y0g.shape[0] * sol.shape[2])
+    loss.backward()
+    return sol.detach(), [p.grad.clone() for p in ps], [(a[1], a[3]) for a in s.attempts]
+
+
+def _dopri_worker(rank, world, port, q, sizes):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sol, grads, att = _sharded_grad(rank, world, sizes, "world")
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        dist.all_reduce(flat)           # == allreduce_gradients(average=False)
+        q.put((rank, sol, flat, att))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sizes", [(3, 3), (4, 2)])
+def test_sharded_dopri5_gradient_through_step_control_fp64(sizes):
+    """fp64 on CPU (no rounding noise): 2 ranks with the global-batch RMS norm take the single
+    process's steps, and the summed gradients equal the single-process gradient — including the
+    d loss / d dt terms that cross ranks (the all-reduced norm adjoint), with unequal shards too."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dopri_worker, args=(r, 2, port, q, sizes)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, s0, g0, a0), (_, s1, g1, a1) = res
+    sol, grads, att = _sharded_grad(0, 1, (6,), None)
+    ref = torch.cat([g.reshape(-1) for g in grads])
+    assert a0 == a1 and [a[1] for a in a0] == [a[1] for a in att] and len(att) > 3
+    for (d0, _), (dr, _) in zip(a0, att):
+        assert abs(d0 - dr) <= 1e-12 * abs(dr)
+    assert torch.allclose(torch.cat([s0, s1], dim=1), sol, rtol=1e-12, atol=1e-14)
+    assert torch.equal(g0, g1)
+    assert ((g0 - ref).norm() / ref.norm()).item() <= 1e-10, ((g0 - ref).norm() / ref.norm()).item()

@@ -109,23 +109,34 @@ def test_sharded_fused_rk4_training_gradients(dev):
     assert _rel(g0, ref) <= 1e-5, _rel(g0, ref)
 
 
-def test_sharded_dopri5_training_gradients(dev):
-    import fet_ode_amd as F
-    g = load_golden("traj_kanfet")
+def _dopri5_grads(F, g, dev, flip=False):
     m = _model(F, golden_sd(g))
     y0 = torch.from_numpy(g["y0_B64"]).to(dev)
+    if flip:      # the same global loss with the batch in reverse order: only fp32 sums reorder
+        y0 = y0.flip(0)
     sol = F.odeint(lambda tt, yy: m(yy), y0, torch.tensor(T_DOPRI, dtype=torch.float64), rtol=1e-3, atol=1e-4)
     (sol.square().sum() / sol.numel()).backward()
-    ref = _grads(m)
-    ref_att = [(a[1], a[3]) for a in F.dopri5.dopri5_solve.last.attempts]
+    att = [(a[1], a[3]) for a in F.dopri5.dopri5_solve.last.attempts]
+    return _grads(m), (sol.flip(1) if flip else sol).detach().cpu(), att
+
+
+def test_sharded_dopri5_training_gradients(dev):
+    """Same attempts and solution as one device; the gradient within the fp32 noise floor of the
+    single-device gradient itself.  The gradient through dopri5's step-size control is
+    ill-conditioned in fp32, so the floor is measured: the single-device gradient
+    of the same loss with the batch reversed (the norms' summation order changes, nothing else).
+    The exact cross-rank algebra is pinned in fp64 by tests/test_dist_gloo.py
+    (test_sharded_dopri5_gradient_through_step_control_fp64)."""
+    import fet_ode_amd as F
+    g = load_golden("traj_kanfet")
+    ref, sol, ref_att = _dopri5_grads(F, g, dev)
+    ref_flip, _, _ = _dopri5_grads(F, g, dev, flip=True)
+    floor = _rel(ref_flip, ref)
     (_, s0, g0, a0), (_, s1, g1, a1) = _run("dopri5")
     assert [a[1] for a in a0] == [a[1] for a in ref_att] and a0 == a1   # same accept pattern, both ranks
     for (d0, _), (dr, _) in zip(a0, ref_att):
         assert abs(d0 - dr) <= 1e-5 * abs(dr)
-    assert torch.allclose(g0, g1, rtol=0, atol=0)
+    assert torch.equal(g0, g1)
     full = torch.cat([s0, s1], dim=1)
-    assert ((full - sol.detach().cpu()).norm() / sol.detach().cpu().norm()).item() <= 1e-5
-    # the only difference from the single device is the norm's summation order (fp64 partial sums
-    # vs one fp32 mean), felt through dt; without the all-reduced norm adjoint the cross-rank
-    # terms of d loss / d dt would be missing
-    assert _rel(g0, ref) <= 1e-4, _rel(g0, ref)
+    assert ((full - sol).norm() / sol.norm()).item() <= 1e-5
+    assert _rel(g0, ref) <= max(4 * floor, 1e-5), (_rel(g0, ref), floor)

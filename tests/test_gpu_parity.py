@@ -370,3 +370,58 @@ def test_fused_rk4_kanfet_well_conditioned_trajectories_bench_config(dev):
     assert st["n_well"] >= 256, st
     assert st["ok"], st
     assert st["gpu_well_frac"] >= st["oracle_well_frac"] - 0.02, st
+
+
+@pytest.fixture
+def kernel_switch():
+    """Force the fused integrator's kernel: small(True) -> v6 at any batch, small(False) -> v4."""
+    from fet_ode_amd import _lib
+    lib = _lib.load()
+    prev = lib.fetode_fused_set_small_batch_max(-1)
+
+    def small(on):
+        lib.fetode_fused_set_small_batch_max(1 << 40 if on else 0)
+    yield small
+    lib.fetode_fused_set_small_batch_max(prev)
+
+
+@pytest.mark.parametrize("B", [1, 7, 64, 512])
+@pytest.mark.parametrize("method", ["rk4", "rk4_classic", "midpoint", "euler"])
+def test_small_batch_kernel_matches_v4(dev, kernel_switch, B, method):
+    """v6 (one trajectory per 3-wave workgroup, the strong-scaling kernel) and v4 (two per wave)
+    integrate the same KAN-FET solve: 3 steps (each from its own hysteresis state, first-call rule
+    included) within 1e-5 per slice, and the same final hysteresis state; KAN (no hysteresis)
+    over the whole 35-point grid within 1e-5 of the reference fixture."""
+    import fet_ode_amd as F
+    g = load_golden("traj_kanfet")
+    y0 = torch.from_numpy(g["y0_B64"]).repeat(8, 1)[:B].to(dev)
+    t = torch.from_numpy(g["t35"])[:4]
+    outs, states = [], []
+    for small in (True, False):
+        kernel_switch(small)
+        m = _kanfet_from(g, dev)
+        with torch.no_grad():
+            outs.append(F.odeint(F.autonomous(m), y0, t, method=method).cpu())
+        states.append([l.ferro._prev.cpu() for l in m.layers])
+    assert slice_rel_err(outs[0], outs[1]) <= 1e-5
+    for a, b in zip(*states):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
+    if method == "rk4":
+        gk = load_golden("traj_kan")
+        for small in (True, False):
+            kernel_switch(small)
+            m = F.KAN([2, 10, 2], grid_size=5)
+            m.load_state_dict(golden_sd(gk))
+            m = m.to(dev)
+            yk = torch.from_numpy(gk["y0_B64"]).repeat(8, 1)[:B]
+            with torch.no_grad():
+                sol = F.odeint(F.autonomous(m), yk.to(dev), torch.from_numpy(gk["t35"]), method="rk4").cpu()
+            # KAN is stateless: row i of the repeated batch is fixture trajectory i % 64
+            exp = torch.from_numpy(gk["sol_B64_t35"])[:, torch.arange(B) % 64]
+            assert slice_rel_err(sol, exp) <= REL, small
+
+
+def test_small_batch_kernel_single_eval_and_reference(dev, kernel_switch):
+    """fetode_field_forward on v6: two stateful KAN-FET calls against the reference fixture."""
+    kernel_switch(True)
+    test_kanfet_field_two_calls(dev)
