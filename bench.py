@@ -418,23 +418,6 @@ def cpu_train_baseline(sd, y0, t, n_iters):
                       f"with oracle/torch_ref.py autograd (torch CPU fp32): " + ", ".join(f"{x:.2f}" for x in ts) + " s"}
 
 
-def well_conditioned_stats(gpu, e32, e64, tol_ref=1e-5, tol_gpu=2e-5):
-    """tests/test_gpu_parity.py well_conditioned_parity: the trajectories the reference's fp32 solve
-    keeps within 1e-5 of fp64, and how the GPU does on them."""
-    def te(a, b):
-        a, b = a.double(), b.double()
-        return ((a - b).norm(dim=2) / b.norm(dim=2).clamp_min(1e-30)).max(0).values
-    well = te(e32, e64) <= tol_ref
-    g_ref = te(gpu, e32)
-    return {"oracle_fp32_well_frac": float(well.double().mean()),
-            "gpu_well_frac": float((te(gpu, e64) <= tol_ref).double().mean()),
-            "n_well": int(well.sum()),
-            "max_gpu_vs_oracle_fp32_on_well": float(g_ref[well].max()) if bool(well.any()) else 0.0,
-            "all_within_2e-5": bool((g_ref[well] <= tol_gpu).all()),
-            "criterion": "per trajectory, max over time of ||y_t - ref_t|| / ||ref_t||; 'well' = the reference "
-                         "fp32 solve within 1e-5 of fp64 (tests/test_gpu_parity.py)"}
-
-
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -537,6 +520,9 @@ def main():
                 from oracle import torch_ref as O
                 r64 = O.KANFETRef.from_state_dict(sd, 2).to(torch.float64)
                 e64 = O.odeint(lambda tt, yy: r64(yy), y0.double(), t, method="rk4")
+            from oracle import parity as P
+            runs = P.perturbed_solves(sd, y0, t, 5)
+            robust = P.robust_parity(sol.cpu(), ref_sol, e64, runs[:3], runs[3:])
             g = sol.cpu().double()
             r = ref_sol.double()
             out["parity"] = {
@@ -545,10 +531,12 @@ def main():
                                              / r.reshape(T, -1).norm(dim=1)).max().item(),
                 "cpu_ref_fp32_vs_fp64_max_slice_rel": ((r - e64).reshape(T, -1).norm(dim=1)
                                                        / e64.reshape(T, -1).norm(dim=1)).max().item(),
-                "well_conditioned": well_conditioned_stats(g, r, e64),
+                "robust_subset": robust,
+                "robust_subset_ok": P.robust_parity_ok(robust),
                 "note": "KAN-FET is ill-conditioned in fp32: the CPU reference's own fp32 solve departs from "
-                        "fp64 by the per-slice error above; the 1e-5 bar is checked on the trajectories fp32 "
-                        "can meet it on (well_conditioned; DESIGN.md §2)",
+                        "fp64 by the per-slice error above, and which trajectories stay within 1e-5 depends on "
+                        "the rounding; the 1e-5 bar is checked on the trajectories every equally valid "
+                        "reference rounding keeps within 1e-5 (robust_subset, oracle/parity.py; DESIGN.md §2)",
             }
         print(json.dumps(out), flush=True)
     if world > 1:
