@@ -129,6 +129,10 @@ def kan_backward(mod, xc, grad, want_x, want_params, gx_accum=None):
 
 
 def kanlinear_apply(mod, x2d):
+    if not grad_enabled_for(x2d, *[p for p in kan_params(mod) if p is not None]):
+        out = wide_apply(mod, None, x2d)   # production widths: the MFMA wide-layer kernel
+        if out is not None:
+            return out
     return _KANLinearFn.apply(mod, x2d, *kan_params(mod))
 
 
@@ -194,6 +198,11 @@ def ferro_backward(mod, xc, prev, reinit, bsign, grad, want_x, want_params, gx_a
 
 def ferro_apply(mod, x, reinit: bool, bsign, want_basis: bool, accumulate_into=None):
     params = [getattr(mod, n) for n in FERRO_PARAM_NAMES]
+    if (bsign is None and not want_basis and accumulate_into is None
+            and not grad_enabled_for(x, *params)):
+        out = wide_apply(None, mod, _lib.f32c(x), reinit=reinit)   # production widths: wide-layer kernel
+        if out is not None:
+            return out, None
     out, basis = _FerroFn.apply(mod, x, reinit, bsign, want_basis, accumulate_into, *params)
     return out, basis
 
@@ -325,7 +334,18 @@ def field_apply(model, x: torch.Tensor) -> torch.Tensor:
             out = _fused_eval(model, handle, x2)
             return out.reshape(*lead, out.shape[-1]) if not model.has_ferro else out
     h = x2
+    grad = grad_enabled_for(x2, *params)
     for kan, fer in field_layers(model):
+        if not grad:
+            # production widths (ETT KANFET[64,128,64], ...): the whole layer KANLinear + Ferro in one launch
+            reinit = fer._needs_reinit(h) if fer is not None else False
+            if fer is None or fer._branch_sign_for(h) is None:
+                y = wide_apply(kan, fer, h.contiguous(), reinit=reinit)
+                if y is not None:
+                    if fer is not None:
+                        fer._commit_state(h, reinit)
+                    h = y
+                    continue
         y = kanlinear_apply(kan, h)
         if fer is not None:
             reinit = fer._needs_reinit(h)
@@ -336,4 +356,82 @@ def field_apply(model, x: torch.Tensor) -> torch.Tensor:
     out = h
     if not model.has_ferro:
         out = out.reshape(*lead, out.shape[-1])
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# wide layers (fetode_wide_layer_*): KANLinear + Ferro of one layer in one launch, Ferro on VALU,
+# the KAN contraction on MFMA (production widths: ETT 64/128, ECG FerroElectricNet 64/128)
+# ---------------------------------------------------------------------------------------------
+
+def _wide_key(kan, fer, device):
+    ts = []
+    if kan is not None:
+        ts += [kan.grid, *[p for p in kan_params(kan) if p is not None]]
+    if fer is not None:
+        ts += [getattr(fer, n) for n in FERRO_PARAM_NAMES]
+    key = [str(device)]
+    for t in ts:
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.device != device:
+            return None
+        key += [t.data_ptr(), t._version]
+    return tuple(key)
+
+
+def wide_plan(kan, fer, device):
+    """(plan, kan descriptor, ferro descriptor) of a wide layer, or None when the layer has no
+    wide kernel.  Packed once per parameter version (the tensors' version counters, like the
+    fused plan), cached on the KANLinear (or the Ferro module when alone)."""
+    owner = kan if kan is not None else fer
+    attr = "_fetode_wide_kf" if (kan is not None and fer is not None) else "_fetode_wide"
+    key = _wide_key(kan, fer, device)
+    cached = owner.__dict__.get(attr)
+    if cached is not None and key is not None and cached[0] == key:
+        return cached[1]
+    lib = _lib.load()
+    keep = []
+    kd = kan.desc(keep) if kan is not None else None
+    fd = fer.desc(keep, None) if fer is not None else None
+    kp = _lib.ctypes.byref(kd) if kd is not None else None
+    fp = _lib.ctypes.byref(fd) if fd is not None else None
+    if not lib.fetode_wide_layer_supported(kp, fp):
+        owner.__dict__[attr] = (key, None)
+        return None
+    n = lib.fetode_wide_layer_plan_bytes(kp, fp)
+    plan = torch.empty(max(1, n // 4), device=device, dtype=torch.float32)
+    _lib.check(lib.fetode_wide_layer_plan_build(kp, fp, plan.data_ptr(), _lib.stream_handle(device)),
+               "fetode_wide_layer_plan_build")
+    entry = (plan, kd, fd, keep)
+    owner.__dict__[attr] = (key, entry)
+    return entry
+
+
+def wide_apply(kan, fer, x, reinit: bool = False):
+    """out = KANLinear(x) + Ferro(x) (either may be None) through fetode_wide_layer_forward, or None
+    if the layer has no wide kernel.  Reads the Ferro module's prev_x; the caller commits the new
+    state (ferro_class.py:409)."""
+    B = x.shape[0]
+    dev = x.device
+    if fer is not None:
+        width = fer.in_dim
+        outf = fer.out_dim
+    else:
+        width, outf = kan.in_features, kan.out_features
+    if width < 16 or outf < 16:
+        return None
+    entry = wide_plan(kan, fer, dev)
+    if entry is None:
+        return None
+    plan, kd, fd, _ = entry
+    prev = None
+    if fer is not None and not reinit:
+        prev = fer._prev
+        if prev.shape != (B, width) or not prev.is_contiguous():
+            prev = prev.contiguous()
+    out = torch.empty(B, outf, device=dev, dtype=torch.float32)
+    lib = _lib.load()
+    _lib.check(lib.fetode_wide_layer_forward(
+        _lib.ctypes.byref(kd) if kd is not None else None, _lib.ctypes.byref(fd) if fd is not None else None,
+        plan.data_ptr(), x.data_ptr(), B, _lib.ptr(prev), int(reinit), out.data_ptr(), _stream(x)),
+        "fetode_wide_layer_forward")
     return out

@@ -807,9 +807,9 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       const float pv = fgate[s] ? (re0 ? x : (fx[s] ? pv0b : pv0a)) : 0.f;
       const float e = ex2(ffma(fna[s], x - pv, fab[s]));
       const float sg = rcp(1.0f + e);
-      float v = ffma(sg, fsilu[s] ? x : fmul[s], fadd[s]);
+      const float v = ffma(sg, fsilu[s] ? x : fmul[s], fadd[s]);
+      acc = ffma(fw[s], v, acc);  // gate / exp jobs carry weight 0: MAC the finite v, never e (inf * 0)
       fv[s] = fexp[s] ? e : v;
-      acc = ffma(fw[s], fv[s], acc);
     }
     if constexpr (FERRO) {
       // gate_i / exp_i of the two inputs: slot 1, lanes 6..9 of every row (row_newbcast)
@@ -849,9 +849,9 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       const float e = ex2(ffma(hna, h - pv, hab));
       const float sg = rcp(1.0f + e);
       float v = ffma(sg, hsilu ? h : hmul, hadd);
-      v = hexp ? e : v;
-      acc0 = hw0 * v;
+      acc0 = hw0 * v;  // weight 0 on the gate / exp lanes: MAC the finite v before it becomes e
       acc1 = hw1 * v;
+      v = hexp ? e : v;
       if constexpr (FERRO) {
         const float gt = dpp<0x15B>(v), ee = dpp<0x15C>(v);  // row_newbcast:11 / :12
         const f2 pr = v4_pair<F_>(make_float4(h, gt, ee, 0.f), ep1, k21, kE1, cp1, splat(0.0f), a.P1.gsl2e);
@@ -1045,7 +1045,7 @@ const FusedEntry kFused[] = {
 // only.  FETODE_SMALL_MAX overrides the switch point (diagnostics / tuning).
 int64_t g_small_max = [] {
   const char* e = getenv("FETODE_SMALL_MAX");
-  return e ? (int64_t)atoll(e) : (int64_t)2048;
+  return e ? (int64_t)atoll(e) : (int64_t)512;  // measured switch point (tools/diag/batch_sweep.py)
 }();
 int64_t small_max() { return g_small_max; }
 

@@ -1,0 +1,431 @@
+// fetode_wide.hip — one KAN-FET layer at production widths (64..128 in / out) in ONE launch:
+//   out[b, o] = KANLinear(x)[b, o] + FerroelectricBasis(x)[b, o]          (KANFET layer, A9)
+// or either half alone (KANLinear.forward / FerroelectricBasis.forward with the constant
+// branch_sign, no activations).  BASELINE configs[3] runs KANFET([64, 128, 64], K = 10) this way,
+// two launches per field evaluation (train_kan_fet_ett.py:136-197 with the KAN-FET field;
+// efficientkan.py:160-182; ferro_class.py:368-420).
+//
+// Workgroup = 4 waves = a tile of 64 rows x 16 outputs; the inputs are walked in chunks of kCh:
+//   staging   one (row, input) item per thread: the hysteresis gate w = -2(1-alpha)(1-sigma(gs(x -
+//             prev))) and e = e^{gs x} for the Ferro elements, and the 20 KAN features (SiLU, the 8
+//             cubic B-spline bases by the reference's Cox-de Boor, 10 logistic bases) into LDS;
+//   Ferro     wave w owns outputs 4w..4w+3 for all 64 rows (lane = row), so every Ferro parameter
+//             is wave-uniform (scalar loads, SGPR operands): per element
+//               s = 1/(1 + e P),  m = 1 + w s,  z = 2 log2e k (x + Ec m),  th = 1 - 2/(1 + 2^z)
+//             (P = e^{gs Ec} packed once; branch_sign = 1 makes the crossing gate cp drop out, as in
+//             the fused LV kernel), 7 VALU + 3 transcendental instructions;
+//   KAN       the (64 x 16) x (in * 20) contraction on v_mfma_f32_16x16x4_f32: wave w owns rows
+//             16w..16w+15, A = the staged features (LDS, pitch = 2 mod 32: conflict-free), B = the
+//             packed weights (global, L2-resident, loaded at the chunk start).
+// Epilogue: the Ferro sums (lane = row) meet the MFMA tile (lane = column) in LDS.
+//
+// Direct form: a wave whose chunk input has |gs x| > 80 anywhere, or whose (output, input) has
+// |gs Ec| > 80, evaluates s = 1/(1 + 2^{gs log2e (x + Ec)}) with one more exponential (the
+// product e P could overflow a factor there).
+#include <algorithm>
+
+#include "fetode_common.h"
+
+using namespace fetode;
+
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWF = 20;       // KAN features per input: SiLU, B_0..B_7, phi_0..phi_9, 0
+constexpr int kNS = 8, kNB = 10, kNG = 12;
+constexpr int kRows = 64, kOuts = 16, kCh = 4, kThreads = 256;
+constexpr int kPitch = kCh * kWF + 18;  // 98 = 2 (mod 32): MFMA A-operand reads are conflict-free
+
+// packed plan of one layer (offsets in floats)
+struct WideLayout {
+  int in, out, K;
+  bool kan, ferro;
+  int64_t fe4;     // (out, in, K) float4 {P = 2^{gs log2e Ec}, 2 log2e k, 2 log2e k Ec, coef Ps}
+  int64_t gec;     // (out, in, K) gs log2e Ec (direct form)
+  int64_t dflag;   // (out, in) 1 if some |gs Ec| > 80 for (o, i)
+  int64_t fconst;  // (out) sum_{i,k} coef bias
+  int64_t wp;      // (in, 20, out) packed KAN weights
+  int64_t lg;      // (in, NB, 2) (-a log2e, a b log2e)
+  int64_t knots;   // (in, 12) knot grid (efficientkan.py:55-61 buffer)
+  int64_t rh;      // (in, 11) 1 / (g[m+1] - g[m])
+  int64_t bt;      // (in, 12, 8) float4: basis c on knot interval m as a cubic in u (m = 11: zero)
+  int64_t end;
+  float gsl2e, gs, wc;
+};
+
+WideLayout wide_layout(const fetode_kanlinear_t* kl, const fetode_ferro_t* fl) {
+  WideLayout L{};
+  L.kan = kl != nullptr;
+  L.ferro = fl != nullptr;
+  L.in = kl ? kl->in_features : fl->in_dim;
+  L.out = kl ? kl->out_features : fl->out_dim;
+  L.K = fl ? fl->num_basis : 0;
+  int64_t o = 0;
+  if (L.ferro) {
+    const int64_t NE = (int64_t)L.out * L.in * L.K;
+    L.fe4 = o; o += 4 * NE;
+    L.gec = o; o += NE;
+    L.dflag = o; o += (int64_t)L.out * L.in;
+  }
+  L.fconst = o; o += L.out;
+  o = (o + 3) & ~int64_t(3);
+  if (L.kan) {
+    L.wp = o; o += (int64_t)L.in * kWF * L.out;
+    L.lg = o; o += (int64_t)L.in * kNB * 2;
+    L.knots = o; o += (int64_t)L.in * kNG;
+    L.rh = o; o += (int64_t)L.in * (kNG - 1);
+    o = (o + 3) & ~int64_t(3);
+    L.bt = o; o += (int64_t)L.in * kNG * kNS * 4;
+  }
+  L.end = (o + 3) & ~int64_t(3);
+  L.gs = fl ? (float)fl->gate_slope : 0.f;
+  L.gsl2e = L.gs * FETODE_LOG2E;
+  L.wc = fl ? -2.0f * (float)(1.0 - fl->alpha) : 0.f;
+  return L;
+}
+
+bool wide_supported(const fetode_kanlinear_t* kl, const fetode_ferro_t* fl) {
+  if (!kl && !fl) return false;
+  if (kl && (kl->grid_size != 5 || kl->spline_order != 3 || kl->num_logistic != kNB || !kl->grid || !kl->base_weight ||
+             !kl->spline_weight || !kl->logistic_a || !kl->logistic_b || !kl->logistic_weight))
+    return false;
+  if (fl && (fl->num_basis != 10 && fl->num_basis != 12)) return false;
+  if (fl && (fl->branch_sign || !fl->k || !fl->Ec || !fl->Ps || !fl->bias || !fl->coef)) return false;
+  if (kl && fl && (kl->in_features != fl->in_dim || kl->out_features != fl->out_dim)) return false;
+  const int in = kl ? kl->in_features : fl->in_dim, out = kl ? kl->out_features : fl->out_dim;
+  return in >= 16 && out >= 16 && out % kOuts == 0 && in % kCh == 0;
+}
+
+// ---- packing (once per parameter version) ------------------------------------------------------
+// Cox-de Boor (efficientkan.py:117-131) in fp64 restricted to knot interval m: the cubic bases
+// B_{m-3..m} that are non-zero on [g_m, g_{m+1}) at x.
+__device__ void bases_on_interval(double x, int m, const float* g, double* N) {
+  constexpr int SO = 3;
+  for (int r = 0; r < SO + 2; ++r) N[r] = 0.0;
+  N[SO] = 1.0;
+  for (int k = 1; k <= SO; ++k) {
+    double M[SO + 2];
+    for (int r = 0; r < SO + 2; ++r) M[r] = 0.0;
+    for (int r = SO - k; r <= SO; ++r) {
+      const int j = m - SO + r;
+      if (j >= 0 && j <= kNG - 2 - k) {
+        const double left = (x - g[j]) / ((double)g[j + k] - g[j]) * N[r];
+        const double right = ((double)g[j + k + 1] - x) / ((double)g[j + k + 1] - g[j + 1]) * N[r + 1];
+        M[r] = left + right;
+      }
+    }
+    for (int r = 0; r < SO + 2; ++r) N[r] = M[r];
+  }
+}
+
+__global__ void wide_pack_kernel(fetode_kanlinear_t kl, fetode_ferro_t fl, WideLayout L, float* __restrict__ plan) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int in = L.in, out = L.out, K = L.K;
+  const float l2 = FETODE_LOG2E;
+  if (L.ferro && t < (int64_t)out * in * K) {
+    const int o = (int)(t / ((int64_t)in * K)), r = (int)(t % ((int64_t)in * K)), i = r / K, k = r % K;
+    const int src = (i * out + o) * K + k;  // reference layout (in, out, K)
+    const float kk = fl.k[src], Ec = fl.Ec[src], Ps = fl.Ps[src], co = fl.coef[src];
+    const float gec = L.gsl2e * Ec;
+    const float k2 = 2.0f * l2 * kk;
+    float* d = plan + L.fe4 + 4 * t;
+    d[0] = ex2(gec);
+    d[1] = k2;
+    d[2] = k2 * Ec;
+    d[3] = co * Ps;
+    plan[L.gec + t] = gec;
+  }
+  if (L.ferro && t < (int64_t)out * in) {
+    const int o = (int)(t / in), i = (int)(t % in);
+    float f = 0.f;
+    for (int k = 0; k < K; ++k) f = fabsf(L.gs * fl.Ec[(i * out + o) * K + k]) > 80.0f ? 1.0f : f;
+    plan[L.dflag + t] = f;
+  }
+  if (L.kan && t < (int64_t)in * kWF * out) {
+    const int o = (int)(t % out), f = (int)((t / out) % kWF), i = (int)(t / ((int64_t)out * kWF));
+    float v = 0.f;
+    if (f == 0) {
+      v = kl.base_weight[(int64_t)o * in + i];
+    } else if (f <= kNS) {
+      const float sc = kl.spline_scaler ? kl.spline_scaler[(int64_t)o * in + i] : 1.0f;
+      v = kl.spline_weight[((int64_t)o * in + i) * kNS + (f - 1)] * sc;
+    } else if (f <= kNS + kNB) {
+      const float ls = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
+      // phi = 2 sigma(a (x - b)) (efficientkan.py:24): the 2 lives in the weight
+      v = 2.0f * ((kl.logistic_weight[(int64_t)o * (in * kNB) + i * kNB + (f - 1 - kNS)] * kl.scale_logistic) * ls);
+    }
+    plan[L.wp + t] = v;
+  }
+  if (L.kan && t < (int64_t)in * kNB) {
+    const float a = kl.logistic_a[t], b = kl.logistic_b[t];
+    plan[L.lg + 2 * t + 0] = -a * l2;
+    plan[L.lg + 2 * t + 1] = (a * b) * l2;
+  }
+  if (L.kan && t < (int64_t)in * kNG) {
+    const int i = (int)(t / kNG), j = (int)(t % kNG);
+    const float* g = kl.grid + (int64_t)i * kNG;
+    plan[L.knots + t] = g[j];
+    if (j < kNG - 1) plan[L.rh + (int64_t)i * (kNG - 1) + j] = 1.0f / (g[j + 1] - g[j]);
+    // basis table of interval m = j: the 8 bases as cubics in u = (x - g_m) / (g_{m+1} - g_m),
+    // fitted in fp64 through u = 0, 1/3, 2/3, 1 (exact: each basis is a cubic on the interval)
+    float* d = plan + L.bt + ((int64_t)i * kNG + j) * kNS * 4;
+    for (int c = 0; c < kNS * 4; ++c) d[c] = 0.f;
+    if (j < kNG - 1) {
+      const double h = (double)g[j + 1] - g[j];
+      double v[4][kNS];
+      for (int q = 0; q < 4; ++q) {
+        for (int c = 0; c < kNS; ++c) v[q][c] = 0.0;
+        double N[5];
+        bases_on_interval(g[j] + h * (q / 3.0), j, g, N);
+        for (int r = 0; r <= 3; ++r) {
+          const int c = j - 3 + r;
+          if (c >= 0 && c < kNS) v[q][c] = N[r];
+        }
+      }
+      for (int c = 0; c < kNS; ++c) {
+        d[4 * c + 0] = (float)v[0][c];
+        d[4 * c + 1] = (float)((-11.0 * v[0][c] + 18.0 * v[1][c] - 9.0 * v[2][c] + 2.0 * v[3][c]) / 2.0);
+        d[4 * c + 2] = (float)(9.0 * (2.0 * v[0][c] - 5.0 * v[1][c] + 4.0 * v[2][c] - v[3][c]) / 2.0);
+        d[4 * c + 3] = (float)(9.0 * (-v[0][c] + 3.0 * v[1][c] - 3.0 * v[2][c] + v[3][c]) / 2.0);
+      }
+    }
+  }
+}
+
+// per-output constant sum_{i,k} coef * bias: one wave per output, fixed order
+__global__ void wide_const_kernel(fetode_ferro_t fl, WideLayout L, float* __restrict__ plan) {
+  const int o = blockIdx.x, lane = threadIdx.x;
+  float s = 0.f;
+  if (L.ferro)
+    for (int p = lane; p < L.in * L.K; p += 64) {
+      const int i = p / L.K, k = p % L.K;
+      const int src = (i * L.out + o) * L.K + k;
+      s += fl.coef[src] * fl.bias[src];
+    }
+  for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (lane == 0) plan[L.fconst + o] = s;
+}
+
+struct WideArgs {
+  const float* plan;
+  WideLayout L;
+  const float* x;
+  const float* prev;
+  const float* grid;  // (in, 12) knots
+  int64_t B;
+  int reinit;
+  float* out;
+};
+
+// ---- the layer --------------------------------------------------------------------------------
+template <int K, bool KAN, bool FERRO>
+__global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
+  constexpr int KP = FERRO ? K : 1;
+  __shared__ float s_x[kCh * kRows], s_w[kCh * kRows], s_e[kCh * kRows];
+  __shared__ float4 s_par[kOuts * kCh * KP];  // the chunk's Ferro constants, read as wave broadcasts
+  __shared__ float s_dfl[kOuts * kCh];
+  // KAN features of the chunk (MFMA A operand); the epilogue reuses the space for the Ferro sums
+  constexpr int kPhi = KAN ? kRows * kPitch : 0, kFer = kRows * (kOuts + 1);
+  __shared__ __attribute__((aligned(16))) float s_phi[kPhi > kFer ? kPhi : kFer];
+  float* s_fer = s_phi;
+  const WideLayout& L = a.L;
+  const int in = L.in, out = L.out;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t b0 = (int64_t)blockIdx.x * kRows;
+  const int o0 = blockIdx.y * kOuts;
+  const float* __restrict__ plan = a.plan;
+  const float gs = L.gs, gsl2e = L.gsl2e, wc = L.wc, l2 = FETODE_LOG2E;
+
+  float facc[4] = {0.f, 0.f, 0.f, 0.f};  // Ferro: row = lane, output o0 + 4w + j
+  f32x4 kacc = {0.f, 0.f, 0.f, 0.f};     // KAN: rows 16w + 4 (lane >> 4) + v, column lane & 15
+  const int kr = lane & 15, kq = lane >> 4;
+
+  // staging item of this thread: row sr, chunk input si
+  const int sr = tid >> 2, si = tid & 3;
+  const int64_t sb = b0 + sr;
+  const bool slive = sb < a.B;
+
+  for (int i0 = 0; i0 < in; i0 += kCh) {
+    // KAN weights of this chunk for the MFMA B operand (L2-resident; issued before the staging)
+    float wb[KAN ? kCh * 5 : 1];
+    if constexpr (KAN) {
+#pragma unroll
+      for (int ii = 0; ii < kCh; ++ii)
+#pragma unroll
+        for (int s = 0; s < 5; ++s)
+          wb[ii * 5 + s] = plan[L.wp + ((int64_t)(i0 + ii) * kWF + 4 * s + kq) * out + o0 + kr];
+    }
+    __syncthreads();  // the previous chunk is consumed
+    const float x = slive ? a.x[sb * in + i0 + si] : 0.f;
+    if constexpr (FERRO) {
+      const float pv = a.reinit ? x : (slive ? a.prev[sb * in + i0 + si] : 0.f);
+      // is_moving_up = sigmoid(gate_slope (x - prev_x)) (ferro_class.py:387), w = wc (1 - up)
+      const float up = rcp(1.0f + ex2(-gsl2e * (x - pv)));
+      s_x[si * kRows + sr] = x;
+      s_w[si * kRows + sr] = wc * (1.0f - up);
+      s_e[si * kRows + sr] = ex2(gsl2e * x);
+      const float4* fe = reinterpret_cast<const float4*>(plan + L.fe4);
+      for (int idx = tid; idx < kOuts * kCh * K; idx += kThreads) {
+        const int j = idx / (kCh * K), r = idx - j * (kCh * K);
+        s_par[idx] = fe[((int64_t)(o0 + j) * in + i0) * K + r];   // (ii, k) contiguous per output
+      }
+      if (tid < kOuts * kCh) s_dfl[tid] = plan[L.dflag + (int64_t)(o0 + tid / kCh) * in + i0 + tid % kCh];
+    }
+    if constexpr (KAN) {
+      const int i = i0 + si;
+      float f[kWF];
+      f[0] = x * rcp(1.0f + ex2(-x * l2));  // SiLU (efficientkan.py:166)
+      // cubic B-spline bases (efficientkan.py:117-131): knot interval m by the half-open order-0
+      // indicator, then the 8 bases as cubics of u from the fp64-fitted table (zero outside the grid)
+      const float* g = plan + L.knots + (int64_t)i * kNG;
+      int m = -1;
+#pragma unroll
+      for (int j = 0; j < kNG; ++j) m += (x >= g[j]) ? 1 : 0;
+      const bool fin = __builtin_isfinite(x);
+      const int mi = ((unsigned)m < (unsigned)(kNG - 1) && fin) ? m : kNG - 1;
+      const float u = mi < kNG - 1 ? (x - g[mi]) * plan[L.rh + (int64_t)i * (kNG - 1) + mi] : 0.f;
+      const float4* bt = reinterpret_cast<const float4*>(plan + L.bt) + ((int64_t)i * kNG + mi) * kNS;
+#pragma unroll
+      for (int c = 0; c < kNS; ++c) {
+        const float4 cf = bt[c];
+        f[1 + c] = fin ? ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x) : __builtin_nanf("");
+      }
+      const float* lg = plan + L.lg + (int64_t)i * kNB * 2;
+#pragma unroll
+      for (int j = 0; j < kNB; ++j) f[1 + kNS + j] = rcp(1.0f + ex2(ffma(lg[2 * j], x, lg[2 * j + 1])));
+      f[kWF - 1] = 0.f;
+      float* d = &s_phi[sr * kPitch + si * kWF];
+#pragma unroll
+      for (int q = 0; q < kWF; q += 2) *reinterpret_cast<float2*>(d + q) = make_float2(f[q], f[q + 1]);
+    }
+    __syncthreads();
+    if constexpr (KAN) {
+      const float* arow = &s_phi[(16 * w + kr) * kPitch + kq];
+#pragma unroll
+      for (int ii = 0; ii < kCh; ++ii)
+#pragma unroll
+        for (int s = 0; s < 5; ++s)
+          kacc = __builtin_amdgcn_mfma_f32_16x16x4f32(arow[ii * kWF + 4 * s], wb[ii * 5 + s], kacc, 0, 0, 0);
+    }
+    if constexpr (FERRO) {
+#pragma unroll 1
+      for (int ii = 0; ii < kCh; ++ii) {
+        const int i = i0 + ii;
+        const float xv = s_x[ii * kRows + lane], wg = s_w[ii * kRows + lane], e = s_e[ii * kRows + lane];
+        const bool xbig = __any(fabsf(gs * xv) > 80.0f);  // wave-uniform
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int jo = 4 * w + j;
+          const float4* par = &s_par[(jo * kCh + ii) * K];
+          float acc = 0.f;
+          if (!xbig && s_dfl[jo * kCh + ii] == 0.f) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              const float4 p = par[k];  // {P, k2, k2Ec, cps}, same address on every lane
+              const float sg = rcp(ffma(e, p.x, 1.0f));
+              const float mm = ffma(wg, sg, 1.0f);
+              const float z = ffma(p.z, mm, p.y * xv);
+              const float th = ffma(-2.0f, rcp(ex2(z) + 1.0f), 1.0f);
+              acc = ffma(p.w, th, acc);
+            }
+          } else {
+            const float* gec = plan + L.gec + ((int64_t)(o0 + jo) * in + i) * K;
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+              const float4 p = par[k];
+              const float sg = rcp(1.0f + ex2(ffma(gsl2e, xv, gec[k])));
+              const float mm = ffma(wg, sg, 1.0f);
+              const float z = ffma(p.z, mm, p.y * xv);
+              const float th = ffma(-2.0f, rcp(ex2(z) + 1.0f), 1.0f);
+              acc = ffma(p.w, th, acc);
+            }
+          }
+          facc[j] += acc;  // K bases of one input first, then inputs (the reference's two-level sum)
+        }
+      }
+    }
+  }
+  // epilogue: Ferro sums (+ sum coef bias) meet the KAN tile in LDS (s_phi's space)
+  __syncthreads();
+  if constexpr (FERRO) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s_fer[lane * (kOuts + 1) + 4 * w + j] = facc[j] + plan[L.fconst + o0 + 4 * w + j];
+  }
+  __syncthreads();
+  if constexpr (KAN) {
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int r = 16 * w + 4 * kq + v;
+      const int64_t b = b0 + r;
+      if (b < a.B) a.out[b * out + o0 + kr] = FERRO ? kacc[v] + s_fer[r * (kOuts + 1) + kr] : kacc[v];
+    }
+  } else {
+    for (int t = tid; t < kRows * kOuts; t += kThreads) {
+      const int r = t / kOuts, c = t % kOuts;
+      const int64_t b = b0 + r;
+      if (b < a.B) a.out[b * out + o0 + c] = s_fer[r * (kOuts + 1) + c];
+    }
+  }
+}
+
+typedef void (*wide_fn)(WideArgs);
+wide_fn pick(int K, bool kan, bool ferro) {
+  if (kan && !ferro) return wide_layer_kernel<10, true, false>;
+  if (K == 12) return kan ? wide_layer_kernel<12, true, true> : wide_layer_kernel<12, false, true>;
+  return kan ? wide_layer_kernel<10, true, true> : wide_layer_kernel<10, false, true>;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fetode_wide_layer_supported(const fetode_kanlinear_t* kl, const fetode_ferro_t* fl) {
+  return wide_supported(kl, fl) ? 1 : 0;
+}
+
+int64_t fetode_wide_layer_plan_bytes(const fetode_kanlinear_t* kl, const fetode_ferro_t* fl) {
+  if (!wide_supported(kl, fl)) return -1;
+  return wide_layout(kl, fl).end * (int64_t)sizeof(float);
+}
+
+int fetode_wide_layer_plan_build(const fetode_kanlinear_t* kl, const fetode_ferro_t* fl, void* plan, void* stream) {
+  if (!wide_supported(kl, fl)) return set_err(FETODE_EUNSUPPORTED, "wide layer: unsupported shape / parameters");
+  if (!plan) return set_err(FETODE_EINVAL, "wide layer: null plan");
+  const WideLayout L = wide_layout(kl, fl);
+  const fetode_kanlinear_t k0 = kl ? *kl : fetode_kanlinear_t{};
+  const fetode_ferro_t f0 = fl ? *fl : fetode_ferro_t{};
+  const int64_t n = std::max<int64_t>({(int64_t)L.out * L.in * std::max(L.K, 1), (int64_t)L.in * kWF * L.out});
+  const hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(wide_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, k0, f0, L, (float*)plan);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(wide_const_kernel, dim3((unsigned)L.out), dim3(64), 0, s, f0, L, (float*)plan);
+  LAUNCH_CHECK();
+  return FETODE_OK;
+}
+
+int fetode_wide_layer_forward(const fetode_kanlinear_t* kl, const fetode_ferro_t* fl, const void* plan, const float* x,
+                              int64_t B, const float* prev, int32_t reinit, float* out, void* stream) {
+  if (!wide_supported(kl, fl)) return set_err(FETODE_EUNSUPPORTED, "wide layer: unsupported shape / parameters");
+  if (B <= 0) return FETODE_OK;
+  if (!plan || !x || !out || (fl && !reinit && !prev)) return set_err(FETODE_EINVAL, "wide layer: null pointer");
+  if (x == out) return set_err(FETODE_EINVAL, "wide layer: out must not alias x");
+  WideArgs a;
+  a.plan = (const float*)plan;
+  a.L = wide_layout(kl, fl);
+  a.x = x;
+  a.prev = prev;
+  a.grid = kl ? kl->grid : nullptr;
+  a.B = B;
+  a.reinit = reinit;
+  a.out = out;
+  const int64_t tiles = (B + kRows - 1) / kRows;
+  if (tiles > 0x7fffffff) return set_err(FETODE_EINVAL, "wide layer: batch too large");
+  hipLaunchKernelGGL(pick(a.L.K, a.L.kan, a.L.ferro), dim3((unsigned)tiles, (unsigned)(a.L.out / kOuts)), dim3(kThreads), 0,
+                     (hipStream_t)stream, a);
+  LAUNCH_CHECK();
+  return FETODE_OK;
+}
+
+}  // extern "C"

@@ -106,7 +106,7 @@ int32_t fetode_state_width(const fetode_field_t* field);
 /* 1 if a fused (single-launch) integrator kernel exists for this field shape. */
 int fetode_fused_supported(const fetode_field_t* field);
 
-/* Kernel choice of the fused integrator: batches B <= this value (default 2048, env
+/* Kernel choice of the fused integrator: batches B <= this value (default 512, env
  * FETODE_SMALL_MAX) take the small-batch kernel (one trajectory per 3-wave workgroup: the
  * strong-scaling shard size), larger ones and every training tape the two-trajectories-per-wave
  * kernel.  Sets the value when b >= 0; returns the previous one.  Process-wide tuning knob. */
@@ -133,6 +133,23 @@ int fetode_integrate_fixed(const fetode_field_t* field, const void* plan, int32_
                            const int32_t* out_step, const int32_t* out_mode, const float* out_slope,
                            int32_t T, float* solution, float* state, uint32_t init_mask,
                            float* tape, void* stream);
+
+/* One KAN-FET layer at production widths in ONE launch (ETT KANFET[64,128,64], ECG FerroNet):
+ *   out = KANLinear(x) + FerroelectricBasis(x)   (layer = KANFETLayer), or either
+ *   half alone (layer / ferro NULL) — efficientkan.py:160-182, ferro_class.py:368-420 with the
+ *   constant branch_sign and no activations.  Supported: grid_size 5, spline_order 3, 10 logistic
+ *   bases; Ferro K = 10 or 12; in >= 16, in % 4 == 0, out % 16 == 0 (fetode_wide_layer_supported).
+ *   The plan (fetode_wide_layer_plan_bytes, built once per parameter version) packs the Ferro
+ *   constants and the KAN weights for the MFMA contraction.  prev (B, in) is read (ignored when
+ *   reinit); the caller stores the new prev_x = x afterwards (ferro_class.py:409).  out must not
+ *   alias x.  Replaces: KANFETLayer.forward / KANLinear.forward / FerroelectricBasis.forward. */
+int fetode_wide_layer_supported(const fetode_kanlinear_t* layer, const fetode_ferro_t* ferro);
+int64_t fetode_wide_layer_plan_bytes(const fetode_kanlinear_t* layer, const fetode_ferro_t* ferro);
+int fetode_wide_layer_plan_build(const fetode_kanlinear_t* layer, const fetode_ferro_t* ferro, void* plan,
+                                 void* stream);
+int fetode_wide_layer_forward(const fetode_kanlinear_t* layer, const fetode_ferro_t* ferro, const void* plan,
+                              const float* x, int64_t B, const float* prev, int32_t reinit, float* out,
+                              void* stream);
 
 /* Standalone module kernels (generic widths). */
 /* KANLinear.forward (efficientkan.py:160-182): x (B,in) -> out (B,out). */
