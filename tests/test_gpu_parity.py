@@ -388,8 +388,8 @@ def test_small_batch_kernel_matches_v4(dev, kernel_switch, B, method):
             outs.append(F.odeint(F.autonomous(m), y0, t, method=method).cpu())
         states.append([l.ferro._prev.cpu() for l in m.layers])
     assert slice_rel_err(outs[0], outs[1]) <= 1e-5
-    for a, b in zip(*states):   # layer-1 state = hidden h (sums with cancellation): 1e-4
-        assert torch.allclose(a, b, rtol=1e-4, atol=1e-5)
+    for a, b in zip(*states):   # layer-1 state = hidden h (sums with cancellation): 1e-4 normwise
+        assert ((a - b).norm() / b.norm()).item() <= 1e-4
     if method == "rk4":
         gk = load_golden("traj_kan")
         for small in (True, False):
