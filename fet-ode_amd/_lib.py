@@ -73,6 +73,11 @@ SIGNATURES = {
     "fetode_state_width": (ctypes.c_int32, [ctypes.POINTER(FieldDesc)]),
     "fetode_fused_supported": (ctypes.c_int, [ctypes.POINTER(FieldDesc)]),
     "fetode_fused_set_small_batch_max": (ctypes.c_int64, [ctypes.c_int64]),
+    "fetode_integrate_dopri5": (ctypes.c_int, [ctypes.POINTER(FieldDesc), _vp, _vp, ctypes.c_int64, _vp,
+                                               ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+                                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_float), _vp,
+                                               _vp, ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_int32, _vp]),
+    "fetode_integrate_dopri5_workspace": (ctypes.c_int64, [ctypes.c_int64]),
     "fetode_wide_layer_supported": (ctypes.c_int, [ctypes.POINTER(KANLinearDesc), ctypes.POINTER(FerroDesc)]),
     "fetode_wide_layer_plan_bytes": (ctypes.c_int64, [ctypes.POINTER(KANLinearDesc), ctypes.POINTER(FerroDesc)]),
     "fetode_wide_layer_plan_build": (ctypes.c_int, [ctypes.POINTER(KANLinearDesc), ctypes.POINTER(FerroDesc), _vp, _vp]),

@@ -57,6 +57,117 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 
 namespace {
 
+// Device-resident dopri5 (torchdiffeq Dopri5Solver, the default method of every reference odeint
+// without `method`, train_kanfet_node_predprey.py:252): the control arithmetic of the host-driven
+// path (fet-ode_amd/dopri5.py _Dopri5 with fetode_lincomb / fetode_scaled_rms / fetode_interp_*).
+struct DopriParams {
+  int32_t on;
+  const double* t;  // (T) output times, fp64, strictly increasing
+  int32_t T;
+  float rtol, atol;
+  double first_step, safety, ifactor, dfactor, min_step, max_step;
+  int32_t max_steps;
+  float beta[6][6], cerr[7], cmid[7];  // tableau in fp32 (RKAdaptiveStepsizeODESolver casts it to y0's dtype)
+  unsigned* bar;    // grid-reduction words (zeroed before the launch)
+  double* slot;     // (grid, 2) per-workgroup partial sums
+  double* xs;       // (8, 2) per-XCD-group sums
+  double* tot;      // (2) the total
+  int32_t* stats;   // nfev, attempts, status
+  double* att;      // (max_att, 4): t0, dt, error ratio, accepted
+  int32_t max_att;
+};
+
+// Grid-wide sum of two fp64 values, one per workgroup (valid on every lane of a one-wave
+// workgroup), returned to every workgroup in the same fixed summation order: each workgroup
+// stores its partial and arrives on the counter of its group (blockIdx % 8); the group's last
+// arriver sums the group's partials (lane-strided, xor tree) and arrives on the top counter; the
+// last of those sums the group sums in group order, publishes the total and bumps the generation
+// every workgroup polls.  Release before each arrival, acquire after the poll; all shared words
+// through agent-scope atomics (MI355X_MICROARCH.md, inter-workgroup visibility).  Every spin is
+// bounded: after ~1 s the abort word is raised and every later reduction returns at once (the
+// grid was not co-resident); the caller reports status 4.
+constexpr unsigned kDpSpinLimit = 1u << 20;
+constexpr int kDpBarWords = 64 * 10;
+__device__ bool grid_sum2(const DopriParams& P, double v0, double v1, double& s0, double& s1) {
+  const unsigned blk = blockIdx.x, nblk = gridDim.x, x = blk & 7u;
+  const unsigned nx = (nblk + 7u - x) / 8u, ngrp = nblk < 8u ? nblk : 8u;
+  unsigned* cnt = P.bar + 64 * x;
+  unsigned* top = P.bar + 64 * 8;
+  unsigned* gen = P.bar + 64 * 9;
+  unsigned* abw = gen + 1;
+  const int lane = threadIdx.x & 63;
+  int ab = 0, leader = 0;
+  unsigned g = 0;
+  if (lane == 0) {
+    ab = __hip_atomic_load(abw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (!ab) {
+      g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&P.slot[2 * blk], v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&P.slot[2 * blk + 1], v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      leader = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nx - 1u;
+    }
+  }
+  ab = __shfl(ab, 0);
+  leader = __shfl(leader, 0);
+  if (!ab && leader) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    double a0 = 0.0, a1 = 0.0;
+    for (unsigned j = lane; j < nx; j += 64) {
+      const unsigned bb = x + 8u * j;
+      a0 += __hip_atomic_load(&P.slot[2 * bb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      a1 += __hip_atomic_load(&P.slot[2 * bb + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      a0 += __shfl_xor(a0, o);
+      a1 += __shfl_xor(a1, o);
+    }
+    if (lane == 0) {
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&P.xs[2 * x], a0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&P.xs[2 * x + 1], a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == ngrp - 1u) {
+        __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        double t0 = 0.0, t1 = 0.0;
+        for (unsigned u = 0; u < ngrp; ++u) {
+          t0 += __hip_atomic_load(&P.xs[2 * u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          t1 += __hip_atomic_load(&P.xs[2 * u + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __hip_atomic_store(&P.tot[0], t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&P.tot[1], t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+  }
+  double r0 = 0.0, r1 = 0.0;
+  if (lane == 0 && !ab) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+      __builtin_amdgcn_s_sleep(1);
+      if (__hip_atomic_load(abw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        ab = 1;
+        break;
+      }
+      if (++spins == kDpSpinLimit) {
+        __hip_atomic_store(abw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ab = 1;
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    r0 = __hip_atomic_load(&P.tot[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    r1 = __hip_atomic_load(&P.tot[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  ab = __shfl(ab, 0);
+  s0 = __shfl(r0, 0);
+  s1 = __shfl(r1, 0);
+  return ab != 0;
+}
+
 struct FusedArgs {
   const float* plan;
   LayerPlan P0, P1;
@@ -76,6 +187,7 @@ struct FusedArgs {
   int32_t single_eval;  // 1: eval_out = field(y0) once (fetode_field_forward)
   float* eval_out;
   float factor_limit;   // kFactorLimit (FETODE_FACTOR_LIMIT=-1 disables the factored gate: diagnostics)
+  DopriParams dp;       // dp.on: the whole dopri5 solve in this launch (fetode_integrate_dopri5)
 };
 
 // ---- cross-lane helpers (DPP) -------------------------------------------------------------
@@ -179,7 +291,7 @@ __device__ __forceinline__ float v4_edges(const V4Lds<IN, FLEN>& L, const float*
 
 // HOT = true: the rk4 (3/8) integrate path only, every stage inlined, outputs predicated;
 // HOT = false: single evaluations and every other method.
-template <int H, int K_, int NB, int NG, bool FERRO, bool HOT>
+template <int H, int K_, int NB, int NG, bool FERRO, bool HOT, bool DOPRI = false>
 __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
   constexpr int D = 2, NI = NG - 1, NFL = 1 + NB, NFP = (NFL + 1) & ~1, K = FERRO ? K_ : 0;
   // feature jobs: logistic 0..NB-1, SiLU, [gate, exp(gs x)], then x / u / m stores
@@ -583,7 +695,135 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
       if (fact) return eval_body(xin, FT{});
       return eval_body(xin, FF{});
     };
-    if (a.single_eval) {
+    if constexpr (DOPRI) {
+      // ---- device-resident dopri5 (dopri5.py _Dopri5, lane (traj, dim = row) carries y_row) ----
+      const DopriParams& P = a.dp;
+      const bool real = valid && c1 == 0;  // one lane per (trajectory, state dim) in the sums
+      const double n_el = (double)(a.B * D);
+      int nfev = 0, n_att = 0, status = 0;
+      auto gsum2 = [&](double v0, double v1, double& s0, double& s1) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          v0 += __shfl_xor(v0, o);
+          v1 += __shfl_xor(v1, o);
+        }
+        if (grid_sum2(P, v0, v1, s0, s1)) status = 4;
+      };
+      float f0 = eval(y);
+      ++nfev;
+      double dt;
+      if (P.first_step > 0.0) {
+        dt = P.first_step;
+      } else {  // misc._select_initial_step in fp32 (dopri5.py select_initial_step)
+        const float scale = P.atol + P.rtol * fabsf(y);
+        const float q0 = y / scale, q1 = f0 / scale;
+        double s, s1;
+        gsum2(real ? (double)q0 * q0 : 0.0, real ? (double)q1 * q1 : 0.0, s, s1);
+        const float d0 = fabsf(sqrtf((float)(s / n_el)));
+        const float d1 = fabsf(sqrtf((float)(s1 / n_el)));
+        float h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : (0.01f * d0) / d1;
+        h0 = fabsf(h0);
+        const float f1 = eval(y + f0 * h0);
+        ++nfev;
+        const float q2 = (f1 - f0) / scale;
+        gsum2(real ? (double)q2 * q2 : 0.0, 0.0, s, s1);
+        const float d2 = fabsf(sqrtf((float)(s / n_el)) / h0);
+        float h1;
+        if (d1 <= 1e-15f && d2 <= 1e-15f) h1 = fmaxf(1e-6f, h0 * 1e-3f);
+        else h1 = powf(0.01f / fmaxf(d1, d2), 0.2f);
+        dt = (double)fminf(100.0f * h0, fabsf(h1));
+      }
+      float co[5] = {y, 0.f, 0.f, 0.f, 0.f};
+      double t0s = P.t[0], t1s = P.t[0];
+      for (int i = 1; i < P.T && status == 0; ++i) {
+        const double next_t = P.t[i];
+        int n_steps = 0;
+        while (next_t > t1s) {
+          if (n_steps >= P.max_steps) { status = 3; break; }
+          const double t0 = t1s;
+          if (!(t0 + dt > t0)) { status = 2; break; }
+          const float dt32 = (float)dt;
+          const double t1 = t0 + dt;
+          // rk_common._runge_kutta_step in fetode_lincomb's op order, accumulated as the stages
+          // arrive: A[i] is stage s+1+i's sum k0 c0 + k1 c1 + ... (the same left-to-right sums)
+          float A[6];
+#pragma unroll
+          for (int q = 0; q < 6; ++q) A[q] = f0 * (P.beta[q][0] * dt32);
+          float err = f0 * (P.cerr[0] * dt32);
+          float mid = f0 * (P.cmid[0] * dt32);
+          float yi = y, kn = f0;
+#pragma unroll 1
+          for (int st = 0; st < 6; ++st) {
+            yi = y + A[0];
+            kn = eval(yi);
+            ++nfev;
+            const int j = st + 1;
+#pragma unroll
+            for (int q = 0; q < 5; ++q) A[q] = (j + q <= 5) ? A[q + 1] + kn * (P.beta[j + q][j] * dt32) : 0.f;
+            err = err + kn * (P.cerr[j] * dt32);
+            mid = mid + kn * (P.cmid[j] * dt32);
+          }
+          const float y1 = yi;
+          const float tol = P.atol + P.rtol * fmaxf(fabsf(y), fabsf(y1));
+          const float qe = err / tol;
+          double s, nbad;
+          gsum2(real ? (double)qe * qe : 0.0, (real && !__builtin_isfinite(y)) ? 1.0 : 0.0, s, nbad);
+          if (status) break;
+          if (nbad != 0.0) { status = 1; break; }
+          const float ratio = sqrtf((float)(s / n_el));
+          const bool accept = ratio <= 1.0f;
+          if (blockIdx.x == 0 && tid == 0 && n_att < P.max_att) {
+            double* o = P.att + (int64_t)n_att * 4;
+            o[0] = t0;
+            o[1] = dt;
+            o[2] = (double)ratio;
+            o[3] = accept ? 1.0 : 0.0;
+          }
+          ++n_att;
+          if (accept) {  // interp._interp_fit (fetode_interp_fit's op order)
+            const float ym = y + mid, fa = f0, fb6 = kn;
+            co[4] = ((2.0f * dt32) * (fb6 - fa) - 8.0f * (y1 + y)) + 16.0f * ym;
+            co[3] = ((dt32 * (5.0f * fa - 3.0f * fb6) + 18.0f * y) + 14.0f * y1) - 32.0f * ym;
+            co[2] = ((dt32 * (fb6 - 4.0f * fa) - 11.0f * y) - 5.0f * y1) + 16.0f * ym;
+            co[1] = dt32 * fa;
+            co[0] = y;
+            y = y1;
+            f0 = kn;
+            t0s = t0;
+            t1s = t1;
+          } else {
+            t0s = t0;
+          }
+          // rk_common._optimal_step_size in fp64 (dopri5.py optimal_step)
+          const double rr = (double)ratio;
+          double nxt;
+          if (rr == 0.0) {
+            nxt = dt * P.ifactor;
+          } else {
+            const double dfac = rr < 1.0 ? 1.0 : P.dfactor;
+            const double factor = __builtin_isnan(rr) ? rr : fmin(P.ifactor, fmax(P.safety / pow(rr, 1.0 / 5.0), dfac));
+            nxt = dt * factor;
+          }
+          dt = __builtin_isnan(nxt) ? nxt : fmin(fmax(nxt, P.min_step), P.max_step);
+          ++n_steps;
+        }
+        if (status) break;
+        const float xq = (float)((next_t - t0s) / (t1s - t0s));  // interp._interp_evaluate
+        float total = co[0] + xq * co[1];
+        float xp = xq;
+#pragma unroll
+        for (int j = 2; j < 5; ++j) {
+          xp = xp * xq;
+          total = total + xp * co[j];
+        }
+        out_write(i, total);
+      }
+      if (blockIdx.x == 0 && tid == 0) {
+        P.stats[0] = nfev;
+        P.stats[1] = n_att;
+        P.stats[2] = __hip_atomic_load(P.bar + 64 * 9 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 4 : status;
+      }
+    } else if (a.single_eval) {
       const float f = eval(y);
       if (valid && c1 == 0) a.eval_out[b * D + row] = f;
     } else {
@@ -1030,14 +1270,15 @@ struct FusedEntry {
   fused_fn fn_rk4;    // v4: the rk4 (3/8) integrate path, all four stages inlined
   fused_fn small;     // v6 (one trajectory per workgroup): generic
   fused_fn small_rk4; // v6: rk4
+  fused_fn dopri;     // v4 with the device-resident dopri5 driver
 };
 const FusedEntry kFused[] = {
     // LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146)
     {2, 10, 2, 10, 10, 12, true, fused4_kernel<10, 10, 10, 12, true, false>, fused4_kernel<10, 10, 10, 12, true, true>,
-     small6_kernel<true, false>, small6_kernel<true, true>},
+     small6_kernel<true, false>, small6_kernel<true, true>, fused4_kernel<10, 10, 10, 12, true, false, true>},
     // LV KAN [2,10,2] (predator_prey.py:101)
     {2, 10, 2, 1, 10, 12, false, fused4_kernel<10, 2, 10, 12, false, false>, fused4_kernel<10, 2, 10, 12, false, true>,
-     small6_kernel<false, false>, small6_kernel<false, true>},
+     small6_kernel<false, false>, small6_kernel<false, true>, fused4_kernel<10, 2, 10, 12, false, false, true>},
 };
 
 // Batches up to kSmallMax take v6 (one trajectory per 3-wave workgroup, latency-bound chain split
@@ -1126,6 +1367,82 @@ int fetode_field_forward(const fetode_field_t* f, const void* plan, const float*
   a.single_eval = 1;
   a.eval_out = out;
   return launch_fused(f, a, stream);
+}
+
+int64_t fetode_integrate_dopri5_workspace(int64_t B) {
+  const int64_t grid = (B + 1) / 2;
+  return (int64_t)sizeof(unsigned) * kDpBarWords + (int64_t)sizeof(double) * (2 * grid + 16 + 2);
+}
+
+int fetode_integrate_dopri5(const fetode_field_t* f, const void* plan, const float* y0, int64_t B, const double* t,
+                            int32_t T, double rtol, double atol, const double* opts, const float* tableau,
+                            float* solution, float* state, uint32_t init_mask, void* workspace, int32_t* stats,
+                            double* attempts, int32_t max_attempts, void* stream) {
+  int rc = validate_field(f);
+  if (rc) return rc;
+  if (B <= 0 || T <= 0) return FETODE_OK;
+  if (!plan || !y0 || !t || !opts || !tableau || !solution || !workspace || !stats || (f->ferro && !state))
+    return set_err(FETODE_EINVAL, "dopri5: null pointer");
+  if (f->kan[0].in_features != f->kan[f->n_layers - 1].out_features)
+    return set_err(FETODE_EINVAL, "field is not R^D -> R^D");
+  const FusedEntry* e = find_fused(f);
+  if (!e) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
+  // every workgroup must be resident at once (grid reductions): one-wave workgroups of two
+  // trajectories, as many as the occupancy of the generic v4 kernel admits
+  static int n_cu = 0, per_cu[2] = {0, 0};
+  const int fi = f->ferro ? 0 : 1;
+  if (!n_cu) {
+    int dev = 0;
+    HIP_CHECK_RET(hipGetDevice(&dev));
+    HIP_CHECK_RET(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  if (!per_cu[fi]) HIP_CHECK_RET(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[fi], e->dopri, 64, 0));
+  const int64_t grid = nblk(B, 2);
+  if (grid > (int64_t)per_cu[fi] * n_cu)
+    return set_err(FETODE_EUNSUPPORTED, "dopri5: batch %lld needs %lld workgroups, %d resident", (long long)B,
+                   (long long)grid, per_cu[fi] * n_cu);
+  FusedArgs a;
+  memset(&a, 0, sizeof(a));
+  a.plan = (const float*)plan;
+  a.method = FETODE_RK4;
+  a.y0 = y0;
+  a.B = B;
+  a.T = T;
+  a.solution = solution;
+  a.state = state;
+  a.init_mask = init_mask;
+  DopriParams& P = a.dp;
+  P.on = 1;
+  P.t = t;
+  P.T = T;
+  P.rtol = (float)rtol;
+  P.atol = (float)atol;
+  P.first_step = opts[0];
+  P.safety = opts[1];
+  P.ifactor = opts[2];
+  P.dfactor = opts[3];
+  P.min_step = opts[4];
+  P.max_step = opts[5];
+  P.max_steps = opts[6] > 2e9 ? 2000000000 : (int)opts[6];
+  memcpy(P.beta, tableau, sizeof(float) * 36);
+  memcpy(P.cerr, tableau + 36, sizeof(float) * 7);
+  memcpy(P.cmid, tableau + 43, sizeof(float) * 7);
+  P.bar = (unsigned*)workspace;
+  double* d = (double*)((char*)workspace + sizeof(unsigned) * kDpBarWords);
+  P.slot = d;
+  P.xs = d + 2 * grid;
+  P.tot = P.xs + 16;
+  P.stats = stats;
+  P.att = attempts;
+  P.max_att = attempts ? max_attempts : 0;
+  layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
+  layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
+  a.factor_limit = kFactorLimit;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kDpBarWords, s));
+  void* args[] = {&a};
+  HIP_CHECK_RET(hipLaunchCooperativeKernel((const void*)e->dopri, dim3((unsigned)grid), dim3(64), args, 0, s));
+  return FETODE_OK;
 }
 
 int fetode_integrate_fixed(const fetode_field_t* f, const void* plan, int32_t method, const float* y0,

@@ -5,24 +5,26 @@
 // two launches per field evaluation (train_kan_fet_ett.py:136-197 with the KAN-FET field;
 // efficientkan.py:160-182; ferro_class.py:368-420).
 //
-// Workgroup = 4 waves = a tile of 64 rows x 16 outputs; the inputs are walked in chunks of kCh:
+// Workgroup = 8 waves = a tile of 64 rows x 16 outputs; the inputs are walked in chunks of kCh = 8:
 //   staging   one (row, input) item per thread: the hysteresis gate w = -2(1-alpha)(1-sigma(gs(x -
 //             prev))) and e = e^{gs x} for the Ferro elements, and the 20 KAN features (SiLU, the 8
 //             cubic B-spline bases by the reference's Cox-de Boor, 10 logistic bases) into LDS;
-//   Ferro     wave w owns outputs 4w..4w+3 for all 64 rows (lane = row), so every Ferro parameter
-//             is wave-uniform (scalar loads, SGPR operands): per element
+//   Ferro     wave w owns outputs 2w, 2w+1 for all 64 rows (lane = row), so every Ferro constant
+//             is wave-uniform (staged per chunk in LDS, read as broadcasts): per element
 //               s = 1/(1 + e P),  m = 1 + w s,  z = 2 log2e k (x + Ec m),  th = 1 - 2/(1 + 2^z)
 //             (P = e^{gs Ec} packed once; branch_sign = 1 makes the crossing gate cp drop out, as in
 //             the fused LV kernel), 7 VALU + 3 transcendental instructions;
 //   KAN       the (64 x 16) x (in * 20) contraction on v_mfma_f32_16x16x4_f32: wave w owns rows
-//             16w..16w+15, A = the staged features (LDS, pitch = 2 mod 32: conflict-free), B = the
-//             packed weights (global, L2-resident, loaded at the chunk start).
-// Epilogue: the Ferro sums (lane = row) meet the MFMA tile (lane = column) in LDS.
+//             16 (w % 4).. and the chunk inputs of parity w / 4, A = the staged features (LDS, pitch
+//             = 2 mod 32: conflict-free), B = the packed weights (global, L2-resident, loaded at the
+//             chunk start), two accumulators alternating per input (half the dependent MFMA chain).
+// Epilogue: the two K-halves and the Ferro sums (lane = row) meet the MFMA tile in LDS, fixed order.
 //
 // Direct form: a wave whose chunk input has |gs x| > 80 anywhere, or whose (output, input) has
 // |gs Ec| > 80, evaluates s = 1/(1 + 2^{gs log2e (x + Ec)}) with one more exponential (the
 // product e P could overflow a factor there).
 #include <algorithm>
+#include <cstdlib>
 
 #include "fetode_common.h"
 
@@ -34,8 +36,10 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWF = 20;       // KAN features per input: SiLU, B_0..B_7, phi_0..phi_9, 0
 constexpr int kNS = 8, kNB = 10, kNG = 12;
-constexpr int kRows = 64, kOuts = 16, kCh = 4, kThreads = 256;
-constexpr int kPitch = kCh * kWF + 18;  // 98 = 2 (mod 32): MFMA A-operand reads are conflict-free
+constexpr int kRows = 64, kOuts = 16, kChMax = 8, kWaves = 8, kThreads = 64 * kWaves;
+constexpr int kJ = kOuts / kWaves;      // Ferro outputs per wave
+// LDS pitch of a row of staged features: = 2 (mod 32), so the MFMA A-operand reads are conflict-free
+constexpr int pitch_of(int ch) { return ((ch * kWF + 29) / 32) * 32 + 2; }
 
 // packed plan of one layer (offsets in floats)
 struct WideLayout {
@@ -94,7 +98,7 @@ bool wide_supported(const fetode_kanlinear_t* kl, const fetode_ferro_t* fl) {
   if (fl && (fl->branch_sign || !fl->k || !fl->Ec || !fl->Ps || !fl->bias || !fl->coef)) return false;
   if (kl && fl && (kl->in_features != fl->in_dim || kl->out_features != fl->out_dim)) return false;
   const int in = kl ? kl->in_features : fl->in_dim, out = kl ? kl->out_features : fl->out_dim;
-  return in >= 16 && out >= 16 && out % kOuts == 0 && in % kCh == 0;
+  return in >= 16 && out >= 16 && out % kOuts == 0 && in % kChMax == 0;
 }
 
 // ---- packing (once per parameter version) ------------------------------------------------------
@@ -167,30 +171,37 @@ __global__ void wide_pack_kernel(fetode_kanlinear_t kl, fetode_ferro_t fl, WideL
     const float* g = kl.grid + (int64_t)i * kNG;
     plan[L.knots + t] = g[j];
     if (j < kNG - 1) plan[L.rh + (int64_t)i * (kNG - 1) + j] = 1.0f / (g[j + 1] - g[j]);
-    // basis table of interval m = j: the 8 bases as cubics in u = (x - g_m) / (g_{m+1} - g_m),
-    // fitted in fp64 through u = 0, 1/3, 2/3, 1 (exact: each basis is a cubic on the interval)
-    float* d = plan + L.bt + ((int64_t)i * kNG + j) * kNS * 4;
-    for (int c = 0; c < kNS * 4; ++c) d[c] = 0.f;
-    if (j < kNG - 1) {
-      const double h = (double)g[j + 1] - g[j];
-      double v[4][kNS];
-      for (int q = 0; q < 4; ++q) {
-        for (int c = 0; c < kNS; ++c) v[q][c] = 0.0;
-        double N[5];
-        bases_on_interval(g[j] + h * (q / 3.0), j, g, N);
-        for (int r = 0; r <= 3; ++r) {
-          const int c = j - 3 + r;
-          if (c >= 0 && c < kNS) v[q][c] = N[r];
-        }
-      }
-      for (int c = 0; c < kNS; ++c) {
-        d[4 * c + 0] = (float)v[0][c];
-        d[4 * c + 1] = (float)((-11.0 * v[0][c] + 18.0 * v[1][c] - 9.0 * v[2][c] + 2.0 * v[3][c]) / 2.0);
-        d[4 * c + 2] = (float)(9.0 * (2.0 * v[0][c] - 5.0 * v[1][c] + 4.0 * v[2][c] - v[3][c]) / 2.0);
-        d[4 * c + 3] = (float)(9.0 * (-v[0][c] + 3.0 * v[1][c] - 3.0 * v[2][c] + v[3][c]) / 2.0);
-      }
+  }
+}
+
+// basis table: thread per (input i, knot interval m, basis c): B_c on [g_m, g_{m+1}) as a cubic
+// in u = (x - g_m) / (g_{m+1} - g_m), fitted in fp64 through u = 0, 1/3, 2/3, 1 (exact: each basis
+// is a cubic on the interval); m = 11 (outside the grid) and bases not supported there: zero
+__global__ void wide_basis_kernel(fetode_kanlinear_t kl, WideLayout L, float* __restrict__ plan) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (!L.kan || t >= (int64_t)L.in * kNG * kNS) return;
+  const int c = (int)(t % kNS), m = (int)((t / kNS) % kNG), i = (int)(t / (kNS * kNG));
+  const float* g = kl.grid + (int64_t)i * kNG;
+  const int r = c - m + 3;  // slot of basis c among the interval's B_{m-3..m}
+  double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+  if (m < kNG - 1 && r >= 0 && r <= 3) {
+    const double h = (double)g[m + 1] - g[m];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      double N[5];
+      bases_on_interval(g[m] + h * (q / 3.0), m, g, N);
+      const double v = r == 0 ? N[0] : r == 1 ? N[1] : r == 2 ? N[2] : N[3];
+      if (q == 0) v0 = v;
+      else if (q == 1) v1 = v;
+      else if (q == 2) v2 = v;
+      else v3 = v;
     }
   }
+  float* d = plan + L.bt + t * 4;
+  d[0] = (float)v0;
+  d[1] = (float)((-11.0 * v0 + 18.0 * v1 - 9.0 * v2 + 2.0 * v3) / 2.0);
+  d[2] = (float)(9.0 * (2.0 * v0 - 5.0 * v1 + 4.0 * v2 - v3) / 2.0);
+  d[3] = (float)(9.0 * (-v0 + 3.0 * v1 - 3.0 * v2 + v3) / 2.0);
 }
 
 // per-output constant sum_{i,k} coef * bias: one wave per output, fixed order
@@ -219,16 +230,20 @@ struct WideArgs {
 };
 
 // ---- the layer --------------------------------------------------------------------------------
-template <int K, bool KAN, bool FERRO>
+template <int K, bool KAN, bool FERRO, int kCh>
 __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
   constexpr int KP = FERRO ? K : 1;
+  constexpr int kPitch = pitch_of(kCh);
+  static_assert(kCh * kRows <= kThreads && (kCh & 1) == 0, "one staging item per thread, even chunks");
   __shared__ float s_x[kCh * kRows], s_w[kCh * kRows], s_e[kCh * kRows];
   __shared__ float4 s_par[kOuts * kCh * KP];  // the chunk's Ferro constants, read as wave broadcasts
   __shared__ float s_dfl[kOuts * kCh];
   // KAN features of the chunk (MFMA A operand); the epilogue reuses the space for the Ferro sums
-  constexpr int kPhi = KAN ? kRows * kPitch : 0, kFer = kRows * (kOuts + 1);
+  // and the second K-half of the MFMA tile
+  constexpr int kPhi = KAN ? kRows * kPitch : 0, kFer = 2 * kRows * (kOuts + 1);
   __shared__ __attribute__((aligned(16))) float s_phi[kPhi > kFer ? kPhi : kFer];
   float* s_fer = s_phi;
+  float* s_kc = s_phi + kRows * (kOuts + 1);
   const WideLayout& L = a.L;
   const int in = L.in, out = L.out;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -238,34 +253,40 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
   const float* __restrict__ plan = a.plan;
   const float gs = L.gs, gsl2e = L.gsl2e, wc = L.wc, l2 = FETODE_LOG2E;
 
-  float facc[4] = {0.f, 0.f, 0.f, 0.f};  // Ferro: row = lane, output o0 + 4w + j
-  f32x4 kacc = {0.f, 0.f, 0.f, 0.f};     // KAN: rows 16w + 4 (lane >> 4) + v, column lane & 15
-  const int kr = lane & 15, kq = lane >> 4;
+  float facc[kJ];  // Ferro: row = lane, output o0 + kJ w + j
+#pragma unroll
+  for (int j = 0; j < kJ; ++j) facc[j] = 0.f;
+  f32x4 kacc0 = {0.f, 0.f, 0.f, 0.f}, kacc1 = {0.f, 0.f, 0.f, 0.f};  // KAN: rows 16 (w % 4) + 4 (lane >> 4) + v
+  const int kr = lane & 15, kq = lane >> 4, rt = w & 3, kh = w >> 2;
 
   // staging item of this thread: row sr, chunk input si
-  const int sr = tid >> 2, si = tid & 3;
+  const int sr = tid / kCh, si = tid % kCh;
   const int64_t sb = b0 + sr;
-  const bool slive = sb < a.B;
+  const bool stager = tid < kCh * kRows;
+  const bool slive = stager && sb < a.B;
 
   for (int i0 = 0; i0 < in; i0 += kCh) {
-    // KAN weights of this chunk for the MFMA B operand (L2-resident; issued before the staging)
-    float wb[KAN ? kCh * 5 : 1];
+    // KAN weights of this wave's chunk inputs (ii = 2 q + kh) for the MFMA B operand (L2-resident;
+    // issued before the staging)
+    float wb[KAN ? kCh / 2 * 5 : 1];
     if constexpr (KAN) {
 #pragma unroll
-      for (int ii = 0; ii < kCh; ++ii)
+      for (int q = 0; q < kCh / 2; ++q)
 #pragma unroll
         for (int s = 0; s < 5; ++s)
-          wb[ii * 5 + s] = plan[L.wp + ((int64_t)(i0 + ii) * kWF + 4 * s + kq) * out + o0 + kr];
+          wb[q * 5 + s] = plan[L.wp + ((int64_t)(i0 + 2 * q + kh) * kWF + 4 * s + kq) * out + o0 + kr];
     }
     __syncthreads();  // the previous chunk is consumed
     const float x = slive ? a.x[sb * in + i0 + si] : 0.f;
     if constexpr (FERRO) {
       const float pv = a.reinit ? x : (slive ? a.prev[sb * in + i0 + si] : 0.f);
+      if (stager) {
       // is_moving_up = sigmoid(gate_slope (x - prev_x)) (ferro_class.py:387), w = wc (1 - up)
       const float up = rcp(1.0f + ex2(-gsl2e * (x - pv)));
       s_x[si * kRows + sr] = x;
       s_w[si * kRows + sr] = wc * (1.0f - up);
       s_e[si * kRows + sr] = ex2(gsl2e * x);
+      }
       const float4* fe = reinterpret_cast<const float4*>(plan + L.fe4);
       for (int idx = tid; idx < kOuts * kCh * K; idx += kThreads) {
         const int j = idx / (kCh * K), r = idx - j * (kCh * K);
@@ -273,7 +294,7 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
       }
       if (tid < kOuts * kCh) s_dfl[tid] = plan[L.dflag + (int64_t)(o0 + tid / kCh) * in + i0 + tid % kCh];
     }
-    if constexpr (KAN) {
+    if (KAN && stager) {
       const int i = i0 + si;
       float f[kWF];
       f[0] = x * rcp(1.0f + ex2(-x * l2));  // SiLU (efficientkan.py:166)
@@ -302,22 +323,26 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
     }
     __syncthreads();
     if constexpr (KAN) {
-      const float* arow = &s_phi[(16 * w + kr) * kPitch + kq];
+      const float* arow = &s_phi[(16 * rt + kr) * kPitch + kq];
 #pragma unroll
-      for (int ii = 0; ii < kCh; ++ii)
+      for (int q = 0; q < kCh / 2; ++q) {
+        const int ii = 2 * q + kh;
 #pragma unroll
-        for (int s = 0; s < 5; ++s)
-          kacc = __builtin_amdgcn_mfma_f32_16x16x4f32(arow[ii * kWF + 4 * s], wb[ii * 5 + s], kacc, 0, 0, 0);
+        for (int s = 0; s < 5; ++s) {
+          if (q & 1) kacc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(arow[ii * kWF + 4 * s], wb[q * 5 + s], kacc1, 0, 0, 0);
+          else kacc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(arow[ii * kWF + 4 * s], wb[q * 5 + s], kacc0, 0, 0, 0);
+        }
+      }
     }
     if constexpr (FERRO) {
-#pragma unroll 1
+#pragma unroll 2
       for (int ii = 0; ii < kCh; ++ii) {
         const int i = i0 + ii;
         const float xv = s_x[ii * kRows + lane], wg = s_w[ii * kRows + lane], e = s_e[ii * kRows + lane];
         const bool xbig = __any(fabsf(gs * xv) > 80.0f);  // wave-uniform
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int jo = 4 * w + j;
+        for (int j = 0; j < kJ; ++j) {
+          const int jo = kJ * w + j;
           const float4* par = &s_par[(jo * kCh + ii) * K];
           float acc = 0.f;
           if (!xbig && s_dfl[jo * kCh + ii] == 0.f) {
@@ -347,20 +372,28 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
       }
     }
   }
-  // epilogue: Ferro sums (+ sum coef bias) meet the KAN tile in LDS (s_phi's space)
+  // epilogue: the Ferro sums (+ sum coef bias) and the second K-half meet the KAN tile in LDS
   __syncthreads();
   if constexpr (FERRO) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) s_fer[lane * (kOuts + 1) + 4 * w + j] = facc[j] + plan[L.fconst + o0 + 4 * w + j];
+    for (int j = 0; j < kJ; ++j)
+      s_fer[lane * (kOuts + 1) + kJ * w + j] = facc[j] + plan[L.fconst + o0 + kJ * w + j];
+  }
+  if constexpr (KAN) {
+    if (kh == 1)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) s_kc[(16 * rt + 4 * kq + v) * (kOuts + 1) + kr] = kacc0[v] + kacc1[v];
   }
   __syncthreads();
   if constexpr (KAN) {
+    if (kh == 0)
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int r = 16 * w + 4 * kq + v;
-      const int64_t b = b0 + r;
-      if (b < a.B) a.out[b * out + o0 + kr] = FERRO ? kacc[v] + s_fer[r * (kOuts + 1) + kr] : kacc[v];
-    }
+      for (int v = 0; v < 4; ++v) {
+        const int r = 16 * rt + 4 * kq + v;
+        const int64_t b = b0 + r;
+        const float kv = (kacc0[v] + kacc1[v]) + s_kc[r * (kOuts + 1) + kr];
+        if (b < a.B) a.out[b * out + o0 + kr] = FERRO ? kv + s_fer[r * (kOuts + 1) + kr] : kv;
+      }
   } else {
     for (int t = tid; t < kRows * kOuts; t += kThreads) {
       const int r = t / kOuts, c = t % kOuts;
@@ -371,10 +404,20 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
 }
 
 typedef void (*wide_fn)(WideArgs);
+template <int CH>
+wide_fn pick_ch(int K, bool kan, bool ferro) {
+  if (kan && !ferro) return wide_layer_kernel<10, true, false, CH>;
+  if (K == 12) return kan ? wide_layer_kernel<12, true, true, CH> : wide_layer_kernel<12, false, true, CH>;
+  return kan ? wide_layer_kernel<10, true, true, CH> : wide_layer_kernel<10, false, true, CH>;
+}
+// inputs per staged chunk: 8 (fewer barriers) or 4 (less LDS, more resident workgroups);
+// FETODE_WIDE_CH picks (tuning knob, default 8)
 wide_fn pick(int K, bool kan, bool ferro) {
-  if (kan && !ferro) return wide_layer_kernel<10, true, false>;
-  if (K == 12) return kan ? wide_layer_kernel<12, true, true> : wide_layer_kernel<12, false, true>;
-  return kan ? wide_layer_kernel<10, true, true> : wide_layer_kernel<10, false, true>;
+  static const int ch = [] {
+    const char* e = getenv("FETODE_WIDE_CH");
+    return e && atoi(e) == 4 ? 4 : 8;
+  }();
+  return ch == 4 ? pick_ch<4>(K, kan, ferro) : pick_ch<8>(K, kan, ferro);
 }
 
 }  // namespace
@@ -402,6 +445,11 @@ int fetode_wide_layer_plan_build(const fetode_kanlinear_t* kl, const fetode_ferr
   LAUNCH_CHECK();
   hipLaunchKernelGGL(wide_const_kernel, dim3((unsigned)L.out), dim3(64), 0, s, f0, L, (float*)plan);
   LAUNCH_CHECK();
+  if (L.kan) {
+    const int64_t nb = (int64_t)L.in * kNG * kNS;
+    hipLaunchKernelGGL(wide_basis_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, s, k0, L, (float*)plan);
+    LAUNCH_CHECK();
+  }
   return FETODE_OK;
 }
 

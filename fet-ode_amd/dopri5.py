@@ -329,6 +329,68 @@ def _try_ecg_resident(func, y0, tp, reversed_, rtol, atol, options):
     return sol
 
 
+def _try_field_resident(func, y0, tp, reversed_, rtol, atol, options):
+    """The whole solve in one launch when `func` is a tagged KAN / KAN-FET field with a fused
+    kernel (fet_ode_amd.autonomous(model): the LV [2,10,2] fields), nothing needs gradients and
+    the options are the scalar ones (fetode_integrate_dopri5)."""
+    from .autograd_ops import build_plan, make_handle, pack_state, unpack_state
+    from .odeint import fused_field
+    field = fused_field(func)
+    if field is None or reversed_ or y0.dim() != 2 or set(options) - _RESIDENT_OPTS:
+        return None
+    if not (isinstance(rtol, (int, float)) and isinstance(atol, (int, float))):
+        return None
+    if torch.is_grad_enabled() and (y0.requires_grad or any(p.requires_grad for p in field.parameters())):
+        return None
+    lib = _lib.load()
+    dev = y0.device
+    B = y0.shape[0]
+    handle = make_handle(field, B, dev)
+    if not lib.fetode_fused_supported(handle.ref):
+        return None
+    plan = build_plan(field, handle, dev)
+    state, mask = pack_state(field, B, dev)
+    yc = _lib.f32c(y0)
+    tkey = (dev, tuple(tp.tolist()))
+    t_dev = _T_DEV.get(tkey)
+    if t_dev is None:
+        if len(_T_DEV) > 64:
+            _T_DEV.clear()
+        t_dev = _T_DEV[tkey] = tp.to(torch.float64).to(dev)
+    T = t_dev.numel()
+    sol = torch.empty(T, B, y0.shape[1], device=dev, dtype=torch.float32)
+    ws = torch.empty(max(1, lib.fetode_integrate_dopri5_workspace(B) // 4), device=dev, dtype=torch.float32)
+    stats = torch.empty(3, device=dev, dtype=torch.int32)
+    att = torch.empty(_MAX_TRACE, 4, device=dev, dtype=torch.float64)
+    fs = options.get("first_step")
+    opts = np.array([float(fs) if fs is not None else 0.0, float(options.get("safety", 0.9)),
+                     float(options.get("ifactor", 10.0)), float(options.get("dfactor", 0.2)),
+                     float(options.get("min_step", 0.0)), float(options.get("max_step", math.inf)),
+                     float(options.get("max_num_steps", 2 ** 31 - 1))], dtype=np.float64)
+    rc = lib.fetode_integrate_dopri5(
+        handle.ref, plan.data_ptr(), yc.data_ptr(), B, t_dev.data_ptr(), T, float(rtol), float(atol),
+        opts.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_double)),
+        _TABLEAU.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_float)), sol.data_ptr(), _lib.ptr(state), mask,
+        ws.data_ptr(), stats.data_ptr(), att.data_ptr(), _MAX_TRACE, _lib.stream_handle(dev))
+    if rc == _lib.FETODE_EUNSUPPORTED:   # the grid does not fit one resident launch: host-driven loop
+        return None
+    _lib.check(rc, "fetode_integrate_dopri5")
+    if state is not None:
+        unpack_state(field, state)
+    status = int(stats[2].item())   # one read per solve: torchdiffeq's assertions
+    if status == 1:
+        raise AssertionError("non-finite values in state `y`")
+    if status == 2:
+        raise AssertionError("underflow in dt")
+    if status == 3:
+        raise AssertionError("max_num_steps exceeded")
+    if status == 4:
+        raise RuntimeError("fetode_integrate_dopri5: a grid reduction timed out (workgroups not co-resident); "
+                           "the solution is invalid")
+    dopri5_solve.last = ResidentSolve(stats, att)
+    return sol
+
+
 _RESIDENT = True
 
 
@@ -526,6 +588,8 @@ def _needs_grad(func, y0) -> bool:
 def dopri5_solve(func, y0, tc, tp, reversed_, rtol, atol, options):
     if _RESIDENT:
         sol = _try_ecg_resident(func, y0, tp, reversed_, rtol, atol, options)
+        if sol is None:
+            sol = _try_field_resident(func, y0, tp, reversed_, rtol, atol, options)
         if sol is not None:
             return sol
     if _needs_grad(func, y0):

@@ -151,6 +151,27 @@ int fetode_wide_layer_forward(const fetode_kanlinear_t* layer, const fetode_ferr
                               const float* x, int64_t B, const float* prev, int32_t reinit, float* out,
                               void* stream);
 
+/* The whole dopri5 solve of a fused-shape field (the LV KAN / KAN-FET [2,10,2] fields) in ONE
+ * cooperative launch — torchdiffeq's default method of every reference odeint without `method`
+ * (train_kanfet_node_predprey.py:252,260, rtol 1e-7 / atol 1e-9): f0, misc._select_initial_step
+ * (unless opts[0] = first_step > 0), 6 evaluations per attempt incl. rejected ones (the hysteresis
+ * state sees every call, ferro_class.py:409), the global RMS error norm, accept/reject,
+ * _optimal_step_size, _interp_fit/_interp_evaluate at every output time, in the arithmetic of the
+ * host-driven path (fetode_lincomb / fetode_scaled_rms / fetode_interp_*).
+ *   y0 (B, D); t (dev, fp64, T) strictly increasing; opts / tableau as fetode_ecg_dopri5;
+ *   solution (T, B, D); state / init_mask as fetode_field_forward (final state written back);
+ *   workspace: fetode_integrate_dopri5_workspace(B) bytes; stats (dev, 3 ints) = nfev, attempts,
+ *   status (0 ok, 1 non-finite state, 2 dt underflow, 3 max_num_steps, 4 a grid reduction timed
+ *   out); attempts (dev, nullable) (max_attempts, 4) doubles: t0, dt, error ratio, accepted.
+ * FETODE_EUNSUPPORTED when the shape has no fused kernel or B needs more workgroups than can be
+ * resident at once (B <= 4096 on MI355X); the caller then takes the host-driven loop. */
+int fetode_integrate_dopri5(const fetode_field_t* field, const void* plan, const float* y0, int64_t B,
+                            const double* t, int32_t T, double rtol, double atol, const double* opts,
+                            const float* tableau, float* solution, float* state, uint32_t init_mask,
+                            void* workspace, int32_t* stats, double* attempts, int32_t max_attempts,
+                            void* stream);
+int64_t fetode_integrate_dopri5_workspace(int64_t B);
+
 /* Standalone module kernels (generic widths). */
 /* KANLinear.forward (efficientkan.py:160-182): x (B,in) -> out (B,out). */
 int fetode_kanlinear_forward(const fetode_kanlinear_t* layer, const float* x, int64_t B, float* out,

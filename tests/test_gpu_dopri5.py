@@ -139,3 +139,98 @@ def test_rk4_classic_fused_and_per_stage(dev, fused):
         gpu = F.odeint(func, y0.to(dev), t, method="rk4_classic").cpu()
     cpu = O.odeint(lambda tt, yy: ref(yy), y0, t, method="rk4_classic")
     assert ((gpu - cpu).norm(dim=(1, 2)) / cpu.norm(dim=(1, 2))).max() < 1e-5
+
+
+# ---------------------------------------------------------------------------------------------
+# device-resident dopri5 for the tagged LV fields (fetode_integrate_dopri5)
+# ---------------------------------------------------------------------------------------------
+
+def test_dopri5_kanfet_trace_resident(dev):
+    """The golden trace again, through the whole-solve-in-one-launch path (the tagged field)."""
+    import fet_ode_amd as F
+    from fet_ode_amd.dopri5 import ResidentSolve
+    g = load_golden("dopri5_kanfet")
+    m = F.KANFET([2, 10, 2], grid_size=5)
+    m.load_state_dict(golden_sd(g))
+    m = m.to(dev)
+    with torch.no_grad():
+        sol = F.odeint(F.autonomous(m), torch.from_numpy(g["y0"]).to(dev), torch.from_numpy(g["t"]),
+                       rtol=1e-3, atol=1e-4).cpu()
+    solver = F.dopri5.dopri5_solve.last
+    assert isinstance(solver, ResidentSolve)
+    att = np.array([[a[0], a[1], a[2], float(a[3])] for a in solver.attempts])
+    exp = g["attempts"]
+    assert att.shape == exp.shape, (att.shape, exp.shape)
+    np.testing.assert_array_equal(att[:, 3], exp[:, 3])
+    np.testing.assert_allclose(att[:, 1], exp[:, 1], rtol=1e-3)
+    np.testing.assert_allclose(att[:, 2], exp[:, 2], rtol=1e-2, atol=1e-6)
+    assert solver.nfev == int(g["nfev"])
+    ref = torch.from_numpy(g["sol"])
+    assert ((sol - ref).norm(dim=(1, 2)) / ref.norm(dim=(1, 2))).max() < 1e-4
+
+
+@pytest.mark.parametrize("B", [1, 64, 1000, 4096])
+@pytest.mark.parametrize("kind", ["kanfet", "kan"])
+def test_dopri5_resident_matches_host_driven(dev, B, kind):
+    """One cooperative launch vs the host-driven loop (one fused field launch per evaluation, the
+    error norm read back per attempt) on the same model and inputs: the same attempts (accept
+    pattern, step sizes), nfev, solution within 1e-5 per slice, the same final hysteresis state."""
+    import fet_ode_amd as F
+    from fet_ode_amd.dopri5 import ResidentSolve, set_resident_dopri5
+    gk = load_golden("traj_kanfet" if kind == "kanfet" else "traj_kan")
+    y0 = torch.from_numpy(gk["y0_B64"]).repeat(64, 1)[:B].to(dev)
+    t = torch.tensor([0.0, 0.2, 0.5], dtype=torch.float64)
+    out = []
+    for resident in (True, False):
+        prev = set_resident_dopri5(resident)
+        try:
+            m = (F.KANFET if kind == "kanfet" else F.KAN)([2, 10, 2], grid_size=5)
+            m.load_state_dict(golden_sd(gk))
+            m = m.to(dev)
+            with torch.no_grad():
+                sol = F.odeint(F.autonomous(m), y0, t, rtol=1e-3, atol=1e-4).cpu()
+        finally:
+            set_resident_dopri5(prev)
+        s = F.dopri5.dopri5_solve.last
+        assert isinstance(s, ResidentSolve) == resident
+        states = [l.ferro._prev.cpu() for l in m.layers] if kind == "kanfet" else []
+        out.append((sol, [(a[1], a[3]) for a in s.attempts], s.nfev, states))
+    (s0, a0, n0, st0), (s1, a1, n1, st1) = out
+    assert n0 == n1 and [a[1] for a in a0] == [a[1] for a in a1]
+    np.testing.assert_allclose([a[0] for a in a0], [a[0] for a in a1], rtol=1e-6)
+    assert ((s0 - s1).norm(dim=(1, 2)) / s1.norm(dim=(1, 2)).clamp_min(1e-30)).max() <= 1e-5
+    for a, b in zip(st0, st1):
+        assert ((a - b).norm() / b.norm()).item() <= 1e-4
+
+
+def test_dopri5_resident_reference_tolerances(dev):
+    """The north-star call itself: torchodeint(calDeriv, X0, t_learn) with torchdiffeq's default
+    rtol 1e-7 / atol 1e-9 on the bench workload (B = 4096, 35 points): thousands of attempts in
+    one launch (rtol 1e-7 sits at fp32 resolution), finite, every attempt 6 evaluations."""
+    import fet_ode_amd as F
+    from fet_ode_amd.dopri5 import ResidentSolve
+    from oracle import torch_ref as O
+    torch.manual_seed(0)
+    m = F.KANFET([2, 10, 2], grid_size=5).to(dev)
+    y0 = O.lv_y0(4096, 0).to(dev)
+    t = torch.tensor(np.linspace(0, 3.5, 35))
+    with torch.no_grad():
+        sol = F.odeint(F.autonomous(m), y0, t)
+    s = F.dopri5.dopri5_solve.last
+    assert isinstance(s, ResidentSolve)
+    assert torch.isfinite(sol).all()
+    assert len(s.attempts) > 100 and s.nfev > 600
+
+
+def test_dopri5_resident_falls_back_beyond_one_grid(dev):
+    """A batch that cannot be co-resident takes the host-driven loop (no error, same API)."""
+    import fet_ode_amd as F
+    from fet_ode_amd.dopri5 import ResidentSolve
+    g = load_golden("traj_kanfet")
+    m = F.KANFET([2, 10, 2], grid_size=5)
+    m.load_state_dict(golden_sd(g))
+    m = m.to(dev)
+    y0 = torch.from_numpy(g["y0_B64"]).repeat(70, 1)[:4480].to(dev)
+    with torch.no_grad():
+        sol = F.odeint(F.autonomous(m), y0, torch.tensor([0.0, 0.1], dtype=torch.float64), rtol=1e-3, atol=1e-4)
+    assert torch.isfinite(sol).all() and not isinstance(F.dopri5.dopri5_solve.last, ResidentSolve)
