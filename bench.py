@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
                     help="strong: global batch 4096 split over ranks (primary); weak: 4096 per rank")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-dopri5", action="store_true", help="skip the LV dopri5 (torchdiffeq defaults) line")
     ap.add_argument("--no-ecg", action="store_true", help="skip the ECG dopri5 (configs[2]) line")
     ap.add_argument("--no-mnist", action="store_true", help="skip the MNIST Kuramoto + KANLinear line")
     ap.add_argument("--no-ett", action="store_true", help="skip the ETT KAN-FET latent-ODE forecaster line")
@@ -191,6 +192,35 @@ def train_rate(model, y0d, t, iters, warmup, world, strong=True):
             "unit": "RK4 steps/s trained (fwd+bwd+allreduce+Adam) of the batch-4096 job",
             "ms_per_iter": el / iters * 1e3, "iters": iters,
             "path": "fused: fetode_integrate_fixed with tape + fetode_integrate_fixed_backward (one launch each)"}
+
+
+def lv_dopri5_rate(sd, y0d, t, reps=3):
+    """The north-star call as the reference makes it: torchodeint(calDeriv, X0, t_learn) with
+    torchdiffeq's defaults (dopri5, rtol 1e-7, atol 1e-9; train_kanfet_node_predprey.py), B = 4096,
+    the 35-point grid, no_grad.  The whole adaptive solve is one cooperative launch
+    (fetode_integrate_dopri5: field, error norm and step control on the device)."""
+    from fet_ode_amd.dopri5 import ResidentSolve
+    m = F.KANFET([2, 10, 2], grid_size=5)
+    m.load_state_dict(sd)
+    m = m.to(y0d.device)
+    func = F.autonomous(m)
+    with torch.no_grad():
+        F.odeint(func, y0d, t)
+        torch.cuda.synchronize(y0d.device)
+        ts = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            sol = F.odeint(func, y0d, t)
+            torch.cuda.synchronize(y0d.device)
+            ts.append(time.perf_counter() - t0)
+    s = F.dopri5.dopri5_solve.last
+    el = float(np.median(ts))
+    acc = sum(1 for a in s.attempts if a[3])   # of the logged attempts (all of them below 16384)
+    return {"value": 1.0 / el, "unit": "dopri5 solves/s (B=4096, rtol 1e-7, atol 1e-9, t=linspace(0,3.5,35))",
+            "ms_per_solve": el * 1e3, "attempts": s.n_attempts, "accepted": acc, "nfev": s.nfev,
+            "field_evals_per_s": s.nfev / el, "rk4_equiv_steps_per_s": s.nfev / 4 / el,
+            "resident": isinstance(s, ResidentSolve), "finite": bool(torch.isfinite(sol).all()),
+            "path": "fetode_integrate_dopri5: fused4_kernel DOPRI instantiation, one cooperative launch"}
 
 
 def ecg_rate(dev, reps=10, cpu_seconds=5.0, with_cpu=True, rtol=1e-3, atol=1e-4):
@@ -501,6 +531,8 @@ def main():
                                            "events, solve = host wall of one odeint call (median)"}
         if train is not None:
             out["train"] = train
+        if world == 1 and not args.no_dopri5:
+            out["lv_dopri5"] = lv_dopri5_rate(sd, y0d, t)
         if world == 1 and not args.no_ecg:
             out["ecg"] = ecg_rate(dev, with_cpu=not args.no_cpu_baseline)
             out["ecg"]["rtol_1e-2"] = ecg_rate(dev, with_cpu=False, rtol=1e-2, atol=1e-3)
@@ -511,6 +543,15 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cb, ref_sol = cpu_baseline(sd, y0, t, args.cpu_solves)
             out["cpu_baseline"] = cb
+            if "lv_dopri5" in out:
+                # the CPU solve at rtol 1e-7 runs ~6 min (thousands of attempts): priced from the RK4
+                # sample's field-evaluation rate (the same oracle field, the same op order) x nfev
+                fe = cb["value"] * 4
+                out["lv_dopri5"]["cpu_baseline"] = {
+                    "value": fe / out["lv_dopri5"]["nfev"], "unit": out["lv_dopri5"]["unit"],
+                    "cores": cb["cores"], "kind": "port",
+                    "sample": f"extrapolated: oracle field evaluations/s from the RK4 sample ({fe:.0f}/s) "
+                              f"/ the GPU solve's nfev ({out['lv_dopri5']['nfev']})"}
             if train is not None:
                 out["train"]["cpu_baseline"] = cpu_train_baseline(sd, y0, t, args.cpu_solves)
             fresh = F.KANFET([2, 10, 2], grid_size=5)

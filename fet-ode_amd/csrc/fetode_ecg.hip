@@ -365,8 +365,11 @@ __device__ __forceinline__ float fast_sigmoid(float z) { return rcp(1.0f + ex2(-
 // Grid barrier, XCD-hierarchical (MI355X_MICROARCH.md "barrier-xcd"): workgroup i runs on XCD
 // i % 8, so each XCD's workgroups arrive on their own counter (256 B apart); the last arriver of an
 // XCD arrives on the top counter, the last of those bumps the generation every workgroup polls.
-// Release before arriving, acquire after: the partial slots written before the barrier are
-// visible after it.  Counters reset themselves; the words are zeroed once per launch.
+// The only data shared across workgroups (the partial slots) moves through agent-scope atomics,
+// coherent across the XCDs' L2s by themselves, so the ordering needed is a vector-memory wait
+// before arriving and after the poll — not agent-scope fences, which would also write back and
+// invalidate the whole L2 (buffer_wbl2 / buffer_inv sc1) at every barrier (fetode_fused.hip
+// dp_order).  Counters reset themselves; the words are zeroed once per launch.
 constexpr int kBarWords = 64 * 10;  // 8 XCD counters, top counter, generation (256 B each)
 // Every spin is bounded (MI355X_MICROARCH.md: a stranded workgroup must not hang the device): after
 // 2^20 polls (about a second) the barrier gives up and raises the abort word 64*9+1.  Once that word
@@ -386,12 +389,14 @@ __device__ bool grid_barrier(unsigned* bar, unsigned nblk) {
     int ab = __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
     if (!ab) {
       const unsigned g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nx - 1u) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the slot stores have landed
+      if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nx - 1u) {
         __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nxcd - 1u) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // reset lands before the release
+        if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nxcd - 1u) {
           __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
       unsigned spins = 0;
@@ -407,7 +412,7 @@ __device__ bool grid_barrier(unsigned* bar, unsigned nblk) {
           break;
         }
       }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     s_abort = ab;
   }
@@ -673,7 +678,7 @@ __global__ __launch_bounds__(kResThreads) void ecg_dopri5_kernel(EcgDopriArgs a)
     const float d2 = fabsf(sqrtf((float)(s / n_el)) / h0);  // (status 4: the loop below is skipped)
     float h1;
     if (d1 <= 1e-15f && d2 <= 1e-15f) h1 = fmaxf(1e-6f, h0 * 1e-3f);
-    else h1 = powf(0.01f / fmaxf(d1, d2), 0.2f);
+    else h1 = (float)pow((double)(0.01f / fmaxf(d1, d2)), (double)0.2f);  // fp64 pow rounded once: host == device
     dt = (double)fminf(100.0f * h0, fabsf(h1));
   }
 

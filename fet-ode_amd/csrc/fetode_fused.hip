@@ -67,88 +67,125 @@ struct DopriParams {
   float rtol, atol;
   double first_step, safety, ifactor, dfactor, min_step, max_step;
   int32_t max_steps;
-  float beta[6][6], cerr[7], cmid[7];  // tableau in fp32 (RKAdaptiveStepsizeODESolver casts it to y0's dtype)
+  // tableau in fp32 (RKAdaptiveStepsizeODESolver casts it to y0's dtype), by stage column j:
+  // stc[j][q] = beta[j + q][j] (q < 6, 0 past the tableau), stc[j][6] = c_error[j], stc[j][7] = c_mid[j]
+  float stc[7][8];
   unsigned* bar;    // grid-reduction words (zeroed before the launch)
   double* slot;     // (grid, 2) per-workgroup partial sums
-  double* xs;       // (8, 2) per-XCD-group sums
-  double* tot;      // (2) the total
+  double* xs;       // (2, kDpGroups, 2) leaf sums, double-buffered by round parity
   int32_t* stats;   // nfev, attempts, status
   double* att;      // (max_att, 4): t0, dt, error ratio, accepted
   int32_t max_att;
 };
 
 // Grid-wide sum of two fp64 values, one per workgroup (valid on every lane of a one-wave
-// workgroup), returned to every workgroup in the same fixed summation order: each workgroup
-// stores its partial and arrives on the counter of its group (blockIdx % 8); the group's last
-// arriver sums the group's partials (lane-strided, xor tree) and arrives on the top counter; the
-// last of those sums the group sums in group order, publishes the total and bumps the generation
-// every workgroup polls.  Release before each arrival, acquire after the poll; all shared words
-// through agent-scope atomics (MI355X_MICROARCH.md, inter-workgroup visibility).  Every spin is
+// workgroup), returned to every workgroup in the same fixed summation order.  Round r:
+//   1. each workgroup stores its partial and arrives on one of kDpGroups leaf counters
+//      (blockIdx % kDpGroups, ~32 arrivals each at the 2048-workgroup grid: same-address atomics
+//      serialise at the memory side, ~25 ns each);
+//   2. the leaf's last arriver sums its leaf's partials (lane per partial, xor tree), stores the
+//      leaf sum in the round's buffer (r & 1) and bumps the monotonic top counter (kDpTopCopies
+//      replicas, one lane each);
+//   3. every workgroup polls its replica of the top counter until all leaves of round r have arrived, then sums
+//      the kDpGroups leaf sums itself (lane per leaf, xor tree: the same order everywhere).
+// Round r + 2 may overwrite buffer r & 1 only after every workgroup has arrived at round r + 1,
+// i.e. after it finished reading round r.  dp_order() between dependent steps.  Every spin is
 // bounded: after ~1 s the abort word is raised and every later reduction returns at once (the
 // grid was not co-resident); the caller reports status 4.
 constexpr unsigned kDpSpinLimit = 1u << 20;
-constexpr int kDpBarWords = 64 * 10;
-__device__ bool grid_sum2(const DopriParams& P, double v0, double v1, double& s0, double& s1) {
-  const unsigned blk = blockIdx.x, nblk = gridDim.x, x = blk & 7u;
-  const unsigned nx = (nblk + 7u - x) / 8u, ngrp = nblk < 8u ? nblk : 8u;
-  unsigned* cnt = P.bar + 64 * x;
-  unsigned* top = P.bar + 64 * 8;
-  unsigned* gen = P.bar + 64 * 9;
-  unsigned* abw = gen + 1;
+constexpr int kDpGroups = 64;
+constexpr int kDpLine = 64;  // words per counter line
+constexpr int kDpTopCopies = 8;  // replicas of the top counter: ~256 pollers per address, not 2048
+constexpr int kDpBarWords = kDpLine * (kDpGroups + 2 + kDpTopCopies);
+__device__ __forceinline__ unsigned* dp_cnt(const DopriParams& P, unsigned x) { return P.bar + kDpLine * x; }
+__device__ __forceinline__ unsigned* dp_top(const DopriParams& P, unsigned c) {
+  return P.bar + kDpLine * (kDpGroups + 2 + c);
+}
+__device__ __forceinline__ unsigned* dp_abort(const DopriParams& P) { return P.bar + kDpLine * (kDpGroups + 1); }
+
+// Ordering between the reduction's atomics.  Every word the reduction shares between workgroups
+// (partials, leaf sums, counters) is accessed only through agent-scope atomics, which are coherent
+// across the XCDs' L2s by themselves (sc1 loads / stores); what the protocol needs is only that a
+// store has landed before the arrival that publishes it, and that the reads after an arrival or a
+// poll start after it — a wait on the vector memory counter.  An agent-scope fence (or an
+// acquire / release atomic) would ALSO write back and invalidate the XCD's whole L2
+// (buffer_wbl2 / buffer_inv sc1) for plain loads and stores this protocol never shares: with 2048
+// workgroups arriving that cost ~50 us per reduction and evicted the field's parameters from L2.
+__device__ __forceinline__ void dp_order() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// One 16-byte {v0, v1} record per write-through (sc1) store / load: the hand-off forms of
+// MI355X_MICROARCH.md's table (16-B sc1 payload, vmcnt(0), then the counter add; loads only after
+// the add returned / the poll matched).  The load waits inside the asm (invisible to the compiler).
+typedef unsigned dp_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void dp_st16(double* p, double v0, double v1) {
+  const unsigned long long a = __double_as_longlong(v0), b = __double_as_longlong(v1);
+  const dp_u32x4 v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void dp_ld16(const double* p, double& v0, double& v1) {
+  dp_u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  v0 = __longlong_as_double(((unsigned long long)v.y << 32) | v.x);
+  v1 = __longlong_as_double(((unsigned long long)v.w << 32) | v.z);
+}
+
+__device__ __forceinline__ double xor_sum64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ bool grid_sum2(const DopriParams& P, unsigned& round, double v0, double v1, double& s0, double& s1) {
+#ifdef FETODE_EXP_NO_GRIDSUM  // diagnostics only: per-workgroup control, no synchronisation
+  s0 = v0 * gridDim.x;
+  s1 = v1 * gridDim.x;
+  return false;
+#endif
+  const unsigned blk = blockIdx.x, nblk = gridDim.x, x = blk % kDpGroups;
+  if (nblk == 1u) {  // one workgroup: the sums below would return v0, v1 exactly
+    s0 = v0;
+    s1 = v1;
+    return false;
+  }
+  const unsigned ngrp = nblk < (unsigned)kDpGroups ? nblk : (unsigned)kDpGroups;
+  const unsigned nx = (nblk + kDpGroups - 1u - x) / kDpGroups;
+  const unsigned r = round++;
+  double* xs = P.xs + 2 * kDpGroups * (r & 1u);
+  unsigned* abw = dp_abort(P);
   const int lane = threadIdx.x & 63;
   int ab = 0, leader = 0;
-  unsigned g = 0;
   if (lane == 0) {
     ab = __hip_atomic_load(abw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-    if (!ab) {
-      g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&P.slot[2 * blk], v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&P.slot[2 * blk + 1], v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      leader = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == nx - 1u;
-    }
+    dp_st16(&P.slot[2 * blk], v0, v1);
+    dp_order();
+    if (!ab)
+      leader = __hip_atomic_fetch_add(dp_cnt(P, x), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nx * (r + 1u) - 1u;
   }
   ab = __shfl(ab, 0);
   leader = __shfl(leader, 0);
   if (!ab && leader) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    dp_order();
     double a0 = 0.0, a1 = 0.0;
     for (unsigned j = lane; j < nx; j += 64) {
-      const unsigned bb = x + 8u * j;
-      a0 += __hip_atomic_load(&P.slot[2 * bb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      a1 += __hip_atomic_load(&P.slot[2 * bb + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      double u0, u1;
+      dp_ld16(&P.slot[2 * (x + kDpGroups * j)], u0, u1);
+      a0 += u0;
+      a1 += u1;
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      a0 += __shfl_xor(a0, o);
-      a1 += __shfl_xor(a1, o);
-    }
-    if (lane == 0) {
-      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&P.xs[2 * x], a0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&P.xs[2 * x + 1], a1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == ngrp - 1u) {
-        __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        double t0 = 0.0, t1 = 0.0;
-        for (unsigned u = 0; u < ngrp; ++u) {
-          t0 += __hip_atomic_load(&P.xs[2 * u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          t1 += __hip_atomic_load(&P.xs[2 * u + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        __hip_atomic_store(&P.tot[0], t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&P.tot[1], t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
+    a0 = xor_sum64(a0);
+    a1 = xor_sum64(a1);
+    if (lane == 0) dp_st16(&xs[2 * x], a0, a1);
+    dp_order();
+    if (lane < kDpTopCopies) __hip_atomic_fetch_add(dp_top(P, lane), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  double r0 = 0.0, r1 = 0.0;
   if (lane == 0 && !ab) {
+    const unsigned want = ngrp * (r + 1u);
     unsigned spins = 0;
-    while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+    // wrap-safe: (int)(top - want) < 0 while fewer than `want` leaf arrivals have landed
+    unsigned* top = dp_top(P, blk % kDpTopCopies);
+    while ((int)(__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
       __builtin_amdgcn_s_sleep(1);
-      if (__hip_atomic_load(abw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      if ((spins & 15u) == 15u && __hip_atomic_load(abw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         ab = 1;
         break;
       }
@@ -158,13 +195,13 @@ __device__ bool grid_sum2(const DopriParams& P, double v0, double v1, double& s0
         break;
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    r0 = __hip_atomic_load(&P.tot[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    r1 = __hip_atomic_load(&P.tot[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    dp_order();
   }
   ab = __shfl(ab, 0);
-  s0 = __shfl(r0, 0);
-  s1 = __shfl(r1, 0);
+  double u0 = 0.0, u1 = 0.0;
+  if ((unsigned)lane < ngrp && !ab) dp_ld16(&xs[2 * lane], u0, u1);
+  s0 = xor_sum64(u0);
+  s1 = xor_sum64(u1);
   return ab != 0;
 }
 
@@ -290,9 +327,10 @@ __device__ __forceinline__ float v4_edges(const V4Lds<IN, FLEN>& L, const float*
 }
 
 // HOT = true: the rk4 (3/8) integrate path only, every stage inlined, outputs predicated;
-// HOT = false: single evaluations and every other method.
+// HOT = false: single evaluations and every other method.  At least 2 waves per SIMD in every
+// variant: the resident dopri5 grid (DOPRI) needs B / 2 co-resident waves.
 template <int H, int K_, int NB, int NG, bool FERRO, bool HOT, bool DOPRI = false>
-__global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fused4_kernel(FusedArgs a) {
   constexpr int D = 2, NI = NG - 1, NFL = 1 + NB, NFP = (NFL + 1) & ~1, K = FERRO ? K_ : 0;
   // feature jobs: logistic 0..NB-1, SiLU, [gate, exp(gs x)], then x / u / m stores
   constexpr int J_SILU = NB, J_GATE = NB + 1, J_EXP = NB + 2, J_X = FERRO ? NB + 3 : NB + 1;
@@ -701,13 +739,17 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
       const bool real = valid && c1 == 0;  // one lane per (trajectory, state dim) in the sums
       const double n_el = (double)(a.B * D);
       int nfev = 0, n_att = 0, status = 0;
+      unsigned round = 0;
+#ifdef FETODE_EXP_NO_EVAL  // diagnostics only: a trivial field, the reductions and control as is
+      auto eval = [&](float xin) -> float { return -0.5f * xin; };
+#endif
       auto gsum2 = [&](double v0, double v1, double& s0, double& s1) {
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
           v0 += __shfl_xor(v0, o);
           v1 += __shfl_xor(v1, o);
         }
-        if (grid_sum2(P, v0, v1, s0, s1)) status = 4;
+        if (grid_sum2(P, round, v0, v1, s0, s1)) status = 4;
       };
       float f0 = eval(y);
       ++nfev;
@@ -730,7 +772,7 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
         const float d2 = fabsf(sqrtf((float)(s / n_el)) / h0);
         float h1;
         if (d1 <= 1e-15f && d2 <= 1e-15f) h1 = fmaxf(1e-6f, h0 * 1e-3f);
-        else h1 = powf(0.01f / fmaxf(d1, d2), 0.2f);
+        else h1 = (float)pow((double)(0.01f / fmaxf(d1, d2)), (double)0.2f);  // fp64 pow rounded once: host == device
         dt = (double)fminf(100.0f * h0, fabsf(h1));
       }
       float co[5] = {y, 0.f, 0.f, 0.f, 0.f};
@@ -748,26 +790,32 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
           // arrive: A[i] is stage s+1+i's sum k0 c0 + k1 c1 + ... (the same left-to-right sums)
           float A[6];
 #pragma unroll
-          for (int q = 0; q < 6; ++q) A[q] = f0 * (P.beta[q][0] * dt32);
-          float err = f0 * (P.cerr[0] * dt32);
-          float mid = f0 * (P.cmid[0] * dt32);
+          for (int q = 0; q < 6; ++q) A[q] = f0 * (P.stc[0][q] * dt32);
+          float err = f0 * (P.stc[0][6] * dt32);
+          float mid = f0 * (P.stc[0][7] * dt32);
           float yi = y, kn = f0;
 #pragma unroll 1
           for (int st = 0; st < 6; ++st) {
             yi = y + A[0];
+            // stage column st + 1 into SGPRs before the evaluation (the loads complete under it)
+            float c[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) c[q] = P.stc[st + 1][q];
             kn = eval(yi);
             ++nfev;
-            const int j = st + 1;
+            // entries past the tableau (coefficient 0) are never read again
 #pragma unroll
-            for (int q = 0; q < 5; ++q) A[q] = (j + q <= 5) ? A[q + 1] + kn * (P.beta[j + q][j] * dt32) : 0.f;
-            err = err + kn * (P.cerr[j] * dt32);
-            mid = mid + kn * (P.cmid[j] * dt32);
+            for (int q = 0; q < 5; ++q) A[q] = A[q + 1] + kn * (c[q] * dt32);
+            err = err + kn * (c[6] * dt32);
+            mid = mid + kn * (c[7] * dt32);
+            STAMP(6);
           }
           const float y1 = yi;
           const float tol = P.atol + P.rtol * fmaxf(fabsf(y), fabsf(y1));
           const float qe = err / tol;
           double s, nbad;
           gsum2(real ? (double)qe * qe : 0.0, (real && !__builtin_isfinite(y)) ? 1.0 : 0.0, s, nbad);
+          STAMP(1);
           if (status) break;
           if (nbad != 0.0) { status = 1; break; }
           const float ratio = sqrtf((float)(s / n_el));
@@ -806,6 +854,7 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
           }
           dt = __builtin_isnan(nxt) ? nxt : fmin(fmax(nxt, P.min_step), P.max_step);
           ++n_steps;
+          STAMP(7);
         }
         if (status) break;
         const float xq = (float)((next_t - t0s) / (t1s - t0s));  // interp._interp_evaluate
@@ -821,7 +870,7 @@ __global__ __launch_bounds__(64) void fused4_kernel(FusedArgs a) {
       if (blockIdx.x == 0 && tid == 0) {
         P.stats[0] = nfev;
         P.stats[1] = n_att;
-        P.stats[2] = __hip_atomic_load(P.bar + 64 * 9 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 4 : status;
+        P.stats[2] = __hip_atomic_load(P.bar + kDpLine * (kDpGroups + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 4 : status;
       }
     } else if (a.single_eval) {
       const float f = eval(y);
@@ -1371,7 +1420,7 @@ int fetode_field_forward(const fetode_field_t* f, const void* plan, const float*
 
 int64_t fetode_integrate_dopri5_workspace(int64_t B) {
   const int64_t grid = (B + 1) / 2;
-  return (int64_t)sizeof(unsigned) * kDpBarWords + (int64_t)sizeof(double) * (2 * grid + 16 + 2);
+  return (int64_t)sizeof(unsigned) * kDpBarWords + (int64_t)sizeof(double) * (2 * grid + 4 * kDpGroups);
 }
 
 int fetode_integrate_dopri5(const fetode_field_t* f, const void* plan, const float* y0, int64_t B, const double* t,
@@ -1424,14 +1473,15 @@ int fetode_integrate_dopri5(const fetode_field_t* f, const void* plan, const flo
   P.min_step = opts[4];
   P.max_step = opts[5];
   P.max_steps = opts[6] > 2e9 ? 2000000000 : (int)opts[6];
-  memcpy(P.beta, tableau, sizeof(float) * 36);
-  memcpy(P.cerr, tableau + 36, sizeof(float) * 7);
-  memcpy(P.cmid, tableau + 43, sizeof(float) * 7);
+  for (int j = 0; j < 7; ++j) {  // tableau = beta (6 x 6, row i = stage i + 1), c_error (7), c_mid (7)
+    for (int q = 0; q < 6; ++q) P.stc[j][q] = (j < 6 && j + q < 6) ? tableau[(j + q) * 6 + j] : 0.0f;
+    P.stc[j][6] = tableau[36 + j];
+    P.stc[j][7] = tableau[43 + j];
+  }
   P.bar = (unsigned*)workspace;
   double* d = (double*)((char*)workspace + sizeof(unsigned) * kDpBarWords);
   P.slot = d;
   P.xs = d + 2 * grid;
-  P.tot = P.xs + 16;
   P.stats = stats;
   P.att = attempts;
   P.max_att = attempts ? max_attempts : 0;

@@ -153,7 +153,8 @@ class _Dopri5:
         if d1 <= 1e-15 and d2 <= 1e-15:
             h1 = max(f32(1e-6), f32(h0 * f32(1e-3)))
         else:
-            h1 = f32(np.power(f32(0.01) / max(d1, d2), f32(1.0 / float(ORDER - 1 + 1))))
+            # fp32 power as fp64 pow rounded once (libm powf and the device's differ in the last ulp)
+            h1 = f32(np.power(np.float64(f32(0.01) / max(d1, d2)), np.float64(f32(1.0 / float(ORDER - 1 + 1)))))
         return float(min(f32(100 * h0), abs(h1)))
 
     def integrate(self, tp: torch.Tensor) -> torch.Tensor:
@@ -224,7 +225,7 @@ class _Dopri5:
 _TABLEAU = np.concatenate([np.concatenate([b, np.zeros(6 - len(b), np.float32)]) for b in BETA32]
                           + [CERR32, CMID32]).astype(np.float32)
 _RESIDENT_OPTS = {"first_step", "safety", "ifactor", "dfactor", "min_step", "max_step", "max_num_steps"}
-_MAX_TRACE = 4096
+_MAX_TRACE = 16384   # attempts logged per resident solve (the count itself is exact beyond it)
 
 
 class ResidentSolve:
@@ -248,7 +249,12 @@ class ResidentSolve:
 
     @property
     def attempts(self):
+        """(t0, dt, error ratio, accepted) of the first _MAX_TRACE attempts."""
         return self._load()[1]
+
+    @property
+    def n_attempts(self):
+        return int(self._stats.tolist()[1])
 
 
 _T_DEV = {}   # (device, time grid) -> the grid as a device fp64 tensor

@@ -29,3 +29,16 @@ def dev():
     if not torch.cuda.is_available():
         pytest.fail("gpu test requested but torch.cuda.is_available() is False")
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def kernel_switch():
+    """Force the fused integrator's kernel: small(True) -> v6 at any batch, small(False) -> v4."""
+    from fet_ode_amd import _lib
+    lib = _lib.load()
+    prev = lib.fetode_fused_set_small_batch_max(-1)
+
+    def small(on):
+        lib.fetode_fused_set_small_batch_max(1 << 40 if on else 0)
+    yield small
+    lib.fetode_fused_set_small_batch_max(prev)

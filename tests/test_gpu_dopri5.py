@@ -171,12 +171,18 @@ def test_dopri5_kanfet_trace_resident(dev):
 
 @pytest.mark.parametrize("B", [1, 64, 1000, 4096])
 @pytest.mark.parametrize("kind", ["kanfet", "kan"])
-def test_dopri5_resident_matches_host_driven(dev, B, kind):
-    """One cooperative launch vs the host-driven loop (one fused field launch per evaluation, the
-    error norm read back per attempt) on the same model and inputs: the same attempts (accept
-    pattern, step sizes), nfev, solution within 1e-5 per slice, the same final hysteresis state."""
+def test_dopri5_resident_matches_host_driven(dev, kernel_switch, B, kind):
+    """One cooperative launch vs the host-driven loop (one fused v4 field launch per evaluation,
+    the error norm read back per attempt) on the same model and inputs.  The field arithmetic is
+    the same and the norms are fp64 sums in both, so up to B = 1000 the attempt sequences and nfev
+    are identical, the step sizes equal up to the last ulp of fp64 pow (device libm vs host), the
+    solution and hysteresis state within 1e-6.  At B = 4096 the fp64 sums' order differs enough to
+    move a ratio by an fp32 ulp now and then, which the KAN-FET hysteresis amplifies — same accept
+    pattern and nfev, dt within 1e-5, solution within 1e-4.  (The host path below B = 512 would run v6, a different rounding of the same
+    field: tests/test_gpu_parity.py::test_small_batch_kernel_matches_v4 covers that pair.)"""
     import fet_ode_amd as F
     from fet_ode_amd.dopri5 import ResidentSolve, set_resident_dopri5
+    kernel_switch(False)
     gk = load_golden("traj_kanfet" if kind == "kanfet" else "traj_kan")
     y0 = torch.from_numpy(gk["y0_B64"]).repeat(64, 1)[:B].to(dev)
     t = torch.tensor([0.0, 0.2, 0.5], dtype=torch.float64)
@@ -194,11 +200,17 @@ def test_dopri5_resident_matches_host_driven(dev, B, kind):
         s = F.dopri5.dopri5_solve.last
         assert isinstance(s, ResidentSolve) == resident
         states = [l.ferro._prev.cpu() for l in m.layers] if kind == "kanfet" else []
-        out.append((sol, [(a[1], a[3]) for a in s.attempts], s.nfev, states))
+        out.append((sol, [(float(a[1]), float(a[3])) for a in s.attempts], s.nfev, states))
     (s0, a0, n0, st0), (s1, a1, n1, st1) = out
     assert n0 == n1 and [a[1] for a in a0] == [a[1] for a in a1]
-    np.testing.assert_allclose([a[0] for a in a0], [a[0] for a in a1], rtol=1e-6)
-    assert ((s0 - s1).norm(dim=(1, 2)) / s1.norm(dim=(1, 2)).clamp_min(1e-30)).max() <= 1e-5
+    if B <= 1000:   # the same fp32 arithmetic; dt differs at most by fp64 pow's last ulp
+        np.testing.assert_allclose([a[0] for a in a0], [a[0] for a in a1], rtol=1e-13)
+        assert ((s0 - s1).norm(dim=(1, 2)) / s1.norm(dim=(1, 2)).clamp_min(1e-30)).max() <= 1e-6
+        for a, b in zip(st0, st1):
+            assert ((a - b).norm() / b.norm()).item() <= 1e-6
+        return
+    np.testing.assert_allclose([a[0] for a in a0], [a[0] for a in a1], rtol=1e-5)
+    assert ((s0 - s1).norm(dim=(1, 2)) / s1.norm(dim=(1, 2)).clamp_min(1e-30)).max() <= 1e-4
     for a, b in zip(st0, st1):
         assert ((a - b).norm() / b.norm()).item() <= 1e-4
 

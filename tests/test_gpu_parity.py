@@ -356,19 +356,6 @@ def test_fused_rk4_kanfet_robust_subset_bench_config(dev):
     assert P.robust_parity_ok(st), st
 
 
-@pytest.fixture
-def kernel_switch():
-    """Force the fused integrator's kernel: small(True) -> v6 at any batch, small(False) -> v4."""
-    from fet_ode_amd import _lib
-    lib = _lib.load()
-    prev = lib.fetode_fused_set_small_batch_max(-1)
-
-    def small(on):
-        lib.fetode_fused_set_small_batch_max(1 << 40 if on else 0)
-    yield small
-    lib.fetode_fused_set_small_batch_max(prev)
-
-
 @pytest.mark.parametrize("B", [1, 7, 64, 512])
 @pytest.mark.parametrize("method", ["rk4", "rk4_classic", "midpoint", "euler"])
 def test_small_batch_kernel_matches_v4(dev, kernel_switch, B, method):
