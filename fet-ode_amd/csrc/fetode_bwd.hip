@@ -440,9 +440,12 @@ __device__ __forceinline__ void step_coefs(int method, float dt, float hh, float
 }
 
 constexpr int kTPB = 4;  // trajectories (waves) per workgroup, sharing one copy of the tables
+#ifndef FETODE_BWD_WAVES
+#define FETODE_BWD_WAVES 2  // minimum waves per SIMD the register allocation must allow
+#endif
 
 template <int D, int H, int K, int NB, int NG, bool FERRO>
-__global__ __launch_bounds__(64 * kTPB) void fixed_bwd_kernel(BwdArgs a) {
+__global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(FETODE_BWD_WAVES))) void fixed_bwd_kernel(BwdArgs a) {
   using L0 = BL<D, H, K, NB, NG, FERRO>;
   using L1 = BL<H, D, K, NB, NG, FERRO>;
   constexpr int W = D + H, NS = NG - 1 - kSO;

@@ -213,7 +213,8 @@ __global__ __launch_bounds__(256) void wide_gw_kernel(fetode_kanlinear_t kl, con
   __shared__ float Fs[4][kGwF][64];
   __shared__ float gs[64][16];
   __shared__ float gk[4][kGwNG];
-  __shared__ float lab[4][2 * kGwNB];
+  __shared__ float rk[4][3 * (kGwNG - 1)];  // 1 / (g[j+k] - g[j]) (bspline_local)
+  __shared__ float lab[4][2 * kGwNB];       // -a log2(e) | b
   __shared__ float sbs[kGwNS][256];
   const int in = kl.in_features, out = kl.out_features;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -223,8 +224,13 @@ __global__ __launch_bounds__(256) void wide_gw_kernel(fetode_kanlinear_t kl, con
   const int64_t c0 = sp * nch / kGwSplit, c1 = (sp + 1) * nch / kGwSplit;
   const bool lg = kl.num_logistic != 0;
   if (tid < 4 * kGwNG) gk[tid / kGwNG][tid % kGwNG] = kl.grid[(int64_t)i0 * kGwNG + tid];
+  if (tid < 4 * 3 * (kGwNG - 1)) {
+    const int ii = tid / (3 * (kGwNG - 1)), q = tid % (3 * (kGwNG - 1)), k = q / (kGwNG - 1) + 1, j = q % (kGwNG - 1);
+    const float* gg = kl.grid + (int64_t)(i0 + ii) * kGwNG;
+    rk[ii][q] = j + k < kGwNG ? 1.0f / (gg[j + k] - gg[j]) : 0.f;
+  }
   if (lg && tid < 4 * kGwNB) {
-    lab[tid / kGwNB][tid % kGwNB] = kl.logistic_a[(int64_t)i0 * kGwNB + tid];
+    lab[tid / kGwNB][tid % kGwNB] = -kl.logistic_a[(int64_t)i0 * kGwNB + tid] * FETODE_LOG2E;
     lab[tid / kGwNB][kGwNB + tid % kGwNB] = kl.logistic_b[(int64_t)i0 * kGwNB + tid];
   }
   gw_f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
@@ -234,14 +240,15 @@ __global__ __launch_bounds__(256) void wide_gw_kernel(fetode_kanlinear_t kl, con
     {  // features of (row b, input i0 + wv)
       const bool ok = b < B;
       const float xv = ok ? x[b * in + i0 + wv] : 0.f;
-      Fs[wv][0][lane] = ok ? xv * sigm(xv) : 0.f;   // the reference's base branch SiLU(x)
-      bspline_local_div<3>(xv, kGwNG, gk[wv], [&](int cc, float v) { sbs[cc][tid] = v; });
+      // the forward head's feature forms (fetode_mnist.hip wide_fwd_kernel): v_exp / v_rcp, spans
+      Fs[wv][0][lane] = ok ? silu(xv) : 0.f;   // the reference's base branch SiLU(x)
+      bspline_local<3>(xv, kGwNG, &gk[wv][0], &rk[wv][0], [&](int cc, float v) { sbs[cc][tid] = v; });
 #pragma unroll
       for (int k = 0; k < kGwNS; ++k) Fs[wv][1 + k][lane] = ok ? sbs[k][tid] : 0.f;
 #pragma unroll
       for (int j = 0; j < kGwNB; ++j)
         Fs[wv][1 + kGwNS + j][lane] =
-            (ok && lg) ? 2.0f / (1.0f + expf(-lab[wv][j] * (xv - lab[wv][kGwNB + j]))) : 0.f;
+            (ok && lg) ? 2.0f * sig_from_neg_l2((xv - lab[wv][kGwNB + j]) * lab[wv][j]) : 0.f;
     }
     for (int t = tid; t < 64 * 16; t += 256) {
       const int rr = t / 16, o = t % 16;

@@ -182,10 +182,16 @@ __global__ void column_sum_final_kernel(const double* __restrict__ mid, int n, f
 //   B (4 k x 16 outputs): lane (kq, o) holds Wp[4 g + kq, f, o] (o >= out: 0), read from LDS;
 //   one MFMA per (input group g, feature f).
 // A 256-thread workgroup = 4 waves x 16 rows; the inputs are split over gridDim.y (split-K) into
-// fixed chunks whose packed weights (and knots, logistic a / b) are staged in LDS for all 64 rows.
-// Partials (S, B, 16) are added in split order by a second kernel with the logistic bias.
+// fixed chunks whose packed weights (and knots, reciprocal knot spans, logistic -a log2(e) / b)
+// are staged in LDS for all 64 rows.  Partials (S, B, 16) are added in split order by a second
+// kernel with the logistic bias.
+// The features run on the transcendental unit directly (v_exp_f32, v_rcp_f32; 1 ulp each) and the
+// Cox-de Boor divisions are products with the staged reciprocal spans: IEEE expf and divisions
+// made ~650 VALU instructions per (row, input) and the head 385 us at B = 8192 (rocprofv3,
+// profiles/r02_mnist_pmc.txt); the feature error stays ~1e-7 relative, far inside the 1e-5 test
+// bar on the 1568 x 17-term sums.
 // =============================================================================================
-constexpr int kWideCh = 32;            // inputs per staged chunk
+constexpr int kWideCh = 16;            // inputs per staged chunk (LDS ~26 KB: 6 workgroups per CU)
 constexpr int kWideNS = 8, kWideNB = 8, kWideNG = 12;
 constexpr int kWideF = 1 + kWideNS + kWideNB;
 constexpr int kWideRows = 64;          // rows per workgroup (4 waves x 16)
@@ -219,8 +225,8 @@ __global__ __launch_bounds__(256) void wide_fwd_kernel(fetode_kanlinear_t kl, co
   __shared__ float ws[kWideCh * kWideF * 16];   // packed weights of the chunk
   __shared__ float xs[kWideRows][kWideCh + 1];  // the 64 rows' inputs of the chunk
   __shared__ float gk[kWideCh][kWideNG];        // knots
-  __shared__ float lab[kWideCh][2 * kWideNB];   // logistic a | b
-  __shared__ float sbs[kWideNS][256];            // each lane's spline bases (runtime-indexed writes)
+  __shared__ float rk[kWideCh][3 * (kWideNG - 1)];  // 1 / (g[j+k] - g[j]), k = 1..3 (bspline_local)
+  __shared__ float lab[kWideCh][2 * kWideNB];   // logistic -a log2(e) | b
   const int in = kl.in_features;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = lane & 15, kq = lane >> 4;
@@ -238,9 +244,14 @@ __global__ __launch_bounds__(256) void wide_fwd_kernel(fetode_kanlinear_t kl, co
       xs[rr][ii] = (row0 + rr < B && ii < ni) ? x[(row0 + rr) * in + i0 + ii] : 0.f;
     }
     for (int t = tid; t < ni * kWideNG; t += 256) gk[t / kWideNG][t % kWideNG] = kl.grid[(int64_t)i0 * kWideNG + t];
+    for (int t = tid; t < ni * 3 * (kWideNG - 1); t += 256) {
+      const int ii = t / (3 * (kWideNG - 1)), q = t % (3 * (kWideNG - 1)), k = q / (kWideNG - 1) + 1, j = q % (kWideNG - 1);
+      const float* g = kl.grid + (int64_t)(i0 + ii) * kWideNG;
+      rk[ii][q] = j + k < kWideNG ? 1.0f / (g[j + k] - g[j]) : 0.f;
+    }
     if (lg)
       for (int t = tid; t < ni * kWideNB; t += 256) {
-        lab[t / kWideNB][t % kWideNB] = kl.logistic_a[(int64_t)i0 * kWideNB + t];
+        lab[t / kWideNB][t % kWideNB] = -kl.logistic_a[(int64_t)i0 * kWideNB + t] * FETODE_LOG2E;
         lab[t / kWideNB][kWideNB + t % kWideNB] = kl.logistic_b[(int64_t)i0 * kWideNB + t];
       }
     __syncthreads();
@@ -248,13 +259,15 @@ __global__ __launch_bounds__(256) void wide_fwd_kernel(fetode_kanlinear_t kl, co
       const int il = 4 * g + kq;
       const float xi = xs[wv * 16 + r][il];
       float feat[kWideF];
-      feat[0] = xi / (1.0f + expf(-xi));  // SiLU, efficientkan.py:166 / mnist :131
-      bspline_local_div<3>(xi, kWideNG, gk[il], [&](int cc, float v) { sbs[cc][tid] = v; });
+      feat[0] = silu(xi);  // SiLU, efficientkan.py:166 / mnist :131
+      // runtime-indexed basis writes as register select chains (no LDS round trip)
+      bspline_local<3>(xi, kWideNG, &gk[il][0], &rk[il][0], [&](int cc, float v) {
 #pragma unroll
-      for (int k = 0; k < kWideNS; ++k) feat[1 + k] = sbs[k][tid];
+        for (int k = 0; k < kWideNS; ++k) feat[1 + k] = k == cc ? v : feat[1 + k];
+      });
 #pragma unroll
-      for (int j = 0; j < kWideNB; ++j)
-        feat[1 + kWideNS + j] = lg ? 2.0f / (1.0f + expf(-lab[il][j] * (xi - lab[il][kWideNB + j]))) : 0.f;
+      for (int j = 0; j < kWideNB; ++j)  // 2 sigmoid(a (x - b)), mnist_kuramoto_kan.py:22
+        feat[1 + kWideNS + j] = lg ? 2.0f * sig_from_neg_l2((xi - lab[il][kWideNB + j]) * lab[il][j]) : 0.f;
       const float* wrow = ws + (il * kWideF) * 16 + r;   // lane (kq, o = r): Wp[i, f, o]
 #pragma unroll
       for (int f = 0; f < kWideF; ++f) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(feat[f], wrow[f * 16], acc, 0, 0, 0);

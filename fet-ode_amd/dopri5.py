@@ -263,6 +263,13 @@ _T_DEV = {}   # (device, time grid) -> the grid as a device fp64 tensor
 atexit.register(_T_DEV.clear)
 
 
+def _drop_last_solve():
+    dopri5_solve.last = None   # the last solve's device buffers (resident stats / attempt log, k)
+
+
+atexit.register(_drop_last_solve)
+
+
 def _try_ecg_resident(func, y0, tp, reversed_, rtol, atol, options):
     """The whole solve in one launch when `func` is the ECG field (No_MLP_KANODEFunc with the
     sigmoid mixer), nothing needs gradients, and the options are the scalar ones."""

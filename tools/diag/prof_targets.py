@@ -1,5 +1,6 @@
 """Small driver for rocprofv3 PMC passes: the wide KAN-FET layer kernels at the ETT widths
-(B = 8192) and the MNIST KANLinear head (B = 8192), a few launches each."""
+(B = 8192), the MNIST KANLinear head (B = 8192) and the LV training step (B = 4096 rk4 forward
+with tape + the fused reverse sweep), a few launches each.  argv[1] / $PROF_WHICH selects one."""
 import os
 import sys
 
@@ -11,7 +12,7 @@ import fet_ode_amd as F  # noqa: E402
 from fet_ode_amd import mnist  # noqa: E402
 
 dev = torch.device("cuda:0")
-which = sys.argv[1] if len(sys.argv) > 1 else "all"
+which = sys.argv[1] if len(sys.argv) > 1 else os.environ.get("PROF_WHICH", "all")
 with torch.no_grad():
     if which in ("all", "wide"):
         for (i, o) in [(64, 128), (128, 64)]:
@@ -22,9 +23,22 @@ with torch.no_grad():
                 m(x)
     if which in ("all", "mnist"):
         torch.manual_seed(0)
-        head = mnist.KANLinear(1568, 10).to(dev)
+        clf = mnist.KuramotoKANClassifier().to(dev)          # the bench's classifier (head nb 8)
         xh = torch.rand(8192, 1568, device=dev) * 2 - 1
+        img = torch.rand(8192, 1, 28, 28, device=dev)
         for _ in range(5):
-            head(xh)
+            clf.head(xh)
+            clf(img)
+    torch.cuda.synchronize()
+if which in ("all", "train"):
+    import numpy as np
+    import bench
+    torch.manual_seed(0)
+    m = F.KANFET([2, 10, 2], grid_size=5).to(dev)
+    y0 = bench.lv_y0(4096, 0).to(dev)
+    t = torch.tensor(np.linspace(0, 3.5, 35))
+    for _ in range(4):
+        m.zero_grad()
+        F.odeint(F.autonomous(m), y0, t, method="rk4").square().mean().backward()
     torch.cuda.synchronize()
 print("done")
