@@ -110,7 +110,9 @@ SIGNATURES = {
     "fetode_ferro_backward": (ctypes.c_int, [ctypes.POINTER(FerroDesc), _vp, ctypes.c_int64, _vp, ctypes.c_int32,
                                              _vp, _vp, ctypes.POINTER(FerroGrad), ctypes.c_int32, _vp]),
     "fetode_fused_backward_supported": (ctypes.c_int, [ctypes.POINTER(FieldDesc)]),
-    "fetode_integrate_fixed_backward_workspace": (ctypes.c_int64, [ctypes.POINTER(FieldDesc), ctypes.c_int64]),
+    "fetode_backward_set_split": (ctypes.c_int, [ctypes.c_int32]),
+    "fetode_integrate_fixed_backward_workspace": (ctypes.c_int64, [ctypes.POINTER(FieldDesc), ctypes.c_int32,
+                                                                  ctypes.c_int32, ctypes.c_int64]),
     "fetode_integrate_fixed_backward": (ctypes.c_int, [ctypes.POINTER(FieldDesc), _vp, ctypes.c_int32, ctypes.c_int64,
                                                        _vp, ctypes.c_int32, _vp, _vp, _vp, ctypes.c_int32,
                                                        _vp, _vp, _vp, ctypes.c_uint32, _vp,
@@ -167,7 +169,7 @@ def load() -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.fetode_abi_version() != 1:
+    if lib.fetode_abi_version() != 2:
         raise FetodeError("libfetode ABI version mismatch")
     _lib = lib
     return lib

@@ -29,7 +29,9 @@
 //                       dbias = coef G_o, dcoef = Ps A + bias G_o
 //   KAN (o,i):          base = sum g_o SiLU(x_i), spline_c = sum g_o B_c(x_i)
 //   logistic (o,i,j):   sum g_o sigmoid_ij;  a_ij, b_ij directly.
+#include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "fetode_common.h"
 
@@ -80,6 +82,9 @@ struct BL {  // compile-time shape of one layer
   static constexpr int RF = (E + 63) / 64, RE = (NE + 63) / 64, RL = (NL + 63) / 64;
   static constexpr int RF1 = RF > 0 ? RF : 1, RL1 = RL > 0 ? RL : 1;
   static constexpr int LPI = pow2_floor(64 / IN);  // lanes per input in the d/dx segmented sum
+  // cb row pitch: NTM rounded up to LPI mod 32, so the LPI-lane groups of one half-wave read
+  // distinct LDS banks in reduce_gin (a pitch of 32 put all ten inputs of layer 1 on banks 0-3)
+  static constexpr int NTMP = LPI >= 32 ? NTM : NTM + ((LPI - NTM % 32) % 32 + 32) % 32;
   static_assert(IN <= 64 && OUT <= 64, "layer widths up to 64");
   static_assert(NS >= 1, "grid too small for cubic splines");
 };
@@ -291,7 +296,7 @@ __device__ __forceinline__ void feat_input(BFeat<W, NG - 1 - kSO, NB>& F, const 
 
 // the VJP jobs of one layer (inputs at combined offset TB) for one evaluation: gradient sums into
 // R, d out/d x contributions into cb[i * NTM + t]
-template <class L, int TB, class FT>
+template <class L, int TB, bool ACC, class FT>
 __device__ __forceinline__ void layer_jobs(const FT& F, const float* __restrict__ gout, const BTab<L>& Tb,
                                            const float* __restrict__ rhs, BReg<L>& R, float* __restrict__ cb,
                                            float gsl2e, float wc, float gs, int lane, int z) {
@@ -311,16 +316,21 @@ __device__ __forceinline__ void layer_jobs(const FT& F, const float* __restrict_
         const float sh = ffma(Ec, mm, x);                     // shifted_x
         const float th = ffma(-2.0f, sigm_l2(2.0f * FETODE_LOG2E * kk * sh), 1.0f);  // tanh(k sh)
         const float q = go * ffma(-th, th, 1.0f);
-        R.A[r] = ffma(go, th, R.A[r]);
-        R.C[r] = ffma(q, sh, R.C[r]);
+        if constexpr (ACC) {
+          R.A[r] = ffma(go, th, R.A[r]);
+          R.C[r] = ffma(q, sh, R.C[r]);
+        }
         const float dcn = gs * cn * (1.0f - cn), du = gs * up * omu;
-        const float dmdEc = -wc * omu * dcn;
-        R.Ev[r] = ffma(q, ffma(Ec, dmdEc, mm), R.Ev[r]);
+        if constexpr (ACC) {
+          const float dmdEc = -wc * omu * dcn;
+          R.Ev[r] = ffma(q, ffma(Ec, dmdEc, mm), R.Ev[r]);
+        }
         const float dmdx = -wc * ffma(du, cn, omu * dcn);
-        cb[i * L::NTM + ok_] = q * pe.z * ffma(Ec, dmdx, 1.0f);
+        cb[i * L::NTMP + ok_] = q * pe.z * ffma(Ec, dmdx, 1.0f);
       }
     }
-    if (lane < L::OUT) R.G += gout[lane];
+    if constexpr (ACC)
+      if (lane < L::OUT) R.G += gout[lane];
   }
 #pragma unroll
   for (int r = 0; r < L::RE; ++r) {
@@ -328,9 +338,11 @@ __device__ __forceinline__ void layer_jobs(const FT& F, const float* __restrict_
     if (q < L::NE) {
       const int o = q / L::IN, i = q % L::IN;
       const float go = gout[o];
-      R.base[r] = ffma(go, F.silu[TB + i], R.base[r]);
+      if constexpr (ACC) {
+        R.base[r] = ffma(go, F.silu[TB + i], R.base[r]);
 #pragma unroll
-      for (int c = 0; c < L::NS; ++c) R.spl[r][c] = ffma(go, F.bd[(TB + i) * L::NS + c], R.spl[r][c]);
+        for (int c = 0; c < L::NS; ++c) R.spl[r][c] = ffma(go, F.bd[(TB + i) * L::NS + c], R.spl[r][c]);
+      }
       const int m = F.m[TB + i];
       const float u = F.u[TB + i];
       float dsdx;
@@ -341,7 +353,7 @@ __device__ __forceinline__ void layer_jobs(const FT& F, const float* __restrict_
         dsdx = u * 0.0f;  // 0 outside the grid, NaN for non-finite inputs (the reference's NaN bases)
       }
       const float wb = Tb.kw[o * (L::IN * L::NFL) + i * L::NFL + z];
-      cb[i * L::NTM + L::OUT * L::K + o] = go * ffma(wb, F.dsilu[TB + i], dsdx);
+      cb[i * L::NTMP + L::OUT * L::K + o] = go * ffma(wb, F.dsilu[TB + i], dsdx);
     }
   }
 #pragma unroll
@@ -355,13 +367,15 @@ __device__ __forceinline__ void layer_jobs(const FT& F, const float* __restrict_
       for (int o = 0; o < L::OUT; ++o) {
         const float go = gout[o];
         S = ffma(go, Tb.kw[o * (L::IN * L::NFL) + i * L::NFL + 1 + j + z], S);
-        R.lw[r][o] = ffma(go, s, R.lw[r][o]);
+        if constexpr (ACC) R.lw[r][o] = ffma(go, s, R.lw[r][o]);
       }
       const float T = S * ds;  // kw holds 2 * scaled logistic weight: d(2 sigmoid) folded in
       const float pa = Tb.pa[q + z];
-      R.la[r] = ffma(T, x - Tb.pb[q + z], R.la[r]);
-      R.lb[r] = ffma(-T, pa, R.lb[r]);
-      cb[i * L::NTM + L::OUT * L::K + L::OUT + j] = T * pa;
+      if constexpr (ACC) {
+        R.la[r] = ffma(T, x - Tb.pb[q + z], R.la[r]);
+        R.lb[r] = ffma(-T, pa, R.lb[r]);
+      }
+      cb[i * L::NTMP + L::OUT * L::K + L::OUT + j] = T * pa;
     }
   }
 }
@@ -374,7 +388,7 @@ __device__ __forceinline__ void reduce_gin(const float* __restrict__ cb, float* 
   float s = 0.f;
   if (i < L::IN) {
 #pragma unroll
-    for (int t = sub; t < L::NTM; t += LPI) s += cb[i * L::NTM + t];
+    for (int t = sub; t < L::NTM; t += LPI) s += cb[i * L::NTMP + t];
   }
   s = group_sum<LPI>(s);
   if (i < L::IN && sub == 0) gin[i] = s;
@@ -398,8 +412,9 @@ struct BwdArgs {
   const float* state0;  // hysteresis state before the solve (include/fetode.h layout)
   uint32_t init_mask;
   float* gy0;           // (B, D) or null
-  float* part;          // (gridDim.x * kTPB, nacc)
+  float* part;          // (rows, nacc)
   int32_t nacc;
+  float* gadj;          // (n_evals, B, D + H): d loss / d k (D) and d loss / d h (H) per evaluation
 };
 
 // stage-combine coefficients of one step in the forward's fp32 arithmetic (odeint.py
@@ -444,12 +459,16 @@ constexpr int kTPB = 4;  // trajectories (waves) per workgroup, sharing one copy
 #define FETODE_BWD_WAVES 2  // minimum waves per SIMD the register allocation must allow
 #endif
 
-template <int D, int H, int K, int NB, int NG, bool FERRO>
-__global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(FETODE_BWD_WAVES))) void fixed_bwd_kernel(BwdArgs a) {
+// ACC = true: the whole reverse sweep in one kernel — adjoints and the parameter-gradient sums (in
+// VGPRs, one partial row per wave).  ACC = false: the adjoint sweep only (no sums: 118 VGPRs, four
+// waves per SIMD, all B = 4096 trajectories resident at once); it records every evaluation's
+// output and hidden adjoints in a.gadj and param_sum_kernel forms the sums in parallel.
+template <int D, int H, int K, int NB, int NG, bool FERRO, bool ACC>
+__global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ? FETODE_BWD_WAVES : 4))) void fixed_bwd_kernel(BwdArgs a) {
   using L0 = BL<D, H, K, NB, NG, FERRO>;
   using L1 = BL<H, D, K, NB, NG, FERRO>;
   constexpr int W = D + H, NS = NG - 1 - kSO;
-  constexpr int CB = L0::IN * L0::NTM > L1::IN * L1::NTM ? L0::IN * L0::NTM : L1::IN * L1::NTM;
+  constexpr int CB = L0::IN * L0::NTMP > L1::IN * L1::NTMP ? L0::IN * L0::NTMP : L1::IN * L1::NTMP;
   static_assert(W <= 64, "one lane per input");
   __shared__ BInTab<W, NG, NB> TI;
   __shared__ BTab<L0> T0;
@@ -465,8 +484,10 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(FETOD
   T1.stage(a.k1, a.f1, a.plan, a.P1, threadIdx.x, 64 * kTPB);
   BReg<L0> R0;
   BReg<L1> R1;
-  R0.zero();
-  R1.zero();
+  if constexpr (ACC) {
+    R0.zero();
+    R1.zero();
+  }
   __syncthreads();  // tables staged; from here on every wave syncs only with itself
 
   BFeat<W, NS, NB>& F = sF[wid];
@@ -545,11 +566,16 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(FETOD
         for (int q = lane; q < W * NB; q += 64)
           F.sg[q] = sigm_l2(ffma(TI.lg[2 * q + z], F.x[q / NB], TI.lg[2 * q + 1 + z]));
         wsync();
-        layer_jobs<L1, D>(F, g1, T1, TI.rh, R1, cb, gl1, wc1, gs1, lane, z);
+        layer_jobs<L1, D, ACC>(F, g1, T1, TI.rh, R1, cb, gl1, wc1, gs1, lane, z);
         wsync();
         reduce_gin<L1>(cb, g0, lane);  // d loss / d h
         wsync();
-        layer_jobs<L0, 0>(F, g0, T0, TI.rh, R0, cb, gl0, wc0, gs0, lane, z);
+        if constexpr (!ACC) {  // this evaluation's adjoints for param_sum_kernel
+          float* gr = a.gadj + ((int64_t)ev * a.B + b) * W;
+          if (lane < D) gr[lane] = g1[lane];
+          else if (lane < W) gr[lane] = g0[lane - D];
+        }
+        layer_jobs<L0, 0, ACC>(F, g0, T0, TI.rh, R0, cb, gl0, wc0, gs0, lane, z);
         wsync();
         reduce_gin<L0>(cb, gx, lane);
         wsync();
@@ -567,9 +593,217 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(FETOD
     if (lane < D && a.gy0) a.gy0[b * D + lane] = ay1 + a.gsol[b * D + lane];  // solution[0] = y0
     wsync();
   }
-  float* part = a.part + ((int64_t)blockIdx.x * kTPB + wid) * a.nacc;
-  R0.store(part, lane);
-  R1.store(part + L0::AL.n, lane);
+  if constexpr (ACC) {
+    float* part = a.part + ((int64_t)blockIdx.x * kTPB + wid) * a.nacc;
+    R0.store(part, lane);
+    R1.store(part + L0::AL.n, lane);
+  }
+}
+
+// Parameter-gradient sums of one layer from the recorded adjoints (after fixed_bwd_kernel<ACC =
+// false>): every sample (evaluation ev, trajectory b) is independent, so the sums are formed
+// element-major — a thread owns fixed jobs of the layer (a Ferro element, a KAN edge, one or two
+// logistic (input, basis) pairs) with their sums in a few VGPRs, and walks its block's samples in
+// tiles of TS whose per-input features (SiLU, dense B-spline bases, hysteresis gate, logistic
+// sigmoids) are computed once per tile into LDS.  The per-sample arithmetic is layer_jobs'; only
+// the summation order differs (per block, samples in (ev, b) order; blocks in a fixed order).
+// Jobs (256 threads): Ferro element e = tid (E = 200); edge q = tid - E (NE = 20; the i = 0 edge of
+// output o also sums G_o); logistic (i, j) jobs tid - E - NE and, if NL exceeds what is left, a
+// second one on threads 0.. (L1: 36 + 64 of 100).
+constexpr int kPsTS = 32;  // samples per tile
+template <int D, int H, int K, int NB, int NG, int LAYER>
+__global__ __launch_bounds__(256) void param_sum_kernel(BwdArgs a) {
+  using LA = BL<D, H, K, NB, NG, true>;
+  using LB = BL<H, D, K, NB, NG, true>;
+  using L = typename std::conditional<LAYER == 0, LA, LB>::type;
+  constexpr int W = D + H, NS = NG - 1 - kSO, NI = NG - 1, TS = kPsTS;
+  constexpr int IN = L::IN, OUT = L::OUT, E = L::E, NE = L::NE, NL = L::NL;
+  constexpr int TB = LAYER == 0 ? 0 : D;          // the layer's inputs in a tape row
+  constexpr int GB = LAYER == 0 ? D : 0;          // its output adjoints in a gadj row (h | k)
+  constexpr int J1 = 256 - E - NE;                 // logistic jobs of the first round
+  static_assert(E + NE <= 256 && NL <= J1 + 64 && (NL <= J1 || NL - J1 <= E), "param_sum job map");
+  constexpr AccLayout AL = L::AL;
+  __shared__ BInTab<W, NG, NB> TI;
+  __shared__ BTab<L> Tb;
+  __shared__ float sx[TS][IN], sup[TS][IN], ssl[TS][IN], sgo[TS][OUT];
+  __shared__ float sbd[TS][IN][NS + 1];            // +1: no bank aliasing between inputs
+  __shared__ float ssg[TS][IN * NB];
+  const int tid = threadIdx.x;
+  const LayerPlan& P = LAYER == 0 ? a.P0 : a.P1;
+  TI.stage(a.plan, a.P0, a.P1, D, tid, 256);
+  Tb.stage(LAYER == 0 ? a.k0 : a.k1, LAYER == 0 ? a.f0 : a.f1, a.plan, P, tid, 256);
+  const float gsl = P.gsl2e, wc = P.wc, gs = (float)(LAYER == 0 ? a.f0.gate_slope : a.f1.gate_slope);
+  const uint32_t imask = (a.init_mask >> LAYER) & 1u;
+  const int64_t N = (int64_t)a.n_steps * (a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4
+                                          : a.method == FETODE_MIDPOINT ? 2 : 1) * a.B;
+  const int64_t n0 = (int64_t)blockIdx.x * N / gridDim.x, n1 = (int64_t)(blockIdx.x + 1) * N / gridDim.x;
+  __syncthreads();
+
+  // this thread's jobs and their constants
+  const bool fjob = tid < E;
+  const int e = fjob ? tid : 0, fi = e / (OUT * K), fo = (e % (OUT * K)) / K;
+  const float4 fe = Tb.fe[e];
+  const bool ejob = tid >= E && tid < E + NE;
+  const int q = ejob ? tid - E : 0, eo = q / IN, ei = q % IN;
+  const int lq0 = tid - E - NE;
+  const bool ljob0 = lq0 >= 0 && lq0 < NL;
+  const bool ljob1 = NL > J1 && tid < NL - J1;
+  const int l0 = ljob0 ? lq0 : 0, l1 = ljob1 ? J1 + tid : 0;
+  float A = 0.f, C = 0.f, Ev = 0.f, G = 0.f, base = 0.f, spl[NS];
+#pragma unroll
+  for (int c = 0; c < NS; ++c) spl[c] = 0.f;
+  float lw0[OUT], lw1[OUT], la0 = 0.f, lb0 = 0.f, la1 = 0.f, lb1 = 0.f;
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) lw0[o] = lw1[o] = 0.f;
+  auto logistic = [&](int ql, int s, float* lw, float& la, float& lb) __attribute__((always_inline)) {
+    const int i = ql / NB, j = ql % NB;
+    const float sg = ssg[s][ql], ds = sg * (1.0f - sg), x = sx[s][i];
+    float S = 0.f;
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) {
+      const float go = sgo[s][o];
+      S = ffma(go, Tb.kw[o * (IN * L::NFL) + i * L::NFL + 1 + j], S);
+      lw[o] = ffma(go, sg, lw[o]);
+    }
+    const float T = S * ds;
+    la = ffma(T, x - Tb.pb[ql], la);
+    lb = ffma(-T, Tb.pa[ql], lb);
+  };
+
+  // the tile's raw inputs (x, prev, output adjoints) are fetched one tile ahead, into registers,
+  // while the current tile's jobs run
+  constexpr int KI = (TS * IN + 255) / 256, KO = (TS * OUT + 255) / 256;
+  float px[KI], pp[KI], pg[KO];
+  auto fetch = [&](int64_t tt) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      const int it = tid + 256 * k, s = it / IN, i = it % IN;
+      const int64_t n = tt + s;
+      px[k] = pp[k] = 0.f;
+      if (it < TS * IN && n < n1) {
+        const int64_t ev = n / a.B;
+        px[k] = a.tape[n * W + TB + i];
+        if (ev > 0) pp[k] = a.tape[(n - a.B) * W + TB + i];
+        else if (!imask) pp[k] = a.state0[(LAYER == 0 ? (n % a.B) * D : a.B * D + (n % a.B) * H) + i];
+        else pp[k] = px[k];  // the tape_at(-1) rule: first call, dx = 0
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KO; ++k) {
+      const int it = tid + 256 * k, s = it / OUT, o = it % OUT;
+      pg[k] = (it < TS * OUT && tt + s < n1) ? a.gadj[(tt + s) * W + GB + o] : 0.f;
+    }
+  };
+  fetch(n0);
+  for (int64_t t0 = n0; t0 < n1; t0 += TS) {
+    // ---- per-tile features (one thread per (sample, input)) ----
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      const int it = tid + 256 * k;
+      if (it >= TS * IN) break;
+      const int s = it / IN, i = it % IN, t = TB + i;
+      const float x = px[k], pv = pp[k];
+      // SiLU, interval, dense bases and gate: feat_input's arithmetic
+      const float sx_ = sigm_l2(-x * FETODE_LOG2E);
+      ssl[s][i] = x * sx_;
+      int m = -1;
+#pragma unroll
+      for (int jj = 0; jj < NG; ++jj) m += (x >= TI.knots[t * NG + jj]) ? 1 : 0;
+      const bool fin = __builtin_isfinite(x);
+      const bool in = fin && m >= 0 && m < NI;
+      const int mc = in ? m : 0;
+      const float u = in ? (x - TI.knots[t * NG + mc]) * TI.rh[t * NI + mc] : (fin ? 0.f : __builtin_nanf(""));
+      const float fill = fin ? 0.f : __builtin_nanf("");
+      float bd[NS];
+#pragma unroll
+      for (int c = 0; c < NS; ++c) bd[c] = fill;
+      if (in) {
+#pragma unroll
+        for (int r = 0; r <= kSO; ++r) {
+          const int c = mc - kSO + r;
+          const float4 p = TI.bp[(t * NI + mc) * 4 + r];
+          const float v = ffma(ffma(ffma(p.w, u, p.z), u, p.y), u, p.x);
+#pragma unroll
+          for (int cc = 0; cc < NS; ++cc) bd[cc] = cc == c ? v : bd[cc];
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < NS; ++c) sbd[s][i][c] = bd[c];
+      sx[s][i] = x;
+      sup[s][i] = sigm_l2(-gsl * (x - pv));
+    }
+#pragma unroll
+    for (int k = 0; k < KO; ++k) {  // the layer's output adjoints
+      const int it = tid + 256 * k;
+      if (it < TS * OUT) sgo[it / OUT][it % OUT] = pg[k];
+    }
+    __syncthreads();  // sx of the tile (the logistic sigmoids read it)
+    for (int it = tid; it < TS * IN * NB; it += 256) {
+      const int s = it / (IN * NB), ql = it % (IN * NB), i = ql / NB;
+      const int qq = (TB * NB) + ql;  // combined (t, j) index of the lg table
+      ssg[s][ql] = sigm_l2(ffma(TI.lg[2 * qq], sx[s][i] , TI.lg[2 * qq + 1]));
+    }
+    __syncthreads();
+    if (t0 + TS < n1) fetch(t0 + TS);
+    const int ns = (int)(n1 - t0 < TS ? n1 - t0 : TS);
+    // ---- jobs: each thread walks the tile's samples ----
+    if (fjob) {
+      for (int s = 0; s < ns; ++s) {  // layer_jobs' Ferro element VJP, sums only
+        const float x = sx[s][fi], up = sup[s][fi], go = sgo[s][fo];
+        const float kk = fe.x, Ec = fe.y;
+        const float cn = sigm_l2(gsl * (x + Ec));
+        const float omu = 1.0f - up;
+        const float mm = ffma(wc, omu * cn, 1.0f);
+        const float sh = ffma(Ec, mm, x);
+        const float th = ffma(-2.0f, sigm_l2(2.0f * FETODE_LOG2E * kk * sh), 1.0f);
+        const float qv = go * ffma(-th, th, 1.0f);
+        A = ffma(go, th, A);
+        C = ffma(qv, sh, C);
+        const float dcn = gs * cn * (1.0f - cn);
+        const float dmdEc = -wc * omu * dcn;
+        Ev = ffma(qv, ffma(Ec, dmdEc, mm), Ev);
+      }
+    }
+    if (ejob) {
+      for (int s = 0; s < ns; ++s) {
+        const float go = sgo[s][eo];
+        base = ffma(go, ssl[s][ei], base);
+#pragma unroll
+        for (int c = 0; c < NS; ++c) spl[c] = ffma(go, sbd[s][ei][c], spl[c]);
+        G += go;  // read only on the i = 0 edge of each output
+      }
+    }
+    if (ljob0)
+      for (int s = 0; s < ns; ++s) logistic(l0, s, lw0, la0, lb0);
+    if (ljob1)
+      for (int s = 0; s < ns; ++s) logistic(l1, s, lw1, la1, lb1);
+    __syncthreads();
+  }
+  // ---- this block's partial row (the layer's half; the other launch writes the other half) ----
+  float* part = a.part + (int64_t)blockIdx.x * a.nacc + (LAYER == 0 ? 0 : LA::AL.n);
+  if (fjob) {
+    part[AL.oA + e] = A;
+    part[AL.oC + e] = C;
+    part[AL.oE + e] = Ev;
+  }
+  if (ejob) {
+    if (ei == 0) part[AL.oG + eo] = G;
+    part[AL.oBase + q] = base;
+#pragma unroll
+    for (int c = 0; c < NS; ++c) part[AL.oSpl + q * NS + c] = spl[c];
+  }
+  if (ljob0) {
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) part[AL.oLw + o * NL + l0] = lw0[o];
+    part[AL.oLa + l0] = la0;
+    part[AL.oLb + l0] = lb0;
+  }
+  if (ljob1) {
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) part[AL.oLw + o * NL + l1] = lw1[o];
+    part[AL.oLa + l1] = la1;
+    part[AL.oLb + l1] = lb1;
+  }
 }
 
 // partial rows -> chunk sums (fp64), fixed order
@@ -662,12 +896,32 @@ typedef void (*bwd_fn)(BwdArgs);
 struct BwdEntry {
   int D, H, K, NB, NG;
   bool ferro;
-  bwd_fn fn;
+  bwd_fn fn;                   // the one-kernel sweep (sums in VGPRs)
+  bwd_fn adj, sum0, sum1;      // the split: adjoint sweep + per-layer parameter sums (or null)
 };
 const BwdEntry kBwd[] = {
-    {2, 10, 10, 10, 12, true, fixed_bwd_kernel<2, 10, 10, 10, 12, true>},   // LV KAN-FET [2,10,2]
-    {2, 10, 0, 10, 12, false, fixed_bwd_kernel<2, 10, 1, 10, 12, false>},   // LV KAN [2,10,2]
+    // LV KAN-FET [2,10,2]: the split (the one-kernel sweep needs 239 VGPRs: two rounds of waves)
+    {2, 10, 10, 10, 12, true, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true>,
+     fixed_bwd_kernel<2, 10, 10, 10, 12, true, false>, param_sum_kernel<2, 10, 10, 10, 12, 0>,
+     param_sum_kernel<2, 10, 10, 10, 12, 1>},
+    // LV KAN [2,10,2] (126 VGPRs: four waves per SIMD already)
+    {2, 10, 0, 10, 12, false, fixed_bwd_kernel<2, 10, 1, 10, 12, false, true>, nullptr, nullptr, nullptr},
 };
+// Which path the KAN-FET sweep takes (fetode_backward_set_split; env FETODE_BWD_SPLIT).  Default:
+// the one-kernel sweep — measured on MI355X at B = 4096, rk4, 34 steps: one kernel 1.06 ms vs the
+// split 0.69 (adjoint sweep) + 0.25 + 0.31 (layer sums) ms (profiles/r02_split_pmc.txt).
+int g_bwd_split = -1;
+bool use_split(const BwdEntry* e) {
+  if (g_bwd_split < 0) {
+    const char* v = getenv("FETODE_BWD_SPLIT");
+    g_bwd_split = v ? atoi(v) != 0 : 0;
+  }
+  return e->adj && g_bwd_split != 0;
+}
+constexpr int64_t kSumBlocks = 1024;  // param_sum_kernel blocks per layer (= partial rows)
+int64_t n_evals_of(int32_t method, int32_t n_steps) {
+  return (int64_t)n_steps * (method == FETODE_RK4 || method == FETODE_RK4_CLASSIC ? 4 : method == FETODE_MIDPOINT ? 2 : 1);
+}
 
 const BwdEntry* find_bwd(const fetode_field_t* f) {
   if (f->n_layers != 2) return nullptr;
@@ -708,19 +962,36 @@ void layouts(const fetode_field_t* f, AccLayout* L0, AccLayout* L1) {
 
 extern "C" {
 
+int fetode_backward_set_split(int32_t enable) {
+  use_split(&kBwd[0]);  // resolve the env default first
+  const int prev = g_bwd_split;
+  if (enable >= 0) g_bwd_split = enable != 0;
+  return prev;
+}
+
 int fetode_fused_backward_supported(const fetode_field_t* f) {
   if (validate_field(f) != FETODE_OK) return 0;
   return find_bwd(f) != nullptr;
 }
 
-int64_t fetode_integrate_fixed_backward_workspace(const fetode_field_t* f, int64_t B) {
-  if (validate_field(f) != FETODE_OK || !find_bwd(f) || B <= 0) return -1;
+// partial rows of the chosen path: one per wave (one-kernel sweep) or per param_sum block (split)
+int64_t sum_rows(const BwdEntry* e, int64_t B, int64_t n_ev) {
+  if (!use_split(e)) return bwd_rows(B);
+  const int64_t tiles = (n_ev * B + kPsTS - 1) / kPsTS;
+  return tiles < kSumBlocks ? (tiles > 0 ? tiles : 1) : kSumBlocks;
+}
+
+int64_t fetode_integrate_fixed_backward_workspace(const fetode_field_t* f, int32_t method, int32_t n_steps, int64_t B) {
+  if (validate_field(f) != FETODE_OK || !find_bwd(f) || B <= 0 || n_steps < 0) return -1;
+  const BwdEntry* e = find_bwd(f);
   AccLayout L0, L1;
   layouts(f, &L0, &L1);
   const int64_t nacc = L0.n + L1.n;
-  const int64_t nrow = bwd_rows(B);
+  const int64_t n_ev = n_evals_of(method, n_steps);
+  const int64_t nrow = sum_rows(e, B, n_ev);
   const int64_t nch = nrow < kChunks ? nrow : kChunks;
-  return (int64_t)sizeof(double) * nacc * (nch + 1) + (int64_t)sizeof(float) * nrow * nacc;
+  const int64_t adj = use_split(e) ? n_ev * B * (f->kan[0].in_features + f->kan[0].out_features) : 0;
+  return (int64_t)sizeof(double) * nacc * (nch + 1) + (int64_t)sizeof(float) * (nrow * nacc + adj);
 }
 
 int fetode_integrate_fixed_backward(const fetode_field_t* f, const void* plan, int32_t method, int64_t B,
@@ -743,11 +1014,14 @@ int fetode_integrate_fixed_backward(const fetode_field_t* f, const void* plan, i
   AccLayout AL0, AL1;
   layouts(f, &AL0, &AL1);
   const int nacc = AL0.n + AL1.n;
-  const int64_t nrow = bwd_rows(B);
+  const bool split = use_split(e);
+  const int64_t n_ev = n_evals_of(method, n_steps);
+  const int64_t nrow = sum_rows(e, B, n_ev);
   const int64_t nch = nrow < kChunks ? nrow : kChunks;
   double* S = (double*)workspace;
   double* chunks = S + nacc;
   float* part = (float*)(chunks + nch * nacc);
+  float* gadj = part + nrow * nacc;  // (n_ev, B, D + H), split path only
 
   BwdArgs a;
   memset(&a, 0, sizeof(a));
@@ -775,8 +1049,24 @@ int fetode_integrate_fixed_backward(const fetode_field_t* f, const void* plan, i
   a.gy0 = grad_y0;
   a.part = part;
   a.nacc = nacc;
-  hipLaunchKernelGGL(e->fn, dim3((unsigned)(nrow / kTPB)), dim3(64 * kTPB), 0, s, a);
-  LAUNCH_CHECK();
+  a.gadj = gadj;
+  if (split) {
+    // adjoint sweep: one wave per trajectory, every trajectory resident (grid-stride beyond)
+    const int64_t blocks = (B + kTPB - 1) / kTPB;
+    hipLaunchKernelGGL(e->adj, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(64 * kTPB), 0, s, a);
+    LAUNCH_CHECK();
+    if (n_ev > 0) {
+      hipLaunchKernelGGL(e->sum0, dim3((unsigned)nrow), dim3(256), 0, s, a);
+      LAUNCH_CHECK();
+      hipLaunchKernelGGL(e->sum1, dim3((unsigned)nrow), dim3(256), 0, s, a);
+      LAUNCH_CHECK();
+    } else {
+      HIP_CHECK_RET(hipMemsetAsync(part, 0, sizeof(float) * nrow * nacc, s));
+    }
+  } else {
+    hipLaunchKernelGGL(e->fn, dim3((unsigned)(nrow / kTPB)), dim3(64 * kTPB), 0, s, a);
+    LAUNCH_CHECK();
+  }
   const int64_t per = (nrow + nch - 1) / nch;
   hipLaunchKernelGGL(part_reduce_kernel, dim3(nblk(nacc, 64), (unsigned)nch), dim3(64), 0, s, part, nrow, nacc, per,
                      chunks);

@@ -228,7 +228,7 @@ class _FusedFixedFn(torch.autograd.Function):
             kg[l] = _lib.KANLinearGrad(*[_lib.ptr(gbuf(p)) for p in kan_params(kan)])
             if fg is not None:
                 fg[l] = _lib.FerroGrad(*[_lib.ptr(gbuf(getattr(fer, n))) for n in FERRO_PARAM_NAMES])
-        nbytes = lib.fetode_integrate_fixed_backward_workspace(handle.ref, B)
+        nbytes = lib.fetode_integrate_fixed_backward_workspace(handle.ref, ctx.method, sched.n_steps, B)
         if nbytes < 0:
             _lib.check(_lib.FETODE_EUNSUPPORTED, "fetode_integrate_fixed_backward_workspace")
         ws = torch.empty(max(1, nbytes // 4), device=dev, dtype=torch.float32)

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define FETODE_ABI_VERSION 1
+#define FETODE_ABI_VERSION 2
 
 enum {
   FETODE_OK = 0,
@@ -254,8 +254,15 @@ int fetode_ferro_backward(const fetode_ferro_t* layer, const float* x, int64_t B
  * detached prev_x :381-382), the stage combines and the output interpolation.
  * 1 if a fused backward kernel exists for this field shape (the fused forward's shapes). */
 int fetode_fused_backward_supported(const fetode_field_t* field);
-/* Workspace bytes for fetode_integrate_fixed_backward at batch B. */
-int64_t fetode_integrate_fixed_backward_workspace(const fetode_field_t* field, int64_t B);
+/* The KAN-FET sweep's structure: 0 = one kernel (adjoints and parameter-gradient sums together,
+ * the default), 1 = split (an adjoint sweep that records every evaluation's adjoints, then the
+ * parameter sums of each layer in parallel over the samples).  Same results up to fp32 summation
+ * order.  Returns the previous setting; enable < 0 only queries.  Call before sizing workspaces. */
+int fetode_backward_set_split(int32_t enable);
+/* Workspace bytes for fetode_integrate_fixed_backward of a (method, n_steps) forward at batch B
+ * (the split path records every evaluation's adjoints: n_evals * B * (D + H) floats of it). */
+int64_t fetode_integrate_fixed_backward_workspace(const fetode_field_t* field, int32_t method, int32_t n_steps,
+                                                  int64_t B);
 /* The schedule arguments are the forward's.  grad_solution (T, B, D) = d loss / d solution;
  * tape = the forward's tape; state0 (B*state_width) = the hysteresis state BEFORE the forward
  * solve (nullable when every init_mask bit is set), init_mask = the forward's.

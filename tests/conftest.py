@@ -42,3 +42,13 @@ def kernel_switch():
         lib.fetode_fused_set_small_batch_max(1 << 40 if on else 0)
     yield small
     lib.fetode_fused_set_small_batch_max(prev)
+
+
+@pytest.fixture(params=[0, 1], ids=["one-kernel", "split"])
+def bwd_split(request):
+    """Run a fused-backward test through both sweep structures (fetode_backward_set_split)."""
+    from fet_ode_amd import _lib
+    lib = _lib.load()
+    prev = lib.fetode_backward_set_split(request.param)
+    yield request.param
+    lib.fetode_backward_set_split(prev)

@@ -205,7 +205,7 @@ def test_fused_backward_kan_vs_oracle_fp64(dev, method):
 
 
 @pytest.mark.parametrize("method", ["rk4", "rk4_classic", "midpoint", "euler"])
-def test_fused_backward_kanfet_vs_oracle_fp64(dev, method):
+def test_fused_backward_kanfet_vs_oracle_fp64(dev, bwd_split, method):
     """KAN-FET, 6 points (short enough to be well conditioned in fp32), B=16, every method."""
     from oracle import torch_ref as O
     g = load_golden("traj_kanfet")
@@ -218,7 +218,7 @@ def test_fused_backward_kanfet_vs_oracle_fp64(dev, method):
         assert_grad_close(got[n], exp[n], n, rel=1e-3)
 
 
-def test_fused_backward_interpolated_outputs_and_reversed_time(dev):
+def test_fused_backward_interpolated_outputs_and_reversed_time(dev, bwd_split):
     """step_size grid with outputs between grid points (linear interpolation adjoint) and a
     decreasing t (sign-flipped steps)."""
     from oracle import torch_ref as O
@@ -243,7 +243,7 @@ def test_fused_backward_interpolated_outputs_and_reversed_time(dev):
         assert_grad_close(got[n], exp[n], n, rel=1e-4)
 
 
-def test_fused_backward_first_call_rules(dev):
+def test_fused_backward_first_call_rules(dev, bwd_split):
     """B=1 fresh module (prev_x = zeros, dx = x) and B>1 fresh (dx = 0) as the backward's
     evaluation 0 (ferro_class.py:373-375), and a second solve that starts from the stored state."""
     import fet_ode_amd as F
@@ -302,7 +302,7 @@ def test_fused_backward_matches_per_stage_path_large_batch(dev):
         assert_grad_close(res[0][n], res[1][n], n, rel=1e-4)
 
 
-def test_fused_backward_deterministic(dev):
+def test_fused_backward_deterministic(dev, bwd_split):
     """Two identical training solves give bitwise-identical gradients (fixed-order reductions)."""
     import fet_ode_amd as F
     from oracle import torch_ref as O
