@@ -33,6 +33,11 @@ using namespace fetode;
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 splat(float v) { return f2{v, v}; }
+__device__ __forceinline__ f2 ex2x2(f2 v) { return f2{ex2(v.x), ex2(v.y)}; }
+__device__ __forceinline__ f2 rcpx2(f2 v) { return f2{rcp(v.x), rcp(v.y)}; }
 
 constexpr int kWF = 20;       // KAN features per input: SiLU, B_0..B_7, phi_0..phi_9, 0
 constexpr int kNS = 8, kNB = 10, kNG = 12;
@@ -235,6 +240,7 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
   constexpr int KP = FERRO ? K : 1;
   constexpr int kPitch = pitch_of(kCh);
   static_assert(kCh * kRows <= kThreads && (kCh & 1) == 0, "one staging item per thread, even chunks");
+  static_assert(!FERRO || K % 2 == 0, "Ferro elements in (k, k+1) pairs");
   __shared__ float s_x[kCh * kRows], s_w[kCh * kRows], s_e[kCh * kRows];
   __shared__ float4 s_par[kOuts * kCh * KP];  // the chunk's Ferro constants, read as wave broadcasts
   __shared__ float s_dfl[kOuts * kCh];
@@ -346,15 +352,19 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
           const float4* par = &s_par[(jo * kCh + ii) * K];
           float acc = 0.f;
           if (!xbig && s_dfl[jo * kCh + ii] == 0.f) {
+            // elements (k, k+1) in the two halves of packed-fp32 VALU ops (v_pk_fma / mul / add:
+            // 3.5 instead of 7 non-transcendental issues per element); even and odd k sum apart
+            f2 acc2 = splat(0.0f);
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-              const float4 p = par[k];  // {P, k2, k2Ec, cps}, same address on every lane
-              const float sg = rcp(ffma(e, p.x, 1.0f));
-              const float mm = ffma(wg, sg, 1.0f);
-              const float z = ffma(p.z, mm, p.y * xv);
-              const float th = ffma(-2.0f, rcp(ex2(z) + 1.0f), 1.0f);
-              acc = ffma(p.w, th, acc);
+            for (int k = 0; k < K; k += 2) {
+              const float4 p0 = par[k], p1 = par[k + 1];  // {P, k2, k2Ec, cps}, same address on every lane
+              const f2 sg = rcpx2(pfma(splat(e), f2{p0.x, p1.x}, splat(1.0f)));
+              const f2 mm = pfma(splat(wg), sg, splat(1.0f));
+              const f2 z = pfma(f2{p0.z, p1.z}, mm, f2{p0.y, p1.y} * splat(xv));
+              const f2 th = pfma(splat(-2.0f), rcpx2(ex2x2(z) + splat(1.0f)), splat(1.0f));
+              acc2 = pfma(f2{p0.w, p1.w}, th, acc2);
             }
+            acc = acc2.x + acc2.y;
           } else {
             const float* gec = plan + L.gec + ((int64_t)(o0 + jo) * in + i) * K;
 #pragma unroll
