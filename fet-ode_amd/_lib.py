@@ -224,3 +224,10 @@ class FieldHandle:
     @property
     def ref(self):
         return ctypes.byref(self.desc)
+
+    def supported(self, lib) -> bool:
+        """fetode_fused_supported for this descriptor (asked once per handle)."""
+        s = self.__dict__.get("_supported")
+        if s is None:
+            s = self._supported = bool(lib.fetode_fused_supported(self.ref))
+        return s

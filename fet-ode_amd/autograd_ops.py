@@ -222,20 +222,36 @@ def field_layers(model):
     return out
 
 
-def _handle_key(model, B, device):
-    """Identity of every tensor the descriptor points at, or None when a tensor would be
-    converted (non-fp32 / non-contiguous) — the converted copy could go stale silently."""
-    key = [B, str(device)]
-    for k, f in field_layers(model):
-        ts = [k.grid, *[p for p in kan_params(k) if p is not None]]
+def _field_tensors(model):
+    """Every tensor a field descriptor points at, read straight from the modules' parameter /
+    buffer dicts (nn.Module.__getattr__ costs ~0.3 us per access; this runs on every solve)."""
+    ts = []
+    for l in model.layers.__dict__["_modules"].values():
+        md = l.__dict__["_modules"]
+        k, f = (md["kan"], md["ferro"]) if "kan" in md else (l, None)
+        kp, kb = k.__dict__["_parameters"], k.__dict__["_buffers"]
+        ts.append(kb["grid"])
+        ts += [t for t in kp.values() if t is not None]
+        lb = k.__dict__["_modules"].get("logistic_basis")
+        if lb is not None:
+            ts += [t for t in lb.__dict__["_parameters"].values() if t is not None]
         if f is not None:
-            ts += [getattr(f, n) for n in FERRO_PARAM_NAMES]
-            if f._bsign is not None:
-                ts.append(f._bsign)
-        for t in ts:
-            if t.dtype != torch.float32 or not t.is_contiguous():
-                return None
-            key += [t.data_ptr(), t._version, t.shape[0]]
+            ts += [t for t in f.__dict__["_parameters"].values() if t is not None]
+            b = f.__dict__["_buffers"].get("_bsign")
+            if b is not None:
+                ts.append(b)
+    return ts
+
+
+def _handle_key(model, B, device):
+    """Identity (storage, version counter, leading size) of every tensor the descriptor points
+    at, or None when a tensor would be converted (non-fp32 / non-contiguous) — the converted copy
+    could go stale silently."""
+    key = [B, device]
+    for t in _field_tensors(model):
+        if t.dtype != torch.float32 or not t.is_contiguous():
+            return None
+        key += [t.data_ptr(), t._version, t.shape[0]]
     return tuple(key)
 
 
@@ -243,7 +259,7 @@ def make_handle(model, B: int, device) -> _lib.FieldHandle:
     """Descriptor of the field (+ explicit branch_sign tensors; None = ones), cached on the model
     while no parameter has been replaced or modified in place (tensor version counters)."""
     key = _handle_key(model, B, device)
-    cached = getattr(model, "_fetode_handle", None)
+    cached = model.__dict__.get("_fetode_handle")
     if key is not None and cached is not None and cached[0] == key:
         return cached[1]
     keep = []
@@ -263,11 +279,21 @@ def make_handle(model, B: int, device) -> _lib.FieldHandle:
 
 
 def _state_views(buf, model, B):
+    """The per-layer (B, in_l) views of the state buffer, made once per buffer (slicing and
+    view() cost a few us each on every solve otherwise)."""
+    cached = model.__dict__.get("_fetode_views")
+    if cached is not None and cached[0] is buf and cached[1] == B:
+        return cached[2]
     views, off = [], 0
     for _, f in field_layers(model):
         views.append(buf[B * off:B * (off + f.in_dim)].view(B, f.in_dim))
         off += f.in_dim
+    model.__dict__["_fetode_views"] = (buf, B, views)
     return views
+
+
+def _ferro_modules(model):
+    return [l.__dict__["_modules"]["ferro"] for l in model.layers.__dict__["_modules"].values()]
 
 
 def pack_state(model, B: int, device):
@@ -276,31 +302,38 @@ def pack_state(model, B: int, device):
     of that buffer between calls, so packing costs nothing in steady state.  Returns the buffer
     and the init-mask bits of the layers whose stored state does not match the batch
     (ferro_class.py:373-375 re-initialisation rule)."""
-    layers = field_layers(model)
-    if layers[0][1] is None:
+    if not model.has_ferro:
         return None, 0
-    W = sum(f.in_dim for _, f in layers)
-    buf = getattr(model, "_fetode_state", None)
+    fs = _ferro_modules(model)
+    W = sum(f.in_dim for f in fs)
+    buf = model.__dict__.get("_fetode_state")
     if buf is None or buf.numel() != B * W or buf.device != device:
         buf = torch.zeros(B * W, device=device, dtype=torch.float32)
         model._fetode_state = buf
     mask = 0
-    for l, ((_, f), v) in enumerate(zip(layers, _state_views(buf, model, B))):
-        p = f._prev
+    for l, (f, v) in enumerate(zip(fs, _state_views(buf, model, B))):
+        bufs = f.__dict__["_buffers"]
+        p = bufs["_prev"]
+        if p is v:   # steady state: the layer's prev_x already is this view
+            continue
         if p.shape[0] != B or p.device != device or p.dtype != torch.float32:
             mask |= 1 << l
         elif p.data_ptr() != v.data_ptr():
             v.copy_(p)
-        f._prev = v
+        bufs["_prev"] = v   # what Module.__setattr__ does for a registered buffer
     return buf, mask
 
 
 def unpack_state(model, state: torch.Tensor):
-    B = state.numel() // sum(f.in_dim for _, f in field_layers(model))
-    for (_, f), v in zip(field_layers(model), _state_views(state, model, B)):
-        f._prev = v
-        if f._bsign is not None and f._bsign.shape[0] != B:
-            f._bsign = None
+    fs = _ferro_modules(model)
+    B = state.numel() // sum(f.in_dim for f in fs)
+    for f, v in zip(fs, _state_views(state, model, B)):
+        bufs = f.__dict__["_buffers"]
+        if bufs["_prev"] is not v:
+            bufs["_prev"] = v
+        b = bufs.get("_bsign")
+        if b is not None and b.shape[0] != B:
+            bufs["_bsign"] = None
 
 
 def _fused_eval(model, handle, x):

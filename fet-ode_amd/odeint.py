@@ -16,6 +16,7 @@ Two execution paths, both HIP:
 """
 from __future__ import annotations
 
+import atexit
 import math
 import os
 from typing import Dict, Optional, Tuple
@@ -257,6 +258,25 @@ def set_fused_training(enabled: bool) -> bool:
     return prev
 
 
+def _fused_infer(field, handle, method, y0, sched):
+    """_FusedFixedFn.forward without autograd (no tape): the inference solve's host side is
+    ~100 us of Python per call otherwise — as long as the whole B = 512 kernel of an 8-way
+    strong-scaled shard."""
+    dev = y0.device
+    B, D = y0.shape
+    plan = build_plan(field, handle, dev)
+    state, mask = pack_state(field, B, dev)
+    _, coef, ostep, omode, oslope = sched.device_arrays(dev)
+    sol = torch.empty(sched.T, B, D, device=dev, dtype=torch.float32)
+    _lib.check(_lib.load().fetode_integrate_fixed(
+        handle.ref, plan.data_ptr(), method, y0.data_ptr(), B, coef.data_ptr(), sched.n_steps,
+        ostep.data_ptr(), omode.data_ptr(), oslope.data_ptr(), sched.T, sol.data_ptr(),
+        _lib.ptr(state), mask, None, _lib.stream_handle(dev)), "fetode_integrate_fixed")
+    if state is not None:
+        unpack_state(field, state)
+    return sol
+
+
 def _try_fused(func, y0, sched, method_code):
     field = fused_field(func)
     if field is None or y0.dim() != 2:
@@ -264,8 +284,10 @@ def _try_fused(func, y0, sched, method_code):
     B = y0.shape[0]
     handle = make_handle(field, B, y0.device)
     lib = _lib.load()
-    if not lib.fetode_fused_supported(handle.ref):
+    if not handle.supported(lib):
         return None
+    if not torch.is_grad_enabled():
+        return _fused_infer(field, handle, method_code, y0.contiguous(), sched)
     params = [p for p in field.parameters()]
     training = grad_enabled_for(y0, *params)
     if training:
@@ -374,6 +396,22 @@ def _per_stage_fixed(func, y0, sched: Schedule, method: str, tc_dtype, reversed_
 # public entry
 # ---------------------------------------------------------------------------------------------
 
+_LAST_T = [None, None, None, None]   # the last t tensor, its version, method, checked inputs
+atexit.register(lambda: _LAST_T.__setitem__(slice(None), [None] * 4))   # before the runtime's teardown
+
+
+def _check_inputs_cached(y0, t, method):
+    """_check_inputs, reusing the result while the same t tensor comes back unmodified (a
+    training / bench loop passes one t object: the checks are several small CPU tensor ops)."""
+    if (isinstance(t, torch.Tensor) and _LAST_T[0] is t and _LAST_T[1] == t._version and _LAST_T[2] == method
+            and isinstance(y0, torch.Tensor) and torch.is_floating_point(y0)):
+        return _LAST_T[3]
+    r = _check_inputs(y0, t, method)
+    if isinstance(t, torch.Tensor):
+        _LAST_T[:] = [t, t._version, method, r]
+    return r
+
+
 def odeint(func, y0, t, *, rtol=1e-7, atol=1e-9, method=None, options=None, event_fn=None):
     """torchdiffeq.odeint(func, y0, t, *, rtol, atol, method, options, event_fn) on the GPU.
 
@@ -382,7 +420,7 @@ def odeint(func, y0, t, *, rtol=1e-7, atol=1e-9, method=None, options=None, even
     """
     if event_fn is not None:
         raise NotImplementedError("event_fn is not on the hot path")
-    method, tc, tp, reversed_ = _check_inputs(y0, t, method)
+    method, tc, tp, reversed_ = _check_inputs_cached(y0, t, method)
     _lib.require_gpu_tensor(y0, "odeint")
     options = dict(options or {})
     if method == "dopri5":
