@@ -745,10 +745,11 @@ __global__ __launch_bounds__(256) void param_sum_kernel(BwdArgs a) {
     }
     __syncthreads();
     if (t0 + TS < n1) fetch(t0 + TS);
-    const int ns = (int)(n1 - t0 < TS ? n1 - t0 : TS);
-    // ---- jobs: each thread walks the tile's samples ----
+    // ---- jobs: each thread walks the tile's samples (all TS: samples past the block's range
+    // have x = prev = 0 and zero adjoints, so they add exact zeros; unrolled for ILP) ----
     if (fjob) {
-      for (int s = 0; s < ns; ++s) {  // layer_jobs' Ferro element VJP, sums only
+#pragma unroll 4
+      for (int s = 0; s < TS; ++s) {  // layer_jobs' Ferro element VJP, sums only
         const float x = sx[s][fi], up = sup[s][fi], go = sgo[s][fo];
         const float kk = fe.x, Ec = fe.y;
         const float cn = sigm_l2(gsl * (x + Ec));
@@ -765,7 +766,8 @@ __global__ __launch_bounds__(256) void param_sum_kernel(BwdArgs a) {
       }
     }
     if (ejob) {
-      for (int s = 0; s < ns; ++s) {
+#pragma unroll 4
+      for (int s = 0; s < TS; ++s) {
         const float go = sgo[s][eo];
         base = ffma(go, ssl[s][ei], base);
 #pragma unroll
@@ -773,10 +775,14 @@ __global__ __launch_bounds__(256) void param_sum_kernel(BwdArgs a) {
         G += go;  // read only on the i = 0 edge of each output
       }
     }
-    if (ljob0)
-      for (int s = 0; s < ns; ++s) logistic(l0, s, lw0, la0, lb0);
-    if (ljob1)
-      for (int s = 0; s < ns; ++s) logistic(l1, s, lw1, la1, lb1);
+    if (ljob0) {
+#pragma unroll 4
+      for (int s = 0; s < TS; ++s) logistic(l0, s, lw0, la0, lb0);
+    }
+    if (ljob1) {
+#pragma unroll 4
+      for (int s = 0; s < TS; ++s) logistic(l1, s, lw1, la1, lb1);
+    }
     __syncthreads();
   }
   // ---- this block's partial row (the layer's half; the other launch writes the other half) ----

@@ -1,5 +1,6 @@
 """Small driver for rocprofv3 PMC passes: the wide KAN-FET layer kernels at the ETT widths
-(B = 8192), the MNIST KANLinear head (B = 8192) and the LV training step (B = 4096 rk4 forward
+(B = 8192), the MNIST KANLinear head (B = 8192), the LV rk4 solve at the strong-scaling shard
+(B = 512, v6) and the full batch (B = 4096, v4), and the LV training step (B = 4096 rk4 forward
 with tape + the fused reverse sweep), a few launches each.  argv[1] / $PROF_WHICH selects one."""
 import os
 import sys
@@ -29,6 +30,18 @@ with torch.no_grad():
         for _ in range(5):
             clf.head(xh)
             clf(img)
+    torch.cuda.synchronize()
+if which in ("all", "small"):   # the strong-scaling shard (v6, B = 512) next to the full batch (v4)
+    import numpy as np
+    import bench
+    torch.manual_seed(0)
+    m = F.KANFET([2, 10, 2], grid_size=5).to(dev)
+    t = torch.tensor(np.linspace(0, 3.5, 35))
+    with torch.no_grad():
+        for B in (512, 4096):
+            y0 = bench.lv_y0(B, 0).to(dev)
+            for _ in range(4):
+                F.odeint(F.autonomous(m), y0, t, method="rk4")
     torch.cuda.synchronize()
 if which in ("all", "train"):
     import numpy as np
