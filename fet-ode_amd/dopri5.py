@@ -225,6 +225,59 @@ class _Dopri5:
 _TABLEAU = np.concatenate([np.concatenate([b, np.zeros(6 - len(b), np.float32)]) for b in BETA32]
                           + [CERR32, CMID32]).astype(np.float32)
 _RESIDENT_OPTS = {"first_step", "safety", "ifactor", "dfactor", "min_step", "max_step", "max_num_steps"}
+
+
+def _raise_status(status: int, timeout_msg: str):
+    if status == 1:
+        raise AssertionError("non-finite values in state `y`")
+    if status == 2:
+        raise AssertionError("underflow in dt")
+    if status == 3:
+        raise AssertionError("max_num_steps exceeded")
+    if status == 4:
+        raise RuntimeError(timeout_msg)
+
+
+_DEFERRED: list = []   # (stats, message) of resident solves whose status a caller checks later
+_DEFER = [0]
+
+
+class deferred_status:
+    """Inside this context the resident solvers do not read their status word back at once (one
+    device->host read = a full synchronisation per solve); `check_deferred()` — which the context
+    calls on exit — raises torchdiffeq's assertion of the first failed solve.  Used by model
+    forwards that launch more work after the solve (KanFet_NODE: the classifier), so the host
+    does not wait for the solve before issuing it; the exception still comes out of the same
+    forward call."""
+
+    def __enter__(self):
+        _DEFER[0] += 1
+        return self
+
+    def __exit__(self, exc_type, exc, tb):
+        _DEFER[0] -= 1
+        if _DEFER[0] == 0:
+            if exc_type is None:
+                check_deferred()
+            else:
+                _DEFERRED.clear()
+        return False
+
+
+def check_deferred():
+    pending = list(_DEFERRED)
+    _DEFERRED.clear()
+    for stats, msg in pending:
+        _raise_status(int(stats[2].item()), msg)
+
+
+def _status_check(stats, timeout_msg):
+    """torchdiffeq's assertions from the kernel's status word (one read per solve), or queued
+    for `check_deferred` inside `deferred_status`."""
+    if _DEFER[0]:
+        _DEFERRED.append((stats, timeout_msg))
+        return
+    _raise_status(int(stats[2].item()), timeout_msg)
 _MAX_TRACE = 16384   # attempts logged per resident solve (the count itself is exact beyond it)
 
 
@@ -328,17 +381,9 @@ def _try_ecg_resident(func, y0, tp, reversed_, rtol, atol, options):
         return None
     _lib.check(rc, "fetode_ecg_dopri5")   # prev_x was rewritten in place (read before, written after)
     basis.branch_state = branch
-    status = int(stats[2].item())   # one read per solve: torchdiffeq's assertions
-    if status == 1:
-        raise AssertionError("non-finite values in state `y`")
-    if status == 2:
-        raise AssertionError("underflow in dt")
-    if status == 3:
-        raise AssertionError("max_num_steps exceeded")
-    if status == 4:
-        raise RuntimeError("fetode_ecg_dopri5: a grid barrier timed out (workgroups not co-resident); "
-                           "the solution is invalid")
     dopri5_solve.last = ResidentSolve(stats, att)
+    _status_check(stats, "fetode_ecg_dopri5: a grid barrier timed out (workgroups not co-resident); "
+                         "the solution is invalid")
     return sol
 
 
@@ -390,17 +435,9 @@ def _try_field_resident(func, y0, tp, reversed_, rtol, atol, options):
     _lib.check(rc, "fetode_integrate_dopri5")
     if state is not None:
         unpack_state(field, state)
-    status = int(stats[2].item())   # one read per solve: torchdiffeq's assertions
-    if status == 1:
-        raise AssertionError("non-finite values in state `y`")
-    if status == 2:
-        raise AssertionError("underflow in dt")
-    if status == 3:
-        raise AssertionError("max_num_steps exceeded")
-    if status == 4:
-        raise RuntimeError("fetode_integrate_dopri5: a grid reduction timed out (workgroups not co-resident); "
-                           "the solution is invalid")
     dopri5_solve.last = ResidentSolve(stats, att)
+    _status_check(stats, "fetode_integrate_dopri5: a grid reduction timed out (workgroups not co-resident); "
+                         "the solution is invalid")
     return sol
 
 

@@ -222,18 +222,25 @@ class KanFet_NODE(nn.Module):
 
     def forward(self, x):
         _lib.require_gpu_tensor(x, "KanFet_NODE.forward")
-        h0 = self.encoder(x)
-        # the reference builds t on x's device; odeint reads the grid on the host, so it is built
-        # there (same values and dtype, no device round trip)
-        t_eval = torch.tensor([0.0, 1.0], dtype=x.dtype)
-        h_traj = odeint(self.odefunc, h0, t_eval, method=self.solver, rtol=self.rtol, atol=self.atol)
-        if self.solver == "dopri5":
-            from .dopri5 import dopri5_solve
-            self.last_solve = getattr(dopri5_solve, "last", None)
-        hT = h_traj[-1]
-        hT = self.dropout(hT)
-        feat = self.cls_feat(hT)
-        return self.cls(feat)
+        from .dopri5 import deferred_status, dopri5_solve
+        # the solve's status is read once, after the classifier is launched too (deferred_status):
+        # a failed solve still raises from this forward, but the host issues the whole forward
+        # without waiting for the solve in between
+        with deferred_status():
+            h0 = self.encoder(x)
+            # the reference builds t on x's device; odeint reads the grid on the host, so it is
+            # built there (same values and dtype, no device round trip), once per dtype
+            t_eval = self.__dict__.get("_t_eval")
+            if t_eval is None or t_eval.dtype != x.dtype:
+                t_eval = torch.tensor([0.0, 1.0], dtype=x.dtype)
+                self.__dict__["_t_eval"] = t_eval
+            h_traj = odeint(self.odefunc, h0, t_eval, method=self.solver, rtol=self.rtol, atol=self.atol)
+            if self.solver == "dopri5":
+                self.last_solve = getattr(dopri5_solve, "last", None)
+            hT = h_traj[-1]
+            hT = self.dropout(hT)
+            feat = self.cls_feat(hT)
+            return self.cls(feat)
 
 
 # ---------------------------------------------------------------------------------------------

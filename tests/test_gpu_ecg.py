@@ -236,6 +236,23 @@ def test_resident_dopri5_nonfinite_raises(dev):
         F.odeint(m, h0, torch.tensor([0.0, 1.0]), method="dopri5", options={"first_step": 0.1})
 
 
+def test_kanfet_node_forward_raises_deferred_status(dev):
+    """KanFet_NODE.forward reads the resident solve's status after launching the classifier
+    (dopri5.deferred_status): a non-finite state still raises AssertionError from the forward,
+    and the next forward is unaffected."""
+    from fet_ode_amd import ecg
+    torch.manual_seed(3)
+    m = ecg.KanFet_NODE(T=24, num_classes=2, latent_dim=8, num_basis=4).to(dev).eval()
+    x = torch.randn(6, 24, device=dev)
+    bad = x.clone()
+    bad[2, 5] = float("nan")
+    with torch.no_grad():
+        with pytest.raises(AssertionError):
+            m(bad)
+        out = m(x)
+    assert torch.isfinite(out).all()
+
+
 # ---------------------------------------------------------------------------------------------
 # The FerroElectricNet field of train_ecg.py (KANFetODEFunc, SURVEY §8f rank 2)
 # ---------------------------------------------------------------------------------------------
