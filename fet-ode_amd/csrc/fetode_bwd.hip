@@ -294,17 +294,24 @@ __device__ __forceinline__ void feat_input(BFeat<W, NG - 1 - kSO, NB>& F, const 
   F.up[t] = sigm_l2(-gsl2e * (x - F.pv[t]));
 }
 
-// the VJP jobs of one layer (inputs at combined offset TB) for one evaluation: gradient sums into
-// R, d out/d x contributions into cb[i * NTM + t]
-template <class L, int TB, bool ACC, class FT>
-__device__ __forceinline__ void layer_jobs(const FT& F, const float* __restrict__ gout, const BTab<L>& Tb,
-                                           const float* __restrict__ rhs, BReg<L>& R, float* __restrict__ cb,
+// the VJP jobs of one layer (inputs at combined offset TB) for one evaluation of each of the
+// wave's TPW trajectories (Fs[tt], gouts + tt * GS, cbs + tt * CBS): gradient sums into R (the
+// lane's job slots, summed over the trajectories in order), d out/d x contributions into
+// cb[i * NTMP + t]
+template <class L, int TB, bool ACC, int TPW, int GS, int CBS, class FT>
+__device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict__ gouts, const BTab<L>& Tb,
+                                           const float* __restrict__ rhs, BReg<L>& R, float* __restrict__ cbs,
                                            float gsl2e, float wc, float gs, int lane, int z) {
   if constexpr (L::FERRO) {
+#pragma unroll 1
+    for (int tt = 0; tt < TPW; ++tt)  // trajectories in turn, each one's rounds interleaved
 #pragma unroll
     for (int r = 0; r < L::RF; ++r) {
       const int e = lane + 64 * r;
       if (e < L::E) {
+        const FT& F = Fs[tt];
+        const float* gout = gouts + tt * GS;
+        float* cb = cbs + tt * CBS;
         const int i = e / (L::OUT * L::K), ok_ = e % (L::OUT * L::K);
         const int o = ok_ / L::K;
         const float x = F.x[TB + i], up = F.up[TB + i], go = gout[o];
@@ -330,14 +337,20 @@ __device__ __forceinline__ void layer_jobs(const FT& F, const float* __restrict_
       }
     }
     if constexpr (ACC)
-      if (lane < L::OUT) R.G += gout[lane];
+      if (lane < L::OUT)
+#pragma unroll
+        for (int tt = 0; tt < TPW; ++tt) R.G += gouts[tt * GS + lane];
   }
+#pragma unroll 1
+  for (int tt = 0; tt < TPW; ++tt)
 #pragma unroll
   for (int r = 0; r < L::RE; ++r) {
     const int q = lane + 64 * r;
     if (q < L::NE) {
+      const FT& F = Fs[tt];
+      float* cb = cbs + tt * CBS;
       const int o = q / L::IN, i = q % L::IN;
-      const float go = gout[o];
+      const float go = gouts[tt * GS + o];
       if constexpr (ACC) {
         R.base[r] = ffma(go, F.silu[TB + i], R.base[r]);
 #pragma unroll
@@ -356,10 +369,15 @@ __device__ __forceinline__ void layer_jobs(const FT& F, const float* __restrict_
       cb[i * L::NTMP + L::OUT * L::K + o] = go * ffma(wb, F.dsilu[TB + i], dsdx);
     }
   }
+#pragma unroll 1
+  for (int tt = 0; tt < TPW; ++tt)
 #pragma unroll
   for (int r = 0; r < L::RL; ++r) {
     const int q = lane + 64 * r;
     if (q < L::NL) {
+      const FT& F = Fs[tt];
+      const float* gout = gouts + tt * GS;
+      float* cb = cbs + tt * CBS;
       const int i = q / L::NB, j = q % L::NB;
       const float s = F.sg[TB * L::NB + q], ds = s * (1.0f - s), x = F.x[TB + i];
       float S = 0.f;
@@ -380,18 +398,26 @@ __device__ __forceinline__ void layer_jobs(const FT& F, const float* __restrict_
   }
 }
 
-// gin[i] = sum_t cb[i * NTM + t], fixed order: LPI lanes per input, strided partial sums, DPP tree
-template <class L>
-__device__ __forceinline__ void reduce_gin(const float* __restrict__ cb, float* gin, int lane) {
-  constexpr int LPI = L::LPI > 32 ? 32 : L::LPI;
-  const int i = lane / LPI, sub = lane % LPI;
+// gin[i] = sum_t cb[i * NTM + t], fixed order: LPI lanes per input, strided partial sums, DPP tree;
+// with TPW trajectories per wave each takes 64 / TPW lanes (cbs + tt * CBS -> gins + tt * GS)
+template <class L, int TPW, int GS, int CBS>
+__device__ __forceinline__ void reduce_gin(const float* __restrict__ cbs, float* gins, int lane) {
+  constexpr int HALF = 64 / TPW;
+  constexpr int LPI0 = pow2_floor(HALF / L::IN);
+  constexpr int LPI = LPI0 > 32 ? 32 : (L::LPI < LPI0 ? L::LPI : LPI0);
+  const int tt = lane / HALF, sl = lane % HALF;
+  const int i = sl / LPI, sub = sl % LPI;
+  const float* cb = cbs + tt * CBS;
   float s = 0.f;
   if (i < L::IN) {
 #pragma unroll
-    for (int t = sub; t < L::NTM; t += LPI) s += cb[i * L::NTMP + t];
+    for (int k = 0; k < (L::NTM + LPI - 1) / LPI; ++k) {
+      const int t = sub + k * LPI;
+      if (t < L::NTM) s += cb[i * L::NTMP + t];
+    }
   }
   s = group_sum<LPI>(s);
-  if (i < L::IN && sub == 0) gin[i] = s;
+  if (i < L::IN && sub == 0) gins[tt * GS + i] = s;
 }
 
 struct BwdArgs {
@@ -460,25 +486,30 @@ constexpr int kTPB = 4;  // trajectories (waves) per workgroup, sharing one copy
 #endif
 
 // ACC = true: the whole reverse sweep in one kernel — adjoints and the parameter-gradient sums (in
-// VGPRs, one partial row per wave).  ACC = false: the adjoint sweep only (no sums: 118 VGPRs, four
+// VGPRs, one partial row per wave).  ACC = false: the adjoint sweep only (no sums: 114 VGPRs, four
 // waves per SIMD, all B = 4096 trajectories resident at once); it records every evaluation's
 // output and hidden adjoints in a.gadj and param_sum_kernel forms the sums in parallel.
-template <int D, int H, int K, int NB, int NG, bool FERRO, bool ACC>
+// TPW trajectories per wave: lane l serves trajectory tt = l / (64 / TPW) in the per-input phases
+// (tape, features, d out/d x sums, adjoint scalars) and owns its job slots for all TPW of them in
+// the VJP phases, so the gradient sums do not grow with TPW.  TPW = 2 halves the waves (B = 4096:
+// 2 048 waves = every trajectory resident in one round at the sums' 2 waves per SIMD).
+template <int D, int H, int K, int NB, int NG, bool FERRO, bool ACC, int TPW>
 __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ? FETODE_BWD_WAVES : 4))) void fixed_bwd_kernel(BwdArgs a) {
   using L0 = BL<D, H, K, NB, NG, FERRO>;
   using L1 = BL<H, D, K, NB, NG, FERRO>;
-  constexpr int W = D + H, NS = NG - 1 - kSO;
+  constexpr int W = D + H, NS = NG - 1 - kSO, HALF = 64 / TPW;
   constexpr int CB = L0::IN * L0::NTMP > L1::IN * L1::NTMP ? L0::IN * L0::NTMP : L1::IN * L1::NTMP;
-  static_assert(W <= 64, "one lane per input");
+  static_assert(W <= HALF && (TPW == 1 || TPW == 2), "one lane per input of each trajectory");
   __shared__ BInTab<W, NG, NB> TI;
   __shared__ BTab<L0> T0;
   __shared__ BTab<L1> T1;
-  __shared__ BFeat<W, NS, NB> sF[kTPB];
-  __shared__ float s_cb[kTPB][CB];
-  __shared__ float s_g1[kTPB][D], s_g0[kTPB][H], s_gx[kTPB][D];
-  __shared__ float s_ak[kTPB][4][D], s_ay[kTPB][D], s_ac[kTPB][4][3];
+  __shared__ BFeat<W, NS, NB> sF[kTPB][TPW];
+  __shared__ float s_cb[kTPB][TPW][CB];
+  __shared__ float s_g1[kTPB][TPW][D], s_g0[kTPB][TPW][H], s_gx[kTPB][TPW][D];
+  __shared__ float s_ak[kTPB][TPW][4][D], s_ay[kTPB][TPW][D], s_ac[kTPB][4][3];
 
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tt = lane / HALF, sl = lane % HALF;  // this lane's trajectory in the per-input phases
   TI.stage(a.plan, a.P0, a.P1, D, threadIdx.x, 64 * kTPB);
   T0.stage(a.k0, a.f0, a.plan, a.P0, threadIdx.x, 64 * kTPB);
   T1.stage(a.k1, a.f1, a.plan, a.P1, threadIdx.x, 64 * kTPB);
@@ -490,32 +521,38 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
   }
   __syncthreads();  // tables staged; from here on every wave syncs only with itself
 
-  BFeat<W, NS, NB>& F = sF[wid];
-  float* cb = s_cb[wid];
-  float* g1 = s_g1[wid];  // layer-1 output adjoint = d loss / d k_stage
-  float* g0 = s_g0[wid];  // layer-0 output adjoint = d loss / d h
-  float* gx = s_gx[wid];
-  float(&ak)[4][D] = s_ak[wid];
-  float(&ay)[D] = s_ay[wid];
+  BFeat<W, NS, NB>* Fs = sF[wid];
+  BFeat<W, NS, NB>& F = Fs[tt];
+  float* cbs = &s_cb[wid][0][0];
+  float* g1s = &s_g1[wid][0][0];  // layer-1 output adjoint = d loss / d k_stage
+  float* g0s = &s_g0[wid][0][0];  // layer-0 output adjoint = d loss / d h
+  float* gxs = &s_gx[wid][0][0];
+  float(&ak)[4][D] = s_ak[wid][tt];
+  float(&ay)[D] = s_ay[wid][tt];
   float(&acs)[4][3] = s_ac[wid];
   const float gs0 = (float)a.f0.gate_slope, gs1 = (float)a.f1.gate_slope;
   const float gl0 = a.P0.gsl2e, gl1 = a.P1.gsl2e, wc0 = a.P0.wc, wc1 = a.P1.wc;
-  const float glane = lane < D ? gl0 : gl1;  // the feature lane's layer
+  const float glane = sl < D ? gl0 : gl1;  // the feature lane's layer
   const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4 : a.method == FETODE_MIDPOINT ? 2 : 1;
   const int64_t tstride = a.B * W;
   const int n_ev = a.n_steps * ns;
 
-  for (int64_t b = (int64_t)blockIdx.x * kTPB + wid; b < a.B; b += (int64_t)gridDim.x * kTPB) {
+  for (int64_t b0 = ((int64_t)blockIdx.x * kTPB + wid) * TPW; b0 < a.B; b0 += (int64_t)gridDim.x * kTPB * TPW) {
+    // this lane's trajectory; a missing partner (B odd) runs on zeros: finite inputs, zero
+    // adjoints, exact-zero contributions to every sum
+    const int64_t b = b0 + tt;
+    const bool live = b < a.B;
+    const int64_t bc_ = live ? b : b0;
     // the hysteresis input of evaluation ev is the layer input of ev - 1 (ferro_class.py:409)
     auto tape_at = [&](int ev) -> float {
-      if (lane >= W) return 0.f;
-      if (ev >= 0) return a.tape[(int64_t)ev * tstride + b * W + lane];
-      const float v = a.tape[b * W + lane];  // before evaluation 0: the stored state / reinit rule
-      if (lane < D) return (a.init_mask & 1u) ? v : (FERRO ? a.state0[b * D + lane] : 0.f);
-      return (a.init_mask & 2u) ? v : (FERRO ? a.state0[a.B * D + b * H + (lane - D)] : 0.f);
+      if (sl >= W || !live) return 0.f;
+      if (ev >= 0) return a.tape[(int64_t)ev * tstride + b * W + sl];
+      const float v = a.tape[b * W + sl];  // before evaluation 0: the stored state / reinit rule
+      if (sl < D) return (a.init_mask & 1u) ? v : (FERRO ? a.state0[b * D + sl] : 0.f);
+      return (a.init_mask & 2u) ? v : (FERRO ? a.state0[a.B * D + b * H + (sl - D)] : 0.f);
     };
     float cur = tape_at(n_ev - 1), prv = tape_at(n_ev - 2);
-    float ay1 = 0.f;  // adjoint of y at the end of the current step (lanes d < D)
+    float ay1 = 0.f;  // adjoint of y at the end of the current step (lanes sl < D)
     int jj = a.T - 1;
     for (int s = a.n_steps - 1; s >= 0; --s) {
       float bc[4], ac[4][3];
@@ -523,23 +560,23 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
       // outputs produced in this step (FixedGridODESolver: y at step start, end, or interpolated)
       float ay0x = 0.f;
       for (; jj >= 1 && a.out_step[jj] == s; --jj) {
-        if (lane < D) {
-          const float g = a.gsol[((int64_t)jj * a.B + b) * D + lane];
+        if (sl < D) {
+          const float g = live ? a.gsol[((int64_t)jj * a.B + bc_) * D + sl] : 0.f;
           const int mode = a.out_mode[jj];
           if (mode == 0) {
             ay0x += g;
           } else if (mode == 1) {
             ay1 += g;
           } else {
-            const float sl = a.out_slope[jj];
-            ay1 = ffma(sl, g, ay1);
-            ay0x = ffma(1.0f - sl, g, ay0x);
+            const float slo = a.out_slope[jj];
+            ay1 = ffma(slo, g, ay1);
+            ay0x = ffma(1.0f - slo, g, ay0x);
           }
         }
       }
-      if (lane < D) {
-        for (int j = 0; j < ns; ++j) ak[j][lane] = bc[j] * ay1;
-        ay[lane] = ay1 + ay0x;
+      if (sl < D) {
+        for (int j = 0; j < ns; ++j) ak[j][sl] = bc[j] * ay1;
+        ay[sl] = ay1 + ay0x;
       }
       if (lane == 0) {  // through LDS: the stage index below is a runtime value
 #pragma unroll
@@ -554,43 +591,46 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
         int z = 0;
         asm volatile("" : "+s"(z));
         const float nxt = tape_at(ev - 2);  // prefetch: consumed by the next evaluation
-        if (lane < W) {
-          F.x[lane] = cur;
-          F.pv[lane] = prv;
+        if (sl < W) {
+          F.x[sl] = cur;
+          F.pv[sl] = prv;
         }
-        if (lane < D) g1[lane] = ak[st][lane];
+        if (sl < D) g1s[tt * D + sl] = ak[st][sl];
         wsync();
         // features of both layers' inputs: one code path over the combined input index
-        if (lane < W) feat_input<W, NG, NB>(F, TI, lane, glane, z);
-#pragma unroll
-        for (int q = lane; q < W * NB; q += 64)
-          F.sg[q] = sigm_l2(ffma(TI.lg[2 * q + z], F.x[q / NB], TI.lg[2 * q + 1 + z]));
+        if (sl < W) feat_input<W, NG, NB>(F, TI, sl, glane, z);
+        for (int q = lane; q < TPW * W * NB; q += 64) {
+          const int qt = q / (W * NB), qq = q % (W * NB);
+          Fs[qt].sg[qq] = sigm_l2(ffma(TI.lg[2 * qq + z], Fs[qt].x[qq / NB], TI.lg[2 * qq + 1 + z]));
+        }
         wsync();
-        layer_jobs<L1, D, ACC>(F, g1, T1, TI.rh, R1, cb, gl1, wc1, gs1, lane, z);
+        layer_jobs<L1, D, ACC, TPW, D, CB>(Fs, g1s, T1, TI.rh, R1, cbs, gl1, wc1, gs1, lane, z);
         wsync();
-        reduce_gin<L1>(cb, g0, lane);  // d loss / d h
+        reduce_gin<L1, TPW, H, CB>(cbs, g0s, lane);  // d loss / d h
         wsync();
         if constexpr (!ACC) {  // this evaluation's adjoints for param_sum_kernel
-          float* gr = a.gadj + ((int64_t)ev * a.B + b) * W;
-          if (lane < D) gr[lane] = g1[lane];
-          else if (lane < W) gr[lane] = g0[lane - D];
+          if (live) {
+            float* gr = a.gadj + ((int64_t)ev * a.B + b) * W;
+            if (sl < D) gr[sl] = g1s[tt * D + sl];
+            else if (sl < W) gr[sl] = g0s[tt * H + sl - D];
+          }
         }
-        layer_jobs<L0, 0, ACC>(F, g0, T0, TI.rh, R0, cb, gl0, wc0, gs0, lane, z);
+        layer_jobs<L0, 0, ACC, TPW, H, CB>(Fs, g0s, T0, TI.rh, R0, cbs, gl0, wc0, gs0, lane, z);
         wsync();
-        reduce_gin<L0>(cb, gx, lane);
+        reduce_gin<L0, TPW, D, CB>(cbs, gxs, lane);
         wsync();
-        if (lane < D) {
-          const float ax = gx[lane];
-          ay[lane] += ax;
-          for (int j = 0; j < st; ++j) ak[j][lane] = ffma(acs[st][j], ax, ak[j][lane]);
+        if (sl < D) {
+          const float ax = gxs[tt * D + sl];
+          ay[sl] += ax;
+          for (int j = 0; j < st; ++j) ak[j][sl] = ffma(acs[st][j], ax, ak[j][sl]);
         }
         wsync();
         cur = prv;
         prv = nxt;
       }
-      ay1 = lane < D ? ay[lane] : 0.f;
+      ay1 = sl < D ? ay[sl] : 0.f;
     }
-    if (lane < D && a.gy0) a.gy0[b * D + lane] = ay1 + a.gsol[b * D + lane];  // solution[0] = y0
+    if (sl < D && live && a.gy0) a.gy0[b * D + sl] = ay1 + a.gsol[b * D + sl];  // solution[0] = y0
     wsync();
   }
   if constexpr (ACC) {
@@ -902,16 +942,17 @@ typedef void (*bwd_fn)(BwdArgs);
 struct BwdEntry {
   int D, H, K, NB, NG;
   bool ferro;
+  int tpw;                     // trajectories per wave of fn
   bwd_fn fn;                   // the one-kernel sweep (sums in VGPRs)
   bwd_fn adj, sum0, sum1;      // the split: adjoint sweep + per-layer parameter sums (or null)
 };
 const BwdEntry kBwd[] = {
     // LV KAN-FET [2,10,2]: the split (the one-kernel sweep needs 239 VGPRs: two rounds of waves)
-    {2, 10, 10, 10, 12, true, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true>,
-     fixed_bwd_kernel<2, 10, 10, 10, 12, true, false>, param_sum_kernel<2, 10, 10, 10, 12, 0>,
+    {2, 10, 10, 10, 12, true, 2, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 2>,
+     fixed_bwd_kernel<2, 10, 10, 10, 12, true, false, 1>, param_sum_kernel<2, 10, 10, 10, 12, 0>,
      param_sum_kernel<2, 10, 10, 10, 12, 1>},
     // LV KAN [2,10,2] (126 VGPRs: four waves per SIMD already)
-    {2, 10, 0, 10, 12, false, fixed_bwd_kernel<2, 10, 1, 10, 12, false, true>, nullptr, nullptr, nullptr},
+    {2, 10, 0, 10, 12, false, 1, fixed_bwd_kernel<2, 10, 1, 10, 12, false, true, 1>, nullptr, nullptr, nullptr},
 };
 // Which path the KAN-FET sweep takes (fetode_backward_set_split; env FETODE_BWD_SPLIT).  Default:
 // the one-kernel sweep — measured on MI355X at B = 4096, rk4, 34 steps: one kernel 1.06 ms vs the
@@ -951,8 +992,9 @@ const BwdEntry* find_bwd(const fetode_field_t* f) {
 constexpr int64_t kMaxBwdRows = 8192;  // partial rows (one per wave)
 constexpr int kChunks = 64;
 // one partial row per wave: the grid's waves, a multiple of kTPB
-int64_t bwd_rows(int64_t B) {
-  const int64_t w = B < kMaxBwdRows ? B : kMaxBwdRows;
+int64_t bwd_rows(int64_t B, int tpw) {
+  const int64_t nw = (B + tpw - 1) / tpw;  // waves the trajectories need
+  const int64_t w = nw < kMaxBwdRows ? nw : kMaxBwdRows;
   return (w + kTPB - 1) / kTPB * kTPB;
 }
 
@@ -982,7 +1024,7 @@ int fetode_fused_backward_supported(const fetode_field_t* f) {
 
 // partial rows of the chosen path: one per wave (one-kernel sweep) or per param_sum block (split)
 int64_t sum_rows(const BwdEntry* e, int64_t B, int64_t n_ev) {
-  if (!use_split(e)) return bwd_rows(B);
+  if (!use_split(e)) return bwd_rows(B, e->tpw);
   const int64_t tiles = (n_ev * B + kPsTS - 1) / kPsTS;
   return tiles < kSumBlocks ? (tiles > 0 ? tiles : 1) : kSumBlocks;
 }
