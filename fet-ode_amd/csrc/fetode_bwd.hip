@@ -499,7 +499,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
   using L1 = BL<H, D, K, NB, NG, FERRO>;
   constexpr int W = D + H, NS = NG - 1 - kSO, HALF = 64 / TPW;
   constexpr int CB = L0::IN * L0::NTMP > L1::IN * L1::NTMP ? L0::IN * L0::NTMP : L1::IN * L1::NTMP;
-  static_assert(W <= HALF && (TPW == 1 || TPW == 2), "one lane per input of each trajectory");
+  static_assert(W <= HALF && (TPW == 1 || TPW == 2 || TPW == 4), "one lane per input of each trajectory");
   __shared__ BInTab<W, NG, NB> TI;
   __shared__ BTab<L0> T0;
   __shared__ BTab<L1> T1;
@@ -947,7 +947,8 @@ struct BwdEntry {
   bwd_fn adj, sum0, sum1;      // the split: adjoint sweep + per-layer parameter sums (or null)
 };
 const BwdEntry kBwd[] = {
-    // LV KAN-FET [2,10,2]: the split (the one-kernel sweep needs 239 VGPRs: two rounds of waves)
+    // LV KAN-FET [2,10,2]: one kernel, two trajectories per wave (measured: TPW 1 / 2 / 4 = 1034 / 897 /
+    // 1203 us at B = 4096); the split structure as the alternative
     {2, 10, 10, 10, 12, true, 2, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 2>,
      fixed_bwd_kernel<2, 10, 10, 10, 12, true, false, 1>, param_sum_kernel<2, 10, 10, 10, 12, 0>,
      param_sum_kernel<2, 10, 10, 10, 12, 1>},
