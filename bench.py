@@ -223,6 +223,24 @@ def lv_dopri5_rate(sd, y0d, t, reps=3):
             "path": "fetode_integrate_dopri5: fused4_kernel DOPRI instantiation, one cooperative launch"}
 
 
+def plain_closure_rate(model, y0d, t, reps=3):
+    """The literal drop-in: the reference's `calDeriv(t, X) = kan_fet_model(X)` closure unchanged
+    (INTEGRATION.md §1).  odeint cannot see the model behind a closure, so this is the per-stage
+    path: one fused single-evaluation launch + one stage-combine launch per stage (272 per solve)
+    — what `fet_ode_amd.autonomous(model)` avoids."""
+    func = lambda tt, yy: model(yy)  # noqa: E731
+    with torch.no_grad():
+        F.odeint(func, y0d, t, method="rk4")
+        torch.cuda.synchronize(y0d.device)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            F.odeint(func, y0d, t, method="rk4")
+        torch.cuda.synchronize(y0d.device)
+        el = (time.perf_counter() - t0) / reps
+    return {"value": STEPS_PER_SOLVE / el, "unit": "RK4 steps/s of the batch-4096 job, plain calDeriv closure",
+            "ms_per_solve": el * 1e3, "path": "per-stage: fetode_field_forward + fetode_rk_combine per stage"}
+
+
 def ecg_rate(dev, reps=10, cpu_seconds=5.0, with_cpu=True, rtol=1e-3, atol=1e-4):
     """BASELINE configs[2] (train_ecg_kan_fet_nn_ode.py:512-572): KanFet_NODE.eval() forward on a
     batch of 200 synthetic ECG200-shaped series (T = 96; the dataset is not in the image), latent
@@ -531,6 +549,8 @@ def main():
                                            "events, solve = host wall of one odeint call (median)"}
         if train is not None:
             out["train"] = train
+        if world == 1:
+            out["lv_plain_closure"] = plain_closure_rate(model, y0d, t)
         if world == 1 and not args.no_dopri5:
             out["lv_dopri5"] = lv_dopri5_rate(sd, y0d, t)
         if world == 1 and not args.no_ecg:

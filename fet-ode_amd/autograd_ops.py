@@ -340,7 +340,9 @@ def _fused_eval(model, handle, x):
     B = x.shape[0]
     plan = build_plan(model, handle, x.device)
     state, mask = pack_state(model, B, x.device)
-    out = torch.empty(B, field_layers(model)[-1][0].out_features, device=x.device, dtype=torch.float32)
+    io = model.__dict__.get("_fetode_io")
+    n_out = io[1] if io is not None else field_layers(model)[-1][0].out_features
+    out = torch.empty(B, n_out, device=x.device, dtype=torch.float32)
     _lib.check(_lib.load().fetode_field_forward(handle.ref, plan.data_ptr(), x.data_ptr(), B, _lib.ptr(state),
                                                 mask, out.data_ptr(), _stream(x)), "field forward")
     if state is not None:
@@ -352,22 +354,25 @@ def field_apply(model, x: torch.Tensor) -> torch.Tensor:
     """KAN.forward / KANFET.forward: one evaluation.  Inference on a shape with a fused kernel
     is one launch; otherwise (other widths, or autograd recording) one HIP kernel per
     KANLinear / Ferro layer, each with its HIP backward."""
-    in0 = field_layers(model)[0][0].in_features
+    io = model.__dict__.get("_fetode_io")   # (in, out) of the stack (module attribute reads are slow)
+    if io is None:
+        ls = field_layers(model)
+        io = model.__dict__["_fetode_io"] = (ls[0][0].in_features, ls[-1][0].out_features)
+    in0 = io[0]
     lead = x.shape[:-1]
     if model.has_ferro and x.dim() != 2:
         raise ValueError("KANFET expects x of shape (B, in_features)")
     x2 = x.reshape(-1, in0)
     _lib.require_gpu_tensor(x2, type(model).__name__ + ".forward")
     B = x2.shape[0]
-    params = list(model.parameters())
-    if not grad_enabled_for(x2, *params):
+    grad = torch.is_grad_enabled() and grad_enabled_for(x2, *model.parameters())
+    if not grad:
         x2 = x2.contiguous()
         handle = make_handle(model, B, x2.device)
-        if _lib.load().fetode_fused_supported(handle.ref):
+        if handle.supported(_lib.load()):
             out = _fused_eval(model, handle, x2)
             return out.reshape(*lead, out.shape[-1]) if not model.has_ferro else out
     h = x2
-    grad = grad_enabled_for(x2, *params)
     for kan, fer in field_layers(model):
         if not grad:
             # production widths (ETT KANFET[64,128,64], ...): the whole layer KANLinear + Ferro in one launch

@@ -343,6 +343,13 @@ def _c(v):
 
 
 def _combine(method, stage, dt, y, k1, k2=None, k3=None, k4=None):
+    if not torch.is_grad_enabled():   # inference: the kernel without the autograd.Function layer
+        y, k1, k2, k3, k4 = _c(y), _c(k1), _c(k2), _c(k3), _c(k4)
+        out = torch.empty_like(y)
+        _lib.check(_lib.load().fetode_rk_combine(method, stage, y.data_ptr(), k1.data_ptr(), _lib.ptr(k2),
+                                                 _lib.ptr(k3), _lib.ptr(k4), float(dt), out.data_ptr(), y.numel(),
+                                                 _lib.stream_handle(y.device)), "fetode_rk_combine")
+        return out
     return _CombineFn.apply(method, stage, float(dt), _c(y), _c(k1), _c(k2), _c(k3), _c(k4))
 
 
@@ -353,8 +360,16 @@ def _per_stage_fixed(func, y0, sched: Schedule, method: str, tc_dtype, reversed_
     g = sched.grid
     sign = -1.0 if reversed_ else 1.0
 
-    def tt(v):  # on y0's device, like torchdiffeq's t (fields may torch.cat it with the state)
-        return torch.tensor(sign * v, dtype=y0.dtype).to(y0.device, non_blocking=True)
+    # stage times on y0's device, like torchdiffeq's t (fields may torch.cat it with the state):
+    # every distinct time of the solve uploaded once, then 0-dim views (a tensor per stage would
+    # cost a host tensor + a copy launch each)
+    times = {}
+
+    def tt(v):
+        r = times.get(v)
+        if r is None:
+            r = times[v] = torch.tensor(sign * v, dtype=y0.dtype).to(y0.device, non_blocking=True)
+        return r
 
     j = 1
     for s in range(sched.n_steps):

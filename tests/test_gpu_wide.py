@@ -117,3 +117,83 @@ def test_ett_field_through_odeint_rk4_production_width(dev):
     assert err <= 4 * spread + 1e-5, (err, spread)
     # the hysteresis state after the solve is the last stage input of each layer (ferro_class.py:409)
     assert dyn.net.layers[0].ferro.prev_x.shape == (256, 64, 128, 10)
+
+
+# ---------------------------------------------------------------------------------------------
+# the autograd path at production widths: under autograd the layers run the generic wide kernels
+# (kanlinear_fwd_wave_kernel with its OB variants, ferro_fwd_wide_kernel<10>) and their VJPs —
+# what training the config-4 forecaster executes
+# ---------------------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("i,o", [(64, 128), (128, 64)])
+@pytest.mark.parametrize("B", [256, 4096])
+def test_wide_kanlinear_autograd_forward_and_grads(dev, i, o, B):
+    """KANLinear forward + every parameter gradient and d x under autograd vs the oracle's
+    autograd (B sweeps the OB = 8 / 2 launcher choice)."""
+    torch.manual_seed(i * 3 + o + B)
+    m = F.KANLinear(i, o)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    x = _x(B, i, seed=B + 1)
+    w = torch.randn(B, o, generator=torch.Generator().manual_seed(B + 2))
+    xg = x.to(dev).requires_grad_(True)
+    got = m(xg)
+    (got * w.to(dev)).sum().backward()
+    p = O.KANLinearParams.from_state_dict(sd)
+    field_of = {"base_weight": "base_weight", "spline_weight": "spline_weight", "spline_scaler": "spline_scaler",
+                "logistic_basis.a": "a", "logistic_basis.b": "b", "logistic_weight": "logistic_weight",
+                "logistic_scaler": "logistic_scaler"}
+    ps = {}
+    for name, f in field_of.items():
+        v = getattr(p, f)
+        if v is not None:
+            ps[name] = v.clone().requires_grad_(True)
+            setattr(p, f, ps[name])
+    xr = x.clone().requires_grad_(True)
+    exp = O.kanlinear_forward(xr, p)
+    (exp * w).sum().backward()
+    assert row_rel(got.detach(), exp.detach()) <= 1e-5
+    gx = (xg.grad.cpu() - xr.grad).abs().max().item()
+    assert gx <= 1e-4 * xr.grad.abs().max().item(), gx
+    checked = 0
+    for name, t in m.named_parameters():
+        ref = ps.get(name)
+        if ref is None or ref.grad is None:
+            continue
+        err = (t.grad.cpu() - ref.grad).abs().max().item()
+        assert err <= 2e-4 * ref.grad.abs().max().item() + 1e-7, (name, err)
+        checked += 1
+    assert checked >= 6, checked
+
+
+@pytest.mark.parametrize("i,o", [(64, 128), (128, 64)])
+def test_wide_ferro_autograd_sequence_and_grads(dev, i, o):
+    """FerroelectricBasis(K = 10) under autograd — the generic wide forward with wild rows and
+    |gs Ec| > 80 parameters, two stateful calls — and the parameter / input gradients of the
+    second call vs the oracle's autograd."""
+    m = _ferro_with_edges(i, o, 10, seed=7 * i + o)
+    names = ("k", "Ec", "Ps", "bias", "coef")
+    p0 = [getattr(m, n).detach().clone() for n in names]
+    m = m.to(dev)
+    st = O.FerroState(i, o, 10)
+    B = 300
+    x1 = _x(B, i, seed=5, wild_rows=(3, 200))
+    x2 = _x(B, i, seed=6) * 0.9
+    w = torch.randn(B, o, generator=torch.Generator().manual_seed(8))
+    with torch.no_grad():
+        m(x1.to(dev))
+    O.ferro_forward(x1, O.FerroParams(*p0), st)
+    xg = x2.to(dev).requires_grad_(True)
+    got = m(xg)
+    (got * w.to(dev)).sum().backward()
+    pr = [t.clone().requires_grad_(True) for t in p0]
+    xr = x2.clone().requires_grad_(True)
+    exp = O.ferro_forward(xr, O.FerroParams(*pr), st)
+    (exp * w).sum().backward()
+    assert row_rel(got.detach(), exp.detach()) <= 1e-5
+    gx = (xg.grad.cpu() - xr.grad).abs().max().item()
+    assert gx <= 2e-4 * xr.grad.abs().max().item(), gx
+    for n, r in zip(names, pr):
+        g = getattr(m, n).grad.cpu()
+        err = (g - r.grad).abs().max().item()
+        assert err <= 2e-4 * r.grad.abs().max().item() + 1e-7, (n, err)
