@@ -10,7 +10,7 @@
 //             prev))) and e = e^{gs x} for the Ferro elements, and the 20 KAN features (SiLU, the 8
 //             cubic B-spline bases by the reference's Cox-de Boor, 10 logistic bases) into LDS;
 //   Ferro     wave w owns outputs 2w, 2w+1 for all 64 rows (lane = row), so every Ferro constant
-//             is wave-uniform (staged per chunk in LDS, read as broadcasts): per element
+//             is wave-uniform (scalar loads into SGPR operands, no LDS traffic): per element
 //               s = 1/(1 + e P),  m = 1 + w s,  z = 2 log2e k (x + Ec m),  th = 1 - 2/(1 + 2^z)
 //             (P = e^{gs Ec} packed once; branch_sign = 1 makes the crossing gate cp drop out, as in
 //             the fused LV kernel), 7 VALU + 3 transcendental instructions;
@@ -237,12 +237,10 @@ struct WideArgs {
 // ---- the layer --------------------------------------------------------------------------------
 template <int K, bool KAN, bool FERRO, int kCh>
 __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
-  constexpr int KP = FERRO ? K : 1;
   constexpr int kPitch = pitch_of(kCh);
   static_assert(kCh * kRows <= kThreads && (kCh & 1) == 0, "one staging item per thread, even chunks");
   static_assert(!FERRO || K % 2 == 0, "Ferro elements in (k, k+1) pairs");
   __shared__ float s_x[kCh * kRows], s_w[kCh * kRows], s_e[kCh * kRows];
-  __shared__ float4 s_par[kOuts * kCh * KP];  // the chunk's Ferro constants, read as wave broadcasts
   __shared__ float s_dfl[kOuts * kCh];
   // KAN features of the chunk (MFMA A operand); the epilogue reuses the space for the Ferro sums
   // and the second K-half of the MFMA tile
@@ -292,11 +290,6 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
       s_x[si * kRows + sr] = x;
       s_w[si * kRows + sr] = wc * (1.0f - up);
       s_e[si * kRows + sr] = ex2(gsl2e * x);
-      }
-      const float4* fe = reinterpret_cast<const float4*>(plan + L.fe4);
-      for (int idx = tid; idx < kOuts * kCh * K; idx += kThreads) {
-        const int j = idx / (kCh * K), r = idx - j * (kCh * K);
-        s_par[idx] = fe[((int64_t)(o0 + j) * in + i0) * K + r];   // (ii, k) contiguous per output
       }
       if (tid < kOuts * kCh) s_dfl[tid] = plan[L.dflag + (int64_t)(o0 + tid / kCh) * in + i0 + tid % kCh];
     }
@@ -349,7 +342,9 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
 #pragma unroll
         for (int j = 0; j < kJ; ++j) {
           const int jo = kJ * w + j;
-          const float4* par = &s_par[(jo * kCh + ii) * K];
+          // the element constants are wave-uniform: scalar loads (s_load, SGPR operands) — through
+          // LDS they cost a ds_read_b128 per element (Ferro alone 270 -> 230 us at 64 -> 128)
+          const float4* par = reinterpret_cast<const float4*>(plan + L.fe4) + ((int64_t)(o0 + jo) * in + i) * K;
           float acc = 0.f;
           if (!xbig && s_dfl[jo * kCh + ii] == 0.f) {
             // elements (k, k+1) in the two halves of packed-fp32 VALU ops (v_pk_fma / mul / add:
