@@ -241,6 +241,15 @@ __device__ __forceinline__ float row_sum16(float v) {
   v += dpp<0x121>(v);  // row_ror:1
   return v;
 }
+// gfx950 lane swaps, in place: permlane32 swaps lanes 32-63 of p with lanes 0-31 of q; permlane16
+// swaps the odd rows of p with the even rows of q.  Inline asm: this compiler's builtins for them
+// treat the two results as one register.  The s_nop covers the VALU-write -> permlane-read hazard.
+__device__ __forceinline__ void permlane32_swap(float& p, float& q) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(p), "+v"(q));
+}
+__device__ __forceinline__ void permlane16_swap(float& p, float& q) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(p), "+v"(q));
+}
 // sum over lanes 3k, 3k+1, 3k+2 of a row (k < 5), result on all three
 __device__ __forceinline__ float group3_sum(float v, int c) {
   const float s0 = v + dpp<0x101>(v) + dpp<0x102>(v);  // row_shl:1, row_shl:2 -> valid at c == 0
@@ -957,9 +966,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
 template <bool FERRO, bool HOT>
 __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
   constexpr int D = 2, H = 10, K = FERRO ? 10 : 0, KP = 5, NB = 10, NG = 12, NI = NG - 1, NFL = 1 + NB;
-  constexpr int SPT = H * D * (NI + 1) * 4;
-  __shared__ __attribute__((aligned(16))) float s_sp0[SPT];
-  __shared__ __attribute__((aligned(16))) float s_sp1[SPT];
   __shared__ __attribute__((aligned(8))) f2 s_part[2][3];
   constexpr int SCH = 32;
   __shared__ float s_dt[SCH], s_hh[SCH], s_h6[SCH], s_oslope[SCH];
@@ -970,10 +976,6 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
   const int rr = act ? r : 0;
   const int64_t b = blockIdx.x;
   const float l2 = FETODE_LOG2E;
-  for (int i = tid; i < SPT; i += 192) {
-    s_sp0[i] = a.plan[a.P0.sp + i];
-    s_sp1[i] = a.plan[a.P1.sp + i];
-  }
   const bool fact = FERRO && a.plan[a.P0.flag] <= a.factor_limit && a.plan[a.P1.flag] <= a.factor_limit;
 
   // ---- layer 0, row rr = output o: one Ferro pair (input i0, bases 2kp, 2kp+1) on lanes c < 10
@@ -1034,13 +1036,35 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       fexp[s] = true;
     }
   }
+  // Each lane computes ONE of them: even rows job c, odd rows job c + 16 (one permlane16 swap
+  // per evaluation then gives every lane both values); the MAC weights stay per slot and row.
+  const int so = r & 1;
+  const float ona = so ? fna[1] : fna[0], oab = so ? fab[1] : fab[0];
+  const float omul = so ? fmul[1] : fmul[0], oadd = so ? fadd[1] : fadd[0];
+  const int ofx = so ? fx[1] : fx[0];
+  const bool osilu = so ? fsilu[1] : fsilu[0], ogate = so ? fgate[1] : fgate[0], oexp = so ? fexp[1] : fexp[0];
+  const bool fmac1 = !(fgate[1] || fexp[1]);  // slot-1 values to MAC (weight 0 elsewhere; never e)
   // knots of the two layer-0 inputs on lanes c < NG (every row holds the same)
   const float kn0 = c < NG ? a.plan[a.P0.knots + c] : __builtin_inff();
   const float kn1 = c < NG ? a.plan[a.P0.knots + NG + c] : __builtin_inff();
   const float rh0 = c < NI ? a.plan[a.P0.rh + c] : 0.f;
   const float rh1 = c < NI ? a.plan[a.P0.rh + NI + c] : 0.f;
   const float c0o = act ? a.plan[a.P0.fconst + rr] : 0.f;
-  const float* sp0_r = &s_sp0[rr * D * (NI + 1) * 4];
+  // the spline cubics live in registers: lane c holds knot interval c's cubic (c = NI: the zero
+  // row) of its row's edges — layer 0 (r, 0), (r, 1), layer 1 (0, r), (1, r) — so the lane that
+  // owns x's interval evaluates it with no LDS round trip on the evaluation's chain
+  float4 cs0[D], cs1[D];
+  {
+    const bool hc = act && c <= NI;
+    const float4* sp0 = reinterpret_cast<const float4*>(a.plan + a.P0.sp);
+    const float4* sp1 = reinterpret_cast<const float4*>(a.plan + a.P1.sp);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      cs0[i] = hc ? sp0[(rr * D + i) * (NI + 1) + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+      cs1[i] = hc ? sp1[(i * H + rr) * (NI + 1) + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  auto cubic = [](float4 cf, float u) { return ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x); };
 
   // ---- layer 1, row rr = input i: feature job c (logistic j = c < 10, SiLU, gate, exp)
   float hna = 0.f, hab = 0.f, hmul = 1.f, hadd = 0.f, hw0 = 0.f, hw1 = 0.f;
@@ -1064,90 +1088,82 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       hexp = true;
     }
   }
-  const float knh = (act && c < NG) ? a.plan[a.P1.knots + rr * NG + c] : __builtin_inff();
-  const float rhh = (act && c < NI) ? a.plan[a.P1.rh + rr * NI + c] : 0.f;
+  // (idle rows read row 0's knots: finite u, zero cubics, zero weights -> they add exact zeros)
+  const float knh = c < NG ? a.plan[a.P1.knots + rr * NG + c] : __builtin_inff();
+  const float rhh = c < NI ? a.plan[a.P1.rh + rr * NI + c] : 0.f;
+  const f2 hw = f2{hw0, hw1};
+  const f2 psel = o1 ? f2{0.f, 1.f} : f2{1.f, 0.f};  // the lane's layer-1 Ferro pair feeds output o1
   const float c1o0 = a.plan[a.P1.fconst + 0], c1o1 = a.plan[a.P1.fconst + 1];
-  const float* sp1_a = &s_sp1[(0 * H + rr) * (NI + 1) * 4];
-  const float* sp1_b = &s_sp1[(1 * H + rr) * (NI + 1) * 4];
 
   // hysteresis state (ferro_class.py:409): both layer-0 inputs on every lane, input rr of layer 1
   // on its row
-  float pv0a = 0.f, pv0b = 0.f, pv1 = 0.f;
-  if (FERRO) {
-    pv0a = a.state[b * D + 0];
-    pv0b = a.state[b * D + 1];
-    pv1 = a.state[a.B * D + b * H + rr];
-  }
-  bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
+  // Each gate job keeps its own previous input (0 on every other job): pvs[s] for the layer-0
+  // slots, pvh for layer 1.  The first evaluation is always at y0, so a fresh layer-0 state
+  // (init_mask) starts from y0 directly; layer 1's first input is only known inside it (re1).
+  const bool re0 = FERRO && (a.init_mask & 1u);
+  bool re1 = FERRO && (a.init_mask & 2u);
   f2 y = f2{a.y0[b * D + 0], a.y0[b * D + 1]};
+  float pvs = 0.f, pvh = 0.f;
+  if (FERRO) {
+    if (ogate) pvs = re0 ? (ofx ? y.y : y.x) : a.state[b * D + ofx];
+    if (hgate) pvh = a.state[a.B * D + b * H + rr];
+  }
   if (!a.single_eval && tid == 0) *reinterpret_cast<f2*>(&a.solution[b * D]) = y;
   int par = 0;
-  __syncthreads();  // tables staged
 
   auto eval_body = [&](f2 xin, auto fact_tag) __attribute__((always_inline)) -> f2 {
     constexpr bool F_ = decltype(fact_tag)::value;
     const float x0 = xin.x, x1 = xin.y;
     // ---------------- layer 0 ----------------
-    float acc = 0.f;
-    float fv[2];
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const float x = fx[s] ? x1 : x0;
-      const float pv = fgate[s] ? (re0 ? x : (fx[s] ? pv0b : pv0a)) : 0.f;
-      const float e = ex2(ffma(fna[s], x - pv, fab[s]));
+    float acc, fv1;
+    {
+      const float x = ofx ? x1 : x0;
+      const float e = ex2(ffma(ona, x - pvs, oab));
+      if (FERRO) pvs = ogate ? x : 0.f;  // ferro_class.py:409
       const float sg = rcp(1.0f + e);
-      const float v = ffma(sg, fsilu[s] ? x : fmul[s], fadd[s]);
-      acc = ffma(fw[s], v, acc);  // gate / exp jobs carry weight 0: MAC the finite v, never e (inf * 0)
-      fv[s] = fexp[s] ? e : v;
+      const float v = ffma(sg, osilu ? x : omul, oadd);
+      float f0 = oexp ? e : v, f1 = f0;
+      permlane16_swap(f0, f1);  // f0: job c (the even rows' values), f1: job c + 16 (the odd rows')
+      acc = fw[0] * f0;
+      acc = ffma(fw[1], fmac1 ? f1 : 0.f, acc);  // gate / exp jobs carry weight 0: never MAC e (inf * 0)
+      fv1 = f1;
     }
     if constexpr (FERRO) {
       // gate_i / exp_i of the two inputs: slot 1, lanes 6..9 of every row (row_newbcast)
-      const float g0 = dpp<0x156>(fv[1]), g1 = dpp<0x157>(fv[1]);
-      const float e0 = dpp<0x158>(fv[1]), e1 = dpp<0x159>(fv[1]);
+      const float g0 = dpp<0x156>(fv1), g1 = dpp<0x157>(fv1);
+      const float e0 = dpp<0x158>(fv1), e1 = dpp<0x159>(fv1);
       const float4 gi = i0 ? make_float4(x1, g1, e1, 0.f) : make_float4(x0, g0, e0, 0.f);
       const f2 pr = v4_pair<F_>(gi, ep0, k20, kE0, cp0, splat(0.0f), a.P0.gsl2e);
       acc += pr.x + pr.y;
-      pv0a = x0;  // ferro_class.py:409
-      pv0b = x1;
-      re0 = false;
     }
-    // spline edges (r, 0), (r, 1): the lane whose knot opens the interval (ballot count over a row)
+    // spline edges (r, 0), (r, 1): the lane whose knot opens the interval (ballot count over a
+    // row), branch-free.  A non-finite x selects the zero row on lane NI, whose (x - knot) * 0
+    // is NaN: the reference's NaN bases.
     {
       const bool fin0 = __builtin_isfinite(x0), fin1 = __builtin_isfinite(x1);
       int m0 = (int)__builtin_popcountll(__builtin_amdgcn_ballot_w64(x0 >= kn0) & 0xFFFFull) - 1;
       int m1 = (int)__builtin_popcountll(__builtin_amdgcn_ballot_w64(x1 >= kn1) & 0xFFFFull) - 1;
       m0 = ((unsigned)m0 < (unsigned)NI && fin0) ? m0 : NI;
       m1 = ((unsigned)m1 < (unsigned)NI && fin1) ? m1 : NI;
-      if (c == m0) {
-        const float u = (x0 - kn0) * rh0;
-        const float4 cf = *reinterpret_cast<const float4*>(&sp0_r[(0 * (NI + 1) + m0) * 4]);
-        acc += ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
-      }
-      if (c == m1) {
-        const float u = (x1 - kn1) * rh1;
-        const float4 cf = *reinterpret_cast<const float4*>(&sp0_r[(1 * (NI + 1) + m1) * 4]);
-        acc += ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
-      }
-      if (c == 0 && !(fin0 && fin1)) acc += __builtin_nanf("");  // the reference's NaN bases
+      const float sv0 = cubic(cs0[0], (x0 - kn0) * rh0), sv1 = cubic(cs0[1], (x1 - kn1) * rh1);
+      acc += c == m0 ? sv0 : 0.0f;
+      acc += c == m1 ? sv1 : 0.0f;
     }
     const float h = row_sum16(acc) + c0o;
     // ---------------- layer 1 (input h = h_rr) ----------------
-    float acc0 = 0.f, acc1 = 0.f;
+    f2 acc01;
     {
-      const float pv = hgate ? (re1 ? h : pv1) : 0.f;
+      const float pv = re1 ? (hgate ? h : 0.f) : pvh;
       const float e = ex2(ffma(hna, h - pv, hab));
       const float sg = rcp(1.0f + e);
       float v = ffma(sg, hsilu ? h : hmul, hadd);
-      acc0 = hw0 * v;  // weight 0 on the gate / exp lanes: MAC the finite v before it becomes e
-      acc1 = hw1 * v;
+      acc01 = hw * splat(v);  // weight 0 on the gate / exp lanes: MAC the finite v before it becomes e
       v = hexp ? e : v;
       if constexpr (FERRO) {
         const float gt = dpp<0x15B>(v), ee = dpp<0x15C>(v);  // row_newbcast:11 / :12
         const f2 pr = v4_pair<F_>(make_float4(h, gt, ee, 0.f), ep1, k21, kE1, cp1, splat(0.0f), a.P1.gsl2e);
-        const float ps = pr.x + pr.y;
-        acc0 += o1 ? 0.0f : ps;
-        acc1 += o1 ? ps : 0.0f;
-        pv1 = h;
+        acc01 = pfma(psel, splat(pr.x + pr.y), acc01);  // 1 * ps onto output o1, 0 * ps (exact) onto the other
+        pvh = hgate ? h : 0.f;
         re1 = false;
       }
     }
@@ -1156,25 +1172,21 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       const uint64_t bal = __builtin_amdgcn_ballot_w64(h >= knh);
       int m = (int)__builtin_popcountll((bal >> (lane & 48)) & 0xFFFFull) - 1;
       m = ((unsigned)m < (unsigned)NI && fin) ? m : NI;
-      if (c == m) {
-        const float u = (h - knh) * rhh;
-        const float4 ca = *reinterpret_cast<const float4*>(&sp1_a[m * 4]);
-        const float4 cb = *reinterpret_cast<const float4*>(&sp1_b[m * 4]);
-        acc0 += ffma(ffma(ffma(ca.w, u, ca.z), u, ca.y), u, ca.x);
-        acc1 += ffma(ffma(ffma(cb.w, u, cb.z), u, cb.y), u, cb.x);
-      }
-      if (c == 0 && !fin) {
-        acc0 += __builtin_nanf("");
-        acc1 += __builtin_nanf("");
-      }
+      const float u = (h - knh) * rhh;
+      const f2 sab = f2{cubic(cs1[0], u), cubic(cs1[1], u)};
+      acc01 += c == m ? sab : splat(0.0f);
     }
-    acc0 = act ? acc0 : 0.0f;
-    acc1 = act ? acc1 : 0.0f;
-    const float v0 = row_sum16(acc0), v1 = row_sum16(acc1);
-    auto rl = [](float v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l)); };
-    const float s0 = (rl(v0, 0) + rl(v0, 16)) + (rl(v0, 32) + rl(v0, 48));
-    const float s1 = (rl(v1, 0) + rl(v1, 16)) + (rl(v1, 32) + rl(v1, 48));
-    if (lane == 0) s_part[par][w] = f2{s0, s1};
+    // the wave's sums of both outputs in one pass: the permlane32 swap folds rows (0, 2), (1, 3)
+    // of acc0 into lanes 0-31 and of acc1 into lanes 32-63, the permlane16 swap folds the two
+    // remaining rows of each half, a row sum finishes (lane 0: output 0, lane 32: output 1)
+    {
+      float p = acc01.x, q = acc01.y;
+      permlane32_swap(p, q);
+      float r = p + q, t = r;
+      permlane16_swap(r, t);
+      const float sv = row_sum16(r + t);
+      if ((lane & 31) == 0) reinterpret_cast<float*>(&s_part[par][w])[lane >> 5] = sv;
+    }
     __syncthreads();
     const f2 p0 = s_part[par][0], p1 = s_part[par][1], p2 = s_part[par][2];
     par ^= 1;
@@ -1301,12 +1313,9 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       }
     }
   }
-  if (FERRO) {
-    if (tid == 0) {
-      a.state[b * D + 0] = pv0a;
-      a.state[b * D + 1] = pv0b;
-    }
-    if (act && c == 0) a.state[a.B * D + b * H + rr] = pv1;
+  if (FERRO && (a.single_eval || a.n_steps > 0)) {  // no evaluation: the state stays as it was
+    if (r == 1 && ogate) a.state[b * D + ofx] = pvs;
+    if (act && hgate) a.state[a.B * D + b * H + rr] = pvh;
   }
 }
 
