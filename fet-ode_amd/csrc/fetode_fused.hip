@@ -233,6 +233,12 @@ __device__ __forceinline__ float dpp(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF,
                                                                false));
 }
+// the same with an undefined old value (no zero-init move): only for controls where every lane
+// reads a valid source (row_newbcast)
+template <int CTRL>
+__device__ __forceinline__ float dppm(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
 // sum over the 16 lanes of a row, result on every lane of the row
 __device__ __forceinline__ float row_sum16(float v) {
   v += dpp<0x128>(v);  // row_ror:8
@@ -1064,6 +1070,10 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       cs1[i] = hc ? sp1[(i * H + rr) * (NI + 1) + c] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   }
+  // layer 0's two edges as packed pairs (input 0, input 1)
+  const f2 s0x = f2{cs0[0].x, cs0[1].x}, s0y = f2{cs0[0].y, cs0[1].y};
+  const f2 s0z = f2{cs0[0].z, cs0[1].z}, s0w = f2{cs0[0].w, cs0[1].w};
+  const f2 nkn01 = f2{-kn0, -kn1}, rh01 = f2{rh0, rh1};
   auto cubic = [](float4 cf, float u) { return ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x); };
 
   // ---- layer 1, row rr = input i: feature job c (logistic j = c < 10, SiLU, gate, exp)
@@ -1130,24 +1140,24 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
     }
     if constexpr (FERRO) {
       // gate_i / exp_i of the two inputs: slot 1, lanes 6..9 of every row (row_newbcast)
-      const float g0 = dpp<0x156>(fv1), g1 = dpp<0x157>(fv1);
-      const float e0 = dpp<0x158>(fv1), e1 = dpp<0x159>(fv1);
+      const float g0 = dppm<0x156>(fv1), g1 = dppm<0x157>(fv1);
+      const float e0 = dppm<0x158>(fv1), e1 = dppm<0x159>(fv1);
       const float4 gi = i0 ? make_float4(x1, g1, e1, 0.f) : make_float4(x0, g0, e0, 0.f);
       const f2 pr = v4_pair<F_>(gi, ep0, k20, kE0, cp0, splat(0.0f), a.P0.gsl2e);
       acc += pr.x + pr.y;
     }
     // spline edges (r, 0), (r, 1): the lane whose knot opens the interval (ballot count over a
-    // row), branch-free.  A non-finite x selects the zero row on lane NI, whose (x - knot) * 0
-    // is NaN: the reference's NaN bases.
+    // row), branch-free.  A non-finite x counts 0 or 16 knots (lanes >= NG hold +inf), so it
+    // selects the zero row on lane NI, whose (x - knot) * 0 is NaN: the reference's NaN bases.
     {
-      const bool fin0 = __builtin_isfinite(x0), fin1 = __builtin_isfinite(x1);
       int m0 = (int)__builtin_popcountll(__builtin_amdgcn_ballot_w64(x0 >= kn0) & 0xFFFFull) - 1;
       int m1 = (int)__builtin_popcountll(__builtin_amdgcn_ballot_w64(x1 >= kn1) & 0xFFFFull) - 1;
-      m0 = ((unsigned)m0 < (unsigned)NI && fin0) ? m0 : NI;
-      m1 = ((unsigned)m1 < (unsigned)NI && fin1) ? m1 : NI;
-      const float sv0 = cubic(cs0[0], (x0 - kn0) * rh0), sv1 = cubic(cs0[1], (x1 - kn1) * rh1);
-      acc += c == m0 ? sv0 : 0.0f;
-      acc += c == m1 ? sv1 : 0.0f;
+      m0 = (unsigned)m0 < (unsigned)NI ? m0 : NI;
+      m1 = (unsigned)m1 < (unsigned)NI ? m1 : NI;
+      const f2 u = (xin + nkn01) * rh01;
+      const f2 sv = pfma(pfma(pfma(s0w, u, s0z), u, s0y), u, s0x);
+      acc += c == m0 ? sv.x : 0.0f;
+      acc += c == m1 ? sv.y : 0.0f;
     }
     const float h = row_sum16(acc) + c0o;
     // ---------------- layer 1 (input h = h_rr) ----------------
@@ -1160,7 +1170,7 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       acc01 = hw * splat(v);  // weight 0 on the gate / exp lanes: MAC the finite v before it becomes e
       v = hexp ? e : v;
       if constexpr (FERRO) {
-        const float gt = dpp<0x15B>(v), ee = dpp<0x15C>(v);  // row_newbcast:11 / :12
+        const float gt = dppm<0x15B>(v), ee = dppm<0x15C>(v);  // row_newbcast:11 / :12
         const f2 pr = v4_pair<F_>(make_float4(h, gt, ee, 0.f), ep1, k21, kE1, cp1, splat(0.0f), a.P1.gsl2e);
         acc01 = pfma(psel, splat(pr.x + pr.y), acc01);  // 1 * ps onto output o1, 0 * ps (exact) onto the other
         pvh = hgate ? h : 0.f;
@@ -1168,10 +1178,9 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       }
     }
     {
-      const bool fin = __builtin_isfinite(h);
       const uint64_t bal = __builtin_amdgcn_ballot_w64(h >= knh);
       int m = (int)__builtin_popcountll((bal >> (lane & 48)) & 0xFFFFull) - 1;
-      m = ((unsigned)m < (unsigned)NI && fin) ? m : NI;
+      m = (unsigned)m < (unsigned)NI ? m : NI;  // non-finite h: 0 or 16 knots -> the zero row (NaN)
       const float u = (h - knh) * rhh;
       const f2 sab = f2{cubic(cs1[0], u), cubic(cs1[1], u)};
       acc01 += c == m ? sab : splat(0.0f);

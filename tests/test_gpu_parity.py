@@ -396,3 +396,33 @@ def test_small_batch_kernel_single_eval_and_reference(dev, kernel_switch):
     """fetode_field_forward on v6: two stateful KAN-FET calls against the reference fixture."""
     kernel_switch(True)
     test_kanfet_field_two_calls(dev)
+
+
+def test_small_batch_kernel_nonfinite_and_offgrid_inputs(dev, kernel_switch):
+    """v6 and v4 field evaluations on rows with NaN / +-inf / off-grid / on-knot inputs, two
+    stateful calls (the second sees the first's non-finite hysteresis inputs): the same NaN
+    pattern as the reference oracle (non-finite x -> NaN bases, efficientkan.py:34-40) and the
+    same finite values (1e-5)."""
+    from oracle import torch_ref as O
+    g = load_golden("kanfet_field")
+    nan, inf = float("nan"), float("inf")
+    y = torch.tensor([[nan, 0.5], [0.5, inf], [-inf, 1.0], [12.0, -12.0], [-1.0, 1.0], [0.6, 2.2],
+                      [-2.2, -0.2], [0.3, -0.7], [1.5, 1.5], [2.19, -2.19]], dtype=torch.float32)
+    y2 = y.flip(0) * 0.9 + 0.05
+    outs = {}
+    for small in (True, False):
+        kernel_switch(small)
+        m = _kanfet_from(g, dev)
+        with torch.no_grad():
+            outs[small] = (m(y.to(dev)).cpu(), m(y2.to(dev)).cpu())
+    ref = O.KANFETRef.from_state_dict(golden_sd(g), 2)
+    with torch.no_grad():
+        exp = (ref(y), ref(y2))
+    for k in range(2):
+        a, b, e = outs[True][k], outs[False][k], exp[k]
+        assert torch.equal(torch.isnan(a), torch.isnan(e)), (k, a, e)
+        assert torch.equal(torch.isnan(b), torch.isnan(e)), (k, b, e)
+        ok, md = close(torch.nan_to_num(a), torch.nan_to_num(b), floor=1e-5)
+        assert ok, (k, md)
+        ok, md = close(torch.nan_to_num(a), torch.nan_to_num(e), floor=1e-5)
+        assert ok, (k, md)
