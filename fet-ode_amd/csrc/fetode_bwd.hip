@@ -41,6 +41,12 @@ namespace {
 
 constexpr int kSO = 3;  // spline order of the fused kernels (efficientkan default)
 
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 splat(float v) { return f2{v, v}; }
+__device__ __forceinline__ f2 ex2x2(f2 v) { return f2{ex2(v.x), ex2(v.y)}; }
+__device__ __forceinline__ f2 rcpx2(f2 v) { return f2{rcp(v.x), rcp(v.y)}; }
+
 constexpr int pow2_floor(int v) {
   int p = 1;
   while (p * 2 <= v) p *= 2;
@@ -81,6 +87,8 @@ struct BL {  // compile-time shape of one layer
   static constexpr int E = AL.E, NE = AL.NE, NL = AL.NL, NTM = AL.NTM;
   static constexpr int RF = (E + 63) / 64, RE = (NE + 63) / 64, RL = (NL + 63) / 64;
   static constexpr int RF1 = RF > 0 ? RF : 1, RL1 = RL > 0 ? RL : 1;
+  static constexpr int EP = E / 2, RP = (EP + 63) / 64, RP1 = RP > 0 ? RP : 1;  // Ferro element pairs (k, k+1)
+  static_assert(K % 2 == 0, "Ferro elements are walked in (k, k+1) pairs");
   static constexpr int LPI = pow2_floor(64 / IN);  // lanes per input in the d/dx segmented sum
   // cb row pitch: NTM rounded up to LPI mod 32, so the LPI-lane groups of one half-wave read
   // distinct LDS banks in reduce_gin (a pitch of 32 put all ten inputs of layer 1 on banks 0-3)
@@ -153,11 +161,19 @@ struct BTab {  // per-block LDS copy of one layer's edge tables
   float4 sp[L::OUT * L::IN * (L::NI + 1)];  // spline edge (o, i) as a cubic in u per interval
   float kw[L::OUT * L::IN * L::NFL];        // SiLU weight, 2 * scaled logistic weights
   float pa[L::NL > 0 ? L::NL : 1], pb[L::NL > 0 ? L::NL : 1];
-  float4 fe[L::E > 0 ? L::E : 1];           // Ferro element (i,o,k): k, Ec, coef*Ps*k
+  // Ferro element pair p = elements (2p, 2p + 1) = (i, o, k..k+1):
+  //   fpa = (Ec, Ec', 2 log2e k, 2 log2e k'),  fpb = (coef Ps k, coef' Ps' k', -gs Ec, -gs Ec')
+  float4 fpa[L::EP > 0 ? L::EP : 1], fpb[L::EP > 0 ? L::EP : 1];
 
   __device__ void stage(const fetode_kanlinear_t& kl, const fetode_ferro_t& fl, const float* __restrict__ plan,
                         const LayerPlan& P, int tid, int nt) {
-    for (int e = tid; e < L::E; e += nt) fe[e] = make_float4(fl.k[e], fl.Ec[e], (fl.coef[e] * fl.Ps[e]) * fl.k[e], 0.f);
+    const float gs = L::FERRO ? (float)fl.gate_slope : 0.f, k2 = 2.0f * FETODE_LOG2E;
+    for (int p = tid; p < L::EP; p += nt) {
+      const int e = 2 * p;
+      fpa[p] = make_float4(fl.Ec[e], fl.Ec[e + 1], k2 * fl.k[e], k2 * fl.k[e + 1]);
+      fpb[p] = make_float4((fl.coef[e] * fl.Ps[e]) * fl.k[e], (fl.coef[e + 1] * fl.Ps[e + 1]) * fl.k[e + 1],
+                           -gs * fl.Ec[e], -gs * fl.Ec[e + 1]);
+    }
     const float4* src = reinterpret_cast<const float4*>(plan + P.sp);
     for (int q = tid; q < L::OUT * L::IN * (L::NI + 1); q += nt) sp[q] = src[q];
     for (int q = tid; q < L::OUT * L::IN * L::NFL; q += nt) kw[q] = plan[P.kw + q];
@@ -170,7 +186,8 @@ struct BTab {  // per-block LDS copy of one layer's edge tables
 
 template <int W, int NS, int NB>
 struct BFeat {  // per-wave LDS features of both layers' inputs, combined index t
-  float x[W], pv[W], silu[W], dsilu[W], u[W], up[W];
+  float4 g4[W];  // Ferro per-input terms: x, gate up, wc (1 - up), -gs wc (1 - up)
+  float x[W], pv[W], silu[W], dsilu[W], u[W];
   int m[W];
   float bd[W * NS];
   float sg[NB > 0 ? W * NB : 1];
@@ -178,14 +195,14 @@ struct BFeat {  // per-wave LDS features of both layers' inputs, combined index 
 
 template <class L>
 struct BReg {  // per-lane register slice of one layer: its gradient sums
-  float A[L::RF1], C[L::RF1], Ev[L::RF1];
+  f2 A[L::RP1], C[L::RP1], Ev[L::RP1];  // element pairs
   float G;
   float base[L::RE], spl[L::RE][L::NS];
   float lw[L::RL1][L::OUT], la[L::RL1], lb[L::RL1];
 
   __device__ void zero() {
 #pragma unroll
-    for (int r = 0; r < L::RF1; ++r) A[r] = C[r] = Ev[r] = 0.f;
+    for (int r = 0; r < L::RP1; ++r) A[r] = C[r] = Ev[r] = splat(0.f);
     G = 0.f;
 #pragma unroll
     for (int r = 0; r < L::RE; ++r) {
@@ -204,12 +221,15 @@ struct BReg {  // per-lane register slice of one layer: its gradient sums
   __device__ void store(float* __restrict__ part, int lane) const {
     constexpr AccLayout AL = L::AL;
 #pragma unroll
-    for (int r = 0; r < L::RF; ++r) {
-      const int e = lane + 64 * r;
+    for (int r = 0; r < L::RP; ++r) {
+      const int e = 2 * (lane + 64 * r);
       if (e < L::E) {
-        part[AL.oA + e] = A[r];
-        part[AL.oC + e] = C[r];
-        part[AL.oE + e] = Ev[r];
+        part[AL.oA + e] = A[r].x;
+        part[AL.oA + e + 1] = A[r].y;
+        part[AL.oC + e] = C[r].x;
+        part[AL.oC + e + 1] = C[r].y;
+        part[AL.oE + e] = Ev[r].x;
+        part[AL.oE + e + 1] = Ev[r].y;
       }
     }
     if (L::FERRO && lane < L::OUT) part[AL.oG + lane] = G;
@@ -261,7 +281,7 @@ __device__ __forceinline__ float group_sum(float v) {
 // features of combined input t (one lane): SiLU, SiLU', knot interval, u, dense bases, gate
 template <int W, int NG, int NB>
 __device__ __forceinline__ void feat_input(BFeat<W, NG - 1 - kSO, NB>& F, const BInTab<W, NG, NB>& Tb, int t,
-                                           float gsl2e, int z) {
+                                           float gsl2e, float wc, float gs, int z) {
   constexpr int NI = NG - 1, NS = NG - 1 - kSO;
   const float x = F.x[t];
   const float sx = sigm_l2(-x * FETODE_LOG2E);
@@ -291,7 +311,9 @@ __device__ __forceinline__ void feat_input(BFeat<W, NG - 1 - kSO, NB>& F, const 
       if (c >= 0 && c < NS) bd[c] = ffma(ffma(ffma(p.w, u, p.z), u, p.y), u, p.x);
     }
   }
-  F.up[t] = sigm_l2(-gsl2e * (x - F.pv[t]));
+  const float up = sigm_l2(-gsl2e * (x - F.pv[t]));
+  const float wo = wc * (1.0f - up);
+  F.g4[t] = make_float4(x, up, wo, -gs * wo);
 }
 
 // the VJP jobs of one layer (inputs at combined offset TB) for one evaluation of each of the
@@ -303,37 +325,39 @@ __device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict
                                            const float* __restrict__ rhs, BReg<L>& R, float* __restrict__ cbs,
                                            float gsl2e, float wc, float gs, int lane, int z) {
   if constexpr (L::FERRO) {
+    // element pairs (k, k+1) of one (i, o) on packed-fp32 ops; with wo = wc (1 - up), c' = c (1 - c):
+    //   c = sigmoid(gs(-x - Ec)), m = 1 + wo c, sh = x + Ec m, th = tanh(k sh), q = g (1 - th^2)
+    //   A += g th, C += q sh, E += q (m + Ec dm/dEc) with Ec dm/dEc = (-gs Ec) wo c'
+    //   d out/d x = q coef Ps k (1 + Ec dm/dx) with dm/dx = -gs wo (up c + c')
 #pragma unroll 1
     for (int tt = 0; tt < TPW; ++tt)  // trajectories in turn, each one's rounds interleaved
 #pragma unroll
-    for (int r = 0; r < L::RF; ++r) {
-      const int e = lane + 64 * r;
-      if (e < L::E) {
+    for (int r = 0; r < L::RP; ++r) {
+      const int p = lane + 64 * r;
+      if (p < L::EP) {
         const FT& F = Fs[tt];
         const float* gout = gouts + tt * GS;
         float* cb = cbs + tt * CBS;
-        const int i = e / (L::OUT * L::K), ok_ = e % (L::OUT * L::K);
+        const int e = 2 * p, i = e / (L::OUT * L::K), ok_ = e % (L::OUT * L::K);
         const int o = ok_ / L::K;
-        const float x = F.x[TB + i], up = F.up[TB + i], go = gout[o];
-        const float4 pe = Tb.fe[e + z];
-        const float kk = pe.x, Ec = pe.y;
-        const float cn = sigm_l2(gsl2e * (x + Ec));           // sigmoid(gs(-x - Ec))
-        const float omu = 1.0f - up;
-        const float mm = ffma(wc, omu * cn, 1.0f);            // branch_mom with branch_sign = 1
-        const float sh = ffma(Ec, mm, x);                     // shifted_x
-        const float th = ffma(-2.0f, sigm_l2(2.0f * FETODE_LOG2E * kk * sh), 1.0f);  // tanh(k sh)
-        const float q = go * ffma(-th, th, 1.0f);
+        const float4 g = F.g4[TB + i];
+        const float go = gout[o];
+        const float4 fa = Tb.fpa[p + z], fb = Tb.fpb[p + z];
+        const f2 Ec = f2{fa.x, fa.y}, k2 = f2{fa.z, fa.w}, cPk = f2{fb.x, fb.y}, Egs = f2{fb.z, fb.w};
+        const f2 x = splat(g.x), wo = splat(g.z), gv = splat(go);
+        const f2 cn = rcpx2(ex2x2((x + Ec) * splat(gsl2e)) + splat(1.0f));  // sigmoid(gs(-x - Ec))
+        const f2 mm = pfma(wo, cn, splat(1.0f));                           // branch_mom, branch_sign = 1
+        const f2 sh = pfma(Ec, mm, x);                                     // shifted_x
+        const f2 th = pfma(splat(-2.0f), rcpx2(ex2x2(k2 * sh) + splat(1.0f)), splat(1.0f));  // tanh(k sh)
+        const f2 q = gv * pfma(-th, th, splat(1.0f));
+        const f2 dcn = pfma(-cn, cn, cn);
         if constexpr (ACC) {
-          R.A[r] = ffma(go, th, R.A[r]);
-          R.C[r] = ffma(q, sh, R.C[r]);
+          R.A[r] = pfma(gv, th, R.A[r]);
+          R.C[r] = pfma(q, sh, R.C[r]);
+          R.Ev[r] = pfma(q, pfma(Egs, wo * dcn, mm), R.Ev[r]);
         }
-        const float dcn = gs * cn * (1.0f - cn), du = gs * up * omu;
-        if constexpr (ACC) {
-          const float dmdEc = -wc * omu * dcn;
-          R.Ev[r] = ffma(q, ffma(Ec, dmdEc, mm), R.Ev[r]);
-        }
-        const float dmdx = -wc * ffma(du, cn, omu * dcn);
-        cb[i * L::NTMP + ok_] = q * pe.z * ffma(Ec, dmdx, 1.0f);
+        const f2 dm = splat(g.w) * pfma(splat(g.y), cn, dcn);
+        *reinterpret_cast<f2*>(&cb[i * L::NTMP + ok_]) = (q * cPk) * pfma(Ec, dm, splat(1.0f));
       }
     }
     if constexpr (ACC)
@@ -499,12 +523,13 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
   using L1 = BL<H, D, K, NB, NG, FERRO>;
   constexpr int W = D + H, NS = NG - 1 - kSO, HALF = 64 / TPW;
   constexpr int CB = L0::IN * L0::NTMP > L1::IN * L1::NTMP ? L0::IN * L0::NTMP : L1::IN * L1::NTMP;
+  static_assert(CB % 2 == 0 && L0::NTMP % 2 == 0 && L1::NTMP % 2 == 0, "8-byte pair stores into the cb table");
   static_assert(W <= HALF && (TPW == 1 || TPW == 2 || TPW == 4), "one lane per input of each trajectory");
   __shared__ BInTab<W, NG, NB> TI;
   __shared__ BTab<L0> T0;
   __shared__ BTab<L1> T1;
   __shared__ BFeat<W, NS, NB> sF[kTPB][TPW];
-  __shared__ float s_cb[kTPB][TPW][CB];
+  __shared__ __attribute__((aligned(16))) float s_cb[kTPB][TPW][CB];  // f2 stores (pairs)
   __shared__ float s_g1[kTPB][TPW][D], s_g0[kTPB][TPW][H], s_gx[kTPB][TPW][D];
   __shared__ float s_ak[kTPB][TPW][4][D], s_ay[kTPB][TPW][D], s_ac[kTPB][4][3];
 
@@ -598,7 +623,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
         if (sl < D) g1s[tt * D + sl] = ak[st][sl];
         wsync();
         // features of both layers' inputs: one code path over the combined input index
-        if (sl < W) feat_input<W, NG, NB>(F, TI, sl, glane, z);
+        if (sl < W) feat_input<W, NG, NB>(F, TI, sl, glane, sl < D ? wc0 : wc1, sl < D ? gs0 : gs1, z);
         for (int q = lane; q < TPW * W * NB; q += 64) {
           const int qt = q / (W * NB), qq = q % (W * NB);
           Fs[qt].sg[qq] = sigm_l2(ffma(TI.lg[2 * qq + z], Fs[qt].x[qq / NB], TI.lg[2 * qq + 1 + z]));
@@ -682,7 +707,8 @@ __global__ __launch_bounds__(256) void param_sum_kernel(BwdArgs a) {
   // this thread's jobs and their constants
   const bool fjob = tid < E;
   const int e = fjob ? tid : 0, fi = e / (OUT * K), fo = (e % (OUT * K)) / K;
-  const float4 fe = Tb.fe[e];
+  const float4 fpa = Tb.fpa[e >> 1];
+  const float fEc = (e & 1) ? fpa.y : fpa.x, fk2 = (e & 1) ? fpa.w : fpa.z;  // Ec, 2 log2e k
   const bool ejob = tid >= E && tid < E + NE;
   const int q = ejob ? tid - E : 0, eo = q / IN, ei = q % IN;
   const int lq0 = tid - E - NE;
@@ -791,12 +817,12 @@ __global__ __launch_bounds__(256) void param_sum_kernel(BwdArgs a) {
 #pragma unroll 4
       for (int s = 0; s < TS; ++s) {  // layer_jobs' Ferro element VJP, sums only
         const float x = sx[s][fi], up = sup[s][fi], go = sgo[s][fo];
-        const float kk = fe.x, Ec = fe.y;
+        const float Ec = fEc;
         const float cn = sigm_l2(gsl * (x + Ec));
         const float omu = 1.0f - up;
         const float mm = ffma(wc, omu * cn, 1.0f);
         const float sh = ffma(Ec, mm, x);
-        const float th = ffma(-2.0f, sigm_l2(2.0f * FETODE_LOG2E * kk * sh), 1.0f);
+        const float th = ffma(-2.0f, sigm_l2(fk2 * sh), 1.0f);
         const float qv = go * ffma(-th, th, 1.0f);
         A = ffma(go, th, A);
         C = ffma(qv, sh, C);
