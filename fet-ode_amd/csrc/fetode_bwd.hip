@@ -218,8 +218,29 @@ struct BReg {  // per-lane register slice of one layer: its gradient sums
     }
   }
 
-  __device__ void store(float* __restrict__ part, int lane) const {
+  // TPW > 1: job sets that fit in 64 / TPW lanes ran once per trajectory on lanes tt * LPT + job
+  // (layer_jobs), so their sums are combined here, trajectories in order
+  template <int TPW>
+  __device__ void store(float* __restrict__ part, int lane) {
     constexpr AccLayout AL = L::AL;
+    constexpr int LPT = 64 / TPW;
+    auto comb = [&](float v) {
+      float t = v;
+#pragma unroll
+      for (int k = 1; k < TPW; ++k) t += __shfl(v, lane + k * LPT);
+      return t;
+    };
+    if constexpr (TPW > 1 && L::NE <= LPT) {
+      base[0] = comb(base[0]);
+#pragma unroll
+      for (int c = 0; c < L::NS; ++c) spl[0][c] = comb(spl[0][c]);
+    }
+    if constexpr (TPW > 1 && L::NL <= LPT) {
+#pragma unroll
+      for (int o = 0; o < L::OUT; ++o) lw[0][o] = comb(lw[0][o]);
+      la[0] = comb(la[0]);
+      lb[0] = comb(lb[0]);
+    }
 #pragma unroll
     for (int r = 0; r < L::RP; ++r) {
       const int e = 2 * (lane + 64 * r);
@@ -365,12 +386,11 @@ __device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict
 #pragma unroll
         for (int tt = 0; tt < TPW; ++tt) R.G += gouts[tt * GS + lane];
   }
-#pragma unroll 1
-  for (int tt = 0; tt < TPW; ++tt)
-#pragma unroll
-  for (int r = 0; r < L::RE; ++r) {
-    const int q = lane + 64 * r;
-    if (q < L::NE) {
+  // KAN edges (and below, logistic pairs): when one trajectory's jobs fit in 64 / TPW lanes, every
+  // trajectory's jobs run in ONE round (lane = tt * 64 / TPW + job); the lane sums of one job are
+  // combined across trajectories once, at store
+  auto edge = [&](int tt, int q, int r) __attribute__((always_inline)) {
+    {
       const FT& F = Fs[tt];
       float* cb = cbs + tt * CBS;
       const int o = q / L::IN, i = q % L::IN;
@@ -392,13 +412,19 @@ __device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict
       const float wb = Tb.kw[o * (L::IN * L::NFL) + i * L::NFL + z];
       cb[i * L::NTMP + L::OUT * L::K + o] = go * ffma(wb, F.dsilu[TB + i], dsdx);
     }
-  }
+  };
+  constexpr int LPT = 64 / TPW;
+  if constexpr (L::NE <= LPT) {
+    if (lane % LPT < L::NE) edge(lane / LPT, lane % LPT, 0);
+  } else {
 #pragma unroll 1
-  for (int tt = 0; tt < TPW; ++tt)
+    for (int tt = 0; tt < TPW; ++tt)
 #pragma unroll
-  for (int r = 0; r < L::RL; ++r) {
-    const int q = lane + 64 * r;
-    if (q < L::NL) {
+    for (int r = 0; r < L::RE; ++r)
+      if (lane + 64 * r < L::NE) edge(tt, lane + 64 * r, r);
+  }
+  auto logi = [&](int tt, int q, int r) __attribute__((always_inline)) {
+    {
       const FT& F = Fs[tt];
       const float* gout = gouts + tt * GS;
       float* cb = cbs + tt * CBS;
@@ -419,6 +445,15 @@ __device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict
       }
       cb[i * L::NTMP + L::OUT * L::K + L::OUT + j] = T * pa;
     }
+  };
+  if constexpr (L::NL <= LPT) {
+    if (lane % LPT < L::NL) logi(lane / LPT, lane % LPT, 0);
+  } else {
+#pragma unroll 1
+    for (int tt = 0; tt < TPW; ++tt)
+#pragma unroll
+    for (int r = 0; r < L::RL; ++r)
+      if (lane + 64 * r < L::NL) logi(tt, lane + 64 * r, r);
   }
 }
 
@@ -660,8 +695,8 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
   }
   if constexpr (ACC) {
     float* part = a.part + ((int64_t)blockIdx.x * kTPB + wid) * a.nacc;
-    R0.store(part, lane);
-    R1.store(part + L0::AL.n, lane);
+    R0.template store<TPW>(part, lane);
+    R1.template store<TPW>(part + L0::AL.n, lane);
   }
 }
 
