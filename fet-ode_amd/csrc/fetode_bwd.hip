@@ -40,6 +40,9 @@ using namespace fetode;
 namespace {
 
 constexpr int kSO = 3;  // spline order of the fused kernels (efficientkan default)
+#ifndef FETODE_EXP_SKIP  // diagnostics only (phase-cost attribution): 1 Ferro, 2 edges, 4 logistic,
+#define FETODE_EXP_SKIP 0  // 8 features, 16 d/dx reductions — results are wrong when set
+#endif
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2 pfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
@@ -345,7 +348,7 @@ template <class L, int TB, bool ACC, int TPW, int GS, int CBS, class FT>
 __device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict__ gouts, const BTab<L>& Tb,
                                            const float* __restrict__ rhs, BReg<L>& R, float* __restrict__ cbs,
                                            float gsl2e, float wc, float gs, int lane, int z) {
-  if constexpr (L::FERRO) {
+  if constexpr (L::FERRO && !(FETODE_EXP_SKIP & 1)) {
     // element pairs (k, k+1) of one (i, o) on packed-fp32 ops; with wo = wc (1 - up), c' = c (1 - c):
     //   c = sigmoid(gs(-x - Ec)), m = 1 + wo c, sh = x + Ec m, th = tanh(k sh), q = g (1 - th^2)
     //   A += g th, C += q sh, E += q (m + Ec dm/dEc) with Ec dm/dEc = (-gs Ec) wo c'
@@ -414,7 +417,8 @@ __device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict
     }
   };
   constexpr int LPT = 64 / TPW;
-  if constexpr (L::NE <= LPT) {
+  if constexpr (FETODE_EXP_SKIP & 2) {
+  } else if constexpr (L::NE <= LPT) {
     if (lane % LPT < L::NE) edge(lane / LPT, lane % LPT, 0);
   } else {
 #pragma unroll 1
@@ -446,7 +450,8 @@ __device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict
       cb[i * L::NTMP + L::OUT * L::K + L::OUT + j] = T * pa;
     }
   };
-  if constexpr (L::NL <= LPT) {
+  if constexpr (FETODE_EXP_SKIP & 4) {
+  } else if constexpr (L::NL <= LPT) {
     if (lane % LPT < L::NL) logi(lane / LPT, lane % LPT, 0);
   } else {
 #pragma unroll 1
@@ -457,22 +462,29 @@ __device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict
   }
 }
 
-// gin[i] = sum_t cb[i * NTM + t], fixed order: LPI lanes per input, strided partial sums, DPP tree;
-// with TPW trajectories per wave each takes 64 / TPW lanes (cbs + tt * CBS -> gins + tt * GS)
+// gin[i] = sum_t cb[i * NTMP + t], fixed order: LPI lanes per input, each summing a contiguous
+// run of float4 chunks, then a DPP tree; with TPW trajectories per wave each takes 64 / TPW lanes
+// (cbs + tt * CBS -> gins + tt * GS)
 template <class L, int TPW, int GS, int CBS>
 __device__ __forceinline__ void reduce_gin(const float* __restrict__ cbs, float* gins, int lane) {
+  if constexpr (FETODE_EXP_SKIP & 16) return;
   constexpr int HALF = 64 / TPW;
   constexpr int LPI0 = pow2_floor(HALF / L::IN);
   constexpr int LPI = LPI0 > 32 ? 32 : (L::LPI < LPI0 ? L::LPI : LPI0);
+  constexpr int C4 = (L::NTM + 4 * LPI - 1) / (4 * LPI);  // float4 chunks per lane
+  static_assert(L::NTM % 4 == 0 && L::NTMP % 4 == 0 && CBS % 4 == 0, "float4 rows of the cb table");
   const int tt = lane / HALF, sl = lane % HALF;
   const int i = sl / LPI, sub = sl % LPI;
-  const float* cb = cbs + tt * CBS;
+  const float4* cb = reinterpret_cast<const float4*>(cbs + tt * CBS + i * L::NTMP);
   float s = 0.f;
   if (i < L::IN) {
 #pragma unroll
-    for (int k = 0; k < (L::NTM + LPI - 1) / LPI; ++k) {
-      const int t = sub + k * LPI;
-      if (t < L::NTM) s += cb[i * L::NTMP + t];
+    for (int k = 0; k < C4; ++k) {
+      const int c = sub * C4 + k;
+      if (4 * c < L::NTM) {
+        const float4 v = cb[c];
+        s += (v.x + v.y) + (v.z + v.w);
+      }
     }
   }
   s = group_sum<LPI>(s);
@@ -658,7 +670,8 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
         if (sl < D) g1s[tt * D + sl] = ak[st][sl];
         wsync();
         // features of both layers' inputs: one code path over the combined input index
-        if (sl < W) feat_input<W, NG, NB>(F, TI, sl, glane, sl < D ? wc0 : wc1, sl < D ? gs0 : gs1, z);
+        if (!(FETODE_EXP_SKIP & 8) && sl < W) feat_input<W, NG, NB>(F, TI, sl, glane, sl < D ? wc0 : wc1, sl < D ? gs0 : gs1, z);
+        if (!(FETODE_EXP_SKIP & 8))
         for (int q = lane; q < TPW * W * NB; q += 64) {
           const int qt = q / (W * NB), qq = q % (W * NB);
           Fs[qt].sg[qq] = sigm_l2(ffma(TI.lg[2 * qq + z], Fs[qt].x[qq / NB], TI.lg[2 * qq + 1 + z]));
