@@ -190,7 +190,7 @@ struct BTab {  // per-block LDS copy of one layer's edge tables
 template <int W, int NS, int NB>
 struct BFeat {  // per-wave LDS features of both layers' inputs, combined index t
   float4 g4[W];  // Ferro per-input terms: x, gate up, wc (1 - up), -gs wc (1 - up)
-  float x[W], pv[W], silu[W], dsilu[W], u[W];
+  float x[W], pv[W], silu[W], dsilu[W], u[W], rhm[W];  // rhm: 1 / (knot step) of x's interval
   int m[W];
   float bd[W * NS];
   float sg[NB > 0 ? W * NB : 1];
@@ -313,27 +313,43 @@ __device__ __forceinline__ void feat_input(BFeat<W, NG - 1 - kSO, NB>& F, const 
   F.dsilu[t] = sx * ffma(x, 1.0f - sx, 1.0f);
   const float* g = &Tb.knots[t * NG + z];
   int m = -1;
+  if constexpr (NG % 4 == 0) {  // the row as float4s: every knot read issued at once
+    const float4* g4 = reinterpret_cast<const float4*>(g);
 #pragma unroll
-  for (int j = 0; j < NG; ++j) m += (x >= g[j]) ? 1 : 0;
+    for (int j = 0; j < NG / 4; ++j) {
+      const float4 v = g4[j];
+      m += ((x >= v.x) ? 1 : 0) + ((x >= v.y) ? 1 : 0) + ((x >= v.z) ? 1 : 0) + ((x >= v.w) ? 1 : 0);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NG; ++j) m += (x >= g[j]) ? 1 : 0;
+  }
   const bool fin = __builtin_isfinite(x);
   const bool in = fin && m >= 0 && m < NI;
   const int mc = in ? m : 0;
-  const float u = in ? (x - g[mc]) * Tb.rh[t * NI + mc + z] : (fin ? 0.f : __builtin_nanf(""));
+  const float rhm = Tb.rh[t * NI + mc + z];
+  const float u = in ? (x - g[mc]) * rhm : (fin ? 0.f : __builtin_nanf(""));
+  F.rhm[t] = rhm;
   F.m[t] = in ? m : NI;
   F.u[t] = u;
   float* bd = &F.bd[t * NS];
   // non-finite x: NaN bases like the reference's (x - g)/d * 0; outside the grid: all zero
   const float fill = fin ? 0.f : __builtin_nanf("");
+  // the interval's four basis cubics, all reads issued before any use; the dense row is formed
+  // in registers and written once
+  const float4* bp = &Tb.bp[(t * NI + mc) * 4 + z];
+  float4 p[kSO + 1];
 #pragma unroll
-  for (int c = 0; c < NS; ++c) bd[c] = fill;
-  if (in) {
-    const float4* bp = &Tb.bp[(t * NI + mc) * 4 + z];
+  for (int r = 0; r <= kSO; ++r) p[r] = bp[r];
+  float v[kSO + 1];
 #pragma unroll
-    for (int r = 0; r <= kSO; ++r) {
-      const int c = mc - kSO + r;
-      const float4 p = bp[r];
-      if (c >= 0 && c < NS) bd[c] = ffma(ffma(ffma(p.w, u, p.z), u, p.y), u, p.x);
-    }
+  for (int r = 0; r <= kSO; ++r) v[r] = ffma(ffma(ffma(p[r].w, u, p[r].z), u, p[r].y), u, p[r].x);
+#pragma unroll
+  for (int c = 0; c < NS; ++c) {
+    float b = fill;
+#pragma unroll
+    for (int r = 0; r <= kSO; ++r) b = (in && c == mc - kSO + r) ? v[r] : b;
+    bd[c] = b;
   }
   const float up = sigm_l2(-gsl2e * (x - F.pv[t]));
   const float wo = wc * (1.0f - up);
@@ -408,7 +424,7 @@ __device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict
       float dsdx;
       if (m < L::NI) {
         const float4 cf = Tb.sp[q * (L::NI + 1) + m + z];  // (o, i, interval), q = o*IN + i
-        dsdx = ffma(u, ffma(3.0f * u, cf.w, 2.0f * cf.z), cf.y) * rhs[(TB + i) * L::NI + m + z];
+        dsdx = ffma(u, ffma(3.0f * u, cf.w, 2.0f * cf.z), cf.y) * F.rhm[TB + i];
       } else {
         dsdx = u * 0.0f;  // 0 outside the grid, NaN for non-finite inputs (the reference's NaN bases)
       }
@@ -671,10 +687,25 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
         wsync();
         // features of both layers' inputs: one code path over the combined input index
         if (!(FETODE_EXP_SKIP & 8) && sl < W) feat_input<W, NG, NB>(F, TI, sl, glane, sl < D ? wc0 : wc1, sl < D ? gs0 : gs1, z);
-        if (!(FETODE_EXP_SKIP & 8))
-        for (int q = lane; q < TPW * W * NB; q += 64) {
-          const int qt = q / (W * NB), qq = q % (W * NB);
-          Fs[qt].sg[qq] = sigm_l2(ffma(TI.lg[2 * qq + z], Fs[qt].x[qq / NB], TI.lg[2 * qq + 1 + z]));
+        if (!(FETODE_EXP_SKIP & 8)) {
+          constexpr int NSG = TPW * W * NB, RSG = (NSG + 63) / 64;
+          float sa[RSG], sb[RSG], sx[RSG];
+#pragma unroll
+          for (int k = 0; k < RSG; ++k) {  // every round's operands read before any sigmoid
+            const int q = lane + 64 * k, qc = q < NSG ? q : 0;
+            const int qt = qc / (W * NB), qq = qc % (W * NB);
+            sa[k] = TI.lg[2 * qq + z];
+            sb[k] = TI.lg[2 * qq + 1 + z];
+            sx[k] = Fs[qt].x[qq / NB];
+          }
+#pragma unroll
+          for (int k = 0; k < RSG; ++k) {
+            const int q = lane + 64 * k;
+            if (q < NSG) {
+              const int qt = q / (W * NB), qq = q % (W * NB);
+              Fs[qt].sg[qq] = sigm_l2(ffma(sa[k], sx[k], sb[k]));
+            }
+          }
         }
         wsync();
         layer_jobs<L1, D, ACC, TPW, D, CB>(Fs, g1s, T1, TI.rh, R1, cbs, gl1, wc1, gs1, lane, z);
