@@ -369,7 +369,7 @@ __device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict
     //   c = sigmoid(gs(-x - Ec)), m = 1 + wo c, sh = x + Ec m, th = tanh(k sh), q = g (1 - th^2)
     //   A += g th, C += q sh, E += q (m + Ec dm/dEc) with Ec dm/dEc = (-gs Ec) wo c'
     //   d out/d x = q coef Ps k (1 + Ec dm/dx) with dm/dx = -gs wo (up c + c')
-#pragma unroll 1
+#pragma unroll
     for (int tt = 0; tt < TPW; ++tt)  // trajectories in turn, each one's rounds interleaved
 #pragma unroll
     for (int r = 0; r < L::RP; ++r) {
