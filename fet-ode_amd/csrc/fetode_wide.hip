@@ -20,9 +20,12 @@
 //             chunk start), two accumulators alternating per input (half the dependent MFMA chain).
 // Epilogue: the two K-halves and the Ferro sums (lane = row) meet the MFMA tile in LDS, fixed order.
 //
-// Direct form: a wave whose chunk input has |gs x| > 80 anywhere, or whose (output, input) has
-// |gs Ec| > 80, evaluates s = 1/(1 + 2^{gs log2e (x + Ec)}) with one more exponential (the
-// product e P could overflow a factor there).
+// Factored gate: s = 1/(1 + e P) with e = 2^{gs log2e x} staged per (row, input) and P =
+// 2^{gs log2e Ec} per element.  With |gs Ec| <= 60 for every element of an (output, input), e
+// overflowing (gs x > 88.7) or flushing (gs x < -87.3) only happens where the fp32 sigmoid is
+// already saturated (|gs (x + Ec)| > 27), and inf * P / 0 * P give its limits, so no bound on x
+// is needed.  An (output, input) with some |gs Ec| > 60 evaluates s = 1/(1 + 2^{gs log2e (x +
+// Ec)}) directly, one more exponential per element.
 #include <algorithm>
 #include <cstdlib>
 
@@ -31,6 +34,8 @@
 using namespace fetode;
 
 namespace {
+
+constexpr float kWideFactorLimit = 60.0f;  // |gs Ec| bound of the factored gate (header comment)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -52,7 +57,7 @@ struct WideLayout {
   bool kan, ferro;
   int64_t fe4;     // (out, in, K) float4 {P = 2^{gs log2e Ec}, 2 log2e k, 2 log2e k Ec, coef Ps}
   int64_t gec;     // (out, in, K) gs log2e Ec (direct form)
-  int64_t dflag;   // (out, in) 1 if some |gs Ec| > 80 for (o, i)
+  int64_t dflag;   // (out, in) 1 if some |gs Ec| > kWideFactorLimit for (o, i)
   int64_t fconst;  // (out) sum_{i,k} coef bias
   int64_t wp;      // (in, 20, out) packed KAN weights
   int64_t lg;      // (in, NB, 2) (-a log2e, a b log2e)
@@ -148,7 +153,7 @@ __global__ void wide_pack_kernel(fetode_kanlinear_t kl, fetode_ferro_t fl, WideL
   if (L.ferro && t < (int64_t)out * in) {
     const int o = (int)(t / in), i = (int)(t % in);
     float f = 0.f;
-    for (int k = 0; k < K; ++k) f = fabsf(L.gs * fl.Ec[(i * out + o) * K + k]) > 80.0f ? 1.0f : f;
+    for (int k = 0; k < K; ++k) f = fabsf(L.gs * fl.Ec[(i * out + o) * K + k]) > kWideFactorLimit ? 1.0f : f;
     plan[L.dflag + t] = f;
   }
   if (L.kan && t < (int64_t)in * kWF * out) {
@@ -255,7 +260,7 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
   const int64_t b0 = (int64_t)blockIdx.x * kRows;
   const int o0 = blockIdx.y * kOuts;
   const float* __restrict__ plan = a.plan;
-  const float gs = L.gs, gsl2e = L.gsl2e, wc = L.wc, l2 = FETODE_LOG2E;
+  const float gsl2e = L.gsl2e, wc = L.wc, l2 = FETODE_LOG2E;
 
   float facc[kJ];  // Ferro: row = lane, output o0 + kJ w + j
 #pragma unroll
@@ -338,7 +343,6 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
       for (int ii = 0; ii < kCh; ++ii) {
         const int i = i0 + ii;
         const float xv = s_x[ii * kRows + lane], wg = s_w[ii * kRows + lane], e = s_e[ii * kRows + lane];
-        const bool xbig = __any(fabsf(gs * xv) > 80.0f);  // wave-uniform
 #pragma unroll
         for (int j = 0; j < kJ; ++j) {
           const int jo = kJ * w + j;
@@ -346,7 +350,7 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
           // LDS they cost a ds_read_b128 per element (Ferro alone 270 -> 230 us at 64 -> 128)
           const float4* par = reinterpret_cast<const float4*>(plan + L.fe4) + ((int64_t)(o0 + jo) * in + i) * K;
           float acc = 0.f;
-          if (!xbig && s_dfl[jo * kCh + ii] == 0.f) {
+          if (s_dfl[jo * kCh + ii] == 0.f) {  // wave-uniform
             // elements (k, k+1) in the two halves of packed-fp32 VALU ops (v_pk_fma / mul / add:
             // 3.5 instead of 7 non-transcendental issues per element); even and odd k sum apart
             f2 acc2 = splat(0.0f);
