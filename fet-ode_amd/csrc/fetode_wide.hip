@@ -274,7 +274,16 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
   const bool stager = tid < kCh * kRows;
   const bool slive = stager && sb < a.B;
 
+  // the staging item's x / prev_x, loaded one chunk ahead (their HBM latency hides under the
+  // previous chunk's work)
+  float xn = slive ? a.x[sb * in + si] : 0.f;
+  float pn = (FERRO && slive && !a.reinit) ? a.prev[sb * in + si] : 0.f;
   for (int i0 = 0; i0 < in; i0 += kCh) {
+    const float x = xn, pvl = pn;
+    if (i0 + kCh < in) {
+      xn = slive ? a.x[sb * in + i0 + kCh + si] : 0.f;
+      pn = (FERRO && slive && !a.reinit) ? a.prev[sb * in + i0 + kCh + si] : 0.f;
+    }
     // KAN weights of this wave's chunk inputs (ii = 2 q + kh) for the MFMA B operand (L2-resident;
     // issued before the staging)
     float wb[KAN ? kCh / 2 * 5 : 1];
@@ -286,9 +295,8 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
           wb[q * 5 + s] = plan[L.wp + ((int64_t)(i0 + 2 * q + kh) * kWF + 4 * s + kq) * out + o0 + kr];
     }
     __syncthreads();  // the previous chunk is consumed
-    const float x = slive ? a.x[sb * in + i0 + si] : 0.f;
     if constexpr (FERRO) {
-      const float pv = a.reinit ? x : (slive ? a.prev[sb * in + i0 + si] : 0.f);
+      const float pv = a.reinit ? x : pvl;
       if (stager) {
       // is_moving_up = sigmoid(gate_slope (x - prev_x)) (ferro_class.py:387), w = wc (1 - up)
       const float up = rcp(1.0f + ex2(-gsl2e * (x - pv)));
