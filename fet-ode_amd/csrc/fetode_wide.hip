@@ -241,7 +241,7 @@ struct WideArgs {
 
 // ---- the layer --------------------------------------------------------------------------------
 template <int K, bool KAN, bool FERRO, int kCh>
-__global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) void wide_layer_kernel(WideArgs a) {
   constexpr int kPitch = pitch_of(kCh);
   static_assert(kCh * kRows <= kThreads && (kCh & 1) == 0, "one staging item per thread, even chunks");
   static_assert(!FERRO || K % 2 == 0, "Ferro elements in (k, k+1) pairs");
@@ -284,16 +284,6 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
       xn = slive ? a.x[sb * in + i0 + kCh + si] : 0.f;
       pn = (FERRO && slive && !a.reinit) ? a.prev[sb * in + i0 + kCh + si] : 0.f;
     }
-    // KAN weights of this wave's chunk inputs (ii = 2 q + kh) for the MFMA B operand (L2-resident;
-    // issued before the staging)
-    float wb[KAN ? kCh / 2 * 5 : 1];
-    if constexpr (KAN) {
-#pragma unroll
-      for (int q = 0; q < kCh / 2; ++q)
-#pragma unroll
-        for (int s = 0; s < 5; ++s)
-          wb[q * 5 + s] = plan[L.wp + ((int64_t)(i0 + 2 * q + kh) * kWF + 4 * s + kq) * out + o0 + kr];
-    }
     __syncthreads();  // the previous chunk is consumed
     if constexpr (FERRO) {
       const float pv = a.reinit ? x : pvl;
@@ -334,17 +324,15 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
       for (int q = 0; q < kWF; q += 2) *reinterpret_cast<float2*>(d + q) = make_float2(f[q], f[q + 1]);
     }
     __syncthreads();
+    // KAN weights of this wave's chunk inputs (ii = 2 q + kh) for the MFMA B operand (L2-resident;
+    // issued here so their latency hides under the Ferro work, and not live across the staging)
+    float wb[KAN ? kCh / 2 * 5 : 1];
     if constexpr (KAN) {
-      const float* arow = &s_phi[(16 * rt + kr) * kPitch + kq];
 #pragma unroll
-      for (int q = 0; q < kCh / 2; ++q) {
-        const int ii = 2 * q + kh;
+      for (int q = 0; q < kCh / 2; ++q)
 #pragma unroll
-        for (int s = 0; s < 5; ++s) {
-          if (q & 1) kacc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(arow[ii * kWF + 4 * s], wb[q * 5 + s], kacc1, 0, 0, 0);
-          else kacc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(arow[ii * kWF + 4 * s], wb[q * 5 + s], kacc0, 0, 0, 0);
-        }
-      }
+        for (int s = 0; s < 5; ++s)
+          wb[q * 5 + s] = plan[L.wp + ((int64_t)(i0 + 2 * q + kh) * kWF + 4 * s + kq) * out + o0 + kr];
     }
     if constexpr (FERRO) {
 #pragma unroll 2
@@ -384,6 +372,18 @@ __global__ __launch_bounds__(kThreads) void wide_layer_kernel(WideArgs a) {
             }
           }
           facc[j] += acc;  // K bases of one input first, then inputs (the reference's two-level sum)
+        }
+      }
+    }
+    if constexpr (KAN) {
+      const float* arow = &s_phi[(16 * rt + kr) * kPitch + kq];
+#pragma unroll
+      for (int q = 0; q < kCh / 2; ++q) {
+        const int ii = 2 * q + kh;
+#pragma unroll
+        for (int s = 0; s < 5; ++s) {
+          if (q & 1) kacc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(arow[ii * kWF + 4 * s], wb[q * 5 + s], kacc1, 0, 0, 0);
+          else kacc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(arow[ii * kWF + 4 * s], wb[q * 5 + s], kacc0, 0, 0, 0);
         }
       }
     }
