@@ -236,8 +236,16 @@ struct WideArgs {
   const float* grid;  // (in, 12) knots
   int64_t B;
   int reinit;
+  int nslice;  // 1, or 2: blockIdx.z takes half of the inputs and adds into a zeroed out
   float* out;
 };
+
+// One slice stores; two add into a zeroed out with vector atomics: 0 + a + b in either order is the
+// same fp32 value (addition commutes), so the split stays bitwise deterministic.
+__device__ __forceinline__ void store_out(float* p, float v, int nslice) {
+  if (nslice == 1) *p = v;
+  else atomicAdd(p, v);
+}
 
 // ---- the layer --------------------------------------------------------------------------------
 template <int K, bool KAN, bool FERRO, int kCh>
@@ -276,11 +284,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) v
 
   // the staging item's x / prev_x, loaded one chunk ahead (their HBM latency hides under the
   // previous chunk's work)
-  float xn = slive ? a.x[sb * in + si] : 0.f;
-  float pn = (FERRO && slive && !a.reinit) ? a.prev[sb * in + si] : 0.f;
-  for (int i0 = 0; i0 < in; i0 += kCh) {
+  const int ibeg = blockIdx.z * (in / a.nslice), iend = ibeg + in / a.nslice;
+  float xn = slive ? a.x[sb * in + ibeg + si] : 0.f;
+  float pn = (FERRO && slive && !a.reinit) ? a.prev[sb * in + ibeg + si] : 0.f;
+  for (int i0 = ibeg; i0 < iend; i0 += kCh) {
     const float x = xn, pvl = pn;
-    if (i0 + kCh < in) {
+    if (i0 + kCh < iend) {
       xn = slive ? a.x[sb * in + i0 + kCh + si] : 0.f;
       pn = (FERRO && slive && !a.reinit) ? a.prev[sb * in + i0 + kCh + si] : 0.f;
     }
@@ -393,7 +402,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) v
   if constexpr (FERRO) {
 #pragma unroll
     for (int j = 0; j < kJ; ++j)
-      s_fer[lane * (kOuts + 1) + kJ * w + j] = facc[j] + plan[L.fconst + o0 + kJ * w + j];
+      s_fer[lane * (kOuts + 1) + kJ * w + j] = facc[j] + (blockIdx.z == 0 ? plan[L.fconst + o0 + kJ * w + j] : 0.f);
   }
   if constexpr (KAN) {
     if (kh == 1)
@@ -408,13 +417,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) v
         const int r = 16 * rt + 4 * kq + v;
         const int64_t b = b0 + r;
         const float kv = (kacc0[v] + kacc1[v]) + s_kc[r * (kOuts + 1) + kr];
-        if (b < a.B) a.out[b * out + o0 + kr] = FERRO ? kv + s_fer[r * (kOuts + 1) + kr] : kv;
+        if (b < a.B) store_out(&a.out[b * out + o0 + kr], FERRO ? kv + s_fer[r * (kOuts + 1) + kr] : kv, a.nslice);
       }
   } else {
     for (int t = tid; t < kRows * kOuts; t += kThreads) {
       const int r = t / kOuts, c = t % kOuts;
       const int64_t b = b0 + r;
-      if (b < a.B) a.out[b * out + o0 + c] = s_fer[r * (kOuts + 1) + c];
+      if (b < a.B) store_out(&a.out[b * out + o0 + c], s_fer[r * (kOuts + 1) + c], a.nslice);
     }
   }
 }
@@ -486,8 +495,13 @@ int fetode_wide_layer_forward(const fetode_kanlinear_t* kl, const fetode_ferro_t
   a.out = out;
   const int64_t tiles = (B + kRows - 1) / kRows;
   if (tiles > 0x7fffffff) return set_err(FETODE_EINVAL, "wide layer: batch too large");
-  hipLaunchKernelGGL(pick(a.L.K, a.L.kan, a.L.ferro), dim3((unsigned)tiles, (unsigned)(a.L.out / kOuts)), dim3(kThreads), 0,
-                     (hipStream_t)stream, a);
+  // Few tiles (e.g. 128 -> 64 at B = 8192: 512 workgroups for 256 CUs x 3 resident) leave the CUs
+  // short of waves to hide the staging latency: split the inputs over two workgroups per tile.
+  const int64_t wgs = tiles * (a.L.out / kOuts);
+  a.nslice = (wgs <= 2 * 256 && (a.L.in / 2) % kChMax == 0) ? 2 : 1;
+  if (a.nslice == 2) HIP_CHECK_RET(hipMemsetAsync(out, 0, sizeof(float) * B * a.L.out, (hipStream_t)stream));
+  hipLaunchKernelGGL(pick(a.L.K, a.L.kan, a.L.ferro), dim3((unsigned)tiles, (unsigned)(a.L.out / kOuts), (unsigned)a.nslice),
+                     dim3(kThreads), 0, (hipStream_t)stream, a);
   LAUNCH_CHECK();
   return FETODE_OK;
 }
