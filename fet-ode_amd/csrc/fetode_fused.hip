@@ -259,8 +259,8 @@ __device__ __forceinline__ void permlane16_swap(float& p, float& q) {
 // sum over lanes 3k, 3k+1, 3k+2 of a row (k < 5), result on all three
 __device__ __forceinline__ float group3_sum(float v, int c) {
   const float s0 = v + dpp<0x101>(v) + dpp<0x102>(v);  // row_shl:1, row_shl:2 -> valid at c == 0
-  const float b1 = dpp<0x111>(s0);                      // row_shr:1 -> lane 3k+1 gets s0[3k]
-  const float b2 = dpp<0x112>(s0);                      // row_shr:2 -> lane 3k+2 gets s0[3k]
+  const float b1 = dppm<0x111>(s0);                     // row_shr:1 -> lane 3k+1 gets s0[3k]
+  const float b2 = dppm<0x112>(s0);                     // row_shr:2 -> lane 3k+2 gets s0[3k]
   return c == 0 ? s0 : (c == 1 ? b1 : b2);
 }
 
@@ -572,12 +572,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
       float val = ffma(sg, x_silu ? xin : xmul, xadd);
       val = x_exp ? e : val;
       val = x_x ? xin : val;
-      // knot interval: lanes c1 < NG compare against their knot, DPP row count
-      int cnt = xin >= xknot ? 1 : 0;
-      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x128, 0xF, 0xF, false);
-      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x124, 0xF, 0xF, false);
-      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x122, 0xF, 0xF, false);
-      cnt += __builtin_amdgcn_update_dpp(0, cnt, 0x121, 0xF, 0xF, false);
+      // knot interval: lanes c1 < NG compare against their knot (the rest hold +inf), the row's
+      // count from the wave ballot
+      const int cnt = (int)__builtin_popcountll((__builtin_amdgcn_ballot_w64(xin >= xknot) >> (tid & 48)) & 0xFFFFull);
       const int mm = cnt - 1;
       const bool fin = __builtin_isfinite(xin);
       const int mfix = ((unsigned)mm < (unsigned)NI && fin) ? mm : NI;
