@@ -587,17 +587,24 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
   constexpr int W = D + H, NS = NG - 1 - kSO, HALF = 64 / TPW;
   constexpr int CB = L0::IN * L0::NTMP > L1::IN * L1::NTMP ? L0::IN * L0::NTMP : L1::IN * L1::NTMP;
   static_assert(CB % 2 == 0 && L0::NTMP % 2 == 0 && L1::NTMP % 2 == 0, "8-byte pair stores into the cb table");
-  static_assert(W <= HALF && (TPW == 1 || TPW == 2 || TPW == 4), "one lane per input of each trajectory");
+  // PF: features are adjoint-free, so they are formed for two evaluations at once (ev on lanes
+  // [0, FH) of a trajectory's half, ev - 1 on [FH, HALF)) every other evaluation, into LDS buffers
+  // indexed by evaluation parity: the per-input phase's instructions serve twice the lanes.  Only
+  // the Ferro sweep with sums pairs them (the others would lose occupancy to the second buffer).
+  constexpr bool PF = FERRO && ACC && 2 * W <= HALF;
+  constexpr int FH = PF ? HALF / 2 : HALF, NBUF = PF ? 2 : 1;
+  static_assert(W <= FH && (TPW == 1 || TPW == 2 || TPW == 4), "one lane per input of each trajectory and evaluation");
   __shared__ BInTab<W, NG, NB> TI;
   __shared__ BTab<L0> T0;
   __shared__ BTab<L1> T1;
-  __shared__ BFeat<W, NS, NB> sF[kTPB][TPW];
+  __shared__ BFeat<W, NS, NB> sF[kTPB][NBUF][TPW];
   __shared__ __attribute__((aligned(16))) float s_cb[kTPB][TPW][CB];  // f2 stores (pairs)
   __shared__ float s_g1[kTPB][TPW][D], s_g0[kTPB][TPW][H], s_gx[kTPB][TPW][D];
   __shared__ float s_ak[kTPB][TPW][4][D], s_ay[kTPB][TPW][D], s_ac[kTPB][4][3];
 
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int tt = lane / HALF, sl = lane % HALF;  // this lane's trajectory in the per-input phases
+  const int fb = sl / FH, fsl = sl % FH;          // feature lanes: evaluation ev - fb, input fsl
   TI.stage(a.plan, a.P0, a.P1, D, threadIdx.x, 64 * kTPB);
   T0.stage(a.k0, a.f0, a.plan, a.P0, threadIdx.x, 64 * kTPB);
   T1.stage(a.k1, a.f1, a.plan, a.P1, threadIdx.x, 64 * kTPB);
@@ -609,8 +616,6 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
   }
   __syncthreads();  // tables staged; from here on every wave syncs only with itself
 
-  BFeat<W, NS, NB>* Fs = sF[wid];
-  BFeat<W, NS, NB>& F = Fs[tt];
   float* cbs = &s_cb[wid][0][0];
   float* g1s = &s_g1[wid][0][0];  // layer-1 output adjoint = d loss / d k_stage
   float* g0s = &s_g0[wid][0][0];  // layer-0 output adjoint = d loss / d h
@@ -620,7 +625,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
   float(&acs)[4][3] = s_ac[wid];
   const float gs0 = (float)a.f0.gate_slope, gs1 = (float)a.f1.gate_slope;
   const float gl0 = a.P0.gsl2e, gl1 = a.P1.gsl2e, wc0 = a.P0.wc, wc1 = a.P1.wc;
-  const float glane = sl < D ? gl0 : gl1;  // the feature lane's layer
+  const float glane = fsl < D ? gl0 : gl1, wlane = fsl < D ? wc0 : wc1, slane = fsl < D ? gs0 : gs1;  // the feature lane's layer
   const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4 : a.method == FETODE_MIDPOINT ? 2 : 1;
   const int64_t tstride = a.B * W;
   const int n_ev = a.n_steps * ns;
@@ -632,14 +637,17 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
     const bool live = b < a.B;
     const int64_t bc_ = live ? b : b0;
     // the hysteresis input of evaluation ev is the layer input of ev - 1 (ferro_class.py:409)
+    // (any ev < 0 reads the state before the solve: the paired feature lanes of a last pair (0, -1)
+    // fill a buffer nothing reads)
     auto tape_at = [&](int ev) -> float {
-      if (sl >= W || !live) return 0.f;
-      if (ev >= 0) return a.tape[(int64_t)ev * tstride + b * W + sl];
-      const float v = a.tape[b * W + sl];  // before evaluation 0: the stored state / reinit rule
-      if (sl < D) return (a.init_mask & 1u) ? v : (FERRO ? a.state0[b * D + sl] : 0.f);
-      return (a.init_mask & 2u) ? v : (FERRO ? a.state0[a.B * D + b * H + (sl - D)] : 0.f);
+      if (fsl >= W || !live) return 0.f;
+      if (ev >= 0) return a.tape[(int64_t)ev * tstride + b * W + fsl];
+      const float v = a.tape[b * W + fsl];  // before evaluation 0: the stored state / reinit rule
+      if (fsl < D) return (a.init_mask & 1u) ? v : (FERRO ? a.state0[b * D + fsl] : 0.f);
+      return (a.init_mask & 2u) ? v : (FERRO ? a.state0[a.B * D + b * H + (fsl - D)] : 0.f);
     };
-    float cur = tape_at(n_ev - 1), prv = tape_at(n_ev - 2);
+    // this feature lane's layer input and hysteresis input, for evaluation ev - fb of the next pair
+    float cur = tape_at(n_ev - 1 - fb), prv = tape_at(n_ev - 2 - fb);
     float ay1 = 0.f;  // adjoint of y at the end of the current step (lanes sl < D)
     int jj = a.T - 1;
     for (int s = a.n_steps - 1; s >= 0; --s) {
@@ -678,36 +686,57 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
         // from hoisting ~100 loop-invariant LDS values into VGPRs, which halves occupancy)
         int z = 0;
         asm volatile("" : "+s"(z));
-        const float nxt = tape_at(ev - 2);  // prefetch: consumed by the next evaluation
-        if (sl < W) {
-          F.x[sl] = cur;
-          F.pv[sl] = prv;
+        // features of evaluations ev and ev - 1 (every other evaluation; wave-uniform)
+        const bool fstep = !PF || ((n_ev - 1 - ev) & 1) == 0;
+        float nx1 = 0.f, nx2 = 0.f;
+        BFeat<W, NS, NB>& FF = sF[wid][PF ? (ev - fb) & 1 : 0][tt];
+        if (fstep) {
+          if constexpr (PF) {  // prefetch: consumed by the next pair
+            nx1 = tape_at(ev - fb - 2);
+            nx2 = tape_at(ev - fb - 3);
+          } else {  // the next evaluation's layer input is this one's hysteresis input
+            nx1 = prv;
+            nx2 = tape_at(ev - 2);
+          }
+          if (fsl < W) {
+            FF.x[fsl] = cur;
+            FF.pv[fsl] = prv;
+          }
         }
         if (sl < D) g1s[tt * D + sl] = ak[st][sl];
         wsync();
-        // features of both layers' inputs: one code path over the combined input index
-        if (!(FETODE_EXP_SKIP & 8) && sl < W) feat_input<W, NG, NB>(F, TI, sl, glane, sl < D ? wc0 : wc1, sl < D ? gs0 : gs1, z);
-        if (!(FETODE_EXP_SKIP & 8)) {
-          constexpr int NSG = TPW * W * NB, RSG = (NSG + 63) / 64;
-          float sa[RSG], sb[RSG], sx[RSG];
+        if (fstep) {
+          // both layers' inputs on one code path over the combined input index
+          if (!(FETODE_EXP_SKIP & 8) && fsl < W) feat_input<W, NG, NB>(FF, TI, fsl, glane, wlane, slane, z);
+          if (!(FETODE_EXP_SKIP & 8)) {
+            constexpr int NSG = TPW * W * NB, RSG = (NSG + 63) / 64;
 #pragma unroll
-          for (int k = 0; k < RSG; ++k) {  // every round's operands read before any sigmoid
-            const int q = lane + 64 * k, qc = q < NSG ? q : 0;
-            const int qt = qc / (W * NB), qq = qc % (W * NB);
-            sa[k] = TI.lg[2 * qq + z];
-            sb[k] = TI.lg[2 * qq + 1 + z];
-            sx[k] = Fs[qt].x[qq / NB];
-          }
+            for (int pb = 0; pb < NBUF; ++pb) {  // one parity buffer at a time (register pressure)
+              BFeat<W, NS, NB>* Fp = sF[wid][pb];
+              float sa[RSG], sb[RSG], sx[RSG];
 #pragma unroll
-          for (int k = 0; k < RSG; ++k) {
-            const int q = lane + 64 * k;
-            if (q < NSG) {
-              const int qt = q / (W * NB), qq = q % (W * NB);
-              Fs[qt].sg[qq] = sigm_l2(ffma(sa[k], sx[k], sb[k]));
+              for (int k = 0; k < RSG; ++k) {  // every round's operands read before any sigmoid
+                const int q = lane + 64 * k, qc = q < NSG ? q : 0;
+                const int qt = qc / (W * NB), qq = qc % (W * NB);
+                sa[k] = TI.lg[2 * qq + z];
+                sb[k] = TI.lg[2 * qq + 1 + z];
+                sx[k] = Fp[qt].x[qq / NB];
+              }
+#pragma unroll
+              for (int k = 0; k < RSG; ++k) {
+                const int q = lane + 64 * k;
+                if (q < NSG) {
+                  const int qt = q / (W * NB), qq = q % (W * NB);
+                  Fp[qt].sg[qq] = sigm_l2(ffma(sa[k], sx[k], sb[k]));
+                }
+              }
             }
           }
+          wsync();
+          cur = nx1;
+          prv = nx2;
         }
-        wsync();
+        BFeat<W, NS, NB>* Fs = sF[wid][PF ? ev & 1 : 0];
         layer_jobs<L1, D, ACC, TPW, D, CB>(Fs, g1s, T1, TI.rh, R1, cbs, gl1, wc1, gs1, lane, z);
         wsync();
         reduce_gin<L1, TPW, H, CB>(cbs, g0s, lane);  // d loss / d h
@@ -729,8 +758,6 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
           for (int j = 0; j < st; ++j) ak[j][sl] = ffma(acs[st][j], ax, ak[j][sl]);
         }
         wsync();
-        cur = prv;
-        prv = nxt;
       }
       ay1 = sl < D ? ay[sl] : 0.f;
     }
