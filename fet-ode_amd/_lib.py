@@ -12,6 +12,26 @@ from typing import List, Optional, Sequence
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+
+# Parameter generation: bumped after every torch optimizer step (any optimizer, global hook).
+# The descriptor / plan / packed-weight caches key on (storage, version counter) of every
+# parameter, but fused optimizers (torch.optim.Adam(fused=True): torch._fused_adam_) update
+# parameters in place WITHOUT bumping version counters, so the generation is part of each key.
+_PARAM_GEN = [0]
+
+
+def _on_optimizer_step(optimizer, args, kwargs) -> None:
+    _PARAM_GEN[0] += 1
+
+
+from torch.optim.optimizer import register_optimizer_step_post_hook  # noqa: E402
+
+register_optimizer_step_post_hook(_on_optimizer_step)
+
+
+def param_generation() -> int:
+    """Number of optimizer steps taken in this process (any optimizer)."""
+    return _PARAM_GEN[0]
 LIB_PATH = os.environ.get("FETODE_LIB", os.path.join(_HERE, "libfetode.so"))
 
 FETODE_OK, FETODE_EINVAL, FETODE_EUNSUPPORTED, FETODE_EHIP = 0, 1, 2, 3

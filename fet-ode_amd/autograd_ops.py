@@ -245,9 +245,9 @@ def _field_tensors(model):
 
 def _handle_key(model, B, device):
     """Identity (storage, version counter, leading size) of every tensor the descriptor points
-    at, or None when a tensor would be converted (non-fp32 / non-contiguous) — the converted copy
+    at plus the optimizer-step generation (_lib.param_generation), or None when a tensor would be converted (non-fp32 / non-contiguous) — the converted copy
     could go stale silently."""
-    key = [B, device]
+    key = [B, device, _lib.param_generation()]
     for t in _field_tensors(model):
         if t.dtype != torch.float32 or not t.is_contiguous():
             return None
@@ -408,7 +408,7 @@ def _wide_key(kan, fer, device):
         ts += [kan.grid, *[p for p in kan_params(kan) if p is not None]]
     if fer is not None:
         ts += [getattr(fer, n) for n in FERRO_PARAM_NAMES]
-    key = [str(device)]
+    key = [str(device), _lib.param_generation()]
     for t in ts:
         if t.dtype != torch.float32 or not t.is_contiguous() or t.device != device:
             return None

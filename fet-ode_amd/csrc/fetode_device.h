@@ -115,4 +115,33 @@ __device__ __forceinline__ void bspline_local_div(float x, int NG, const float* 
   }
 }
 
+// ---- cross-lane helpers (DPP) -------------------------------------------------------------
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF,
+                                                               false));
+}
+// the same with an undefined old value (no zero-init move): only for controls where every lane
+// reads a valid source (row_newbcast)
+template <int CTRL>
+__device__ __forceinline__ float dppm(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// sum over the 16 lanes of a row, result on every lane of the row
+__device__ __forceinline__ float row_sum16(float v) {
+  v += dpp<0x128>(v);  // row_ror:8
+  v += dpp<0x124>(v);  // row_ror:4
+  v += dpp<0x122>(v);  // row_ror:2
+  v += dpp<0x121>(v);  // row_ror:1
+  return v;
+}
+// gfx950 lane swaps, in place: permlane32 swaps lanes 32-63 of p with lanes 0-31 of q; permlane16
+// swaps the odd rows of p with the even rows of q.  Inline asm: this compiler's builtins for them
+// treat the two results as one register.  The s_nop covers the VALU-write -> permlane-read hazard.
+__device__ __forceinline__ void permlane32_swap(float& p, float& q) {
+  asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(p), "+v"(q));
+}
+__device__ __forceinline__ void permlane16_swap(float& p, float& q) {
+  asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(p), "+v"(q));
+}
 }  // namespace fetode

@@ -345,7 +345,7 @@ def _try_ecg_resident(func, y0, tp, reversed_, rtol, atol, options):
     keep = []
     d = basis.desc(keep)
     w = func.proj.weight
-    key = (w.data_ptr(), w._version)
+    key = (w.data_ptr(), w._version, _lib.param_generation())
     cached = getattr(func, "_fetode_wT", None)
     if cached is None or cached[0] != key:
         cached = (key, w.detach().t().contiguous().float())

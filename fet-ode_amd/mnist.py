@@ -147,7 +147,7 @@ class KANLinear(nn.Module):
         """The weights in the MFMA head's layout, re-packed whenever a weight tensor changes."""
         ws = [t for t in (self.base_weight, self.spline_weight, getattr(self, "spline_scaler", None),
                           getattr(self, "logistic_weight", None)) if t is not None]
-        key = tuple((t.data_ptr(), t._version) for t in ws)
+        key = (_lib.param_generation(), *((t.data_ptr(), t._version) for t in ws))
         cached = getattr(self, "_wide_cache", None)
         if cached is None or cached[0] != key:
             lib = _lib.load()

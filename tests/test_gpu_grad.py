@@ -367,3 +367,29 @@ def test_training_grads_through_dopri5_kan(dev):
     env(y0g.grad, ref[torch.float32][1], ref[torch.float64][1], "y0")
     for n, p in m.named_parameters():
         env(p.grad, ref[torch.float32][2][n], ref[torch.float64][2][n], n)
+
+
+def test_fused_solve_follows_fused_adam_steps(dev):
+    """torch.optim.Adam(fused=True) updates parameters without bumping version counters; the
+    cached descriptor / plan must still follow every step (_lib.param_generation): after each
+    step the fused solve equals a solve of a fresh copy of the model with the stepped weights."""
+    import fet_ode_amd as F
+    from oracle import torch_ref as O
+    torch.manual_seed(0)
+    m = F.KANFET([2, 10, 2], grid_size=5).to(dev)
+    y0 = O.lv_y0(64).to(dev)
+    t = torch.tensor(np.linspace(0, 3.5, 35))
+    opt = torch.optim.Adam(m.parameters(), lr=1e-2, fused=True)
+    for _ in range(3):
+        opt.zero_grad(set_to_none=True)
+        m.reset_state()
+        F.odeint(F.autonomous(m), y0, t, method="rk4").square().mean().backward()
+        opt.step()
+        fresh = F.KANFET([2, 10, 2], grid_size=5).to(dev)
+        fresh.load_state_dict(m.state_dict())
+        with torch.no_grad():
+            m.reset_state()
+            fresh.reset_state()
+            a = F.odeint(F.autonomous(m), y0, t, method="rk4")
+            b = F.odeint(F.autonomous(fresh), y0, t, method="rk4")
+        assert torch.equal(a, b)

@@ -1,0 +1,35 @@
+"""Host-side cache keys (no GPU): the descriptor / plan caches must follow every optimizer step,
+including fused optimizers that update parameters without bumping version counters."""
+import torch
+
+import fet_ode_amd as F
+from fet_ode_amd import _lib
+from fet_ode_amd.autograd_ops import _handle_key
+
+
+def _step(opt, m):
+    for p in m.parameters():
+        p.grad = torch.ones_like(p)
+    opt.step()
+
+
+def test_fused_adam_does_not_bump_versions_but_invalidates_the_key():
+    torch.manual_seed(0)
+    m = F.KANFET([2, 10, 2], grid_size=5)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3, fused=True)
+    versions = [p._version for p in m.parameters()]
+    k0 = _handle_key(m, 8, torch.device("cpu"))
+    g0 = _lib.param_generation()
+    _step(opt, m)
+    assert [p._version for p in m.parameters()] == versions  # why the generation exists
+    assert _lib.param_generation() == g0 + 1
+    assert _handle_key(m, 8, torch.device("cpu")) != k0
+
+
+def test_plain_optimizers_invalidate_the_key():
+    torch.manual_seed(0)
+    m = F.KANFET([2, 10, 2], grid_size=5)
+    for opt in (torch.optim.Adam(m.parameters(), lr=1e-3), torch.optim.SGD(m.parameters(), lr=1e-2)):
+        k0 = _handle_key(m, 8, torch.device("cpu"))
+        _step(opt, m)
+        assert _handle_key(m, 8, torch.device("cpu")) != k0
