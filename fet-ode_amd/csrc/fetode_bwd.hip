@@ -165,17 +165,17 @@ struct BTab {  // per-block LDS copy of one layer's edge tables
   float kw[L::OUT * L::IN * L::NFL];        // SiLU weight, 2 * scaled logistic weights
   float pa[L::NL > 0 ? L::NL : 1], pb[L::NL > 0 ? L::NL : 1];
   // Ferro element pair p = elements (2p, 2p + 1) = (i, o, k..k+1):
-  //   fpa = (Ec, Ec', 2 log2e k, 2 log2e k'),  fpb = (coef Ps k, coef' Ps' k', -gs Ec, -gs Ec')
+  //   fpa = (Ec, Ec', 2 log2e k, 2 log2e k'),  fpb = (coef Ps k, coef' Ps' k', gs log2e Ec, gs log2e Ec')
   float4 fpa[L::EP > 0 ? L::EP : 1], fpb[L::EP > 0 ? L::EP : 1];
 
   __device__ void stage(const fetode_kanlinear_t& kl, const fetode_ferro_t& fl, const float* __restrict__ plan,
                         const LayerPlan& P, int tid, int nt) {
-    const float gs = L::FERRO ? (float)fl.gate_slope : 0.f, k2 = 2.0f * FETODE_LOG2E;
+    const float gl = L::FERRO ? P.gsl2e : 0.f, k2 = 2.0f * FETODE_LOG2E;
     for (int p = tid; p < L::EP; p += nt) {
       const int e = 2 * p;
       fpa[p] = make_float4(fl.Ec[e], fl.Ec[e + 1], k2 * fl.k[e], k2 * fl.k[e + 1]);
       fpb[p] = make_float4((fl.coef[e] * fl.Ps[e]) * fl.k[e], (fl.coef[e + 1] * fl.Ps[e + 1]) * fl.k[e + 1],
-                           -gs * fl.Ec[e], -gs * fl.Ec[e + 1]);
+                           gl * fl.Ec[e], gl * fl.Ec[e + 1]);
     }
     const float4* src = reinterpret_cast<const float4*>(plan + P.sp);
     for (int q = tid; q < L::OUT * L::IN * (L::NI + 1); q += nt) sp[q] = src[q];
@@ -189,7 +189,7 @@ struct BTab {  // per-block LDS copy of one layer's edge tables
 
 template <int W, int NS, int NB>
 struct BFeat {  // per-wave LDS features of both layers' inputs, combined index t
-  float4 g4[W];  // Ferro per-input terms: x, gate up, wc (1 - up), -gs wc (1 - up)
+  float4 g4[W];  // Ferro per-input terms: x, gate up, wo = wc (1 - up), -ln2 wo
   float x[W], pv[W], silu[W], dsilu[W], u[W], rhm[W];  // rhm: 1 / (knot step) of x's interval
   int m[W];
   float bd[W * NS];
@@ -353,7 +353,7 @@ __device__ __forceinline__ void feat_input(BFeat<W, NG - 1 - kSO, NB>& F, const 
   }
   const float up = sigm_l2(-gsl2e * (x - F.pv[t]));
   const float wo = wc * (1.0f - up);
-  F.g4[t] = make_float4(x, up, wo, -gs * wo);
+  F.g4[t] = make_float4(x, up, wo, -0.69314718f * wo);
 }
 
 // the VJP jobs of one layer (inputs at combined offset TB) for one evaluation of each of the
@@ -368,7 +368,8 @@ __device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict
     // element pairs (k, k+1) of one (i, o) on packed-fp32 ops; with wo = wc (1 - up), c' = c (1 - c):
     //   c = sigmoid(gs(-x - Ec)), m = 1 + wo c, sh = x + Ec m, th = tanh(k sh), q = g (1 - th^2)
     //   A += g th, C += q sh, E += q (m + Ec dm/dEc) with Ec dm/dEc = (-gs Ec) wo c'
-    //   d out/d x = q coef Ps k (1 + Ec dm/dx) with dm/dx = -gs wo (up c + c')
+    //   d out/d x = q coef Ps k (1 + Ec dm/dx) with dm/dx = -gs wo (up c + c');
+    //   (-gs Ec) wo is formed once per pair as (gs log2e Ec)(-ln2 wo)
 #pragma unroll
     for (int tt = 0; tt < TPW; ++tt)  // trajectories in turn, each one's rounds interleaved
 #pragma unroll
@@ -383,21 +384,22 @@ __device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict
         const float4 g = F.g4[TB + i];
         const float go = gout[o];
         const float4 fa = Tb.fpa[p + z], fb = Tb.fpb[p + z];
-        const f2 Ec = f2{fa.x, fa.y}, k2 = f2{fa.z, fa.w}, cPk = f2{fb.x, fb.y}, Egs = f2{fb.z, fb.w};
+        const f2 Ec = f2{fa.x, fa.y}, k2 = f2{fa.z, fa.w}, cPk = f2{fb.x, fb.y}, Eg2 = f2{fb.z, fb.w};
         const f2 x = splat(g.x), wo = splat(g.z), gv = splat(go);
-        const f2 cn = rcpx2(ex2x2((x + Ec) * splat(gsl2e)) + splat(1.0f));  // sigmoid(gs(-x - Ec))
+        const f2 cn = rcpx2(ex2x2(pfma(x, splat(gsl2e), Eg2)) + splat(1.0f));  // sigmoid(gs(-x - Ec))
         const f2 mm = pfma(wo, cn, splat(1.0f));                           // branch_mom, branch_sign = 1
         const f2 sh = pfma(Ec, mm, x);                                     // shifted_x
         const f2 th = pfma(splat(-2.0f), rcpx2(ex2x2(k2 * sh) + splat(1.0f)), splat(1.0f));  // tanh(k sh)
         const f2 q = gv * pfma(-th, th, splat(1.0f));
         const f2 dcn = pfma(-cn, cn, cn);
+        const f2 ew = Eg2 * splat(g.w);  // (-gs Ec) wo
         if constexpr (ACC) {
           R.A[r] = pfma(gv, th, R.A[r]);
           R.C[r] = pfma(q, sh, R.C[r]);
-          R.Ev[r] = pfma(q, pfma(Egs, wo * dcn, mm), R.Ev[r]);
+          R.Ev[r] = pfma(q, pfma(ew, dcn, mm), R.Ev[r]);
         }
-        const f2 dm = splat(g.w) * pfma(splat(g.y), cn, dcn);
-        *reinterpret_cast<f2*>(&cb[i * L::NTMP + ok_]) = (q * cPk) * pfma(Ec, dm, splat(1.0f));
+        // Ec dm/dx = ew (up c + c')
+        *reinterpret_cast<f2*>(&cb[i * L::NTMP + ok_]) = (q * cPk) * pfma(ew, pfma(splat(g.y), cn, dcn), splat(1.0f));
       }
     }
     if constexpr (ACC)
@@ -991,16 +993,32 @@ __global__ void part_reduce_kernel(const float* __restrict__ part, int64_t nrows
   if (slot >= nacc) return;
   const int64_t r0 = (int64_t)blockIdx.y * per, r1 = r0 + per < nrows ? r0 + per : nrows;
   double s = 0.0;
+#pragma unroll 8
   for (int64_t r = r0; r < r1; ++r) s += part[r * nacc + slot];
   out[(int64_t)blockIdx.y * nacc + slot] = s;
 }
 
-__global__ void chunk_sum_kernel(const double* __restrict__ ch, int nch, int nacc, double* __restrict__ S) {
-  const int slot = blockIdx.x * blockDim.x + threadIdx.x;
-  if (slot >= nacc) return;
+// chunk sums -> S: four waves per 64 columns each sum a quarter of the chunks (loads issued
+// together), then the four partials are added in a fixed order
+constexpr int kChunkWaves = 4;
+__global__ __launch_bounds__(64 * kChunkWaves) void chunk_sum_kernel(const double* __restrict__ ch, int nch, int nacc,
+                                                                     double* __restrict__ S) {
+  __shared__ double ps[kChunkWaves][64];
+  const int w = threadIdx.x / 64, lane = threadIdx.x % 64, slot = blockIdx.x * 64 + lane;
+  const int per = (nch + kChunkWaves - 1) / kChunkWaves, c0 = w * per, c1 = c0 + per < nch ? c0 + per : nch;
   double s = 0.0;
-  for (int c = 0; c < nch; ++c) s += ch[(int64_t)c * nacc + slot];
-  S[slot] = s;
+  if (slot < nacc) {
+#pragma unroll 8
+    for (int c = c0; c < c1; ++c) s += ch[(int64_t)c * nacc + slot];
+  }
+  ps[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && slot < nacc) {
+    double t = ps[0][lane];
+#pragma unroll
+    for (int k = 1; k < kChunkWaves; ++k) t += ps[k][lane];
+    S[slot] = t;
+  }
 }
 
 struct ApplyLayer {
@@ -1016,11 +1034,38 @@ __device__ __forceinline__ void put(float* p, int64_t i, double v) {
   if (p) p[i] = (float)v;
 }
 
-// gradient sums of one layer -> parameter gradients (reference parameter layouts)
-__global__ void grad_apply_kernel(const double* __restrict__ S, ApplyLayer L) {
+// work items of one layer in grad_apply_kernel: elements / edges / logistic weights / logistic
+// (a, b) pairs, padded to whole waves, then one wave per output for the logistic scalers
+__host__ __device__ inline int apply_items(const ApplyLayer& L) {
   const AccLayout& A = L.AL;
-  const int in = L.kl.in_features, out = L.kl.out_features, NS = A.NS;
-  int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int out = L.kl.out_features;
+  const int n = (A.E + A.NE + out * A.NL + A.NL + 63) / 64 * 64;
+  return n + (A.NL && L.kl.logistic_scaler ? 64 * out : 0);
+}
+
+// gradient sums of both layers -> parameter gradients (reference parameter layouts); 64-thread
+// blocks never straddle a layer (apply_items pads), so the layer choice is wave-uniform
+__global__ __launch_bounds__(64) void grad_apply_kernel(const double* __restrict__ S_, ApplyLayer L0_, ApplyLayer L1_,
+                                                        int n0) {
+  int t = blockIdx.x * 64 + threadIdx.x;
+  const bool second = t >= n0;
+  const ApplyLayer& L = second ? L1_ : L0_;
+  const double* S = S_ + (second ? L0_.AL.n : 0);
+  if (second) t -= n0;
+  const AccLayout& A = L.AL;
+  const int out = L.kl.out_features, NS = A.NS;
+  const int nitems = (A.E + A.NE + out * A.NL + A.NL + 63) / 64 * 64;
+  if (t >= nitems) {  // logistic scaler of output o: one wave, lanes over the NL weights, fixed-order tree
+    const int o = (t - nitems) / 64, lane = (t - nitems) % 64;
+    const double sl = L.kl.scale_logistic;
+    double g = 0.0;
+    for (int q = lane; q < A.NL; q += 64)
+      g += 2.0 * S[A.oLw + o * A.NL + q] * (double)L.kl.logistic_weight[(int64_t)o * A.NL + q] * sl;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) g += __shfl_xor(g, m);
+    if (lane == 0) put(L.kg.logistic_scaler, o, g);
+    return;
+  }
   if (t < A.E) {  // Ferro element e = (i, o, k)
     const int K = L.fl.num_basis, o = (t / K) % out;
     const double co = L.fl.coef[t], Ps = L.fl.Ps[t], kk = L.fl.k[t], bi = L.fl.bias[t];
@@ -1047,27 +1092,17 @@ __global__ void grad_apply_kernel(const double* __restrict__ S, ApplyLayer L) {
   }
   t -= A.NE;
   if (A.NL == 0) return;
-  const double sl = L.kl.scale_logistic;
   if (t < out * A.NL) {  // logistic weight (o, i*NB + j); the basis is 2 sigmoid
     const int o = t / A.NL;
     const double ls = L.kl.logistic_scaler ? (double)L.kl.logistic_scaler[o] : 1.0;
-    put(L.kg.logistic_weight, t, 2.0 * S[A.oLw + t] * sl * ls);
+    put(L.kg.logistic_weight, t, 2.0 * S[A.oLw + t] * L.kl.scale_logistic * ls);
     return;
   }
   t -= out * A.NL;
   if (t < A.NL) {
     put(L.kg.logistic_a, t, S[A.oLa + t]);
     put(L.kg.logistic_b, t, S[A.oLb + t]);
-    return;
   }
-  t -= A.NL;
-  if (t < out && L.kl.logistic_scaler) {
-    double g = 0.0;
-    for (int q = 0; q < A.NL; ++q)
-      g += 2.0 * S[A.oLw + t * A.NL + q] * (double)L.kl.logistic_weight[(int64_t)t * A.NL + q] * sl;
-    put(L.kg.logistic_scaler, t, g);
-  }
-  (void)in;
 }
 
 typedef void (*bwd_fn)(BwdArgs);
@@ -1252,22 +1287,22 @@ int fetode_integrate_fixed_backward(const fetode_field_t* f, const void* plan, i
   hipLaunchKernelGGL(part_reduce_kernel, dim3(nblk(nacc, 64), (unsigned)nch), dim3(64), 0, s, part, nrow, nacc, per,
                      chunks);
   LAUNCH_CHECK();
-  hipLaunchKernelGGL(chunk_sum_kernel, dim3(nblk(nacc, 64)), dim3(64), 0, s, chunks, (int)nch, nacc, S);
+  hipLaunchKernelGGL(chunk_sum_kernel, dim3(nblk(nacc, 64)), dim3(64 * kChunkWaves), 0, s, chunks, (int)nch, nacc, S);
   LAUNCH_CHECK();
   if (!kan_grads && !ferro_grads) return FETODE_OK;
+  ApplyLayer L[2];
   for (int l = 0; l < 2; ++l) {
-    ApplyLayer L;
-    memset(&L, 0, sizeof(L));
-    L.kl = f->kan[l];
-    if (f->ferro) L.fl = f->ferro[l];
-    L.has_ferro = f->ferro != nullptr;
-    L.AL = l == 0 ? AL0 : AL1;
-    if (kan_grads) L.kg = kan_grads[l];
-    if (ferro_grads && f->ferro) L.fg = ferro_grads[l];
-    const int n = L.AL.E + L.AL.NE + L.kl.out_features * L.AL.NL + L.AL.NL + L.kl.out_features;
-    hipLaunchKernelGGL(grad_apply_kernel, dim3(nblk(n, 64)), dim3(64), 0, s, S + (l == 0 ? 0 : AL0.n), L);
-    LAUNCH_CHECK();
+    memset(&L[l], 0, sizeof(ApplyLayer));
+    L[l].kl = f->kan[l];
+    if (f->ferro) L[l].fl = f->ferro[l];
+    L[l].has_ferro = f->ferro != nullptr;
+    L[l].AL = l == 0 ? AL0 : AL1;
+    if (kan_grads) L[l].kg = kan_grads[l];
+    if (ferro_grads && f->ferro) L[l].fg = ferro_grads[l];
   }
+  const int n0 = apply_items(L[0]), n1 = apply_items(L[1]);
+  hipLaunchKernelGGL(grad_apply_kernel, dim3((unsigned)((n0 + n1) / 64)), dim3(64), 0, s, S, L[0], L[1], n0);
+  LAUNCH_CHECK();
   return FETODE_OK;
 }
 
