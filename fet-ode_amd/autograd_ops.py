@@ -42,13 +42,15 @@ _PLAN_CACHE = os.environ.get("FETODE_NO_PLAN_CACHE", "0") != "1"
 
 def build_plan(owner, handle: _lib.FieldHandle, device) -> torch.Tensor:
     """The pre-transformed parameters of the field (fetode_plan_build).  Rebuilt whenever the
-    descriptor is: make_handle keeps a descriptor only while every parameter tensor is the same
-    storage at the same version counter, i.e. until anything writes a parameter through autograd-
-    visible ops (optimizer steps, load_state_dict, in-place updates).  Writes through `.data`
+    parameter values may have changed (handle.vkey: version counters + optimizer-step generation),
+    i.e. after optimizer steps (fused ones included), load_state_dict and in-place updates.  Writes through `.data`
     bypass version counters; call `owner._fetode_handle = None` after those (or set
     FETODE_NO_PLAN_CACHE=1 to rebuild on every solve)."""
     plan = getattr(owner, "_fetode_plan", None)
-    if _PLAN_CACHE and plan is not None and getattr(owner, "_fetode_plan_for", None) is handle:
+    pfor = getattr(owner, "_fetode_plan_for", None)
+    vkey = getattr(handle, "vkey", None)
+    if _PLAN_CACHE and plan is not None and vkey is not None and pfor is not None and pfor[0] is handle \
+            and pfor[1] == vkey:
         return plan
     lib = _lib.load()
     nbytes = lib.fetode_plan_bytes(handle.ref)
@@ -61,7 +63,7 @@ def build_plan(owner, handle: _lib.FieldHandle, device) -> torch.Tensor:
         owner._fetode_plan = plan
     _lib.check(lib.fetode_plan_build(handle.ref, plan.data_ptr(), _lib.stream_handle(device)),
                "fetode_plan_build")
-    owner._fetode_plan_for = handle
+    owner._fetode_plan_for = (handle, vkey)
     return plan
 
 
@@ -244,24 +246,31 @@ def _field_tensors(model):
 
 
 def _handle_key(model, B, device):
-    """Identity (storage, version counter, leading size) of every tensor the descriptor points
-    at plus the optimizer-step generation (_lib.param_generation), or None when a tensor would be converted (non-fp32 / non-contiguous) — the converted copy
-    could go stale silently."""
-    key = [B, device, _lib.param_generation()]
+    """(descriptor key, value key) of the field, or None when a tensor would be converted
+    (non-fp32 / non-contiguous: the converted copy could go stale silently).  The descriptor holds
+    only pointers and shapes, so it is reused while every tensor keeps its storage; the plan holds
+    the parameter VALUES and is rebuilt when a version counter or the optimizer-step generation
+    (_lib.param_generation: fused optimizers do not bump version counters) changes."""
+    key = [B, device]
+    vkey = [_lib.param_generation()]
     for t in _field_tensors(model):
         if t.dtype != torch.float32 or not t.is_contiguous():
             return None
-        key += [t.data_ptr(), t._version, t.shape[0]]
-    return tuple(key)
+        key += [t.data_ptr(), t.shape[0]]
+        vkey.append(t._version)
+    return tuple(key), tuple(vkey)
 
 
 def make_handle(model, B: int, device) -> _lib.FieldHandle:
     """Descriptor of the field (+ explicit branch_sign tensors; None = ones), cached on the model
-    while no parameter has been replaced or modified in place (tensor version counters)."""
-    key = _handle_key(model, B, device)
+    while every tensor keeps its storage; handle.vkey identifies the parameter values it was
+    asked for (build_plan rebuilds the plan when it changes)."""
+    keys = _handle_key(model, B, device)
     cached = model.__dict__.get("_fetode_handle")
-    if key is not None and cached is not None and cached[0] == key:
-        return cached[1]
+    if keys is not None and cached is not None and cached[0] == keys[0]:
+        h = cached[1]
+        h.vkey = keys[1]
+        return h
     keep = []
     layers = field_layers(model)
     kan = [k.desc(keep) for k, _ in layers]
@@ -274,7 +283,8 @@ def make_handle(model, B: int, device) -> _lib.FieldHandle:
                 b = None
             ferro.append(f.desc(keep, b))
     h = _lib.FieldHandle(kan, ferro, keep)
-    model._fetode_handle = (key, h)
+    h.vkey = None if keys is None else keys[1]   # None: never reuse a plan built for it
+    model._fetode_handle = (None if keys is None else keys[0], h)
     return h
 
 

@@ -80,7 +80,10 @@ def allreduce_gradients(params: Iterable[torch.nn.Parameter], average: bool = Tr
     grads: List[torch.Tensor] = [p.grad for p in params if p.grad is not None]
     if w == 1 or not grads:
         return
-    flat = torch._utils._flatten_dense_tensors(grads)
+    flat = _shared_flat(grads)
+    views = flat is not None   # the gradients already are views of one buffer (fused backward)
+    if not views:
+        flat = torch._utils._flatten_dense_tensors(grads)
     if weights is not None:
         flat.mul_(weights)
     # RCCL ("nccl") reduces device buffers in place; gloo (CPU tests, several ranks on one GPU)
@@ -92,8 +95,22 @@ def allreduce_gradients(params: Iterable[torch.nn.Parameter], average: bool = Tr
         flat.copy_(buf)
     if weights is None and average:
         flat.div_(w)
-    for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
-        g.copy_(f)
+    if not views:
+        for g, f in zip(grads, torch._utils._unflatten_dense_tensors(flat, grads)):
+            g.copy_(f)
+
+
+def _shared_flat(grads: List[torch.Tensor]) -> Optional[torch.Tensor]:
+    """The one contiguous buffer the gradients tile exactly, in order, or None."""
+    base = grads[0]._base
+    if base is None or not base.is_contiguous() or base.dim() != 1:
+        return None
+    off = 0
+    for g in grads:
+        if g._base is not base or not g.is_contiguous() or g.storage_offset() - base.storage_offset() != off:
+            return None
+        off += g.numel()
+    return base if off == base.numel() else None
 
 
 def odeint_sharded(func, y0_local: torch.Tensor, t: torch.Tensor, *, rtol=1e-7, atol=1e-9, method=None,

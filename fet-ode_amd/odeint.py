@@ -212,16 +212,18 @@ class _FusedFixedFn(torch.autograd.Function):
         gy0 = torch.empty(B, g.shape[-1], device=dev, dtype=torch.float32) if ctx.needs_input_grad[3] else None
         want = ctx.needs_input_grad[6:]
         params = list(field.parameters())
-        wanted = {id(p) for p, w in zip(params, want) if w}
-        grads = {}
+        # every wanted gradient is a view of ONE flat buffer, in parameter order: autograd hands
+        # the views over as .grad, and dist.allreduce_gradients then reduces the buffer in place
+        # (no flatten / unflatten copies per iteration)
+        wp = [p for p, w in zip(params, want) if w]
+        flat = torch.empty(sum(p.numel() for p in wp), device=dev, dtype=torch.float32)
+        grads, off = {}, 0
+        for p in wp:
+            grads[id(p)] = flat[off:off + p.numel()].view(p.shape)
+            off += p.numel()
 
         def gbuf(p):
-            if p is None or id(p) not in wanted:
-                return None
-            t = grads.get(id(p))
-            if t is None:
-                t = grads[id(p)] = torch.empty_like(p, dtype=torch.float32)
-            return t
+            return None if p is None else grads.get(id(p))
 
         kg = (_lib.KANLinearGrad * len(layers))()
         fg = (_lib.FerroGrad * len(layers))() if layers[0][1] is not None else None

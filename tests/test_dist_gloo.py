@@ -139,3 +139,35 @@ def test_sharded_dopri5_gradient_through_step_control_fp64(sizes):
     assert torch.allclose(torch.cat([s0, s1], dim=1), sol, rtol=1e-12, atol=1e-14)
     assert torch.equal(g0, g1)
     assert ((g0 - ref).norm() / ref.norm()).item() <= 1e-10, ((g0 - ref).norm() / ref.norm()).item()
+
+
+def _views_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import fet_ode_amd.dist as D
+    # gradients that are views of one flat buffer (what the fused backward hands autograd):
+    # reduced in place, no copies; a mixed set falls back to the flatten path
+    ps = [torch.nn.Parameter(torch.zeros(3, 2)), torch.nn.Parameter(torch.zeros(4))]
+    flat = torch.arange(10, dtype=torch.float32) * (rank + 1)
+    ps[0].grad, ps[1].grad = flat[:6].view(3, 2), flat[6:]
+    assert D._shared_flat([p.grad for p in ps]) is flat
+    D.allreduce_gradients(ps)
+    q.put((rank, flat.clone(), ps[0].grad._base is flat))
+    dist.destroy_process_group()
+
+
+def test_allreduce_in_place_on_shared_gradient_buffer():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_views_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in procs], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    exp = torch.arange(10, dtype=torch.float32) * 1.5   # mean of rank 0 (x1) and rank 1 (x2)
+    for _, flat, still_view in res:
+        assert still_view and torch.equal(flat, exp)
