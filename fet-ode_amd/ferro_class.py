@@ -129,7 +129,8 @@ class FerroelectricBasis(nn.Module):
         return out
 
     def reset_state(self):
-        """ferro_class.py:422-424."""
+        """ferro_class.py:422-424: prev_x.zero_() AND branch_sign.fill_(1.0) — so a branch_sign
+        loaded from a state_dict is reset to ones here too (None is the all-ones encoding)."""
         self._prev.zero_()
         self._bsign = None
 
