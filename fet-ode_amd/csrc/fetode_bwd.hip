@@ -95,6 +95,7 @@ struct BL {  // compile-time shape of one layer
   static constexpr int LPI = pow2_floor(64 / IN);  // lanes per input in the d/dx segmented sum
   // cb row pitch: NTM rounded up to LPI mod 32, so the LPI-lane groups of one half-wave read
   // distinct LDS banks in reduce_gin (a pitch of 32 put all ten inputs of layer 1 on banks 0-3)
+  // (extra padding of 4 / 12 / 16 floats measured within 1 %: the pitch is not a lever)
   static constexpr int NTMP = LPI >= 32 ? NTM : NTM + ((LPI - NTM % 32) % 32 + 32) % 32;
   static_assert(IN <= 64 && OUT <= 64, "layer widths up to 64");
   static_assert(NS >= 1, "grid too small for cubic splines");
@@ -106,10 +107,14 @@ struct BL {  // compile-time shape of one layer
 template <int W, int NG, int NB>
 struct BInTab {
   static constexpr int NI = NG - 1;
-  float4 bp[W * NI * 4];  // basis B_{m-3+r} on interval m as a cubic in u: [t][m][r] (power basis)
+  // basis B_{m-3+r} on interval m as a cubic in u: [t][m][r] (power basis); one float4 of
+  // padding per input so that lanes gathering different inputs' rows spread over the LDS banks
+  static constexpr int BPS = NI * 4 + 1;
+  float4 bp[W * BPS];
+  __device__ static int bpi(int t, int m) { return t * BPS + m * 4; }
   float knots[W * NG];
   float rh[W * NI];       // 1/(g[m+1] - g[m])
-  float lg[NB > 0 ? 2 * W * NB : 1];  // (-a log2e, a b log2e) per (t, j)
+  __attribute__((aligned(8))) float lg[NB > 0 ? 2 * W * NB : 1];  // (-a log2e, a b log2e) per (t, j)
 
   __device__ void stage(const float* __restrict__ plan, const LayerPlan& P0, const LayerPlan& P1, int D, int tid,
                         int nt) {
@@ -151,7 +156,7 @@ struct BInTab {
       }
       for (int r = 0; r <= kSO; ++r) {
         const double a0 = v[0][r], a1 = v[1][r], a2 = v[2][r], a3 = v[3][r];
-        bp[q * 4 + r] = make_float4((float)a0, (float)((-11.0 * a0 + 18.0 * a1 - 9.0 * a2 + 2.0 * a3) / 2.0),
+        bp[bpi(t, m) + r] = make_float4((float)a0, (float)((-11.0 * a0 + 18.0 * a1 - 9.0 * a2 + 2.0 * a3) / 2.0),
                                     (float)(9.0 * (2.0 * a0 - 5.0 * a1 + 4.0 * a2 - a3) / 2.0),
                                     (float)(9.0 * (-a0 + 3.0 * a1 - 3.0 * a2 + a3) / 2.0));
       }
@@ -161,7 +166,10 @@ struct BInTab {
 
 template <class L>
 struct BTab {  // per-block LDS copy of one layer's edge tables
-  float4 sp[L::OUT * L::IN * (L::NI + 1)];  // spline edge (o, i) as a cubic in u per interval
+  // spline edge (o, i) as a cubic in u per interval (NI + 1 rows: the last is the zero row), rows
+  // of one edge padded to SPS float4s (lanes gather different edges: spread over the banks)
+  static constexpr int SPS = L::NI + 2;
+  float4 sp[L::OUT * L::IN * SPS];
   float kw[L::OUT * L::IN * L::NFL];        // SiLU weight, 2 * scaled logistic weights
   float pa[L::NL > 0 ? L::NL : 1], pb[L::NL > 0 ? L::NL : 1];
   // Ferro element pair p = elements (2p, 2p + 1) = (i, o, k..k+1):
@@ -178,7 +186,7 @@ struct BTab {  // per-block LDS copy of one layer's edge tables
                            gl * fl.Ec[e], gl * fl.Ec[e + 1]);
     }
     const float4* src = reinterpret_cast<const float4*>(plan + P.sp);
-    for (int q = tid; q < L::OUT * L::IN * (L::NI + 1); q += nt) sp[q] = src[q];
+    for (int q = tid; q < L::OUT * L::IN * (L::NI + 1); q += nt) sp[q / (L::NI + 1) * SPS + q % (L::NI + 1)] = src[q];
     for (int q = tid; q < L::OUT * L::IN * L::NFL; q += nt) kw[q] = plan[P.kw + q];
     for (int q = tid; q < L::NL; q += nt) {
       pa[q] = kl.logistic_a[q];
@@ -337,7 +345,7 @@ __device__ __forceinline__ void feat_input(BFeat<W, NG - 1 - kSO, NB>& F, const 
   const float fill = fin ? 0.f : __builtin_nanf("");
   // the interval's four basis cubics, all reads issued before any use; the dense row is formed
   // in registers and written once
-  const float4* bp = &Tb.bp[(t * NI + mc) * 4 + z];
+  const float4* bp = &Tb.bp[Tb.bpi(t, mc) + z];
   float4 p[kSO + 1];
 #pragma unroll
   for (int r = 0; r <= kSO; ++r) p[r] = bp[r];
@@ -425,7 +433,7 @@ __device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict
       const float u = F.u[TB + i];
       float dsdx;
       if (m < L::NI) {
-        const float4 cf = Tb.sp[q * (L::NI + 1) + m + z];  // (o, i, interval), q = o*IN + i
+        const float4 cf = Tb.sp[q * BTab<L>::SPS + m + z];  // (o, i, interval), q = o*IN + i
         dsdx = ffma(u, ffma(3.0f * u, cf.w, 2.0f * cf.z), cf.y) * F.rhm[TB + i];
       } else {
         dsdx = u * 0.0f;  // 0 outside the grid, NaN for non-finite inputs (the reference's NaN bases)
@@ -720,8 +728,9 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
               for (int k = 0; k < RSG; ++k) {  // every round's operands read before any sigmoid
                 const int q = lane + 64 * k, qc = q < NSG ? q : 0;
                 const int qt = qc / (W * NB), qq = qc % (W * NB);
-                sa[k] = TI.lg[2 * qq + z];
-                sb[k] = TI.lg[2 * qq + 1 + z];
+                const float2 ab = *reinterpret_cast<const float2*>(&TI.lg[2 * qq + z]);  // one 8-byte read
+                sa[k] = ab.x;
+                sb[k] = ab.y;
                 sx[k] = Fp[qt].x[qq / NB];
               }
 #pragma unroll
@@ -895,7 +904,7 @@ __global__ __launch_bounds__(256) void param_sum_kernel(BwdArgs a) {
 #pragma unroll
         for (int r = 0; r <= kSO; ++r) {
           const int c = mc - kSO + r;
-          const float4 p = TI.bp[(t * NI + mc) * 4 + r];
+          const float4 p = TI.bp[TI.bpi(t, mc) + r];
           const float v = ffma(ffma(ffma(p.w, u, p.z), u, p.y), u, p.x);
 #pragma unroll
           for (int cc = 0; cc < NS; ++cc) bd[cc] = cc == c ? v : bd[cc];
