@@ -17,6 +17,26 @@ using namespace fetode;
 namespace {
 
 constexpr int kKThreads = 256;
+
+#ifndef FETODE_KURA_FAST
+#define FETODE_KURA_FAST 1
+#endif
+// sin and cos of one phase.  Fast form: a two-constant Cody-Waite reduction of theta to
+// r in [-pi, pi] (k = rint(theta / 2 pi); 2 pi = hi + lo), then v_sin_f32 / v_cos_f32 of r / 2 pi
+// revolutions — 4 VALU + 2 transcendentals instead of OCML's two full sinf / cosf (the phases
+// stay within a few periods; the hardware functions' error is ~1e-7 absolute there).
+__device__ __forceinline__ void phase_sincos(float t, float& sn, float& cs) {
+  if constexpr (FETODE_KURA_FAST) {
+    constexpr float inv2pi = 0.159154943091895336f, hi = 6.28318548202514648f, lo = -1.74845553146951715e-07f;
+    const float k = __builtin_rintf(t * inv2pi);
+    const float r = __builtin_fmaf(-k, lo, __builtin_fmaf(-k, hi, t));
+    const float rv = r * inv2pi;
+    sn = __builtin_amdgcn_sinf(rv);
+    cs = __builtin_amdgcn_cosf(rv);
+  } else {
+    sincosf(t, &sn, &cs);
+  }
+}
 constexpr int kMaxPix = 3072;  // H * W: the backward keeps 4 * H * W floats in LDS (< 64 KB)
 
 // 4-neighbour sum in the cross kernel's tap order: up (0,1), left (1,0), right (1,2), down (2,1)
@@ -47,8 +67,7 @@ __global__ __launch_bounds__(kKThreads) void kuramoto_fwd_kernel(const float* __
     for (int p = threadIdx.x; p < HW; p += kKThreads) {
       const float t = th[p];
       if (tape) tape[(b * (steps + 1) + s) * HW + p] = t;
-      sn[p] = sinf(t);
-      cs[p] = cosf(t);
+      phase_sincos(t, sn[p], cs[p]);
     }
     __syncthreads();
     for (int p = threadIdx.x; p < HW; p += kKThreads) {
@@ -62,8 +81,10 @@ __global__ __launch_bounds__(kKThreads) void kuramoto_fwd_kernel(const float* __
   for (int p = threadIdx.x; p < HW; p += kKThreads) {
     const float t = th[p];
     if (tape) tape[(b * (steps + 1) + steps) * HW + p] = t;
-    feat[b * 2 * HW + p] = cosf(t);
-    feat[b * 2 * HW + HW + p] = sinf(t);
+    float sv, cv;
+    phase_sincos(t, sv, cv);
+    feat[b * 2 * HW + p] = cv;
+    feat[b * 2 * HW + HW + p] = sv;
   }
 }
 
@@ -91,15 +112,16 @@ __global__ __launch_bounds__(kKThreads) void kuramoto_bwd_kernel(int H, int W, i
   for (int p = threadIdx.x; p < HW; p += kKThreads) {
     const float t = tb[steps * HW + p];
     // feat = [cos, sin]: d theta_T = -sin g_cos + cos g_sin
-    g[p] = (-sinf(t)) * gfeat[b * 2 * HW + p] + cosf(t) * gfeat[b * 2 * HW + HW + p];
+    float sv, cv;
+    phase_sincos(t, sv, cv);
+    g[p] = (-sv) * gfeat[b * 2 * HW + p] + cv * gfeat[b * 2 * HW + HW + p];
     go[p] = 0.f;
   }
   for (int s = steps - 1; s >= 0; --s) {
     __syncthreads();
     for (int p = threadIdx.x; p < HW; p += kKThreads) {
       const float t = tb[s * HW + p];
-      sn[p] = sinf(t);
-      cs[p] = cosf(t);
+      phase_sincos(t, sn[p], cs[p]);
     }
     __syncthreads();
     float gnew[kMaxPix / kKThreads];
@@ -191,14 +213,33 @@ __global__ void column_sum_final_kernel(const double* __restrict__ mid, int n, f
 // profiles/r02_mnist_pmc.txt); the feature error stays ~1e-7 relative, far inside the 1e-5 test
 // bar on the 1568 x 17-term sums.
 // =============================================================================================
-constexpr int kWideCh = 16;            // inputs per staged chunk (LDS ~26 KB: 6 workgroups per CU)
-constexpr int kWideNS = 8, kWideNB = 8, kWideNG = 12;
+#ifndef FETODE_WIDE_SKIP  // diagnostics only (timing attribution; results wrong when set)
+#define FETODE_WIDE_SKIP 0
+#endif
+#ifndef FETODE_WIDE_CH
+#define FETODE_WIDE_CH 8
+#endif
+constexpr int kWideCh = FETODE_WIDE_CH;  // inputs per staged chunk
+constexpr int kWideNS = 8, kWideNB = 8, kWideNG = 12, kWideNI = kWideNG - 1;
 constexpr int kWideF = 1 + kWideNS + kWideNB;
-constexpr int kWideRows = 64;          // rows per workgroup (4 waves x 16)
+#ifndef FETODE_WIDE_WGS
+#define FETODE_WIDE_WGS 2048
+#endif
+#ifndef FETODE_WIDE_ROWS
+#define FETODE_WIDE_ROWS 64
+#endif
+constexpr int kWideRows = FETODE_WIDE_ROWS;  // rows per workgroup (16 per wave): the staged chunk serves them all
+constexpr int kWideThreads = kWideRows * 4;
+constexpr int kWideTab = kWideNI * 5;  // float4s per input of the basis table
+constexpr int kWinStride = 20;         // per-lane dense-basis window (floats; b128 reads conflict-free)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-// Wp[i][f][o16]: f = 0 base, 1 + c scaled spline, 1 + NS + j scaled logistic
+// Pack = [in][F][16] weights (f = 0 base, 1 + c scaled spline, 1 + NS + j 2 x scaled logistic:
+// the basis is 2 sigmoid) followed by the per-input basis table [in][interval m][5] float4s: the
+// four non-zero cubic B-splines B_{m-3+r} of interval m as power-basis cubics in u = (x - g_m) / h_m
+// (fit in fp64 from the Cox-de Boor recursion restricted to the interval, efficientkan.py:117-131),
+// then (g_m, 1 / h_m, 0, 0).
 __global__ void wide_pack_kernel(fetode_kanlinear_t kl, float* __restrict__ wp) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int in = kl.in_features, outf = kl.out_features;
@@ -213,20 +254,58 @@ __global__ void wide_pack_kernel(fetode_kanlinear_t kl, float* __restrict__ wp) 
       v = kl.spline_weight[((int64_t)o * in + i) * kWideNS + (f - 1)] * sc;
     } else if (kl.num_logistic) {
       const float lsc = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
-      v = (kl.logistic_weight[(int64_t)o * in * kWideNB + i * kWideNB + (f - 1 - kWideNS)] * kl.scale_logistic) * lsc;
+      v = 2.0f * ((kl.logistic_weight[(int64_t)o * in * kWideNB + i * kWideNB + (f - 1 - kWideNS)] * kl.scale_logistic) * lsc);
     }
   }
   wp[t] = v;
 }
 
-__global__ __launch_bounds__(256) void wide_fwd_kernel(fetode_kanlinear_t kl, const float* __restrict__ wp,
+__global__ void wide_table_kernel(fetode_kanlinear_t kl, float4* __restrict__ tab) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= kl.in_features * kWideNI) return;
+  const int i = t / kWideNI, m = t % kWideNI;
+  const float* g = kl.grid + (int64_t)i * kWideNG;
+  const double h = (double)g[m + 1] - g[m];
+  double v[4][4];
+  for (int s = 0; s < 4; ++s) {  // the interval's bases at u = s / 3
+    const double x = g[m] + h * (s / 3.0);
+    double N[5] = {0, 0, 0, 1, 0};
+    for (int k = 1; k <= 3; ++k) {
+      double M[5] = {0, 0, 0, 0, 0};
+      for (int r = 3 - k; r <= 3; ++r) {
+        const int j = m - 3 + r;
+        if (j >= 0 && j <= kWideNG - 2 - k)
+          M[r] = (x - g[j]) / ((double)g[j + k] - g[j]) * N[r] +
+                 ((double)g[j + k + 1] - x) / ((double)g[j + k + 1] - g[j + 1]) * N[r + 1];
+      }
+      for (int r = 0; r < 5; ++r) N[r] = M[r];
+    }
+    for (int r = 0; r < 4; ++r) v[s][r] = N[r];
+  }
+  float4* out = tab + (int64_t)t * 5;
+  for (int r = 0; r < 4; ++r) {  // cubic through (0, v0), (1/3, v1), (2/3, v2), (1, v3) in power basis
+    const double a0 = v[0][r], a1 = v[1][r], a2 = v[2][r], a3 = v[3][r];
+    out[r] = make_float4((float)a0, (float)((-11.0 * a0 + 18.0 * a1 - 9.0 * a2 + 2.0 * a3) / 2.0),
+                         (float)(9.0 * (2.0 * a0 - 5.0 * a1 + 4.0 * a2 - a3) / 2.0),
+                         (float)(9.0 * (-a0 + 3.0 * a1 - 3.0 * a2 + a3) / 2.0));
+  }
+  out[4] = make_float4(g[m], 1.0f / (g[m + 1] - g[m]), 0.f, 0.f);
+}
+
+// Per (row, input) the 17 features are formed once and contracted on v_mfma_f32_16x16x4_f32:
+//   SiLU; the knot interval m (12 compares), u, the 4 non-zero bases as Horner cubics from the
+//   table, placed into the dense 8 through the lane's LDS window (4 b32 writes at m + r, two b128
+//   reads, 4 zeroing writes: runtime-indexed placement without select chains); the 8 logistic
+//   sigmoids as 1 / (1 + 2^(-a log2e x + a b log2e)) (the 2 is in the packed weights).
+__global__ __launch_bounds__(kWideThreads) void wide_fwd_kernel(fetode_kanlinear_t kl, const float* __restrict__ wp,
                                                       const float* __restrict__ x, int64_t B, int nch,
                                                       float* __restrict__ part) {
   __shared__ float ws[kWideCh * kWideF * 16];   // packed weights of the chunk
-  __shared__ float xs[kWideRows][kWideCh + 1];  // the 64 rows' inputs of the chunk
-  __shared__ float gk[kWideCh][kWideNG];        // knots
-  __shared__ float rk[kWideCh][3 * (kWideNG - 1)];  // 1 / (g[j+k] - g[j]), k = 1..3 (bspline_local)
-  __shared__ float lab[kWideCh][2 * kWideNB];   // logistic -a log2(e) | b
+  __shared__ float xs[kWideRows][kWideCh + 1];  // the rows' inputs of the chunk
+  __shared__ float4 gk[kWideCh][kWideNG / 4];   // knots
+  __shared__ float4 tb[kWideCh * kWideTab];     // basis tables of the chunk's inputs
+  __shared__ float2 lab[kWideCh][kWideNB];      // logistic (-a log2e, a b log2e)
+  __shared__ __attribute__((aligned(16))) float win[kWideThreads * kWinStride];  // per-lane dense-basis window
   const int in = kl.in_features;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = lane & 15, kq = lane >> 4;
@@ -234,43 +313,125 @@ __global__ __launch_bounds__(256) void wide_fwd_kernel(fetode_kanlinear_t kl, co
   const int S = gridDim.y, s = blockIdx.y;
   const int c0 = s * nch / S, c1 = (s + 1) * nch / S;
   const bool lg = kl.num_logistic != 0;
+  const float4* wtab = reinterpret_cast<const float4*>(wp + (int64_t)in * kWideF * 16);
+  float* mywin = win + tid * kWinStride;  // [0, 16): window slot m + r + 1 holds B_{m-3+r}; dense c at 4 + c
+  for (int q = 0; q < kWinStride; ++q) mywin[q] = 0.f;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  // chunk c's global data is fetched into registers while chunk c - 1 is contracted
+  constexpr int PW = (kWideCh * kWideF * 16 + kWideThreads - 1) / kWideThreads, PX = (kWideRows * kWideCh + kWideThreads - 1) / kWideThreads;
+  constexpr int PT = (kWideCh * kWideTab + kWideThreads - 1) / kWideThreads, PG = (kWideCh * kWideNG + kWideThreads - 1) / kWideThreads;
+  constexpr int PL = (kWideCh * kWideNB + kWideThreads - 1) / kWideThreads;
+  float rw[PW], rx[PX], rg[PG], ra[PL], rb[PL];
+  float4 rt[PT];
+  auto fetch = [&](int c) __attribute__((always_inline)) {
+    const int i0 = c * kWideCh, ni = min(kWideCh, in - i0);
+#pragma unroll
+    for (int k = 0; k < PW; ++k) {
+      const int t = tid + kWideThreads * k;
+      rw[k] = t < ni * kWideF * 16 ? wp[(int64_t)i0 * kWideF * 16 + t] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+      const int t = tid + kWideThreads * k, rr = t / kWideCh, ii = t - rr * kWideCh;
+      rx[k] = (t < kWideRows * kWideCh && row0 + rr < B && ii < ni) ? x[(row0 + rr) * in + i0 + ii] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      const int t = tid + kWideThreads * k;
+      rt[k] = t < ni * kWideTab ? wtab[(int64_t)i0 * kWideTab + t] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < PG; ++k) {
+      const int t = tid + kWideThreads * k;
+      rg[k] = t < ni * kWideNG ? kl.grid[(int64_t)i0 * kWideNG + t] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+      const int t = tid + kWideThreads * k;
+      const bool ok = lg && t < ni * kWideNB;
+      ra[k] = ok ? kl.logistic_a[(int64_t)i0 * kWideNB + t] : 0.f;
+      rb[k] = ok ? kl.logistic_b[(int64_t)i0 * kWideNB + t] : 0.f;
+    }
+  };
+  if (c0 < c1) fetch(c0);
   for (int c = c0; c < c1; ++c) {
     const int i0 = c * kWideCh, ni = min(kWideCh, in - i0);
-    __syncthreads();
-    for (int t = tid; t < ni * kWideF * 16; t += 256) ws[t] = wp[(int64_t)i0 * kWideF * 16 + t];
-    for (int t = tid; t < kWideRows * kWideCh; t += 256) {
-      const int rr = t / kWideCh, ii = t - rr * kWideCh;
-      xs[rr][ii] = (row0 + rr < B && ii < ni) ? x[(row0 + rr) * in + i0 + ii] : 0.f;
+    __syncthreads();  // the previous chunk's contraction is done with the LDS copies
+#pragma unroll
+    for (int k = 0; k < PW; ++k)
+      if (tid + kWideThreads * k < kWideCh * kWideF * 16) ws[tid + kWideThreads * k] = rw[k];
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+      const int t = tid + kWideThreads * k, rr = t / kWideCh, ii = t - rr * kWideCh;
+      if (t < kWideRows * kWideCh) xs[rr][ii] = rx[k];
     }
-    for (int t = tid; t < ni * kWideNG; t += 256) gk[t / kWideNG][t % kWideNG] = kl.grid[(int64_t)i0 * kWideNG + t];
-    for (int t = tid; t < ni * 3 * (kWideNG - 1); t += 256) {
-      const int ii = t / (3 * (kWideNG - 1)), q = t % (3 * (kWideNG - 1)), k = q / (kWideNG - 1) + 1, j = q % (kWideNG - 1);
-      const float* g = kl.grid + (int64_t)(i0 + ii) * kWideNG;
-      rk[ii][q] = j + k < kWideNG ? 1.0f / (g[j + k] - g[j]) : 0.f;
+#pragma unroll
+    for (int k = 0; k < PT; ++k)
+      if (tid + kWideThreads * k < kWideCh * kWideTab) tb[tid + kWideThreads * k] = rt[k];
+#pragma unroll
+    for (int k = 0; k < PG; ++k)
+      if (tid + kWideThreads * k < kWideCh * kWideNG) reinterpret_cast<float*>(&gk[0][0])[tid + kWideThreads * k] = rg[k];
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+      const int t = tid + kWideThreads * k;
+      if (t < kWideCh * kWideNB) lab[t / kWideNB][t % kWideNB] = make_float2(-ra[k] * FETODE_LOG2E, (ra[k] * rb[k]) * FETODE_LOG2E);
     }
-    if (lg)
-      for (int t = tid; t < ni * kWideNB; t += 256) {
-        lab[t / kWideNB][t % kWideNB] = -kl.logistic_a[(int64_t)i0 * kWideNB + t] * FETODE_LOG2E;
-        lab[t / kWideNB][kWideNB + t % kWideNB] = kl.logistic_b[(int64_t)i0 * kWideNB + t];
-      }
     __syncthreads();
+    if (c + 1 < c1) fetch(c + 1);
     for (int g = 0; g < ni / 4; ++g) {
       const int il = 4 * g + kq;
       const float xi = xs[wv * 16 + r][il];
       float feat[kWideF];
+#if FETODE_WIDE_SKIP & 2  // diagnostics: MFMAs only
+#pragma unroll
+      for (int f = 0; f < kWideF; ++f) feat[f] = xi * (float)(f + 1);
+      if (0)
+#endif
+      {
       feat[0] = silu(xi);  // SiLU, efficientkan.py:166 / mnist :131
-      // runtime-indexed basis writes as register select chains (no LDS round trip)
-      bspline_local<3>(xi, kWideNG, &gk[il][0], &rk[il][0], [&](int cc, float v) {
+      int m = -1;
 #pragma unroll
-        for (int k = 0; k < kWideNS; ++k) feat[1 + k] = k == cc ? v : feat[1 + k];
-      });
+      for (int j = 0; j < kWideNG / 4; ++j) {
+        const float4 v = gk[il][j];
+        m += ((xi >= v.x) ? 1 : 0) + ((xi >= v.y) ? 1 : 0) + ((xi >= v.z) ? 1 : 0) + ((xi >= v.w) ? 1 : 0);
+      }
+      const bool fin = __builtin_isfinite(xi), ing = fin && m >= 0 && m < kWideNI;
+      const float4* tm = &tb[il * kWideTab + (ing ? m : 0) * 5];
+      const float4 gr = tm[4];
+      const float u = (xi - gr.x) * gr.y;
+      if (ing) {
 #pragma unroll
-      for (int j = 0; j < kWideNB; ++j)  // 2 sigmoid(a (x - b)), mnist_kuramoto_kan.py:22
-        feat[1 + kWideNS + j] = lg ? 2.0f * sig_from_neg_l2((xi - lab[il][kWideNB + j]) * lab[il][j]) : 0.f;
+        for (int q = 0; q < 4; ++q) {
+          const float4 p = tm[q];
+          mywin[m + q + 1] = ffma(ffma(ffma(p.w, u, p.z), u, p.y), u, p.x);
+        }
+      }
+      asm volatile("" ::: "memory");  // the window writes stay before the vector reads
+      {
+        const float4 d0 = *reinterpret_cast<const float4*>(mywin + 4), d1 = *reinterpret_cast<const float4*>(mywin + 8);
+        const float nf = fin ? 0.f : __builtin_nanf("");  // non-finite x: NaN bases, as (x - g) / d * 0
+        feat[1] = d0.x + nf; feat[2] = d0.y + nf; feat[3] = d0.z + nf; feat[4] = d0.w + nf;
+        feat[5] = d1.x + nf; feat[6] = d1.y + nf; feat[7] = d1.z + nf; feat[8] = d1.w + nf;
+      }
+      asm volatile("" ::: "memory");
+      if (ing) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mywin[m + q + 1] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < kWideNB; ++j) {  // 2 sigmoid(a (x - b)), mnist_kuramoto_kan.py:22 (2 in the weights)
+        const float2 ab = lab[il][j];
+        feat[1 + kWideNS + j] = lg ? rcp(1.0f + ex2(ffma(ab.x, xi, ab.y))) : 0.f;
+      }
+      }
       const float* wrow = ws + (il * kWideF) * 16 + r;   // lane (kq, o = r): Wp[i, f, o]
+#if FETODE_WIDE_SKIP & 1  // diagnostics: features only
+#pragma unroll
+      for (int f = 0; f < kWideF; ++f) acc[f & 3] += feat[f] * wrow[f * 16];
+#else
 #pragma unroll
       for (int f = 0; f < kWideF; ++f) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(feat[f], wrow[f * 16], acc, 0, 0, 0);
+#endif
     }
   }
   // D: lane l holds rows 4 (l >> 4) + v, column l & 15
@@ -302,7 +463,7 @@ int wide_supported(const fetode_kanlinear_t* kl) {
 int wide_splits(const fetode_kanlinear_t* kl, int64_t B) {
   const int nch = (kl->in_features + kWideCh - 1) / kWideCh;
   const int64_t tiles = (B + kWideRows - 1) / kWideRows;
-  int64_t S = (2048 + tiles - 1) / tiles;   // aim at >= 2048 workgroups
+  int64_t S = (FETODE_WIDE_WGS + tiles - 1) / tiles;   // aim at >= FETODE_WIDE_WGS workgroups
   if (S > nch) S = nch;
   return (int)(S < 1 ? 1 : S);
 }
@@ -367,7 +528,7 @@ int fetode_kuramoto_backward(int64_t B, int32_t H, int32_t W, int32_t steps, flo
 int fetode_kanlinear_wide_supported(const fetode_kanlinear_t* kl) { return wide_supported(kl); }
 
 int64_t fetode_kanlinear_wide_pack_bytes(const fetode_kanlinear_t* kl) {
-  return kl ? (int64_t)sizeof(float) * kl->in_features * kWideF * 16 : 0;
+  return kl ? (int64_t)sizeof(float) * kl->in_features * (kWideF * 16 + 4 * kWideTab) : 0;
 }
 
 int fetode_kanlinear_wide_pack(const fetode_kanlinear_t* kl, float* wpack, void* stream) {
@@ -375,6 +536,10 @@ int fetode_kanlinear_wide_pack(const fetode_kanlinear_t* kl, float* wpack, void*
   if (!wpack) return set_err(FETODE_EINVAL, "kanlinear wide: null pack");
   const int64_t n = (int64_t)kl->in_features * kWideF * 16;
   hipLaunchKernelGGL(wide_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *kl, wpack);
+  LAUNCH_CHECK();
+  const int nt = kl->in_features * kWideNI;
+  hipLaunchKernelGGL(wide_table_kernel, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *kl,
+                     reinterpret_cast<float4*>(wpack + n));
   LAUNCH_CHECK();
   return FETODE_OK;
 }
@@ -394,7 +559,7 @@ int fetode_kanlinear_wide_forward(const fetode_kanlinear_t* kl, const float* wpa
   const int64_t tiles = (B + kWideRows - 1) / kWideRows;
   if (tiles > 0x7fffffff) return set_err(FETODE_EINVAL, "kanlinear wide: batch too large");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(wide_fwd_kernel, dim3((unsigned)tiles, (unsigned)S), dim3(256), 0, s, *kl, wpack, x, B, nch,
+  hipLaunchKernelGGL(wide_fwd_kernel, dim3((unsigned)tiles, (unsigned)S), dim3(kWideThreads), 0, s, *kl, wpack, x, B, nch,
                      (float*)workspace);
   LAUNCH_CHECK();
   const int64_t n = B * kl->out_features;

@@ -146,7 +146,7 @@ class KANLinear(nn.Module):
     def _wide_pack_for(self, d, keep):
         """The weights in the MFMA head's layout, re-packed whenever a weight tensor changes."""
         ws = [t for t in (self.base_weight, self.spline_weight, getattr(self, "spline_scaler", None),
-                          getattr(self, "logistic_weight", None)) if t is not None]
+                          getattr(self, "logistic_weight", None), self.grid) if t is not None]   # grid: basis tables
         key = (_lib.param_generation(), *((t.data_ptr(), t._version) for t in ws))
         cached = getattr(self, "_wide_cache", None)
         if cached is None or cached[0] != key:
