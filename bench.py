@@ -225,20 +225,30 @@ def lv_dopri5_rate(sd, y0d, t, reps=3):
 
 def plain_closure_rate(model, y0d, t, reps=3):
     """The literal drop-in: the reference's `calDeriv(t, X) = kan_fet_model(X)` closure unchanged
-    (INTEGRATION.md §1).  odeint cannot see the model behind a closure, so this is the per-stage
-    path: one fused single-evaluation launch + one stage-combine launch per stage (272 per solve)
-    — what `fet_ode_amd.autonomous(model)` avoids."""
-    func = lambda tt, yy: model(yy)  # noqa: E731
-    with torch.no_grad():
-        F.odeint(func, y0d, t, method="rk4")
-        torch.cuda.synchronize(y0d.device)
-        t0 = time.perf_counter()
-        for _ in range(reps):
-            F.odeint(func, y0d, t, method="rk4")
-        torch.cuda.synchronize(y0d.device)
-        el = (time.perf_counter() - t0) / reps
+    (train_kanfet_node_predprey.py:159-161).  odeint recognises the closure as
+    the module call it is (fet_ode_amd.odeint.closure_field) and integrates it in one launch; the
+    `per_stage` sub-line times the same closure with the recognition switched off (one fused
+    single-evaluation launch + one stage-combine launch per stage, 272 per solve) — the path any
+    closure that does more than call the module takes."""
+    def calDeriv(t, X):
+        dXdt = model(X)
+        return dXdt
+
+    def rate(fuse, n):
+        with torch.no_grad(), F.closure_fusion(fuse):
+            F.odeint(calDeriv, y0d, t, method="rk4")
+            torch.cuda.synchronize(y0d.device)
+            t0 = time.perf_counter()
+            for _ in range(n):
+                F.odeint(calDeriv, y0d, t, method="rk4")
+            torch.cuda.synchronize(y0d.device)
+            return (time.perf_counter() - t0) / n
+
+    el, el_ps = rate(True, 20), rate(False, reps)
     return {"value": STEPS_PER_SOLVE / el, "unit": "RK4 steps/s of the batch-4096 job, plain calDeriv closure",
-            "ms_per_solve": el * 1e3, "path": "per-stage: fetode_field_forward + fetode_rk_combine per stage"}
+            "ms_per_solve": el * 1e3, "path": "fused: the closure recognised as the module call (one launch per solve)",
+            "per_stage": {"value": STEPS_PER_SOLVE / el_ps, "ms_per_solve": el_ps * 1e3,
+                          "path": "closure_fusion(False): fetode_field_forward + fetode_rk_combine per stage"}}
 
 
 def ecg_rate(dev, reps=10, cpu_seconds=5.0, with_cpu=True, rtol=1e-3, atol=1e-4):

@@ -10,15 +10,17 @@ Drop-in surface of the reference hot path (sallywang147/FET-ODE):
   * ``ett``                  — odeint_rk4, EnergyWindowDataset, the KAN-FET LatentNeuralODEForecaster
                                (train_kan_fet_ett.py)
   * ``autonomous(field)``    — calDeriv-style func(t, y) = field(y) that odeint integrates in a
-                               single fused HIP launch
+                               single fused HIP launch; the reference's own unchanged
+                               ``def calDeriv(t, X): return kan_fet_model(X)`` is recognised as
+                               the same thing (``set_closure_fusion`` / ``closure_fusion`` switch it)
 All compute runs in libfetode.so (HIP, gfx950) through the C ABI of include/fetode.h.
 """
 from . import _lib
 from . import ecg, efficientkan, ett, ferro_class, lv, mnist
 from .efficientkan import KAN, KANFET, KANFETLayer, KANLinear, LogisticBasis, ODEFunc, autonomous
 from .ferro_class import FerroelectricBasis
-from .odeint import SOLVERS, odeint, set_fused_training
+from .odeint import SOLVERS, closure_fusion, odeint, set_closure_fusion, set_fused_training
 
-__all__ = ["odeint", "SOLVERS", "set_fused_training", "KAN", "KANFET", "KANFETLayer", "KANLinear", "LogisticBasis",
+__all__ = ["odeint", "SOLVERS", "set_fused_training", "set_closure_fusion", "closure_fusion", "KAN", "KANFET", "KANFETLayer", "KANLinear", "LogisticBasis",
            "FerroelectricBasis", "ODEFunc", "autonomous", "ecg", "efficientkan", "ett", "ferro_class", "lv", "mnist"]
 __version__ = "0.1.0"

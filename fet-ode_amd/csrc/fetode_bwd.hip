@@ -195,12 +195,21 @@ struct BTab {  // per-block LDS copy of one layer's edge tables
   }
 };
 
-template <int W, int NS, int NB>
+template <int W, int NS, int NB, bool WIN = false>
 struct BFeat {  // per-wave LDS features of both layers' inputs, combined index t
+  // dense B-spline row of input t at bd[t * BDP + BD0 + c].  WIN: the interval's four bases are
+  // written at c = m - 3 .. m into a filled row, so the rows carry kSO guard floats on either side
+  // (BD0 keeps the data 16-byte aligned; BDP = 4 mod 8 spreads the inputs over the banks); without
+  // WIN (the adjoint-only sweep, whose 4 waves per SIMD leave no LDS for guards) the row is dense
+  static constexpr bool WINDOW = WIN;
+  static constexpr int BD0 = WIN ? 4 : 0;
+  static constexpr int BDP0 = (BD0 + NS + kSO + 3) / 4 * 4;
+  static constexpr int BDP = !WIN ? NS : BDP0 % 8 == 0 ? BDP0 + 4 : BDP0;
+  __device__ static int bdi(int t, int c) { return t * BDP + BD0 + c; }
   float4 g4[W];  // Ferro per-input terms: x, gate up, wo = wc (1 - up), -ln2 wo
   float x[W], pv[W], silu[W], dsilu[W], u[W], rhm[W];  // rhm: 1 / (knot step) of x's interval
   int m[W];
-  float bd[W * NS];
+  __attribute__((aligned(16))) float bd[W * BDP];
   float sg[NB > 0 ? W * NB : 1];
 };
 
@@ -311,8 +320,8 @@ __device__ __forceinline__ float group_sum(float v) {
 }
 
 // features of combined input t (one lane): SiLU, SiLU', knot interval, u, dense bases, gate
-template <int W, int NG, int NB>
-__device__ __forceinline__ void feat_input(BFeat<W, NG - 1 - kSO, NB>& F, const BInTab<W, NG, NB>& Tb, int t,
+template <int W, int NG, int NB, bool WIN>
+__device__ __forceinline__ void feat_input(BFeat<W, NG - 1 - kSO, NB, WIN>& F, const BInTab<W, NG, NB>& Tb, int t,
                                            float gsl2e, float wc, float gs, int z) {
   constexpr int NI = NG - 1, NS = NG - 1 - kSO;
   const float x = F.x[t];
@@ -340,11 +349,11 @@ __device__ __forceinline__ void feat_input(BFeat<W, NG - 1 - kSO, NB>& F, const 
   F.rhm[t] = rhm;
   F.m[t] = in ? m : NI;
   F.u[t] = u;
-  float* bd = &F.bd[t * NS];
+  using FB = BFeat<W, NS, NB, WIN>;
+  float* bd = &F.bd[FB::bdi(t, 0)];
   // non-finite x: NaN bases like the reference's (x - g)/d * 0; outside the grid: all zero
   const float fill = fin ? 0.f : __builtin_nanf("");
-  // the interval's four basis cubics, all reads issued before any use; the dense row is formed
-  // in registers and written once
+  // the interval's four basis cubics, all reads issued before any use
   const float4* bp = &Tb.bp[Tb.bpi(t, mc) + z];
   float4 p[kSO + 1];
 #pragma unroll
@@ -352,12 +361,27 @@ __device__ __forceinline__ void feat_input(BFeat<W, NG - 1 - kSO, NB>& F, const 
   float v[kSO + 1];
 #pragma unroll
   for (int r = 0; r <= kSO; ++r) v[r] = ffma(ffma(ffma(p[r].w, u, p[r].z), u, p[r].y), u, p[r].x);
+  // dense row through the LDS window: the row filled, then bases m - 3 .. m written over it (one
+  // wave's LDS writes land in issue order; c outside [0, NS) falls in the guards, and off the grid
+  // mc = 0 puts the fill over c = 0 again)
+  if constexpr (WIN) {
+    if constexpr (NS % 4 == 0) {
 #pragma unroll
-  for (int c = 0; c < NS; ++c) {
-    float b = fill;
+      for (int c = 0; c < NS; c += 4) *reinterpret_cast<float4*>(&bd[c]) = make_float4(fill, fill, fill, fill);
+    } else {
 #pragma unroll
-    for (int r = 0; r <= kSO; ++r) b = (in && c == mc - kSO + r) ? v[r] : b;
-    bd[c] = b;
+      for (int c = 0; c < NS; ++c) bd[c] = fill;
+    }
+#pragma unroll
+    for (int r = 0; r <= kSO; ++r) bd[mc - kSO + r] = in ? v[r] : fill;
+  } else {  // formed in registers (select chains) and written once
+#pragma unroll
+    for (int c = 0; c < NS; ++c) {
+      float b = fill;
+#pragma unroll
+      for (int r = 0; r <= kSO; ++r) b = (in && c == mc - kSO + r) ? v[r] : b;
+      bd[c] = b;
+    }
   }
   const float up = sigm_l2(-gsl2e * (x - F.pv[t]));
   const float wo = wc * (1.0f - up);
@@ -427,17 +451,14 @@ __device__ __forceinline__ void layer_jobs(const FT* Fs, const float* __restrict
       if constexpr (ACC) {
         R.base[r] = ffma(go, F.silu[TB + i], R.base[r]);
 #pragma unroll
-        for (int c = 0; c < L::NS; ++c) R.spl[r][c] = ffma(go, F.bd[(TB + i) * L::NS + c], R.spl[r][c]);
+        for (int c = 0; c < L::NS; ++c) R.spl[r][c] = ffma(go, F.bd[FT::bdi(TB + i, c)], R.spl[r][c]);
       }
       const int m = F.m[TB + i];
       const float u = F.u[TB + i];
-      float dsdx;
-      if (m < L::NI) {
-        const float4 cf = Tb.sp[q * BTab<L>::SPS + m + z];  // (o, i, interval), q = o*IN + i
-        dsdx = ffma(u, ffma(3.0f * u, cf.w, 2.0f * cf.z), cf.y) * F.rhm[TB + i];
-      } else {
-        dsdx = u * 0.0f;  // 0 outside the grid, NaN for non-finite inputs (the reference's NaN bases)
-      }
+      // (o, i, interval), q = o*IN + i; off the grid m = NI reads the zero row, so dsdx is 0 there
+      // (u = 0) and NaN for non-finite inputs (u = NaN): the reference's NaN bases, branch-free
+      const float4 cf = Tb.sp[q * BTab<L>::SPS + m + z];
+      const float dsdx = ffma(u, ffma(3.0f * u, cf.w, 2.0f * cf.z), cf.y) * F.rhm[TB + i];
       const float wb = Tb.kw[o * (L::IN * L::NFL) + i * L::NFL + z];
       cb[i * L::NTMP + L::OUT * L::K + o] = go * ffma(wb, F.dsilu[TB + i], dsdx);
     }
@@ -607,7 +628,8 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
   __shared__ BInTab<W, NG, NB> TI;
   __shared__ BTab<L0> T0;
   __shared__ BTab<L1> T1;
-  __shared__ BFeat<W, NS, NB> sF[kTPB][NBUF][TPW];
+  using FB = BFeat<W, NS, NB, PF>;
+  __shared__ FB sF[kTPB][NBUF][TPW];
   __shared__ __attribute__((aligned(16))) float s_cb[kTPB][TPW][CB];  // f2 stores (pairs)
   __shared__ float s_g1[kTPB][TPW][D], s_g0[kTPB][TPW][H], s_gx[kTPB][TPW][D];
   __shared__ float s_ak[kTPB][TPW][4][D], s_ay[kTPB][TPW][D], s_ac[kTPB][4][3];
@@ -699,7 +721,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
         // features of evaluations ev and ev - 1 (every other evaluation; wave-uniform)
         const bool fstep = !PF || ((n_ev - 1 - ev) & 1) == 0;
         float nx1 = 0.f, nx2 = 0.f;
-        BFeat<W, NS, NB>& FF = sF[wid][PF ? (ev - fb) & 1 : 0][tt];
+        FB& FF = sF[wid][PF ? (ev - fb) & 1 : 0][tt];
         if (fstep) {
           if constexpr (PF) {  // prefetch: consumed by the next pair
             nx1 = tape_at(ev - fb - 2);
@@ -717,12 +739,12 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
         wsync();
         if (fstep) {
           // both layers' inputs on one code path over the combined input index
-          if (!(FETODE_EXP_SKIP & 8) && fsl < W) feat_input<W, NG, NB>(FF, TI, fsl, glane, wlane, slane, z);
+          if (!(FETODE_EXP_SKIP & 8) && fsl < W) feat_input<W, NG, NB, PF>(FF, TI, fsl, glane, wlane, slane, z);
           if (!(FETODE_EXP_SKIP & 8)) {
             constexpr int NSG = TPW * W * NB, RSG = (NSG + 63) / 64;
 #pragma unroll
             for (int pb = 0; pb < NBUF; ++pb) {  // one parity buffer at a time (register pressure)
-              BFeat<W, NS, NB>* Fp = sF[wid][pb];
+              FB* Fp = sF[wid][pb];
               float sa[RSG], sb[RSG], sx[RSG];
 #pragma unroll
               for (int k = 0; k < RSG; ++k) {  // every round's operands read before any sigmoid
@@ -747,7 +769,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
           cur = nx1;
           prv = nx2;
         }
-        BFeat<W, NS, NB>* Fs = sF[wid][PF ? ev & 1 : 0];
+        FB* Fs = sF[wid][PF ? ev & 1 : 0];
         layer_jobs<L1, D, ACC, TPW, D, CB>(Fs, g1s, T1, TI.rh, R1, cbs, gl1, wc1, gs1, lane, z);
         wsync();
         reduce_gin<L1, TPW, H, CB>(cbs, g0s, lane);  // d loss / d h

@@ -8,9 +8,10 @@ RKAdaptiveStepsizeODESolver + Dopri5Solver), including the call order of ``func`
 matters because the hysteresis basis is stateful (ferro_class.py:409).
 
 Two execution paths, both HIP:
-  * fused: ``func`` is ``fet_ode_amd.autonomous(field)`` (or ``field.as_ode_func()``) for a
-    KAN / KANFET shape with a fused kernel and a fixed-grid method -> the whole solve is one
-    kernel launch (``fetode_integrate_fixed``).
+  * fused: ``func`` is ``fet_ode_amd.autonomous(field)`` (or ``field.as_ode_func()``), or the
+    reference's unchanged ``calDeriv`` closure ``return kan_fet_model(X)`` (recognised, see
+    ``closure_field``), for a KAN / KANFET shape with a fused kernel and a fixed-grid method ->
+    the whole solve is one kernel launch (``fetode_integrate_fixed``).
   * per-stage: any other callable -> ``func`` is called stage by stage exactly like
     torchdiffeq, and the stage combines run as HIP kernels (``fetode_rk_combine``).
 """
@@ -245,8 +246,108 @@ class _FusedFixedFn(torch.autograd.Function):
 
 
 def fused_field(func):
-    """The KAN/KANFET module behind ``func`` if it was tagged by ``autonomous``."""
-    return getattr(func, "_fetode_field", None)
+    """The KAN/KANFET module behind ``func``: tagged by ``autonomous``, or a plain closure that
+    only returns the module's call on the state (the reference's unchanged ``calDeriv``)."""
+    field = getattr(func, "_fetode_field", None)
+    if field is None and _CLOSURE_FUSION:
+        field = closure_field(func)
+    return field
+
+
+# ---------------------------------------------------------------------------------------------
+# the reference's calDeriv, recognised
+# ---------------------------------------------------------------------------------------------
+# train_kanfet_node_predprey.py:159-161 (and predator_prey.py:113-115) integrate
+#     def calDeriv(t, X):
+#         dXdt = kan_fet_model(X)
+#         return dXdt
+# which calls the module once per stage and does nothing else, so integrating it IS integrating
+# autonomous(kan_fet_model): same evaluations, same order, same hysteresis updates.  The function's
+# bytecode is checked for exactly that shape (load the module by name, call it on the second
+# argument, return the result — nothing else), the name is resolved at every solve (globals or
+# closure cell), and only an exact KAN / KANFET instance without hooks qualifies (a subclass may
+# override forward; a hook would not run on the fused path).  Anything else takes the per-stage
+# path, which calls the closure stage by stage like torchdiffeq.
+
+_CLOSURE_FUSION = os.environ.get("FETODE_CLOSURE_FUSION", "1") != "0"
+_IGNORED_OPS = {"NOP", "RESUME", "PUSH_NULL", "PRECALL", "CACHE", "EXTENDED_ARG", "COPY_FREE_VARS"}
+_CLOSURE_SHAPES: Dict[object, Optional[Tuple[str, str]]] = {}
+
+
+def set_closure_fusion(enabled: bool) -> bool:
+    """Recognise ``return model(X)`` closures as the module (default on; env
+    FETODE_CLOSURE_FUSION=0 turns it off).  Returns the previous value."""
+    global _CLOSURE_FUSION
+    prev, _CLOSURE_FUSION = _CLOSURE_FUSION, bool(enabled)
+    return prev
+
+
+class closure_fusion:
+    """Context manager: ``with closure_fusion(False): ...`` integrates closures stage by stage."""
+
+    def __init__(self, enabled: bool):
+        self.enabled = enabled
+
+    def __enter__(self):
+        self.prev = set_closure_fusion(self.enabled)
+        return self
+
+    def __exit__(self, *exc):
+        set_closure_fusion(self.prev)
+        return False
+
+
+def _closure_shape(code) -> Optional[Tuple[str, str]]:
+    """('global' | 'deref', name) if `code` is `return M(a1)` or `v = M(a1); return v` over its
+    second positional argument a1 (two positional parameters, no *args / **kwargs / keyword-only)."""
+    import dis
+    if code.co_argcount != 2 or code.co_kwonlyargcount or code.co_flags & 0x0C:
+        return None
+    arg = code.co_varnames[1]
+    ins = [(i.opname, i.argval) for i in dis.get_instructions(code) if i.opname not in _IGNORED_OPS]
+    if len(ins) < 4 or ins[0][0] not in ("LOAD_GLOBAL", "LOAD_DEREF") or ins[1] != ("LOAD_FAST", arg):
+        return None
+    if ins[2][0] not in ("CALL_FUNCTION", "CALL") or ins[2][1] != 1:
+        return None
+    tail = ins[3:]
+    if tail != [("RETURN_VALUE", None)]:
+        if len(tail) != 3 or tail[0][0] != "STORE_FAST" or tail[1] != ("LOAD_FAST", tail[0][1]) \
+                or tail[2] != ("RETURN_VALUE", None) or tail[0][1] == arg:
+            return None
+    return ("global" if ins[0][0] == "LOAD_GLOBAL" else "deref", ins[0][1])
+
+
+def _plain_field(obj) -> bool:
+    from .efficientkan import KAN, KANFET
+    if type(obj) not in (KAN, KANFET):
+        return False
+    from torch.nn.modules import module as M
+    hooks = (obj._forward_hooks, obj._forward_pre_hooks, obj._backward_hooks,
+             getattr(obj, "_backward_pre_hooks", {}), M._global_forward_hooks, M._global_forward_pre_hooks,
+             M._global_backward_hooks, getattr(M, "_global_backward_pre_hooks", {}))
+    return not any(hooks)
+
+
+def closure_field(func):
+    """The module a ``calDeriv``-shaped plain function calls, or None (see above)."""
+    import types
+    if not isinstance(func, types.FunctionType):
+        return None
+    code = func.__code__
+    shape = _CLOSURE_SHAPES.get(code, False)
+    if shape is False:
+        shape = _CLOSURE_SHAPES[code] = _closure_shape(code)
+    if shape is None:
+        return None
+    kind, name = shape
+    if kind == "global":
+        obj = func.__globals__.get(name)
+    else:
+        try:
+            obj = func.__closure__[code.co_freevars.index(name)].cell_contents
+        except (ValueError, IndexError, TypeError):   # not a free variable, or an empty cell
+            return None
+    return obj if _plain_field(obj) else None
 
 
 _FUSED_TRAINING = os.environ.get("FETODE_FUSED_TRAINING", "1") != "0"

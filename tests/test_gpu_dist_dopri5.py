@@ -53,7 +53,7 @@ def test_sharded_dopri5_matches_single_device(dev):
     import fet_ode_amd as F
     g = load_golden("traj_kanfet")
     m = _model(F, golden_sd(g))
-    with torch.no_grad():
+    with torch.no_grad(), F.closure_fusion(False):   # the host-driven solver (its attempt record)
         ref = F.odeint(lambda tt, yy: m(yy), torch.from_numpy(g["y0_B64"]).to(dev),
                        torch.tensor(T_GRID, dtype=torch.float64), rtol=1e-3, atol=1e-4).cpu()
     s = F.dopri5.dopri5_solve.last

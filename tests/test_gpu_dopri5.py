@@ -55,7 +55,7 @@ def test_dopri5_kanfet_trace(dev):
     m = F.KANFET([2, 10, 2], grid_size=5)
     m.load_state_dict(golden_sd(g))
     m = m.to(dev)
-    with torch.no_grad():
+    with torch.no_grad(), F.closure_fusion(False):   # the host-driven solver (its attempt record)
         sol = F.odeint(lambda tt, yy: m(yy), torch.from_numpy(g["y0"]).to(dev), torch.from_numpy(g["t"]),
                        rtol=1e-3, atol=1e-4).cpu()
     solver = F.dopri5.dopri5_solve.last
@@ -135,7 +135,7 @@ def test_rk4_classic_fused_and_per_stage(dev, fused):
     y0 = torch.from_numpy(g["y0_B64"])
     t = torch.from_numpy(g["t35"])
     func = F.autonomous(m) if fused else (lambda tt, yy: m(yy))
-    with torch.no_grad():
+    with torch.no_grad(), F.closure_fusion(fused):
         gpu = F.odeint(func, y0.to(dev), t, method="rk4_classic").cpu()
     cpu = O.odeint(lambda tt, yy: ref(yy), y0, t, method="rk4_classic")
     assert ((gpu - cpu).norm(dim=(1, 2)) / cpu.norm(dim=(1, 2))).max() < 1e-5

@@ -94,7 +94,8 @@ def _loss_grads_gpu(model, y0, t, target, dev, use_autonomous):
     import fet_ode_amd as F
     y0g = y0.clone().to(dev).requires_grad_(True)
     func = F.autonomous(model) if use_autonomous else (lambda tt, yy: model(yy))
-    pred = F.odeint(func, y0g, t, method="rk4")
+    with F.closure_fusion(use_autonomous):   # the closure stage by stage (HIP VJPs per stage)
+        pred = F.odeint(func, y0g, t, method="rk4")
     loss = torch.mean(torch.square(pred[:, 0, :] - target.to(dev)))
     loss.backward()
     return loss.item(), y0g.grad.cpu(), {n: p.grad.cpu() for n, p in model.named_parameters()}

@@ -234,10 +234,46 @@ def test_per_stage_path_matches_fused(dev):
     t = torch.from_numpy(g["t35"])
     with torch.no_grad():
         a = F.odeint(F.autonomous(m1), y0, t, method="rk4")
-        b = F.odeint(lambda tt, yy: m2(yy), y0, t, method="rk4")
+        with F.closure_fusion(False):   # the closure stage by stage
+            b = F.odeint(lambda tt, yy: m2(yy), y0, t, method="rk4")
     # same kernels and op order per stage: identical up to launch-boundary effects (none expected)
     assert slice_rel_err(b.cpu(), a.cpu()) <= 1e-6
     assert torch.allclose(m1.layers[1].ferro.prev_x, m2.layers[1].ferro.prev_x, rtol=1e-5, atol=1e-6)
+
+
+def test_reference_caldriv_closure_takes_fused_path(dev):
+    """The reference's unchanged calDeriv (train_kanfet_node_predprey.py:159-161) is integrated on
+    the fused path: bitwise the autonomous() solve, hysteresis state included; the training solve
+    (tape + reverse sweep) gives bitwise the same gradients; dopri5 runs resident."""
+    import fet_ode_amd as F
+    from fet_ode_amd.dopri5 import ResidentSolve
+    g = load_golden("traj_kanfet")
+    m1 = _kanfet_from(g, dev)
+    m2 = _kanfet_from(g, dev)
+    y0 = torch.from_numpy(g["y0_B64"]).to(dev)
+    t = torch.from_numpy(g["t35"])
+
+    def calDeriv(t, X):
+        dXdt = m2(X)
+        return dXdt
+
+    with torch.no_grad():
+        a = F.odeint(F.autonomous(m1), y0, t, method="rk4")
+        b = F.odeint(calDeriv, y0, t, method="rk4")
+    assert torch.equal(a, b)
+    for l1, l2 in zip(m1.layers, m2.layers):
+        assert torch.equal(l1.ferro.prev_x, l2.ferro.prev_x)
+    grads = []
+    for func, m in ((F.autonomous(m1), m1), (calDeriv, m2)):
+        m.reset_state()
+        m.zero_grad(set_to_none=True)
+        F.odeint(func, y0, t[:8], method="rk4").square().mean().backward()
+        grads.append([p.grad.clone() for p in m.parameters()])
+    for ga, gb in zip(*grads):
+        assert torch.equal(ga, gb)
+    with torch.no_grad():
+        F.odeint(calDeriv, y0, t[:6], rtol=1e-3, atol=1e-4)
+    assert isinstance(F.dopri5.dopri5_solve.last, ResidentSolve)
 
 
 def test_state_carries_over_between_solves(dev):
