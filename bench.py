@@ -185,7 +185,8 @@ def train_rate(model, y0d, t, iters, warmup, world, strong=True):
         torch.distributed.barrier()
     el = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([el], device=dev, dtype=torch.float64)
+        nccl = torch.distributed.get_backend() == "nccl"
+        tt = torch.tensor([el], device=dev if nccl else "cpu", dtype=torch.float64)
         torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
         el = tt.item()
     return {"value": (1 if strong else world) * iters * STEPS_PER_SOLVE / el,
@@ -481,11 +482,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; FETODE_BENCH_BACKEND=gloo rehearses the N > 1 path with several ranks on
+    # fewer GPUs (ranks share devices round-robin; timings are not meaningful then)
+    backend = os.environ.get("FETODE_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local %= torch.cuda.device_count()
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device("cuda", local)
     strong = args.scaling == "strong"
     model, sd, y0, y0g, t = make_problem(rank, world, args.scaling, dev)
@@ -511,7 +520,7 @@ def main():
             dist.barrier()
         el = time.perf_counter() - t0
         if world > 1:
-            tt = torch.tensor([el], device=dev, dtype=torch.float64)
+            tt = torch.tensor([el], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             el = tt.item()
         k_ms = kernel_time_ms(model, y0d, t)
@@ -541,7 +550,8 @@ def main():
                        "parallelism": f"trajectory-sharded x{world} (no collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "fused4_kernel<10,10,10,12,true,true> (v4 rk4 path)",
+                         "kernel": ("fused4_kernel<10,10,10,12,true,true> (v4 rk4 path)" if Bl > 512
+                                    else "small6_kernel<true,true> (v6 small-batch rk4 path)"),
                          "kernel_ms": k_ms, "alg_bytes_per_launch": bytes_launch,
                          "traffic_source": traffic_src,
                          "valu": {"achieved_tflops": tflops, "peak_tflops": FP32_PEAK_TFLOPS,
