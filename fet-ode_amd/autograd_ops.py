@@ -58,12 +58,21 @@ def build_plan(owner, handle: _lib.FieldHandle, device) -> torch.Tensor:
         _lib.check(_lib.FETODE_EINVAL, "fetode_plan_bytes")
     n = max(1, nbytes // 4)
     plan = getattr(owner, "_fetode_plan", None)
-    if plan is None or plan.numel() < n or plan.device != device:
+    # a plan a pending backward still reads (pin_plan) is never rebuilt in place: the rebuild gets a
+    # fresh buffer and the pinned one lives on in that backward's context
+    if plan is None or plan.numel() < n or plan.device != device or owner.__dict__.get("_fetode_plan_pin") is plan:
         plan = torch.empty(n, dtype=torch.float32, device=device)
         owner._fetode_plan = plan
     _lib.check(lib.fetode_plan_build(handle.ref, plan.data_ptr(), _lib.stream_handle(device)),
                "fetode_plan_build")
     owner._fetode_plan_for = (handle, vkey)
+    return plan
+
+
+def pin_plan(owner, plan: torch.Tensor) -> torch.Tensor:
+    """Keep `plan` unchanged for a backward that runs after later solves (build_plan then
+    rebuilds into a new buffer instead of this one): no per-iteration copy of the plan."""
+    owner.__dict__["_fetode_plan_pin"] = plan
     return plan
 
 

@@ -27,7 +27,7 @@ import torch
 
 from . import _lib
 from .autograd_ops import (FERRO_PARAM_NAMES, axpby, build_plan, field_layers, grad_enabled_for, kan_params,
-                           make_handle, pack_state, unpack_state)
+                           make_handle, pack_state, pin_plan, unpack_state)
 
 FIXED_METHODS = {"euler": _lib.EULER, "midpoint": _lib.MIDPOINT, "rk4": _lib.RK4,
                  "rk4_classic": _lib.RK4_CLASSIC}
@@ -189,8 +189,9 @@ class _FusedFixedFn(torch.autograd.Function):
         if training:
             H = field_layers(field)[0][0].out_features
             tape = torch.empty(sched.n_steps * _STAGES[method], B, D + H, device=dev, dtype=torch.float32)
-            # the backward needs the plan and the state of THIS solve: later solves overwrite both
-            ctx.plan = plan.clone()
+            # the backward needs the plan and the state of THIS solve: later solves overwrite the
+            # state in place (a copy), and rebuild the plan into a new buffer once it is pinned
+            ctx.plan = pin_plan(field, plan)
             ctx.state0 = None if state is None else state.clone()
             ctx.mask, ctx.handle, ctx.method, ctx.sched, ctx.field = mask, handle, method, sched, field
             ctx.tape, ctx.B = tape, B
