@@ -19,6 +19,9 @@ namespace {
 constexpr int RB = 256;  // reduction block
 
 __device__ __forceinline__ float sigm(float z) { return 1.0f / (1.0f + expf(-z)); }
+#ifndef FETODE_GXAB_FAST
+#define FETODE_GXAB_FAST 1
+#endif
 
 template <int N>
 __device__ __forceinline__ void block_sum(float (&v)[N], float* red /* RB*N */) {
@@ -89,6 +92,56 @@ __device__ int bspline_vals_derivs(float x, int NG, const float* __restrict__ g,
     if (j >= 0 && j <= NG - 2 - SO) {
       const float a = P[r] / (g[j + SO] - g[j]);
       const float b = (r + 1 <= SO) ? P[r + 1] / (g[j + SO + 1] - g[j + 1]) : 0.f;
+      der[r] = SO * (a - b);
+    }
+  }
+  return m;
+}
+
+// bspline_vals_derivs with the divisions replaced by reciprocal knot spans
+// rk[(k-1)*(NG-1)+j] = 1/(g[j+k]-g[j]) (as bspline_local does for the forward head)
+template <int SO>
+__device__ int bspline_vals_derivs_rk(float x, int NG, const float* __restrict__ g, const float* __restrict__ rk,
+                                      float* val, float* der) {
+#pragma unroll
+  for (int r = 0; r <= SO; ++r) val[r] = der[r] = 0.f;
+  if (!__builtin_isfinite(x)) {
+    for (int r = 0; r <= SO; ++r) val[r] = der[r] = __builtin_nanf("");
+    return -2;
+  }
+  int m = -1;
+  for (int j = 0; j < NG; ++j) m += (x >= g[j]) ? 1 : 0;
+  if (m < 0 || m > NG - 2) return -1;
+  const int S = NG - 1;
+  float N[SO + 2], P[SO + 2];
+#pragma unroll
+  for (int r = 0; r < SO + 2; ++r) N[r] = P[r] = 0.f;
+  N[SO] = 1.f;
+#pragma unroll
+  for (int k = 1; k <= SO; ++k) {
+    if (k == SO) {
+#pragma unroll
+      for (int r = 0; r < SO + 2; ++r) P[r] = N[r];
+    }
+    float M[SO + 2];
+#pragma unroll
+    for (int r = 0; r < SO + 2; ++r) M[r] = 0.f;
+#pragma unroll
+    for (int r = SO - k; r <= SO; ++r) {
+      const int j = m - SO + r;
+      if (j >= 0 && j <= NG - 2 - k)
+        M[r] = ((x - g[j]) * rk[(k - 1) * S + j]) * N[r] + ((g[j + k + 1] - x) * rk[(k - 1) * S + j + 1]) * N[r + 1];
+    }
+#pragma unroll
+    for (int r = 0; r < SO + 2; ++r) N[r] = M[r];
+  }
+#pragma unroll
+  for (int r = 0; r <= SO; ++r) {
+    const int j = m - SO + r;
+    val[r] = N[r];
+    if (j >= 0 && j <= NG - 2 - SO) {
+      const float a = P[r] * rk[(SO - 1) * S + j];
+      const float b = (r + 1 <= SO) ? P[r + 1] * rk[(SO - 1) * S + j + 1] : 0.f;
       der[r] = SO * (a - b);
     }
   }
@@ -279,14 +332,16 @@ __global__ __launch_bounds__(256) void wide_gw_kernel(fetode_kanlinear_t kl, con
 // G_f = sum_o g[b, o] W_f[i, o] (the packed weights of 4 inputs staged in LDS, one input per
 // wave: broadcast reads), then d x = sum_f G_f d feat_f / d x and the logistic bases' a / b sums
 // (per-lane partials -> wave sum in a fixed order -> per-split slots -> wide_ab_reduce_kernel).
+// NO: outputs walked per (row, input) — 12 when out <= 12 (the MNIST head's 10), else 16
+template <int NO>
 __global__ __launch_bounds__(256) void wide_gxab_kernel(fetode_kanlinear_t kl, const float* __restrict__ x,
                                                        const float* __restrict__ g, int64_t B, float* __restrict__ gx,
                                                        float* __restrict__ abpart, int accumulate) {
   __shared__ float wts[4][kGwF][16];
   __shared__ float gs[64][17];
   __shared__ float gk[4][kGwNG];
+  __shared__ float rk[4][3 * (kGwNG - 1)];  // reciprocal knot spans (bspline_vals_derivs_rk)
   __shared__ float lab[4][2 * kGwNB];
-  __shared__ float red[4][64];
   const int in = kl.in_features, out = kl.out_features;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int i0 = blockIdx.x * 4, i = i0 + wv;
@@ -312,6 +367,11 @@ __global__ __launch_bounds__(256) void wide_gxab_kernel(fetode_kanlinear_t kl, c
     wts[ii][f][o] = v;
   }
   if (tid < 4 * kGwNG) gk[tid / kGwNG][tid % kGwNG] = kl.grid[(int64_t)i0 * kGwNG + tid];
+  if (tid < 4 * 3 * (kGwNG - 1)) {
+    const int ii = tid / (3 * (kGwNG - 1)), q = tid % (3 * (kGwNG - 1)), k = q / (kGwNG - 1) + 1, j = q % (kGwNG - 1);
+    const float* gg = kl.grid + (int64_t)(i0 + ii) * kGwNG;
+    rk[ii][q] = j + k < kGwNG ? 1.0f / (gg[j + k] - gg[j]) : 0.f;
+  }
   if (lg && tid < 4 * kGwNB) {
     lab[tid / kGwNB][tid % kGwNB] = kl.logistic_a[(int64_t)i0 * kGwNB + tid];
     lab[tid / kGwNB][kGwNB + tid % kGwNB] = kl.logistic_b[(int64_t)i0 * kGwNB + tid];
@@ -330,21 +390,25 @@ __global__ __launch_bounds__(256) void wide_gxab_kernel(fetode_kanlinear_t kl, c
     const int64_t b = c * 64 + lane;
     if (b >= B) continue;
     const float xv = x[b * in + i];
-    float go[16];
+    float go[NO];
 #pragma unroll
-    for (int o = 0; o < 16; ++o) go[o] = gs[lane][o];
+    for (int o = 0; o < NO; ++o) go[o] = gs[lane][o];
     float G[kGwF];
 #pragma unroll
     for (int f = 0; f < kGwF; ++f) {
       float acc = 0.f;
 #pragma unroll
-      for (int o = 0; o < 16; ++o) acc = __builtin_fmaf(go[o], wts[wv][f][o], acc);
+      for (int o = 0; o < NO; ++o) acc = __builtin_fmaf(go[o], wts[wv][f][o], acc);
       G[f] = acc;
     }
+#if FETODE_GXAB_FAST  // v_exp / v_rcp sigmoids (1 ulp), as the forward head (wide_fwd_kernel)
+    const float sg = sig_from_neg_l2(-xv * FETODE_LOG2E);
+#else
     const float sg = sigm(xv);
+#endif
     float d = G[0] * (sg * (1.0f + xv * (1.0f - sg)));
     float val[4], der[4];
-    const int m = bspline_vals_derivs<3>(xv, kGwNG, gk[wv], val, der);
+    const int m = bspline_vals_derivs_rk<3>(xv, kGwNG, gk[wv], rk[wv], val, der);
     if (m >= 0) {
 #pragma unroll
       for (int r = 0; r <= 3; ++r) {
@@ -360,7 +424,11 @@ __global__ __launch_bounds__(256) void wide_gxab_kernel(fetode_kanlinear_t kl, c
 #pragma unroll
       for (int j = 0; j < kGwNB; ++j) {
         const float a = lab[wv][j], bj = lab[wv][kGwNB + j];
+#if FETODE_GXAB_FAST
+        const float sj = sig_from_neg_l2((a * (xv - bj)) * -FETODE_LOG2E);
+#else
         const float sj = sigm(a * (xv - bj));
+#endif
         const float dz = G[1 + kGwNS + j] * (2.0f * sj * (1.0f - sj));
         d += dz * a;
         ga[j] += dz * (xv - bj);
@@ -384,7 +452,6 @@ __global__ __launch_bounds__(256) void wide_gxab_kernel(fetode_kanlinear_t kl, c
       }
     }
   }
-  (void)red;
 }
 
 __global__ void wide_ab_reduce_kernel(fetode_kanlinear_t kl, const float* __restrict__ abpart, fetode_kanlinear_grad_t gr,
@@ -612,7 +679,10 @@ int fetode_kanlinear_backward(const fetode_kanlinear_t* kl, const float* x, int6
     float* abpart = (grads && NB > 0)
                         ? (float*)workspace + (int64_t)out * in * (NS + NB) + (int64_t)kGwSplit * in * kGwF * 16
                         : nullptr;
-    hipLaunchKernelGGL(wide_gxab_kernel, dim3(in / 4, kGwSplit), dim3(256), 0, s, *kl, x, g, B, gx, abpart, accumulate);
+    if (kl->out_features <= 12)
+      hipLaunchKernelGGL(wide_gxab_kernel<12>, dim3(in / 4, kGwSplit), dim3(256), 0, s, *kl, x, g, B, gx, abpart, accumulate);
+    else
+      hipLaunchKernelGGL(wide_gxab_kernel<16>, dim3(in / 4, kGwSplit), dim3(256), 0, s, *kl, x, g, B, gx, abpart, accumulate);
     LAUNCH_CHECK();
     if (abpart) {
       hipLaunchKernelGGL(wide_ab_reduce_kernel, dim3(nblk((int64_t)in * NB, 256)), dim3(256), 0, s, *kl, abpart, *grads,
