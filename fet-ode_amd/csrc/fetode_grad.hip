@@ -379,17 +379,32 @@ __global__ __launch_bounds__(256) void wide_gxab_kernel(fetode_kanlinear_t kl, c
   float ga[kGwNB], gb[kGwNB];
 #pragma unroll
   for (int j = 0; j < kGwNB; ++j) ga[j] = gb[j] = 0.f;
-  for (int64_t c = c0; c < c1; ++c) {
-    __syncthreads();
-    for (int t = tid; t < 64 * 16; t += 256) {
-      const int rr = t / 16, o = t % 16;
+  // the next chunk's g tile (4 values per thread) and x are loaded while the current chunk is
+  // computed (their global-load latency was exposed once per chunk: ~half the wave cycles waiting)
+  float gnx[4], xnx = 0.f;
+  auto fetch = [&](int64_t c) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int t = tid + 256 * k, rr = t / 16, o = t % 16;
       const int64_t bb = c * 64 + rr;
-      gs[rr][o] = (bb < B && o < out) ? g[bb * out + o] : 0.f;
+      gnx[k] = (bb < B && o < out) ? g[bb * out + o] : 0.f;
     }
+    const int64_t bl = c * 64 + lane;
+    xnx = bl < B ? x[bl * in + i] : 0.f;
+  };
+  if (c0 < c1) fetch(c0);
+  for (int64_t c = c0; c < c1; ++c) {
+    __syncthreads();  // the previous chunk's tile is consumed
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int t = tid + 256 * k;
+      gs[t / 16][t % 16] = gnx[k];
+    }
+    const float xv = xnx;
+    if (c + 1 < c1) fetch(c + 1);
     __syncthreads();
     const int64_t b = c * 64 + lane;
     if (b >= B) continue;
-    const float xv = x[b * in + i];
     float go[NO];
 #pragma unroll
     for (int o = 0; o < NO; ++o) go[o] = gs[lane][o];
