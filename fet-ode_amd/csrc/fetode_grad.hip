@@ -287,12 +287,32 @@ __global__ __launch_bounds__(256) void wide_gw_kernel(fetode_kanlinear_t kl, con
     lab[tid / kGwNB][kGwNB + tid % kGwNB] = kl.logistic_b[(int64_t)i0 * kGwNB + tid];
   }
   gw_f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  // the next chunk's x and g tile are fetched into registers while the current chunk computes
+  float gnx[4], xnx = 0.f;
+  auto fetch = [&](int64_t c) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int t = tid + 256 * k, rr = t / 16, o = t % 16;
+      const int64_t bb = c * 64 + rr;
+      gnx[k] = (bb < B && o < out) ? g[bb * out + o] : 0.f;
+    }
+    const int64_t bl = c * 64 + lane;
+    xnx = bl < B ? x[bl * in + i0 + wv] : 0.f;
+  };
+  if (c0 < c1) fetch(c0);
   for (int64_t c = c0; c < c1; ++c) {
     const int64_t b = c * 64 + lane;
     __syncthreads();
+    const float xcur = xnx;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int t = tid + 256 * k;
+      gs[t / 16][t % 16] = gnx[k];
+    }
+    if (c + 1 < c1) fetch(c + 1);
     {  // features of (row b, input i0 + wv)
       const bool ok = b < B;
-      const float xv = ok ? x[b * in + i0 + wv] : 0.f;
+      const float xv = xcur;
       // the forward head's feature forms (fetode_mnist.hip wide_fwd_kernel): v_exp / v_rcp, spans
       Fs[wv][0][lane] = ok ? silu(xv) : 0.f;   // the reference's base branch SiLU(x)
       bspline_local<3>(xv, kGwNG, &gk[wv][0], &rk[wv][0], [&](int cc, float v) { sbs[cc][tid] = v; });
@@ -302,11 +322,6 @@ __global__ __launch_bounds__(256) void wide_gw_kernel(fetode_kanlinear_t kl, con
       for (int j = 0; j < kGwNB; ++j)
         Fs[wv][1 + kGwNS + j][lane] =
             (ok && lg) ? 2.0f * sig_from_neg_l2((xv - lab[wv][kGwNB + j]) * lab[wv][j]) : 0.f;
-    }
-    for (int t = tid; t < 64 * 16; t += 256) {
-      const int rr = t / 16, o = t % 16;
-      const int64_t bb = c * 64 + rr;
-      gs[rr][o] = (bb < B && o < out) ? g[bb * out + o] : 0.f;
     }
     __syncthreads();
     const int m = lane & 15, kq = lane >> 4;
