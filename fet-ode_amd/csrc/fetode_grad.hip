@@ -423,14 +423,18 @@ __global__ __launch_bounds__(256) void wide_gxab_kernel(fetode_kanlinear_t kl, c
     float go[NO];
 #pragma unroll
     for (int o = 0; o < NO; ++o) go[o] = gs[lane][o];
-    float G[kGwF];
-#pragma unroll
-    for (int f = 0; f < kGwF; ++f) {
+    // G_f = sum_o g[b, o] W_f[i, o] for the SiLU and logistic features; of the spline features only
+    // the (at most 4) bases active at x are formed, below (the others multiply a zero derivative)
+    auto gdot = [&](int f) __attribute__((always_inline)) {
       float acc = 0.f;
 #pragma unroll
       for (int o = 0; o < NO; ++o) acc = __builtin_fmaf(go[o], wts[wv][f][o], acc);
-      G[f] = acc;
-    }
+      return acc;
+    };
+    float G[kGwF];
+    G[0] = gdot(0);
+#pragma unroll
+    for (int f = 1 + kGwNS; f < kGwF; ++f) G[f] = gdot(f);
 #if FETODE_GXAB_FAST  // v_exp / v_rcp sigmoids (1 ulp), as the forward head (wide_fwd_kernel)
     const float sg = sig_from_neg_l2(-xv * FETODE_LOG2E);
 #else
@@ -442,10 +446,8 @@ __global__ __launch_bounds__(256) void wide_gxab_kernel(fetode_kanlinear_t kl, c
     if (m >= 0) {
 #pragma unroll
       for (int r = 0; r <= 3; ++r) {
-        const int cc = m - 3 + r;
-#pragma unroll
-        for (int k = 0; k < kGwNS; ++k)
-          if (k == cc) d += G[1 + k] * der[r];
+        const int cc = m - 3 + r;   // spline basis cc, when 0 <= cc < NS
+        if ((unsigned)cc < (unsigned)kGwNS) d += gdot(1 + cc) * der[r];
       }
     } else if (m == -2) {
       d = __builtin_nanf("");
