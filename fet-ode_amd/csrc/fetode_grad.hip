@@ -268,7 +268,6 @@ __global__ __launch_bounds__(256) void wide_gw_kernel(fetode_kanlinear_t kl, con
   __shared__ float gk[4][kGwNG];
   __shared__ float rk[4][3 * (kGwNG - 1)];  // 1 / (g[j+k] - g[j]) (bspline_local)
   __shared__ float lab[4][2 * kGwNB];       // -a log2(e) | b
-  __shared__ float sbs[kGwNS][256];
   const int in = kl.in_features, out = kl.out_features;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int i0 = blockIdx.x * 4;
@@ -315,9 +314,8 @@ __global__ __launch_bounds__(256) void wide_gw_kernel(fetode_kanlinear_t kl, con
       const float xv = xcur;
       // the forward head's feature forms (fetode_mnist.hip wide_fwd_kernel): v_exp / v_rcp, spans
       Fs[wv][0][lane] = ok ? silu(xv) : 0.f;   // the reference's base branch SiLU(x)
-      bspline_local<3>(xv, kGwNG, &gk[wv][0], &rk[wv][0], [&](int cc, float v) { sbs[cc][tid] = v; });
-#pragma unroll
-      for (int k = 0; k < kGwNS; ++k) Fs[wv][1 + k][lane] = ok ? sbs[k][tid] : 0.f;
+      // the spline rows written in place (zeros, then the active bases over them)
+      bspline_local<3>(xv, kGwNG, &gk[wv][0], &rk[wv][0], [&](int cc, float v) { Fs[wv][1 + cc][lane] = ok ? v : 0.f; });
 #pragma unroll
       for (int j = 0; j < kGwNB; ++j)
         Fs[wv][1 + kGwNS + j][lane] =
