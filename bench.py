@@ -64,7 +64,7 @@ def parse():
     ap.add_argument("--no-ett", action="store_true", help="skip the ETT KAN-FET latent-ODE forecaster line")
     ap.add_argument("--ett-batch", type=int, default=8192)
     ap.add_argument("--cpu-solves", type=int, default=3, help="CPU baseline: median over this many solves")
-    ap.add_argument("--train-iters", type=int, default=20, help="0 skips the training-rate line")
+    ap.add_argument("--train-iters", type=int, default=50, help="0 skips the training-rate line")
     return ap.parse_args()
 
 
@@ -524,7 +524,7 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             el = tt.item()
         k_ms = kernel_time_ms(model, y0d, t)
-    train = train_rate(model, y0d, t, args.train_iters, 2, world, strong) if args.train_iters > 0 else None
+    train = train_rate(model, y0d, t, args.train_iters, 5, world, strong) if args.train_iters > 0 else None
     ms_per_step = el / args.steps * 1e3
     # strong: every solve covers the global batch once; weak: each rank's solve is a batch of its own
     value = (1 if strong else world) * args.steps * STEPS_PER_SOLVE / el
