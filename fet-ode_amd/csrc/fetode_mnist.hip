@@ -117,11 +117,28 @@ __global__ __launch_bounds__(kKThreads) void kuramoto_bwd_kernel(int H, int W, i
     g[p] = (-sv) * gfeat[b * 2 * HW + p] + cv * gfeat[b * 2 * HW + HW + p];
     go[p] = 0.f;
   }
+  // the phases of step s - 1 are fetched into registers while step s runs (a global-load round
+  // trip per step was exposed after the barrier)
+  constexpr int kPP = kMaxPix / kKThreads;
+  float tn[kPP];
+#pragma unroll
+  for (int j = 0; j < kPP; ++j) {
+    const int q = threadIdx.x + j * kKThreads;
+    tn[j] = (steps > 0 && q < HW) ? tb[(steps - 1) * HW + q] : 0.f;
+  }
   for (int s = steps - 1; s >= 0; --s) {
     __syncthreads();
-    for (int p = threadIdx.x; p < HW; p += kKThreads) {
-      const float t = tb[s * HW + p];
-      phase_sincos(t, sn[p], cs[p]);
+#pragma unroll
+    for (int j = 0; j < kPP; ++j) {
+      const int q = threadIdx.x + j * kKThreads;
+      if (q < HW) phase_sincos(tn[j], sn[q], cs[q]);
+    }
+    if (s > 0) {
+#pragma unroll
+      for (int j = 0; j < kPP; ++j) {
+        const int q = threadIdx.x + j * kKThreads;
+        tn[j] = q < HW ? tb[(s - 1) * HW + q] : 0.f;
+      }
     }
     __syncthreads();
     float gnew[kMaxPix / kKThreads];
