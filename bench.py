@@ -540,6 +540,8 @@ def main():
             "unit": "RK4 steps/s of the batch-4096 job" + (" (global batch split over GPUs)" if strong
                                                           else " (4096 per GPU, summed over GPUs)"),
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+            # a bench "step" is one 34-step odeint solve; per RK4 step of the batch:
+            "ms_per_rk4_step": ms_per_step / STEPS_PER_SOLVE,
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "fp32",
             "data": "synthetic (seeded y0, torch.manual_seed(0) weights; no dataset)",
             "config": {"workload": "LV KAN-FET NODE: KANFET[2,10,2] G=5 k=3 nb=10 K=10, rk4 (3/8), "
@@ -614,6 +616,7 @@ def main():
                                                        / e64.reshape(T, -1).norm(dim=1)).max().item(),
                 "robust_subset": robust,
                 "robust_subset_ok": P.robust_parity_ok(robust),
+                "robust_subset_at_1e-5_ok": P.robust_parity_at_tol_ref_ok(robust),
                 "note": "KAN-FET is ill-conditioned in fp32: the CPU reference's own fp32 solve departs from "
                         "fp64 by the per-slice error above, and which trajectories stay within 1e-5 depends on "
                         "the rounding; the 1e-5 bar is checked on the trajectories every equally valid "

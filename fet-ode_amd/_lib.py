@@ -76,6 +76,12 @@ class HLogisticDesc(ctypes.Structure):
                 ("gate_slope", ctypes.c_double), ("breaking_point", ctypes.c_double)]
 
 
+class KANRNNDesc(ctypes.Structure):
+    _fields_ = [("num_features", ctypes.c_int32), ("hidden", ctypes.c_int32), ("num_basis", ctypes.c_int32),
+                ("latent", ctypes.c_int32), ("ax", _fp), ("bx", _fp), ("ah", _fp), ("bh", _fp), ("w", _fp),
+                ("bias", _fp)]
+
+
 class FieldDesc(ctypes.Structure):
     _fields_ = [
         ("n_layers", ctypes.c_int32),
@@ -167,6 +173,17 @@ SIGNATURES = {
     "fetode_hlogistic_mixer_backward": (ctypes.c_int, [ctypes.POINTER(HLogisticDesc), _vp, ctypes.c_int64, _vp,
                                                        ctypes.c_int32, _vp, _vp, ctypes.c_int32, _vp, _vp, _vp, _vp,
                                                        _vp, _vp, _vp, _vp, _vp, _vp]),
+    "fetode_kanrnn_forward": (ctypes.c_int, [ctypes.POINTER(KANRNNDesc), _vp, ctypes.c_int64, ctypes.c_int32, _vp,
+                                             _vp, _vp, _vp, ctypes.c_int32, _vp]),
+    "fetode_kanrnn_depth": (ctypes.c_int32, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32]),
+    "fetode_kanrnn_backward_workspace": (ctypes.c_int64, [ctypes.POINTER(KANRNNDesc), ctypes.c_int64]),
+    "fetode_kanrnn_backward": (ctypes.c_int, [ctypes.POINTER(KANRNNDesc), _vp, ctypes.c_int64, ctypes.c_int32, _vp,
+                                              _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "fetode_logistic_basis_forward": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _vp, _vp,
+                                                     _vp, _vp]),
+    "fetode_logistic_basis_backward_workspace": (ctypes.c_int64, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64]),
+    "fetode_logistic_basis_backward": (ctypes.c_int, [_vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _vp, _vp,
+                                                      _vp, _vp, _vp, _vp, _vp, _vp]),
 }
 
 _lib: Optional[ctypes.CDLL] = None

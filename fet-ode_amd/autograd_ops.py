@@ -141,7 +141,7 @@ def kan_backward(mod, xc, grad, want_x, want_params, gx_accum=None):
 
 def kanlinear_apply(mod, x2d):
     if not grad_enabled_for(x2d, *[p for p in kan_params(mod) if p is not None]):
-        out = wide_apply(mod, None, x2d)   # production widths: the MFMA wide-layer kernel
+        out = wide_apply(mod, None, _lib.f32c(x2d))   # production widths: the MFMA wide-layer kernel
         if out is not None:
             return out
     return _KANLinearFn.apply(mod, x2d, *kan_params(mod))
@@ -466,7 +466,9 @@ def wide_plan(kan, fer, device):
 def wide_apply(kan, fer, x, reinit: bool = False):
     """out = KANLinear(x) + Ferro(x) (either may be None) through fetode_wide_layer_forward, or None
     if the layer has no wide kernel.  Reads the Ferro module's prev_x; the caller commits the new
-    state (ferro_class.py:409)."""
+    state (ferro_class.py:409).  The ABI takes a raw row-major pointer: x is made contiguous here
+    whatever the caller passed (a column slice or an expanded view would be read as wrong rows)."""
+    x = _lib.f32c(x)
     B = x.shape[0]
     dev = x.device
     if fer is not None:

@@ -142,3 +142,208 @@ class LatentNeuralODEForecaster(nn.Module):
             from .odeint import odeint
             zt = odeint(self.dynamics, z0, t_fut, rtol=self.rtol, atol=self.atol, method="dopri5")
         return self.decoder(zt).squeeze(-1).transpose(0, 1)
+
+
+# ---------------------------------------------------------------------------------------------
+# KAN-RNN encoder of KAN_FET_LatentODE_DiffusionForecaster (train_kan_fet_ett.py:741-818, used at
+# :832-837): LogisticBasis, LogisticBasisLinear, FullyNonlinearKANCell, KANRNNEncoder.  Same
+# constructor arguments, parameter names / shapes and init RNG order as the reference; the
+# recurrence runs in ONE HIP launch (fetode_kanrnn_forward, h on chip, to_latent fused) with a HIP
+# VJP (fetode_kanrnn_backward); LogisticBasis alone runs fetode_logistic_basis_*.
+# ---------------------------------------------------------------------------------------------
+
+def _stream(t):
+    return _lib.stream_handle(t.device)
+
+
+class _LogisticBasisFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, a, b):
+        xc = _lib.f32c(x)
+        B, n = xc.shape
+        nb = a.shape[1]
+        ac, bc = _lib.f32c(a), _lib.f32c(b)
+        phi = torch.empty(B, n, nb, device=x.device, dtype=torch.float32)
+        _lib.check(_lib.load().fetode_logistic_basis_forward(xc.data_ptr(), B, n, nb, ac.data_ptr(), bc.data_ptr(),
+                                                             phi.data_ptr(), _stream(x)), "LogisticBasis.forward")
+        ctx.save_for_backward(xc, ac, bc)
+        return phi
+
+    @staticmethod
+    def backward(ctx, g):
+        xc, ac, bc = ctx.saved_tensors
+        B, n = xc.shape
+        nb = ac.shape[1]
+        lib = _lib.load()
+        gx = torch.empty_like(xc) if ctx.needs_input_grad[0] else None
+        want_p = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        ga = torch.empty_like(ac) if want_p else None
+        gb = torch.empty_like(bc) if want_p else None
+        ws = None
+        if want_p:
+            ws = torch.empty(max(1, lib.fetode_logistic_basis_backward_workspace(n, nb, B) // 4), device=xc.device)
+        _lib.check(lib.fetode_logistic_basis_backward(xc.data_ptr(), B, n, nb, ac.data_ptr(), bc.data_ptr(),
+                                                      _lib.f32c(g).data_ptr(), _lib.ptr(gx), _lib.ptr(ga), _lib.ptr(gb),
+                                                      _lib.ptr(ws), _stream(xc)), "LogisticBasis backward")
+        return gx, ga, gb
+
+
+class LogisticBasis(nn.Module):
+    """train_kan_fet_ett.py:741-749: phi = 2 / (1 + exp(-a (x - b))), x (B, in) -> (B, in, nb)."""
+
+    def __init__(self, in_dim, num_basis):
+        super().__init__()
+        self.a = nn.Parameter(torch.randn(in_dim, num_basis))
+        self.b = nn.Parameter(torch.randn(in_dim, num_basis))
+
+    def forward(self, x):
+        _lib.require_gpu_tensor(x, "LogisticBasis.forward")
+        if x.dim() != 2 or x.shape[1] != self.a.shape[0]:
+            raise ValueError(f"LogisticBasis expects x of shape (B, {self.a.shape[0]}), got {tuple(x.shape)}")
+        return _LogisticBasisFn.apply(x, self.a, self.b)
+
+
+class LogisticBasisLinear(nn.Module):
+    """train_kan_fet_ett.py:753-776: logistic basis expansion, then phi @ weight + bias (the
+    contraction is a plain library GEMM through torch)."""
+
+    def __init__(self, in_dim: int, out_dim: int, num_basis: int, bias: bool = True):
+        super().__init__()
+        self.in_dim = in_dim
+        self.out_dim = out_dim
+        self.num_basis = num_basis
+        self.basis = LogisticBasis(in_dim, num_basis)
+        self.weight = nn.Parameter(torch.randn(in_dim * num_basis, out_dim) * 0.02)
+        self.bias = nn.Parameter(torch.zeros(out_dim)) if bias else None
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        phi = self.basis(x).reshape(x.shape[0], -1)
+        y = phi @ self.weight
+        if self.bias is not None:
+            y = y + self.bias
+        return y
+
+
+def _rnn_desc(cell, lin, keep):
+    ps = [_lib.f32c(p) for p in (cell.input_basis.a, cell.input_basis.b, cell.hidden_basis.a, cell.hidden_basis.b)]
+    w = b = None
+    latent = 0
+    if lin is not None:
+        w, b = _lib.f32c(lin.weight), _lib.f32c(lin.bias) if lin.bias is not None else None
+        latent = w.shape[0]
+        if b is None:
+            b = torch.zeros(latent, device=w.device)
+    keep += ps + [w, b]
+    F_, nb = ps[0].shape
+    H = ps[2].shape[0]
+    return _lib.KANRNNDesc(F_, H, nb, latent, *(t.data_ptr() for t in ps), _lib.ptr(w), _lib.ptr(b))
+
+
+def _fused_projection(lin, H) -> bool:
+    """to_latent inside the recurrence launch (W^T in LDS) when it fits."""
+    return lin is not None and lin.weight.shape[0] <= 256 and lin.weight.shape[0] * H <= 16384
+
+
+class _KANRNNFn(torch.autograd.Function):
+    """h_T of the recurrence (and z0 = to_latent(h_T) when `lin` is given and fits the launch)."""
+
+    @staticmethod
+    def forward(ctx, cell, lin, x, h0, ax, bx, ah, bh, w, bias):
+        keep = []
+        fuse = _fused_projection(lin, cell.hidden_size)
+        d = _rnn_desc(cell, lin if fuse else None, keep)
+        xc = _lib.f32c(x)
+        B, T, _ = xc.shape
+        H = cell.hidden_size
+        h0c = _lib.f32c(h0) if h0 is not None else None
+        grad = any(ctx.needs_input_grad[2:])
+        tape = torch.empty(B, T, H, device=x.device) if grad else None
+        hT = torch.empty(B, H, device=x.device) if (grad or not fuse) else None
+        z0 = torch.empty(B, d.latent, device=x.device) if fuse else None
+        _lib.check(_lib.load().fetode_kanrnn_forward(ctypes_byref(d), xc.data_ptr(), B, T, _lib.ptr(h0c), _lib.ptr(hT),
+                                                     _lib.ptr(z0), _lib.ptr(tape), 0, _stream(x)), "KAN-RNN forward")
+        ctx.cell, ctx.lin, ctx.fuse = cell, lin, fuse
+        ctx.save_for_backward(xc, h0c, tape, hT)
+        if lin is not None and not fuse:
+            return torch.nn.functional.linear(hT, lin.weight, lin.bias)
+        return z0 if fuse else hT
+
+    @staticmethod
+    def backward(ctx, g):
+        xc, h0c, tape, hT = ctx.saved_tensors
+        cell, lin = ctx.cell, ctx.lin
+        B, T, _ = xc.shape
+        g = _lib.f32c(g)
+        gw = gbias = None
+        if lin is not None:
+            w = lin.weight.detach()
+            if ctx.needs_input_grad[8]:
+                gw = g.t() @ hT
+            if ctx.needs_input_grad[9]:
+                gbias = g.sum(0)
+            g_h = (g @ w).contiguous()
+        else:
+            g_h = g
+        keep = []
+        d = _rnn_desc(cell, None, keep)
+        lib = _lib.load()
+        gx = torch.empty_like(xc) if ctx.needs_input_grad[2] else None
+        gh0 = torch.empty_like(h0c) if (h0c is not None and ctx.needs_input_grad[3]) else None
+        want_p = any(ctx.needs_input_grad[4:8])
+        gp = [torch.empty_like(p) for p in (cell.input_basis.a, cell.input_basis.b, cell.hidden_basis.a,
+                                            cell.hidden_basis.b)] if want_p else [None] * 4
+        ws = torch.empty(max(1, lib.fetode_kanrnn_backward_workspace(ctypes_byref(d), B) // 4), device=xc.device)
+        _lib.check(lib.fetode_kanrnn_backward(ctypes_byref(d), xc.data_ptr(), B, T, _lib.ptr(h0c), tape.data_ptr(),
+                                              g_h.data_ptr(), _lib.ptr(gx), _lib.ptr(gh0), *(_lib.ptr(t) for t in gp),
+                                              ws.data_ptr(), _stream(xc)), "KAN-RNN backward")
+        return (None, None, gx, gh0, *gp, gw, gbias)
+
+
+def ctypes_byref(d):
+    return _lib.ctypes.byref(d)
+
+
+def kanrnn_apply(cell, x, h0=None, lin=None):
+    """h_T (or to_latent(h_T)) of FullyNonlinearKANCell run over x (B, T, F) from h0 (None = zeros)."""
+    _lib.require_gpu_tensor(x, "KAN-RNN")
+    params = (cell.input_basis.a, cell.input_basis.b, cell.hidden_basis.a, cell.hidden_basis.b)
+    w = lin.weight if lin is not None else None
+    bias = lin.bias if lin is not None else None
+    return _KANRNNFn.apply(cell, lin, x, h0, *params, w, bias)
+
+
+class FullyNonlinearKANCell(nn.Module):
+    """train_kan_fet_ett.py:780-795: h = sigmoid(cat(phi_x(x_t), phi_h(h_prev)))[:, :hidden_size]."""
+
+    def __init__(self, input_size, hidden_size, num_basis):
+        super().__init__()
+        self.input_basis = LogisticBasis(input_size, num_basis)
+        self.hidden_basis = LogisticBasis(hidden_size, num_basis)
+        self.activation = nn.Sigmoid()
+        self.hidden_size = hidden_size
+        self.num_basis = num_basis
+
+    def forward(self, x_t, h_prev):
+        if x_t.dim() != 2 or h_prev.dim() != 2 or h_prev.shape[1] != self.hidden_size:
+            raise ValueError("FullyNonlinearKANCell expects x_t (B, input_size) and h_prev (B, hidden_size)")
+        _lib.require_gpu_tensor(h_prev, "FullyNonlinearKANCell.forward")
+        return kanrnn_apply(self, x_t.unsqueeze(1), h_prev)
+
+
+class KANRNNEncoder(nn.Module):
+    """train_kan_fet_ett.py:798-818: the cell over the context from h = 0, then to_latent(h_T).
+    The whole recurrence + projection is one launch."""
+
+    def __init__(self, num_features: int, hidden_size: int, latent_dim: int, num_basis: int):
+        super().__init__()
+        self.hidden_size = hidden_size
+        self.rnn_cell = FullyNonlinearKANCell(num_features, hidden_size, num_basis)
+        self.to_latent = nn.Linear(hidden_size, latent_dim)
+
+    def forward(self, x_ctx: torch.Tensor) -> torch.Tensor:
+        B, T, F_ = x_ctx.shape
+        if T == 0:
+            _lib.require_gpu_tensor(x_ctx, "KANRNNEncoder.forward")
+            h = torch.zeros(B, self.hidden_size, device=x_ctx.device, dtype=x_ctx.dtype)
+            return self.to_latent(h)
+        return kanrnn_apply(self.rnn_cell, x_ctx, None, self.to_latent)

@@ -516,7 +516,13 @@ def _per_stage_fixed(func, y0, sched: Schedule, method: str, tc_dtype, reversed_
 # ---------------------------------------------------------------------------------------------
 
 _LAST_T = [None, None, None, None]   # the last t tensor, its version, method, checked inputs
-atexit.register(lambda: _LAST_T.__setitem__(slice(None), [None] * 4))   # before the runtime's teardown
+
+
+def _clear_last_t():
+    _LAST_T[:] = [None] * 4
+
+
+atexit.register(_clear_last_t)   # before the runtime's teardown
 
 
 def _check_inputs_cached(y0, t, method):

@@ -380,6 +380,49 @@ int64_t fetode_kanlinear_wide_workspace(const fetode_kanlinear_t* layer, int64_t
 int fetode_kanlinear_wide_forward(const fetode_kanlinear_t* layer, const float* wpack, const float* bias, const float* x,
                                   int64_t B, float* out, void* workspace, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * ETT KAN-RNN encoder (train_kan_fet_ett.py:741-818; the encoder of
+ * KAN_FET_LatentODE_DiffusionForecaster, :822-837).  One cell step (FullyNonlinearKANCell.forward,
+ * :790-795) is h_t = sigmoid(cat(phi_x(x_t), phi_h(h_{t-1})))[:, :H] with
+ * phi(v)[i, k] = 2 / (1 + exp(-a[i,k] (v[i] - b[i,k]))) (LogisticBasis.forward, :747-749);
+ * KANRNNEncoder.forward (:809-818) runs the cell over the context from h = 0 and projects
+ * z0 = to_latent(h_T).  (dev) pointers: ax, bx (F, nb); ah, bh (H, nb); w (latent, H); bias (latent).
+ * -------------------------------------------------------------------------------------------- */
+typedef struct fetode_kanrnn {
+  int32_t num_features, hidden, num_basis, latent; /* latent = 0: no projection */
+  const float *ax, *bx, *ah, *bh;                  /* rnn_cell.{input,hidden}_basis.{a,b} */
+  const float *w, *bias;                           /* to_latent.weight / .bias (NULL if latent = 0) */
+} fetode_kanrnn_t;
+
+/* h_T of the recurrence over x (B, T, F) from h0 (B, H) (NULL = zeros) in ONE launch, h on chip.
+ * h_out (B, H) (nullable), z0 (B, latent) = to_latent(h_T) (nullable; needs latent*H <= 16384).
+ * tape (B, T, H) (nullable): every h_t, for fetode_kanrnn_backward; a tape forces the full
+ * recurrence.  full = 0 evaluates only the steps whose outputs can reach h_T: column j of h_t reads
+ * h_{t-1} only through column (j - F nb) / nb (the truncated cat), so every dependency chain is at
+ * most depth(H, F, nb) steps long (exact, NaN included).  H <= 256, F <= 64. */
+int fetode_kanrnn_forward(const fetode_kanrnn_t* m, const float* x, int64_t B, int32_t T, const float* h0,
+                          float* h_out, float* z0, float* tape, int32_t full, void* stream);
+/* the number of steps before h_T that can influence it (the cone depth) */
+int32_t fetode_kanrnn_depth(int32_t num_features, int32_t hidden, int32_t num_basis);
+/* VJP of the recurrence with the reference autograd's IEEE semantics (a dropped column's zero
+ * gradient times an overflowing exp is NaN, as torch computes it).  g_h (B, H) = d loss / d h_T;
+ * tape from fetode_kanrnn_forward; outputs (nullable): g_x (B, T, F), g_h0 (B, H), and the parameter
+ * gradients g_ax, g_bx (F, nb), g_ah, g_bh (H, nb) (overwritten, reduced in a fixed order: run-to-run
+ * identical).  workspace: fetode_kanrnn_backward_workspace(m, B) bytes. */
+int64_t fetode_kanrnn_backward_workspace(const fetode_kanrnn_t* m, int64_t B);
+int fetode_kanrnn_backward(const fetode_kanrnn_t* m, const float* x, int64_t B, int32_t T, const float* h0,
+                           const float* tape, const float* g_h, float* g_x, float* g_h0, float* g_ax, float* g_bx,
+                           float* g_ah, float* g_bh, void* workspace, void* stream);
+/* LogisticBasis.forward (:747-749) alone: x (B, in) -> phi (B, in, nb), and its VJP
+ * (g_x (B, in), g_a, g_b (in, nb); nullable; g_a / g_b reduced over the batch in a fixed order;
+ * workspace fetode_logistic_basis_backward_workspace(in, nb, B) bytes). */
+int fetode_logistic_basis_forward(const float* x, int64_t B, int32_t in, int32_t nb, const float* a, const float* b,
+                                  float* phi, void* stream);
+int64_t fetode_logistic_basis_backward_workspace(int32_t in, int32_t nb, int64_t B);
+int fetode_logistic_basis_backward(const float* x, int64_t B, int32_t in, int32_t nb, const float* a,
+                                   const float* b, const float* g_phi, float* g_x, float* g_a, float* g_b,
+                                   void* workspace, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -53,14 +53,23 @@ def robust_parity(gpu: torch.Tensor, e32: torch.Tensor, e64: torch.Tensor, envel
         "n": int(robust.numel()), "n_robust": int(robust.sum()),
         "gpu_max_vs_ref_on_robust": float(g_ref.max()) if g_ref.numel() else 0.0,
         "gpu_n_over_tol_on_robust": int((g_ref > tol_gpu).sum()),
+        # at the north-star bar itself (1e-5 = tol_ref), next to the same count for the controls
+        "gpu_n_over_tol_ref_on_robust": int((g_ref > tol_ref).sum()),
         "gpu_frac_within_tol_on_robust": float((g_ref <= tol_gpu).double().mean()) if g_ref.numel() else 1.0,
         "control_max_vs_ref_on_robust": [float(c.max()) if c.numel() else 0.0 for c in c_ref],
         "control_n_over_tol_on_robust": [int((c > tol_gpu).sum()) for c in c_ref],
+        "control_n_over_tol_ref_on_robust": [int((c > tol_ref).sum()) for c in c_ref],
         "gpu_well_frac": float((traj_err(gpu, e64) <= tol_ref).double().mean()),
         "ref_well_frac_spread": [min(fr), max(fr)],
         "ref_well_frac": fr[0],
         "tol_ref": tol_ref, "tol_gpu": tol_gpu,
     }
+
+
+def robust_parity_at_tol_ref_ok(st: Dict) -> bool:
+    """The north-star 1e-5 count: on the robust subset no more GPU trajectories leave 1e-5 of the
+    reference fp32 solve than the worst independent re-rounding of the reference itself."""
+    return st["gpu_n_over_tol_ref_on_robust"] <= max(st["control_n_over_tol_ref_on_robust"] or [0])
 
 
 def robust_parity_ok(st: Dict) -> bool:

@@ -390,6 +390,9 @@ def test_fused_rk4_kanfet_robust_subset_bench_config(dev):
     print("robust-subset parity (bench config):", st)
     assert st["n_robust"] >= 256, st
     assert P.robust_parity_ok(st), st
+    # north-star 1e-5 itself: no more GPU trajectories beyond it than the worst re-rounded reference
+    # (round 3 measurement: GPU 29, controls 36 / 40 of 978)
+    assert P.robust_parity_at_tol_ref_ok(st), st
 
 
 @pytest.mark.parametrize("B", [1, 7, 64, 512])

@@ -197,3 +197,54 @@ def test_wide_ferro_autograd_sequence_and_grads(dev, i, o):
         g = getattr(m, n).grad.cpu()
         err = (g - r.grad).abs().max().item()
         assert err <= 2e-4 * r.grad.abs().max().item() + 1e-7, (n, err)
+
+
+# ---------------------------------------------------------------------------------------------
+# the ETT bench batch itself (B = 8192): layer 0 (64 -> 128) launches 1 024 tiles and takes the
+# nslice = 1 branch of wide_layer_kernel<10, true, true, 8> (fetode_wide.hip wide_layer_forward);
+# layer 1 (128 -> 64) has 512 tiles and takes nslice = 2.  The oracle runs on a subset of rows
+# (rows are independent given their own prev_x; a subset of B > 1 rows keeps the first-call rule).
+# ---------------------------------------------------------------------------------------------
+
+def test_wide_kanfet_field_b8192_both_slice_branches(dev):
+    """KANFET([64, 128, 64], K = 10) at B = 8192, three stateful evaluations, with |gs x| > 80
+    rows and |gs Ec| > 80 parameters in both layers: 1e-5 per row against the fp32 oracle on 640
+    rows (the wild rows, rows at both ends of every 64-row tile, and a random sample)."""
+    torch.manual_seed(81)
+    m = F.KANFET([64, 128, 64], grid_size=5, num_fet_basis=10)
+    with torch.no_grad():
+        for fer in (m.layers[0].ferro, m.layers[1].ferro):
+            fer.Ec[0, :, 0] = 9.5
+            fer.Ec[1, :, 1] = -9.0
+            fer.Ec[2, 3, :] = -0.3
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    B = 8192
+    wild = (5, 63, 64, 4095, 4096, 8191)
+    g = torch.Generator().manual_seed(82)
+    rows = torch.cat([torch.tensor(wild), torch.arange(0, B, 64), torch.arange(63, B, 64),
+                      torch.randperm(B, generator=g)[:256]]).unique()
+    ref = O.KANFETRef.from_state_dict(sd, 2)
+    for call in range(3):
+        x = _x(B, 64, seed=8192 + call, wild_rows=wild if call != 1 else ()) * (1.0 + 0.1 * call)
+        with torch.no_grad():
+            got = m(x.to(dev))
+        exp = ref(x[rows])
+        assert torch.isfinite(got).all()
+        err = row_rel(got.cpu()[rows], exp)
+        assert err <= 1e-5, (call, err)
+        assert torch.equal(m.layers[0].ferro.prev_x[:, :, 0, 0].cpu(), x)
+
+
+def test_wide_kanlinear_noncontiguous_input(dev):
+    """A column slice of a wider tensor (non-contiguous 2-D view) into a 64 -> 128 KANLinear under
+    no_grad (the MFMA wide-layer path) gives the same rows as the autograd path."""
+    torch.manual_seed(3)
+    m = F.KANLinear(64, 128).to(dev)
+    big = _x(1000, 96, seed=4).to(dev)
+    xs = big[:, 16:80]
+    assert not xs.is_contiguous()
+    with torch.no_grad():
+        got = m(xs)
+    exp = m(xs.clone().requires_grad_(True)).detach()
+    assert row_rel(got, exp) <= 1e-5, row_rel(got, exp)
