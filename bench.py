@@ -402,6 +402,102 @@ def ett_rate(dev, batch=8192, reps=2, substeps=4, cpu_seconds=5.0, with_cpu=True
     return out
 
 
+def ett_encoder_rate(dev, batch=8192, ctx=96, reps=20, with_cpu=True, cpu_seconds=5.0):
+    """The encoder of the reference's KAN-FET ETT model (KAN_FET_LatentODE_DiffusionForecaster,
+    train_kan_fet_ett.py:822-837): KANRNNEncoder(7 features, hidden 64, latent 64, 10 bases) over
+    96-step contexts (:798-818), B = 8192 windows of a synthetic series.  Forward (no_grad: one
+    launch; only the steps that can reach h_T run), the full 96-step recurrence
+    (the same launch with full = 1), and a training step (forward with tape + HIP VJP + the
+    to_latent GEMMs)."""
+    from fet_ode_amd import ett, _lib as L
+    from oracle import ett_ref as E
+    torch.manual_seed(0)
+    enc = ett.KANRNNEncoder(7, 64, 64, 10)
+    sd = {k: v.clone() for k, v in enc.state_dict().items()}
+    enc = enc.to(dev)
+    g = torch.Generator().manual_seed(6)
+    series = torch.cumsum(torch.randn(batch + ctx, 7, generator=g), 0) * 0.05
+    x = series.unfold(0, ctx, 1)[:batch].transpose(1, 2).contiguous()      # (B, 96, 7) windows
+    xd = x.to(dev)
+    lib = L.load()
+    keep = []
+    d = ett._rnn_desc(enc.rnn_cell, enc.to_latent, keep)
+    z0 = torch.empty(batch, 64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def launch(full):
+        L.check(lib.fetode_kanrnn_forward(L.ctypes.byref(d), xd.data_ptr(), batch, ctx, None, None, z0.data_ptr(),
+                                          None, full, stream.cuda_stream), "kanrnn")
+
+    def ev_time(fn, n):
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize(dev)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(n):
+            fn()
+        b.record(stream)
+        torch.cuda.synchronize(dev)
+        return a.elapsed_time(b) / n
+
+    k_cone = ev_time(lambda: launch(0), reps)
+    k_full = ev_time(lambda: launch(1), reps)
+    with torch.no_grad():
+        for _ in range(2):
+            enc(xd)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            enc(xd)
+        torch.cuda.synchronize(dev)
+        fwd = (time.perf_counter() - t0) / reps
+    gz = torch.randn(batch, 64, device=dev)
+
+    def step():
+        enc.zero_grad(set_to_none=True)
+        enc(xd).backward(gz)
+
+    for _ in range(2):
+        step()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        step()
+    torch.cuda.synchronize(dev)
+    trn = (time.perf_counter() - t0) / reps
+    depth = lib.fetode_kanrnn_depth(7, 64, 10)
+    # algorithmic bytes: the cone reads x of the last depth+1 steps (7 floats each) and writes z0;
+    # the full recurrence reads the whole context
+    cone_bytes = batch * 4 * ((depth + 1) * 7 + 64)
+    full_bytes = batch * 4 * (ctx * 7 + 64)
+    out = {"value": batch / fwd, "unit": "windows/s encoded (KANRNNEncoder forward, 1 GPU)", "ms_per_batch": fwd * 1e3,
+           "kernel_ms_cone": k_cone, "kernel_ms_full_recurrence": k_full, "cone_depth": depth,
+           "full_recurrence_windows_per_s": batch / (k_full * 1e-3),
+           "train_windows_per_s": batch / trn, "train_ms_per_batch": trn * 1e3,
+           "roofline_full": {"bound": "transcendental (4 exp/rcp per hidden unit per step)",
+                             "alg_bytes": full_bytes, "achieved_GBs": full_bytes / (k_full * 1e-3) / 1e9},
+           "roofline_cone": {"alg_bytes": cone_bytes, "achieved_GBs": cone_bytes / (k_cone * 1e-3) / 1e9},
+           "workload": f"KANRNNEncoder(7, hidden 64, latent 64, nb 10), context {ctx}, batch {batch}, synthetic series",
+           "path": "fetode_kanrnn_forward (one launch, to_latent fused) / fetode_kanrnn_backward"}
+    if with_cpu:
+        cores, _ = cpu_cores()
+        torch.set_num_threads(cores)
+        ref = E.KANRNNEncoderRef(sd)
+        xs = x[:1024]
+        n, t0 = 0, time.perf_counter()
+        with torch.no_grad():
+            while n < 1 or (time.perf_counter() - t0 < cpu_seconds and n < 20):
+                ref(xs)
+                n += 1
+        cel = (time.perf_counter() - t0) / n
+        out["cpu_baseline"] = {"value": 1024 / cel, "unit": "windows/s encoded (CPU)", "cores": cores, "kind": "port",
+                               "sample": f"{n} forward(s) of 1024 of the windows with oracle/ett_ref.py "
+                                         f"KANRNNEncoderRef (reference op order, all 96 steps, torch CPU fp32), "
+                                         f"{cel * n:.1f} s"}
+    return out
+
+
 def cpu_cores():
     """(threads used, physical cores of this host from lscpu).  The threads are the physical cores,
     capped at the process's CPU share (OMP_NUM_THREADS; 16 per GPU on the GPU box)."""
@@ -582,6 +678,7 @@ def main():
             out["mnist"] = mnist_rate(dev, with_cpu=not args.no_cpu_baseline)
         if world == 1 and not args.no_ett:
             out["ett"] = ett_rate(dev, batch=args.ett_batch, with_cpu=not args.no_cpu_baseline)
+            out["ett"]["encoder"] = ett_encoder_rate(dev, with_cpu=not args.no_cpu_baseline)
         if world == 1 and not args.no_cpu_baseline:
             cb, ref_sol = cpu_baseline(sd, y0, t, args.cpu_solves)
             out["cpu_baseline"] = cb

@@ -94,6 +94,7 @@ class FieldDesc(ctypes.Structure):
 SIGNATURES = {
     "fetode_last_error": (ctypes.c_char_p, []),
     "fetode_abi_version": (ctypes.c_int, []),
+    "fetode_resident_launch_mode": (ctypes.c_int32, [ctypes.c_int32]),
     "fetode_plan_bytes": (ctypes.c_int64, [ctypes.POINTER(FieldDesc)]),
     "fetode_plan_build": (ctypes.c_int, [ctypes.POINTER(FieldDesc), _vp, _vp]),
     "fetode_state_width": (ctypes.c_int32, [ctypes.POINTER(FieldDesc)]),

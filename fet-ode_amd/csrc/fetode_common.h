@@ -50,6 +50,14 @@ struct LayerPlan {
 void layer_plan(const fetode_kanlinear_t& kl, const fetode_ferro_t* fl, int64_t base, LayerPlan* p);
 int validate_field(const fetode_field_t* f);
 
+// Launch of a grid that must be co-resident (the device-resident solvers' grid reductions).  The
+// callers size the grid by occupancy; by default it is an ordinary launch (bounded spins turn a
+// grid that is not co-resident into status 4), or hipLaunchCooperativeKernel when switched on
+// (fetode_resident_launch_mode(1), env FETODE_COOPERATIVE=1).
+hipError_t resident_launch(const void* fn, dim3 grid, dim3 block, void** args, size_t lds, hipStream_t s);
+int resident_mode();
+extern int g_resident_mode;
+
 // The factored gate exp(gs(x+Ec)) = exp(gs x) * exp(gs Ec) is used only when
 // |gs*log2e*Ec| <= kFactorLimit everywhere in the layer: then exp(gs x) overflowing /
 // underflowing can only happen where the fp32 sigmoid is already saturated at 0 / 1.

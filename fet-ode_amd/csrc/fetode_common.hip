@@ -2,6 +2,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -10,6 +11,21 @@
 namespace fetode {
 
 static thread_local std::string g_last_error;
+
+// -1: not yet read from the environment
+int g_resident_mode = -1;
+int resident_mode() {
+  if (g_resident_mode < 0) {
+    const char* v = getenv("FETODE_COOPERATIVE");
+    g_resident_mode = v && atoi(v) != 0;
+  }
+  return g_resident_mode;
+}
+
+hipError_t resident_launch(const void* fn, dim3 grid, dim3 block, void** args, size_t lds, hipStream_t s) {
+  if (resident_mode()) return hipLaunchCooperativeKernel(fn, grid, block, args, (unsigned)lds, s);
+  return hipLaunchKernel(fn, grid, block, args, lds, s);
+}
 
 int set_err(int code, const char* fmt, ...) {
   char buf[512];
@@ -255,6 +271,12 @@ using namespace fetode;
 extern "C" {
 
 const char* fetode_last_error(void) { return g_last_error.c_str(); }
+
+int32_t fetode_resident_launch_mode(int32_t mode) {
+  const int32_t prev = fetode::resident_mode();
+  if (mode >= 0) fetode::g_resident_mode = mode != 0;
+  return prev;
+}
 int fetode_abi_version(void) { return FETODE_ABI_VERSION; }
 
 int32_t fetode_state_width(const fetode_field_t* f) {

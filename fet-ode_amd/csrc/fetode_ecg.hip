@@ -903,7 +903,7 @@ int fetode_ecg_dopri5(const fetode_hlogistic_t* layer, const float* wT, const fl
     hipStream_t s = (hipStream_t)stream;
     HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kBarWords, s));
     void* args[] = {&a};
-    HIP_CHECK_RET(hipLaunchCooperativeKernel(v.fn, dim3((unsigned)grid), dim3(kResThreads), args, (unsigned)lds, s));
+    HIP_CHECK_RET(resident_launch(v.fn, dim3((unsigned)grid), dim3(kResThreads), args, lds, s));
     return FETODE_OK;
   }
   return set_err(FETODE_EUNSUPPORTED, "ecg dopri5: batch %lld x in*num_basis %d does not fit one resident grid",

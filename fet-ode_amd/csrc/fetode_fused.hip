@@ -1477,7 +1477,7 @@ int fetode_integrate_dopri5(const fetode_field_t* f, const void* plan, const flo
   hipStream_t s = (hipStream_t)stream;
   HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kDpBarWords, s));
   void* args[] = {&a};
-  HIP_CHECK_RET(hipLaunchCooperativeKernel((const void*)e->dopri, dim3((unsigned)grid), dim3(64), args, 0, s));
+  HIP_CHECK_RET(resident_launch((const void*)e->dopri, dim3((unsigned)grid), dim3(64), args, 0, s));
   return FETODE_OK;
 }
 

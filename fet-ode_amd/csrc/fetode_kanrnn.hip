@@ -29,6 +29,7 @@ constexpr int kMaxF = 64;         // input features
 constexpr int kMaxQ = 2048;       // combined basis columns (F + H) * nb, 32 per lane
 constexpr int kMaxW = 16384;      // latent * H floats of W^T in LDS (64 KiB)
 constexpr int kBwdWaves = 4096;   // waves of the backward (rows are strided over them)
+constexpr int kFwdGroups = 1024;  // forward workgroups (4 waves each)
 constexpr int kRedChunks = 32;    // first-pass chunks of the fixed-order partial reduction
 // expf(z) is finite iff z <= 88.72283172607421875f (the next float, 0x42B17218, overflows)
 constexpr float kExpFinite = 88.72283172607421875f;
@@ -97,8 +98,7 @@ __global__ __launch_bounds__(256) void kanrnn_fwd_kernel(RnnArgs a) {
     na[m] = 0.f, bb[m] = 0.f, src[m] = 0, isx[m] = true;
     if (c < a.H) col_params(a, c, na[m], bb[m], src[m], isx[m]);
   }
-  const int64_t row = (int64_t)blockIdx.x * kWaves + wv;
-  if (row >= a.B) return;
+  for (int64_t row = (int64_t)blockIdx.x * kWaves + wv; row < a.B; row += (int64_t)gridDim.x * kWaves) {
   // h_{t_first - 1}: h0 when the cone reaches the start, else anything (no chain reads it)
 #pragma unroll
   for (int m = 0; m < MC; ++m) {
@@ -141,6 +141,8 @@ __global__ __launch_bounds__(256) void kanrnn_fwd_kernel(RnnArgs a) {
       a.z0[row * a.latent + o] = acc + a.bias[o];
     }
   }
+  wsync();   // the next row overwrites this wave's LDS slots
+  }
 }
 
 struct BwdArgs {
@@ -152,31 +154,29 @@ struct BwdArgs {
   int n_waves;
 };
 
-template <int MQ>
+template <int MQ, int MCL>   // MQ column slots per lane (Q <= 64 MQ), MCL of them can be live (H <= 64 MCL)
 __global__ __launch_bounds__(256) void kanrnn_bwd_kernel(BwdArgs A) {
   const RnnArgs& a = A.f;
-  __shared__ float s_x[kWaves][kMaxF];
-  __shared__ float s_hp[kWaves][kMaxH];          // h_{t-1}
-  __shared__ float s_cg[kWaves][kMaxH];          // d loss / d (v - b) of the live columns
-  __shared__ float s_gn[kWaves][kMaxH];          // d loss / d h_{t-1}
-  __shared__ int s_bad[kWaves][kMaxF + kMaxH];   // a dropped column of this input gave NaN
+  constexpr int kIn = kMaxF + kMaxH;              // staged inputs: x_t at [0, F), h_{t-1} at [kMaxF, kMaxF + H)
+  __shared__ float s_in[kWaves][kIn];
+  __shared__ float s_cg[kWaves][kMaxH + 16];      // d loss / d (v - b) of the live columns (+ read padding)
+  __shared__ float s_gn[kWaves][kMaxH];           // d loss / d h_{t-1}
+  __shared__ int s_bad[kWaves][kIn];              // a dropped column reading this input gave NaN
+  extern __shared__ float4 s_par[];               // per combined column {-a, b, input slot, 0}
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int gw = blockIdx.x * kWaves + wv;
-  constexpr int MCL = (MQ < 4 ? MQ : 4);          // slots that can hold live columns (H <= 256)
-  float na[MQ], bb[MQ], ga[MQ], gb[MQ];
-  int info[MQ];
-#pragma unroll
-  for (int m = 0; m < MQ; ++m) {
-    const int c = lane + 64 * m;
-    na[m] = 0.f, bb[m] = 0.f, ga[m] = 0.f, gb[m] = 0.f, info[m] = 0;
-    if (c < a.Q) {
-      int src;
-      bool isx;
-      col_params(a, c, na[m], bb[m], src, isx);
-      info[m] = isx ? src : kMaxF + src;   // index into s_bad / the staged inputs
-    }
+  for (int c = threadIdx.x; c < a.Q; c += blockDim.x) {
+    float na, b;
+    int src;
+    bool isx;
+    col_params(a, c, na, b, src, isx);
+    s_par[c] = make_float4(na, b, __int_as_float(isx ? src : kMaxF + src), 0.0f);
   }
-  const int NU = a.F + a.H;
+  __syncthreads();
+  float ga[MQ], gb[MQ];
+#pragma unroll
+  for (int m = 0; m < MQ; ++m) ga[m] = 0.f, gb[m] = 0.f;
+  const int NU = a.F + a.H;   // inputs: x_t (F) and h_{t-1} (H)
   for (int64_t row = gw; row < a.B; row += A.n_waves) {
     const float* xr = a.x + row * (int64_t)a.T * a.F;
     const float* tr = A.f.tape + row * (int64_t)a.T * a.H;
@@ -203,9 +203,9 @@ __global__ __launch_bounds__(256) void kanrnn_bwd_kernel(BwdArgs A) {
 #pragma unroll
       for (int m = 0; m < MCL; ++m) {
         const int c = lane + 64 * m;
-        if (c < a.H) s_hp[wv][c] = hp[m];
+        if (c < a.H) s_in[wv][kMaxF + c] = hp[m];
       }
-      if (lane < a.F) s_x[wv][lane] = xv;
+      if (lane < a.F) s_in[wv][lane] = xv;
       for (int u = lane; u < NU; u += 64) s_bad[wv][u < a.F ? u : kMaxF + u - a.F] = 0;
       float hpn[MCL], xn = 0.0f;
       if (t > 0) {
@@ -217,24 +217,25 @@ __global__ __launch_bounds__(256) void kanrnn_bwd_kernel(BwdArgs A) {
       for (int m = 0; m < MQ; ++m) {
         const int c = lane + 64 * m;
         if (c >= a.Q) continue;
-        const int u = info[m];
-        const float v = u < kMaxF ? s_x[wv][u] : s_hp[wv][u - kMaxF];
+        const float4 pc = s_par[c];
+        const int u = __float_as_int(pc.z);
+        const float v = s_in[wv][u];
         if (m < MCL && c < a.H) {
           // live column: torch's autograd of sigmoid(reciprocal(1 + exp(na * (v - b))) * 2)
           float e, r, d1;
-          basis_col(v, na[m], bb[m], e, r, d1);
-          const float s = sv[m < MCL ? m : 0];
-          const float gphi = g[m < MCL ? m : 0] * (1.0f - s) * s;   // sigmoid_backward
+          basis_col(v, pc.x, pc.y, e, r, d1);
+          const float sg = sv[m < MCL ? m : 0];
+          const float gphi = g[m < MCL ? m : 0] * (1.0f - sg) * sg;   // sigmoid_backward
           const float gr = gphi * 2.0f;
-          const float gden = -gr * (r * r);                          // reciprocal backward
-          const float gz = gden * e;                                 // exp backward
-          const float gna = gz * d1, gd1 = gz * na[m];
-          ga[m] += -gna;                                             // neg backward
-          gb[m] += -gd1;                                             // sub backward (other)
+          const float gden = -gr * (r * r);                            // reciprocal backward
+          const float gz = gden * e;                                   // exp backward
+          const float gna = gz * d1, gd1 = gz * pc.x;
+          ga[m] += -gna;                                               // neg backward
+          gb[m] += -gd1;                                               // sub backward (other)
           s_cg[wv][c] = gd1;
         } else {
           // dropped column: zero gradient; NaN iff exp(z) is not finite
-          const float z = na[m] * (v - bb[m]);
+          const float z = pc.x * (v - pc.y);
           if (!(z <= kExpFinite)) {
             const float qnan = __builtin_nanf("");
             ga[m] += qnan;
@@ -244,13 +245,27 @@ __global__ __launch_bounds__(256) void kanrnn_bwd_kernel(BwdArgs A) {
         }
       }
       wsync();
-      // d loss / d v per input: the live columns of input u in k order (+ NaN from a dropped one)
+      // d loss / d v per input: its live columns in k order (+ NaN from a dropped one); the reads
+      // of one input are independent (unrolled), so the sum waits for one LDS round trip
       for (int u = lane; u < NU; u += 64) {
         const bool ux = u < a.F;
         const int i = ux ? u : u - a.F;
-        const int c0 = ux ? i * a.nb : a.Fnb + i * a.nb;
+        const int c0 = ux ? i * a.nb : a.Fnb + i * a.nb;   // first column reading input u
+        const int live = a.H - c0;
+        const int cnt = live < 0 ? 0 : live < a.nb ? live : a.nb;
         float sum = 0.0f;
-        for (int k = 0; k < a.nb && c0 + k < a.H; ++k) sum += s_cg[wv][c0 + k];
+        if (cnt > 0) {
+          if (a.nb <= 16) {
+            float vals[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) vals[k] = s_cg[wv][c0 + k];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+              if (k < cnt) sum += vals[k];
+          } else {
+            for (int k = 0; k < cnt; ++k) sum += s_cg[wv][c0 + k];
+          }
+        }
         if (s_bad[wv][ux ? u : kMaxF + i]) sum += __builtin_nanf("");
         if (ux) {
           if (A.g_x) A.g_x[(row * a.T + t) * a.F + i] = sum;
@@ -369,7 +384,11 @@ RnnArgs rnn_args(const fetode_kanrnn_t* m) {
 
 template <int MQ>
 void launch_bwd(const BwdArgs& A, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(kanrnn_bwd_kernel<MQ>, dim3((unsigned)grid), dim3(64 * kWaves), 0, s, A);
+  const size_t lds = sizeof(float4) * A.f.Q;
+  if (A.f.H <= 64)
+    hipLaunchKernelGGL((kanrnn_bwd_kernel<MQ, 1>), dim3((unsigned)grid), dim3(64 * kWaves), lds, s, A);
+  else if constexpr (MQ >= 4)
+    hipLaunchKernelGGL((kanrnn_bwd_kernel<MQ, 4>), dim3((unsigned)grid), dim3(64 * kWaves), lds, s, A);
 }
 
 }  // namespace
@@ -400,7 +419,9 @@ int fetode_kanrnn_forward(const fetode_kanrnn_t* m, const float* x, int64_t B, i
   a.x = x, a.B = B, a.T = T, a.h0 = h0, a.hout = h_out, a.z0 = z0, a.tape = tape;
   const int D = depth_of(a.F, a.H, a.nb);
   a.t_first = (full || tape || T - 1 - D <= 0) ? 0 : T - 1 - D;
-  const unsigned grid = (unsigned)((B + kWaves - 1) / kWaves);
+  // enough workgroups to fill the chip; rows are strided over the waves (W^T is staged once per workgroup)
+  const int64_t nwg = (B + kWaves - 1) / kWaves;
+  const unsigned grid = (unsigned)(nwg < kFwdGroups ? nwg : kFwdGroups);
   const size_t lds = z0 ? sizeof(float) * (size_t)m->latent * m->hidden : 0;
   hipStream_t s = (hipStream_t)stream;
   if (a.H <= 64)
@@ -439,7 +460,7 @@ int fetode_kanrnn_backward(const fetode_kanrnn_t* m, const float* x, int64_t B, 
   double* tmp = (double*)(((uintptr_t)(A.part + (int64_t)A.n_waves * 2 * Q) + 15) & ~(uintptr_t)15);
   hipStream_t s = (hipStream_t)stream;
   const int mq = (Q + 63) / 64;
-  if (mq <= 2) launch_bwd<2>(A, grid, s);
+  if (mq <= 2 && A.f.H <= 64) launch_bwd<2>(A, grid, s);
   else if (mq <= 4) launch_bwd<4>(A, grid, s);
   else if (mq <= 8) launch_bwd<8>(A, grid, s);
   else if (mq <= 12) launch_bwd<12>(A, grid, s);

@@ -329,8 +329,37 @@ def _plain_field(obj) -> bool:
     return not any(hooks)
 
 
+_WARNED_CODES = set()
+
+
+def _reachable_fields(func):
+    """KAN / KANFET modules the function's code can name (globals it loads, closure cells)."""
+    from .efficientkan import KAN, KANFET
+    code = func.__code__
+    objs = [func.__globals__.get(n) for n in code.co_names]
+    for cell in func.__closure__ or ():
+        try:
+            objs.append(cell.cell_contents)
+        except ValueError:
+            pass
+    return [o for o in objs if isinstance(o, (KAN, KANFET))]
+
+
+def _warn_unfused(func, why):
+    code = func.__code__
+    if code in _WARNED_CODES or not _reachable_fields(func):
+        return
+    _WARNED_CODES.add(code)
+    import warnings
+    warnings.warn(f"fet_ode_amd.odeint: {func.__qualname__} ({code.co_filename}:{code.co_firstlineno}) uses a "
+                  f"KAN/KANFET module but {why}, so it is integrated stage by stage (one field launch + one "
+                  "combine per stage, ~25x slower than the fused solve).  Write it as `return model(X)` or pass "
+                  "fet_ode_amd.autonomous(model).", RuntimeWarning, stacklevel=4)
+
+
 def closure_field(func):
-    """The module a ``calDeriv``-shaped plain function calls, or None (see above)."""
+    """The module a ``calDeriv``-shaped plain function calls, or None (see above).  A function that
+    can reach a KAN / KANFET module but does not have that shape warns once (it runs per stage)."""
     import types
     if not isinstance(func, types.FunctionType):
         return None
@@ -339,6 +368,7 @@ def closure_field(func):
     if shape is False:
         shape = _CLOSURE_SHAPES[code] = _closure_shape(code)
     if shape is None:
+        _warn_unfused(func, "does more than `return model(X)`")
         return None
     kind, name = shape
     if kind == "global":
@@ -348,7 +378,10 @@ def closure_field(func):
             obj = func.__closure__[code.co_freevars.index(name)].cell_contents
         except (ValueError, IndexError, TypeError):   # not a free variable, or an empty cell
             return None
-    return obj if _plain_field(obj) else None
+    if _plain_field(obj):
+        return obj
+    _warn_unfused(func, "the module has hooks or is a subclass")
+    return None
 
 
 _FUSED_TRAINING = os.environ.get("FETODE_FUSED_TRAINING", "1") != "0"

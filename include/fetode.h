@@ -93,6 +93,11 @@ typedef struct fetode_field {
  * (prev_x := x, i.e. dx = 0, ferro_class.py:373-375); clear => use the stored prev_x. */
 
 const char* fetode_last_error(void);
+/* How the device-resident solvers (fetode_integrate_dopri5, fetode_ecg_dopri5) launch their grid,
+ * which is sized by occupancy to be co-resident: 0 (default) an ordinary launch, 1
+ * hipLaunchCooperativeKernel (env FETODE_COOPERATIVE=1).  A grid that is not co-resident ends
+ * in status 4 (bounded spins), never a hang.  mode < 0 queries.  Returns the previous mode. */
+int32_t fetode_resident_launch_mode(int32_t mode);
 int fetode_abi_version(void);
 
 /* Size in bytes of the packed "plan" (pre-transformed parameters). */

@@ -76,3 +76,28 @@ def test_hooks_and_switch_disable_recognition():
         assert fused_field(f) is None
         assert fused_field(F.autonomous(m)) is m     # the explicit tag still fuses
     assert fused_field(f) is m
+
+
+def test_unrecognised_closure_over_a_field_warns_once():
+    """A closure that reaches a KAN / KANFET module but is not `return model(X)` runs per stage and
+    says so once (per code object); closures over anything else stay silent."""
+    import warnings
+    m = F.KANFET([2, 10, 2])
+
+    def scaled(t, X):
+        return m(X) * 2.0
+
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        assert closure_field(scaled) is None
+        assert closure_field(scaled) is None
+        lin = torch.nn.Linear(2, 2)
+        assert closure_field(lambda tt, yy: lin(yy) * 2) is None
+        h = m.register_forward_hook(lambda mod, i, o: None)
+        hooked = lambda tt, yy: m(yy)  # noqa: E731
+        assert closure_field(hooked) is None
+        h.remove()
+    msgs = [str(x.message) for x in w if issubclass(x.category, RuntimeWarning)]
+    assert len(msgs) == 2, msgs
+    assert "scaled" in msgs[0] and "stage by stage" in msgs[0]
+    assert "hooks" in msgs[1]

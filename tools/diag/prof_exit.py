@@ -5,6 +5,7 @@ their library (tools/diag/resolve_pcs.py).
   mode torch   : torch only (a cuda tensor, one kernel) - no fet_ode_amd at all
   mode fetode  : one fused rk4 solve through fet_ode_amd (registers its exit-time release hooks)
   mode nohooks : as fetode, with the package's atexit release hooks unregistered first
+  mode rk4only : as fetode without the resident dopri5 solve (no cooperative launch)
 """
 import atexit
 import os
@@ -34,7 +35,7 @@ else:
     with torch.no_grad():
         for _ in range(3):
             sol = F.odeint(F.autonomous(m), y0, t, method="rk4")
-        sol2 = F.odeint(F.autonomous(m), y0, t)   # resident dopri5 (registers its hooks)
+        sol2 = sol if mode == "rk4only" else F.odeint(F.autonomous(m), y0, t)   # resident dopri5 (cooperative)
     torch.cuda.synchronize()
     print("solve ok", float(sol[-1].abs().sum()), float(sol2[-1].abs().sum()))
 os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
