@@ -74,6 +74,8 @@ def make_problem(rank, world, scaling, dev):
     import fet_ode_amd.dist as D
     torch.manual_seed(0)
     model = F.KANFET([2, 10, 2], grid_size=5)
+    if world > 1:   # one model for the job: the efficient_kan init is not reproducible across processes
+        D.broadcast_parameters(model)
     sd = {k: v.clone() for k, v in model.state_dict().items()}
     model = model.to(dev)
     if scaling == "strong":
@@ -222,6 +224,40 @@ def lv_dopri5_rate(sd, y0d, t, reps=3):
             "field_evals_per_s": s.nfev / el, "rk4_equiv_steps_per_s": s.nfev / 4 / el,
             "resident": isinstance(s, ResidentSolve), "finite": bool(torch.isfinite(sol).all()),
             "path": "fetode_integrate_dopri5: fused4_kernel DOPRI instantiation, one cooperative launch"}
+
+
+def lv_dopri5_sharded_rate(sd, y0d, t, world, B_global, reps=3):
+    """The north-star default call sharded over the ranks (dist.odeint_sharded): each rank solves
+    its block of the global batch in ONE resident launch whose exchange workgroup sums every error
+    norm across the ranks (fetode_integrate_dopri5_xrank), so all ranks take the global batch's
+    steps.  Time = max over ranks between barriers."""
+    import torch.distributed as dist
+    import fet_ode_amd.dist as D
+    from fet_ode_amd.dopri5 import ResidentSolve
+    m = F.KANFET([2, 10, 2], grid_size=5)
+    m.load_state_dict(sd)
+    m = m.to(y0d.device)
+    func = F.autonomous(m)
+    with torch.no_grad():
+        D.odeint_sharded(func, y0d, t)
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize(y0d.device)
+            dist.barrier()
+            t0 = time.perf_counter()
+            sol = D.odeint_sharded(func, y0d, t)
+            torch.cuda.synchronize(y0d.device)
+            ts.append(time.perf_counter() - t0)
+    el = torch.tensor([float(np.median(ts))], dtype=torch.float64,
+                      device=y0d.device if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = el.item()
+    s = F.dopri5.dopri5_solve.last
+    return {"value": 1.0 / el, "unit": f"dopri5 solves/s (global B={B_global} over {world} GPUs, rtol 1e-7, "
+                                       "atol 1e-9, t=linspace(0,3.5,35))",
+            "ms_per_solve": el * 1e3, "attempts": s.n_attempts, "nfev": s.nfev,
+            "resident": isinstance(s, ResidentSolve), "finite": bool(torch.isfinite(sol).all()),
+            "path": "fetode_integrate_dopri5_xrank: one launch per rank, norms exchanged between the kernels"}
 
 
 def plain_closure_rate(model, y0d, t, reps=3):
@@ -621,6 +657,9 @@ def main():
             el = tt.item()
         k_ms = kernel_time_ms(model, y0d, t)
     train = train_rate(model, y0d, t, args.train_iters, 5, world, strong) if args.train_iters > 0 else None
+    dp5_sharded = None
+    if world > 1 and strong and not args.no_dopri5:
+        dp5_sharded = lv_dopri5_sharded_rate(sd, y0d, t, world, B)
     ms_per_step = el / args.steps * 1e3
     # strong: every solve covers the global batch once; weak: each rank's solve is a batch of its own
     value = (1 if strong else world) * args.steps * STEPS_PER_SOLVE / el
@@ -671,6 +710,8 @@ def main():
             out["lv_plain_closure"] = plain_closure_rate(model, y0d, t)
         if world == 1 and not args.no_dopri5:
             out["lv_dopri5"] = lv_dopri5_rate(sd, y0d, t)
+        if dp5_sharded is not None:
+            out["lv_dopri5"] = dp5_sharded
         if world == 1 and not args.no_ecg:
             out["ecg"] = ecg_rate(dev, with_cpu=not args.no_cpu_baseline)
             out["ecg"]["rtol_1e-2"] = ecg_rate(dev, with_cpu=False, rtol=1e-2, atol=1e-3)

@@ -82,6 +82,11 @@ class KANRNNDesc(ctypes.Structure):
                 ("bias", _fp)]
 
 
+class XRankDesc(ctypes.Structure):
+    _fields_ = [("rank", ctypes.c_int32), ("world", ctypes.c_int32), ("epoch", ctypes.c_uint32),
+                ("inbox", _vp), ("peers", _vp), ("b_offset", ctypes.c_int64)]
+
+
 class FieldDesc(ctypes.Structure):
     _fields_ = [
         ("n_layers", ctypes.c_int32),
@@ -105,6 +110,17 @@ SIGNATURES = {
                                                ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_float), _vp,
                                                _vp, ctypes.c_uint32, _vp, _vp, _vp, ctypes.c_int32, _vp]),
     "fetode_integrate_dopri5_workspace": (ctypes.c_int64, [ctypes.c_int64]),
+    "fetode_integrate_dopri5_xrank": (ctypes.c_int, [ctypes.POINTER(FieldDesc), _vp, _vp, ctypes.c_int64,
+                                                     ctypes.c_int64, _vp, ctypes.c_int32, ctypes.c_double,
+                                                     ctypes.c_double, ctypes.POINTER(ctypes.c_double),
+                                                     ctypes.POINTER(ctypes.c_float), _vp, _vp, ctypes.c_uint32,
+                                                     _vp, _vp, _vp, ctypes.c_int32, ctypes.POINTER(XRankDesc), _vp]),
+    "fetode_xrank_inbox_bytes": (ctypes.c_int64, [ctypes.c_int32]),
+    "fetode_integrate_dopri5_max_batch": (ctypes.c_int64, [ctypes.POINTER(FieldDesc), ctypes.c_int32]),
+    "fetode_xrank_alloc": (ctypes.c_int, [ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p), _vp]),
+    "fetode_xrank_open": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_void_p)]),
+    "fetode_xrank_close": (ctypes.c_int, [_vp]),
+    "fetode_xrank_free": (ctypes.c_int, [_vp]),
     "fetode_wide_layer_supported": (ctypes.c_int, [ctypes.POINTER(KANLinearDesc), ctypes.POINTER(FerroDesc)]),
     "fetode_wide_layer_plan_bytes": (ctypes.c_int64, [ctypes.POINTER(KANLinearDesc), ctypes.POINTER(FerroDesc)]),
     "fetode_wide_layer_plan_build": (ctypes.c_int, [ctypes.POINTER(KANLinearDesc), ctypes.POINTER(FerroDesc), _vp, _vp]),

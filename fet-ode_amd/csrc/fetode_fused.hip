@@ -76,6 +76,18 @@ struct DopriParams {
   int32_t* stats;   // nfev, attempts, status
   double* att;      // (max_att, 4): t0, dt, error ratio, accepted
   int32_t max_att;
+  // trajectory-sharded solve (fetode_integrate_dopri5_xrank): every norm is the sum over all ranks
+  double n_total;              // global element count of the norms (B_global * D)
+  int32_t xr_rank, xr_world;   // xr_world <= 1: single device
+  uint32_t xr_epoch;           // per-solve tag (the same on every rank)
+  double* const* xr_peers;     // (dev) xr_world inbox base pointers as mapped here (peers[rank] = own)
+  double* xr_inbox;            // (dev) own inbox: (2, world) records {v0, v1, tag, pad}
+  double* xr_g;                // (2, 2) the global sums of the round, double-buffered by parity
+  // leaves of the grid reduction: contiguous runs of leaf_len workgroups in GLOBAL workgroup numbers
+  // (this grid's workgroup b is global workgroup wg_off + b); this grid owns leaves
+  // [leaf_lo, leaf_lo + n_leaf_local) of n_leaf_global.  xr_exact: every rank owns whole leaves of
+  // the single-device grid, so the rank-summed result is bitwise the single device's
+  int32_t leaf_shift, wg_off, leaf_lo, n_leaf_local, n_leaf_global, nblk_global, xr_exact;  // leaf_len = 1 << leaf_shift
 };
 
 // Grid-wide sum of two fp64 values, one per workgroup (valid on every lane of a one-wave
@@ -96,7 +108,12 @@ constexpr unsigned kDpSpinLimit = 1u << 20;
 constexpr int kDpGroups = 64;
 constexpr int kDpLine = 64;  // words per counter line
 constexpr int kDpTopCopies = 8;  // replicas of the top counter: ~256 pollers per address, not 2048
-constexpr int kDpBarWords = kDpLine * (kDpGroups + 2 + kDpTopCopies);
+constexpr int kDpBarWords = kDpLine * (kDpGroups + 2 + 2 * kDpTopCopies);
+// replicas of the cross-rank "global sum ready" counter (after the top-counter replicas)
+__device__ __forceinline__ unsigned* dp_ready(const DopriParams& P, unsigned c) {
+  return P.bar + kDpLine * (kDpGroups + 2 + kDpTopCopies + c);
+}
+constexpr unsigned kXrSpinLimit = 1u << 24;   // cross-rank polls: ranks may start seconds apart
 __device__ __forceinline__ unsigned* dp_cnt(const DopriParams& P, unsigned x) { return P.bar + kDpLine * x; }
 __device__ __forceinline__ unsigned* dp_top(const DopriParams& P, unsigned c) {
   return P.bar + kDpLine * (kDpGroups + 2 + c);
@@ -135,20 +152,150 @@ __device__ __forceinline__ double xor_sum64(double v) {
   return v;
 }
 
+// System-scope (sc0 sc1: write-through to memory / read past every cache) records for the
+// cross-rank exchange: the payload lands before the tag that publishes it (vmcnt(0) between).
+__device__ __forceinline__ void xr_st16(double* p, double v0, double v1) {
+  const unsigned long long a = __double_as_longlong(v0), b = __double_as_longlong(v1);
+  const dp_u32x4 v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void xr_st_tag(double* p, unsigned long long tag) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 v = {(unsigned)tag, (unsigned)(tag >> 32)};
+  asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ unsigned long long xr_ld_tag(const double* p) {
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  u32x2 v;
+  asm volatile("global_load_dwordx2 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return ((unsigned long long)v.y << 32) | v.x;
+}
+__device__ __forceinline__ void xr_ld16(const double* p, double& v0, double& v1) {
+  dp_u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  v0 = __longlong_as_double(((unsigned long long)v.y << 32) | v.x);
+  v1 = __longlong_as_double(((unsigned long long)v.w << 32) | v.z);
+}
+
+// Trajectory-sharded solve (xr_world > 1): the rank sum of every grid reduction is formed by ONE
+// extra workgroup (the last of the grid; the compute workgroups' path changes only in which counter
+// they poll and where they read the result, so their registers do not grow).  Per round r it waits
+// for the local top counter, sums the local leaf sums (the single-device order), writes this GPU's
+// {s0, s1} into slot `rank` of every rank's inbox (remote stores over xGMI; its own by a local
+// store), polls its own inbox until every rank's record of round r is there, sums them in rank
+// order (the same order on every rank: every rank takes the same decisions) and publishes the
+// result through xr_g and the ready-counter replicas the compute workgroups poll.  Inbox records are
+// double-buffered by round parity: a rank writes round r + 2 into a peer's slot only after it has
+// received that peer's round r + 1 record, which the peer sent after reading round r.  The loop
+// ends when the compute workgroups post the solve's round count (dp_fin) or the abort word rises.
+// Bounded spins; a timeout raises the abort word (status 4) and the peers time out in turn.
+__device__ __forceinline__ unsigned* dp_fin(const DopriParams& P) { return P.bar + kDpLine * kDpGroups; }
+// inbox: (2 parity, 64 items) {v0, v1} records, then (2 parity, 64 ranks) tags (fetode_xrank_inbox_bytes)
+__device__ __forceinline__ double* xr_rec(double* inbox, unsigned par, int item) { return inbox + 2 * (64 * par + item); }
+__device__ __forceinline__ double* xr_tagp(double* inbox, unsigned par, int rank) {
+  return inbox + 2 * 2 * 64 + (64 * par + rank);
+}
+
+__device__ void xrank_comm(const DopriParams& P) {
+  const int lane = threadIdx.x & 63;
+  const int W = P.xr_world;
+  const unsigned nloc = (unsigned)P.n_leaf_local;
+  unsigned* abw = dp_abort(P);
+  for (unsigned r = 0;; ++r) {
+    const unsigned par = r & 1u;
+    // 1. this grid's leaves of round r (or the end of the solve)
+    int stop = 0;
+    if (lane == 0) {
+      const unsigned want = nloc * (r + 1u);
+      unsigned spins = 0;
+      for (;;) {
+        if ((int)(__hip_atomic_load(dp_top(P, 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) >= 0) break;
+        const unsigned fin = __hip_atomic_load(dp_fin(P), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((fin != 0u && fin <= r + 1u) || __hip_atomic_load(abw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          stop = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins == kXrSpinLimit) {
+          __hip_atomic_store(abw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          stop = 1;
+          break;
+        }
+      }
+      dp_order();
+    }
+    if (__shfl(stop, 0)) return;
+    const double* xs = P.xs + 2 * kDpGroups * par;
+    double u0 = 0.0, u1 = 0.0;
+    if ((unsigned)lane < nloc) dp_ld16(&xs[2 * (P.leaf_lo + lane)], u0, u1);
+    // 2. send: the leaves themselves at their global leaf index (exact), or this grid's total at
+    //    index `rank`; then the round's tag (after the payload stores have completed)
+    if (P.xr_exact) {
+      if ((unsigned)lane < nloc)
+        for (int p = 0; p < W; ++p) xr_st16(xr_rec(P.xr_peers[p], par, P.leaf_lo + lane), u0, u1);
+    } else {
+      const double t0 = xor_sum64(u0), t1 = xor_sum64(u1);
+      if (lane < W) xr_st16(xr_rec(P.xr_peers[lane], par, P.xr_rank), t0, t1);
+    }
+    const unsigned long long tag = ((unsigned long long)P.xr_epoch << 32) | (unsigned long long)(r + 1u);
+    if (lane < W) xr_st_tag(xr_tagp(P.xr_peers[lane], par, P.xr_rank), tag);
+    // 3. receive every rank's round-r tag, then the records
+    int ab = 0;
+    if (lane < W) {
+      const double* tg = xr_tagp(P.xr_inbox, par, lane);
+      unsigned spins = 0;
+      while (xr_ld_tag(tg) != tag) {
+        __builtin_amdgcn_s_sleep(2);
+        if ((spins & 255u) == 255u && __hip_atomic_load(abw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          ab = 1;
+          break;
+        }
+        if (++spins == kXrSpinLimit) {
+          __hip_atomic_store(abw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ab = 1;
+          break;
+        }
+      }
+    }
+    if (__any(ab)) return;
+    double g0 = 0.0, g1 = 0.0;
+    if (P.xr_exact) {   // the single device's final step: lane per leaf, xor tree
+      double v0 = 0.0, v1 = 0.0;
+      if (lane < P.n_leaf_global) xr_ld16(xr_rec(P.xr_inbox, par, lane), v0, v1);
+      g0 = xor_sum64(v0);
+      g1 = xor_sum64(v1);
+    } else {            // rank totals in rank order (the same order on every rank)
+      double v0 = 0.0, v1 = 0.0;
+      if (lane < W) xr_ld16(xr_rec(P.xr_inbox, par, lane), v0, v1);
+      for (int j = 0; j < W; ++j) {
+        g0 += __shfl(v0, j);
+        g1 += __shfl(v1, j);
+      }
+    }
+    // 4. publish to this grid
+    if (lane == 0) dp_st16(P.xr_g + 2 * par, g0, g1);
+    dp_order();
+    if (lane < kDpTopCopies) __hip_atomic_fetch_add(dp_ready(P, lane), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 __device__ bool grid_sum2(const DopriParams& P, unsigned& round, double v0, double v1, double& s0, double& s1) {
 #ifdef FETODE_EXP_NO_GRIDSUM  // diagnostics only: per-workgroup control, no synchronisation
   s0 = v0 * gridDim.x;
   s1 = v1 * gridDim.x;
   return false;
 #endif
-  const unsigned blk = blockIdx.x, nblk = gridDim.x, x = blk % kDpGroups;
-  if (nblk == 1u) {  // one workgroup: the sums below would return v0, v1 exactly
+  const bool xr = P.xr_world > 1;   // the last workgroup is the cross-rank exchange (xrank_comm)
+  const unsigned blk = blockIdx.x, nblk = gridDim.x - (xr ? 1u : 0u);
+  if (nblk == 1u && !xr) {  // one workgroup: the sums below would return v0, v1 exactly
     s0 = v0;
     s1 = v1;
     return false;
   }
-  const unsigned ngrp = nblk < (unsigned)kDpGroups ? nblk : (unsigned)kDpGroups;
-  const unsigned nx = (nblk + kDpGroups - 1u - x) / kDpGroups;
+  // leaf x = global workgroups [x L, x L + nx) (contiguous; the same leaves on one device and sharded)
+  const unsigned sh = (unsigned)P.leaf_shift, L = 1u << sh, gb = blk + (unsigned)P.wg_off, x = gb >> sh;
+  const unsigned nx = min(L, (unsigned)P.nblk_global - (x << sh));
+  const unsigned ngrp = (unsigned)P.n_leaf_local;
   const unsigned r = round++;
   double* xs = P.xs + 2 * kDpGroups * (r & 1u);
   unsigned* abw = dp_abort(P);
@@ -168,7 +315,7 @@ __device__ bool grid_sum2(const DopriParams& P, unsigned& round, double v0, doub
     double a0 = 0.0, a1 = 0.0;
     for (unsigned j = lane; j < nx; j += 64) {
       double u0, u1;
-      dp_ld16(&P.slot[2 * (x + kDpGroups * j)], u0, u1);
+      dp_ld16(&P.slot[2 * ((x << sh) + j - (unsigned)P.wg_off)], u0, u1);
       a0 += u0;
       a1 += u1;
     }
@@ -179,17 +326,18 @@ __device__ bool grid_sum2(const DopriParams& P, unsigned& round, double v0, doub
     if (lane < kDpTopCopies) __hip_atomic_fetch_add(dp_top(P, lane), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (lane == 0 && !ab) {
-    const unsigned want = ngrp * (r + 1u);
+    // single device: all leaves of round r; sharded: the exchange workgroup's rank sum of round r
+    const unsigned want = xr ? r + 1u : ngrp * (r + 1u);
     unsigned spins = 0;
     // wrap-safe: (int)(top - want) < 0 while fewer than `want` leaf arrivals have landed
-    unsigned* top = dp_top(P, blk % kDpTopCopies);
+    unsigned* top = xr ? dp_ready(P, blk % kDpTopCopies) : dp_top(P, blk % kDpTopCopies);
     while ((int)(__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
       __builtin_amdgcn_s_sleep(1);
       if ((spins & 15u) == 15u && __hip_atomic_load(abw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         ab = 1;
         break;
       }
-      if (++spins == kDpSpinLimit) {
+      if (++spins == (xr ? kXrSpinLimit : kDpSpinLimit)) {
         __hip_atomic_store(abw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ab = 1;
         break;
@@ -198,8 +346,12 @@ __device__ bool grid_sum2(const DopriParams& P, unsigned& round, double v0, doub
     dp_order();
   }
   ab = __shfl(ab, 0);
+  if (xr) {
+    if (!ab) dp_ld16(P.xr_g + 2 * (r & 1u), s0, s1);
+    return ab != 0;
+  }
   double u0 = 0.0, u1 = 0.0;
-  if ((unsigned)lane < ngrp && !ab) dp_ld16(&xs[2 * lane], u0, u1);
+  if ((unsigned)lane < ngrp && !ab) dp_ld16(&xs[2 * lane], u0, u1);   // one device: leaves 0 .. ngrp-1
   s0 = xor_sum64(u0);
   s1 = xor_sum64(u1);
   return ab != 0;
@@ -329,6 +481,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   constexpr int NPL0 = FERRO ? (D * KP + 2) / 3 : 0, NPL1 = FERRO ? (H * KP + 15) / 16 : 0;
   constexpr int FPL0 = ((D * NFP + 2) / 3 + 3) & ~3, FPL1 = ((H * NFP + 15) / 16 + 3) & ~3;
   constexpr int FLEN0 = (3 * FPL0 > D * NFP ? 3 * FPL0 : D * NFP);
+  if constexpr (DOPRI) {
+    if (a.dp.xr_world > 1 && blockIdx.x == gridDim.x - 1) {   // the cross-rank exchange workgroup
+      xrank_comm(a.dp);
+      return;
+    }
+  }
   constexpr int FLEN1 = (16 * FPL1 > H * NFP ? 16 * FPL1 : H * NFP);
   constexpr int NJH = FERRO ? NB + 3 : NB + 1;      // sigmoid-stream jobs per hidden input
   constexpr int RH = (NJH + 2) / 3;                  // rounds over the 3 lanes of a group
@@ -720,7 +878,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
       // ---- device-resident dopri5 (dopri5.py _Dopri5, lane (traj, dim = row) carries y_row) ----
       const DopriParams& P = a.dp;
       const bool real = valid && c1 == 0;  // one lane per (trajectory, state dim) in the sums
-      const double n_el = (double)(a.B * D);
+      const double n_el = P.n_total;   // B * D, or the global batch's in a sharded solve
       int nfev = 0, n_att = 0, status = 0;
       unsigned round = 0;
 #ifdef FETODE_EXP_NO_EVAL  // diagnostics only: a trivial field, the reductions and control as is
@@ -850,6 +1008,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
         }
         out_write(i, total);
       }
+      if (P.xr_world > 1 && blockIdx.x == 0 && tid == 0)   // the exchange workgroup may stop
+        __hip_atomic_store(dp_fin(P), round + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (blockIdx.x == 0 && tid == 0) {
         P.stats[0] = nfev;
         P.stats[1] = n_att;
@@ -1406,13 +1566,36 @@ int fetode_field_forward(const fetode_field_t* f, const void* plan, const float*
 
 int64_t fetode_integrate_dopri5_workspace(int64_t B) {
   const int64_t grid = (B + 1) / 2;
-  return (int64_t)sizeof(unsigned) * kDpBarWords + (int64_t)sizeof(double) * (2 * grid + 4 * kDpGroups);
+  return (int64_t)sizeof(unsigned) * kDpBarWords + (int64_t)sizeof(double) * (2 * grid + 4 * kDpGroups + 4);
 }
 
-int fetode_integrate_dopri5(const fetode_field_t* f, const void* plan, const float* y0, int64_t B, const double* t,
-                            int32_t T, double rtol, double atol, const double* opts, const float* tableau,
-                            float* solution, float* state, uint32_t init_mask, void* workspace, int32_t* stats,
-                            double* attempts, int32_t max_attempts, void* stream) {
+// every workgroup must be resident at once (grid reductions): one-wave workgroups of two
+// trajectories, as many as the occupancy of the DOPRI instantiation admits (-1: query failed)
+static int64_t dopri5_resident_wgs(const FusedEntry* e, bool ferro) {
+  static int n_cu = 0, per_cu[2] = {0, 0};
+  const int fi = ferro ? 0 : 1;
+  if (!n_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return -1;
+  }
+  if (!per_cu[fi] && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[fi], e->dopri, 64, 0) != hipSuccess) return -1;
+  return (int64_t)per_cu[fi] * n_cu;
+}
+
+int64_t fetode_integrate_dopri5_max_batch(const fetode_field_t* f, int32_t sharded) {
+  if (validate_field(f) != FETODE_OK) return 0;
+  const FusedEntry* e = find_fused(f);
+  if (!e) return 0;
+  const int64_t w = dopri5_resident_wgs(e, f->ferro != nullptr) - (sharded ? 1 : 0);
+  return w > 0 ? 2 * w : 0;
+}
+
+static int dopri5_launch(const fetode_field_t* f, const void* plan, const float* y0, int64_t B, const double* t,
+                         int32_t T, double rtol, double atol, const double* opts, const float* tableau,
+                         float* solution, float* state, uint32_t init_mask, void* workspace, int32_t* stats,
+                         double* attempts, int32_t max_attempts, const fetode_xrank_t* xr, int64_t B_total,
+                         void* stream) {
   int rc = validate_field(f);
   if (rc) return rc;
   if (B <= 0 || T <= 0) return FETODE_OK;
@@ -1422,20 +1605,14 @@ int fetode_integrate_dopri5(const fetode_field_t* f, const void* plan, const flo
     return set_err(FETODE_EINVAL, "field is not R^D -> R^D");
   const FusedEntry* e = find_fused(f);
   if (!e) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
-  // every workgroup must be resident at once (grid reductions): one-wave workgroups of two
-  // trajectories, as many as the occupancy of the generic v4 kernel admits
-  static int n_cu = 0, per_cu[2] = {0, 0};
-  const int fi = f->ferro ? 0 : 1;
-  if (!n_cu) {
-    int dev = 0;
-    HIP_CHECK_RET(hipGetDevice(&dev));
-    HIP_CHECK_RET(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  if (!per_cu[fi]) HIP_CHECK_RET(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[fi], e->dopri, 64, 0));
+  const int64_t resident = dopri5_resident_wgs(e, f->ferro != nullptr);
+  if (resident < 0) return set_err(FETODE_EHIP, "dopri5: occupancy query failed");
   const int64_t grid = nblk(B, 2);
-  if (grid > (int64_t)per_cu[fi] * n_cu)
-    return set_err(FETODE_EUNSUPPORTED, "dopri5: batch %lld needs %lld workgroups, %d resident", (long long)B,
-                   (long long)grid, per_cu[fi] * n_cu);
+  const bool sharded = xr && xr->world > 1;
+  const int64_t lgrid = grid + (sharded ? 1 : 0);   // + the cross-rank exchange workgroup
+  if (lgrid > resident)
+    return set_err(FETODE_EUNSUPPORTED, "dopri5: batch %lld needs %lld workgroups, %lld resident", (long long)B,
+                   (long long)lgrid, (long long)resident);
   FusedArgs a;
   memset(&a, 0, sizeof(a));
   a.plan = (const float*)plan;
@@ -1471,13 +1648,114 @@ int fetode_integrate_dopri5(const fetode_field_t* f, const void* plan, const flo
   P.stats = stats;
   P.att = attempts;
   P.max_att = attempts ? max_attempts : 0;
+  P.xr_g = P.xs + 4 * kDpGroups;
+  P.n_total = (double)B_total * f->kan[0].in_features;
+  // leaves: runs of L workgroups; exact when this rank's workgroups are whole leaves of the
+  // single-device grid over the global batch (two trajectories per workgroup everywhere)
+  auto cdiv = [](int64_t a_, int64_t b_) { return (a_ + b_ - 1) / b_; };
+  auto lshift = [&](int64_t nb) {   // the smallest power-of-two run that needs <= kDpGroups leaves
+    int sh = 0;
+    while ((int64_t)kDpGroups << sh < nb) ++sh;
+    return sh;
+  };
+  P.xr_exact = 0;
+  P.wg_off = 0;
+  P.nblk_global = (int32_t)grid;
+  P.leaf_shift = lshift(grid);
+  if (sharded) {
+    P.xr_rank = xr->rank;
+    P.xr_world = xr->world;
+    P.xr_epoch = xr->epoch;
+    P.xr_peers = (double* const*)xr->peers;
+    P.xr_inbox = (double*)xr->inbox;
+    const int64_t gg = cdiv(B_total, 2), shg = lshift(gg), Lg = (int64_t)1 << shg, off = xr->b_offset / 2;
+    const bool last = xr->b_offset + B == B_total;
+    if (xr->b_offset % 2 == 0 && (B % 2 == 0 || last) && off % Lg == 0 && ((off + grid) % Lg == 0 || last)) {
+      P.xr_exact = 1;
+      P.wg_off = (int32_t)off;
+      P.nblk_global = (int32_t)gg;
+      P.leaf_shift = (int32_t)shg;
+    }
+  } else {
+    P.xr_world = 1;
+  }
+  P.leaf_lo = P.wg_off >> P.leaf_shift;
+  P.n_leaf_local = (int32_t)cdiv(grid, (int64_t)1 << P.leaf_shift);
+  P.n_leaf_global = (int32_t)cdiv(P.nblk_global, (int64_t)1 << P.leaf_shift);
   layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
   layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
   a.factor_limit = kFactorLimit;
   hipStream_t s = (hipStream_t)stream;
   HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kDpBarWords, s));
   void* args[] = {&a};
-  HIP_CHECK_RET(resident_launch((const void*)e->dopri, dim3((unsigned)grid), dim3(64), args, 0, s));
+  HIP_CHECK_RET(resident_launch((const void*)e->dopri, dim3((unsigned)lgrid), dim3(64), args, 0, s));
+  return FETODE_OK;
+}
+
+int fetode_integrate_dopri5(const fetode_field_t* f, const void* plan, const float* y0, int64_t B, const double* t,
+                            int32_t T, double rtol, double atol, const double* opts, const float* tableau,
+                            float* solution, float* state, uint32_t init_mask, void* workspace, int32_t* stats,
+                            double* attempts, int32_t max_attempts, void* stream) {
+  return dopri5_launch(f, plan, y0, B, t, T, rtol, atol, opts, tableau, solution, state, init_mask, workspace, stats,
+                       attempts, max_attempts, nullptr, B, stream);
+}
+
+int fetode_integrate_dopri5_xrank(const fetode_field_t* f, const void* plan, const float* y0, int64_t B,
+                                  int64_t B_total, const double* t, int32_t T, double rtol, double atol,
+                                  const double* opts, const float* tableau, float* solution, float* state,
+                                  uint32_t init_mask, void* workspace, int32_t* stats, double* attempts,
+                                  int32_t max_attempts, const fetode_xrank_t* xr, void* stream) {
+  if (!xr || xr->world < 1 || xr->rank < 0 || xr->rank >= xr->world || xr->world > 64)
+    return set_err(FETODE_EINVAL, "dopri5 xrank: bad rank / world");
+  if (xr->world > 1 && (!xr->peers || !xr->inbox)) return set_err(FETODE_EINVAL, "dopri5 xrank: null inbox / peers");
+  if (B_total < B || xr->b_offset < 0 || xr->b_offset + B > B_total)
+    return set_err(FETODE_EINVAL, "dopri5 xrank: shard [%lld, %lld) outside the global batch %lld",
+                   (long long)xr->b_offset, (long long)(xr->b_offset + B), (long long)B_total);
+  return dopri5_launch(f, plan, y0, B, t, T, rtol, atol, opts, tableau, solution, state, init_mask, workspace, stats,
+                       attempts, max_attempts, xr, B_total, stream);
+}
+
+int64_t fetode_xrank_inbox_bytes(int32_t world) {
+  if (world < 1 || world > 64) return -1;
+  return (int64_t)sizeof(double) * (2 * 2 * 64 + 2 * 64);   // (2, 64) records + (2, 64) tags
+}
+
+int fetode_xrank_alloc(int64_t bytes, void** dev_ptr, void* handle) {
+  if (bytes <= 0 || !dev_ptr || !handle) return set_err(FETODE_EINVAL, "xrank alloc: bad argument");
+  void* p = nullptr;
+  // fine-grained device memory: coherent for the system-scope stores / loads of the exchange
+  if (hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocFinegrained) != hipSuccess || !p) {
+    (void)hipGetLastError();
+    HIP_CHECK_RET(hipMalloc(&p, (size_t)bytes));
+  }
+  HIP_CHECK_RET(hipMemset(p, 0, (size_t)bytes));
+  hipIpcMemHandle_t h;
+  const hipError_t e = hipIpcGetMemHandle(&h, p);
+  if (e != hipSuccess) {
+    (void)hipFree(p);
+    return set_err(FETODE_EHIP, "hipIpcGetMemHandle: %s", hipGetErrorString(e));
+  }
+  memcpy(handle, &h, sizeof(h) < 64 ? sizeof(h) : 64);
+  *dev_ptr = p;
+  return FETODE_OK;
+}
+
+int fetode_xrank_open(const void* handle, void** dev_ptr) {
+  if (!handle || !dev_ptr) return set_err(FETODE_EINVAL, "xrank open: bad argument");
+  hipIpcMemHandle_t h;
+  memset(&h, 0, sizeof(h));
+  memcpy(&h, handle, sizeof(h) < 64 ? sizeof(h) : 64);
+  HIP_CHECK_RET(hipIpcOpenMemHandle(dev_ptr, h, hipIpcMemLazyEnablePeerAccess));
+  return FETODE_OK;
+}
+
+int fetode_xrank_close(void* dev_ptr) {
+  if (dev_ptr) HIP_CHECK_RET(hipIpcCloseMemHandle(dev_ptr));
+  return FETODE_OK;
+}
+
+int fetode_xrank_free(void* dev_ptr) {
+  if (dev_ptr) HIP_CHECK_RET(hipFree(dev_ptr));
   return FETODE_OK;
 }
 

@@ -113,10 +113,112 @@ def _shared_flat(grads: List[torch.Tensor]) -> Optional[torch.Tensor]:
     return base if off == base.numel() else None
 
 
+def broadcast_parameters(module: torch.nn.Module, src: int = 0, group=None) -> None:
+    """Make every rank's parameters and buffers rank `src`'s, in place (what DDP does at
+    construction).  Needed before data-parallel training: the efficient_kan init the drop-ins
+    reproduce (curve2coeff's lstsq) is not bitwise reproducible across processes even with the
+    same seed, so ranks that each construct the model start from slightly different weights."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return
+    nccl = dist.get_backend(group) == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu")
+    with torch.no_grad():
+        for t in list(module.parameters()) + list(module.buffers()):
+            buf = t.detach() if t.device == dev else t.detach().to(dev)
+            dist.broadcast(buf, src=src, group=group)
+            if buf is not t:
+                t.copy_(buf)
+
+
+class XRank:
+    """The cross-rank exchange of a trajectory-sharded device-resident dopri5
+    (fetode_integrate_dopri5_xrank): this rank's inbox (device memory, IPC-exported) and every
+    peer's inbox mapped into this process, as a device array of pointers the kernel's exchange
+    workgroup writes through (remote stores over xGMI).  One per (group, device); created
+    collectively (all_gather of the 64-byte IPC handles) the first time a sharded resident solve
+    runs.  Mappings live until the process exits."""
+
+    _cache: dict = {}
+
+    @classmethod
+    def get(cls, group, device) -> "XRank":
+        key = (id(group) if group is not None else None, torch.device(device).index)
+        x = cls._cache.get(key)
+        if x is None:
+            x = cls._cache[key] = cls(group, device)
+        return x
+
+    def __init__(self, group, device):
+        import ctypes
+        from . import _lib
+        lib = _lib.load()
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        nbytes = lib.fetode_xrank_inbox_bytes(self.world)
+        if nbytes < 0:
+            raise ValueError(f"sharded resident dopri5: world size {self.world} not supported")
+        ptr = ctypes.c_void_p()
+        handle = (ctypes.c_uint8 * 64)()
+        with torch.cuda.device(device):
+            _lib.check(lib.fetode_xrank_alloc(nbytes, ctypes.byref(ptr), handle), "fetode_xrank_alloc")
+            handles = [None] * self.world
+            dist.all_gather_object(handles, bytes(handle), group=group)
+            peers = []
+            for j, h in enumerate(handles):
+                if j == self.rank:
+                    peers.append(ptr.value)
+                    continue
+                hb = (ctypes.c_uint8 * 64).from_buffer_copy(h)
+                q = ctypes.c_void_p()
+                _lib.check(lib.fetode_xrank_open(hb, ctypes.byref(q)), "fetode_xrank_open")
+                peers.append(q.value)
+        self.inbox = ptr.value
+        self.peers = torch.tensor(peers, dtype=torch.int64, device=device)
+        self.epoch = 0
+
+    def desc(self, b_offset: int):
+        from . import _lib
+        self.epoch = (self.epoch + 1) & 0xFFFFFFFF or 1
+        return _lib.XRankDesc(self.rank, self.world, self.epoch, self.inbox, self.peers.data_ptr(), int(b_offset))
+
+
+import os as _os
+
+# FETODE_RESIDENT_SHARDED=0: the host-driven loop (e.g. when several ranks share ONE GPU, whose
+# resident grids together would not be co-resident)
+_RESIDENT_SHARDED = [_os.environ.get("FETODE_RESIDENT_SHARDED", "1") != "0"]
+
+
+def set_resident_sharded(enabled: bool) -> bool:
+    """Sharded dopri5 solves of fused fields in one launch per rank with the in-kernel cross-rank
+    exchange (default), or the host-driven loop with one all-reduce per attempt."""
+    prev, _RESIDENT_SHARDED[0] = _RESIDENT_SHARDED[0], bool(enabled)
+    return prev
+
+
+def resident_agreement(group, device, local_batch: int, ok: bool) -> Optional[Tuple[int, int]]:
+    """One all-gather: (global batch, this rank's offset in it), or None unless every rank can take
+    the resident path (all ranks must take the same one: their kernels exchange with each other)."""
+    cpu = dist.get_backend(group) != "nccl"
+    t = torch.tensor([float(local_batch), 1.0 if ok else 0.0], dtype=torch.float64,
+                     device="cpu" if cpu else device)
+    w = dist.get_world_size(group)
+    out = [torch.empty_like(t) for _ in range(w)]
+    dist.all_gather(out, t, group=group)
+    rows = [o.tolist() for o in out]
+    if not all(int(r[1]) for r in rows):
+        return None
+    r = dist.get_rank(group)
+    return int(sum(x[0] for x in rows)), int(sum(x[0] for x in rows[:r]))
+
+
 def odeint_sharded(func, y0_local: torch.Tensor, t: torch.Tensor, *, rtol=1e-7, atol=1e-9, method=None,
                    options: Optional[dict] = None, group=None):
     """odeint over this rank's shard of a trajectory-sharded batch.  Fixed-grid methods need no
     communication; adaptive ones use the global-batch error norm (all ranks, same steps).
+
+    Without autograd, a fused field (fet_ode_amd.autonomous / the plain calDeriv closure) solves
+    in ONE launch per rank with the norms exchanged between the ranks' kernels
+    (fetode_integrate_dopri5_xrank, XRank); otherwise the host-driven loop all-reduces them.
 
     Training through dopri5: the norm's gradient is all-reduced in the backward
     (dopri5._NormAllReduce), so rank r's parameter gradient holds its trajectories' share of

@@ -94,6 +94,10 @@ class _Dopri5:
         self.nfev = 0
         self.attempts = []   # (t0, dt, error_ratio, accepted) like the oracle's Dopri5Trace
 
+    @property
+    def n_attempts(self) -> int:
+        return len(self.attempts)
+
     # func with torchdiffeq's _PerturbFunc (t cast to the state dtype) and _ReverseFunc
     def f(self, t: float, y: torch.Tensor) -> torch.Tensor:
         self.nfev += 1
@@ -394,6 +398,8 @@ def _try_field_resident(func, y0, tp, reversed_, rtol, atol, options):
     from .autograd_ops import build_plan, make_handle, pack_state, unpack_state
     from .odeint import fused_field
     field = fused_field(func)
+    options = dict(options)
+    group = options.pop("norm_group", None)
     if field is None or reversed_ or y0.dim() != 2 or set(options) - _RESIDENT_OPTS:
         return None
     if not (isinstance(rtol, (int, float)) and isinstance(atol, (int, float))):
@@ -404,7 +410,19 @@ def _try_field_resident(func, y0, tp, reversed_, rtol, atol, options):
     dev = y0.device
     B = y0.shape[0]
     handle = make_handle(field, B, dev)
-    if not lib.fetode_fused_supported(handle.ref):
+    xr = None
+    if group is not None:
+        # trajectory-sharded: every rank must take the resident path, or none (their kernels exchange)
+        from . import dist as D
+        grp = None if group == "world" else group
+        ok = (D._RESIDENT_SHARDED[0] and bool(lib.fetode_fused_supported(handle.ref))
+              and B <= lib.fetode_integrate_dopri5_max_batch(handle.ref, 1))
+        agreed = D.resident_agreement(grp, dev, B, ok)
+        if agreed is None:
+            return None
+        B_total, b_off = agreed
+        xr = D.XRank.get(grp, dev)
+    elif not lib.fetode_fused_supported(handle.ref):
         return None
     plan = build_plan(field, handle, dev)
     state, mask = pack_state(field, B, dev)
@@ -425,11 +443,19 @@ def _try_field_resident(func, y0, tp, reversed_, rtol, atol, options):
                      float(options.get("ifactor", 10.0)), float(options.get("dfactor", 0.2)),
                      float(options.get("min_step", 0.0)), float(options.get("max_step", math.inf)),
                      float(options.get("max_num_steps", 2 ** 31 - 1))], dtype=np.float64)
-    rc = lib.fetode_integrate_dopri5(
-        handle.ref, plan.data_ptr(), yc.data_ptr(), B, t_dev.data_ptr(), T, float(rtol), float(atol),
-        opts.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_double)),
-        _TABLEAU.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_float)), sol.data_ptr(), _lib.ptr(state), mask,
-        ws.data_ptr(), stats.data_ptr(), att.data_ptr(), _MAX_TRACE, _lib.stream_handle(dev))
+    optp = opts.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_double))
+    tabp = _TABLEAU.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_float))
+    if xr is not None:
+        xd = xr.desc(b_off)
+        rc = lib.fetode_integrate_dopri5_xrank(
+            handle.ref, plan.data_ptr(), yc.data_ptr(), B, B_total, t_dev.data_ptr(), T, float(rtol), float(atol),
+            optp, tabp, sol.data_ptr(), _lib.ptr(state), mask, ws.data_ptr(), stats.data_ptr(), att.data_ptr(),
+            _MAX_TRACE, _lib.ctypes.byref(xd), _lib.stream_handle(dev))
+    else:
+        rc = lib.fetode_integrate_dopri5(
+            handle.ref, plan.data_ptr(), yc.data_ptr(), B, t_dev.data_ptr(), T, float(rtol), float(atol),
+            optp, tabp, sol.data_ptr(), _lib.ptr(state), mask, ws.data_ptr(), stats.data_ptr(), att.data_ptr(),
+            _MAX_TRACE, _lib.stream_handle(dev))
     if rc == _lib.FETODE_EUNSUPPORTED:   # the grid does not fit one resident launch: host-driven loop
         return None
     _lib.check(rc, "fetode_integrate_dopri5")
@@ -530,12 +556,17 @@ class _Dopri5Grad:
             _lib.require_gpu_tensor(out, "odeint func output")
         return -out if self.sign < 0 else out
 
+    @property
+    def n_attempts(self) -> int:
+        return len(self.attempts)
+
     def rms(self, x, finite_of=None):
         """misc._rms_norm; sharded: RMS over the global batch.  With ``finite_of`` also returns
         whether that tensor is finite on every rank (one collective for both)."""
         if not self.distributed:
+            # single device: the loop-top assert already checked this y (no second read-back)
             r = x.abs().pow(2).mean().sqrt()
-            return r if finite_of is None else (r, bool(torch.isfinite(finite_of).all()))
+            return r if finite_of is None else (r, True)
         bad = torch.zeros((), dtype=torch.float64, device=x.device)
         if finite_of is not None:
             bad = (~torch.isfinite(finite_of)).any().to(torch.float64)

@@ -177,6 +177,40 @@ int fetode_integrate_dopri5(const fetode_field_t* field, const void* plan, const
                             void* stream);
 int64_t fetode_integrate_dopri5_workspace(int64_t B);
 
+/* Trajectory-sharded device-resident dopri5 (one process per GPU, the global batch split into
+ * contiguous shards; SURVEY §8e caveat 2): torchdiffeq's error ratio is an RMS over the WHOLE
+ * batch, so every norm of the solve (the two initial-step norms, each attempt's error norm and
+ * non-finite flag) is summed over the ranks inside the launch: workgroup 0 of each rank writes its
+ * GPU's partial into slot `rank` of every rank's inbox (IPC-mapped device memory, remote stores
+ * over xGMI) and sums the world's records in rank order, so all ranks take the same steps as one
+ * device would on the global batch.  When every rank's shard is whole leaves of the single-device
+ * reduction tree (e.g. equal even shards of 2^k batches) the ranks exchange the leaf sums and the
+ * norms are bitwise the single device's: the same attempts, steps and solution.  Replaces the host loop's per-attempt read-back + all-reduce
+ * (dist.odeint_sharded, norm_group).  Every rank calls it with the same t / tolerances / options
+ * and the same `epoch` (a per-solve counter); B_total = the global batch. */
+typedef struct fetode_xrank {
+  int32_t rank, world;
+  uint32_t epoch;        /* distinct per solve, equal on every rank */
+  void* inbox;           /* (dev) this rank's inbox (fetode_xrank_alloc) */
+  void* const* peers;    /* (dev) array of `world` inbox pointers as mapped in this process */
+  int64_t b_offset;      /* global index of this rank's first trajectory (contiguous shards) */
+} fetode_xrank_t;
+int fetode_integrate_dopri5_xrank(const fetode_field_t* field, const void* plan, const float* y0, int64_t B,
+                                  int64_t B_total, const double* t, int32_t T, double rtol, double atol,
+                                  const double* opts, const float* tableau, float* solution, float* state,
+                                  uint32_t init_mask, void* workspace, int32_t* stats, double* attempts,
+                                  int32_t max_attempts, const fetode_xrank_t* xr, void* stream);
+/* inbox bytes for a world; allocate + export (handle: 64 bytes, hipIpcMemHandle_t), open a peer's
+ * handle in this process, close / free.  Host calls (synchronous). */
+int64_t fetode_xrank_inbox_bytes(int32_t world);
+/* the largest batch one resident dopri5 launch takes on this device (sharded = 1: with the exchange
+ * workgroup), 0 if the field has no resident kernel.  Host call (occupancy query, cached). */
+int64_t fetode_integrate_dopri5_max_batch(const fetode_field_t* field, int32_t sharded);
+int fetode_xrank_alloc(int64_t bytes, void** dev_ptr, void* handle);
+int fetode_xrank_open(const void* handle, void** dev_ptr);
+int fetode_xrank_close(void* dev_ptr);
+int fetode_xrank_free(void* dev_ptr);
+
 /* Standalone module kernels (generic widths). */
 /* KANLinear.forward (efficientkan.py:160-182): x (B,in) -> out (B,out). */
 int fetode_kanlinear_forward(const fetode_kanlinear_t* layer, const float* x, int64_t B, float* out,

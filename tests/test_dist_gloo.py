@@ -171,3 +171,41 @@ def test_allreduce_in_place_on_shared_gradient_buffer():
     exp = torch.arange(10, dtype=torch.float32) * 1.5   # mean of rank 0 (x1) and rank 1 (x2)
     for _, flat, still_view in res:
         assert still_view and torch.equal(flat, exp)
+
+
+def _bcast_worker(rank, world, port, q):
+    import os
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import fet_ode_amd as F
+    import fet_ode_amd.dist as D
+    torch.manual_seed(rank)          # deliberately different weights per rank
+    m = F.KANFET([2, 10, 2], grid_size=5)
+    D.broadcast_parameters(m)
+    q.put((rank, {k: v.clone().numpy() for k, v in m.state_dict().items()}))
+    dist.destroy_process_group()
+
+
+def test_broadcast_parameters_gives_every_rank_rank0_weights():
+    """dist.broadcast_parameters (the efficient_kan init is not bitwise reproducible across
+    processes, so DP ranks take rank 0's weights and buffers)."""
+    import socket
+    import numpy as np
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_bcast_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+        assert p.exitcode == 0
+    for k in res[0]:
+        assert np.array_equal(res[0][k], res[1][k]), k

@@ -1,5 +1,6 @@
 // Microbenchmark: issue cost of v_pk_fma_f32 vs two v_fma_f32 (gfx950), one and two waves per
 // SIMD.  8 independent accumulator chains per lane, N iterations; reports cycles per instruction.
+// Build (not tracked):  hipcc --offload-arch=gfx950 -O3 -o tools/diag/pk_issue tools/diag/pk_issue.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
 typedef float f2 __attribute__((ext_vector_type(2)));
