@@ -257,7 +257,9 @@ def lv_dopri5_sharded_rate(sd, y0d, t, world, B_global, reps=3):
                                        "atol 1e-9, t=linspace(0,3.5,35))",
             "ms_per_solve": el * 1e3, "attempts": s.n_attempts, "nfev": s.nfev,
             "resident": isinstance(s, ResidentSolve), "finite": bool(torch.isfinite(sol).all()),
-            "path": "fetode_integrate_dopri5_xrank: one launch per rank, norms exchanged between the kernels"}
+            "path": ("fetode_integrate_dopri5_xrank: one launch per rank, norms exchanged between the kernels"
+                     if isinstance(s, ResidentSolve) else
+                     "host-driven loop: one field launch per evaluation, one norm all-reduce per attempt")}
 
 
 def plain_closure_rate(model, y0d, t, reps=3):
@@ -436,6 +438,49 @@ def ett_rate(dev, batch=8192, reps=2, substeps=4, cpu_seconds=5.0, with_cpu=True
                                "kind": "port", "sample": f"{n} forward(s) of 8 of the windows with oracle/ett_ref.py "
                                                          f"+ torch_ref.py (torch CPU fp32), {cel * n:.1f} s"}
     return out
+
+
+def ett_dopri5_rate(dev, batch=8192, rtol=1e-3, atol=1e-4):
+    """The reference forecaster's own solver call, odeint(dynamics, z0, t_fut, method="dopri5")
+    (train_kan_fet_ett.py:192), with the KAN-FET latent field [64, 128, 64] (K = 10) on B = 8192
+    96 -> 96 windows.  At torchdiffeq's default rtol 1e-7 / atol 1e-9 the fp32 KAN-FET field needs
+    ~160 k attempts per forward (measured at B = 256: 159 373 attempts, 956 k evaluations, 184 s;
+    DESIGN.md §4.5), so the line runs at rtol 1e-3 / atol 1e-4.  Each evaluation is two fused
+    wide-layer launches; the loop issues the attempts from the host (one status read per
+    attempt): `host_share` = 1 - nfev x (one evaluation's time) / wall."""
+    from fet_ode_amd import ett
+    c = p = 96
+    torch.manual_seed(0)
+    m = ett.LatentNeuralODEForecaster(num_features=7, context_len=c, pred_len=p, latent_dim=64, solver="dopri5",
+                                      rtol=rtol, atol=atol).to(dev)
+    g = torch.Generator().manual_seed(4)
+    series = torch.cumsum(torch.randn(batch + c + p, 7, generator=g), 0) * 0.05
+    ds = ett.EnergyWindowDataset(series, series[:, -1], c, p, device=dev)
+    xb, _ = ds.batch(torch.arange(batch, device=dev))
+    t_fut = torch.linspace(0.0, float(p - 1), steps=p, device=dev)
+    with torch.no_grad():
+        z0 = m.encoder(xb)
+        for _ in range(2):
+            m.dynamics(0.0, z0)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(10):
+            m.dynamics(0.0, z0)
+        torch.cuda.synchronize(dev)
+        ev = (time.perf_counter() - t0) / 10
+        m.dynamics.net.reset_state()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        y = m(xb, t_fut)
+        torch.cuda.synchronize(dev)
+        wall = time.perf_counter() - t0
+    s = F.dopri5.dopri5_solve.last
+    return {"value": batch / wall, "unit": "forecast windows/s forward, dopri5 (96->96, 1 GPU)", "ms_per_batch": wall * 1e3,
+            "rtol": rtol, "atol": atol, "attempts": s.n_attempts, "nfev": s.nfev, "field_eval_ms": ev * 1e3,
+            "host_share": 1.0 - s.nfev * ev / wall, "finite": bool(torch.isfinite(y).all()),
+            "workload": f"LatentNeuralODEForecaster(7 features, 96->96, latent 64, KANFET[64,128,64] K=10), dopri5 "
+                        f"rtol {rtol:g} atol {atol:g}, batch {batch}, synthetic series",
+            "path": "dopri5 host loop; each evaluation = 2 fused wide-layer launches (fetode_wide_layer_forward)"}
 
 
 def ett_encoder_rate(dev, batch=8192, ctx=96, reps=20, with_cpu=True, cpu_seconds=5.0):
@@ -720,6 +765,7 @@ def main():
         if world == 1 and not args.no_ett:
             out["ett"] = ett_rate(dev, batch=args.ett_batch, with_cpu=not args.no_cpu_baseline)
             out["ett"]["encoder"] = ett_encoder_rate(dev, with_cpu=not args.no_cpu_baseline)
+            out["ett"]["dopri5"] = ett_dopri5_rate(dev, batch=args.ett_batch)
         if world == 1 and not args.no_cpu_baseline:
             cb, ref_sol = cpu_baseline(sd, y0, t, args.cpu_solves)
             out["cpu_baseline"] = cb

@@ -40,8 +40,14 @@ using namespace fetode;
 namespace {
 
 constexpr int kSO = 3;  // spline order of the fused kernels (efficientkan default)
-#ifndef FETODE_EXP_SKIP  // diagnostics only (phase-cost attribution): 1 Ferro, 2 edges, 4 logistic,
-#define FETODE_EXP_SKIP 0  // 8 features, 16 d/dx reductions — results are wrong when set
+// FETODE_EXP_SKIP (phase-cost attribution: 1 Ferro, 2 edges, 4 logistic, 8 features, 16 d/dx
+// reductions compiled out — results are wrong when set) exists only in the diagnostic build
+// (make diag EXTRA=-DFETODE_EXP_SKIP=n); the product library is always built with 0.
+#if defined(FETODE_EXP_SKIP) && !defined(FETODE_DIAG)
+#error "FETODE_EXP_SKIP is a diagnostic knob: build it with make diag"
+#endif
+#ifndef FETODE_EXP_SKIP
+#define FETODE_EXP_SKIP 0
 #endif
 
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -1147,9 +1153,13 @@ struct BwdEntry {
 const BwdEntry kBwd[] = {
     // LV KAN-FET [2,10,2]: one kernel, two trajectories per wave (measured: TPW 1 / 2 / 4 = 1034 / 897 /
     // 1203 us at B = 4096); the split structure as the alternative
+#ifdef FETODE_DIAG   // the split structure (measured slower) lives in the diagnostic build only
     {2, 10, 10, 10, 12, true, 2, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 2>,
      fixed_bwd_kernel<2, 10, 10, 10, 12, true, false, 1>, param_sum_kernel<2, 10, 10, 10, 12, 0>,
      param_sum_kernel<2, 10, 10, 10, 12, 1>},
+#else
+    {2, 10, 10, 10, 12, true, 2, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 2>, nullptr, nullptr, nullptr},
+#endif
     // LV KAN [2,10,2] (126 VGPRs: four waves per SIMD already)
     {2, 10, 0, 10, 12, false, 1, fixed_bwd_kernel<2, 10, 1, 10, 12, false, true, 1>, nullptr, nullptr, nullptr},
 };
@@ -1210,10 +1220,18 @@ void layouts(const fetode_field_t* f, AccLayout* L0, AccLayout* L1) {
 extern "C" {
 
 int fetode_backward_set_split(int32_t enable) {
+#ifndef FETODE_DIAG
+  if (enable > 0) {   // the split sweep is compiled into the diagnostic build only
+    set_err(FETODE_EUNSUPPORTED, "the split backward is a diagnostic path (make diag)");
+    return -2;
+  }
+  return 0;
+#else
   use_split(&kBwd[0]);  // resolve the env default first
   const int prev = g_bwd_split;
   if (enable >= 0) g_bwd_split = enable != 0;
   return prev;
+#endif
 }
 
 int fetode_fused_backward_supported(const fetode_field_t* f) {

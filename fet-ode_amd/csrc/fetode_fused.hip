@@ -14,6 +14,9 @@
 #include <type_traits>
 
 #include "fetode_common.h"
+#if (defined(FETODE_EXP_NO_GRIDSUM) || defined(FETODE_EXP_NO_EVAL)) && !defined(FETODE_DIAG)
+#error "FETODE_EXP_NO_GRIDSUM / FETODE_EXP_NO_EVAL are diagnostic knobs: build them with make diag"
+#endif
 
 using namespace fetode;
 

@@ -230,7 +230,11 @@ __global__ void column_sum_final_kernel(const double* __restrict__ mid, int n, f
 // profiles/r02_mnist_pmc.txt); the feature error stays ~1e-7 relative, far inside the 1e-5 test
 // bar on the 1568 x 17-term sums.
 // =============================================================================================
-#ifndef FETODE_WIDE_SKIP  // diagnostics only (timing attribution; results wrong when set)
+// FETODE_WIDE_SKIP (timing attribution; results wrong when set): diagnostic build only (make diag)
+#if defined(FETODE_WIDE_SKIP) && !defined(FETODE_DIAG)
+#error "FETODE_WIDE_SKIP is a diagnostic knob: build it with make diag"
+#endif
+#ifndef FETODE_WIDE_SKIP
 #define FETODE_WIDE_SKIP 0
 #endif
 #ifndef FETODE_WIDE_CH

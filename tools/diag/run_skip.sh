@@ -1,6 +1,6 @@
 #!/bin/bash
 # Phase-cost attribution of the reverse sweep: fixed_bwd time with each FETODE_EXP_SKIP variant
-# (built by: make OBJDIR=build_x$n OUT=../libfetode_x$n.so EXTRA=-DFETODE_EXP_SKIP=$n).
+# (built by: make OBJDIR=build_x$n OUT=../libfetode_x$n.so EXTRA="-DFETODE_DIAG -DFETODE_EXP_SKIP=$n").
 cd "$(dirname "$0")/../.."
 export TMPDIR=/tmp
 for n in 0 ${SKIPS:-1 2 4 8 16}; do

@@ -3,7 +3,7 @@
 # the rocprofv3 kernel-trace stats of a short bench.  Every step has its own time limit; a step
 # that crashes / times out (rc > 1) ends the call.
 cd "$(dirname "$0")/.."
-R=${ROUND:-r02}
+R=${ROUND:-r03}
 O=gpurun_out; mkdir -p $O
 export TMPDIR=/tmp
 step() { local name=$1; shift; "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; [ $rc -le 1 ] || exit $rc; return 0; }
@@ -16,4 +16,4 @@ step bench timeout -k 10 600 python bench.py
 tail -1 $O/bench.log > $O/bench_$R.json
 cat $O/bench_$R.json
 [ -n "$NO_PROF" ] && exit 0
-step prof_stats timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$R -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --ett-batch 1024 --train-iters 5
+step prof_stats timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$R -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --train-iters 5
