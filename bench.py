@@ -223,7 +223,7 @@ def lv_dopri5_rate(sd, y0d, t, reps=3):
             "ms_per_solve": el * 1e3, "attempts": s.n_attempts, "accepted": acc, "nfev": s.nfev,
             "field_evals_per_s": s.nfev / el, "rk4_equiv_steps_per_s": s.nfev / 4 / el,
             "resident": isinstance(s, ResidentSolve), "finite": bool(torch.isfinite(sol).all()),
-            "path": "fetode_integrate_dopri5: fused4_kernel DOPRI instantiation, one cooperative launch"}
+            "path": "fetode_integrate_dopri5: fused4_kernel DOPRI instantiation, one launch"}
 
 
 def lv_dopri5_sharded_rate(sd, y0d, t, world, B_global, reps=3):

@@ -141,9 +141,10 @@ SIGNATURES = {
     "fetode_lincomb": (ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_float), ctypes.c_int32,
                                       _vp, ctypes.c_int64, _vp]),
     "fetode_scaled_rms": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_int64,
-                                         _vp, _vp]),
+                                         _vp, _vp, _vp]),
+    "fetode_scaled_rms_workspace": (ctypes.c_int64, [ctypes.c_int64]),
     "fetode_scaled_sumsq": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_int64,
-                                           _vp, _vp]),
+                                           _vp, _vp, _vp]),
     "fetode_interp_fit": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_float),
                                          ctypes.c_float, _vp, ctypes.c_int64, _vp]),
     "fetode_interp_eval": (ctypes.c_int, [_vp, ctypes.c_float, _vp, ctypes.c_int64, _vp]),

@@ -62,6 +62,77 @@ __global__ void scaled_rms_kernel(const float* __restrict__ a, const float* __re
   }
 }
 
+// The same sum over many workgroups (a single workgroup is load-latency-bound: 0.33 ms at n = 524 288,
+// the ETT latent batch): workgroup g sums its contiguous slice [g S, (g + 1) S) (a strided loop per
+// thread, then a fixed tree), writes an fp64 partial, and the last workgroup to arrive sums the
+// partials in index order — deterministic, independent of arrival order.  ws: kRmsMaxGroups
+// (partial, bad) pairs + one arrival counter (zero between calls: the last workgroup resets it).
+constexpr int kRmsMaxGroups = 512;
+constexpr int kRmsThreads = 256;
+template <bool RMS>
+__global__ __launch_bounds__(kRmsThreads) void scaled_rms_grid_kernel(
+    const float* __restrict__ a, const float* __restrict__ sub, const float* __restrict__ y0,
+    const float* __restrict__ y1, float rtol, float atol, int64_t n, int64_t slice, double* __restrict__ ws,
+    void* __restrict__ out_) {
+  __shared__ double red[kRmsThreads];
+  __shared__ int bad, last;
+  if (threadIdx.x == 0) bad = 0;
+  __syncthreads();
+  const int64_t lo = (int64_t)blockIdx.x * slice, hi = lo + slice < n ? lo + slice : n;
+  double s = 0.0;
+  int nf = 0;
+  for (int64_t t = lo + threadIdx.x; t < hi; t += kRmsThreads) {
+    nf |= !__builtin_isfinite(y0[t]);
+    const float v = sub ? a[t] - sub[t] : a[t];
+    const float m = y1 ? fmaxf(fabsf(y0[t]), fabsf(y1[t])) : fabsf(y0[t]);
+    const float q = v / (atol + rtol * m);
+    s += (double)q * (double)q;
+  }
+  red[threadIdx.x] = s;
+  if (nf) atomicOr(&bad, 1);
+  __syncthreads();
+  for (int w = kRmsThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  unsigned* cnt = reinterpret_cast<unsigned*>(ws + 2 * kRmsMaxGroups);
+  if (threadIdx.x == 0) {
+    ws[2 * blockIdx.x] = red[0];
+    ws[2 * blockIdx.x + 1] = bad ? 1.0 : 0.0;
+    __threadfence();
+    last = atomicAdd(cnt, 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();
+  // the last workgroup: partials in index order (thread i sums i, i + 256, ..; then the tree)
+  double p = 0.0, b = 0.0;
+  for (unsigned g = threadIdx.x; g < gridDim.x; g += kRmsThreads) {
+    p += __hip_atomic_load(&ws[2 * g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    b += __hip_atomic_load(&ws[2 * g + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  red[threadIdx.x] = p;
+  __syncthreads();
+  for (int w = kRmsThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (b != 0.0) atomicOr(&bad, 1);   // (bad was this workgroup's own flag: OR the others' in)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if constexpr (RMS) {
+      float* out = static_cast<float*>(out_);
+      out[0] = sqrtf((float)(red[0] / (double)n));
+      out[1] = bad ? 1.0f : 0.0f;
+    } else {
+      double* out = static_cast<double*>(out_);
+      out[0] = red[0];
+      out[1] = bad ? 1.0 : 0.0;
+    }
+    *cnt = 0u;   // ready for the next call on this workspace
+  }
+}
+
 // interp._interp_fit with y_mid = y0 + k . (dt * mid); coeffs (5, n) = [e, d, c, b, a]
 __global__ void interp_fit_kernel(const float* __restrict__ y0, const float* __restrict__ y1,
                                   const float* __restrict__ k, int64_t kstride, Coef8 mid, float dt,
@@ -95,6 +166,25 @@ __global__ void interp_eval_kernel(const float* __restrict__ co, float x, float*
   out[t] = total;
 }
 
+template <bool RMS>
+int scaled_norm(const float* a, const float* sub, const float* y0, const float* y1, double rtol, double atol,
+                       int64_t n, void* out, void* workspace, hipStream_t s) {
+  // small n or no workspace: one workgroup; else workgroups of >= 2048 elements, at most 512
+  const int64_t groups = (n + 2047) / 2048;
+  if (!workspace || groups <= 1) {
+    hipLaunchKernelGGL(scaled_rms_kernel<RMS>, dim3(1), dim3(1024), 0, s, a, sub, y0, y1, (float)rtol, (float)atol, n,
+                       out);
+  } else {
+    const int g = (int)(groups < kRmsMaxGroups ? groups : kRmsMaxGroups);
+    const int64_t slice = (n + g - 1) / g;
+    const int gg = (int)((n + slice - 1) / slice);
+    hipLaunchKernelGGL(scaled_rms_grid_kernel<RMS>, dim3((unsigned)gg), dim3(kRmsThreads), 0, s, a, sub, y0, y1,
+                       (float)rtol, (float)atol, n, slice, (double*)workspace, out);
+  }
+  LAUNCH_CHECK();
+  return FETODE_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -111,25 +201,24 @@ int fetode_lincomb(const float* y0, const float* k, int64_t kstride, const float
   return FETODE_OK;
 }
 
+int64_t fetode_scaled_rms_workspace(int64_t n) {
+  (void)n;
+  return (int64_t)sizeof(double) * (2 * kRmsMaxGroups + 1);
+}
+
 int fetode_scaled_rms(const float* a, const float* sub, const float* y0, const float* y1, double rtol, double atol,
-                      int64_t n, float* out, void* stream) {
+                      int64_t n, float* out, void* workspace, void* stream) {
   if (n <= 0 || !a || !y0 || !out) return set_err(FETODE_EINVAL, "scaled_rms: bad arguments");
-  hipLaunchKernelGGL(scaled_rms_kernel<true>, dim3(1), dim3(1024), 0, (hipStream_t)stream, a, sub, y0, y1,
-                     (float)rtol, (float)atol, n, (void*)out);
-  LAUNCH_CHECK();
-  return FETODE_OK;
+  return scaled_norm<true>(a, sub, y0, y1, rtol, atol, n, out, workspace, (hipStream_t)stream);
 }
 
 int fetode_scaled_sumsq(const float* a, const float* sub, const float* y0, const float* y1, double rtol, double atol,
-                        int64_t n, double* out, void* stream) {
+                        int64_t n, double* out, void* workspace, void* stream) {
   if (n < 0 || !out || (n > 0 && (!a || !y0))) return set_err(FETODE_EINVAL, "scaled_sumsq: bad arguments");
   if (n == 0) return hipMemsetAsync(out, 0, 2 * sizeof(double), (hipStream_t)stream) == hipSuccess
                          ? FETODE_OK
                          : set_err(FETODE_EHIP, "scaled_sumsq: memset failed");
-  hipLaunchKernelGGL(scaled_rms_kernel<false>, dim3(1), dim3(1024), 0, (hipStream_t)stream, a, sub, y0, y1,
-                     (float)rtol, (float)atol, n, (void*)out);
-  LAUNCH_CHECK();
-  return FETODE_OK;
+  return scaled_norm<false>(a, sub, y0, y1, rtol, atol, n, out, workspace, (hipStream_t)stream);
 }
 
 int fetode_interp_fit(const float* y0, const float* y1, const float* k, int64_t kstride, const float* mid_dt,

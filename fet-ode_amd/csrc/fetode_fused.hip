@@ -295,9 +295,14 @@ __device__ bool grid_sum2(const DopriParams& P, unsigned& round, double v0, doub
     s1 = v1;
     return false;
   }
-  // leaf x = global workgroups [x L, x L + nx) (contiguous; the same leaves on one device and sharded)
-  const unsigned sh = (unsigned)P.leaf_shift, L = 1u << sh, gb = blk + (unsigned)P.wg_off, x = gb >> sh;
-  const unsigned nx = min(L, (unsigned)P.nblk_global - (x << sh));
+  // leaves in GLOBAL workgroup numbers: blocks of 8 L consecutive workgroups, each split by
+  // workgroup % 8 into 8 leaves of L — a leaf's workgroups all run on one XCD (workgroups are dealt
+  // to the 8 XCDs round-robin; rank offsets are multiples of 8 L), so its partials and counter stay
+  // in that XCD's L2, and a block is whole on one rank in a sharded solve
+  const unsigned sh = (unsigned)P.leaf_shift, L = 1u << sh, gb = blk + (unsigned)P.wg_off;
+  const unsigned x = ((gb >> (sh + 3u)) << 3u) | (gb & 7u);
+  const unsigned first = ((x >> 3u) << (sh + 3u)) + (x & 7u);
+  const unsigned nx = min(L, ((unsigned)P.nblk_global - first + 7u) >> 3u);
   const unsigned ngrp = (unsigned)P.n_leaf_local;
   const unsigned r = round++;
   double* xs = P.xs + 2 * kDpGroups * (r & 1u);
@@ -318,7 +323,7 @@ __device__ bool grid_sum2(const DopriParams& P, unsigned& round, double v0, doub
     double a0 = 0.0, a1 = 0.0;
     for (unsigned j = lane; j < nx; j += 64) {
       double u0, u1;
-      dp_ld16(&P.slot[2 * ((x << sh) + j - (unsigned)P.wg_off)], u0, u1);
+      dp_ld16(&P.slot[2 * (first + (j << 3u) - (unsigned)P.wg_off)], u0, u1);
       a0 += u0;
       a1 += u1;
     }
@@ -1656,10 +1661,16 @@ static int dopri5_launch(const fetode_field_t* f, const void* plan, const float*
   // leaves: runs of L workgroups; exact when this rank's workgroups are whole leaves of the
   // single-device grid over the global batch (two trajectories per workgroup everywhere)
   auto cdiv = [](int64_t a_, int64_t b_) { return (a_ + b_ - 1) / b_; };
-  auto lshift = [&](int64_t nb) {   // the smallest power-of-two run that needs <= kDpGroups leaves
+  auto lshift = [&](int64_t nb) {   // the smallest power-of-two leaf that needs <= kDpGroups leaves
     int sh = 0;
     while ((int64_t)kDpGroups << sh < nb) ++sh;
     return sh;
+  };
+  // leaves of `n` workgroups from a block boundary: full blocks of 8 leaves, then the last block's
+  // leaves that have at least one workgroup (a prefix of its 8)
+  auto nleaves = [&](int64_t n, int sh) -> int64_t {
+    const int64_t blk = (int64_t)8 << sh, nb = cdiv(n, blk);
+    return nb == 0 ? 0 : 8 * (nb - 1) + std::min<int64_t>(8, n - (nb - 1) * blk);
   };
   P.xr_exact = 0;
   P.wg_off = 0;
@@ -1671,9 +1682,9 @@ static int dopri5_launch(const fetode_field_t* f, const void* plan, const float*
     P.xr_epoch = xr->epoch;
     P.xr_peers = (double* const*)xr->peers;
     P.xr_inbox = (double*)xr->inbox;
-    const int64_t gg = cdiv(B_total, 2), shg = lshift(gg), Lg = (int64_t)1 << shg, off = xr->b_offset / 2;
+    const int64_t gg = cdiv(B_total, 2), shg = lshift(gg), Bk = (int64_t)8 << shg, off = xr->b_offset / 2;
     const bool last = xr->b_offset + B == B_total;
-    if (xr->b_offset % 2 == 0 && (B % 2 == 0 || last) && off % Lg == 0 && ((off + grid) % Lg == 0 || last)) {
+    if (xr->b_offset % 2 == 0 && (B % 2 == 0 || last) && off % Bk == 0 && ((off + grid) % Bk == 0 || last)) {
       P.xr_exact = 1;
       P.wg_off = (int32_t)off;
       P.nblk_global = (int32_t)gg;
@@ -1682,9 +1693,9 @@ static int dopri5_launch(const fetode_field_t* f, const void* plan, const float*
   } else {
     P.xr_world = 1;
   }
-  P.leaf_lo = P.wg_off >> P.leaf_shift;
-  P.n_leaf_local = (int32_t)cdiv(grid, (int64_t)1 << P.leaf_shift);
-  P.n_leaf_global = (int32_t)cdiv(P.nblk_global, (int64_t)1 << P.leaf_shift);
+  P.leaf_lo = (P.wg_off >> (P.leaf_shift + 3)) * 8;
+  P.n_leaf_local = (int32_t)nleaves(grid, P.leaf_shift);
+  P.n_leaf_global = (int32_t)nleaves(P.nblk_global, P.leaf_shift);
   layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
   layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
   a.factor_limit = kFactorLimit;

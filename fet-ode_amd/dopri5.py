@@ -52,6 +52,19 @@ def _cfloat(arr):
     return a, a.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_float))
 
 
+_RMS_WS = {}
+atexit.register(_RMS_WS.clear)
+
+
+def _rms_workspace(dev):
+    """The norms' multi-workgroup workspace (zeroed once; the kernel leaves it zero), one per device."""
+    ws = _RMS_WS.get(dev)
+    if ws is None:
+        n = _lib.load().fetode_scaled_rms_workspace(0)
+        ws = _RMS_WS[dev] = torch.zeros(max(1, n // 8), device=dev, dtype=torch.float64)
+    return ws
+
+
 class _Dopri5:
     def __init__(self, func, y0, rtol, atol, options, reversed_):
         unsupported = [k for k in ("step_t", "jump_t", "norm", "perturb") if options.get(k) is not None]
@@ -77,6 +90,7 @@ class _Dopri5:
         self.max_num_steps = int(options.get("max_num_steps", 2 ** 31 - 1))
         self.k = torch.empty(7, self.n, device=self.dev, dtype=torch.float32)
         self.scal = torch.empty(2, device=self.dev, dtype=torch.float32)
+        self.rms_ws = _rms_workspace(self.dev)
         self.n_global = self.n
         if self.group is not None:
             import torch.distributed as dist
@@ -126,15 +140,15 @@ class _Dopri5:
             # like the single-device kernel: sqrtf((float)(sum / n))
             _lib.check(self.lib.fetode_scaled_sumsq(a.data_ptr(), _lib.ptr(sub), y0.data_ptr(), _lib.ptr(y1),
                                                     self.rtol, self.atol, self.n, self.scal64.data_ptr(),
-                                                    self.stream), "fetode_scaled_sumsq")
+                                                    self.rms_ws.data_ptr(), self.stream), "fetode_scaled_sumsq")
             t = self.scal64.cpu() if self.cpu_reduce else self.scal64
             self.dist.all_reduce(t, group=self.group)
             ssum, bad = t.tolist()
             r = np.sqrt(np.float32(ssum / self.n_global))
         else:
             _lib.check(self.lib.fetode_scaled_rms(a.data_ptr(), _lib.ptr(sub), y0.data_ptr(), _lib.ptr(y1),
-                                                  self.rtol, self.atol, self.n, self.scal.data_ptr(), self.stream),
-                       "fetode_scaled_rms")
+                                                  self.rtol, self.atol, self.n, self.scal.data_ptr(),
+                                                  self.rms_ws.data_ptr(), self.stream), "fetode_scaled_rms")
             r, bad = self.scal.tolist()           # one device->host read per call
         if check_finite and bad:
             raise AssertionError("non-finite values in state `y`")

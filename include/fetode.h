@@ -249,12 +249,15 @@ int fetode_lincomb(const float* y0, const float* k, int64_t kstride, const float
  * scaled error (sub, y1 nullable: _select_initial_step's scale = atol + |y0|*rtol);
  * out[1] = 1 if y0 holds a non-finite value (torchdiffeq's per-step assertion), else 0. */
 int fetode_scaled_rms(const float* a, const float* sub, const float* y0, const float* y1,
-                      double rtol, double atol, int64_t n, float* out, void* stream);
+                      double rtol, double atol, int64_t n, float* out, void* workspace, void* stream);
+/* workspace for both norms (zeroed once by the caller, kept zero by the kernel): the sum then runs
+ * over up to 512 workgroups with a fixed-order combination (NULL: one workgroup). */
+int64_t fetode_scaled_rms_workspace(int64_t n);
 /* The same scaled error as fetode_scaled_rms, unreduced across devices: out[0] (dev, fp64) =
  * sum of squares, out[1] = non-finite flag.  A trajectory-sharded dopri5 all-reduces these two
  * words so every rank takes the global-batch RMS norm of torchdiffeq (SURVEY §8e caveat 2). */
 int fetode_scaled_sumsq(const float* a, const float* sub, const float* y0, const float* y1,
-                        double rtol, double atol, int64_t n, double* out, void* stream);
+                        double rtol, double atol, int64_t n, double* out, void* workspace, void* stream);
 /* interp._interp_fit: coeffs (5, n) = [e, d, c, b, a]; y_mid = y0 + k . mid_dt (7 host floats). */
 int fetode_interp_fit(const float* y0, const float* y1, const float* k, int64_t kstride,
                       const float* mid_dt, float dt, float* coeffs, int64_t n, void* stream);
