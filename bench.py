@@ -156,45 +156,69 @@ def train_rate(model, y0d, t, iters, warmup, world, strong=True):
     """One training iteration = forward rk4 solve with autograd (one launch that also records the
     layer inputs of every evaluation) + backward (one reverse-sweep launch + fixed-order gradient
     reduction) + gradient all-reduce (RCCL when world > 1) + Adam.  Adam runs as
-    torch's fused multi-tensor kernel (same update rule as the reference's torch.optim.Adam)."""
+    torch's fused multi-tensor kernel (same update rule as the reference's torch.optim.Adam).
+    On one GPU the iteration is captured once and replayed as ONE HIP graph
+    (fet_ode_amd.training.CapturedStep: bitwise the eager iterations); `eager` times the same
+    iteration issued op by op from Python (host-bound on a slow host).  N > 1 stays eager (the
+    all-reduce is not captured)."""
+    import copy
     import fet_ode_amd.dist as D
+    from fet_ode_amd.training import CapturedStep
     dev = y0d.device
-    func = F.autonomous(model)
-    try:
-        opt = torch.optim.Adam(model.parameters(), lr=1e-4, fused=True)
-    except (RuntimeError, TypeError):
-        opt = torch.optim.Adam(model.parameters(), lr=1e-4)
     target = torch.zeros(T, y0d.shape[0], 2, device=dev)
 
-    def it():
-        opt.zero_grad(set_to_none=True)
-        sol = F.odeint(func, y0d, t, method="rk4")
-        loss = (sol - target).square().mean()
-        loss.backward()
-        D.allreduce_gradients(list(model.parameters()))
-        opt.step()
+    def make(m, capturable):
+        func = F.autonomous(m)
+        opt = torch.optim.Adam(m.parameters(), lr=1e-4, fused=True, capturable=capturable)
 
+        def it():
+            opt.zero_grad(set_to_none=False)
+            sol = F.odeint(func, y0d, t, method="rk4")
+            loss = (sol - target).square().mean()
+            loss.backward()
+            D.allreduce_gradients(list(m.parameters()))
+            opt.step()
+        return it
+
+    def timed(fn, n):
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            torch.distributed.barrier()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            torch.distributed.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            nccl = torch.distributed.get_backend() == "nccl"
+            tt = torch.tensor([el], device=dev if nccl else "cpu", dtype=torch.float64)
+            torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
+            el = tt.item()
+        return el
+
+    eager_model = copy.deepcopy(model) if world == 1 else model
+    it = make(eager_model, False)
     for _ in range(warmup):
         it()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        torch.distributed.barrier()
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        it()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        torch.distributed.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        nccl = torch.distributed.get_backend() == "nccl"
-        tt = torch.tensor([el], device=dev if nccl else "cpu", dtype=torch.float64)
-        torch.distributed.all_reduce(tt, op=torch.distributed.ReduceOp.MAX)
-        el = tt.item()
-    return {"value": (1 if strong else world) * iters * STEPS_PER_SOLVE / el,
-            "unit": "RK4 steps/s trained (fwd+bwd+allreduce+Adam) of the batch-4096 job",
-            "ms_per_iter": el / iters * 1e3, "iters": iters,
-            "path": "fused: fetode_integrate_fixed with tape + fetode_integrate_fixed_backward (one launch each)"}
+    el_eager = timed(it, iters)
+    scale = (1 if strong else world) * iters * STEPS_PER_SOLVE
+    out = {"unit": "RK4 steps/s trained (fwd+bwd+allreduce+Adam) of the batch-4096 job", "iters": iters,
+           "eager": {"value": scale / el_eager, "ms_per_iter": el_eager / iters * 1e3,
+                     "path": "host-issued: fetode_integrate_fixed with tape + fetode_integrate_fixed_backward "
+                             "+ loss ops + fused Adam, op by op"}}
+    if world == 1:
+        step = CapturedStep(make(copy.deepcopy(model), True), warmup=warmup, device=dev)
+        el = timed(step, iters)
+        out.update({"value": scale / el, "ms_per_iter": el / iters * 1e3,
+                    "path": "one HIP graph replay per iteration (fet_ode_amd.training.CapturedStep) of the same "
+                            "launches: fetode_integrate_fixed with tape + fetode_integrate_fixed_backward + loss + "
+                            "fused Adam"})
+    else:
+        out.update({"value": out["eager"]["value"], "ms_per_iter": out["eager"]["ms_per_iter"],
+                    "path": out["eager"]["path"]})
+    return out
 
 
 def lv_dopri5_rate(sd, y0d, t, reps=3):

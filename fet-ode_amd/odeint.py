@@ -154,7 +154,19 @@ class Schedule:
 _SCHED_CACHE: Dict[tuple, Schedule] = {}
 
 
+_LAST_SCHED = [None, None, None, None]   # tp object, step_size, reversed_, schedule
+
+
 def get_schedule(tp, step_size, reversed_) -> Schedule:
+    # the cached input check hands back the same tp object while t is unchanged: skip the key
+    if _LAST_SCHED[0] is tp and _LAST_SCHED[1] == step_size and _LAST_SCHED[2] == reversed_:
+        return _LAST_SCHED[3]
+    s = _get_schedule(tp, step_size, reversed_)
+    _LAST_SCHED[:] = [tp, step_size, reversed_, s]
+    return s
+
+
+def _get_schedule(tp, step_size, reversed_) -> Schedule:
     key = (tp.dtype, tuple(tp.tolist()), step_size, reversed_)
     s = _SCHED_CACHE.get(key)
     if s is None:
@@ -214,9 +226,9 @@ class _FusedFixedFn(torch.autograd.Function):
         gy0 = torch.empty(B, g.shape[-1], device=dev, dtype=torch.float32) if ctx.needs_input_grad[3] else None
         want = ctx.needs_input_grad[6:]
         params = list(field.parameters())
-        # every wanted gradient is a view of ONE flat buffer, in parameter order: autograd hands
-        # the views over as .grad, and dist.allreduce_gradients then reduces the buffer in place
-        # (no flatten / unflatten copies per iteration)
+        # every wanted gradient is a view of ONE flat buffer, in parameter order; where autograd
+        # keeps the views as .grad, dist.allreduce_gradients reduces the buffer in place, else
+        # (grads accumulated into existing .grad tensors) it flattens them once (12 KB)
         wp = [p for p, w in zip(params, want) if w]
         flat = torch.empty(sum(p.numel() for p in wp), device=dev, dtype=torch.float32)
         grads, off = {}, 0
@@ -553,6 +565,7 @@ _LAST_T = [None, None, None, None]   # the last t tensor, its version, method, c
 
 def _clear_last_t():
     _LAST_T[:] = [None] * 4
+    _LAST_SCHED[:] = [None] * 4
 
 
 atexit.register(_clear_last_t)   # before the runtime's teardown

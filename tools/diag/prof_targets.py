@@ -1,7 +1,7 @@
 """Small driver for rocprofv3 PMC passes: the wide KAN-FET layer kernels at the ETT widths
 (B = 8192), the MNIST KANLinear head (B = 8192), the LV rk4 solve at the strong-scaling shard
-(B = 512, v6) and the full batch (B = 4096, v4), and the LV training step (B = 4096 rk4 forward
-with tape + the fused reverse sweep), a few launches each.  argv[1] / $PROF_WHICH selects one."""
+(B = 512, v6) and the full batch (B = 4096, v4), the LV training step (B = 4096 rk4 forward
+with tape + the fused reverse sweep) and the ETT KAN-RNN encoder (B = 8192), a few launches each.  argv[1] / $PROF_WHICH selects one."""
 import os
 import sys
 
@@ -53,5 +53,17 @@ if which in ("all", "train"):
     for _ in range(4):
         m.zero_grad()
         F.odeint(F.autonomous(m), y0, t, method="rk4").square().mean().backward()
+    torch.cuda.synchronize()
+if which in ("all", "enc"):   # the ETT KAN-RNN encoder at the bench size: forward (cone), training step
+    from fet_ode_amd import ett
+    torch.manual_seed(0)
+    enc = ett.KANRNNEncoder(7, 64, 64, 10).to(dev)
+    xe = torch.cumsum(torch.randn(8192, 96, 7, device=dev), 1) * 0.1
+    with torch.no_grad():
+        for _ in range(4):
+            enc(xe)
+    for _ in range(3):
+        enc.zero_grad(set_to_none=True)
+        enc(xe).square().mean().backward()
     torch.cuda.synchronize()
 print("done")
