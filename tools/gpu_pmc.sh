@@ -5,7 +5,7 @@
 #  (2) tools/pmc_kernels.sh over tools/diag/prof_targets.py (wide ETT layers, MNIST head, training
 #      step) -> a per-kernel summary.
 cd "$(dirname "$0")/.."
-R=${ROUND:-r02}
+R=${ROUND:-r03}
 O=gpurun_out
 mkdir -p $O profiles
 export TMPDIR=/tmp

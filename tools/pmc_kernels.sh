@@ -4,7 +4,7 @@
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 O=gpurun_out; mkdir -p $O
-TAG=${TAG:-r02}
+TAG=${TAG:-r03}
 timeout -s KILL 60 rocprofv3 -L > $O/rocprof_counters.txt 2>&1 || true
 pass() { local name=$1; shift; timeout -s KILL 120 rocprofv3 --kernel-trace --pmc "$@" -d $O/pmc_${TAG}_$name -o run --output-format csv -- python3 tools/diag/prof_targets.py ${PROF_WHICH:-all} > $O/pmc_${TAG}_$name.log 2>&1; echo "pass $name rc=$?"; }
 pass a SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU
