@@ -153,6 +153,15 @@ SIGNATURES = {
                                                  ctypes.POINTER(KANLinearGrad), _vp, ctypes.c_int32, _vp]),
     "fetode_ferro_backward": (ctypes.c_int, [ctypes.POINTER(FerroDesc), _vp, ctypes.c_int64, _vp, ctypes.c_int32,
                                              _vp, _vp, ctypes.POINTER(FerroGrad), ctypes.c_int32, _vp]),
+    "fetode_kanlinear_backward_wide_workspace": (ctypes.c_int64, [ctypes.POINTER(KANLinearDesc),
+                                                                  ctypes.POINTER(FerroDesc), ctypes.c_int64]),
+    "fetode_kanlinear_backward_wide": (ctypes.c_int, [ctypes.POINTER(KANLinearDesc), ctypes.POINTER(FerroDesc), _vp,
+                                                      _vp, ctypes.c_int64, _vp, _vp, ctypes.POINTER(KANLinearGrad),
+                                                      ctypes.c_int32, _vp, _vp]),
+    "fetode_ferro_backward_wide_workspace": (ctypes.c_int64, [ctypes.POINTER(FerroDesc), ctypes.c_int64]),
+    "fetode_ferro_backward_wide": (ctypes.c_int, [ctypes.POINTER(FerroDesc), _vp, _vp, ctypes.c_int64, _vp,
+                                                  ctypes.c_int32, _vp, _vp, ctypes.POINTER(FerroGrad),
+                                                  ctypes.c_int32, _vp, _vp]),
     "fetode_fused_backward_supported": (ctypes.c_int, [ctypes.POINTER(FieldDesc)]),
     "fetode_backward_set_split": (ctypes.c_int, [ctypes.c_int32]),
     "fetode_integrate_fixed_backward_workspace": (ctypes.c_int64, [ctypes.POINTER(FieldDesc), ctypes.c_int32,

@@ -115,7 +115,45 @@ class _KANLinearFn(torch.autograd.Function):
 
 
 def kan_backward(mod, xc, grad, want_x, want_params, gx_accum=None):
-    """HIP VJP of KANLinear: returns (gx, [grad per KAN_PARAM_NAMES or None])."""
+    """HIP VJP of KANLinear: returns (gx, [grad per KAN_PARAM_NAMES or None]).  At the wide-layer
+    widths with 64 / 128 outputs (ETT / ECG fields) the MFMA VJP (fetode_kanlinear_backward_wide);
+    otherwise the generic kernels."""
+    if mod.out_features in (64, 128) and mod.in_features >= 16 and (want_x or any(want_params)):
+        r = _kan_backward_wide(mod, xc, grad, want_x, want_params, gx_accum)
+        if r is not None:
+            return r
+    return _kan_backward_generic(mod, xc, grad, want_x, want_params, gx_accum)
+
+
+def _kan_backward_wide(mod, xc, grad, want_x, want_params, gx_accum=None):
+    entry = wide_plan(mod, None, xc.device)
+    if entry is None:
+        return None
+    plan, kd, _, _ = entry
+    lib = _lib.load()
+    B = xc.shape[0]
+    g = _lib.f32c(grad)
+    if g.data_ptr() % 16:
+        g = g.clone()
+    gx = None
+    if want_x:
+        gx = torch.empty_like(xc) if gx_accum is None else gx_accum
+    alloc = torch.empty_like if gx_accum is None else torch.zeros_like
+    grads = [alloc(p) if (p is not None and w) else None for p, w in zip(kan_params(mod), want_params)]
+    any_param = any(t is not None for t in grads)
+    gstruct = _lib.KANLinearGrad(*[_lib.ptr(t) for t in grads]) if any_param else None
+    nb = lib.fetode_kanlinear_backward_wide_workspace(_lib.ctypes.byref(kd), None, B)
+    if nb < 0:
+        return None
+    ws = torch.empty(max(1, nb // 4), device=xc.device, dtype=torch.float32)
+    _lib.check(lib.fetode_kanlinear_backward_wide(
+        _lib.ctypes.byref(kd), None, plan.data_ptr(), xc.data_ptr(), B, g.data_ptr(), _lib.ptr(gx),
+        _lib.ctypes.byref(gstruct) if any_param else None, int(gx_accum is not None), ws.data_ptr(), _stream(xc)),
+        "KANLinear backward (wide)")
+    return gx, grads
+
+
+def _kan_backward_generic(mod, xc, grad, want_x, want_params, gx_accum=None):
     lib = _lib.load()
     keep = []
     d = mod.desc(keep)
@@ -189,6 +227,17 @@ class _FerroFn(torch.autograd.Function):
 
 
 def ferro_backward(mod, xc, prev, reinit, bsign, grad, want_x, want_params, gx_accum=None):
+    """HIP VJP of FerroelectricBasis: returns (gx, [grad per FERRO_PARAM_NAMES or None]).  At the
+    wide-layer widths (ETT / ECG fields) with the constant branch sign, one pass over the element
+    evaluations gives both (fetode_ferro_backward_wide); otherwise the generic two-kernel VJP."""
+    if bsign is None and mod.in_dim >= 16 and mod.out_dim >= 16 and (want_x or any(want_params)):
+        r = _ferro_backward_wide(mod, xc, prev, reinit, grad, want_x, want_params, gx_accum)
+        if r is not None:
+            return r
+    return _ferro_backward_generic(mod, xc, prev, reinit, bsign, grad, want_x, want_params, gx_accum)
+
+
+def _ferro_backward_generic(mod, xc, prev, reinit, bsign, grad, want_x, want_params, gx_accum=None):
     lib = _lib.load()
     keep = []
     d = mod.desc(keep, bsign)
@@ -204,6 +253,32 @@ def ferro_backward(mod, xc, prev, reinit, bsign, grad, want_x, want_params, gx_a
         _lib.ctypes.byref(d), xc.data_ptr(), xc.shape[0], _lib.ptr(prev), int(reinit), g.data_ptr(),
         _lib.ptr(gx), _lib.ctypes.byref(gstruct) if any_param else None, int(gx_accum is not None),
         _stream(xc)), "FerroelectricBasis backward")
+    return gx, grads
+
+
+def _ferro_backward_wide(mod, xc, prev, reinit, grad, want_x, want_params, gx_accum):
+    entry = wide_plan(None, mod, xc.device)
+    if entry is None:
+        return None
+    plan, _, fd, _ = entry
+    lib = _lib.load()
+    B = xc.shape[0]
+    g = _lib.f32c(grad)
+    gx = None
+    if want_x:
+        gx = torch.empty_like(xc) if gx_accum is None else gx_accum
+    params = [getattr(mod, n) for n in FERRO_PARAM_NAMES]
+    # accumulate applies to d/dx and the parameter sums alike: accumulating parameter sums start at 0
+    alloc = torch.empty_like if gx_accum is None else torch.zeros_like
+    grads = [alloc(p) if w else None for p, w in zip(params, want_params)]
+    any_param = any(t is not None for t in grads)
+    gstruct = _lib.FerroGrad(*[_lib.ptr(t) for t in grads]) if any_param else None
+    nb = lib.fetode_ferro_backward_wide_workspace(_lib.ctypes.byref(fd), B)
+    ws = torch.empty(max(1, nb // 4), device=xc.device, dtype=torch.float32)
+    _lib.check(lib.fetode_ferro_backward_wide(
+        _lib.ctypes.byref(fd), plan.data_ptr(), xc.data_ptr(), B, _lib.ptr(None if reinit else prev), int(reinit),
+        g.data_ptr(), _lib.ptr(gx), _lib.ctypes.byref(gstruct) if any_param else None,
+        int(gx_accum is not None), ws.data_ptr(), _stream(xc)), "FerroelectricBasis backward (wide)")
     return gx, grads
 
 
@@ -403,6 +478,17 @@ def field_apply(model, x: torch.Tensor) -> torch.Tensor:
                         fer._commit_state(h, reinit)
                     h = y
                     continue
+        if grad and _WIDE_GRAD and kan.out_features in (64, 128):
+            # production widths under autograd: the forward in the wide-layer kernel, the VJPs in
+            # the wide MFMA / one-pass kernels (_WideLayerFn)
+            reinit = fer._needs_reinit(h) if fer is not None else False
+            if fer is None or fer._branch_sign_for(h) is None:
+                y = wide_layer_grad(kan, fer, h, reinit)
+                if y is not None:
+                    if fer is not None:
+                        fer._commit_state(h, reinit)
+                    h = y
+                    continue
         y = kanlinear_apply(kan, h)
         if fer is not None:
             reinit = fer._needs_reinit(h)
@@ -461,6 +547,60 @@ def wide_plan(kan, fer, device):
     entry = (plan, kd, fd, keep)
     owner.__dict__[attr] = (key, entry)
     return entry
+
+
+_WIDE_GRAD = True   # tests flip it to compare with the per-module autograd path
+
+
+class _WideLayerFn(torch.autograd.Function):
+    """One KAN-FET (or KANLinear) layer at production widths under autograd: the forward is the
+    wide-layer launch (fetode_wide_layer_forward, as under no_grad), the backward the MFMA KANLinear
+    VJP then the one-pass Ferro VJP accumulating into the same d/dx.  params = the KANLinear's
+    non-None parameters (KAN_PARAM_NAMES order), then the Ferro module's (FERRO_PARAM_NAMES)."""
+
+    @staticmethod
+    def forward(ctx, kan, fer, reinit, nk, x, *params):
+        xc = _lib.f32c(x)
+        out = wide_apply(kan, fer, xc, reinit=reinit)
+        prev = None if (fer is None or reinit) else fer._prev.detach().clone()   # overwritten after this call
+        ctx.kan, ctx.fer, ctx.reinit, ctx.nk = kan, fer, reinit, nk
+        ctx.save_for_backward(xc, prev)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        xc, prev = ctx.saved_tensors
+        kan, fer, nk = ctx.kan, ctx.fer, ctx.nk
+        want_x = ctx.needs_input_grad[4]
+        pn = ctx.needs_input_grad[5:]
+        kp = kan_params(kan)
+        it = iter(pn[:nk])
+        want_k = [next(it) if p is not None else False for p in kp]
+        gx, gk = kan_backward(kan, xc, g, want_x, want_k)
+        gf = []
+        if fer is not None:
+            want_f = list(pn[nk:])
+            if want_x or any(want_f):
+                gxf, gf = ferro_backward(fer, xc, prev, ctx.reinit, None, g, want_x, want_f,
+                                         gx_accum=gx if want_x else None)
+                if want_x and gx is None:
+                    gx = gxf
+            else:
+                gf = [None] * len(want_f)
+        grads_k = [t for t, p in zip(gk, kp) if p is not None]
+        return (None, None, None, None, gx, *grads_k, *gf)
+
+
+def wide_layer_grad(kan, fer, x, reinit: bool):
+    """KANLinear(x) (+ Ferro(x)) with autograd through _WideLayerFn, or None if the layer has no
+    wide kernels (the caller then runs the per-module path)."""
+    if wide_plan(kan, fer, x.device) is None or (fer is not None and wide_plan(None, fer, x.device) is None):
+        return None
+    if wide_plan(kan, None, x.device) is None:
+        return None
+    kp = [p for p in kan_params(kan) if p is not None]
+    fp = [getattr(fer, n) for n in FERRO_PARAM_NAMES] if fer is not None else []
+    return _WideLayerFn.apply(kan, fer, reinit, len(kp), x, *kp, *fp)
 
 
 def wide_apply(kan, fer, x, reinit: bool = False):

@@ -445,6 +445,488 @@ wide_fn pick(int K, bool kan, bool ferro) {
   return ch == 4 ? pick_ch<4>(K, kan, ferro) : pick_ch<8>(K, kan, ferro);
 }
 
+
+
+// ---- the Ferro layer's VJP at production widths (ferro_class.py:368-414 under autograd) ----------
+// d loss / d x and the five parameter gradients of FerroelectricBasis (constant branch_sign) from the
+// output adjoint g, in one pass over the element evaluations.  With branch_sign = 1 (never written,
+// ferro_class.py:366) the crossing gate cp carries a zero coefficient and
+//   cn = sigma(gs (-x - Ec)) = 1 / (1 + e^{gs x} P),  m = 1 + wc (1 - up) cn,   wc = -2 (1 - alpha)
+//   th = tanh(k (x + Ec m)),  out = sum coef (Ps th + bias)
+// with up = sigma(gs (x - prev)) (prev detached, ferro_class.py:381-387), so per element
+//   gP = g coef;  gcoef = g P;  gPs = gP th;  gbias = gP;  gz = gP Ps (1 - th^2);  gk = gz (x + Ec m)
+//   (1 - th^2 = 4 r (1 - r) with th = 1 - 2 r: no cancellation where th saturates)
+//   gsh = gz k;  gm = gsh Ec;  dcn = gs cn (1 - cn)
+//   gx += gsh - gm wc ((1 - up) dcn + cn gs up (1 - up));   gEc = gsh m - gm wc (1 - up) dcn.
+// Mapping: a wave = 4 rows x (3 outputs x 5 pairs) at K = 10 (2 x 6 at K = 12): lane (q, o, kp) of
+// 16-lane quarter q evaluates elements (i, o, 2kp), (i, o, 2kp + 1) of row b + q on packed fp32, so
+// the parameter sums stay in the lane's registers over the whole row range and d/dx of a row is one
+// 16-lane DPP row sum.  A wave walks OGW output groups for its input i and rows [r0, r1).  Partials:
+// d/dx per (output-group block, row, input) and the parameter sums per row segment, both reduced in
+// a fixed order afterwards (run-to-run identical).
+// output groups per wave: 2 (default; 4 holds ~220 VGPRs, two waves per SIMD); FETODE_FERRO_BWD_OGW
+// = 1 | 2 | 4 picks (tuning knob)
+int ferro_bwd_ogw() {
+  static const int v = [] {
+    const char* e = getenv("FETODE_FERRO_BWD_OGW");
+    const int x = e ? atoi(e) : 2;
+    return x == 1 || x == 4 ? x : 2;
+  }();
+  return v;
+}
+
+struct WideFerroBwdArgs {
+  const float* plan;
+  WideLayout L;
+  const float* k, *Ec, *Ps, *bias, *coef;  // reference layout (in, out, K)
+  const float4* U;    // (B, in): {x, e = 2^{gs log2e x}, 1 - up, gs up (1 - up)}
+  const float* g;     // (B, out)
+  int64_t B;
+  int n_og, n_ogb, rs, seg;   // output groups (of OPG outputs), group blocks (of ferro_bwd_ogw()), row segments, rows/segment
+  float* gxp;         // (n_ogb, B, in)
+  float* pp;          // (rs, in, out, K, 5)
+};
+
+__global__ void wide_ferro_prep_kernel(const float* __restrict__ x, const float* __restrict__ prev, int reinit,
+                                       int64_t n, float gsl2e, float gs, float4* __restrict__ U) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  const float xv = x[t], pv = reinit ? xv : prev[t];
+  const float up = rcp(1.0f + ex2(-gsl2e * (xv - pv)));   // the forward's gate (wide_layer_kernel)
+  const float omu = 1.0f - up;
+  U[t] = make_float4(xv, ex2(gsl2e * xv), omu, gs * up * omu);
+}
+
+template <int K, int kBwdOGW>
+__global__ __launch_bounds__(256) void wide_ferro_bwd_kernel(WideFerroBwdArgs a) {
+  constexpr int KP = K / 2, OPG = 16 / KP;   // pairs per output, outputs per 16-lane group (3 | 2)
+  const WideLayout& L = a.L;
+  const int in = L.in, out = L.out;
+  const int lane = threadIdx.x & 63, q = lane >> 4, c = lane & 15;
+  const int64_t task = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int ogb = (int)(task % a.n_ogb);
+  const int64_t rest = task / a.n_ogb;
+  const int i = (int)(rest % in), sgi = (int)(rest / in);
+  if (sgi >= a.rs) return;
+  const int64_t r0 = (int64_t)sgi * a.seg, r1 = r0 + a.seg < a.B ? r0 + a.seg : a.B;
+  const bool act = c < OPG * KP;
+  const int ol = act ? c / KP : 0, kp = act ? c % KP : 0;
+  const float gs = L.gs, wc = L.wc, gsl2e = L.gsl2e;
+  // this lane's element pairs in the kBwdOGW output groups of the block
+  f2 Pf[kBwdOGW], k2[kBwdOGW], kk[kBwdOGW], Ecv[kBwdOGW], Psv[kBwdOGW], cov[kBwdOGW], bsv[kBwdOGW];
+  f2 gec[kBwdOGW];
+  int oo[kBwdOGW];
+  bool ok[kBwdOGW], dir[kBwdOGW];
+  f2 sk[kBwdOGW], sE[kBwdOGW], sPs[kBwdOGW], sb[kBwdOGW], sc[kBwdOGW];
+#pragma unroll
+  for (int j = 0; j < kBwdOGW; ++j) {
+    const int og = ogb * kBwdOGW + j;
+    const int o = og * OPG + ol;
+    ok[j] = act && og < a.n_og && o < out;
+    oo[j] = ok[j] ? o : 0;
+    const int64_t e0 = ((int64_t)i * out + oo[j]) * K + 2 * kp;                 // reference layout
+    const int64_t p0 = ((int64_t)oo[j] * in + i) * K + 2 * kp;                   // plan layout (o, i, k)
+    const float4 a0 = ok[j] ? reinterpret_cast<const float4*>(a.plan + L.fe4)[p0] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 a1 = ok[j] ? reinterpret_cast<const float4*>(a.plan + L.fe4)[p0 + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+    Pf[j] = f2{a0.x, a1.x};
+    k2[j] = f2{a0.y, a1.y};
+    kk[j] = ok[j] ? f2{a.k[e0], a.k[e0 + 1]} : splat(0.f);
+    Ecv[j] = ok[j] ? f2{a.Ec[e0], a.Ec[e0 + 1]} : splat(0.f);
+    Psv[j] = ok[j] ? f2{a.Ps[e0], a.Ps[e0 + 1]} : splat(0.f);
+    cov[j] = ok[j] ? f2{a.coef[e0], a.coef[e0 + 1]} : splat(0.f);
+    bsv[j] = ok[j] ? f2{a.bias[e0], a.bias[e0 + 1]} : splat(0.f);
+    gec[j] = ok[j] ? f2{a.plan[L.gec + p0], a.plan[L.gec + p0 + 1]} : splat(0.f);
+    dir[j] = ok[j] && a.plan[L.dflag + (int64_t)oo[j] * in + i] != 0.f;
+    sk[j] = sE[j] = sPs[j] = sb[j] = sc[j] = splat(0.f);
+  }
+  bool anydir = false;
+#pragma unroll
+  for (int j = 0; j < kBwdOGW; ++j) anydir |= __builtin_amdgcn_ballot_w64(dir[j]) != 0;
+  float* gxp = a.gxp + (int64_t)ogb * a.B * in;
+  for (int64_t b0 = r0; b0 < r1; b0 += 4) {
+    const int64_t b = b0 + q;
+    const bool live = b < r1;
+    const float4 u = live ? a.U[b * in + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float xv = u.x, e = u.y, omu = u.z, dup = u.w;
+    float dx = 0.f;
+#pragma unroll
+    for (int j = 0; j < kBwdOGW; ++j) {
+      const float go = (live && ok[j]) ? a.g[b * out + oo[j]] : 0.f;
+      f2 cn;
+      if (anydir && dir[j]) cn = rcpx2(ex2x2(pfma(splat(gsl2e), splat(xv), gec[j])) + splat(1.0f));
+      else cn = rcpx2(pfma(splat(e), Pf[j], splat(1.0f)));
+      const f2 m = pfma(splat(wc * omu), cn, splat(1.0f));
+      const f2 sh = pfma(Ecv[j], m, splat(xv));                     // x + Ec m
+      const f2 r = rcpx2(ex2x2(k2[j] * sh) + splat(1.0f));          // 2^{2 log2e k sh}
+      const f2 th = pfma(splat(-2.0f), r, splat(1.0f));             // tanh = 1 - 2 / (1 + e^{2 k sh})
+      const f2 gP = splat(go) * cov[j];
+      sc[j] = pfma(splat(go), pfma(Psv[j], th, bsv[j]), sc[j]);
+      sPs[j] = pfma(gP, th, sPs[j]);
+      sb[j] = sb[j] + gP;
+      const f2 gz = gP * Psv[j] * (splat(4.0f) * r * (splat(1.0f) - r));   // 1 - th^2 without cancellation
+      sk[j] = pfma(gz, sh, sk[j]);
+      const f2 gsh = gz * kk[j];
+      const f2 gm = gsh * Ecv[j];
+      const f2 dcn = splat(gs) * cn * (splat(1.0f) - cn);
+      const f2 t1 = splat(omu) * dcn;
+      sE[j] = pfma(gsh, m, sE[j]) - splat(wc) * gm * t1;
+      const f2 dxp = gsh - splat(wc) * gm * pfma(cn, splat(dup), t1);
+      dx += ok[j] ? dxp.x + dxp.y : 0.f;   // idle lanes: e = inf times P = 0 is NaN
+    }
+    const float row = row_sum16(dx);
+    if (c == 0 && live) gxp[b * in + i] = row;
+  }
+  // the four row quarters hold the same elements: quarters (0 + 2) + (1 + 3) onto lanes 0..15
+  float* pp = a.pp + (int64_t)sgi * in * out * K * 5;
+#pragma unroll
+  for (int j = 0; j < kBwdOGW; ++j) {
+    f2 v[5] = {sk[j], sE[j], sPs[j], sb[j], sc[j]};
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float p = h ? v[t].y : v[t].x, qq = p;
+        permlane32_swap(p, qq);
+        float s2 = p + qq, s3 = s2;
+        permlane16_swap(s2, s3);
+        const float tot = s2 + s3;
+        if (lane < 16 && ok[j]) pp[(((int64_t)i * out + oo[j]) * K + 2 * kp + h) * 5 + t] = tot;
+      }
+    }
+  }
+}
+
+// d/dx: the output-group blocks in order (+ the existing gx when accumulating); parameters: the row
+// segments in order, written in the reference layout (+ accumulate)
+__global__ void wide_ferro_gx_reduce_kernel(const float* __restrict__ gxp, int n_ogb, int64_t n, float* __restrict__ gx,
+                                            int accumulate) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  float s = 0.f;
+  for (int j = 0; j < n_ogb; ++j) s += gxp[(int64_t)j * n + t];
+  gx[t] = accumulate ? gx[t] + s : s;
+}
+
+__global__ void wide_ferro_gp_reduce_kernel(const float* __restrict__ pp, int rs, int64_t ne, fetode_ferro_grad_t gr,
+                                            int accumulate) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= ne * 5) return;
+  const int64_t e = t / 5;
+  const int which = (int)(t % 5);
+  float s = 0.f;
+  for (int j = 0; j < rs; ++j) s += pp[(int64_t)j * ne * 5 + t];
+  float* dst = which == 0 ? gr.k : which == 1 ? gr.Ec : which == 2 ? gr.Ps : which == 3 ? gr.bias : gr.coef;
+  if (dst) dst[e] = accumulate ? dst[e] + s : s;
+}
+
+struct FerroBwdPlan {
+  int n_og, n_ogb, rs, seg;
+  int64_t tasks;
+};
+
+FerroBwdPlan ferro_bwd_plan(int in, int out, int K, int64_t B) {
+  FerroBwdPlan p{};
+  const int kBwdOGW = ferro_bwd_ogw();
+  const int OPG = 16 / (K / 2);
+  p.n_og = (out + OPG - 1) / OPG;
+  p.n_ogb = (p.n_og + kBwdOGW - 1) / kBwdOGW;
+  // row segments: enough waves to fill the chip (~8 per SIMD), each at least 256 rows
+  const int64_t base = (int64_t)p.n_ogb * in;
+  int64_t rs = (8 * 1024 + base - 1) / base;
+  const int64_t rmax = (B + 255) / 256;
+  rs = rs < rmax ? rs : rmax;
+  p.rs = (int)(rs > 0 ? rs : 1);
+  p.seg = (int)(((B + p.rs - 1) / p.rs + 3) / 4 * 4);
+  p.rs = (int)((B + p.seg - 1) / p.seg);
+  p.tasks = base * p.rs;
+  return p;
+}
+
+// ---- the KANLinear VJP at production widths (efficientkan.py:160-182 under autograd) -----------
+// With the packed weights Wp (in, 20, out) of the plan and the 20 staged features phi(x) of the
+// forward (SiLU, 8 cubic B-spline bases, 10 logistic sigmoids), the layer is out = phi(x) Wp, so
+//   gphi = g Wp^T            (B x in*20, K = out)   -> d/dx = sum_f gphi phi'_f, and the logistic
+//                                                       a / b sums (sum_b gphi sigma' (x - b), -a ...)
+//   dWp  = phi^T g           (in*20 x out, K = B)  -> the parameter gradients by the chain rule of
+//                                                       the packing (spline scaler, logistic scales)
+// both on v_mfma_f32_16x16x4_f32.  wide_kan_gx_kernel: a wave = 16 rows x 4 inputs (80 feature
+// columns; one (row, input) item per lane); A = g rows, B = Wp columns, both straight from global
+// memory (L2-resident) with the contraction index permuted so each lane reads 4-float runs
+// (o = kg * out/4 + q for lane group kg, k-step q: the MFMA sums over k in any order); gphi meets
+// the per-lane features through a wave-private LDS tile.  It also writes phi (B, in*20) for
+// wide_kan_gw_kernel: a wave = 16 feature columns x 64 outputs over a row segment.  Partials
+// (row segments) add in a fixed order: run-to-run identical.
+constexpr int kKF = kWF;   // features per input (the plan's packing, last one zero)
+
+__device__ __forceinline__ void wsync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+struct WideKanBwdArgs {
+  const float* plan;
+  WideLayout L;
+  const float* la, *lb;   // logistic a, b (in, NB)
+  const float* x, *g;
+  int64_t B;
+  float* gx;
+  int accumulate;
+  float* F;       // (B, in * 20) features
+  float* abp;     // (n_rg, in, NB, 2) logistic a / b partial sums
+  int n_rg, t16;  // row groups, 16-row tiles per group
+};
+
+template <int OUT4>
+__global__ __launch_bounds__(256) void wide_kan_gx_kernel(WideKanBwdArgs a) {
+  constexpr int OUT = 4 * OUT4, kPitch = 4 * kKF + 1;
+  __shared__ float s_gp[4][16 * kPitch];
+  const WideLayout& L = a.L;
+  const int in = L.in, nch = in / 4;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t task = (int64_t)blockIdx.x * 4 + wv;
+  const int c = (int)(task % nch);
+  const int rg = (int)(task / nch);
+  if (rg >= a.n_rg) return;
+  const int kg = lane >> 4, n = lane & 15;
+  const int ii = lane >> 4, r = lane & 15, i = c * 4 + ii;   // the lane's (row, input) item
+  float* gp = s_gp[wv];
+  const float* __restrict__ plan = a.plan;
+  const float l2 = FETODE_LOG2E;
+  float ga[kNB], gb[kNB];
+#pragma unroll
+  for (int j = 0; j < kNB; ++j) ga[j] = gb[j] = 0.f;
+  const int64_t nt = (a.B + 15) / 16;
+  const int64_t t_lo = (int64_t)rg * a.t16, t_hi = t_lo + a.t16 < nt ? t_lo + a.t16 : nt;
+  for (int64_t t = t_lo; t < t_hi; ++t) {
+    const int64_t b0 = t * 16;
+    // gphi (16 rows x 80 columns): A = g rows (row b0 + n, k-group kg), B = Wp columns
+    float4 ar[OUT4 / 4];
+    {
+      const bool ok = b0 + n < a.B;
+      const float4* gr = reinterpret_cast<const float4*>(a.g + (b0 + n) * OUT + kg * OUT4);
+#pragma unroll
+      for (int q = 0; q < OUT4 / 4; ++q) ar[q] = ok ? gr[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int ct = 0; ct < 5; ++ct) {
+      const float4* wr = reinterpret_cast<const float4*>(plan + L.wp + ((int64_t)c * 4 * kKF + ct * 16 + n) * OUT + kg * OUT4);
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int q = 0; q < OUT4 / 4; ++q) {
+        const float4 w = wr[q];
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[q].x, w.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[q].y, w.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[q].z, w.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ar[q].w, w.w, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) gp[(4 * kg + v) * kPitch + ct * 16 + n] = acc[v];
+    }
+    // the lane's item: features and their derivatives (the forward's staging, wide_layer_kernel)
+    const int64_t b = b0 + r;
+    const bool live = b < a.B;
+    const float xv = live ? a.x[b * in + i] : 0.f;
+    float f[kKF], d[kKF];
+    {
+      const float sg = rcp(1.0f + ex2(-xv * l2));
+      f[0] = xv * sg;
+      d[0] = sg * (1.0f + xv * (1.0f - sg));
+      const float* kn = plan + L.knots + (int64_t)i * kNG;
+      int m = -1;
+#pragma unroll
+      for (int j = 0; j < kNG; ++j) m += (xv >= kn[j]) ? 1 : 0;
+      const bool fin = __builtin_isfinite(xv);
+      const int mi = ((unsigned)m < (unsigned)(kNG - 1) && fin) ? m : kNG - 1;
+      const float rh = mi < kNG - 1 ? plan[L.rh + (int64_t)i * (kNG - 1) + mi] : 0.f;
+      const float u = mi < kNG - 1 ? (xv - kn[mi]) * rh : 0.f;
+      const float4* bt = reinterpret_cast<const float4*>(plan + L.bt) + ((int64_t)i * kNG + mi) * kNS;
+#pragma unroll
+      for (int cc = 0; cc < kNS; ++cc) {
+        const float4 cf = bt[cc];
+        f[1 + cc] = fin ? ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x) : __builtin_nanf("");
+        d[1 + cc] = fin ? ffma(ffma(3.0f * cf.w, u, 2.0f * cf.z), u, cf.y) * rh : __builtin_nanf("");
+      }
+      const float* lg = plan + L.lg + (int64_t)i * kNB * 2;
+#pragma unroll
+      for (int j = 0; j < kNB; ++j) {
+        const float sj = rcp(1.0f + ex2(ffma(lg[2 * j], xv, lg[2 * j + 1])));
+        f[1 + kNS + j] = sj;
+        d[1 + kNS + j] = sj * (1.0f - sj);   // sigma'; times a for d/dx
+      }
+      f[kKF - 1] = 0.f;
+      d[kKF - 1] = 0.f;
+    }
+    if (live) {
+      float4* fr = reinterpret_cast<float4*>(a.F + b * (int64_t)in * kKF + (int64_t)i * kKF);
+#pragma unroll
+      for (int q = 0; q < kKF / 4; ++q) fr[q] = make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]);
+    }
+    wsync();
+    const float* gq = gp + r * kPitch + ii * kKF;
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q <= kNS; ++q) s = ffma(gq[q], d[q], s);
+#pragma unroll
+    for (int j = 0; j < kNB; ++j) {
+      const float aj = a.la[i * kNB + j], bj = a.lb[i * kNB + j];
+      const float gz = gq[1 + kNS + j] * d[1 + kNS + j];
+      s = ffma(gz, aj, s);
+      ga[j] = ffma(gz, xv - bj, ga[j]);
+      gb[j] = ffma(gz, -aj, gb[j]);
+    }
+    if (live) a.gx[b * in + i] = a.accumulate ? a.gx[b * in + i] + s : s;
+    wsync();   // the tile is read before the next one is written
+  }
+  // the 16 rows of an input are one DPP row
+#pragma unroll
+  for (int j = 0; j < kNB; ++j) {
+    const float sa = row_sum16(ga[j]), sb = row_sum16(gb[j]);
+    if (r == 0) {
+      float* o = a.abp + (((int64_t)rg * in + i) * kNB + j) * 2;
+      o[0] = sa;
+      o[1] = sb;
+    }
+  }
+}
+
+// dWp partials: a wave = 16 feature columns x 64 outputs over rows [s * seg, (s + 1) * seg)
+__global__ __launch_bounds__(256) void wide_kan_gw_kernel(const float* __restrict__ F, const float* __restrict__ g,
+                                                          int64_t B, int ncol, int out, int rs, int64_t seg,
+                                                          float* __restrict__ pw) {
+  const int lane = threadIdx.x & 63, kg = lane >> 4, n = lane & 15;
+  const int64_t task = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nct = ncol / 16, nog = out / 64;
+  const int ct = (int)(task % nct), og = (int)((task / nct) % nog), sgi = (int)(task / ((int64_t)nct * nog));
+  if (sgi >= rs) return;
+  const int64_t r0 = (int64_t)sgi * seg, r1 = r0 + seg < B ? r0 + seg : B;
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* fa = F + ct * 16 + n;
+  const float* gb = g + og * 64 + n;
+  for (int64_t rr = r0; rr < r1; rr += 16) {
+    float av[4], bv[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t b = rr + 4 * u + kg;
+      const bool ok = b < r1;
+      av[u] = ok ? fa[b * ncol] : 0.f;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) bv[u][t] = ok ? gb[b * out + 16 * t] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[u], bv[u][t], acc[t], 0, 0, 0);
+  }
+  float* o = pw + ((int64_t)sgi * ncol + ct * 16) * out + og * 64 + n;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) o[(int64_t)(4 * kg + v) * out + 16 * t] = acc[t][v];
+}
+
+__device__ __forceinline__ void put_grad(float* p, float v, int accumulate) {
+  if (p) *p = accumulate ? *p + v : v;
+}
+
+// thread per (input i, output o): the row segments in order, then the packing's chain rule
+// (wide_pack_kernel: base_weight; spline_weight * spline_scaler; 2 logistic_weight scale_logistic
+// logistic_scaler); the d/d(2 sigma) sums d_wl for the logistic_scaler pass
+__global__ void wide_kan_grad_kernel(fetode_kanlinear_t kl, const float* __restrict__ pw, int rs,
+                                     fetode_kanlinear_grad_t gr, float* __restrict__ d_wl, int accumulate) {
+  const int in = kl.in_features, out = kl.out_features;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)in * out) return;
+  const int o = (int)(t % out), i = (int)(t / out);
+  const int64_t ncol = (int64_t)in * kKF, oi = (int64_t)o * in + i;
+  float v[kKF - 1];
+#pragma unroll
+  for (int f = 0; f < kKF - 1; ++f) {
+    float s = 0.f;
+    for (int q = 0; q < rs; ++q) s += pw[((int64_t)q * ncol + (int64_t)i * kKF + f) * out + o];
+    v[f] = s;
+  }
+  put_grad(gr.base_weight ? gr.base_weight + oi : nullptr, v[0], accumulate);
+  const float sc = kl.spline_scaler ? kl.spline_scaler[oi] : 1.0f;
+  float dsc = 0.f;
+#pragma unroll
+  for (int c = 0; c < kNS; ++c) {
+    put_grad(gr.spline_weight ? gr.spline_weight + oi * kNS + c : nullptr, v[1 + c] * sc, accumulate);
+    dsc += v[1 + c] * kl.spline_weight[oi * kNS + c];
+  }
+  if (kl.spline_scaler) put_grad(gr.spline_scaler ? gr.spline_scaler + oi : nullptr, dsc, accumulate);
+  const float ls = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
+#pragma unroll
+  for (int j = 0; j < kNB; ++j) {
+    const int64_t w = (int64_t)o * in * kNB + (int64_t)i * kNB + j;
+    const float dw = 2.0f * v[1 + kNS + j];
+    d_wl[w] = dw;
+    put_grad(gr.logistic_weight ? gr.logistic_weight + w : nullptr, (dw * ls) * kl.scale_logistic, accumulate);
+  }
+}
+
+// logistic a / b: the row groups in order; logistic_scaler: one wave per output, fixed-order sums
+__global__ void wide_kan_ab_ls_kernel(fetode_kanlinear_t kl, const float* __restrict__ abp, int n_rg,
+                                      const float* __restrict__ d_wl, fetode_kanlinear_grad_t gr, int accumulate) {
+  const int in = kl.in_features, out = kl.out_features;
+  const int nab = in * kNB;
+  const int nabb = (nab + 255) / 256;
+  if ((int)blockIdx.x < nabb) {
+    const int t = blockIdx.x * 256 + threadIdx.x;
+    if (t >= nab) return;
+    float sa = 0.f, sb = 0.f;
+    for (int q = 0; q < n_rg; ++q) {
+      sa += abp[((int64_t)q * nab + t) * 2];
+      sb += abp[((int64_t)q * nab + t) * 2 + 1];
+    }
+    put_grad(gr.logistic_a ? gr.logistic_a + t : nullptr, sa, accumulate);
+    put_grad(gr.logistic_b ? gr.logistic_b + t : nullptr, sb, accumulate);
+    return;
+  }
+  if (!kl.logistic_scaler) return;
+  const int o = ((int)blockIdx.x - nabb) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (o >= out) return;
+  float s = 0.f;
+  for (int q = lane; q < nab; q += 64)
+    s += d_wl[(int64_t)o * nab + q] * (kl.logistic_weight[(int64_t)o * nab + q] * kl.scale_logistic);
+  for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (lane == 0) put_grad(gr.logistic_scaler ? gr.logistic_scaler + o : nullptr, s, accumulate);
+}
+
+struct KanBwdPlan {
+  int n_rg, t16, rs;
+  int64_t seg, tasks_gx, tasks_gw;
+  int64_t off_F, off_abp, off_pw, off_dwl, off_gxs, end;   // floats
+};
+
+KanBwdPlan kan_bwd_plan(int in, int out, int64_t B) {
+  KanBwdPlan p{};
+  const int64_t nt = (B + 15) / 16, nch = in / 4;
+  // ~4 k waves for the gx pass; the gw pass: segments of >= 256 rows, at most 16
+  int64_t t16 = (nt * nch + 4095) / 4096;
+  p.t16 = (int)(t16 > 0 ? t16 : 1);
+  p.n_rg = (int)((nt + p.t16 - 1) / p.t16);
+  p.tasks_gx = (int64_t)p.n_rg * nch;
+  int64_t rs = (B + 255) / 256;
+  rs = rs < 16 ? rs : 16;
+  p.rs = (int)(rs > 0 ? rs : 1);
+  p.seg = ((B + p.rs - 1) / p.rs + 15) / 16 * 16;
+  p.rs = (int)((B + p.seg - 1) / p.seg);
+  const int64_t ncol = (int64_t)in * kKF;
+  p.tasks_gw = (ncol / 16) * (out / 64) * p.rs;
+  int64_t o = 0;
+  p.off_F = o; o += B * ncol;
+  p.off_abp = o; o += (int64_t)p.n_rg * in * kNB * 2;
+  p.off_pw = o; o += (int64_t)p.rs * ncol * out;
+  p.off_dwl = o; o += (int64_t)out * in * kNB;
+  p.off_gxs = o; o += B * in;   // d/dx when the caller wants only parameter gradients
+  p.end = o;
+  return p;
+}
+
+bool kan_bwd_wide_ok(const fetode_kanlinear_t* kl, const fetode_ferro_t* fl) {
+  return kl && wide_supported(kl, fl) && (kl->out_features == 64 || kl->out_features == 128) &&
+         kl->spline_weight && kl->base_weight;
+}
+
 }  // namespace
 
 extern "C" {
@@ -506,4 +988,125 @@ int fetode_wide_layer_forward(const fetode_kanlinear_t* kl, const fetode_ferro_t
   return FETODE_OK;
 }
 
+int64_t fetode_ferro_backward_wide_workspace(const fetode_ferro_t* fl, int64_t B) {
+  if (!fl || !wide_supported(nullptr, fl)) return -1;
+  if (B <= 0) return 0;
+  const FerroBwdPlan p = ferro_bwd_plan(fl->in_dim, fl->out_dim, fl->num_basis, B);
+  const int64_t nU = B * fl->in_dim * 4, ngx = (int64_t)p.n_ogb * B * fl->in_dim,
+                npp = (int64_t)p.rs * fl->in_dim * fl->out_dim * fl->num_basis * 5;
+  return (nU + ngx + npp) * (int64_t)sizeof(float) + 256;
+}
+
+int fetode_ferro_backward_wide(const fetode_ferro_t* fl, const void* plan, const float* x, int64_t B, const float* prev,
+                               int32_t reinit, const float* g, float* gx, const fetode_ferro_grad_t* grads,
+                               int32_t accumulate, void* workspace, void* stream) {
+  if (!fl || !wide_supported(nullptr, fl)) return set_err(FETODE_EUNSUPPORTED, "ferro wide backward: unsupported shape / parameters");
+  if (B <= 0) return FETODE_OK;
+  if (!plan || !x || !g || !workspace || (!reinit && !prev)) return set_err(FETODE_EINVAL, "ferro wide backward: null pointer");
+  if (!gx && !grads) return FETODE_OK;
+  const int in = fl->in_dim, out = fl->out_dim, K = fl->num_basis;
+  const FerroBwdPlan p = ferro_bwd_plan(in, out, K, B);
+  if ((p.tasks + 3) / 4 > 0x7fffffff) return set_err(FETODE_EINVAL, "ferro wide backward: batch too large");
+  const hipStream_t s = (hipStream_t)stream;
+  const WideLayout L = wide_layout(nullptr, fl);
+  const uintptr_t base = ((uintptr_t)workspace + 255) & ~(uintptr_t)255;
+  float4* U = reinterpret_cast<float4*>(base);
+  float* gxp = reinterpret_cast<float*>(U + B * in);
+  float* pp = gxp + (int64_t)p.n_ogb * B * in;
+  const int64_t n = B * in;
+  hipLaunchKernelGGL(wide_ferro_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, prev, (int)reinit,
+                     n, L.gsl2e, L.gs, U);
+  LAUNCH_CHECK();
+  WideFerroBwdArgs a;
+  a.plan = (const float*)plan;
+  a.L = L;
+  a.k = fl->k;
+  a.Ec = fl->Ec;
+  a.Ps = fl->Ps;
+  a.bias = fl->bias;
+  a.coef = fl->coef;
+  a.U = U;
+  a.g = g;
+  a.B = B;
+  a.n_og = p.n_og;
+  a.n_ogb = p.n_ogb;
+  a.rs = p.rs;
+  a.seg = p.seg;
+  a.gxp = gxp;
+  a.pp = pp;
+  const int ogw = ferro_bwd_ogw();
+  void (*kern)(WideFerroBwdArgs) =
+      K == 12 ? (ogw == 1 ? wide_ferro_bwd_kernel<12, 1> : ogw == 4 ? wide_ferro_bwd_kernel<12, 4> : wide_ferro_bwd_kernel<12, 2>)
+              : (ogw == 1 ? wide_ferro_bwd_kernel<10, 1> : ogw == 4 ? wide_ferro_bwd_kernel<10, 4> : wide_ferro_bwd_kernel<10, 2>);
+  hipLaunchKernelGGL(kern, dim3((unsigned)((p.tasks + 3) / 4)),
+                     dim3(256), 0, s, a);
+  LAUNCH_CHECK();
+  if (gx) {
+    hipLaunchKernelGGL(wide_ferro_gx_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, gxp, p.n_ogb, n,
+                       gx, (int)accumulate);
+    LAUNCH_CHECK();
+  }
+  if (grads) {
+    const int64_t ne = (int64_t)in * out * K;
+    hipLaunchKernelGGL(wide_ferro_gp_reduce_kernel, dim3((unsigned)((ne * 5 + 255) / 256)), dim3(256), 0, s, pp, p.rs,
+                       ne, *grads, (int)accumulate);
+    LAUNCH_CHECK();
+  }
+  return FETODE_OK;
+}
+
+int64_t fetode_kanlinear_backward_wide_workspace(const fetode_kanlinear_t* kl, const fetode_ferro_t* fl, int64_t B) {
+  if (!kan_bwd_wide_ok(kl, fl)) return -1;
+  if (B <= 0) return 0;
+  return kan_bwd_plan(kl->in_features, kl->out_features, B).end * (int64_t)sizeof(float) + 256;
+}
+
+int fetode_kanlinear_backward_wide(const fetode_kanlinear_t* kl, const fetode_ferro_t* fl, const void* plan, const float* x,
+                                   int64_t B, const float* g, float* gx, const fetode_kanlinear_grad_t* grads,
+                                   int32_t accumulate, void* workspace, void* stream) {
+  if (!kan_bwd_wide_ok(kl, fl)) return set_err(FETODE_EUNSUPPORTED, "kanlinear wide backward: unsupported shape / parameters");
+  if (B <= 0) return FETODE_OK;
+  if (!plan || !x || !g || !workspace) return set_err(FETODE_EINVAL, "kanlinear wide backward: null pointer");
+  if ((uintptr_t)g & 15) return set_err(FETODE_EINVAL, "kanlinear wide backward: g must be 16-byte aligned");
+  if (!gx && !grads) return FETODE_OK;
+  const int in = kl->in_features, out = kl->out_features;
+  const KanBwdPlan p = kan_bwd_plan(in, out, B);
+  if ((p.tasks_gx + 3) / 4 > 0x7fffffff || (p.tasks_gw + 3) / 4 > 0x7fffffff)
+    return set_err(FETODE_EINVAL, "kanlinear wide backward: batch too large");
+  const hipStream_t s = (hipStream_t)stream;
+  float* ws = reinterpret_cast<float*>(((uintptr_t)workspace + 255) & ~(uintptr_t)255);
+  WideKanBwdArgs a;
+  a.plan = (const float*)plan;
+  a.L = wide_layout(kl, fl);
+  a.la = kl->logistic_a;
+  a.lb = kl->logistic_b;
+  a.x = x;
+  a.g = g;
+  a.B = B;
+  // d/dx is always formed (the pass also writes the features); without gx it goes to scratch
+  a.gx = gx ? gx : ws + p.off_gxs;
+  a.accumulate = gx ? (int)accumulate : 0;
+  a.F = ws + p.off_F;
+  a.abp = ws + p.off_abp;
+  a.n_rg = p.n_rg;
+  a.t16 = p.t16;
+  hipLaunchKernelGGL(out == 128 ? wide_kan_gx_kernel<32> : wide_kan_gx_kernel<16>, dim3((unsigned)((p.tasks_gx + 3) / 4)),
+                     dim3(256), 0, s, a);
+  LAUNCH_CHECK();
+  if (!grads) return FETODE_OK;
+  const int ncol = in * kKF;
+  hipLaunchKernelGGL(wide_kan_gw_kernel, dim3((unsigned)((p.tasks_gw + 3) / 4)), dim3(256), 0, s, (const float*)a.F, g, B,
+                     ncol, out, p.rs, p.seg, ws + p.off_pw);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(wide_kan_grad_kernel, dim3((unsigned)(((int64_t)in * out + 255) / 256)), dim3(256), 0, s, *kl,
+                     (const float*)(ws + p.off_pw), p.rs, *grads, ws + p.off_dwl, (int)accumulate);
+  LAUNCH_CHECK();
+  const int nabb = (in * kNB + 255) / 256;
+  hipLaunchKernelGGL(wide_kan_ab_ls_kernel, dim3((unsigned)(nabb + (out + 3) / 4)), dim3(256), 0, s, *kl,
+                     (const float*)a.abp, p.n_rg, (const float*)(ws + p.off_dwl), *grads, (int)accumulate);
+  LAUNCH_CHECK();
+  return FETODE_OK;
+}
+
 }  // extern "C"
+

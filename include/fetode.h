@@ -285,10 +285,34 @@ int64_t fetode_kanlinear_backward_workspace(const fetode_kanlinear_t* layer);
 int fetode_kanlinear_backward(const fetode_kanlinear_t* layer, const float* x, int64_t B, const float* g,
                               float* gx, const fetode_kanlinear_grad_t* grads, void* workspace,
                               int32_t accumulate, void* stream);
+/* fetode_kanlinear_backward at production widths (fetode_wide_layer_supported(layer, plan_ferro),
+ * out = 64 or 128): with the plan's packed weights Wp (in, 20, out), gphi = g Wp^T and dWp =
+ * phi(x)^T g on MFMA, d/dx and the logistic a / b sums from gphi and the feature derivatives, the
+ * parameter gradients from dWp by the packing's chain rule; fixed-order reductions.  plan = a
+ * wide-layer plan built for (layer, plan_ferro) (plan_ferro = NULL: KANLinear alone).  Replaces the
+ * autograd VJP of KANLinear.forward (efficientkan.py:160-182) in the reference's training loops
+ * (train_kan_fet_ett.py:333).  g must be 16-byte aligned. */
+int64_t fetode_kanlinear_backward_wide_workspace(const fetode_kanlinear_t* layer, const fetode_ferro_t* plan_ferro,
+                                                 int64_t B);
+int fetode_kanlinear_backward_wide(const fetode_kanlinear_t* layer, const fetode_ferro_t* plan_ferro,
+                                   const void* plan, const float* x, int64_t B, const float* g, float* gx,
+                                   const fetode_kanlinear_grad_t* grads, int32_t accumulate, void* workspace,
+                                   void* stream);
 /* prev/reinit exactly as the forward call that is being differentiated used them. */
 int fetode_ferro_backward(const fetode_ferro_t* layer, const float* x, int64_t B, const float* prev,
                           int32_t reinit, const float* g, float* gx, const fetode_ferro_grad_t* grads,
                           int32_t accumulate, void* stream);
+/* fetode_ferro_backward at production widths (fetode_wide_layer_supported(NULL, layer)): the element
+ * evaluations once, d/dx and the five parameter sums from the same pass (packed fp32, the
+ * parameter sums held per lane over a row segment), reduced in a fixed order.  plan = a wide-layer
+ * plan built for this Ferro layer (alone or inside its KANFET layer: the Ferro part is laid out the
+ * same).  Replaces the autograd VJP of FerroelectricBasis.forward (ferro_class.py:368-414; prev_x
+ * detached :381-382) that the reference's training loops run (train_kan_fet_ett.py:333). */
+int64_t fetode_ferro_backward_wide_workspace(const fetode_ferro_t* layer, int64_t B);
+int fetode_ferro_backward_wide(const fetode_ferro_t* layer, const void* plan, const float* x, int64_t B,
+                               const float* prev, int32_t reinit, const float* g, float* gx,
+                               const fetode_ferro_grad_t* grads, int32_t accumulate, void* workspace,
+                               void* stream);
 
 /* ---- reverse sweep of fetode_integrate_fixed (training) -----------------------------------
  * loss.backward() through a fused fixed-grid solve (train_kanfet_node_predprey.py:254-257):

@@ -248,3 +248,124 @@ def test_wide_kanlinear_noncontiguous_input(dev):
         got = m(xs)
     exp = m(xs.clone().requires_grad_(True)).detach()
     assert row_rel(got, exp) <= 1e-5, row_rel(got, exp)
+
+
+# ---------------------------------------------------------------------------------------------
+# the one-pass Ferro VJP at production widths (fetode_ferro_backward_wide) against the generic
+# two-kernel VJP (itself pinned to the oracle's autograd above and in test_gpu_grad.py)
+# ---------------------------------------------------------------------------------------------
+
+@pytest.mark.parametrize("i,o,K", [(64, 128, 10), (128, 64, 10), (64, 128, 12), (128, 64, 12)])
+@pytest.mark.parametrize("B", [300, 5000])
+def test_wide_ferro_backward_one_pass(dev, i, o, K, B):
+    """d/dx and the five parameter gradients, stateful (prev_x) and first-call (reinit) forms, plain
+    and accumulating, with wild rows (|gs x| > 80) and |gs Ec| > 80 parameters (the direct gate);
+    B = 5000 spans several row segments.  Run twice: the fixed-order reductions repeat bitwise."""
+    from fet_ode_amd import autograd_ops as A
+    m = _ferro_with_edges(i, o, K, seed=3 * i + o + K).to(dev)
+    x = _x(B, i, seed=B + K, wild_rows=(1, 150, B - 1)).to(dev)
+    prev = (_x(B, i, seed=B + K + 1, wild_rows=(2, 150)) * 0.7).to(dev)
+    g = torch.randn(B, o, generator=torch.Generator().manual_seed(B + 3)).to(dev)
+    want = (True,) * 5
+    for reinit in (False, True):
+        gx_w, gp_w = A._ferro_backward_wide(m, x, prev, reinit, g, True, want, None)
+        gx_r, gp_r = A._ferro_backward_generic(m, x, prev, reinit, None, g, True, want, None)
+        gx_w2, gp_w2 = A._ferro_backward_wide(m, x, prev, reinit, g, True, want, None)
+        assert torch.equal(gx_w, gx_w2) and all(torch.equal(a, b) for a, b in zip(gp_w, gp_w2))
+        assert torch.isfinite(gx_w).all()
+        # saturated (wild) rows carry gradients ~1e-5 of the others, where 1 - th^2 loses most of its
+        # digits in either fp32 form: those rows are held to the tensor's scale, the rest per row
+        tame = torch.ones(B, dtype=torch.bool)
+        tame[[1, 150, B - 1]] = False
+        assert row_rel(gx_w[tame], gx_r[tame]) <= 2e-5, (reinit, row_rel(gx_w[tame], gx_r[tame]))
+        assert (gx_w - gx_r).abs().max().item() <= 2e-5 * gx_r.abs().max().item()
+        for n, a, b in zip(A.FERRO_PARAM_NAMES, gp_w, gp_r):
+            err = (a - b).abs().max().item()
+            assert err <= 1e-4 * b.abs().max().item() + 1e-7, (reinit, n, err)
+    # accumulate: d/dx added into an existing buffer, parameter sums from zero
+    base = torch.randn(B, i, generator=torch.Generator().manual_seed(9)).to(dev)
+    acc = base.clone()
+    gx_a, gp_a = A._ferro_backward_wide(m, x, prev, False, g, True, (False, True, False, False, True), acc)
+    assert gx_a is acc
+    gx_w, gp_w = A._ferro_backward_wide(m, x, prev, False, g, True, want, None)
+    assert torch.equal(acc, base + gx_w)            # the same fixed-order sum, added once
+    assert gp_a[0] is None and torch.equal(gp_a[1], gp_w[1]) and torch.equal(gp_a[4], gp_w[4])
+
+
+# the MFMA KANLinear VJP at production widths (fetode_kanlinear_backward_wide) against the generic
+# kernels (pinned to the oracle's autograd in test_gpu_grad.py / above)
+@pytest.mark.parametrize("i,o", [(64, 128), (128, 64), (128, 128)])
+@pytest.mark.parametrize("B", [37, 1000, 9000])
+def test_wide_kanlinear_backward_mfma(dev, i, o, B):
+    """d/dx and the seven parameter gradients; x in and out of the knot grid (and on a knot), a
+    ragged batch (B % 16 != 0), several row segments; plain, accumulating and parameters-only
+    forms; run twice: the fixed-order reductions repeat bitwise."""
+    from fet_ode_amd import autograd_ops as A
+    torch.manual_seed(i + 2 * o + B)
+    m = F.KANLinear(i, o).to(dev)
+    with torch.no_grad():
+        m.spline_scaler.mul_(torch.rand_like(m.spline_scaler) + 0.5)
+        m.logistic_scaler.mul_(torch.rand_like(m.logistic_scaler) + 0.5)
+    x = _x(B, i, seed=B + i).to(dev)
+    x[0, 0] = m.grid[0, 5]                     # exactly on a knot
+    x[min(3, B - 1), :] = 40.0                  # far outside the grid
+    g = torch.randn(B, o, generator=torch.Generator().manual_seed(B)).to(dev)
+    want = tuple(p is not None for p in A.kan_params(m))
+    gx_w, gp_w = A._kan_backward_wide(m, x, g, True, want)
+    gx_w2, gp_w2 = A._kan_backward_wide(m, x, g, True, want)
+    gx_r, gp_r = A._kan_backward_generic(m, x, g, True, want)
+    assert torch.equal(gx_w, gx_w2)
+    assert all(a is None or torch.equal(a, b) for a, b in zip(gp_w, gp_w2))
+    assert row_rel(gx_w, gx_r) <= 1e-5, row_rel(gx_w, gx_r)
+    n = 0
+    for name, a, b in zip(A.KAN_PARAM_NAMES, gp_w, gp_r):
+        if b is None:
+            continue
+        err = (a - b).abs().max().item()
+        assert err <= 2e-5 * b.abs().max().item() + 1e-7, (name, err, b.abs().max().item())
+        n += 1
+    assert n == 7
+    # accumulate into existing d/dx; parameters-only (no d/dx)
+    base = torch.randn(B, i, generator=torch.Generator().manual_seed(2)).to(dev)
+    acc = base.clone()
+    _, gp_a = A._kan_backward_wide(m, x, g, True, want, acc)
+    assert torch.equal(acc, base + gx_w)
+    assert all(a is None or torch.equal(a, b) for a, b in zip(gp_a, gp_w))
+    gx_n, gp_n = A._kan_backward_wide(m, x, g, False, want)
+    assert gx_n is None and all(a is None or torch.equal(a, b) for a, b in zip(gp_n, gp_w))
+
+
+def test_wide_kanfet_field_autograd_two_calls(dev):
+    """KANFET([64, 128, 64]) under autograd (the wide-layer forward + the MFMA / one-pass VJPs,
+    _WideLayerFn) against the per-module autograd path: two stateful calls (first-call rule, then
+    prev_x), loss through both, every parameter gradient and d/dx."""
+    from fet_ode_amd import autograd_ops as A
+    torch.manual_seed(21)
+    base = F.KANFET([64, 128, 64], grid_size=5, num_fet_basis=10)
+    x1 = _x(700, 64, seed=1).to(dev) * 0.5
+    x2 = _x(700, 64, seed=2, wild_rows=(9,)).to(dev) * 0.5
+    w = torch.randn(700, 64, generator=torch.Generator().manual_seed(3)).to(dev)
+    res = []
+    for wide in (True, False):
+        A._WIDE_GRAD = wide
+        try:
+            m = F.KANFET([64, 128, 64], grid_size=5, num_fet_basis=10)
+            m.load_state_dict(base.state_dict())
+            m = m.to(dev)
+            xa = x1.clone().requires_grad_(True)
+            xb = x2.clone().requires_grad_(True)
+            y1 = m(xa)
+            y2 = m(xb)
+            ((y1 * w).sum() + (y2 * y2).mean()).backward()
+            res.append((y1.detach(), y2.detach(), xa.grad, xb.grad,
+                        {n: p.grad.clone() for n, p in m.named_parameters()}))
+        finally:
+            A._WIDE_GRAD = True
+    (a1, a2, ga, gb, pa), (r1, r2, gra, grb, pr) = res
+    assert row_rel(a1, r1) <= 1e-5 and row_rel(a2, r2) <= 1e-5
+    for got, exp in ((ga, gra), (gb, grb)):
+        assert (got - exp).abs().max().item() <= 1e-4 * exp.abs().max().item()
+    assert len(pa) == len(pr) and len(pa) >= 20
+    for n in pr:
+        err = (pa[n] - pr[n]).abs().max().item()
+        assert err <= 1e-4 * pr[n].abs().max().item() + 1e-7, (n, err)
