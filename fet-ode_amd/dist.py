@@ -101,16 +101,20 @@ def allreduce_gradients(params: Iterable[torch.nn.Parameter], average: bool = Tr
 
 
 def _shared_flat(grads: List[torch.Tensor]) -> Optional[torch.Tensor]:
-    """The one contiguous buffer the gradients tile exactly, in order, or None."""
-    base = grads[0]._base
-    if base is None or not base.is_contiguous() or base.dim() != 1:
-        return None
-    off = 0
+    """A flat view of the one storage run the gradients tile exactly, in order, or None.
+
+    Compared by storage, not by ``._base``: AccumulateGrad stores ``new_grad.detach()``, whose
+    ``_base`` is None although it still aliases the fused backward's flat buffer.
+    """
+    g0 = grads[0]
+    st = g0.untyped_storage()
+    start = off = g0.storage_offset()
     for g in grads:
-        if g._base is not base or not g.is_contiguous() or g.storage_offset() - base.storage_offset() != off:
+        if (g.dtype != g0.dtype or g.device != g0.device or not g.is_contiguous()
+                or g.untyped_storage().data_ptr() != st.data_ptr() or g.storage_offset() != off):
             return None
         off += g.numel()
-    return base if off == base.numel() else None
+    return g0.new_empty(0).set_(st, start, (off - start,))
 
 
 def broadcast_parameters(module: torch.nn.Module, src: int = 0, group=None) -> None:

@@ -150,10 +150,15 @@ def _views_worker(rank, world, port, q):
     # reduced in place, no copies; a mixed set falls back to the flatten path
     ps = [torch.nn.Parameter(torch.zeros(3, 2)), torch.nn.Parameter(torch.zeros(4))]
     flat = torch.arange(10, dtype=torch.float32) * (rank + 1)
-    ps[0].grad, ps[1].grad = flat[:6].view(3, 2), flat[6:]
-    assert D._shared_flat([p.grad for p in ps]) is flat
+    # detached, as AccumulateGrad stores them (their ._base is None; the storage is still shared)
+    ps[0].grad, ps[1].grad = flat[:6].view(3, 2).detach(), flat[6:].detach()
+    sf = D._shared_flat([p.grad for p in ps])
+    assert sf is not None and sf.data_ptr() == flat.data_ptr() and sf.numel() == 10
+    # a gap or a reordering is not one run
+    assert D._shared_flat([ps[1].grad, ps[0].grad]) is None
+    assert D._shared_flat([flat[:4], flat[6:]]) is None
     D.allreduce_gradients(ps)
-    q.put((rank, flat.clone(), ps[0].grad._base is flat))
+    q.put((rank, flat.clone(), ps[0].grad.data_ptr() == flat.data_ptr()))
     dist.destroy_process_group()
 
 
