@@ -238,6 +238,10 @@ struct WideArgs {
   int reinit;
   int nslice;  // 1, or 2: blockIdx.z takes half of the inputs and adds into a zeroed out
   float* out;
+  // resident solver only (wide_tile<.., RES = true>): the layer input / its hysteresis memory as the
+  // fixed-order sum of two input-sliced partial slabs (x + x2), null when whole
+  const float* x2;
+  const float* prev2;
 };
 
 // One slice stores; two add into a zeroed out with vector atomics: 0 + a + b in either order is the
@@ -248,8 +252,16 @@ __device__ __forceinline__ void store_out(float* p, float v, int nslice) {
 }
 
 // ---- the layer --------------------------------------------------------------------------------
-template <int K, bool KAN, bool FERRO, int kCh>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) void wide_layer_kernel(WideArgs a) {
+typedef __attribute__((address_space(4))) const float kconst_f;
+typedef __attribute__((address_space(4))) const float4 kconst_f4;
+
+// One tile (row block bx, output block by, input slice bz) of the layer.  The per-layer launch
+// (wide_layer_kernel) runs one per workgroup; the device-resident dopri5 solver (wide_dopri5_kernel)
+// walks every tile of a layer phase with its persistent grid.  RES: the input and the hysteresis
+// memory may be the sum of two partial slabs (x2 / prev2), and every output goes through `epi`
+// (a write-through store, or the solver's per-element stage combine) instead of store_out.
+template <int K, bool KAN, bool FERRO, int kCh, bool RES, class Epi>
+__device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const int by, const int bz, Epi&& epi) {
   constexpr int kPitch = pitch_of(kCh);
   static_assert(kCh * kRows <= kThreads && (kCh & 1) == 0, "one staging item per thread, even chunks");
   static_assert(!FERRO || K % 2 == 0, "Ferro elements in (k, k+1) pairs");
@@ -265,8 +277,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) v
   const int in = L.in, out = L.out;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t b0 = (int64_t)blockIdx.x * kRows;
-  const int o0 = blockIdx.y * kOuts;
+  const int64_t b0 = (int64_t)bx * kRows;
+  const int o0 = by * kOuts;
   const float* __restrict__ plan = a.plan;
   const float gsl2e = L.gsl2e, wc = L.wc, l2 = FETODE_LOG2E;
 
@@ -284,14 +296,22 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) v
 
   // the staging item's x / prev_x, loaded one chunk ahead (their HBM latency hides under the
   // previous chunk's work)
-  const int ibeg = blockIdx.z * (in / a.nslice), iend = ibeg + in / a.nslice;
-  float xn = slive ? a.x[sb * in + ibeg + si] : 0.f;
-  float pn = (FERRO && slive && !a.reinit) ? a.prev[sb * in + ibeg + si] : 0.f;
+  const int ibeg = bz * (in / a.nslice), iend = ibeg + in / a.nslice;
+  auto ldx = [&](int64_t i) -> float {
+    if constexpr (RES) return a.x2 ? a.x[i] + a.x2[i] : a.x[i];   // slab 0 + slab 1: the host path's 0 + a + b
+    return a.x[i];
+  };
+  auto ldp = [&](int64_t i) -> float {
+    if constexpr (RES) return a.prev2 ? a.prev[i] + a.prev2[i] : a.prev[i];
+    return a.prev[i];
+  };
+  float xn = slive ? ldx(sb * in + ibeg + si) : 0.f;
+  float pn = (FERRO && slive && !a.reinit) ? ldp(sb * in + ibeg + si) : 0.f;
   for (int i0 = ibeg; i0 < iend; i0 += kCh) {
     const float x = xn, pvl = pn;
     if (i0 + kCh < iend) {
-      xn = slive ? a.x[sb * in + i0 + kCh + si] : 0.f;
-      pn = (FERRO && slive && !a.reinit) ? a.prev[sb * in + i0 + kCh + si] : 0.f;
+      xn = slive ? ldx(sb * in + i0 + kCh + si) : 0.f;
+      pn = (FERRO && slive && !a.reinit) ? ldp(sb * in + i0 + kCh + si) : 0.f;
     }
     __syncthreads();  // the previous chunk is consumed
     if constexpr (FERRO) {
@@ -353,7 +373,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) v
           const int jo = kJ * w + j;
           // the element constants are wave-uniform: scalar loads (s_load, SGPR operands) — through
           // LDS they cost a ds_read_b128 per element (Ferro alone 270 -> 230 us at 64 -> 128)
+          // (read through the constant address space: the plan is never written during a launch, so the
+          // loads stay scalar even where stores precede them in a loop — the resident solver's tile loop)
           const float4* par = reinterpret_cast<const float4*>(plan + L.fe4) + ((int64_t)(o0 + jo) * in + i) * K;
+          auto pk = [&](int k) -> float4 {
+#if defined(__HIP_DEVICE_COMPILE__)
+            if constexpr (RES) {
+              const kconst_f4* pc = (const kconst_f4*)(uintptr_t)(par + k);
+              return make_float4(pc->x, pc->y, pc->z, pc->w);
+            }
+#endif
+            return par[k];
+          };
           float acc = 0.f;
           if (s_dfl[jo * kCh + ii] == 0.f) {  // wave-uniform
             // elements (k, k+1) in the two halves of packed-fp32 VALU ops (v_pk_fma / mul / add:
@@ -361,7 +392,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) v
             f2 acc2 = splat(0.0f);
 #pragma unroll
             for (int k = 0; k < K; k += 2) {
-              const float4 p0 = par[k], p1 = par[k + 1];  // {P, k2, k2Ec, cps}, same address on every lane
+              const float4 p0 = pk(k), p1 = pk(k + 1);  // {P, k2, k2Ec, cps}, same address on every lane
               const f2 sg = rcpx2(pfma(splat(e), f2{p0.x, p1.x}, splat(1.0f)));
               const f2 mm = pfma(splat(wg), sg, splat(1.0f));
               const f2 z = pfma(f2{p0.z, p1.z}, mm, f2{p0.y, p1.y} * splat(xv));
@@ -373,7 +404,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) v
             const float* gec = plan + L.gec + ((int64_t)(o0 + jo) * in + i) * K;
 #pragma unroll
             for (int k = 0; k < K; ++k) {
-              const float4 p = par[k];
+              const float4 p = pk(k);
               const float sg = rcp(1.0f + ex2(ffma(gsl2e, xv, gec[k])));
               const float mm = ffma(wg, sg, 1.0f);
               const float z = ffma(p.z, mm, p.y * xv);
@@ -402,7 +433,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) v
   if constexpr (FERRO) {
 #pragma unroll
     for (int j = 0; j < kJ; ++j)
-      s_fer[lane * (kOuts + 1) + kJ * w + j] = facc[j] + (blockIdx.z == 0 ? plan[L.fconst + o0 + kJ * w + j] : 0.f);
+      s_fer[lane * (kOuts + 1) + kJ * w + j] = facc[j] + (bz == 0 ? plan[L.fconst + o0 + kJ * w + j] : 0.f);
   }
   if constexpr (KAN) {
     if (kh == 1)
@@ -417,15 +448,23 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) v
         const int r = 16 * rt + 4 * kq + v;
         const int64_t b = b0 + r;
         const float kv = (kacc0[v] + kacc1[v]) + s_kc[r * (kOuts + 1) + kr];
-        if (b < a.B) store_out(&a.out[b * out + o0 + kr], FERRO ? kv + s_fer[r * (kOuts + 1) + kr] : kv, a.nslice);
+        if (b < a.B) epi(b, o0 + kr, FERRO ? kv + s_fer[r * (kOuts + 1) + kr] : kv);
       }
   } else {
     for (int t = tid; t < kRows * kOuts; t += kThreads) {
       const int r = t / kOuts, c = t % kOuts;
       const int64_t b = b0 + r;
-      if (b < a.B) store_out(&a.out[b * out + o0 + c], s_fer[r * (kOuts + 1) + c], a.nslice);
+      if (b < a.B) epi(b, o0 + c, s_fer[r * (kOuts + 1) + c]);
     }
   }
+}
+
+template <int K, bool KAN, bool FERRO, int kCh>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) void wide_layer_kernel(WideArgs a) {
+  const int out = a.L.out, ns = a.nslice;
+  float* const o = a.out;
+  wide_tile<K, KAN, FERRO, kCh, false>(a, blockIdx.x, blockIdx.y, blockIdx.z,
+                                       [&](int64_t b, int c, float v) { store_out(&o[b * out + c], v, ns); });
 }
 
 typedef void (*wide_fn)(WideArgs);
@@ -927,6 +966,550 @@ bool kan_bwd_wide_ok(const fetode_kanlinear_t* kl, const fetode_ferro_t* fl) {
          kl->spline_weight && kl->base_weight;
 }
 
+
+// =============================================================================================
+// Device-resident dopri5 for a two-layer wide KAN-FET field: the ETT forecaster's own latent solve,
+// odeint(self.dynamics, z0, t_fut, method="dopri5") at torchdiffeq's defaults
+// (train_kan_fet_ett.py:192, :858, :879) with the KAN-FET field KANFET([64, 128, 64]).
+//
+// The host-driven solver (dopri5.py _Dopri5) pays per evaluation two wide-layer launches plus the
+// combines, and per attempt a device->host read of the error ratio.  Here ONE launch runs the whole
+// solve with a persistent grid that walks the layers' tiles (wide_tile, the per-layer launch's own
+// body) phase by phase:
+//   L0     tiles (64 rows x 16 hidden, input slice s) of layer 0: x = the stage input, prev = the
+//          previous evaluation's input (ferro_class.py:409), out -> hidden slab hs[e & 1][s]
+//   L1     tiles of layer 1: x = the hidden slabs summed in a fixed order (slab 0 + slab 1: the
+//          per-layer launch's 0 + a + b), out -> k; whole (one slice) layers fold the Dormand-Prince
+//          stage combine into the tile epilogue, sliced ones add a combine pass after a barrier
+// A grid barrier separates the phases; stage inputs and hidden slabs are written through (sc1)
+// and read after the barrier's agent-scope acquire (MI355X_MICROARCH.md, valid hand-off forms).
+// Per-element solver state (y, f0, the running stage sums, err, mid, the interpolation
+// coefficients) lives in HBM and is touched only by the element's owner thread: layer-1 tile t
+// belongs to workgroup t % G, and its element (row, dim) to the epilogue thread that stores it —
+// so none of it crosses workgroups.  The one global quantity per attempt is the RMS error ratio:
+// per-workgroup fp64 partials, the barrier, and every workgroup sums all partials in the same
+// order (the same decisions everywhere).  Control arithmetic: the host-driven path's (fp32 stage
+// sums in fetode_lincomb's order, fp64 step control, fetode_interp_fit / _eval), so the solution
+// equals the host loop's bit for bit up to the norms' fp64 summation order.
+// =============================================================================================
+constexpr int kEs = 17;  // per-element state rows: y, f0, A0..A5, err, mid, co0..co4, y1, k_last
+enum { kEY = 0, kEF0 = 1, kEA = 2, kEErr = 8, kEMid = 9, kECo = 10, kEY1 = 15, kEKl = 16 };
+constexpr int kWBarWords = 64 * 10;  // 8 XCD counters, top counter, generation | abort (256 B apart)
+constexpr unsigned kWSpinLimit = 1u << 22;
+constexpr int kWideDopriMaxGrid = 256 * 8;  // partial slots of the norm reduction
+
+struct WideDopriArgs {
+  WideArgs l0, l1;  // plan + layout of each layer; x / prev / nslice are set per phase
+  int64_t B;
+  int D, H, S0, S1, reinit0, reinit1, nT0, nT1, nOT0, nOT1;
+  const float* y0;
+  const float* prev0;  // (B, D) hysteresis memory of layer 0 before the solve (unused when reinit0)
+  const float* prev1;  // (B, H)
+  float* st0;          // (B, D) / (B, H): the memory after the solve (the last evaluation's inputs)
+  float* st1;
+  float* xin;  // (2, B, D) stage inputs by evaluation parity
+  float* hs;   // (2, S0, B, H) hidden slabs by evaluation parity
+  float* ks;   // (S1, B, D) k slabs (S1 == 2)
+  float* es;   // (kEs, B, D)
+  float* sol;  // (T, B, D)
+  const double* t;
+  int T;
+  float rtol, atol;
+  double first_step, safety, ifactor, dfactor, min_step, max_step;
+  int max_steps;
+  float stc[7][8];  // tableau columns (DopriParams.stc)
+  unsigned* bar;
+  double* slot;  // (grid, 2)
+  int32_t* stats;
+  double* att;
+  int max_att;
+};
+
+__device__ __forceinline__ void st_wt(float* p, float v) {  // write-through (sc1) store
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+typedef unsigned wd_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void wd_st16(double* p, double v0, double v1) {
+  const unsigned long long x = __double_as_longlong(v0), y = __double_as_longlong(v1);
+  const wd_u32x4 v = {(unsigned)x, (unsigned)(x >> 32), (unsigned)y, (unsigned)(y >> 32)};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void wd_ld16(const double* p, double& v0, double& v1) {
+  wd_u32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  v0 = __longlong_as_double(((unsigned long long)v.y << 32) | v.x);
+  v1 = __longlong_as_double(((unsigned long long)v.w << 32) | v.z);
+}
+
+// Grid barrier with a hand-off: every wave drains its write-through stores, the workgroup arrives
+// (XCD-hierarchical counters as fetode_ecg.hip grid_barrier: per-XCD counter, its last arriver on
+// the top counter, the last of those bumps the generation), polls the generation relaxed, then ONE
+// agent-scope acquire (this CU's L1 dropped) before any wave loads what other workgroups wrote.
+// Bounded spins: a grid that is not co-resident raises the abort word and every barrier returns.
+__device__ bool wide_barrier(unsigned* bar) {
+  __shared__ int s_ab;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned nblk = gridDim.x;
+    const unsigned x = blockIdx.x & 7u;
+    const unsigned nx = (nblk + 7u - x) / 8u, nxcd = nblk < 8u ? nblk : 8u;
+    unsigned* cnt = bar + 64 * x;
+    unsigned* top = bar + 64 * 8;
+    unsigned* gen = bar + 64 * 9;
+    unsigned* abw = gen + 1;
+    int ab = __hip_atomic_load(abw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+    if (!ab) {
+      const unsigned g = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (__hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nx - 1u) {
+        __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nxcd - 1u) {
+          __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      unsigned spins = 0;
+      while (__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g) {
+        __builtin_amdgcn_s_sleep(1);
+        if ((spins & 15u) == 15u && __hip_atomic_load(abw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+          ab = 1;
+          break;
+        }
+        if (++spins == kWSpinLimit) {
+          __hip_atomic_store(abw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ab = 1;
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    s_ab = ab;
+  }
+  __syncthreads();
+  return s_ab != 0;
+}
+
+__device__ __forceinline__ double wd_xor_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Sum of two fp64 values over every thread of the grid, the same fixed order in every workgroup:
+// waves (xor tree), the workgroup's waves in index order, then the workgroups' partials (lane j sums
+// partials j, j + 64, .. in order, then an xor tree).  Contains a barrier.
+__device__ bool wide_sum2(unsigned* bar, double* slot, double v0, double v1, double& s0, double& s1) {
+  __shared__ double s_red[kWaves][2];
+  __shared__ double s_out[2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  v0 = wd_xor_sum(v0);
+  v1 = wd_xor_sum(v1);
+  if (lane == 0) {
+    s_red[w][0] = v0;
+    s_red[w][1] = v1;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a0 = 0.0, a1 = 0.0;
+    for (int j = 0; j < kWaves; ++j) {
+      a0 += s_red[j][0];
+      a1 += s_red[j][1];
+    }
+    wd_st16(slot + 2 * blockIdx.x, a0, a1);
+  }
+  if (wide_barrier(bar)) return true;
+  if (w == 0) {
+    double a0 = 0.0, a1 = 0.0;
+    for (unsigned j = lane; j < gridDim.x; j += 64) {
+      double u0, u1;
+      wd_ld16(slot + 2 * j, u0, u1);
+      a0 += u0;
+      a1 += u1;
+    }
+    a0 = wd_xor_sum(a0);
+    a1 = wd_xor_sum(a1);
+    if (lane == 0) {
+      s_out[0] = a0;
+      s_out[1] = a1;
+    }
+  }
+  __syncthreads();
+  s0 = s_out[0];
+  s1 = s_out[1];
+  return false;
+}
+
+enum { kCmbF0 = 0, kCmbF1 = 1, kCmbStage = 2 };
+
+// The solver's uniform state lives in LDS: thread 0 takes every decision, the other threads read
+// it after a workgroup barrier, so none of it is live in registers across a layer phase (the tile
+// body alone fills the SGPR file with its scalar-cache constants).
+struct WdCtl {
+  double dt, t0, t1, t0s, t1s;
+  float h0, d1, dt32, fit_dt32;
+  int nev, nfev, n_att, iout, n_steps, stg, kind, status;
+  int fit, io_lo, io_hi, next;  // after a decision: accept fit?, outputs [io_lo, io_hi), next input
+  float cc[8];                  // tableau column of the stage just evaluated (k_{stg+1})
+};
+enum { kNextNone = 0, kNextProbe = 1, kNextAttempt = 2 };
+
+template <int K>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void wide_dopri5_kernel(WideDopriArgs a) {
+  __shared__ WdCtl ctl;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int G = (int)gridDim.x;
+  const int64_t B = a.B, BD = B * a.D, BH = B * a.H;
+  const int D = a.D, H = a.H;
+  const double n_el = (double)BD;
+  // element ownership: the layer-1 tile epilogue's storing threads (waves 0-3: row 16 (w % 4) +
+  // 4 (lane / 16) + v, dim lane % 16), layer-1 tile t < nT1 on workgroup t % G
+  const bool owner = w < 4;
+  const int rt = w & 3, kq = lane >> 4, kr = lane & 15;
+  auto for_owned = [&](auto&& f) {
+    if (!owner) return;
+    for (int t = blockIdx.x; t < a.nT1; t += G) {
+      const int64_t b0 = (int64_t)(t / a.nOT1) * kRows;
+      const int d = (t % a.nOT1) * kOuts + kr;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int64_t b = b0 + 16 * rt + 4 * kq + v;
+        if (b < B) f(b * D + d);
+      }
+    }
+  };
+  float* const es = a.es;
+  double acc0 = 0.0, acc1 = 0.0;  // this thread's partial norms
+
+  for_owned([&](int64_t i) {
+    const float y = a.y0[i];
+    es[kEY * BD + i] = y;
+    a.sol[i] = y;
+  });
+  if (tid == 0) {
+    ctl.dt = a.first_step;
+    ctl.t0 = ctl.t1 = 0.0;
+    ctl.t0s = ctl.t1s = a.t[0];
+    ctl.h0 = ctl.d1 = ctl.dt32 = 0.f;
+    ctl.nev = ctl.nfev = ctl.n_att = ctl.n_steps = ctl.stg = 0;
+    ctl.iout = 1;
+    ctl.kind = kCmbF0;
+    ctl.status = -1;
+  }
+  __syncthreads();
+  int status = -1;
+#pragma unroll 1
+  for (;;) {
+    // ---- one field evaluation: L0 phase | barrier | L1 phase | barrier ----
+    const int e = ctl.nev, p = e & 1;
+    if (e > 0 && wide_barrier(a.bar)) {  // the stage input came from other workgroups
+      status = 4;
+      break;
+    }
+    bool ab = false;
+#pragma unroll 1
+    for (int l = 0; l < 2 && !ab; ++l) {
+      WideArgs L = l ? a.l1 : a.l0;
+      const int nT = l ? a.nT1 : a.nT0, nOT = l ? a.nOT1 : a.nOT0, S = l ? a.S1 : a.S0;
+      if (l == 0) {
+        L.x = e == 0 ? a.y0 : a.xin + p * BD;
+        L.x2 = nullptr;
+        L.reinit = e == 0 ? a.reinit0 : 0;
+        L.prev = e == 0 ? a.prev0 : (e == 1 ? a.y0 : a.xin + (p ^ 1) * BD);
+        L.prev2 = nullptr;
+      } else {
+        L.x = a.hs + (int64_t)p * a.S0 * BH;
+        L.x2 = a.S0 == 2 ? L.x + BH : nullptr;
+        L.reinit = e == 0 ? a.reinit1 : 0;
+        L.prev = e == 0 ? a.prev1 : a.hs + (int64_t)(p ^ 1) * a.S0 * BH;
+        L.prev2 = (e > 0 && a.S0 == 2) ? L.prev + BH : nullptr;
+      }
+      L.nslice = S;
+      const int ow = l ? D : H;
+      float* const ob = l ? a.ks : a.hs + (int64_t)p * a.S0 * BH;  // k slabs | this parity's hidden slabs
+      const int64_t sl = l ? BD : BH;
+      for (int t = blockIdx.x; t < nT * S; t += G) {
+        const int bz = t / nT, r = t % nT;
+        float* const o = ob + bz * sl;
+        wide_tile<K, true, true, kChMax, true>(L, r / nOT, r % nOT, bz,
+                                               [&](int64_t b, int c, float v) { st_wt(&o[b * ow + c], v); });
+      }
+      ab = wide_barrier(a.bar);
+    }
+    if (ab) {
+      status = 4;
+      break;
+    }
+    // ---- the per-element combine of k (the host loop's fetode_lincomb / scaled_rms order) ----
+    {
+      const int kind = ctl.kind, stg = ctl.stg, pn = (e + 1) & 1;
+      const float dt32 = ctl.dt32;
+      float c[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) c[q] = ctl.cc[q];
+      const bool two = a.S1 == 2;
+      for_owned([&](int64_t i) {
+        const float k = two ? a.ks[i] + a.ks[BD + i] : a.ks[i];  // slab 0 + slab 1: the launch path's 0 + a + b
+        const float y = es[kEY * BD + i];
+        if (kind == kCmbF0) {  // f0 = f(t0, y0); _select_initial_step's d0 / d1 terms
+          es[kEF0 * BD + i] = k;
+          const float scale = a.atol + a.rtol * fabsf(y);
+          const float q0 = y / scale, q1 = k / scale;
+          acc0 += (double)q0 * q0;
+          acc1 += (double)q1 * q1;
+        } else if (kind == kCmbF1) {  // d2 term: (f1 - f0) / scale
+          const float scale = a.atol + a.rtol * fabsf(y);
+          const float q2 = (k - es[kEF0 * BD + i]) / scale;
+          acc0 += (double)q2 * q2;
+        } else {  // Dormand-Prince stage stg (k = k_{stg + 1}): the running sums take k's column
+          float a0 = 0.f;
+#pragma unroll
+          for (int q = 0; q < 5; ++q) {
+            const float v = es[(kEA + q + 1) * BD + i] + k * (c[q] * dt32);
+            es[(kEA + q) * BD + i] = v;
+            if (q == 0) a0 = v;
+          }
+          const float err = es[kEErr * BD + i] + k * (c[6] * dt32);
+          es[kEErr * BD + i] = err;
+          es[kEMid * BD + i] = es[kEMid * BD + i] + k * (c[7] * dt32);
+          if (stg < 5) {
+            const float yi = y + a0;
+            st_wt(a.xin + pn * BD + i, yi);
+            es[kEY1 * BD + i] = yi;
+          } else {  // FSAL: k is f(t1, y1); the error ratio's term and torchdiffeq's finiteness assert
+            es[kEKl * BD + i] = k;
+            const float y1 = es[kEY1 * BD + i];
+            const float tol = a.atol + a.rtol * fmaxf(fabsf(y), fabsf(y1));
+            const float qe = err / tol;
+            acc0 += (double)qe * qe;
+            acc1 += __builtin_isfinite(y) ? 0.0 : 1.0;
+          }
+        }
+      });
+    }
+    // ---- the decision (thread 0) ----
+    const int kind = ctl.kind, stg = ctl.stg;
+    const bool reduce = !(kind == kCmbF0 && a.first_step > 0.0) && !(kind == kCmbStage && stg < 5);
+    double s0 = 0.0, s1 = 0.0;
+    if (reduce && wide_sum2(a.bar, a.slot, acc0, acc1, s0, s1)) {
+      status = 4;
+      break;
+    }
+    acc0 = acc1 = 0.0;  // (f0's norm terms are unused when first_step is given)
+    __syncthreads();  // every wave has read this evaluation's control words before thread 0 rewrites them
+    if (tid == 0) {
+      ctl.nev = e + 1;
+      ++ctl.nfev;
+      ctl.fit = 0;
+      ctl.next = kNextNone;
+      ctl.io_lo = ctl.io_hi = ctl.iout;
+      bool sched = false;  // outputs due, then the next attempt
+      if (kind == kCmbStage && stg < 5) {
+        ctl.stg = stg + 1;
+        ctl.next = kNextNone;  // the combine already wrote the next stage input
+      } else if (kind == kCmbF0 && !(a.first_step > 0.0)) {  // misc._select_initial_step in fp32
+        const float d0 = fabsf(sqrtf((float)(s0 / n_el)));
+        const float d1 = fabsf(sqrtf((float)(s1 / n_el)));
+        float h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : (0.01f * d0) / d1;
+        ctl.h0 = fabsf(h0);
+        ctl.d1 = d1;
+        ctl.kind = kCmbF1;
+        ctl.next = kNextProbe;
+      } else if (kind == kCmbF1) {
+        const float h0 = ctl.h0, d1 = ctl.d1;
+        const float d2 = fabsf(sqrtf((float)(s0 / n_el)) / h0);
+        float h1;
+        if (d1 <= 1e-15f && d2 <= 1e-15f) h1 = fmaxf(1e-6f, h0 * 1e-3f);
+        else h1 = (float)pow((double)(0.01f / fmaxf(d1, d2)), (double)0.2f);  // fp64 pow rounded once: host == device
+        ctl.dt = (double)fminf(100.0f * h0, fabsf(h1));
+        sched = true;
+      } else if (kind == kCmbF0) {  // first_step given
+        sched = true;
+      } else {  // the attempt's error ratio, accept / reject, rk_common._optimal_step_size
+        if (s1 != 0.0) {
+          ctl.status = 1;
+        } else {
+          const float ratio = sqrtf((float)(s0 / n_el));
+          const bool accept = ratio <= 1.0f;
+          const double dt = ctl.dt;
+          if (blockIdx.x == 0 && ctl.n_att < a.max_att) {
+            double* o = a.att + (int64_t)ctl.n_att * 4;
+            o[0] = ctl.t0;
+            o[1] = dt;
+            o[2] = (double)ratio;
+            o[3] = accept ? 1.0 : 0.0;
+          }
+          ++ctl.n_att;
+          if (accept) {
+            ctl.fit = 1;
+            ctl.fit_dt32 = ctl.dt32;  // the accepted attempt's step (dt32 is about to take the next one)
+            ctl.t0s = ctl.t0;
+            ctl.t1s = ctl.t1;
+          } else {
+            ctl.t0s = ctl.t0;
+          }
+          const double rr = (double)ratio;
+          double nxt;
+          if (rr == 0.0) {
+            nxt = dt * a.ifactor;
+          } else {
+            const double dfac = rr < 1.0 ? 1.0 : a.dfactor;
+            const double factor = __builtin_isnan(rr) ? rr : fmin(a.ifactor, fmax(a.safety / pow(rr, 1.0 / 5.0), dfac));
+            nxt = dt * factor;
+          }
+          ctl.dt = __builtin_isnan(nxt) ? nxt : fmin(fmax(nxt, a.min_step), a.max_step);
+          ++ctl.n_steps;
+          sched = true;
+        }
+      }
+      if (sched) {
+        // outputs due (interp._interp_evaluate of the last accepted step), then the next attempt
+        int io = ctl.iout;
+        while (io < a.T && !(a.t[io] > ctl.t1s)) {
+          ++io;
+          ctl.n_steps = 0;
+        }
+        ctl.io_hi = io;
+        ctl.iout = io;
+        if (io >= a.T) {
+          ctl.status = 0;
+        } else if (ctl.n_steps >= a.max_steps) {
+          ctl.status = 3;
+        } else {
+          const double t0 = ctl.t1s, dt = ctl.dt;
+          if (!(t0 + dt > t0)) {
+            ctl.status = 2;
+          } else {
+            ctl.t0 = t0;
+            ctl.t1 = t0 + dt;
+            ctl.dt32 = (float)dt;
+            ctl.kind = kCmbStage;
+            ctl.stg = 0;
+            ctl.next = kNextAttempt;
+          }
+        }
+      }
+      // the tableau column of the next stage evaluation's k (static indices: kernel-argument reads)
+#pragma unroll
+      for (int j = 1; j < 7; ++j)
+        if (j == ctl.stg + 1) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) ctl.cc[q] = a.stc[j][q];
+        }
+    }
+    __syncthreads();
+    // ---- the decision's element passes (owner threads only: no hand-off) ----
+    if (ctl.fit) {  // interp._interp_fit (fetode_interp_fit's op order); y <- y1, f0 <- k7
+      const float dtc = ctl.fit_dt32;
+      for_owned([&](int64_t i) {
+        const float y = es[kEY * BD + i], y1 = es[kEY1 * BD + i];
+        const float fa = es[kEF0 * BD + i], fb = es[kEKl * BD + i];
+        const float ym = y + es[kEMid * BD + i];
+        es[(kECo + 4) * BD + i] = ((2.0f * dtc) * (fb - fa) - 8.0f * (y1 + y)) + 16.0f * ym;
+        es[(kECo + 3) * BD + i] = ((dtc * (5.0f * fa - 3.0f * fb) + 18.0f * y) + 14.0f * y1) - 32.0f * ym;
+        es[(kECo + 2) * BD + i] = ((dtc * (fb - 4.0f * fa) - 11.0f * y) - 5.0f * y1) + 16.0f * ym;
+        es[(kECo + 1) * BD + i] = dtc * fa;
+        es[kECo * BD + i] = y;
+        es[kEY * BD + i] = y1;
+        es[kEF0 * BD + i] = fb;
+      });
+    }
+    for (int j = ctl.io_lo; j < ctl.io_hi; ++j) {
+      const float xq = (float)((a.t[j] - ctl.t0s) / (ctl.t1s - ctl.t0s));
+      float* const so = a.sol + (int64_t)j * BD;
+      for_owned([&](int64_t i) {
+        float total = es[kECo * BD + i] + xq * es[(kECo + 1) * BD + i];
+        float xp = xq;
+#pragma unroll
+        for (int q = 2; q < 5; ++q) {
+          xp = xp * xq;
+          total = total + xp * es[(kECo + q) * BD + i];
+        }
+        so[i] = total;
+      });
+    }
+    if (ctl.status >= 0) {
+      status = ctl.status;
+      break;
+    }
+    const int pw = (e + 1) & 1;
+    if (ctl.next == kNextProbe) {  // y0 + f0 h0 (fetode_lincomb with k[0] = f0)
+      const float hh = ctl.h0;
+      for_owned([&](int64_t i) { st_wt(a.xin + pw * BD + i, es[kEY * BD + i] + es[kEF0 * BD + i] * hh); });
+    } else if (ctl.next == kNextAttempt) {  // the attempt's running sums from f0, its first stage input
+      const float dtc = ctl.dt32;
+      for_owned([&](int64_t i) {
+        const float f0 = es[kEF0 * BD + i];
+        float a0 = 0.f;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) {
+          const float v = f0 * (a.stc[0][q] * dtc);
+          es[(kEA + q) * BD + i] = v;
+          if (q == 0) a0 = v;
+        }
+        es[kEErr * BD + i] = f0 * (a.stc[0][6] * dtc);
+        es[kEMid * BD + i] = f0 * (a.stc[0][7] * dtc);
+        const float yi = es[kEY * BD + i] + a0;
+        st_wt(a.xin + pw * BD + i, yi);
+        es[kEY1 * BD + i] = yi;
+      });
+    }
+  }
+  const int nev = ctl.nev;
+  if (status != 4 && nev > 0) {
+    // the hysteresis memory after the solve: the last evaluation's layer inputs (ferro_class.py:409)
+    const int el = nev - 1, pl = el & 1;
+    const float* x0 = el == 0 ? a.y0 : a.xin + pl * BD;
+    const float* h0 = a.hs + (int64_t)pl * a.S0 * BH;
+    const int64_t nthr = (int64_t)G * kThreads;
+    for (int64_t j = (int64_t)blockIdx.x * kThreads + tid; j < BH; j += nthr) {
+      a.st1[j] = a.S0 == 2 ? h0[j] + h0[BH + j] : h0[j];
+      if (j < BD) a.st0[j] = x0[j];
+    }
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    a.stats[0] = ctl.nfev;
+    a.stats[1] = ctl.n_att;
+    a.stats[2] = __hip_atomic_load(a.bar + 64 * 9 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 4 : status;
+  }
+}
+
+struct WideDopriShape {
+  int S0, S1, nT0, nT1, nOT0, nOT1;
+  int64_t off_slot, off_xin, off_hs, off_ks, off_es, bytes;  // byte offsets in the workspace
+};
+
+// input slices per layer: the per-layer launch's rule (fetode_wide_layer_forward), so each layer's
+// sums are formed in the same order as the host-driven loop's
+WideDopriShape wide_dopri_shape(int64_t B, int D, int H) {
+  WideDopriShape s{};
+  const int64_t rows = (B + kRows - 1) / kRows;
+  s.nOT0 = H / kOuts;
+  s.nOT1 = D / kOuts;
+  s.nT0 = (int)(rows * s.nOT0);
+  s.nT1 = (int)(rows * s.nOT1);
+  s.S0 = (s.nT0 <= 2 * 256 && (D / 2) % kChMax == 0) ? 2 : 1;
+  s.S1 = (s.nT1 <= 2 * 256 && (H / 2) % kChMax == 0) ? 2 : 1;
+  auto al = [](int64_t v) { return (v + 255) & ~int64_t(255); };
+  int64_t o = al((int64_t)sizeof(unsigned) * kWBarWords);
+  s.off_slot = o;
+  o = al(o + (int64_t)sizeof(double) * 2 * kWideDopriMaxGrid);
+  s.off_xin = o;
+  o = al(o + (int64_t)sizeof(float) * 2 * B * D);
+  s.off_hs = o;
+  o = al(o + (int64_t)sizeof(float) * 2 * s.S0 * B * H);
+  s.off_ks = o;
+  o = al(o + (int64_t)sizeof(float) * s.S1 * B * D);
+  s.off_es = o;
+  o = al(o + (int64_t)sizeof(float) * kEs * B * D);
+  s.bytes = o;
+  return s;
+}
+
 }  // namespace
 
 extern "C" {
@@ -966,7 +1549,7 @@ int fetode_wide_layer_forward(const fetode_kanlinear_t* kl, const fetode_ferro_t
   if (B <= 0) return FETODE_OK;
   if (!plan || !x || !out || (fl && !reinit && !prev)) return set_err(FETODE_EINVAL, "wide layer: null pointer");
   if (x == out) return set_err(FETODE_EINVAL, "wide layer: out must not alias x");
-  WideArgs a;
+  WideArgs a{};
   a.plan = (const float*)plan;
   a.L = wide_layout(kl, fl);
   a.x = x;
@@ -1108,5 +1691,107 @@ int fetode_kanlinear_backward_wide(const fetode_kanlinear_t* kl, const fetode_fe
   return FETODE_OK;
 }
 
-}  // extern "C"
 
+int64_t fetode_wide_dopri5_workspace(int64_t B, int32_t D, int32_t H) {
+  if (B <= 0 || D < 16 || H < 16) return -1;
+  return wide_dopri_shape(B, D, H).bytes;
+}
+
+int fetode_wide_dopri5(const fetode_kanlinear_t* kan0, const fetode_ferro_t* fer0, const void* plan0,
+                       const fetode_kanlinear_t* kan1, const fetode_ferro_t* fer1, const void* plan1, const float* y0,
+                       int64_t B, const float* prev0, const float* prev1, uint32_t reinit_mask, const double* t,
+                       int32_t T, double rtol, double atol, const double* opts, const float* tableau, float* solution,
+                       float* state0, float* state1, void* workspace, int32_t* stats, double* attempts,
+                       int32_t max_attempts, void* stream) {
+  if (!kan0 || !fer0 || !kan1 || !fer1) return set_err(FETODE_EUNSUPPORTED, "wide dopri5: needs two KAN-FET layers");
+  if (!wide_supported(kan0, fer0) || !wide_supported(kan1, fer1))
+    return set_err(FETODE_EUNSUPPORTED, "wide dopri5: a layer has no wide kernel");
+  const int D = kan0->in_features, H = kan0->out_features;
+  if (kan1->in_features != H || kan1->out_features != D)
+    return set_err(FETODE_EINVAL, "wide dopri5: layer 1 must map %d -> %d", H, D);
+  if (fer0->num_basis != fer1->num_basis) return set_err(FETODE_EUNSUPPORTED, "wide dopri5: layers with different K");
+  if (B <= 0 || T < 1) return set_err(FETODE_EINVAL, "wide dopri5: B and T must be positive");
+  if (!plan0 || !plan1 || !y0 || !t || !opts || !tableau || !solution || !state0 || !state1 || !workspace || !stats)
+    return set_err(FETODE_EINVAL, "wide dopri5: null pointer");
+  if ((!(reinit_mask & 1u) && !prev0) || (!(reinit_mask & 2u) && !prev1))
+    return set_err(FETODE_EINVAL, "wide dopri5: null hysteresis state");
+  const WideDopriShape sh = wide_dopri_shape(B, D, H);
+  if ((int64_t)sh.nT0 * sh.S0 > 0x7fffffff / 2) return set_err(FETODE_EINVAL, "wide dopri5: batch too large");
+  const int K = fer0->num_basis;
+  const void* fn = K == 12 ? (const void*)wide_dopri5_kernel<12> : (const void*)wide_dopri5_kernel<10>;
+  // persistent grid: every workgroup resident at once (the phases meet at grid barriers)
+  static int per_cu[2] = {0, 0}, n_cu = 0;
+  const int fi = K == 12 ? 1 : 0;
+  if (!n_cu) {
+    int dev = 0;
+    HIP_CHECK_RET(hipGetDevice(&dev));
+    HIP_CHECK_RET(hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  if (!per_cu[fi]) HIP_CHECK_RET(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[fi], fn, kThreads, 0));
+  const int64_t want = std::max<int64_t>((int64_t)sh.nT0 * sh.S0, (int64_t)sh.nT1 * sh.S1);
+  int64_t grid = std::min<int64_t>({want, (int64_t)per_cu[fi] * n_cu, (int64_t)kWideDopriMaxGrid});
+  static const int64_t grid_cap = [] {  // diagnostics: cap the persistent grid (FETODE_WIDE_DOPRI_GRID)
+    const char* e = getenv("FETODE_WIDE_DOPRI_GRID");
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+  }();
+  if (grid_cap > 0) grid = std::min(grid, grid_cap);
+  if (grid < 1) return set_err(FETODE_EHIP, "wide dopri5: no resident workgroup");
+  WideDopriArgs a{};
+  a.l0.plan = (const float*)plan0;
+  a.l0.L = wide_layout(kan0, fer0);
+  a.l0.grid = kan0->grid;
+  a.l0.B = B;
+  a.l1.plan = (const float*)plan1;
+  a.l1.L = wide_layout(kan1, fer1);
+  a.l1.grid = kan1->grid;
+  a.l1.B = B;
+  a.B = B;
+  a.D = D;
+  a.H = H;
+  a.S0 = sh.S0;
+  a.S1 = sh.S1;
+  a.nT0 = sh.nT0;
+  a.nT1 = sh.nT1;
+  a.nOT0 = sh.nOT0;
+  a.nOT1 = sh.nOT1;
+  a.reinit0 = (reinit_mask & 1u) ? 1 : 0;
+  a.reinit1 = (reinit_mask & 2u) ? 1 : 0;
+  a.y0 = y0;
+  a.prev0 = prev0;
+  a.prev1 = prev1;
+  a.st0 = state0;
+  a.st1 = state1;
+  char* ws = (char*)workspace;
+  a.bar = (unsigned*)ws;
+  a.slot = (double*)(ws + sh.off_slot);
+  a.xin = (float*)(ws + sh.off_xin);
+  a.hs = (float*)(ws + sh.off_hs);
+  a.ks = (float*)(ws + sh.off_ks);
+  a.es = (float*)(ws + sh.off_es);
+  a.sol = solution;
+  a.t = t;
+  a.T = T;
+  a.rtol = (float)rtol;
+  a.atol = (float)atol;
+  a.first_step = opts[0];
+  a.safety = opts[1];
+  a.ifactor = opts[2];
+  a.dfactor = opts[3];
+  a.min_step = opts[4];
+  a.max_step = opts[5];
+  a.max_steps = opts[6] > 2e9 ? 2000000000 : (int)opts[6];
+  for (int j = 0; j < 7; ++j) {  // tableau = beta (6 x 6, row i = stage i + 1), c_error (7), c_mid (7)
+    for (int q = 0; q < 6; ++q) a.stc[j][q] = (j < 6 && j + q < 6) ? tableau[(j + q) * 6 + j] : 0.0f;
+    a.stc[j][6] = tableau[36 + j];
+    a.stc[j][7] = tableau[43 + j];
+  }
+  a.stats = stats;
+  a.att = attempts;
+  a.max_att = attempts ? max_attempts : 0;
+  hipStream_t s = (hipStream_t)stream;
+  HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kWBarWords, s));
+  void* args[] = {&a};
+  HIP_CHECK_RET(resident_launch(fn, dim3((unsigned)grid), dim3(kThreads), args, 0, s));
+  return FETODE_OK;
+}
+}  // extern "C"

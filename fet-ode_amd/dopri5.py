@@ -17,6 +17,7 @@ from __future__ import annotations
 
 import atexit
 import math
+import os
 
 import numpy as np
 import torch
@@ -481,7 +482,93 @@ def _try_field_resident(func, y0, tp, reversed_, rtol, atol, options):
     return sol
 
 
+def _try_wide_resident(func, y0, tp, reversed_, rtol, atol, options):
+    """The whole solve in one launch (fetode_wide_dopri5) when `func` is a tagged two-layer wide
+    KAN-FET field — the ETT forecaster's KANFETDynamics, KANFET([latent, hidden, latent]),
+    train_kan_fet_ett.py:192 — nothing needs gradients and the options are the scalar ones."""
+    from .autograd_ops import field_layers, wide_plan
+    from .odeint import fused_field
+    field = fused_field(func)
+    if field is None or reversed_ or y0.dim() != 2 or set(options) - _RESIDENT_OPTS:
+        return None
+    if not getattr(field, "has_ferro", False):
+        return None
+    if not (isinstance(rtol, (int, float)) and isinstance(atol, (int, float))):
+        return None
+    layers = field_layers(field)
+    if len(layers) != 2 or any(f is None or f._bsign is not None or f.use_noise for _, f in layers):
+        return None
+    (k0, f0), (k1, f1) = layers
+    B, D = y0.shape
+    H = k0.out_features
+    if D != k0.in_features or k1.in_features != H or k1.out_features != D or f0.num_basis != f1.num_basis:
+        return None
+    if torch.is_grad_enabled() and (y0.requires_grad or any(p.requires_grad for p in field.parameters())):
+        return None
+    dev = y0.device
+    e0, e1 = wide_plan(k0, f0, dev), wide_plan(k1, f1, dev)
+    if e0 is None or e1 is None:
+        return None
+    lib = _lib.load()
+    ws_bytes = lib.fetode_wide_dopri5_workspace(B, D, H)
+    if ws_bytes < 0:
+        return None
+    yc = _lib.f32c(y0)
+
+    def mem(f, width):
+        p = f._prev
+        fresh = p.shape != (B, width) or p.device != dev or p.dtype != torch.float32 or not p.is_contiguous()
+        return fresh, p
+
+    re0, p0 = mem(f0, D)
+    re1, p1 = mem(f1, H)
+    st0 = torch.empty(B, D, device=dev, dtype=torch.float32) if re0 else p0   # prev_x after the solve
+    st1 = torch.empty(B, H, device=dev, dtype=torch.float32) if re1 else p1
+    tkey = (dev, tuple(tp.tolist()))
+    t_dev = _T_DEV.get(tkey)
+    if t_dev is None:
+        if len(_T_DEV) > 64:
+            _T_DEV.clear()
+        t_dev = _T_DEV[tkey] = tp.to(torch.float64).to(dev)
+    T = t_dev.numel()
+    sol = torch.empty(T, B, D, device=dev, dtype=torch.float32)
+    ws = torch.empty(max(1, ws_bytes // 4), device=dev, dtype=torch.float32)
+    stats = torch.empty(3, device=dev, dtype=torch.int32)
+    att = torch.empty(_MAX_TRACE, 4, device=dev, dtype=torch.float64)
+    fs = options.get("first_step")
+    opts = np.array([float(fs) if fs is not None else 0.0, float(options.get("safety", 0.9)),
+                     float(options.get("ifactor", 10.0)), float(options.get("dfactor", 0.2)),
+                     float(options.get("min_step", 0.0)), float(options.get("max_step", math.inf)),
+                     float(options.get("max_num_steps", 2 ** 31 - 1))], dtype=np.float64)
+    by = _lib.ctypes.byref
+    rc = lib.fetode_wide_dopri5(
+        by(e0[1]), by(e0[2]), e0[0].data_ptr(), by(e1[1]), by(e1[2]), e1[0].data_ptr(), yc.data_ptr(), B,
+        None if re0 else p0.data_ptr(), None if re1 else p1.data_ptr(), (1 if re0 else 0) | (2 if re1 else 0),
+        t_dev.data_ptr(), T, float(rtol), float(atol), opts.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_double)),
+        _TABLEAU.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_float)), sol.data_ptr(), st0.data_ptr(),
+        st1.data_ptr(), ws.data_ptr(), stats.data_ptr(), att.data_ptr(), _MAX_TRACE, _lib.stream_handle(dev))
+    if rc == _lib.FETODE_EUNSUPPORTED:
+        return None
+    _lib.check(rc, "fetode_wide_dopri5")
+    if re0:
+        f0._prev = st0
+    if re1:
+        f1._prev = st1
+    dopri5_solve.last = ResidentSolve(stats, att)
+    _status_check(stats, "fetode_wide_dopri5: a grid barrier timed out (workgroups not co-resident); "
+                         "the solution is invalid")
+    return sol
+
+
 _RESIDENT = True
+_WIDE_RESIDENT = os.environ.get("FETODE_WIDE_RESIDENT", "1") != "0"
+
+
+def set_wide_resident_dopri5(enabled: bool) -> bool:
+    """Device-resident dopri5 for the wide KAN-FET fields (default) or the host-driven loop."""
+    global _WIDE_RESIDENT
+    prev, _WIDE_RESIDENT = _WIDE_RESIDENT, bool(enabled)
+    return prev
 
 
 def set_resident_dopri5(enabled: bool) -> bool:
@@ -685,6 +772,8 @@ def dopri5_solve(func, y0, tc, tp, reversed_, rtol, atol, options):
         sol = _try_ecg_resident(func, y0, tp, reversed_, rtol, atol, options)
         if sol is None:
             sol = _try_field_resident(func, y0, tp, reversed_, rtol, atol, options)
+        if sol is None and _WIDE_RESIDENT:
+            sol = _try_wide_resident(func, y0, tp, reversed_, rtol, atol, options)
         if sol is not None:
             return sol
     if _needs_grad(func, y0):

@@ -156,6 +156,31 @@ int fetode_wide_layer_forward(const fetode_kanlinear_t* layer, const fetode_ferr
                               const float* x, int64_t B, const float* prev, int32_t reinit, float* out,
                               void* stream);
 
+/* The whole dopri5 solve of a two-layer wide KAN-FET field (KANFET([D, H, D]) with both layers
+ * fetode_wide_layer_supported, KAN + Ferro, the same K) in ONE launch: the ETT forecaster's latent
+ * solve odeint(self.dynamics, z0, t_fut, method="dopri5") (train_kan_fet_ett.py:192, :858, :879; the
+ * dynamics' field KANFET([latent, hidden, latent]), BASELINE configs[3]).  A persistent grid walks
+ * the wide-layer tiles phase by phase (layer 0 | grid barrier | layer 1 | grid barrier | stage
+ * combine) with the host-driven loop's arithmetic: each layer's input slices as
+ * fetode_wide_layer_forward picks them, fetode_lincomb's stage sums, fetode_scaled_rms's error ratio
+ * (fp64, over the whole batch), _optimal_step_size in fp64, _interp_fit / _interp_evaluate — so the
+ * attempts, nfev and solution are the host loop's.  Every evaluation (rejected attempts' too) sees
+ * and advances the hysteresis memory (ferro_class.py:409).
+ *   plan0 / plan1: fetode_wide_layer_plan_build of each layer (KAN + Ferro); y0 (B, D);
+ *   prev0 (B, D) / prev1 (B, H): each layer's prev_x before the solve, unread where reinit_mask bit
+ *   0 / 1 is set (first call: prev = x); t (dev, fp64, T) strictly increasing; opts / tableau as
+ *   fetode_integrate_dopri5; solution (T, B, D); state0 (B, D) / state1 (B, H) receive the prev_x
+ *   after the solve (may alias prev0 / prev1); workspace: fetode_wide_dopri5_workspace(B, D, H) bytes;
+ *   stats / attempts as fetode_integrate_dopri5.  Replaces: the host loop of dopri5.py over
+ *   KANFETDynamics (two fetode_wide_layer_forward per evaluation, a read-back per attempt). */
+int fetode_wide_dopri5(const fetode_kanlinear_t* kan0, const fetode_ferro_t* ferro0, const void* plan0,
+                       const fetode_kanlinear_t* kan1, const fetode_ferro_t* ferro1, const void* plan1,
+                       const float* y0, int64_t B, const float* prev0, const float* prev1, uint32_t reinit_mask,
+                       const double* t, int32_t T, double rtol, double atol, const double* opts,
+                       const float* tableau, float* solution, float* state0, float* state1, void* workspace,
+                       int32_t* stats, double* attempts, int32_t max_attempts, void* stream);
+int64_t fetode_wide_dopri5_workspace(int64_t B, int32_t D, int32_t H);
+
 /* The whole dopri5 solve of a fused-shape field (the LV KAN / KAN-FET [2,10,2] fields) in ONE
  * cooperative launch — torchdiffeq's default method of every reference odeint without `method`
  * (train_kanfet_node_predprey.py:252,260, rtol 1e-7 / atol 1e-9): f0, misc._select_initial_step
