@@ -236,19 +236,60 @@ struct WideArgs {
   const float* grid;  // (in, 12) knots
   int64_t B;
   int reinit;
-  int nslice;  // 1, or 2: blockIdx.z takes half of the inputs and adds into a zeroed out
+  int nslice;  // input slices (wide_slices): blockIdx.z takes 1 / nslice of the inputs
   float* out;
   // resident solver only (wide_tile<.., RES = true>): the layer input / its hysteresis memory as the
-  // fixed-order sum of two input-sliced partial slabs (x + x2), null when whole
-  const float* x2;
-  const float* prev2;
+  // fixed-order sum ((s0 + s1) + s2) + .. of nxs / nps input-sliced partial slabs, xss / pss floats apart
+  int nxs, nps;
+  int64_t xss, pss;
 };
+
+// Input slices of a layer launch: with few (row, output) tiles the CUs are short of waves (and at
+// small batches one tile's walk over all inputs is the whole latency), so the inputs are split over
+// up to 8 workgroups per tile, each walking in / nslice of them (whole chunks of 8).  The partial
+// sums meet in a fixed order — slab 0 + slab 1 (+ slab 2 ..), left to right — in both the per-layer
+// launch (two slices: vector atomics into a zeroed out, 0 + a + b; more: slabs + wide_slab_sum_kernel)
+// and the resident solver (the consumer sums the slabs), so the two paths agree bit for bit.
+int wide_slices(int64_t wgs, int in) {
+  int S = 1;
+  while (S < 8 && wgs * S <= 2 * 256 && (in / (2 * S)) % kChMax == 0 && in % (2 * S) == 0) S *= 2;
+  return S;
+}
 
 // One slice stores; two add into a zeroed out with vector atomics: 0 + a + b in either order is the
 // same fp32 value (addition commutes), so the split stays bitwise deterministic.
 __device__ __forceinline__ void store_out(float* p, float v, int nslice) {
-  if (nslice == 1) *p = v;
+  if (nslice != 2) *p = v;  // whole, or this slice's own slab
   else atomicAdd(p, v);
+}
+
+// out = ((s0 + s1) + s2) + .. of the slabs (slice s at s * n)
+__global__ void wide_slab_sum_kernel(const float* __restrict__ slab, int S, int64_t n, float* __restrict__ out) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  float v = slab[j];
+  for (int s = 1; s < S; ++s) v = v + slab[s * n + j];
+  out[j] = v;
+}
+
+// grow-only per-device scratch for the slabs of > 2 input slices (the per-layer launch's ABI has no
+// workspace argument); reallocated outside any stream work only when a larger batch first needs it
+float* slab_scratch(size_t floats) {
+  static float* buf[64] = {};
+  static size_t cap[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (cap[dev] < floats) {
+    if (buf[dev]) {
+      (void)hipDeviceSynchronize();
+      (void)hipFree(buf[dev]);
+    }
+    buf[dev] = nullptr;
+    cap[dev] = 0;
+    if (hipMalloc(&buf[dev], floats * sizeof(float)) != hipSuccess) return nullptr;
+    cap[dev] = floats;
+  }
+  return buf[dev];
 }
 
 // ---- the layer --------------------------------------------------------------------------------
@@ -258,7 +299,7 @@ typedef __attribute__((address_space(4))) const float4 kconst_f4;
 // One tile (row block bx, output block by, input slice bz) of the layer.  The per-layer launch
 // (wide_layer_kernel) runs one per workgroup; the device-resident dopri5 solver (wide_dopri5_kernel)
 // walks every tile of a layer phase with its persistent grid.  RES: the input and the hysteresis
-// memory may be the sum of two partial slabs (x2 / prev2), and every output goes through `epi`
+// memory may be the sum of input-sliced partial slabs (nxs / nps), and every output goes through `epi`
 // (a write-through store, or the solver's per-element stage combine) instead of store_out.
 template <int K, bool KAN, bool FERRO, int kCh, bool RES, class Epi>
 __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const int by, const int bz, Epi&& epi) {
@@ -298,12 +339,16 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
   // previous chunk's work)
   const int ibeg = bz * (in / a.nslice), iend = ibeg + in / a.nslice;
   auto ldx = [&](int64_t i) -> float {
-    if constexpr (RES) return a.x2 ? a.x[i] + a.x2[i] : a.x[i];   // slab 0 + slab 1: the host path's 0 + a + b
-    return a.x[i];
+    float v = a.x[i];
+    if constexpr (RES)
+      for (int s = 1; s < a.nxs; ++s) v = v + a.x[i + s * a.xss];   // slab 0 + slab 1 + ..: the launch path's order
+    return v;
   };
   auto ldp = [&](int64_t i) -> float {
-    if constexpr (RES) return a.prev2 ? a.prev[i] + a.prev2[i] : a.prev[i];
-    return a.prev[i];
+    float v = a.prev[i];
+    if constexpr (RES)
+      for (int s = 1; s < a.nps; ++s) v = v + a.prev[i + s * a.pss];
+    return v;
   };
   float xn = slive ? ldx(sb * in + ibeg + si) : 0.f;
   float pn = (FERRO && slive && !a.reinit) ? ldp(sb * in + ibeg + si) : 0.f;
@@ -462,7 +507,7 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
 template <int K, bool KAN, bool FERRO, int kCh>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6))) void wide_layer_kernel(WideArgs a) {
   const int out = a.L.out, ns = a.nslice;
-  float* const o = a.out;
+  float* const o = a.out + (ns > 2 ? (int64_t)blockIdx.z * a.B * out : 0);
   wide_tile<K, KAN, FERRO, kCh, false>(a, blockIdx.x, blockIdx.y, blockIdx.z,
                                        [&](int64_t b, int c, float v) { store_out(&o[b * out + c], v, ns); });
 }
@@ -1217,16 +1262,17 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       const int nT = l ? a.nT1 : a.nT0, nOT = l ? a.nOT1 : a.nOT0, S = l ? a.S1 : a.S0;
       if (l == 0) {
         L.x = e == 0 ? a.y0 : a.xin + p * BD;
-        L.x2 = nullptr;
+        L.nxs = L.nps = 1;
         L.reinit = e == 0 ? a.reinit0 : 0;
         L.prev = e == 0 ? a.prev0 : (e == 1 ? a.y0 : a.xin + (p ^ 1) * BD);
-        L.prev2 = nullptr;
       } else {
         L.x = a.hs + (int64_t)p * a.S0 * BH;
-        L.x2 = a.S0 == 2 ? L.x + BH : nullptr;
+        L.nxs = a.S0;
+        L.xss = BH;
         L.reinit = e == 0 ? a.reinit1 : 0;
         L.prev = e == 0 ? a.prev1 : a.hs + (int64_t)(p ^ 1) * a.S0 * BH;
-        L.prev2 = (e > 0 && a.S0 == 2) ? L.prev + BH : nullptr;
+        L.nps = e == 0 ? 1 : a.S0;
+        L.pss = BH;
       }
       L.nslice = S;
       const int ow = l ? D : H;
@@ -1251,9 +1297,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       float c[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) c[q] = ctl.cc[q];
-      const bool two = a.S1 == 2;
+      const int S1 = a.S1;
       for_owned([&](int64_t i) {
-        const float k = two ? a.ks[i] + a.ks[BD + i] : a.ks[i];  // slab 0 + slab 1: the launch path's 0 + a + b
+        float k = a.ks[i];
+        for (int s = 1; s < S1; ++s) k = k + a.ks[s * BD + i];  // slab 0 + slab 1 + ..: the launch path's order
         const float y = es[kEY * BD + i];
         if (kind == kCmbF0) {  // f0 = f(t0, y0); _select_initial_step's d0 / d1 terms
           es[kEF0 * BD + i] = k;
@@ -1467,7 +1514,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const float* h0 = a.hs + (int64_t)pl * a.S0 * BH;
     const int64_t nthr = (int64_t)G * kThreads;
     for (int64_t j = (int64_t)blockIdx.x * kThreads + tid; j < BH; j += nthr) {
-      a.st1[j] = a.S0 == 2 ? h0[j] + h0[BH + j] : h0[j];
+      float v = h0[j];
+      for (int s = 1; s < a.S0; ++s) v = v + h0[s * BH + j];
+      a.st1[j] = v;
       if (j < BD) a.st0[j] = x0[j];
     }
   }
@@ -1492,8 +1541,8 @@ WideDopriShape wide_dopri_shape(int64_t B, int D, int H) {
   s.nOT1 = D / kOuts;
   s.nT0 = (int)(rows * s.nOT0);
   s.nT1 = (int)(rows * s.nOT1);
-  s.S0 = (s.nT0 <= 2 * 256 && (D / 2) % kChMax == 0) ? 2 : 1;
-  s.S1 = (s.nT1 <= 2 * 256 && (H / 2) % kChMax == 0) ? 2 : 1;
+  s.S0 = wide_slices(s.nT0, D);
+  s.S1 = wide_slices(s.nT1, H);
   auto al = [](int64_t v) { return (v + 255) & ~int64_t(255); };
   int64_t o = al((int64_t)sizeof(unsigned) * kWBarWords);
   s.off_slot = o;
@@ -1563,10 +1612,23 @@ int fetode_wide_layer_forward(const fetode_kanlinear_t* kl, const fetode_ferro_t
   // Few tiles (e.g. 128 -> 64 at B = 8192: 512 workgroups for 256 CUs x 3 resident) leave the CUs
   // short of waves to hide the staging latency: split the inputs over two workgroups per tile.
   const int64_t wgs = tiles * (a.L.out / kOuts);
-  a.nslice = (wgs <= 2 * 256 && (a.L.in / 2) % kChMax == 0) ? 2 : 1;
-  if (a.nslice == 2) HIP_CHECK_RET(hipMemsetAsync(out, 0, sizeof(float) * B * a.L.out, (hipStream_t)stream));
-  hipLaunchKernelGGL(pick(a.L.K, a.L.kan, a.L.ferro), dim3((unsigned)tiles, (unsigned)(a.L.out / kOuts), (unsigned)a.nslice),
-                     dim3(kThreads), 0, (hipStream_t)stream, a);
+  a.nslice = wide_slices(wgs, a.L.in);
+  a.nxs = a.nps = 1;
+  const hipStream_t st = (hipStream_t)stream;
+  const dim3 grid((unsigned)tiles, (unsigned)(a.L.out / kOuts), (unsigned)a.nslice);
+  if (a.nslice == 2) HIP_CHECK_RET(hipMemsetAsync(out, 0, sizeof(float) * B * a.L.out, st));
+  if (a.nslice <= 2) {
+    hipLaunchKernelGGL(pick(a.L.K, a.L.kan, a.L.ferro), grid, dim3(kThreads), 0, st, a);
+  } else {  // slabs (slice s at s * B * out), then their fixed-order sum into out
+    const int64_t n = B * a.L.out;
+    float* slab = slab_scratch((size_t)a.nslice * n);
+    if (!slab) return set_err(FETODE_EHIP, "wide layer: slab scratch allocation failed");
+    a.out = slab;
+    hipLaunchKernelGGL(pick(a.L.K, a.L.kan, a.L.ferro), grid, dim3(kThreads), 0, st, a);
+    LAUNCH_CHECK();
+    hipLaunchKernelGGL(wide_slab_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (const float*)slab,
+                       a.nslice, n, out);
+  }
   LAUNCH_CHECK();
   return FETODE_OK;
 }
