@@ -464,47 +464,67 @@ def ett_rate(dev, batch=8192, reps=2, substeps=4, cpu_seconds=5.0, with_cpu=True
     return out
 
 
-def ett_dopri5_rate(dev, batch=8192, rtol=1e-3, atol=1e-4):
+def ett_dopri5_rate(dev, batch=8192, rtol=1e-3, atol=1e-4, small=256):
     """The reference forecaster's own solver call, odeint(dynamics, z0, t_fut, method="dopri5")
     (train_kan_fet_ett.py:192), with the KAN-FET latent field [64, 128, 64] (K = 10) on B = 8192
     96 -> 96 windows.  At torchdiffeq's default rtol 1e-7 / atol 1e-9 the fp32 KAN-FET field needs
-    ~160 k attempts per forward (measured at B = 256: 159 373 attempts, 956 k evaluations, 184 s;
-    DESIGN.md §4.5), so the line runs at rtol 1e-3 / atol 1e-4.  Each evaluation is two fused
-    wide-layer launches; the loop issues the attempts from the host (one status read per
-    attempt): `host_share` = 1 - nfev x (one evaluation's time) / wall."""
+    ~160 k attempts per forward (measured at B = 256: 159 373 attempts, 956 k evaluations, 184 s
+    on the host loop), so the line runs at rtol 1e-3 / atol 1e-4.  The forward's
+    solve is ONE launch (fetode_wide_dopri5: persistent grid over the wide-layer tiles, DESIGN.md
+    §4.8); `host_loop` times the host-driven loop on the same inputs (two wide-layer launches per
+    evaluation, one read-back per attempt; bitwise the same solution), `b256` both at B = 256."""
+    from fet_ode_amd import dopri5 as D
     from fet_ode_amd import ett
     c = p = 96
-    torch.manual_seed(0)
-    m = ett.LatentNeuralODEForecaster(num_features=7, context_len=c, pred_len=p, latent_dim=64, solver="dopri5",
-                                      rtol=rtol, atol=atol).to(dev)
-    g = torch.Generator().manual_seed(4)
-    series = torch.cumsum(torch.randn(batch + c + p, 7, generator=g), 0) * 0.05
-    ds = ett.EnergyWindowDataset(series, series[:, -1], c, p, device=dev)
-    xb, _ = ds.batch(torch.arange(batch, device=dev))
-    t_fut = torch.linspace(0.0, float(p - 1), steps=p, device=dev)
-    with torch.no_grad():
-        z0 = m.encoder(xb)
-        for _ in range(2):
-            m.dynamics(0.0, z0)
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(10):
-            m.dynamics(0.0, z0)
-        torch.cuda.synchronize(dev)
-        ev = (time.perf_counter() - t0) / 10
-        m.dynamics.net.reset_state()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        y = m(xb, t_fut)
-        torch.cuda.synchronize(dev)
-        wall = time.perf_counter() - t0
-    s = F.dopri5.dopri5_solve.last
-    return {"value": batch / wall, "unit": "forecast windows/s forward, dopri5 (96->96, 1 GPU)", "ms_per_batch": wall * 1e3,
-            "rtol": rtol, "atol": atol, "attempts": s.n_attempts, "nfev": s.nfev, "field_eval_ms": ev * 1e3,
-            "host_share": 1.0 - s.nfev * ev / wall, "finite": bool(torch.isfinite(y).all()),
-            "workload": f"LatentNeuralODEForecaster(7 features, 96->96, latent 64, KANFET[64,128,64] K=10), dopri5 "
-                        f"rtol {rtol:g} atol {atol:g}, batch {batch}, synthetic series",
-            "path": "dopri5 host loop; each evaluation = 2 fused wide-layer launches (fetode_wide_layer_forward)"}
+
+    def run(B, resident):
+        torch.manual_seed(0)
+        m = ett.LatentNeuralODEForecaster(num_features=7, context_len=c, pred_len=p, latent_dim=64, solver="dopri5",
+                                          rtol=rtol, atol=atol).to(dev)
+        g = torch.Generator().manual_seed(4)
+        series = torch.cumsum(torch.randn(B + c + p, 7, generator=g), 0) * 0.05
+        ds = ett.EnergyWindowDataset(series, series[:, -1], c, p, device=dev)
+        xb, _ = ds.batch(torch.arange(B, device=dev))
+        t_fut = torch.linspace(0.0, float(p - 1), steps=p, device=dev)
+        prev = D.set_wide_resident_dopri5(resident)
+        try:
+            with torch.no_grad():
+                z0 = m.encoder(xb)
+                for _ in range(2):
+                    m.dynamics(0.0, z0)
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                for _ in range(10):
+                    m.dynamics(0.0, z0)
+                torch.cuda.synchronize(dev)
+                ev = (time.perf_counter() - t0) / 10
+                m.dynamics.net.reset_state()
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                y = m(xb, t_fut)
+                torch.cuda.synchronize(dev)
+                wall = time.perf_counter() - t0
+        finally:
+            D.set_wide_resident_dopri5(prev)
+        s = D.dopri5_solve.last
+        return {"value": B / wall, "ms_per_batch": wall * 1e3, "attempts": s.n_attempts, "nfev": s.nfev,
+                "field_eval_ms": ev * 1e3, "eval_share": s.nfev * ev / wall, "finite": bool(torch.isfinite(y).all())}, y
+
+    res, yr = run(batch, True)
+    host, yh = run(batch, False)
+    out = {"value": res["value"], "unit": "forecast windows/s forward, dopri5 (96->96, 1 GPU)", **res,
+           "rtol": rtol, "atol": atol,
+           "workload": f"LatentNeuralODEForecaster(7 features, 96->96, latent 64, KANFET[64,128,64] K=10), dopri5 "
+                       f"rtol {rtol:g} atol {atol:g}, batch {batch}, synthetic series",
+           "path": "fetode_wide_dopri5: the whole solve in one launch (persistent grid over the wide-layer tiles)",
+           "host_loop": {**host, "same_solution": bool(torch.equal(yr, yh)),
+                         "path": "dopri5 host loop: 2 fetode_wide_layer_forward per evaluation, a read-back per attempt"}}
+    if small:
+        rs, ys = run(small, True)
+        hs, yhs = run(small, False)
+        out[f"b{small}"] = {"resident": rs, "host_loop": hs, "same_solution": bool(torch.equal(ys, yhs)),
+                            "speedup": hs["ms_per_batch"] / rs["ms_per_batch"]}
+    return out
 
 
 def ett_encoder_rate(dev, batch=8192, ctx=96, reps=20, with_cpu=True, cpu_seconds=5.0):
