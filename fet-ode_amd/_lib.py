@@ -302,3 +302,17 @@ class FieldHandle:
         if s is None:
             s = self._supported = bool(lib.fetode_fused_supported(self.ref))
         return s
+
+
+_CACHE_PREFIXES = ("_fetode", "_t_eval", "_rhs")
+
+
+class CacheFreeState:
+    """Module mixin: copy.deepcopy / pickle leave out the HIP caches kept in the instance __dict__
+    (ctypes descriptors holding raw pointers, packed plans, pinned state views, closures over the
+    module).  They describe THIS instance's tensors — a copy must not inherit them — and are
+    rebuilt on the copy's first call."""
+
+    def __getstate__(self):
+        st = super().__getstate__()
+        return {k: v for k, v in st.items() if not k.startswith(_CACHE_PREFIXES)}

@@ -31,6 +31,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
+from ._lib import CacheFreeState
 from .ferro_class import FerroelectricBasis
 from .odeint import odeint
 
@@ -107,7 +108,7 @@ def _mixer_apply(basis: "LogisticBasis", x, act_sigmoid: bool, w=None, b=None):
     return _HMixerFn.apply(basis, x, act_sigmoid, training, w, b, *params)
 
 
-class LogisticBasis(nn.Module):
+class LogisticBasis(CacheFreeState, nn.Module):
     """Hysteretic logistic basis, train_ecg_kan_fet_nn_ode.py:54-133."""
 
     def __init__(self, in_dim: int, num_basis: int, gate_slope: float = 5.0, init_prev: float = 0.0,
@@ -162,7 +163,7 @@ class LogisticBasis(nn.Module):
         return _mixer_apply(self, x, False).view(x.shape[0], self.in_dim, self.num_basis)
 
 
-class KANFeatureMixer(nn.Module):
+class KANFeatureMixer(CacheFreeState, nn.Module):
     """:408-421 — act(LogisticBasis(x)) as (B, dim*num_basis); act = Sigmoid runs in the kernel."""
 
     def __init__(self, dim, num_basis, act=nn.Sigmoid()):
@@ -178,7 +179,7 @@ class KANFeatureMixer(nn.Module):
         return phi.reshape(x.size(0), -1)
 
 
-class No_MLP_KANODEFunc(nn.Module):
+class No_MLP_KANODEFunc(CacheFreeState, nn.Module):
     """:483-509 — dh/dt = Linear(KANFeatureMixer(h)); mixer + head in one launch."""
 
     def __init__(self, latent_dim=64, num_basis=10, hidden=128):
@@ -200,7 +201,7 @@ class No_MLP_KANODEFunc(nn.Module):
         return dh
 
 
-class KanFet_NODE(nn.Module):
+class KanFet_NODE(CacheFreeState, nn.Module):
     """:512-572 — encode (B, T) to h0, integrate on [0, 1] with dopri5, decode h(1) -> logits."""
 
     def __init__(self, T: int, num_classes: int, latent_dim: int = 64, num_basis: int = 10,
@@ -324,7 +325,7 @@ def _grad_on(x):
     return torch.is_grad_enabled() and x.requires_grad
 
 
-class KANFetODEFunc(nn.Module):
+class KANFetODEFunc(CacheFreeState, nn.Module):
     """train_ecg.py:986-1013 (compare_noise_ecg.py:1561-1588): the FerroElectricNet ODE field.
     fc1 / fc2 are the drop-in FerroelectricBasis (same RNG order, buffers and state rules)."""
 
@@ -346,7 +347,7 @@ class KANFetODEFunc(nn.Module):
         return _NanClampFn.apply(dh, _grad_on(dh))
 
 
-class KanFet_MLP_NODE(nn.Module):
+class KanFet_MLP_NODE(CacheFreeState, nn.Module):
     """train_ecg.py:1017-1059, as the reference runs it: every row is solved on its own with batch
     1 (the Ferro state carries from row to row) and the classifier of the LAST row's h(1) is
     returned, shape (1, num_classes)."""

@@ -19,11 +19,12 @@ import torch
 import torch.nn as nn
 
 from . import _lib
+from ._lib import CacheFreeState
 from .autograd_ops import field_apply, kanlinear_apply
 from .ferro_class import FerroelectricBasis
 
 
-class LogisticBasis(nn.Module):
+class LogisticBasis(CacheFreeState, nn.Module):
     """efficientkan.py:7-24: phi = 2/(1+exp(-a(x-b))), (B,in) -> (B,in,nb)."""
 
     def __init__(self, in_dim: int, num_basis: int):
@@ -49,7 +50,7 @@ def _b_splines_torch(x, grid, spline_order):
     return bases.contiguous()
 
 
-class KANLinear(nn.Module):
+class KANLinear(CacheFreeState, nn.Module):
     def __init__(self, in_features, out_features, grid_size=5, spline_order=3, scale_noise=0.1,
                  scale_base=1.0, scale_spline=1.0, enable_standalone_scale_spline=True,
                  base_activation=nn.SiLU, grid_eps=0.02, grid_range=[-1, 1],
@@ -207,7 +208,7 @@ class KANLinear(nn.Module):
         return reg
 
 
-class _FieldMixin:
+class _FieldMixin(CacheFreeState):
     """Shared by KAN and KANFET: the whole stack as one fetode field."""
 
     def as_ode_func(self):
@@ -245,7 +246,7 @@ class KAN(_FieldMixin, nn.Module):
                    for layer in self.layers)
 
 
-class KANFETLayer(nn.Module):
+class KANFETLayer(CacheFreeState, nn.Module):
     """One KAN-FET layer: KANLinear(x) + FerroelectricBasis(x)."""
 
     def __init__(self, in_features, out_features, grid_size=5, spline_order=3, num_fet_basis=10,
@@ -293,7 +294,7 @@ class KANFET(_FieldMixin, nn.Module):
         return sum(l.kan.regularization_loss(regularize_activation, regularize_entropy) for l in self.layers)
 
 
-class ODEFunc(nn.Module):
+class ODEFunc(CacheFreeState, nn.Module):
     """``func(t, y) = field(y)`` (the reference's calDeriv, train_kanfet_node_predprey.py:159-161),
     tagged so that ``fet_ode_amd.odeint`` integrates it in one fused launch."""
 

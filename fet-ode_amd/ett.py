@@ -22,6 +22,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
+from ._lib import CacheFreeState
 from .efficientkan import KANFET
 from .odeint import Schedule, _per_stage_fixed, _try_fused
 
@@ -96,7 +97,7 @@ class EnergyWindowDataset:
         return xw.contiguous(), yw.contiguous()
 
 
-class KANFETDynamics(nn.Module):
+class KANFETDynamics(CacheFreeState, nn.Module):
     """Latent vector field f(t, z) = KANFET([latent, hidden, latent])(z) (autonomous; t ignored),
     the KAN-FET field of BASELINE config 4 in the place of ODEDynamics (train_kan_fet_ett.py:136-152).
     Tagged so that the integrators take the HIP fused path whenever the shape has one."""
@@ -113,7 +114,7 @@ class KANFETDynamics(nn.Module):
         return self.net(z)
 
 
-class LatentNeuralODEForecaster(nn.Module):
+class LatentNeuralODEForecaster(CacheFreeState, nn.Module):
     """train_kan_fet_ett.py:155-197 with the KAN-FET latent field.  Same constructor arguments and
     encoder / decoder state_dict keys (encoder.1, encoder.3, decoder.0, decoder.2); ``solver`` picks
     the latent integrator: 'dopri5' (the reference's forward, :192, torchdiffeq defaults) or 'rk4'
@@ -188,7 +189,7 @@ class _LogisticBasisFn(torch.autograd.Function):
         return gx, ga, gb
 
 
-class LogisticBasis(nn.Module):
+class LogisticBasis(CacheFreeState, nn.Module):
     """train_kan_fet_ett.py:741-749: phi = 2 / (1 + exp(-a (x - b))), x (B, in) -> (B, in, nb)."""
 
     def __init__(self, in_dim, num_basis):
@@ -203,7 +204,7 @@ class LogisticBasis(nn.Module):
         return _LogisticBasisFn.apply(x, self.a, self.b)
 
 
-class LogisticBasisLinear(nn.Module):
+class LogisticBasisLinear(CacheFreeState, nn.Module):
     """train_kan_fet_ett.py:753-776: logistic basis expansion, then phi @ weight + bias (the
     contraction is a plain library GEMM through torch)."""
 
@@ -312,7 +313,7 @@ def kanrnn_apply(cell, x, h0=None, lin=None):
     return _KANRNNFn.apply(cell, lin, x, h0, *params, w, bias)
 
 
-class FullyNonlinearKANCell(nn.Module):
+class FullyNonlinearKANCell(CacheFreeState, nn.Module):
     """train_kan_fet_ett.py:780-795: h = sigmoid(cat(phi_x(x_t), phi_h(h_prev)))[:, :hidden_size]."""
 
     def __init__(self, input_size, hidden_size, num_basis):
@@ -330,7 +331,7 @@ class FullyNonlinearKANCell(nn.Module):
         return kanrnn_apply(self, x_t.unsqueeze(1), h_prev)
 
 
-class KANRNNEncoder(nn.Module):
+class KANRNNEncoder(CacheFreeState, nn.Module):
     """train_kan_fet_ett.py:798-818: the cell over the context from h = 0, then to_latent(h_T).
     The whole recurrence + projection is one launch."""
 

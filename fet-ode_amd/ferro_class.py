@@ -16,10 +16,11 @@ import torch
 import torch.nn as nn
 
 from . import _lib
+from ._lib import CacheFreeState
 from .autograd_ops import ferro_apply
 
 
-class FerroelectricBasis(nn.Module):
+class FerroelectricBasis(CacheFreeState, nn.Module):
     """P = Ps*tanh(k*(E + Ec*m)) + bias, m from the hysteresis direction/crossing gates."""
 
     def __init__(self, in_dim, out_dim, num_basis, use_noise=False, gate_slope=10.0, alpha=0.8,

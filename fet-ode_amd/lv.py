@@ -24,6 +24,8 @@ import numpy as np
 import torch
 import torch.nn as nn
 
+from ._lib import CacheFreeState
+
 from .efficientkan import autonomous
 from .odeint import fused_field as fused_field_of
 from .odeint import odeint
@@ -60,7 +62,7 @@ def lv_problem(device="cuda", tf=14.0, tf_learn=3.5, n_train=35, x0=1.0, y0=1.0,
                      soln_arr=torch.Tensor(soln).to(device), n_train=n_train)
 
 
-class ResidualBottleneckMLPHead(nn.Module):
+class ResidualBottleneckMLPHead(CacheFreeState, nn.Module):
     """train_kanfet_mlp_node_predprey.py:192-203."""
 
     def __init__(self, d_out: int, bottleneck: int = 32, dropout: float = 0.0):
@@ -72,7 +74,7 @@ class ResidualBottleneckMLPHead(nn.Module):
         return y + self.net(y)
 
 
-class KANFET_ODE_WithHead(nn.Module):
+class KANFET_ODE_WithHead(CacheFreeState, nn.Module):
     """train_kanfet_mlp_node_predprey.py:206-220: dz/dt = kanfet(z); the head maps the predicted
     trajectory afterwards (not inside the ODE)."""
 

@@ -20,6 +20,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
+from ._lib import CacheFreeState
 from .autograd_ops import kan_backward, kan_params, kanlinear_apply
 
 
@@ -27,7 +28,7 @@ def _stream(x):
     return _lib.stream_handle(x.device)
 
 
-class LogisticBasis(nn.Module):
+class LogisticBasis(CacheFreeState, nn.Module):
     """mnist_kuramoto_kan.py:11-22 (used inside KANLinear's HIP kernel; standalone calls are the
     reference formula on the device)."""
 
@@ -45,7 +46,7 @@ class LogisticBasis(nn.Module):
         return 2.0 / (1.0 + torch.exp(-self.a * (x - self.b)))
 
 
-class KANLinear(nn.Module):
+class KANLinear(CacheFreeState, nn.Module):
     """mnist_kuramoto_kan.py:25-142."""
 
     def __init__(self, in_features, out_features, grid_size=5, spline_order=3, scale_noise=0.1, scale_base=1.0,
@@ -239,7 +240,7 @@ class _KuramotoFn(torch.autograd.Function):
         return gx, (gK.reshape(()) if gK is not None else None), gom, None, None, None
 
 
-class Kuramoto2D(nn.Module):
+class Kuramoto2D(CacheFreeState, nn.Module):
     """mnist_kuramoto_kan.py:145-199."""
 
     def __init__(self, H=28, W=28, steps=10, dt=0.15, learn_K=True, learn_omega=True):
@@ -272,7 +273,7 @@ class Kuramoto2D(nn.Module):
         return _KuramotoFn.apply(x_img, K, self.omega, self.steps, self.dt, training)
 
 
-class KuramotoKANClassifier(nn.Module):
+class KuramotoKANClassifier(CacheFreeState, nn.Module):
     """mnist_kuramoto_kan.py:202-221."""
 
     def __init__(self, H=28, W=28, num_classes=10, kuramoto_steps=10, num_basis=8):
