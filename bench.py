@@ -152,6 +152,22 @@ def pmc_traffic_per_launch():
     return d.get("hbm_bytes_per_launch"), os.path.relpath(files[-1], REPO)
 
 
+def pmc_issue(kernel_key):
+    """VALU-/LDS-busy fractions of a kernel from the newest committed issue summary
+    (tools/pmc_issue.py over a rocprofv3 PMC pass: SQ_ACTIVE_INST_VALU / SQ_ACTIVE_INST_LDS against
+    GRBM_GUI_ACTIVE; the issue model 2 quad-cycles per transcendental, 1 per other VALU instruction
+    reproduces SQ_ACTIVE_INST_VALU)."""
+    files = sorted(f for f in glob.glob(os.path.join(REPO, "profiles", "*pmc_issue.json")) if "raw" not in f)
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    v = d.get(kernel_key)
+    if v is None:
+        return None
+    return {"valu_busy_frac": v["valu_busy_frac"], "lds_busy_frac": v["lds_busy_frac"],
+            "valu_insts_per_wave": v["valu_insts_per_wave"], "source": os.path.relpath(files[-1], REPO)}
+
+
 def train_rate(model, y0d, t, iters, warmup, world, strong=True):
     """One training iteration = forward rk4 solve with autograd (one launch that also records the
     layer inputs of every evaluation) + backward (one reverse-sweep launch + fixed-order gradient
@@ -830,7 +846,10 @@ def main():
                          "traffic_source": traffic_src,
                          "valu": {"achieved_tflops": tflops, "peak_tflops": FP32_PEAK_TFLOPS,
                                   "frac": tflops / FP32_PEAK_TFLOPS,
-                                  "alg_flops_per_launch": flops_launch}},
+                                  "alg_flops_per_launch": flops_launch},
+                         # the kernel's actual bound: the SIMDs' VALU issue (PMC, committed profile)
+                         "issue": pmc_issue("fused4_kernel<10, 10, 10, 12, true, true, false>" if Bl > 512
+                                            else "small6_kernel<true, true>")},
         }
         if world == 1:
             # strong-scaling proxy on one GPU: the per-GPU block of an 8-GPU strong-scaled job
