@@ -10,7 +10,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import fet_ode_amd as F  # noqa: E402
-from fet_ode_amd import ett  # noqa: E402
+from fet_ode_amd import dopri5, ett  # noqa: E402,F401
 
 dev = torch.device("cuda:0")
 B = int(os.environ.get("B", 256))
@@ -34,19 +34,29 @@ with torch.no_grad():
         m.dynamics(0.0, z0)
     torch.cuda.synchronize()
     ev = (time.perf_counter() - t0) / 20
-    m.dynamics.net.reset_state() if hasattr(m.dynamics.net, "reset_state") else None
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    try:
-        y = m(xb, t_fut)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    modes = [int(v) for v in os.environ.get("MODES", "1,0").split(",")]   # 1: resident (fetode_wide_dopri5), 0: host loop
+    ys = {}
+    for resident in modes:
+        F.dopri5.set_wide_resident_dopri5(bool(resident))
+        m.load_state_dict(sd)
+        m.dynamics.net.reset_state()
         torch.cuda.synchronize()
-        ok = bool(torch.isfinite(y).all())
-        err = ""
-    except AssertionError as e:
-        ok, err = False, str(e)
-    wall = time.perf_counter() - t0
-s = F.dopri5.dopri5_solve.last
-n_att = len(s.attempts)
-print(f"B={B} P={P} rtol={rtol:g} atol={atol:g}: attempts {n_att} accepted {sum(1 for a in s.attempts if a[3])} "
-      f"nfev {s.nfev}, wall {wall:.3f} s, field eval {ev * 1e3:.3f} ms -> evals {s.nfev * ev:.3f} s, "
-      f"host/control share {(wall - s.nfev * ev) / wall:.3f}, finite {ok} {err}")
+        print(f"solving ({'resident' if resident else 'host loop'}) ...", flush=True)
+        t0 = time.perf_counter()
+        try:
+            y = m(xb, t_fut)
+            torch.cuda.synchronize()
+            ok = bool(torch.isfinite(y).all())
+            err = ""
+            ys[resident] = y
+        except AssertionError as e:
+            ok, err = False, str(e)
+        wall = time.perf_counter() - t0
+        s = F.dopri5.dopri5_solve.last
+        n_att = s.n_attempts
+        print(f"B={B} P={P} rtol={rtol:g} atol={atol:g} {'resident' if resident else 'host loop'}: attempts {n_att} "
+              f"nfev {s.nfev}, wall {wall:.3f} s, field eval {ev * 1e3:.3f} ms -> evals {s.nfev * ev:.3f} s, "
+              f"{s.nfev / wall:.0f} evals/s, finite {ok} {err}", flush=True)
+    if len(ys) == 2:
+        print("same prediction:", bool(torch.equal(ys[0], ys[1])), flush=True)
