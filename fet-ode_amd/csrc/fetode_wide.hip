@@ -64,6 +64,7 @@ struct WideLayout {
   int64_t knots;   // (in, 12) knot grid (efficientkan.py:55-61 buffer)
   int64_t rh;      // (in, 11) 1 / (g[m+1] - g[m])
   int64_t bt;      // (in, 12, 8) float4: basis c on knot interval m as a cubic in u (m = 11: zero)
+  int64_t par;     // (in, 48): knots (12) | 1 / spans (11) | 0 | logistic (-a log2e, a b log2e) (20) | 0 x 4
   int64_t end;
   float gsl2e, gs, wc;
 };
@@ -91,6 +92,7 @@ WideLayout wide_layout(const fetode_kanlinear_t* kl, const fetode_ferro_t* fl) {
     L.rh = o; o += (int64_t)L.in * (kNG - 1);
     o = (o + 3) & ~int64_t(3);
     L.bt = o; o += (int64_t)L.in * kNG * kNS * 4;
+    L.par = o; o += (int64_t)L.in * 48;
   }
   L.end = (o + 3) & ~int64_t(3);
   L.gs = fl ? (float)fl->gate_slope : 0.f;
@@ -175,6 +177,19 @@ __global__ void wide_pack_kernel(fetode_kanlinear_t kl, fetode_ferro_t fl, WideL
     const float a = kl.logistic_a[t], b = kl.logistic_b[t];
     plan[L.lg + 2 * t + 0] = -a * l2;
     plan[L.lg + 2 * t + 1] = (a * b) * l2;
+  }
+  if (L.kan && t < (int64_t)in * 48) {  // the per-input block the layer tile stages per chunk
+    const int i = (int)(t / 48), q = (int)(t % 48);
+    const float* g = kl.grid + (int64_t)i * kNG;
+    float v = 0.f;
+    if (q < kNG) v = g[q];
+    else if (q < 2 * kNG - 1) v = 1.0f / (g[q - kNG + 1] - g[q - kNG]);
+    else if (q >= 24 && q < 24 + 2 * kNB) {
+      const int j = (q - 24) >> 1;
+      const float a = kl.logistic_a[(int64_t)i * kNB + j], b = kl.logistic_b[(int64_t)i * kNB + j];
+      v = (q & 1) ? (a * b) * l2 : -a * l2;
+    }
+    plan[L.par + t] = v;
   }
   if (L.kan && t < (int64_t)in * kNG) {
     const int i = (int)(t / kNG), j = (int)(t % kNG);
@@ -308,6 +323,12 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
   static_assert(!FERRO || K % 2 == 0, "Ferro elements in (k, k+1) pairs");
   __shared__ float s_x[kCh * kRows], s_w[kCh * kRows], s_e[kCh * kRows];
   __shared__ float s_dfl[kOuts * kCh];
+  // the chunk's per-input KAN parameters (knots | 1 / spans | logistic (-a log2e, a b log2e)), staged
+  // one chunk ahead and double-buffered by chunk parity: the staging items read them from LDS instead
+  // of a dependent L2 round trip per item before the basis-table gather (the KANLinear part of the
+  // layer 98 -> 52 us with the loads taken away entirely)
+  constexpr int kPar = 48, kPK = 0, kPR = 12, kPL = 24;
+  __shared__ __attribute__((aligned(16))) float s_par[KAN ? 2 : 1][KAN ? kCh * kPar : 1];
   // KAN features of the chunk (MFMA A operand); the epilogue reuses the space for the Ferro sums
   // and the second K-half of the MFMA tile
   constexpr int kPhi = KAN ? kRows * kPitch : 0, kFer = 2 * kRows * (kOuts + 1);
@@ -352,6 +373,17 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
   };
   float xn = slive ? ldx(sb * in + ibeg + si) : 0.f;
   float pn = (FERRO && slive && !a.reinit) ? ldp(sb * in + ibeg + si) : 0.f;
+  // thread t < kCh * kPar loads word t of a chunk's parameter block (issued at the chunk's start,
+  // written to LDS just before its staging barrier: the load's latency hides under the staging)
+  const bool pld = KAN && tid < kCh * kPar;
+  auto ld_par = [&](int i0c) -> float {   // the plan's per-input blocks are contiguous: word tid of the chunk
+    return (pld && i0c < iend) ? plan[L.par + (int64_t)i0c * kPar + tid] : 0.f;
+  };
+  if constexpr (KAN) {
+    const float p0 = ld_par(ibeg);
+    if (pld) s_par[0][tid] = p0;  // read after the first chunk's barrier
+  }
+  int pbuf = 0;
   for (int i0 = ibeg; i0 < iend; i0 += kCh) {
     const float x = xn, pvl = pn;
     if (i0 + kCh < iend) {
@@ -359,6 +391,10 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
       pn = (FERRO && slive && !a.reinit) ? ldp(sb * in + i0 + kCh + si) : 0.f;
     }
     __syncthreads();  // the previous chunk is consumed
+    // chunk i0 + kCh's parameters: loaded now, stored into the other buffer before the staging
+    // barrier, read after the next chunk's barrier
+    float parn = 0.f;
+    if constexpr (KAN) parn = ld_par(i0 + kCh);
     if constexpr (FERRO) {
       const float pv = a.reinit ? x : pvl;
       if (stager) {
@@ -372,32 +408,45 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
     }
     if (KAN && stager) {
       const int i = i0 + si;
-      float f[kWF];
+      float f[1 + kNS];
       f[0] = x * rcp(1.0f + ex2(-x * l2));  // SiLU (efficientkan.py:166)
       // cubic B-spline bases (efficientkan.py:117-131): knot interval m by the half-open order-0
       // indicator, then the 8 bases as cubics of u from the fp64-fitted table (zero outside the grid)
-      const float* g = plan + L.knots + (int64_t)i * kNG;
+      const float* P = &s_par[KAN ? pbuf : 0][si * kPar];
+      const float* g = P + kPK;
       int m = -1;
 #pragma unroll
       for (int j = 0; j < kNG; ++j) m += (x >= g[j]) ? 1 : 0;
       const bool fin = __builtin_isfinite(x);
       const int mi = ((unsigned)m < (unsigned)(kNG - 1) && fin) ? m : kNG - 1;
-      const float u = mi < kNG - 1 ? (x - g[mi]) * plan[L.rh + (int64_t)i * (kNG - 1) + mi] : 0.f;
+      const float u = mi < kNG - 1 ? (x - g[mi]) * P[kPR + mi] : 0.f;
       const float4* bt = reinterpret_cast<const float4*>(plan + L.bt) + ((int64_t)i * kNG + mi) * kNS;
 #pragma unroll
       for (int c = 0; c < kNS; ++c) {
         const float4 cf = bt[c];
         f[1 + c] = fin ? ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x) : __builtin_nanf("");
       }
-      const float* lg = plan + L.lg + (int64_t)i * kNB * 2;
-#pragma unroll
-      for (int j = 0; j < kNB; ++j) f[1 + kNS + j] = rcp(1.0f + ex2(ffma(lg[2 * j], x, lg[2 * j + 1])));
-      f[kWF - 1] = 0.f;
       float* d = &s_phi[sr * kPitch + si * kWF];
 #pragma unroll
-      for (int q = 0; q < kWF; q += 2) *reinterpret_cast<float2*>(d + q) = make_float2(f[q], f[q + 1]);
+      for (int q = 0; q < kNS; q += 2) *reinterpret_cast<float2*>(d + q) = make_float2(f[q], f[q + 1]);
+      // the logistic bases straight into the row, their parameters from LDS a pair at a time (few live
+      // VGPRs: the whole block hoisted at once spilled the fused layer)
+      const float4* lg = reinterpret_cast<const float4*>(P + kPL);
+      float prev = f[kNS];  // B_7 pairs with phi_0: the row is written as aligned float2s
+#pragma unroll 1
+      for (int j = 0; j < kNB; j += 2) {
+        const float4 ab = lg[j / 2];  // (-a log2e, a b log2e) of bases j, j + 1
+        const float p0 = rcp(1.0f + ex2(ffma(ab.x, x, ab.y))), p1 = rcp(1.0f + ex2(ffma(ab.z, x, ab.w)));
+        *reinterpret_cast<float2*>(d + kNS + j) = make_float2(prev, p0);
+        prev = p1;
+      }
+      *reinterpret_cast<float2*>(d + kNS + kNB) = make_float2(prev, 0.f);
+    }
+    if constexpr (KAN) {
+      if (pld) s_par[pbuf ^ 1][tid] = parn;
     }
     __syncthreads();
+    if constexpr (KAN) pbuf ^= 1;
     // KAN weights of this wave's chunk inputs (ii = 2 q + kh) for the MFMA B operand (L2-resident;
     // issued here so their latency hides under the Ferro work, and not live across the staging)
     float wb[KAN ? kCh / 2 * 5 : 1];
@@ -419,16 +468,16 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
           // the element constants are wave-uniform: scalar loads (s_load, SGPR operands) — through
           // LDS they cost a ds_read_b128 per element (Ferro alone 270 -> 230 us at 64 -> 128)
           // (read through the constant address space: the plan is never written during a launch, so the
-          // loads stay scalar even where stores precede them in a loop — the resident solver's tile loop)
+          // loads stay scalar whatever precedes them — the resident solver's tile loop, the chunk
+          // loop's vector loads of the staged parameters)
           const float4* par = reinterpret_cast<const float4*>(plan + L.fe4) + ((int64_t)(o0 + jo) * in + i) * K;
           auto pk = [&](int k) -> float4 {
 #if defined(__HIP_DEVICE_COMPILE__)
-            if constexpr (RES) {
-              const kconst_f4* pc = (const kconst_f4*)(uintptr_t)(par + k);
-              return make_float4(pc->x, pc->y, pc->z, pc->w);
-            }
-#endif
+            const kconst_f4* pc = (const kconst_f4*)(uintptr_t)(par + k);
+            return make_float4(pc->x, pc->y, pc->z, pc->w);
+#else
             return par[k];
+#endif
           };
           float acc = 0.f;
           if (s_dfl[jo * kCh + ii] == 0.f) {  // wave-uniform
