@@ -458,7 +458,8 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
           wb[q * 5 + s] = plan[L.wp + ((int64_t)(i0 + 2 * q + kh) * kWF + 4 * s + kq) * out + o0 + kr];
     }
     if constexpr (FERRO) {
-#pragma unroll 2
+      constexpr int kIU = K <= 10 ? 2 : 1;  // two inputs in flight at K = 10; K = 12 would spill
+#pragma unroll kIU
       for (int ii = 0; ii < kCh; ++ii) {
         const int i = i0 + ii;
         const float xv = s_x[ii * kRows + lane], wg = s_w[ii * kRows + lane], e = s_e[ii * kRows + lane];
