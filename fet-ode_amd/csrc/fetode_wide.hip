@@ -64,7 +64,8 @@ struct WideLayout {
   int64_t knots;   // (in, 12) knot grid (efficientkan.py:55-61 buffer)
   int64_t rh;      // (in, 11) 1 / (g[m+1] - g[m])
   int64_t bt;      // (in, 12, 8) float4: basis c on knot interval m as a cubic in u (m = 11: zero)
-  int64_t par;     // (in, 48): knots (12) | 1 / spans (11) | 0 | logistic (-a log2e, a b log2e) (20) | 0 x 4
+  int64_t par;     // (in, 64): knots (12) | 1 / (g[j+1] - g[j]) (11) | 0 | logistic (-a log2e, a b log2e) (20)
+                   //           | 1 / (g[j+2] - g[j]) (10) | 1 / (g[j+3] - g[j]) (9) | 0
   int64_t end;
   float gsl2e, gs, wc;
 };
@@ -92,7 +93,7 @@ WideLayout wide_layout(const fetode_kanlinear_t* kl, const fetode_ferro_t* fl) {
     L.rh = o; o += (int64_t)L.in * (kNG - 1);
     o = (o + 3) & ~int64_t(3);
     L.bt = o; o += (int64_t)L.in * kNG * kNS * 4;
-    L.par = o; o += (int64_t)L.in * 48;
+    L.par = o; o += (int64_t)L.in * 64;
   }
   L.end = (o + 3) & ~int64_t(3);
   L.gs = fl ? (float)fl->gate_slope : 0.f;
@@ -178,8 +179,8 @@ __global__ void wide_pack_kernel(fetode_kanlinear_t kl, fetode_ferro_t fl, WideL
     plan[L.lg + 2 * t + 0] = -a * l2;
     plan[L.lg + 2 * t + 1] = (a * b) * l2;
   }
-  if (L.kan && t < (int64_t)in * 48) {  // the per-input block the layer tile stages per chunk
-    const int i = (int)(t / 48), q = (int)(t % 48);
+  if (L.kan && t < (int64_t)in * 64) {  // the per-input block the layer tile stages per chunk
+    const int i = (int)(t / 64), q = (int)(t % 64);
     const float* g = kl.grid + (int64_t)i * kNG;
     float v = 0.f;
     if (q < kNG) v = g[q];
@@ -188,6 +189,10 @@ __global__ void wide_pack_kernel(fetode_kanlinear_t kl, fetode_ferro_t fl, WideL
       const int j = (q - 24) >> 1;
       const float a = kl.logistic_a[(int64_t)i * kNB + j], b = kl.logistic_b[(int64_t)i * kNB + j];
       v = (q & 1) ? (a * b) * l2 : -a * l2;
+    } else if (q >= 44 && q < 54) {
+      v = 1.0f / (g[q - 44 + 2] - g[q - 44]);
+    } else if (q >= 54 && q < 63) {
+      v = 1.0f / (g[q - 54 + 3] - g[q - 54]);
     }
     plan[L.par + t] = v;
   }
@@ -327,7 +332,7 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
   // one chunk ahead and double-buffered by chunk parity: the staging items read them from LDS instead
   // of a dependent L2 round trip per item before the basis-table gather (the KANLinear part of the
   // layer 98 -> 52 us with the loads taken away entirely)
-  constexpr int kPar = 48, kPK = 0, kPR = 12, kPL = 24;
+  constexpr int kPar = 64, kPK = 0, kPR = 12, kPL = 24, kP2 = 44, kP3 = 54;
   __shared__ __attribute__((aligned(16))) float s_par[KAN ? 2 : 1][KAN ? kCh * kPar : 1];
   // KAN features of the chunk (MFMA A operand); the epilogue reuses the space for the Ferro sums
   // and the second K-half of the MFMA tile
@@ -407,32 +412,40 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
       if (tid < kOuts * kCh) s_dfl[tid] = plan[L.dflag + (int64_t)(o0 + tid / kCh) * in + i0 + tid % kCh];
     }
     if (KAN && stager) {
-      const int i = i0 + si;
-      float f[1 + kNS];
-      f[0] = x * rcp(1.0f + ex2(-x * l2));  // SiLU (efficientkan.py:166)
-      // cubic B-spline bases (efficientkan.py:117-131): knot interval m by the half-open order-0
-      // indicator, then the 8 bases as cubics of u from the fp64-fitted table (zero outside the grid)
+      const float sil = x * rcp(1.0f + ex2(-x * l2));  // SiLU (efficientkan.py:166)
+      // cubic B-spline bases (efficientkan.py:117-131): the knot interval m by the half-open order-0
+      // indicator, then the Cox-de Boor recursion restricted to the interval's triangle (the four
+      // bases B_{m-3..m} that can be non-zero) on the staged knots and reciprocal spans, all from LDS
+      // (no per-item gather of fitted tables: the layer's staging waited on those L2 round trips)
       const float* P = &s_par[KAN ? pbuf : 0][si * kPar];
       const float* g = P + kPK;
       int m = -1;
 #pragma unroll
       for (int j = 0; j < kNG; ++j) m += (x >= g[j]) ? 1 : 0;
       const bool fin = __builtin_isfinite(x);
-      const int mi = ((unsigned)m < (unsigned)(kNG - 1) && fin) ? m : kNG - 1;
-      const float u = mi < kNG - 1 ? (x - g[mi]) * P[kPR + mi] : 0.f;
-      const float4* bt = reinterpret_cast<const float4*>(plan + L.bt) + ((int64_t)i * kNG + mi) * kNS;
-#pragma unroll
-      for (int c = 0; c < kNS; ++c) {
-        const float4 cf = bt[c];
-        f[1 + c] = fin ? ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x) : __builtin_nanf("");
-      }
+      const bool ing = fin && (unsigned)m < (unsigned)(kNG - 1);  // inside the grid
+      const int mc = ing ? m : 0;
+      // knots / spans outside the grid only enter bases B_{<0} or B_{>7}, which are dropped (clamped reads)
+      auto G = [&](int j) { return g[j < 0 ? 0 : (j > kNG - 1 ? kNG - 1 : j)]; };
+      auto R = [&](int off, int j, int n) { return P[off + (j < 0 ? 0 : (j > n - 1 ? n - 1 : j))]; };
+      const float gm = G(mc), gm1 = G(mc + 1), gmm1 = G(mc - 1), gm2 = G(mc + 2), gmm2 = G(mc - 2), gm3 = G(mc + 3);
+      const float r1 = P[kPR + mc];
+      const float n10 = (gm1 - x) * r1, n11 = (x - gm) * r1;                        // B_{m-1,1}, B_{m,1}
+      const float t0 = n10 * R(kP2, mc - 1, 10), t1 = n11 * R(kP2, mc, 10);
+      const float n20 = (gm1 - x) * t0, n21 = (x - gmm1) * t0 + (gm2 - x) * t1, n22 = (x - gm) * t1;
+      const float s0 = n20 * R(kP3, mc - 2, 9), s1 = n21 * R(kP3, mc - 1, 9), s2 = n22 * R(kP3, mc, 9);
+      const float nb[4] = {(gm1 - x) * s0, (x - gmm2) * s0 + (gm2 - x) * s1, (x - gmm1) * s1 + (gm3 - x) * s2,
+                           (x - gm) * s2};                                                // B_{m-3..m, 3}
+      const float z = fin ? 0.f : __builtin_nanf("");  // non-finite x: NaN bases, as (x - g) / d * B
       float* d = &s_phi[sr * kPitch + si * kWF];
+      *reinterpret_cast<float2*>(d) = make_float2(sil, z);
 #pragma unroll
-      for (int q = 0; q < kNS; q += 2) *reinterpret_cast<float2*>(d + q) = make_float2(f[q], f[q + 1]);
+      for (int q = 2; q < kNS; q += 2) *reinterpret_cast<float2*>(d + q) = make_float2(z, z);
+      const float f8 = z;  // (B_7's slot is written with phi_0 below; the interval's bases land after)
       // the logistic bases straight into the row, their parameters from LDS a pair at a time (few live
       // VGPRs: the whole block hoisted at once spilled the fused layer)
       const float4* lg = reinterpret_cast<const float4*>(P + kPL);
-      float prev = f[kNS];  // B_7 pairs with phi_0: the row is written as aligned float2s
+      float prev = f8;  // B_7 pairs with phi_0: the row is written as aligned float2s
 #pragma unroll 1
       for (int j = 0; j < kNB; j += 2) {
         const float4 ab = lg[j / 2];  // (-a log2e, a b log2e) of bases j, j + 1
@@ -441,6 +454,13 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
         prev = p1;
       }
       *reinterpret_cast<float2*>(d + kNS + kNB) = make_float2(prev, 0.f);
+      if (ing) {  // the interval's bases over the zeros (same thread, in order)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = m - 3 + r;
+          if (c >= 0 && c < kNS) d[1 + c] = nb[r];
+        }
+      }
     }
     if constexpr (KAN) {
       if (pld) s_par[pbuf ^ 1][tid] = parn;
