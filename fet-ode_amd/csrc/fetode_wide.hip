@@ -270,9 +270,10 @@ struct WideArgs {
 // sums meet in a fixed order — slab 0 + slab 1 (+ slab 2 ..), left to right — in both the per-layer
 // launch (two slices: vector atomics into a zeroed out, 0 + a + b; more: slabs + wide_slab_sum_kernel)
 // and the resident solver (the consumer sums the slabs), so the two paths agree bit for bit.
+constexpr int kMaxSlices = 16;
 int wide_slices(int64_t wgs, int in) {
   int S = 1;
-  while (S < 8 && wgs * S <= 2 * 256 && (in / (2 * S)) % kChMax == 0 && in % (2 * S) == 0) S *= 2;
+  while (S < kMaxSlices && wgs * S <= 2 * 256 && (in / (2 * S)) % kChMax == 0 && in % (2 * S) == 0) S *= 2;
   return S;
 }
 

@@ -500,6 +500,10 @@ def _try_wide_resident(func, y0, tp, reversed_, rtol, atol, options):
         return None
     (k0, f0), (k1, f1) = layers
     B, D = y0.shape
+    if _WIDE_RESIDENT_GAP[0] < B < _WIDE_RESIDENT_GAP[1]:
+        # measured crossover: between these batches the per-layer launches beat the
+        # persistent grid's tiles plus its three grid barriers per evaluation
+        return None
     H = k0.out_features
     if D != k0.in_features or k1.in_features != H or k1.out_features != D or f0.num_basis != f1.num_basis:
         return None
@@ -562,12 +566,18 @@ def _try_wide_resident(func, y0, tp, reversed_, rtol, atol, options):
 
 _RESIDENT = True
 _WIDE_RESIDENT = os.environ.get("FETODE_WIDE_RESIDENT", "1") != "0"
+# batches strictly inside (lo, hi) take the host loop: resident / host measured at the ETT widths
+# (rtol 1e-3, 96 outputs): B = 256 1.49x, 512 1.14x, 1024 0.84x, 2048 0.88x, 4096 0.94x, 8192 1.02x
+_WIDE_RESIDENT_GAP = [512, 8192]
 
 
-def set_wide_resident_dopri5(enabled: bool) -> bool:
-    """Device-resident dopri5 for the wide KAN-FET fields (default) or the host-driven loop."""
+def set_wide_resident_dopri5(enabled: bool, gap=None) -> bool:
+    """Device-resident dopri5 for the wide KAN-FET fields (default) or the host-driven loop;
+    ``gap = (lo, hi)`` sets the batch range (exclusive) that takes the host loop anyway ((0, 0): none)."""
     global _WIDE_RESIDENT
     prev, _WIDE_RESIDENT = _WIDE_RESIDENT, bool(enabled)
+    if gap is not None:
+        _WIDE_RESIDENT_GAP[:] = [int(gap[0]), int(gap[1])]
     return prev
 
 

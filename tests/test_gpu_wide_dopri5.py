@@ -31,7 +31,7 @@ def _z0(B, dev, D=64, seed=3, scale=0.6):
 
 
 def _solve(dyn, z0, t, resident, **kw):
-    prev = F.dopri5.set_wide_resident_dopri5(resident)
+    prev = F.dopri5.set_wide_resident_dopri5(resident, gap=(0, 0))   # resident at every batch
     try:
         with torch.no_grad():
             sol = F.odeint(dyn, z0, t, method="dopri5", **kw)
@@ -43,7 +43,7 @@ def _solve(dyn, z0, t, resident, **kw):
         state = [f._prev.clone() for _, f in field_layers(dyn.net)]
         return sol, s.nfev, s.attempts, state
     finally:
-        F.dopri5.set_wide_resident_dopri5(prev)
+        F.dopri5.set_wide_resident_dopri5(prev, gap=(512, 8192))
 
 
 def _compare(host, res, what):
@@ -154,3 +154,15 @@ def test_forecaster_dopri5_forward_takes_resident_path(dev):
     assert isinstance(F.dopri5.dopri5_solve.last, ResidentSolve)
     assert yr.shape == yh.shape == (512, 8)
     assert (yr - yh).abs().max().item() <= 1e-5 * (yh.abs().max().item() + 1e-30)
+
+
+def test_wide_resident_dispatch_crossover(dev):
+    """Between the measured crossover batches (512, 8192) the per-layer launches are faster than
+    the persistent grid: the default dispatch takes the host loop there and the
+    resident solver on either side."""
+    t = torch.linspace(0.0, 0.5, steps=3, device=dev)
+    for B, resident in ((512, True), (1024, False)):
+        dyn = _dyn(dev)
+        with torch.no_grad():
+            F.odeint(dyn, _z0(B, dev), t, method="dopri5", rtol=1e-3, atol=1e-4)
+        assert isinstance(F.dopri5.dopri5_solve.last, ResidentSolve) == resident, B

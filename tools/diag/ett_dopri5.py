@@ -38,7 +38,7 @@ with torch.no_grad():
     modes = [int(v) for v in os.environ.get("MODES", "1,0").split(",")]   # 1: resident (fetode_wide_dopri5), 0: host loop
     ys = {}
     for resident in modes:
-        F.dopri5.set_wide_resident_dopri5(bool(resident))
+        F.dopri5.set_wide_resident_dopri5(bool(resident), gap=(0, 0))
         m.load_state_dict(sd)
         m.dynamics.net.reset_state()
         torch.cuda.synchronize()

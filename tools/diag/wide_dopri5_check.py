@@ -19,7 +19,7 @@ z0 = (torch.randn(B, 64, generator=g) * 0.6).to(dev)
 t = torch.linspace(0.0, 3.0, steps=4, device=dev)
 out = {}
 for resident in (False, True):
-    F.dopri5.set_wide_resident_dopri5(resident)
+    F.dopri5.set_wide_resident_dopri5(resident, gap=(0, 0))
     dyn.load_state_dict(sd)
     dyn.net.reset_state()
     with torch.no_grad():

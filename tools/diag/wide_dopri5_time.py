@@ -22,7 +22,7 @@ for B in [int(b) for b in os.environ.get("BS", "256,8192").split(",")]:
     t = torch.linspace(0.0, float(P - 1), steps=P, device=dev)
     res = {}
     for resident in (True, False):
-        F.dopri5.set_wide_resident_dopri5(resident)
+        F.dopri5.set_wide_resident_dopri5(resident, gap=(0, 0))
         times = []
         for rep in range(2):
             dyn.load_state_dict(sd)
