@@ -266,20 +266,22 @@ def lv_dopri5_rate(sd, y0d, t, reps=3):
             "path": "fetode_integrate_dopri5: fused4_kernel DOPRI instantiation, one launch"}
 
 
-def lv_dopri5_train_rate(sd, y0d, t, iters=3, rtol=1e-3, atol=1e-4):
+def lv_dopri5_train_rate(sd, y0d, t, iters=3, rtol=1e-3, atol=1e-4, resident=True, target=None):
     """The reference's training iteration on its default method: odeint(calDeriv, X0, t_learn) with
-    dopri5, then loss.backward() and Adam (train_kanfet_node_predprey.py:252-257), B = 4096.
-    torchdiffeq's direct backprop differentiates every stage of every attempt AND the step-size
-    control (d dt / d theta through the error ratios); here that is _Dopri5Grad:
-    the control flow on the host, each evaluation the per-stage HIP field kernels with their HIP
-    VJPs under autograd.  At the reference's rtol 1e-7 / atol 1e-9 one solve is ~5 800 attempts
-    (~35 k recorded evaluations), so this line runs rtol 1e-3 / atol 1e-4."""
+    dopri5, then loss.backward() and Adam (train_kanfet_node_predprey.py:252-257).  torchdiffeq's
+    direct backprop differentiates every stage of every attempt AND the step-size control (d dt /
+    d theta through the error ratios, the initial step, the output times).  resident: the taped
+    resident solve + one resident reverse sweep (fetode_integrate_dopri5_tape / _backward,
+    DESIGN.md §4.10); else _Dopri5Grad (host-driven attempts, per-stage HIP kernels + HIP VJPs
+    under autograd)."""
+    from fet_ode_amd.dopri5 import ResidentSolve, set_resident_dopri5_training
     m = F.KANFET([2, 10, 2], grid_size=5)
     m.load_state_dict(sd)
     m = m.to(y0d.device)
     func = F.autonomous(m)
     opt = torch.optim.Adam(m.parameters(), lr=1e-4)
-    target = torch.zeros(t.numel(), y0d.shape[0], 2, device=y0d.device)
+    if target is None:
+        target = torch.zeros(t.numel(), y0d.shape[0], 2, device=y0d.device)
 
     def it():
         opt.zero_grad()
@@ -289,20 +291,28 @@ def lv_dopri5_train_rate(sd, y0d, t, iters=3, rtol=1e-3, atol=1e-4):
         opt.step()
         return loss
 
-    it()
-    torch.cuda.synchronize(y0d.device)
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        loss = it()
-    torch.cuda.synchronize(y0d.device)
+    prev = set_resident_dopri5_training(resident)
+    try:
+        it()
+        torch.cuda.synchronize(y0d.device)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            loss = it()
+        torch.cuda.synchronize(y0d.device)
+    finally:
+        set_resident_dopri5_training(prev)
     el = (time.perf_counter() - t0) / iters
     s = F.dopri5.dopri5_solve.last
-    return {"value": 1.0 / el, "unit": f"dopri5 training iterations/s (B=4096, rtol {rtol:g}, atol {atol:g}, "
-                                       "t=linspace(0,3.5,35))",
+    B = y0d.shape[0]
+    return {"value": 1.0 / el, "unit": f"dopri5 training iterations/s (B={B}, rtol {rtol:g}, atol {atol:g}, "
+                                       f"t=linspace(0,3.5,{t.numel()}))",
             "ms_per_iter": el * 1e3, "attempts": s.n_attempts, "nfev": s.nfev,
             "finite": bool(torch.isfinite(loss).item()),
-            "path": "_Dopri5Grad: host-driven attempts, per-stage HIP field kernels + HIP VJPs under autograd "
-                    "(direct backprop incl. the step-size control)"}
+            "path": ("taped resident solve (fetode_integrate_dopri5_tape) + resident reverse sweep "
+                     "(fetode_integrate_dopri5_backward): 2 launches + the parameter-sum reduction"
+                     if isinstance(s, ResidentSolve) else
+                     "_Dopri5Grad: host-driven attempts, per-stage HIP field kernels + HIP VJPs under autograd "
+                     "(direct backprop incl. the step-size control)")}
 
 
 def lv_dopri5_sharded_rate(sd, y0d, t, world, B_global, reps=3):
@@ -866,7 +876,16 @@ def main():
             out["lv_plain_closure"] = plain_closure_rate(model, y0d, t)
         if world == 1 and not args.no_dopri5:
             out["lv_dopri5"] = lv_dopri5_rate(sd, y0d, t)
-            out["lv_dopri5"]["train"] = lv_dopri5_train_rate(sd, y0d, t)
+            tr = lv_dopri5_train_rate(sd, y0d, t)
+            tr["host_autograd"] = lv_dopri5_train_rate(sd, y0d, t, iters=1, resident=False)
+            tr["speedup_vs_host_autograd"] = tr["value"] / tr["host_autograd"]["value"]
+            # the reference's defaults (rtol 1e-7 / atol 1e-9): B = 4096, and its own iteration's
+            # shape, one trajectory from X0 = (1, 1) (train_kanfet_node_predprey.py:49,149,252-257;
+            # synthetic zero target)
+            tr["default_tol_b4096"] = lv_dopri5_train_rate(sd, y0d, t, iters=2, rtol=1e-7, atol=1e-9)
+            tr["reference_iteration"] = lv_dopri5_train_rate(
+                sd, torch.tensor([[1.0, 1.0]], device=y0d.device), t, iters=5, rtol=1e-7, atol=1e-9)
+            out["lv_dopri5"]["train"] = tr
         if dp5_sharded is not None:
             out["lv_dopri5"] = dp5_sharded
         if world == 1 and not args.no_ecg:

@@ -39,6 +39,8 @@ using namespace fetode;
 
 namespace {
 
+#include "fetode_gridsum.h"
+
 constexpr int kSO = 3;  // spline order of the fused kernels (efficientkan default)
 // FETODE_EXP_SKIP (phase-cost attribution: 1 Ferro, 2 edges, 4 logistic, 8 features, 16 d/dx
 // reductions compiled out — results are wrong when set) exists only in the diagnostic build
@@ -810,6 +812,521 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(ACC ?
   }
 }
 
+// =============================================================================================
+// The reverse sweep of the device-resident dopri5 solve: loss.backward() through the reference's
+// own training call, odeint(calDeriv, X0, t_learn) with torchdiffeq's default dopri5
+// (train_kanfet_node_predprey.py:252-257), i.e. reverse-mode autograd through every evaluation of
+// every attempt (rejected ones included), the stage sums, the error norm and the step-size
+// control (rk_common._runge_kutta_step / _optimal_step_size, misc._select_initial_step /
+// _rms_norm, interp._interp_fit / _interp_evaluate — nothing in torchdiffeq detaches dt).
+//
+// Tape (fetode_integrate_dopri5_tape): per evaluation its two layer inputs (as the fixed-grid
+// tape) and its output k; per attempt (t0, dt, error ratio, accepted); the initial-step scalars.
+// Evaluation order: 0 = f(y0), 1 = the initial-step probe (absent with first_step), then six per
+// attempt (stages 2..7; stage 7's input is the attempt's y1, its output the next f0).
+//
+// One wave owns TPW trajectories and walks the evaluations backwards exactly like
+// fixed_bwd_kernel (same per-evaluation VJP, gradient sums in VGPRs); the lanes sl < D of a
+// trajectory carry its state adjoints.  The adjoint of dt couples the batch (the error ratio is a
+// norm over every element), so every attempt ends with one grid-wide fixed-order fp64 sum
+// (grid_sum2) of the per-element d/d dt terms — the whole grid is resident.  Per attempt n, in
+// reverse, with dt_{n+1}'s adjoint known:
+//   control   dt_{n+1} = clamp(dt_n * min(ifactor, max(safety ratio^-1/5, dfactor)))
+//             -> adjoint of ratio_n and dt_n's direct part
+//   outputs   (accepted) every output t_i in (t0, t1]: the interpolant's coefficient adjoints and
+//             d out/d x, x = (t_i - t0s)/(t1s - t0s) -> d/d t0, d/d dt (grid sums)
+//   element   interp fit, error ratio (err / tol, tol = atol + rtol max(|y|, |y1|)) and the stage
+//             sums -> adjoints of k_1..k_7, y and dt; evaluations 7..2 by VJP
+//   carry     y's adjoint and f0's (= k_1's) to the attempt that produced them
+// After attempt 0: _select_initial_step's adjoint (one more grid sum, through the probe).
+// =============================================================================================
+struct DopriBwdArgs {
+  BwdArgs b;            // plan, layers, B, T, gsol, tape ((n_ev, B, 2 D + H): inputs, output), state0, ...
+  const double* att;    // (n_att, 4): t0, dt, error ratio, accepted
+  int32_t n_att, n_ev, base;  // base: evaluation index of attempt 0's stage 2 (1 with first_step, else 2)
+  const double* t;      // (T) output times, fp64
+  const double* init_rec;  // {d0, d1, d2, h0, h1}
+  float beta[6][6], cerr[7], cmid[7];
+  float rtol, atol;
+  double safety, ifactor, dfactor, min_step, max_step, n_el;
+  DopriParams gp;       // the grid-sum words and leaf layout (single device)
+  int32_t* status;      // 0, or 4 when a grid sum timed out
+};
+
+// a wave-uniform value computed on the VALU (or read from LDS) into SGPRs: it stays live across
+// the evaluations' VJPs without holding VGPRs
+__device__ __forceinline__ float unif(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(unsigned, v)));
+}
+__device__ __forceinline__ double uni(double v) {
+  const unsigned long long u = __double_as_longlong(v);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u), hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  return __longlong_as_double(((unsigned long long)hi << 32) | lo);
+}
+
+template <int D, int H, int K, int NB, int NG, bool FERRO, int TPW>
+__global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(FETODE_BWD_WAVES))) void dopri_bwd_kernel(DopriBwdArgs da) {
+  const BwdArgs& a = da.b;
+  using L0 = BL<D, H, K, NB, NG, FERRO>;
+  using L1 = BL<H, D, K, NB, NG, FERRO>;
+  constexpr int W = D + H, NS = NG - 1 - kSO, HALF = 64 / TPW;
+  constexpr int CB = L0::IN * L0::NTMP > L1::IN * L1::NTMP ? L0::IN * L0::NTMP : L1::IN * L1::NTMP;
+  constexpr bool PF = FERRO && 2 * W <= HALF;
+  constexpr int FH = PF ? HALF / 2 : HALF, NBUF = PF ? 2 : 1;
+  static_assert(W <= FH && (TPW == 1 || TPW == 2 || TPW == 4), "one lane per input of each trajectory and evaluation");
+  __shared__ BInTab<W, NG, NB> TI;
+  __shared__ BTab<L0> T0;
+  __shared__ BTab<L1> T1;
+  using FB = BFeat<W, NS, NB, PF>;
+  __shared__ FB sF[kTPB][NBUF][TPW];
+  __shared__ __attribute__((aligned(16))) float s_cb[kTPB][TPW][CB];
+  __shared__ float s_g1[kTPB][TPW][D], s_g0[kTPB][TPW][H], s_gx[kTPB][TPW][D];
+  __shared__ float s_k[kTPB][TPW][8][D], s_kb[kTPB][TPW][8][D];  // k_1..k_7 and their adjoints
+  __shared__ double s_red[kTPB][2], s_res[2];
+  __shared__ int s_ab;
+  // the element lanes' carried adjoints, kept in LDS across the VJPs (register pressure)
+  struct ElSt {
+    double pd, pt;          // this attempt's d/d dt and d/d t0 terms of the outputs (+ d/d dt32 at the end)
+    float yb0, yb1, dtb32;  // adjoints of the attempt's y, y1, dt32
+    float ybc, fbc;         // carried: adjoints of the current y and f0
+    float scb, f0bp;        // initial step: adjoint of scale, the probe's term of f0's adjoint
+  };
+  __shared__ ElSt s_el[kTPB][TPW][D];
+  // the tableau in LDS: kernel-argument reads with constant indices would be hoisted into ~50
+  // SGPRs for the whole loop (the VJP needs the SGPR file)
+  __shared__ float s_beta[6][6], s_cerr[8], s_cmid[8];
+  // the wave-uniform control scalars, per wave in LDS: they are touched once per attempt and would
+  // otherwise hold registers across every VJP (adjoints of the next dt and of t1s, ...)
+  struct WSc {
+    double dtbar, tbar, dtb_base, h0b, d0b, d1b;
+    float dt32, h0f;
+    int jj, acc;
+  };
+  __shared__ WSc s_sc[kTPB];
+  // the arguments the per-attempt code reads, in LDS: read from the kernel arguments inside the
+  // loop they would be hoisted into SGPRs (and spilled) for the whole sweep
+  struct RareArgs {
+    const double* att;
+    const double* t;
+    const float* gsol;
+    float* gy0;
+    const double* init_rec;
+    int64_t B;
+    int base, n_att;
+    float rtol, atol;
+    double n_el, safety, ifactor, dfactor, min_step, max_step;
+  };
+  __shared__ RareArgs s_ra;
+
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tt = lane / HALF, sl = lane % HALF;
+  const int fb = sl / FH, fsl = sl % FH;
+  TI.stage(a.plan, a.P0, a.P1, D, threadIdx.x, 64 * kTPB);
+  T0.stage(a.k0, a.f0, a.plan, a.P0, threadIdx.x, 64 * kTPB);
+  T1.stage(a.k1, a.f1, a.plan, a.P1, threadIdx.x, 64 * kTPB);
+  BReg<L0> R0;
+  BReg<L1> R1;
+  R0.zero();
+  R1.zero();
+  if (threadIdx.x == 0) {
+    s_ab = 0;
+    s_ra = RareArgs{da.att, da.t, a.gsol, a.gy0, da.init_rec, a.B, da.base, da.n_att, da.rtol, da.atol,
+                    da.n_el, da.safety, da.ifactor, da.dfactor, da.min_step, da.max_step};
+#pragma unroll
+    for (int q = 0; q < 36; ++q) s_beta[q / 6][q % 6] = da.beta[q / 6][q % 6];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      s_cerr[q] = da.cerr[q];
+      s_cmid[q] = da.cmid[q];
+    }
+  }
+  __syncthreads();
+
+  float* cbs = &s_cb[wid][0][0];
+  float* g1s = &s_g1[wid][0][0];
+  float* g0s = &s_g0[wid][0][0];
+  float* gxs = &s_gx[wid][0][0];
+  float(&kk)[8][D] = s_k[wid][tt];
+  float(&kb)[8][D] = s_kb[wid][tt];
+  const float gs0 = (float)a.f0.gate_slope, gs1 = (float)a.f1.gate_slope;
+  const float gl0 = a.P0.gsl2e, gl1 = a.P1.gsl2e, wc0 = a.P0.wc, wc1 = a.P1.wc;
+  const float glane = fsl < D ? gl0 : gl1, wlane = fsl < D ? wc0 : wc1, slane = fsl < D ? gs0 : gs1;
+  constexpr int TW = 2 * D + H;  // tape row: layer-0 input, layer-1 input, output k
+  const int64_t tstride = a.B * TW;
+  const int n_ev = da.n_ev;
+  const int64_t b0 = ((int64_t)blockIdx.x * kTPB + wid) * TPW;
+  const int64_t b = b0 + tt;
+  const bool live = b < a.B;
+  const bool el = live && sl < D;  // this lane carries element (b, sl)
+  // per-lane offsets in 32 bits, row bases uniform (scalar base + vector offset addressing)
+  const int bi = live ? (int)b : 0;
+  auto tape_at = [&](int ev) -> float {
+    if (fsl >= W || !live) return 0.f;
+    if (ev >= 0) return (a.tape + (int64_t)ev * tstride)[bi * TW + fsl];
+    const float v = a.tape[bi * TW + fsl];
+    if (fsl < D) return (a.init_mask & 1u) ? v : (FERRO ? a.state0[bi * D + fsl] : 0.f);
+    return (a.init_mask & 2u) ? v : (FERRO ? (a.state0 + a.B * D)[bi * H + (fsl - D)] : 0.f);
+  };
+  auto tx = [&](int ev) -> float { return (a.tape + (int64_t)ev * tstride)[bi * TW + sl]; };      // layer input (el lanes)
+  auto tk = [&](int ev) -> float { return (a.tape + (int64_t)ev * tstride)[bi * TW + W + sl]; };  // output (el lanes)
+  float cur = tape_at(n_ev - 1 - fb), prv = tape_at(n_ev - 2 - fb);
+
+  // the VJP of evaluation ev: g1s (d loss / d k) -> gxs (d loss / d layer-0 input); sums into R0, R1
+  auto vjp = [&](int ev) {
+    int z = 0;
+    asm volatile("" : "+s"(z));
+    const bool fstep = !PF || ((n_ev - 1 - ev) & 1) == 0;
+    float nx1 = 0.f, nx2 = 0.f;
+    FB& FF = sF[wid][PF ? (ev - fb) & 1 : 0][tt];
+    if (fstep) {
+      if constexpr (PF) {
+        nx1 = tape_at(ev - fb - 2);
+        nx2 = tape_at(ev - fb - 3);
+      } else {
+        nx1 = prv;
+        nx2 = tape_at(ev - 2);
+      }
+      if (fsl < W) {
+        FF.x[fsl] = cur;
+        FF.pv[fsl] = prv;
+      }
+    }
+    wsync();
+    if (fstep) {
+      if (fsl < W) feat_input<W, NG, NB, PF>(FF, TI, fsl, glane, wlane, slane, z);
+      constexpr int NSG = TPW * W * NB, RSG = (NSG + 63) / 64;
+#pragma unroll
+      for (int pb = 0; pb < NBUF; ++pb) {
+        FB* Fp = sF[wid][pb];
+        float sa[RSG], sb[RSG], sx[RSG];
+#pragma unroll
+        for (int k = 0; k < RSG; ++k) {
+          const int q = lane + 64 * k, qc = q < NSG ? q : 0;
+          const int qt = qc / (W * NB), qq = qc % (W * NB);
+          const float2 ab = *reinterpret_cast<const float2*>(&TI.lg[2 * qq + z]);
+          sa[k] = ab.x;
+          sb[k] = ab.y;
+          sx[k] = Fp[qt].x[qq / NB];
+        }
+#pragma unroll
+        for (int k = 0; k < RSG; ++k) {
+          const int q = lane + 64 * k;
+          if (q < NSG) {
+            const int qt = q / (W * NB), qq = q % (W * NB);
+            Fp[qt].sg[qq] = sigm_l2(ffma(sa[k], sx[k], sb[k]));
+          }
+        }
+      }
+      wsync();
+      cur = nx1;
+      prv = nx2;
+    }
+    FB* Fs = sF[wid][PF ? ev & 1 : 0];
+    layer_jobs<L1, D, true, TPW, D, CB>(Fs, g1s, T1, TI.rh, R1, cbs, gl1, wc1, gs1, lane, z);
+    wsync();
+    reduce_gin<L1, TPW, H, CB>(cbs, g0s, lane);
+    wsync();
+    layer_jobs<L0, 0, true, TPW, H, CB>(Fs, g0s, T0, TI.rh, R0, cbs, gl0, wc0, gs0, lane, z);
+    wsync();
+    reduce_gin<L0, TPW, D, CB>(cbs, gxs, lane);
+    wsync();
+  };
+
+  // grid-wide fixed-order sum of two per-lane fp64 values (every workgroup gets the same result)
+  unsigned round = 0;
+  auto gsum = [&](double v0, double v1, double& s0, double& s1) {
+    v0 = xor_sum64(v0);
+    v1 = xor_sum64(v1);
+    if (lane == 0) {
+      s_red[wid][0] = v0;
+      s_red[wid][1] = v1;
+    }
+    __syncthreads();
+    if (wid == 0) {
+      double u0 = s_red[0][0], u1 = s_red[0][1];
+#pragma unroll
+      for (int w = 1; w < kTPB; ++w) {
+        u0 += s_red[w][0];
+        u1 += s_red[w][1];
+      }
+      double r0 = 0.0, r1 = 0.0;
+      const bool ab = grid_sum2(da.gp, round, u0, u1, r0, r1);
+      if (lane == 0) {
+        s_res[0] = r0;
+        s_res[1] = r1;
+        if (ab) s_ab = 1;
+      }
+    }
+    __syncthreads();
+    s0 = s_res[0];
+    s1 = s_res[1];
+  };
+
+  ElSt& E = s_el[wid][tt][sl < D ? sl : 0];  // written by lanes sl < D only
+  if (sl < D) {
+    E.ybc = E.fbc = 0.f;
+    E.scb = E.f0bp = 0.f;
+  }
+  // wave-uniform scalars (SGPRs): adjoints of the next dt and of t1s, this attempt's control terms
+  WSc& C = s_sc[wid];  // every lane writes the same values
+  C.dtbar = C.tbar = C.dtb_base = C.h0b = C.d0b = C.d1b = 0.0;
+  C.jj = a.T - 1;  // the last output not yet taken
+  C.dt32 = C.h0f = 0.f;
+  C.acc = 0;
+
+  for (int ev = n_ev - 1; ev >= 0; --ev) {
+    const bool in_att = ev >= s_ra.base;
+    const int n = in_att ? (ev - s_ra.base) / 6 : -1, s = in_att ? 2 + (ev - s_ra.base) % 6 : 0;
+    // ---------------- before the VJP: this evaluation's output adjoint ----------------
+    if (in_att && s == 7) {
+      const double t0 = s_ra.att[4 * n], dt = s_ra.att[4 * n + 1];
+      const float ratio = (float)s_ra.att[4 * n + 2];
+      C.acc = s_ra.att[4 * n + 3] != 0.0;
+      int m = n - 1;  // the attempt whose stage 7 produced this attempt's y and f0
+      while (m >= 0 && s_ra.att[4 * m + 3] == 0.0) --m;
+      const int fe = m >= 0 ? s_ra.base + 6 * m + 5 : 0;
+      const int e2 = s_ra.base + 6 * n;
+      C.dt32 = ((float)dt);
+      // control: dt_{n+1} = clamp(dt * min(ifactor, max(safety ratio^-1/5, dfac))) (rk_common.
+      // _optimal_step_size, fp64).  The factor the forward took is dt_{n+1} / dt_n from the attempt
+      // log, so no pow here: the middle term was taken unless the factor sits on a bound (or the
+      // clamp did), and its derivative is -factor / (5 ratio).  The last attempt's next dt feeds
+      // nothing (its adjoint is 0).
+      const double rr = (double)ratio;
+      double rbar = 0.0, dtbb = 0.0;
+      if (n + 1 < s_ra.n_att) {
+        const double dtn1 = s_ra.att[4 * (n + 1) + 1];
+        const bool clamped = (s_ra.min_step > 0.0 && dtn1 == s_ra.min_step) || dtn1 == s_ra.max_step;
+        if (!clamped) {
+          const double fac = dtn1 / dt;
+          dtbb = C.dtbar * fac;
+          if (rr > 0.0) {
+            const double dfac = rr < 1.0 ? 1.0 : s_ra.dfactor;
+            const bool bound = fabs(fac - s_ra.ifactor) <= 1e-12 * s_ra.ifactor || fabs(fac - dfac) <= 1e-12 * dfac;
+            if (!bound) rbar = C.dtbar * dt * (-0.2 * fac / rr);
+          }
+        }
+      }
+      C.dtb_base = dtbb;
+      double pd = 0.0, pt = 0.0;
+      float dtb32 = 0.f, yb0, yb1;
+      const float ybc = sl < D ? E.ybc : 0.f, fbc = sl < D ? E.fbc : 0.f;
+      float kv[8], kbv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) kv[j] = kbv[j] = 0.f;
+      float y = 0.f, y1 = 0.f;
+      if (el) {
+        y = tx(fe);
+        kv[1] = tk(fe);
+#pragma unroll
+        for (int j = 2; j <= 7; ++j) kv[j] = tk(e2 + j - 2);
+        y1 = tx(e2 + 5);
+      }
+      // err and mid in the forward's op order (fetode_fused.hip DOPRI)
+      float err = kv[1] * (s_cerr[0] * C.dt32), midv = kv[1] * (s_cmid[0] * C.dt32);
+#pragma unroll
+      for (int j = 2; j <= 7; ++j) {
+        err = err + kv[j] * (s_cerr[j - 1] * C.dt32);
+        midv = midv + kv[j] * (s_cmid[j - 1] * C.dt32);
+      }
+      float midb = 0.f, fab;
+      if (C.acc) {
+        yb1 = ybc;
+        kbv[7] = fbc;
+        yb0 = 0.f;
+        fab = 0.f;
+        // interp._interp_fit (fetode_fused.hip's op order)
+        const float ym = y + midv, fa = kv[1], fbk = kv[7];
+        const float co1 = C.dt32 * fa;
+        const float co2 = ((C.dt32 * (fbk - 4.0f * fa) - 11.0f * y) - 5.0f * y1) + 16.0f * ym;
+        const float co3 = ((C.dt32 * (5.0f * fa - 3.0f * fbk) + 18.0f * y) + 14.0f * y1) - 32.0f * ym;
+        const float co4 = ((2.0f * C.dt32) * (fbk - fa) - 8.0f * (y1 + y)) + 16.0f * ym;
+        float c0 = 0.f, c1 = 0.f, c2 = 0.f, c3 = 0.f, c4 = 0.f;
+        const double t1 = t0 + dt, dlt = t1 - t0;
+        for (; C.jj >= 1 && s_ra.t[C.jj] > t0; --C.jj) {  // outputs in (t0, t1]: uniform over the grid
+          const float x = (float)((s_ra.t[C.jj] - t0) / dlt);
+          const float g = el ? (s_ra.gsol + (int64_t)C.jj * a.B * D)[bi * D + sl] : 0.f;
+          const float x2 = x * x, x3 = x2 * x;
+          c0 += g;
+          c1 += g * x;
+          c2 += g * x2;
+          c3 += g * x3;
+          c4 += g * (x3 * x);
+          const float dsdx = co1 + 2.0f * x * co2 + 3.0f * x2 * co3 + 4.0f * x3 * co4;
+          const double xb = (double)(g * dsdx);
+          pt += xb * (-1.0 / dlt);
+          pd += xb * (-(double)x / dlt);
+        }
+        yb0 += ((c0 - 11.0f * c2) + 18.0f * c3) - 8.0f * c4;
+        yb1 += (-5.0f * c2 + 14.0f * c3) - 8.0f * c4;
+        const float ymb = (16.0f * c2 - 32.0f * c3) + 16.0f * c4;
+        fab += C.dt32 * (((c1 - 4.0f * c2) + 5.0f * c3) - 2.0f * c4);
+        kbv[7] += C.dt32 * ((c2 - 3.0f * c3) + 2.0f * c4);
+        dtb32 += ((c1 * fa + c2 * (fbk - 4.0f * fa)) + c3 * (5.0f * fa - 3.0f * fbk)) + c4 * (2.0f * (fbk - fa));
+        yb0 += ymb;
+        midb = ymb;
+      } else {
+        yb0 = ybc;
+        fab = fbc;
+        yb1 = 0.f;
+      }
+      kbv[1] = fab;
+      // error ratio = rms(err / tol): d ratio / d qe = qe / (N ratio)
+      float errb = 0.f;
+      if (rbar != 0.0 && ratio > 0.f) {
+        const float tol = s_ra.atol + s_ra.rtol * fmaxf(fabsf(y), fabsf(y1));
+        const float qe = err / tol;
+        const float qb = (float)(rbar * (double)qe / (s_ra.n_el * rr));
+        errb = qb / tol;
+        const float tolb = -qb * qe / tol, ay = fabsf(y), ay1 = fabsf(y1);
+        const float sy = y > 0.f ? 1.f : (y < 0.f ? -1.f : 0.f), sy1 = y1 > 0.f ? 1.f : (y1 < 0.f ? -1.f : 0.f);
+        const float wy = ay > ay1 ? 1.f : (ay < ay1 ? 0.f : 0.5f);
+        yb0 += tolb * s_ra.rtol * wy * sy;
+        yb1 += tolb * s_ra.rtol * (1.f - wy) * sy1;
+      }
+      float se = 0.f, sm = 0.f;
+#pragma unroll
+      for (int j = 1; j <= 7; ++j) {
+        kbv[j] += errb * (s_cerr[j - 1] * C.dt32) + midb * (s_cmid[j - 1] * C.dt32);
+        se += s_cerr[j - 1] * kv[j];
+        sm += s_cmid[j - 1] * kv[j];
+      }
+      dtb32 += errb * se + midb * sm;
+      if (sl < D) {
+#pragma unroll
+        for (int j = 1; j <= 7; ++j) {
+          kk[j][sl] = kv[j];
+          kb[j][sl] = kbv[j];
+        }
+        E.pd = pd;
+        E.pt = pt;
+        E.yb0 = yb0;
+        E.yb1 = yb1;
+        E.dtb32 = dtb32;
+      }
+    } else if (!in_att && ev == 1) {
+      // _select_initial_step (dopri5.py select_initial_step, fp32): dt0 = min(100 h0, h1)
+      const float d0 = (float)s_ra.init_rec[0], d1 = (float)s_ra.init_rec[1], d2 = (float)s_ra.init_rec[2];
+      const float h0 = (float)s_ra.init_rec[3], h1 = (float)s_ra.init_rec[4];
+      C.h0f = (h0);
+      const double dtb = C.dtbar;
+      double h1b = 0.0;
+      C.h0b = 0.0;
+      const float a100 = 100.0f * h0, ah1 = fabsf(h1), sh1 = h1 < 0.f ? -1.f : 1.f;
+      if (a100 < ah1) C.h0b = 100.0 * dtb;
+      else if (ah1 < a100) h1b = dtb * sh1;
+      else {
+        C.h0b = 50.0 * dtb;
+        h1b = 0.5 * dtb * sh1;
+      }
+      double d2b = 0.0, d1b_ = 0.0;
+      if (d1 <= 1e-15f && d2 <= 1e-15f) {  // h1 = max(1e-6, h0 1e-3)
+        const float v = h0 * 1e-3f;
+        if (v > 1e-6f) C.h0b += 1e-3 * h1b;
+        else if (v == 1e-6f) C.h0b += 0.5e-3 * h1b;
+      } else {  // h1 = (0.01 / max(d1, d2)) ** (1/5); Python's max keeps d1 on a tie
+        const bool take2 = d2 > d1;
+        const double mx = take2 ? d2 : d1, base = 0.01 / mx;
+        const double mxb = -(h1b * 0.2 * (double)h1 / base) * base / mx;
+        if (take2) d2b += mxb;
+        else d1b_ += mxb;
+      }
+      // d2 = |rms((f1 - f0) / scale) / h0|
+      const double r2 = (double)d2 * h0, r2b = d2b / h0;
+      C.h0b = (C.h0b - d2b * d2 / h0);
+      C.d1b = (d1b_);
+      float f1b = 0.f, f0bp = 0.f, scb = 0.f;
+      if (el && r2 > 0.0) {
+        const float y = tx(0), f0 = tk(0), f1 = tk(1);
+        const float scale = s_ra.atol + fabsf(y) * s_ra.rtol;
+        const float q2 = (f1 - f0) / scale;
+        const float q2b = (float)(r2b * (double)q2 / (s_ra.n_el * r2));
+        f1b = q2b / scale;
+        f0bp = -q2b / scale;
+        scb = -q2b * q2 / scale;
+      }
+      if (sl < D) {
+        kb[0][sl] = f1b;
+        E.f0bp = f0bp;
+        E.scb = scb;
+      }
+      C.d0b = 0.0;
+      (void)d0;
+    } else if (ev == 0) {
+      if (s_ra.base == 2) {  // the rest of _select_initial_step: d0 = rms(y0 / scale), d1 = rms(f0 / scale)
+        const float d0 = (float)s_ra.init_rec[0], d1 = (float)s_ra.init_rec[1];
+        if (el) {
+          const float y = tx(0), f0 = tk(0);
+          const float scale = s_ra.atol + fabsf(y) * s_ra.rtol;
+          const float q0 = y / scale, q1 = f0 / scale;
+          const float q0b = d0 > 0.f ? (float)(C.d0b * (double)q0 / (s_ra.n_el * d0)) : 0.f;
+          const float q1b = d1 > 0.f ? (float)(C.d1b * (double)q1 / (s_ra.n_el * d1)) : 0.f;
+          const float scb = E.scb - q0b * q0 / scale - q1b * q1 / scale;
+          const float sy = y > 0.f ? 1.f : (y < 0.f ? -1.f : 0.f);
+          E.ybc += q0b / scale + scb * s_ra.rtol * sy;
+          E.fbc += q1b / scale;
+        }
+      }
+      if (sl < D) kb[0][sl] = el ? E.fbc : 0.f;
+    }
+    // this evaluation's output adjoint -> the layer-1 output slots
+    if (sl < D) g1s[tt * D + sl] = in_att ? kb[s][sl] : kb[0][sl];
+    vjp(ev);
+    // ---------------- after the VJP: the input adjoint ----------------
+    const float xb = sl < D ? gxs[tt * D + sl] : 0.f;
+    if (in_att) {
+      double v0 = 0.0, v1 = 0.0;
+      if (sl < D) {
+        const float X = xb + (s == 7 ? E.yb1 : 0.f);  // stage 7's input IS y1
+        E.yb0 += X;
+        float sb = 0.f;
+        for (int j = 1; j < s; ++j) {  // tableau row s - 2
+          const float c = s_beta[s - 2][j - 1];
+          kb[j][sl] += (c * C.dt32) * X;
+          sb += c * kk[j][sl];
+        }
+        E.dtb32 += X * sb;
+        if (s == 2) {  // attempt n done: the carries
+          E.ybc = el ? E.yb0 : 0.f;
+          E.fbc = el ? kb[1][sl] : 0.f;
+          v0 = el ? E.pd + (double)E.dtb32 : 0.0;
+          v1 = el ? E.pt : 0.0;
+        }
+      }
+      if (s == 2) {  // the grid sum of the attempt's d/d dt and d/d t0 terms
+        double S0, S1;
+        gsum(v0, v1, S0, S1);
+        C.dtbar = (C.dtb_base + (C.acc ? C.tbar : 0.0) + S0);
+        C.tbar = (C.tbar + S1);
+      }
+    } else if (ev == 1) {  // the probe: input y0 + h0 f0
+      const float f0 = el ? tk(0) : 0.f;
+      if (el) {
+        E.ybc += xb;
+        E.fbc += xb * C.h0f + E.f0bp;
+      }
+      double S0, S1;
+      gsum(el ? (double)(xb * f0) : 0.0, 0.0, S0, S1);
+      C.h0b = (C.h0b + S0);
+      const float d0 = (float)s_ra.init_rec[0], d1 = (float)s_ra.init_rec[1];
+      if (!(d0 < 1e-5f || d1 < 1e-5f)) {  // h0 = |0.01 d0 / d1|
+        C.d0b = (C.h0b * 0.01 / d1);
+        C.d1b = (C.d1b - C.h0b * (double)C.h0f / d1);
+      }
+    } else {  // evaluation 0: f(y0)
+      if (el) {
+        E.ybc += xb;
+        if (s_ra.gy0) s_ra.gy0[bi * D + sl] = E.ybc + s_ra.gsol[bi * D + sl];  // solution[0] = y0
+      }
+    }
+  }
+  float* part = a.part + ((int64_t)blockIdx.x * kTPB + wid) * a.nacc;
+  R0.template store<TPW>(part, lane);
+  R1.template store<TPW>(part + L0::AL.n, lane);
+  if (blockIdx.x == 0 && threadIdx.x == 0)
+    da.status[0] = (s_ab || __hip_atomic_load(dp_abort(da.gp), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) ? 4 : 0;
+}
+
 // Parameter-gradient sums of one layer from the recorded adjoints (after fixed_bwd_kernel<ACC =
 // false>): every sample (evaluation ev, trajectory b) is independent, so the sums are formed
 // element-major — a thread owns fixed jobs of the layer (a Ferro element, a KAN edge, one or two
@@ -1143,12 +1660,15 @@ __global__ __launch_bounds__(64) void grad_apply_kernel(const double* __restrict
 }
 
 typedef void (*bwd_fn)(BwdArgs);
+typedef void (*dopri_bwd_fn)(DopriBwdArgs);
 struct BwdEntry {
   int D, H, K, NB, NG;
   bool ferro;
-  int tpw;                     // trajectories per wave of fn
+  int tpw;                     // trajectories per wave of fn (and of dopri)
   bwd_fn fn;                   // the one-kernel sweep (sums in VGPRs)
   bwd_fn adj, sum0, sum1;      // the split: adjoint sweep + per-layer parameter sums (or null)
+  dopri_bwd_fn dopri;          // the reverse sweep of the resident dopri5 solve
+  int dtpw;                    // its trajectories per wave (the whole batch is resident)
 };
 const BwdEntry kBwd[] = {
     // LV KAN-FET [2,10,2]: one kernel, two trajectories per wave (measured: TPW 1 / 2 / 4 = 1034 / 897 /
@@ -1156,12 +1676,14 @@ const BwdEntry kBwd[] = {
 #ifdef FETODE_DIAG   // the split structure (measured slower) lives in the diagnostic build only
     {2, 10, 10, 10, 12, true, 2, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 2>,
      fixed_bwd_kernel<2, 10, 10, 10, 12, true, false, 1>, param_sum_kernel<2, 10, 10, 10, 12, 0>,
-     param_sum_kernel<2, 10, 10, 10, 12, 1>},
+     param_sum_kernel<2, 10, 10, 10, 12, 1>, dopri_bwd_kernel<2, 10, 10, 10, 12, true, 2>, 2},
 #else
-    {2, 10, 10, 10, 12, true, 2, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 2>, nullptr, nullptr, nullptr},
+    {2, 10, 10, 10, 12, true, 2, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 2>, nullptr, nullptr, nullptr,
+     dopri_bwd_kernel<2, 10, 10, 10, 12, true, 2>, 2},
 #endif
     // LV KAN [2,10,2] (126 VGPRs: four waves per SIMD already)
-    {2, 10, 0, 10, 12, false, 1, fixed_bwd_kernel<2, 10, 1, 10, 12, false, true, 1>, nullptr, nullptr, nullptr},
+    {2, 10, 0, 10, 12, false, 1, fixed_bwd_kernel<2, 10, 1, 10, 12, false, true, 1>, nullptr, nullptr, nullptr,
+     dopri_bwd_kernel<2, 10, 1, 10, 12, false, 2>, 2},
 };
 // Which path the KAN-FET sweep takes (fetode_backward_set_split; env FETODE_BWD_SPLIT).  Default:
 // the one-kernel sweep — measured on MI355X at B = 4096, rk4, 34 steps: one kernel 1.06 ms vs the
@@ -1213,6 +1735,27 @@ void layouts(const fetode_field_t* f, AccLayout* L0, AccLayout* L1) {
   const bool fe = f->ferro != nullptr;
   *L0 = acc_layout(f->kan[0].in_features, f->kan[0].out_features, K, f->kan[0].num_logistic, NS, fe);
   *L1 = acc_layout(f->kan[1].in_features, f->kan[1].out_features, K, f->kan[1].num_logistic, NS, fe);
+}
+
+
+// gradient sums S -> parameter gradients in the reference layouts (grad_apply_kernel)
+int apply_grads(const fetode_field_t* f, const double* S, const AccLayout& AL0, const AccLayout& AL1,
+                const fetode_kanlinear_grad_t* kan_grads, const fetode_ferro_grad_t* ferro_grads, hipStream_t s) {
+  if (!kan_grads && !ferro_grads) return FETODE_OK;
+  ApplyLayer L[2];
+  for (int l = 0; l < 2; ++l) {
+    memset(&L[l], 0, sizeof(ApplyLayer));
+    L[l].kl = f->kan[l];
+    if (f->ferro) L[l].fl = f->ferro[l];
+    L[l].has_ferro = f->ferro != nullptr;
+    L[l].AL = l == 0 ? AL0 : AL1;
+    if (kan_grads) L[l].kg = kan_grads[l];
+    if (ferro_grads && f->ferro) L[l].fg = ferro_grads[l];
+  }
+  const int n0 = apply_items(L[0]), n1 = apply_items(L[1]);
+  hipLaunchKernelGGL(grad_apply_kernel, dim3((unsigned)((n0 + n1) / 64)), dim3(64), 0, s, S, L[0], L[1], n0);
+  LAUNCH_CHECK();
+  return FETODE_OK;
 }
 
 }  // namespace
@@ -1338,21 +1881,138 @@ int fetode_integrate_fixed_backward(const fetode_field_t* f, const void* plan, i
   LAUNCH_CHECK();
   hipLaunchKernelGGL(chunk_sum_kernel, dim3(nblk(nacc, 64)), dim3(64 * kChunkWaves), 0, s, chunks, (int)nch, nacc, S);
   LAUNCH_CHECK();
-  if (!kan_grads && !ferro_grads) return FETODE_OK;
-  ApplyLayer L[2];
-  for (int l = 0; l < 2; ++l) {
-    memset(&L[l], 0, sizeof(ApplyLayer));
-    L[l].kl = f->kan[l];
-    if (f->ferro) L[l].fl = f->ferro[l];
-    L[l].has_ferro = f->ferro != nullptr;
-    L[l].AL = l == 0 ? AL0 : AL1;
-    if (kan_grads) L[l].kg = kan_grads[l];
-    if (ferro_grads && f->ferro) L[l].fg = ferro_grads[l];
+  return apply_grads(f, S, AL0, AL1, kan_grads, ferro_grads, s);
+}
+
+// ---- reverse sweep of the resident dopri5 solve ----
+// every workgroup resident at once (one grid sum per attempt): the occupancy of the kernel
+static int64_t dopri_bwd_resident_wgs(const BwdEntry* e) {
+  static int n_cu = 0;
+  static int per_cu[2] = {0, 0};
+  const int fi = e->ferro ? 0 : 1;
+  if (!n_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return -1;
   }
-  const int n0 = apply_items(L[0]), n1 = apply_items(L[1]);
-  hipLaunchKernelGGL(grad_apply_kernel, dim3((unsigned)((n0 + n1) / 64)), dim3(64), 0, s, S, L[0], L[1], n0);
+  if (!per_cu[fi] && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[fi], e->dopri, 64 * kTPB, 0) != hipSuccess)
+    return -1;
+  return (int64_t)per_cu[fi] * n_cu;
+}
+static int64_t dopri_bwd_grid(const BwdEntry* e, int64_t B) { return (B + kTPB * e->dtpw - 1) / (kTPB * e->dtpw); }
+
+int64_t fetode_integrate_dopri5_backward_max_batch(const fetode_field_t* f) {
+  if (validate_field(f) != FETODE_OK) return 0;
+  const BwdEntry* e = find_bwd(f);
+  if (!e || !e->dopri) return 0;
+  const int64_t w = dopri_bwd_resident_wgs(e);
+  return w > 0 ? w * kTPB * e->dtpw : 0;
+}
+
+int64_t fetode_integrate_dopri5_backward_workspace(const fetode_field_t* f, int64_t B) {
+  if (validate_field(f) != FETODE_OK || B <= 0) return -1;
+  const BwdEntry* e = find_bwd(f);
+  if (!e || !e->dopri) return -1;
+  AccLayout L0, L1;
+  layouts(f, &L0, &L1);
+  const int64_t nacc = L0.n + L1.n, grid = dopri_bwd_grid(e, B), nrow = grid * kTPB;
+  const int64_t nch = nrow < kChunks ? nrow : kChunks;
+  return (int64_t)sizeof(unsigned) * kDpBarWords + (int64_t)sizeof(double) * (2 * grid + 4 * kDpGroups) +
+         (int64_t)sizeof(double) * nacc * (nch + 1) + (int64_t)sizeof(float) * nrow * nacc;
+}
+
+int fetode_integrate_dopri5_backward(const fetode_field_t* f, const void* plan, int64_t B, const double* t, int32_t T,
+                                     double rtol, double atol, const double* opts, const float* tableau,
+                                     const float* grad_solution, const float* tape, int32_t n_ev,
+                                     const double* attempts, int32_t n_att, const double* init_rec,
+                                     const float* state0, uint32_t init_mask, float* grad_y0,
+                                     const fetode_kanlinear_grad_t* kan_grads, const fetode_ferro_grad_t* ferro_grads,
+                                     void* workspace, int32_t* status, void* stream) {
+  int rc = validate_field(f);
+  if (rc) return rc;
+  const BwdEntry* e = find_bwd(f);
+  if (!e || !e->dopri) return set_err(FETODE_EUNSUPPORTED, "no dopri5 backward kernel for this field shape");
+  if (B <= 0 || T <= 0) return FETODE_OK;
+  if (!plan || !t || !opts || !tableau || !grad_solution || !tape || !attempts || !init_rec || !workspace ||
+      !status || (f->ferro && !state0 && (init_mask & 3u) != 3u))
+    return set_err(FETODE_EINVAL, "dopri5 backward: null pointer");
+  const int base = opts[0] > 0.0 ? 1 : 2;
+  if (n_att < 0 || n_ev != base + 6 * n_att)
+    return set_err(FETODE_EINVAL, "dopri5 backward: %d evaluations do not match %d attempts", n_ev, n_att);
+  const int64_t resident = dopri_bwd_resident_wgs(e);
+  if (resident < 0) return set_err(FETODE_EHIP, "dopri5 backward: occupancy query failed");
+  const int64_t grid = dopri_bwd_grid(e, B);
+  if (grid > resident)
+    return set_err(FETODE_EUNSUPPORTED, "dopri5 backward: batch %lld needs %lld workgroups, %lld resident",
+                   (long long)B, (long long)grid, (long long)resident);
+  hipStream_t s = (hipStream_t)stream;
+  AccLayout AL0, AL1;
+  layouts(f, &AL0, &AL1);
+  const int nacc = AL0.n + AL1.n;
+  const int64_t nrow = grid * kTPB, nch = nrow < kChunks ? nrow : kChunks;
+  unsigned* bar = (unsigned*)workspace;
+  double* slot = (double*)((char*)workspace + sizeof(unsigned) * kDpBarWords);
+  double* xs = slot + 2 * grid;
+  double* S = xs + 4 * kDpGroups;
+  double* chunks = S + nacc;
+  float* part = (float*)(chunks + nch * nacc);
+
+  DopriBwdArgs d;
+  memset(&d, 0, sizeof(d));
+  BwdArgs& a = d.b;
+  a.plan = (const float*)plan;
+  layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
+  layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
+  a.k0 = f->kan[0];
+  a.k1 = f->kan[1];
+  if (f->ferro) {
+    a.f0 = f->ferro[0];
+    a.f1 = f->ferro[1];
+  }
+  a.B = B;
+  a.T = T;
+  a.gsol = grad_solution;
+  a.tape = tape;
+  a.state0 = state0;
+  a.init_mask = f->ferro ? init_mask : 3u;
+  a.gy0 = grad_y0;
+  a.part = part;
+  a.nacc = nacc;
+  d.att = attempts;
+  d.n_att = n_att;
+  d.n_ev = n_ev;
+  d.base = base;
+  d.t = t;
+  d.init_rec = init_rec;
+  for (int i = 0; i < 6; ++i)
+    for (int j = 0; j < 6; ++j) d.beta[i][j] = tableau[i * 6 + j];
+  for (int j = 0; j < 7; ++j) {
+    d.cerr[j] = tableau[36 + j];
+    d.cmid[j] = tableau[43 + j];
+  }
+  d.rtol = (float)rtol;
+  d.atol = (float)atol;
+  d.safety = opts[1];
+  d.ifactor = opts[2];
+  d.dfactor = opts[3];
+  d.min_step = opts[4];
+  d.max_step = opts[5];
+  d.n_el = (double)B * f->kan[0].in_features;
+  d.gp.bar = bar;
+  d.gp.slot = slot;
+  d.gp.xs = xs;
+  dp_single_device(d.gp, grid);
+  d.status = status;
+  HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kDpBarWords, s));
+  void* args[] = {&d};
+  HIP_CHECK_RET(resident_launch((const void*)e->dopri, dim3((unsigned)grid), dim3(64 * kTPB), args, 0, s));
+  const int64_t per = (nrow + nch - 1) / nch;
+  hipLaunchKernelGGL(part_reduce_kernel, dim3(nblk(nacc, 64), (unsigned)nch), dim3(64), 0, s, part, nrow, nacc, per,
+                     chunks);
   LAUNCH_CHECK();
-  return FETODE_OK;
+  hipLaunchKernelGGL(chunk_sum_kernel, dim3(nblk(nacc, 64)), dim3(64 * kChunkWaves), 0, s, chunks, (int)nch, nacc, S);
+  LAUNCH_CHECK();
+  return apply_grads(f, S, AL0, AL1, kan_grads, ferro_grads, s);
 }
 
 }  // extern "C"

@@ -60,100 +60,7 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 
 namespace {
 
-// Device-resident dopri5 (torchdiffeq Dopri5Solver, the default method of every reference odeint
-// without `method`, train_kanfet_node_predprey.py:252): the control arithmetic of the host-driven
-// path (fet-ode_amd/dopri5.py _Dopri5 with fetode_lincomb / fetode_scaled_rms / fetode_interp_*).
-struct DopriParams {
-  int32_t on;
-  const double* t;  // (T) output times, fp64, strictly increasing
-  int32_t T;
-  float rtol, atol;
-  double first_step, safety, ifactor, dfactor, min_step, max_step;
-  int32_t max_steps;
-  // tableau in fp32 (RKAdaptiveStepsizeODESolver casts it to y0's dtype), by stage column j:
-  // stc[j][q] = beta[j + q][j] (q < 6, 0 past the tableau), stc[j][6] = c_error[j], stc[j][7] = c_mid[j]
-  float stc[7][8];
-  unsigned* bar;    // grid-reduction words (zeroed before the launch)
-  double* slot;     // (grid, 2) per-workgroup partial sums
-  double* xs;       // (2, kDpGroups, 2) leaf sums, double-buffered by round parity
-  int32_t* stats;   // nfev, attempts, status
-  double* att;      // (max_att, 4): t0, dt, error ratio, accepted
-  int32_t max_att;
-  // trajectory-sharded solve (fetode_integrate_dopri5_xrank): every norm is the sum over all ranks
-  double n_total;              // global element count of the norms (B_global * D)
-  int32_t xr_rank, xr_world;   // xr_world <= 1: single device
-  uint32_t xr_epoch;           // per-solve tag (the same on every rank)
-  double* const* xr_peers;     // (dev) xr_world inbox base pointers as mapped here (peers[rank] = own)
-  double* xr_inbox;            // (dev) own inbox: (2, world) records {v0, v1, tag, pad}
-  double* xr_g;                // (2, 2) the global sums of the round, double-buffered by parity
-  // leaves of the grid reduction: contiguous runs of leaf_len workgroups in GLOBAL workgroup numbers
-  // (this grid's workgroup b is global workgroup wg_off + b); this grid owns leaves
-  // [leaf_lo, leaf_lo + n_leaf_local) of n_leaf_global.  xr_exact: every rank owns whole leaves of
-  // the single-device grid, so the rank-summed result is bitwise the single device's
-  int32_t leaf_shift, wg_off, leaf_lo, n_leaf_local, n_leaf_global, nblk_global, xr_exact;  // leaf_len = 1 << leaf_shift
-};
-
-// Grid-wide sum of two fp64 values, one per workgroup (valid on every lane of a one-wave
-// workgroup), returned to every workgroup in the same fixed summation order.  Round r:
-//   1. each workgroup stores its partial and arrives on one of kDpGroups leaf counters
-//      (blockIdx % kDpGroups, ~32 arrivals each at the 2048-workgroup grid: same-address atomics
-//      serialise at the memory side, ~25 ns each);
-//   2. the leaf's last arriver sums its leaf's partials (lane per partial, xor tree), stores the
-//      leaf sum in the round's buffer (r & 1) and bumps the monotonic top counter (kDpTopCopies
-//      replicas, one lane each);
-//   3. every workgroup polls its replica of the top counter until all leaves of round r have arrived, then sums
-//      the kDpGroups leaf sums itself (lane per leaf, xor tree: the same order everywhere).
-// Round r + 2 may overwrite buffer r & 1 only after every workgroup has arrived at round r + 1,
-// i.e. after it finished reading round r.  dp_order() between dependent steps.  Every spin is
-// bounded: after ~1 s the abort word is raised and every later reduction returns at once (the
-// grid was not co-resident); the caller reports status 4.
-constexpr unsigned kDpSpinLimit = 1u << 20;
-constexpr int kDpGroups = 64;
-constexpr int kDpLine = 64;  // words per counter line
-constexpr int kDpTopCopies = 8;  // replicas of the top counter: ~256 pollers per address, not 2048
-constexpr int kDpBarWords = kDpLine * (kDpGroups + 2 + 2 * kDpTopCopies);
-// replicas of the cross-rank "global sum ready" counter (after the top-counter replicas)
-__device__ __forceinline__ unsigned* dp_ready(const DopriParams& P, unsigned c) {
-  return P.bar + kDpLine * (kDpGroups + 2 + kDpTopCopies + c);
-}
-constexpr unsigned kXrSpinLimit = 1u << 24;   // cross-rank polls: ranks may start seconds apart
-__device__ __forceinline__ unsigned* dp_cnt(const DopriParams& P, unsigned x) { return P.bar + kDpLine * x; }
-__device__ __forceinline__ unsigned* dp_top(const DopriParams& P, unsigned c) {
-  return P.bar + kDpLine * (kDpGroups + 2 + c);
-}
-__device__ __forceinline__ unsigned* dp_abort(const DopriParams& P) { return P.bar + kDpLine * (kDpGroups + 1); }
-
-// Ordering between the reduction's atomics.  Every word the reduction shares between workgroups
-// (partials, leaf sums, counters) is accessed only through agent-scope atomics, which are coherent
-// across the XCDs' L2s by themselves (sc1 loads / stores); what the protocol needs is only that a
-// store has landed before the arrival that publishes it, and that the reads after an arrival or a
-// poll start after it — a wait on the vector memory counter.  An agent-scope fence (or an
-// acquire / release atomic) would ALSO write back and invalidate the XCD's whole L2
-// (buffer_wbl2 / buffer_inv sc1) for plain loads and stores this protocol never shares: with 2048
-// workgroups arriving that cost ~50 us per reduction and evicted the field's parameters from L2.
-__device__ __forceinline__ void dp_order() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
-// One 16-byte {v0, v1} record per write-through (sc1) store / load: the hand-off forms of
-// MI355X_MICROARCH.md's table (16-B sc1 payload, vmcnt(0), then the counter add; loads only after
-// the add returned / the poll matched).  The load waits inside the asm (invisible to the compiler).
-typedef unsigned dp_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void dp_st16(double* p, double v0, double v1) {
-  const unsigned long long a = __double_as_longlong(v0), b = __double_as_longlong(v1);
-  const dp_u32x4 v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void dp_ld16(const double* p, double& v0, double& v1) {
-  dp_u32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-  v0 = __longlong_as_double(((unsigned long long)v.y << 32) | v.x);
-  v1 = __longlong_as_double(((unsigned long long)v.w << 32) | v.z);
-}
-
-__device__ __forceinline__ double xor_sum64(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
+#include "fetode_gridsum.h"
 
 // System-scope (sc0 sc1: write-through to memory / read past every cache) records for the
 // cross-rank exchange: the payload lands before the tag that publishes it (vmcnt(0) between).
@@ -282,89 +189,6 @@ __device__ void xrank_comm(const DopriParams& P) {
   }
 }
 
-__device__ bool grid_sum2(const DopriParams& P, unsigned& round, double v0, double v1, double& s0, double& s1) {
-#ifdef FETODE_EXP_NO_GRIDSUM  // diagnostics only: per-workgroup control, no synchronisation
-  s0 = v0 * gridDim.x;
-  s1 = v1 * gridDim.x;
-  return false;
-#endif
-  const bool xr = P.xr_world > 1;   // the last workgroup is the cross-rank exchange (xrank_comm)
-  const unsigned blk = blockIdx.x, nblk = gridDim.x - (xr ? 1u : 0u);
-  if (nblk == 1u && !xr) {  // one workgroup: the sums below would return v0, v1 exactly
-    s0 = v0;
-    s1 = v1;
-    return false;
-  }
-  // leaves in GLOBAL workgroup numbers: blocks of 8 L consecutive workgroups, each split by
-  // workgroup % 8 into 8 leaves of L — a leaf's workgroups all run on one XCD (workgroups are dealt
-  // to the 8 XCDs round-robin; rank offsets are multiples of 8 L), so its partials and counter stay
-  // in that XCD's L2, and a block is whole on one rank in a sharded solve
-  const unsigned sh = (unsigned)P.leaf_shift, L = 1u << sh, gb = blk + (unsigned)P.wg_off;
-  const unsigned x = ((gb >> (sh + 3u)) << 3u) | (gb & 7u);
-  const unsigned first = ((x >> 3u) << (sh + 3u)) + (x & 7u);
-  const unsigned nx = min(L, ((unsigned)P.nblk_global - first + 7u) >> 3u);
-  const unsigned ngrp = (unsigned)P.n_leaf_local;
-  const unsigned r = round++;
-  double* xs = P.xs + 2 * kDpGroups * (r & 1u);
-  unsigned* abw = dp_abort(P);
-  const int lane = threadIdx.x & 63;
-  int ab = 0, leader = 0;
-  if (lane == 0) {
-    ab = __hip_atomic_load(abw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
-    dp_st16(&P.slot[2 * blk], v0, v1);
-    dp_order();
-    if (!ab)
-      leader = __hip_atomic_fetch_add(dp_cnt(P, x), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nx * (r + 1u) - 1u;
-  }
-  ab = __shfl(ab, 0);
-  leader = __shfl(leader, 0);
-  if (!ab && leader) {
-    dp_order();
-    double a0 = 0.0, a1 = 0.0;
-    for (unsigned j = lane; j < nx; j += 64) {
-      double u0, u1;
-      dp_ld16(&P.slot[2 * (first + (j << 3u) - (unsigned)P.wg_off)], u0, u1);
-      a0 += u0;
-      a1 += u1;
-    }
-    a0 = xor_sum64(a0);
-    a1 = xor_sum64(a1);
-    if (lane == 0) dp_st16(&xs[2 * x], a0, a1);
-    dp_order();
-    if (lane < kDpTopCopies) __hip_atomic_fetch_add(dp_top(P, lane), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  if (lane == 0 && !ab) {
-    // single device: all leaves of round r; sharded: the exchange workgroup's rank sum of round r
-    const unsigned want = xr ? r + 1u : ngrp * (r + 1u);
-    unsigned spins = 0;
-    // wrap-safe: (int)(top - want) < 0 while fewer than `want` leaf arrivals have landed
-    unsigned* top = xr ? dp_ready(P, blk % kDpTopCopies) : dp_top(P, blk % kDpTopCopies);
-    while ((int)(__hip_atomic_load(top, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
-      __builtin_amdgcn_s_sleep(1);
-      if ((spins & 15u) == 15u && __hip_atomic_load(abw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        ab = 1;
-        break;
-      }
-      if (++spins == (xr ? kXrSpinLimit : kDpSpinLimit)) {
-        __hip_atomic_store(abw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ab = 1;
-        break;
-      }
-    }
-    dp_order();
-  }
-  ab = __shfl(ab, 0);
-  if (xr) {
-    if (!ab) dp_ld16(P.xr_g + 2 * (r & 1u), s0, s1);
-    return ab != 0;
-  }
-  double u0 = 0.0, u1 = 0.0;
-  if ((unsigned)lane < ngrp && !ab) dp_ld16(&xs[2 * lane], u0, u1);   // one device: leaves 0 .. ngrp-1
-  s0 = xor_sum64(u0);
-  s1 = xor_sum64(u1);
-  return ab != 0;
-}
-
 struct FusedArgs {
   const float* plan;
   LayerPlan P0, P1;
@@ -475,7 +299,7 @@ __device__ __forceinline__ float v4_edges(const V4Lds<IN, FLEN>& L, const float*
 // HOT = true: the rk4 (3/8) integrate path only, every stage inlined, outputs predicated;
 // HOT = false: single evaluations and every other method.  At least 2 waves per SIMD in every
 // variant: the resident dopri5 grid (DOPRI) needs B / 2 co-resident waves.
-template <int H, int K_, int NB, int NG, bool FERRO, bool HOT, bool DOPRI = false>
+template <int H, int K_, int NB, int NG, bool FERRO, bool HOT, bool DOPRI = false, bool TAPE = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fused4_kernel(FusedArgs a) {
   constexpr int D = 2, NI = NG - 1, NFL = 1 + NB, NFP = (NFL + 1) & ~1, K = FERRO ? K_ : 0;
   // feature jobs: logistic 0..NB-1, SiLU, [gate, exp(gs x)], then x / u / m stores
@@ -693,9 +517,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   const int si0 = spl0 ? cc0 : 0, si1 = spl1 ? c1 : 0;
 
   // training tape: the two layer inputs of evaluation `ev` at tape[(ev B + b)(D + H) + c]
-  const bool taping = a.tape != nullptr;  // uniform: the inference path skips every tape op
-  float* tape_b = taping ? a.tape + (valid ? b : 0) * (D + H) : nullptr;
-  const int64_t tape_stride = a.B * (D + H);
+  // uniform: the inference path skips every tape op (the dopri5 driver has a taped instantiation
+  // of its own: the inference one carries no tape code, its registers are full)
+  bool taping = (!DOPRI || TAPE) && a.tape != nullptr;
+  // the dopri5 tape holds the first tape_cap evaluations (the host re-runs a longer solve)
+  int64_t tape_left = DOPRI ? a.dp.tape_cap : 0;
+  // dopri5 training rows also hold the evaluation's output k after the two layer inputs
+  constexpr int TW = DOPRI ? 2 * D + H : D + H;
+  float* tape_b = taping ? a.tape + (valid ? b : 0) * TW : nullptr;
+  const int64_t tape_stride = a.B * TW;
   auto eval_body = [&](float xin, auto fact_tag) __attribute__((always_inline)) -> float {
     constexpr bool F_ = decltype(fact_tag)::value;
     STAMP(6);
@@ -778,7 +608,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
         if (taping && valid) tape_b[D + o0] = h;
       }
     }
-    if (taping) tape_b += tape_stride;
+    if (taping) {
+      tape_b += tape_stride;
+      if constexpr (DOPRI) taping = --tape_left > 0;
+    }
     STAMP(3);
     __syncthreads();
     STAMP(4);
@@ -900,7 +733,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
         }
         if (grid_sum2(P, round, v0, v1, s0, s1)) status = 4;
       };
+      // training: the output of evaluation nfev (the first tape_cap of them) next to its layer
+      // inputs, in the row the evaluation just wrote (tape_b has moved past it)
+      auto ktape = [&](float k) {
+        if constexpr (TAPE)
+          if (nfev < P.tape_cap && valid && c1 == 0) tape_b[D + H + row - tape_stride] = k;
+      };
       float f0 = eval(y);
+      ktape(f0);
       ++nfev;
       double dt;
       if (P.first_step > 0.0) {
@@ -915,6 +755,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
         float h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : (0.01f * d0) / d1;
         h0 = fabsf(h0);
         const float f1 = eval(y + f0 * h0);
+        ktape(f1);
         ++nfev;
         const float q2 = (f1 - f0) / scale;
         gsum2(real ? (double)q2 * q2 : 0.0, 0.0, s, s1);
@@ -923,6 +764,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
         if (d1 <= 1e-15f && d2 <= 1e-15f) h1 = fmaxf(1e-6f, h0 * 1e-3f);
         else h1 = (float)pow((double)(0.01f / fmaxf(d1, d2)), (double)0.2f);  // fp64 pow rounded once: host == device
         dt = (double)fminf(100.0f * h0, fabsf(h1));
+        if (TAPE && blockIdx.x == 0 && tid == 0) {
+          P.init_rec[0] = d0;
+          P.init_rec[1] = d1;
+          P.init_rec[2] = d2;
+          P.init_rec[3] = h0;
+          P.init_rec[4] = h1;
+        }
       }
       float co[5] = {y, 0.f, 0.f, 0.f, 0.f};
       double t0s = P.t[0], t1s = P.t[0];
@@ -951,6 +799,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
 #pragma unroll
             for (int q = 0; q < 8; ++q) c[q] = P.stc[st + 1][q];
             kn = eval(yi);
+            ktape(kn);
             ++nfev;
             // entries past the tableau (coefficient 0) are never read again
 #pragma unroll
@@ -1474,14 +1323,17 @@ struct FusedEntry {
   fused_fn small;     // v6 (one trajectory per workgroup): generic
   fused_fn small_rk4; // v6: rk4
   fused_fn dopri;     // v4 with the device-resident dopri5 driver
+  fused_fn dopri_tape;  // the same, recording the training tape
 };
 const FusedEntry kFused[] = {
     // LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146)
     {2, 10, 2, 10, 10, 12, true, fused4_kernel<10, 10, 10, 12, true, false>, fused4_kernel<10, 10, 10, 12, true, true>,
-     small6_kernel<true, false>, small6_kernel<true, true>, fused4_kernel<10, 10, 10, 12, true, false, true>},
+     small6_kernel<true, false>, small6_kernel<true, true>, fused4_kernel<10, 10, 10, 12, true, false, true>,
+     fused4_kernel<10, 10, 10, 12, true, false, true, true>},
     // LV KAN [2,10,2] (predator_prey.py:101)
     {2, 10, 2, 1, 10, 12, false, fused4_kernel<10, 2, 10, 12, false, false>, fused4_kernel<10, 2, 10, 12, false, true>,
-     small6_kernel<false, false>, small6_kernel<false, true>, fused4_kernel<10, 2, 10, 12, false, false, true>},
+     small6_kernel<false, false>, small6_kernel<false, true>, fused4_kernel<10, 2, 10, 12, false, false, true>,
+     fused4_kernel<10, 2, 10, 12, false, false, true, true>},
 };
 
 // Batches up to kSmallMax take v6 (one trajectory per 3-wave workgroup, latency-bound chain split
@@ -1603,7 +1455,7 @@ static int dopri5_launch(const fetode_field_t* f, const void* plan, const float*
                          int32_t T, double rtol, double atol, const double* opts, const float* tableau,
                          float* solution, float* state, uint32_t init_mask, void* workspace, int32_t* stats,
                          double* attempts, int32_t max_attempts, const fetode_xrank_t* xr, int64_t B_total,
-                         void* stream) {
+                         float* tape, int64_t tape_cap, double* init_rec, void* stream) {
   int rc = validate_field(f);
   if (rc) return rc;
   if (B <= 0 || T <= 0) return FETODE_OK;
@@ -1631,8 +1483,11 @@ static int dopri5_launch(const fetode_field_t* f, const void* plan, const float*
   a.solution = solution;
   a.state = state;
   a.init_mask = init_mask;
+  a.tape = tape_cap > 0 ? tape : nullptr;
   DopriParams& P = a.dp;
   P.on = 1;
+  P.tape_cap = tape_cap;
+  P.init_rec = init_rec;
   P.t = t;
   P.T = T;
   P.rtol = (float)rtol;
@@ -1702,7 +1557,7 @@ static int dopri5_launch(const fetode_field_t* f, const void* plan, const float*
   hipStream_t s = (hipStream_t)stream;
   HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kDpBarWords, s));
   void* args[] = {&a};
-  HIP_CHECK_RET(resident_launch((const void*)e->dopri, dim3((unsigned)lgrid), dim3(64), args, 0, s));
+  HIP_CHECK_RET(resident_launch((const void*)(a.tape ? e->dopri_tape : e->dopri), dim3((unsigned)lgrid), dim3(64), args, 0, s));
   return FETODE_OK;
 }
 
@@ -1711,7 +1566,18 @@ int fetode_integrate_dopri5(const fetode_field_t* f, const void* plan, const flo
                             float* solution, float* state, uint32_t init_mask, void* workspace, int32_t* stats,
                             double* attempts, int32_t max_attempts, void* stream) {
   return dopri5_launch(f, plan, y0, B, t, T, rtol, atol, opts, tableau, solution, state, init_mask, workspace, stats,
-                       attempts, max_attempts, nullptr, B, stream);
+                       attempts, max_attempts, nullptr, B, nullptr, 0, nullptr, stream);
+}
+
+int fetode_integrate_dopri5_tape(const fetode_field_t* f, const void* plan, const float* y0, int64_t B, const double* t,
+                                 int32_t T, double rtol, double atol, const double* opts, const float* tableau,
+                                 float* solution, float* state, uint32_t init_mask, void* workspace, int32_t* stats,
+                                 double* attempts, int32_t max_attempts, float* tape, int64_t tape_cap,
+                                 double* init_rec, void* stream) {
+  if (tape_cap <= 0 || !tape || !init_rec || !attempts)
+    return set_err(FETODE_EINVAL, "dopri5 tape: null tape / init record / attempt log, or tape_cap <= 0");
+  return dopri5_launch(f, plan, y0, B, t, T, rtol, atol, opts, tableau, solution, state, init_mask, workspace, stats,
+                       attempts, max_attempts, nullptr, B, tape, tape_cap, init_rec, stream);
 }
 
 int fetode_integrate_dopri5_xrank(const fetode_field_t* f, const void* plan, const float* y0, int64_t B,
@@ -1726,7 +1592,7 @@ int fetode_integrate_dopri5_xrank(const fetode_field_t* f, const void* plan, con
     return set_err(FETODE_EINVAL, "dopri5 xrank: shard [%lld, %lld) outside the global batch %lld",
                    (long long)xr->b_offset, (long long)(xr->b_offset + B), (long long)B_total);
   return dopri5_launch(f, plan, y0, B, t, T, rtol, atol, opts, tableau, solution, state, init_mask, workspace, stats,
-                       attempts, max_attempts, xr, B_total, stream);
+                       attempts, max_attempts, xr, B_total, nullptr, 0, nullptr, stream);
 }
 
 int64_t fetode_xrank_inbox_bytes(int32_t world) {

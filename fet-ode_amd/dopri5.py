@@ -482,6 +482,167 @@ def _try_field_resident(func, y0, tp, reversed_, rtol, atol, options):
     return sol
 
 
+def _opts_array(options):
+    fs = options.get("first_step")
+    return np.array([float(fs) if fs is not None else 0.0, float(options.get("safety", 0.9)),
+                     float(options.get("ifactor", 10.0)), float(options.get("dfactor", 0.2)),
+                     float(options.get("min_step", 0.0)), float(options.get("max_step", math.inf)),
+                     float(options.get("max_num_steps", 2 ** 31 - 1))], dtype=np.float64)
+
+
+def _t_device(tp, dev):
+    tkey = (dev, tuple(tp.tolist()))
+    t_dev = _T_DEV.get(tkey)
+    if t_dev is None:
+        if len(_T_DEV) > 64:
+            _T_DEV.clear()
+        t_dev = _T_DEV[tkey] = tp.to(torch.float64).to(dev)
+    return t_dev
+
+
+_TAPE_BYTES0 = 1 << 30   # first-call tape budget; later calls size the tape from the last solve
+
+
+class _FusedDopri5Fn(torch.autograd.Function):
+    """Training through the device-resident dopri5 solve of a fused-shape field (the reference's
+    own training call, odeint(calDeriv, X0, t_learn) at rtol 1e-7 / atol 1e-9 followed by
+    loss.backward(), train_kanfet_node_predprey.py:252-257).  Forward: ONE launch
+    (fetode_integrate_dopri5_tape) that also records the layer inputs and the output of every
+    evaluation, the attempt log and the initial-step scalars; the tape is sized from the previous
+    solve of the field, and a longer solve is re-run from the same hysteresis state with a larger
+    one.  Backward: ONE resident launch (fetode_integrate_dopri5_backward) — reverse-mode through
+    every evaluation of every attempt, the stage sums, the interpolant, the error norm and the
+    step-size control, like autograd through torchdiffeq (which detaches none of them)."""
+
+    @staticmethod
+    def forward(ctx, field, handle, y0, t_dev, rtol, atol, opts, *params):
+        from .autograd_ops import build_plan, field_layers, pack_state, pin_plan, unpack_state
+        lib = _lib.load()
+        dev = y0.device
+        B, D = y0.shape
+        T = t_dev.numel()
+        H = field_layers(field)[0][0].out_features
+        plan = build_plan(field, handle, dev)
+        state, mask = pack_state(field, B, dev)
+        state0 = None if state is None else state.clone()
+        per_ev = B * (2 * D + H) * 4
+        cap, max_att = getattr(field, "_fetode_d5tape", (max(64, min(1 << 20, _TAPE_BYTES0 // per_ev)), 4096))
+        sol = torch.empty(T, B, D, device=dev, dtype=torch.float32)
+        ws = torch.empty(max(1, lib.fetode_integrate_dopri5_workspace(B) // 4), device=dev, dtype=torch.float32)
+        stats = torch.empty(3, device=dev, dtype=torch.int32)
+        init_rec = torch.zeros(5, device=dev, dtype=torch.float64)
+        optp = opts.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_double))
+        tabp = _TABLEAU.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_float))
+        while True:
+            tape = torch.empty(cap, B, 2 * D + H, device=dev, dtype=torch.float32)   # x, h, k per evaluation
+            att = torch.empty(max_att, 4, device=dev, dtype=torch.float64)
+            _lib.check(lib.fetode_integrate_dopri5_tape(
+                handle.ref, plan.data_ptr(), y0.data_ptr(), B, t_dev.data_ptr(), T, rtol, atol, optp, tabp,
+                sol.data_ptr(), _lib.ptr(state), mask, ws.data_ptr(), stats.data_ptr(), att.data_ptr(), max_att,
+                tape.data_ptr(), cap, init_rec.data_ptr(), _lib.stream_handle(dev)),
+                "fetode_integrate_dopri5_tape")
+            nfev, n_att, status = stats.tolist()
+            _raise_status(status, "fetode_integrate_dopri5_tape: a grid reduction timed out (workgroups not "
+                                  "co-resident); the solution is invalid")
+            if nfev <= cap and n_att <= max_att:
+                break
+            if state is not None:   # the tape ran out: the same solve again with room for all of it
+                state.copy_(state0)
+            cap, max_att = nfev + 64, n_att + 16
+        field._fetode_d5tape = (nfev + max(64, nfev // 8), n_att + max(16, n_att // 8))
+        if state is not None:
+            unpack_state(field, state)
+        dopri5_solve.last = ResidentSolve(stats, att)
+        ctx.field, ctx.handle, ctx.B, ctx.mask = field, handle, B, mask
+        ctx.plan = pin_plan(field, plan)
+        ctx.state0 = state0
+        ctx.t_dev, ctx.rtol, ctx.atol, ctx.opts = t_dev, rtol, atol, opts
+        ctx.tape, ctx.att, ctx.init_rec = tape, att, init_rec
+        ctx.n_ev, ctx.n_att = nfev, n_att
+        return sol
+
+    @staticmethod
+    def backward(ctx, grad):
+        from .autograd_ops import FERRO_PARAM_NAMES, field_layers, kan_params
+        lib = _lib.load()
+        field, B = ctx.field, ctx.B
+        dev = grad.device
+        g = _lib.f32c(grad)
+        layers = field_layers(field)
+        gy0 = torch.empty(B, g.shape[-1], device=dev, dtype=torch.float32) if ctx.needs_input_grad[2] else None
+        want = ctx.needs_input_grad[7:]
+        params = list(field.parameters())
+        wp = [p for p, w in zip(params, want) if w]
+        flat = torch.empty(sum(p.numel() for p in wp), device=dev, dtype=torch.float32)
+        grads, off = {}, 0
+        for p in wp:
+            grads[id(p)] = flat[off:off + p.numel()].view(p.shape)
+            off += p.numel()
+
+        def gbuf(p):
+            return None if p is None else grads.get(id(p))
+
+        kg = (_lib.KANLinearGrad * len(layers))()
+        fg = (_lib.FerroGrad * len(layers))() if layers[0][1] is not None else None
+        for l, (kan, fer) in enumerate(layers):
+            kg[l] = _lib.KANLinearGrad(*[_lib.ptr(gbuf(p)) for p in kan_params(kan)])
+            if fg is not None:
+                fg[l] = _lib.FerroGrad(*[_lib.ptr(gbuf(getattr(fer, n))) for n in FERRO_PARAM_NAMES])
+        nbytes = lib.fetode_integrate_dopri5_backward_workspace(ctx.handle.ref, B)
+        if nbytes < 0:
+            _lib.check(_lib.FETODE_EUNSUPPORTED, "fetode_integrate_dopri5_backward_workspace")
+        ws = torch.empty(max(1, nbytes // 4), device=dev, dtype=torch.float32)
+        status = torch.empty(1, device=dev, dtype=torch.int32)
+        _lib.check(lib.fetode_integrate_dopri5_backward(
+            ctx.handle.ref, ctx.plan.data_ptr(), B, ctx.t_dev.data_ptr(), ctx.t_dev.numel(), ctx.rtol, ctx.atol,
+            ctx.opts.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_double)),
+            _TABLEAU.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_float)), g.data_ptr(), ctx.tape.data_ptr(),
+            ctx.n_ev, ctx.att.data_ptr(), ctx.n_att, ctx.init_rec.data_ptr(),
+            _lib.ptr(ctx.state0), ctx.mask, _lib.ptr(gy0), kg, fg, ws.data_ptr(), status.data_ptr(),
+            _lib.stream_handle(dev)), "fetode_integrate_dopri5_backward")
+        _raise_status(int(status.item()), "fetode_integrate_dopri5_backward: a grid sum timed out (workgroups "
+                                          "not co-resident); the gradients are invalid")
+        ctx.tape = None
+        pgrads = [grads.get(id(p)) if w else None for p, w in zip(params, want)]
+        return (None, None, gy0, None, None, None, None, *pgrads)
+
+
+_RESIDENT_TRAIN = os.environ.get("FETODE_DOPRI5_TAPE", "1") != "0"
+
+
+def set_resident_dopri5_training(enabled: bool) -> bool:
+    """Route dopri5 training solves of the fused fields through the taped resident solve + reverse
+    sweep (default) or through _Dopri5Grad (host-driven autograd).  Returns the previous value."""
+    global _RESIDENT_TRAIN
+    prev, _RESIDENT_TRAIN = _RESIDENT_TRAIN, bool(enabled)
+    return prev
+
+
+def _try_field_resident_train(func, y0, tp, reversed_, rtol, atol, options):
+    """The taped resident solve + reverse sweep when `func` is a fused-shape field (the LV [2,10,2]
+    KAN / KAN-FET), something needs gradients, the solve is single-device and forward in time, and
+    the options are the scalar ones."""
+    from .autograd_ops import make_handle
+    from .odeint import fused_field
+    field = fused_field(func)
+    if field is None or reversed_ or y0.dim() != 2 or set(options) - _RESIDENT_OPTS:
+        return None
+    if not (isinstance(rtol, (int, float)) and isinstance(atol, (int, float))):
+        return None
+    lib = _lib.load()
+    dev = y0.device
+    B = y0.shape[0]
+    handle = make_handle(field, B, dev)
+    if not (lib.fetode_fused_supported(handle.ref) and lib.fetode_fused_backward_supported(handle.ref)):
+        return None
+    if B > min(lib.fetode_integrate_dopri5_max_batch(handle.ref, 0),
+               lib.fetode_integrate_dopri5_backward_max_batch(handle.ref)):
+        return None
+    params = list(field.parameters())
+    return _FusedDopri5Fn.apply(field, handle, y0.to(torch.float32).contiguous(), _t_device(tp, dev), float(rtol), float(atol),
+                                _opts_array(options), *params)
+
+
 def _try_wide_resident(func, y0, tp, reversed_, rtol, atol, options):
     """The whole solve in one launch (fetode_wide_dopri5) when `func` is a tagged two-layer wide
     KAN-FET field — the ETT forecaster's KANFETDynamics, KANFET([latent, hidden, latent]),
@@ -787,6 +948,10 @@ def dopri5_solve(func, y0, tc, tp, reversed_, rtol, atol, options):
         if sol is not None:
             return sol
     if _needs_grad(func, y0):
+        if _RESIDENT and _RESIDENT_TRAIN:
+            sol = _try_field_resident_train(func, y0, tp, reversed_, rtol, atol, options)
+            if sol is not None:
+                return sol
         solver = _Dopri5Grad(func, y0, rtol, atol, options, reversed_)
         sol = solver.integrate(tp)
         dopri5_solve.last = solver

@@ -202,6 +202,18 @@ int fetode_integrate_dopri5(const fetode_field_t* field, const void* plan, const
                             void* stream);
 int64_t fetode_integrate_dopri5_workspace(int64_t B);
 
+/* Training through the resident dopri5 solve (train_kanfet_node_predprey.py:252-257: the
+ * reference's loss.backward() through odeint's default dopri5).  _tape: fetode_integrate_dopri5
+ * that also records, for the first tape_cap evaluations, the two layer inputs and the output of
+ * every evaluation (tape (tape_cap, B, 2 D + H): x, h, k) and the initial-step scalars {d0, d1,
+ * d2, h0, h1} (init_rec, 5 doubles).  The caller checks stats[0] (nfev) <= tape_cap and stats[1] <=
+ * max_attempts (else re-runs from the same state with larger buffers). */
+int fetode_integrate_dopri5_tape(const fetode_field_t* field, const void* plan, const float* y0, int64_t B,
+                                 const double* t, int32_t T, double rtol, double atol, const double* opts,
+                                 const float* tableau, float* solution, float* state, uint32_t init_mask,
+                                 void* workspace, int32_t* stats, double* attempts, int32_t max_attempts,
+                                 float* tape, int64_t tape_cap, double* init_rec, void* stream);
+
 /* Trajectory-sharded device-resident dopri5 (one process per GPU, the global batch split into
  * contiguous shards; SURVEY §8e caveat 2): torchdiffeq's error ratio is an RMS over the WHOLE
  * batch, so every norm of the solve (the two initial-step norms, each attempt's error norm and
@@ -367,6 +379,28 @@ int fetode_integrate_fixed_backward(const fetode_field_t* field, const void* pla
                                     const float* grad_solution, const float* tape, const float* state0,
                                     uint32_t init_mask, float* grad_y0, const fetode_kanlinear_grad_t* kan_grads,
                                     const fetode_ferro_grad_t* ferro_grads, void* workspace, void* stream);
+
+/* The reverse sweep of a taped solve, ONE resident launch (+ the fixed-order parameter-sum
+ * reduction): reverse-mode autograd through every evaluation (rejected attempts included), the
+ * stage sums, the interpolant, the error norm and the step-size control (rk_common._runge_kutta_step,
+ * _optimal_step_size, misc._select_initial_step, interp._interp_fit / _interp_evaluate — torchdiffeq
+ * detaches none of them), one grid-wide sum per attempt for the batch-coupled adjoint of dt.
+ *   t / T / rtol / atol / opts / tableau: those of the forward; grad_solution (T, B, D); tape /
+ *   attempts / init_rec: the forward's records, n_ev = stats[0], n_att = stats[1];
+ *   state0 / init_mask: the hysteresis state before the solve; grad_y0 (B, D) nullable; the
+ *   gradients as fetode_integrate_fixed_backward (overwritten); status (dev, 1 int): 0, or 4 when a
+ *   grid sum timed out (not co-resident).
+ * Replaces: dopri5.py _Dopri5Grad (host-driven autograd through every stage of every attempt).
+ * FETODE_EUNSUPPORTED beyond fetode_integrate_dopri5_backward_max_batch. */
+int fetode_integrate_dopri5_backward(const fetode_field_t* field, const void* plan, int64_t B, const double* t,
+                                     int32_t T, double rtol, double atol, const double* opts, const float* tableau,
+                                     const float* grad_solution, const float* tape, int32_t n_ev,
+                                     const double* attempts, int32_t n_att, const double* init_rec,
+                                     const float* state0, uint32_t init_mask, float* grad_y0,
+                                     const fetode_kanlinear_grad_t* kan_grads, const fetode_ferro_grad_t* ferro_grads,
+                                     void* workspace, int32_t* status, void* stream);
+int64_t fetode_integrate_dopri5_backward_workspace(const fetode_field_t* field, int64_t B);
+int64_t fetode_integrate_dopri5_backward_max_batch(const fetode_field_t* field);
 
 /* ---- ECG KAN-FET NODE field (BASELINE configs[2]) -----------------------
  * The hysteretic LogisticBasis of train_ecg_kan_fet_nn_ode.py:54-133 (hard branch switch:

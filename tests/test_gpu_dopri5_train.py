@@ -1,0 +1,195 @@
+"""Training through the device-resident dopri5 solve — the reference's own training iteration,
+odeint(calDeriv, X0, t_learn) with torchdiffeq's default dopri5 then loss.backward()
+(train_kanfet_node_predprey.py:252-257) — as one taped forward launch
+(fetode_integrate_dopri5_tape) and one resident reverse sweep (fetode_integrate_dopri5_backward),
+against the oracle's autograd in fp64 (reference modules + the restated torchdiffeq solver,
+oracle/torch_ref.py — torchdiffeq detaches nothing, so d loss / d dt through the error ratio, the
+initial-step selection and the dense-output times is part of the gradient; large rtol makes it a
+first-order part) and against autograd through the host-driven solver (dopri5.py _Dopri5Grad).
+
+Conditioning (tools/diag/d5_grad_check.py): for the smooth KAN field the three
+agree to ~1e-7 (central differences converge to the same value).  For KAN-FET the dopri5 gradient
+is ill-conditioned: the hysteresis gates (gate_slope 10) make each attempt's error ratio — and so
+the next step size — a steep function of the parameters, the dt chain compounds that over the
+attempts, and central differences of the loss do not converge as eps shrinks.  With identical
+attempt sequences the fp32 paths and the fp64 oracle agree to ~0.5 % on short horizons, and at the
+reference's rtol 1e-7 over 35 points the gradient norm reaches ~1e17 in every implementation.  The
+KAN-FET checks are therefore: the fp64 oracle at 2e-2 where the sequences coincide, the loss, and
+bitwise run-to-run determinism."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden_sd, load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(kind, dev):
+    import fet_ode_amd as F
+    g = load_golden("traj_kanfet" if kind == "kanfet" else "traj_kan")
+    m = (F.KANFET if kind == "kanfet" else F.KAN)([2, 10, 2], grid_size=5)
+    m.load_state_dict(golden_sd(g))
+    return m.to(dev), g
+
+
+def _run(kind, dev, B, t, rtol, atol, resident, options=None, y0_grad=False, seed=0):
+    """loss = sum(w * solution) with fixed random w; returns loss, param grads, y0 grad, attempts."""
+    import fet_ode_amd as F
+    from fet_ode_amd.dopri5 import ResidentSolve, set_resident_dopri5_training
+    m, g = _model(kind, dev)
+    y0 = torch.from_numpy(g["y0_B64"]).repeat((B + 63) // 64, 1)[:B].to(dev).clone()
+    y0.requires_grad_(y0_grad)
+    w = torch.randn(len(t), B, 2, generator=torch.Generator().manual_seed(seed)).to(dev)
+    prev = set_resident_dopri5_training(resident)
+    try:
+        sol = F.odeint(F.autonomous(m), y0, t, rtol=rtol, atol=atol, options=options)
+        s = F.dopri5.dopri5_solve.last
+        assert isinstance(s, ResidentSolve) == resident
+        loss = (w * sol).sum()
+        loss.backward()
+    finally:
+        set_resident_dopri5_training(prev)
+    att = [(float(a[1]), bool(a[3])) for a in s.attempts]
+    grads = {n: p.grad.detach().cpu().clone() for n, p in m.named_parameters()}
+    return loss.item(), grads, (y0.grad.cpu() if y0_grad else None), att, s.nfev
+
+
+def _oracle(kind, B, t, rtol, atol, options=None, seed=0):
+    """fp64 autograd through the oracle: loss, param grads, y0 grad, nfev."""
+    from oracle import torch_ref as O
+    g = load_golden("traj_kanfet" if kind == "kanfet" else "traj_kan")
+    sd = golden_sd(g)
+    import fet_ode_amd as F
+    names = [n for n, _ in (F.KANFET if kind == "kanfet" else F.KAN)([2, 10, 2], grid_size=5).named_parameters()]
+    ps = {k: v.clone().double().requires_grad_(k in names) for k, v in sd.items()}
+    ref = (O.KANFETRef.from_state_dict(ps, 2) if kind == "kanfet"
+           else O.KANRef([O.KANLinearParams.from_state_dict(ps, f"layers.{l}.") for l in range(2)]))
+    y0 = torch.from_numpy(g["y0_B64"]).repeat((B + 63) // 64, 1)[:B].double().requires_grad_(True)
+    w = torch.randn(len(t), B, 2, generator=torch.Generator().manual_seed(seed)).double()
+    tr = O.Dopri5Trace()
+    sol = O.odeint(lambda tt, yy: ref(yy), y0, t, rtol=rtol, atol=atol, trace=tr, options=options)
+    loss = (w * sol).sum()
+    gr = torch.autograd.grad(loss, [ps[n] for n in names] + [y0])
+    return loss.item(), dict(zip(names, gr[:-1])), gr[-1], tr.nfev
+
+
+def _rel(a, b):
+    return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-300)).item()
+
+
+def _vs_oracle(kind, dev, B, t, rtol, atol, gtol, options=None, ltol=1e-5):
+    """Per-tensor relative error against the fp64 oracle <= gtol, or (KAN) <= 2x the host autograd
+    path's own error where fp32 summation already costs more (small, cancelling gradients)."""
+    l0, g0, y0g0, _, n0 = _run(kind, dev, B, t, rtol, atol, True, options=options, y0_grad=True)
+    l1, g1, y0g1, n1 = _oracle(kind, B, t, rtol, atol, options=options)
+    assert n0 == n1, (n0, n1)
+    assert abs(l0 - l1) <= ltol * abs(l1) + 1e-5, (l0, l1)
+    worst = {n: _rel(g0[n], g1[n]) for n in g1}
+    worst["y0"] = _rel(y0g0, y0g1)
+    if kind == "kan" and max(worst.values()) > gtol:
+        _, gh, y0gh, _, nh = _run(kind, dev, B, t, rtol, atol, False, options=options, y0_grad=True)
+        assert nh == n1
+        host = {n: _rel(gh[n], g1[n]) for n in g1}
+        host["y0"] = _rel(y0gh, y0g1)
+        bad = {n: (e, host[n]) for n, e in worst.items() if e > max(gtol, 2 * host[n])}
+        assert not bad, bad
+        return
+    assert max(worst.values()) <= gtol, sorted(worst.items(), key=lambda kv: -kv[1])[:4]
+
+
+@pytest.mark.parametrize("B", [1, 16, 64])
+@pytest.mark.parametrize("rtol", [1e-3, 1e-2, 1e-1])
+def test_dopri5_train_kan_vs_oracle_fp64(dev, B, rtol):
+    """Smooth field: the whole gradient (step-size control terms included) to 1e-4."""
+    t = torch.tensor(np.linspace(0, 2.0, 9))
+    _vs_oracle("kan", dev, B, t, rtol, rtol * 0.1, 1e-4)
+
+
+def test_dopri5_train_kan_first_step_vs_oracle_fp64(dev):
+    t = torch.tensor(np.linspace(0, 1.0, 6))
+    _vs_oracle("kan", dev, 16, t, 1e-3, 1e-4, 1e-4, options={"first_step": 0.05})
+
+
+@pytest.mark.parametrize("B,rtol,T", [(1, 1e-1, 0.5), (64, 1e-2, 0.1)])
+def test_dopri5_train_kanfet_vs_oracle_fp64(dev, B, rtol, T):
+    """KAN-FET where the attempt sequences coincide: 2e-2 (ill-conditioned, module docstring)."""
+    t = torch.tensor(np.linspace(0, T, 3))
+    _vs_oracle("kanfet", dev, B, t, rtol, rtol * 0.1, 2e-2, ltol=1e-3)
+
+
+@pytest.mark.parametrize("B", [1, 64, 300])
+def test_dopri5_train_kan_matches_host_autograd(dev, B):
+    t = torch.tensor([0.0, 0.2, 0.5], dtype=torch.float64)
+    r0 = _run("kan", dev, B, t, 1e-3, 1e-4, True, y0_grad=True)
+    r1 = _run("kan", dev, B, t, 1e-3, 1e-4, False, y0_grad=True)
+    assert r0[4] == r1[4] and [a[1] for a in r0[3]] == [a[1] for a in r1[3]]
+    assert abs(r0[0] - r1[0]) <= 1e-5 * abs(r1[0])
+    for n in r1[1]:
+        assert _rel(r0[1][n], r1[1][n]) <= 2e-4, n
+    assert _rel(r0[2], r1[2]) <= 2e-4
+
+
+def test_dopri5_train_tape_rerun(dev):
+    """A tape sized below the solve's evaluations: the forward re-runs from the same hysteresis
+    state with room for all of them — bitwise the same loss and gradients as a roomy tape."""
+    import fet_ode_amd as F
+    t = torch.tensor([0.0, 0.3, 0.6], dtype=torch.float64)
+    out = []
+    for cap in (None, (8, 2)):
+        m, g = _model("kanfet", dev)
+        if cap is not None:
+            m._fetode_d5tape = cap
+        y0 = torch.from_numpy(g["y0_B64"]).to(dev)
+        sol = F.odeint(F.autonomous(m), y0, t, rtol=1e-3, atol=1e-4)
+        sol.square().sum().backward()
+        out.append((sol.detach().cpu(), [p.grad.cpu().clone() for p in m.parameters()],
+                    [l.ferro._prev.cpu() for l in m.layers]))
+    (s0, g0, p0), (s1, g1, p1) = out
+    assert torch.equal(s0, s1)
+    assert all(torch.equal(a, b) for a, b in zip(g0, g1))
+    assert all(torch.equal(a, b) for a, b in zip(p0, p1))
+
+
+def test_dopri5_train_reference_iteration(dev):
+    """The reference's iteration itself: X0 (1, 2), t_learn = linspace(0, 3.5, 35), default rtol
+    1e-7 / atol 1e-9, loss = mean((pred[:, 0, :] - soln)^2) on the KAN-FET field: the loss as the
+    host path's to 1e-5, finite gradients, bitwise the same on a second run (the gradient itself
+    is ill-conditioned here in every implementation, module docstring)."""
+    import fet_ode_amd as F
+    from fet_ode_amd.dopri5 import ResidentSolve, set_resident_dopri5_training
+    from oracle import torch_ref as O
+    _, soln = O.lotka_volterra_truth()
+    target = torch.tensor(soln, dtype=torch.float32)[:35].to(dev)
+    tl = torch.tensor(np.linspace(0, 3.5, 35))
+    res = []
+    for resident in (True, True, False):
+        m, _ = _model("kanfet", dev)
+        prev = set_resident_dopri5_training(resident)
+        try:
+            pred = F.odeint(F.autonomous(m), torch.tensor([[1.0, 1.0]], device=dev), tl)
+            assert isinstance(F.dopri5.dopri5_solve.last, ResidentSolve) == resident
+            loss = torch.mean((pred[:, 0, :] - target) ** 2)
+            loss.backward()
+        finally:
+            set_resident_dopri5_training(prev)
+        res.append((loss.item(), [p.grad.cpu() for p in m.parameters()]))
+    (l0, g0), (l1, g1), (lh, _) = res
+    assert l0 == l1 and all(torch.equal(a, b) for a, b in zip(g0, g1))
+    assert all(torch.isfinite(a).all() for a in g0)
+    assert abs(l0 - lh) <= 1e-5 * abs(lh), (l0, lh)
+
+
+def test_dopri5_train_bench_batch(dev):
+    """B = 4096 (the bench batch, every workgroup of the sweep resident), rtol 1e-3: the KAN field
+    against host autograd; the KAN-FET field finite and bitwise reproducible."""
+    t = torch.tensor(np.linspace(0, 1.0, 11))
+    r0 = _run("kan", dev, 4096, t, 1e-3, 1e-4, True)
+    r1 = _run("kan", dev, 4096, t, 1e-3, 1e-4, False)
+    assert r0[4] == r1[4]
+    for n in r1[1]:
+        assert _rel(r0[1][n], r1[1][n]) <= 1e-3, n
+    a = _run("kanfet", dev, 4096, t, 1e-3, 1e-4, True)
+    b = _run("kanfet", dev, 4096, t, 1e-3, 1e-4, True)
+    assert a[0] == b[0] and all(torch.equal(a[1][n], b[1][n]) for n in a[1])
+    assert all(torch.isfinite(v).all() for v in a[1].values())
