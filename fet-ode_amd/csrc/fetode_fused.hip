@@ -1365,9 +1365,198 @@ const FusedEntry* find_fused(const fetode_field_t* f) {
   return nullptr;
 }
 
+// =============================================================================================
+// fieldn: the single-launch integrator for depth-2 fields of OTHER widths — [D, H, D] with
+// D <= 8, H <= 64 (KAN or KAN-FET, any K / NB, cubic splines): one trajectory per wave, lane o =
+// hidden unit o.  Per evaluation, lane o forms h_o from the D layer inputs (their features are
+// recomputed on every lane: D is small) and then its own input's features and contributions to
+// all D outputs; a butterfly sum over the lanes gives k.  The arithmetic is the fused kernels'
+// (the same plan and element formulas), the sums run in another order.  Inference only: training
+// tapes, the resident dopri5 and the fused backward exist for the specialised [2, 10, 2] shapes.
+// =============================================================================================
+constexpr int kFnMaxD = 8, kFnMaxH = 64;
+constexpr int kFnWaves = 4;
+// one wave's LDS traffic lands in issue order: a compiler barrier + a wait replaces the workgroup barrier
+__device__ __forceinline__ void fn_wsync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__device__ __forceinline__ float fn_sig_l2(float zl) { return rcp(1.0f + ex2(zl)); }  // 1/(1+2^zl)
+
+// KAN edge (o, i) + the Ferro elements (o, i, k) of one layer at input x (gate weight w)
+template <bool FERRO>
+__device__ __forceinline__ float fn_edge(const float* __restrict__ plan, const LayerPlan& P, int o, int i, float x,
+                                         float sx, float w, int mfix, float u) {
+  const float* kw = plan + P.kw + ((int64_t)o * P.in + i) * P.NFL;
+  float v = kw[0] * sx;
+  const float* lg = plan + P.lg + 2 * (int64_t)i * P.NB;
+  for (int j = 0; j < P.NB; ++j) v = ffma(kw[1 + j], fn_sig_l2(ffma(lg[2 * j], x, lg[2 * j + 1])), v);
+  const float4 cf = *reinterpret_cast<const float4*>(plan + P.sp + (((int64_t)o * P.in + i) * (P.NI + 1) + mfix) * 4);
+  v += ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
+  if constexpr (FERRO) {
+    const int64_t e0 = (int64_t)o * P.in * P.K + (int64_t)i * P.K;
+    const float* GEc = plan + P.fe_GEc + e0;
+    const float* k2 = plan + P.fe_k2 + e0;
+    const float* kE = plan + P.fe_k2Ec + e0;
+    const float* cp = plan + P.fe_CPs2 + e0;
+    const float gx = P.gsl2e * x;
+    for (int k = 0; k < P.K; ++k) {
+      const float s = rcp(ex2(gx + GEc[k]) + 1.0f);       // sigma(gs(-x - Ec))
+      const float m = ffma(w, s, 1.0f);                    // branch momentum (branch_sign = 1)
+      const float z = ffma(kE[k], m, k2[k] * x);
+      const float th = ffma(rcp(ex2(z) + 1.0f), -2.0f, 1.0f);
+      v = ffma(cp[k], th, v);
+    }
+  }
+  return v;
+}
+
+// knot interval of x on input i's grid (m = NI: off the grid, the zero row) and its coordinate u
+__device__ __forceinline__ void fn_interval(const float* __restrict__ plan, const LayerPlan& P, int i, float x, int& mfix,
+                                            float& u) {
+  const float* g = plan + P.knots + (int64_t)i * P.NG;
+  int m = -1;
+  for (int j = 0; j < P.NG; ++j) m += x >= g[j] ? 1 : 0;
+  const bool fin = __builtin_isfinite(x);
+  mfix = ((unsigned)m < (unsigned)P.NI && fin) ? m : P.NI;
+  u = mfix < P.NI ? (x - g[mfix]) * plan[P.rh + (int64_t)i * P.NI + mfix] : (fin ? 0.0f : __builtin_nanf(""));
+}
+
+template <bool FERRO>
+__global__ __launch_bounds__(64 * kFnWaves) void fieldn_kernel(FusedArgs a) {
+  __shared__ float s_x[kFnWaves][kFnMaxD], s_k[kFnWaves][kFnMaxD], s_p0[kFnWaves][kFnMaxD];
+  const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * kFnWaves + wid;
+  const bool valid = b < a.B;
+  const LayerPlan& P0 = a.P0;
+  const LayerPlan& P1 = a.P1;
+  const int D = P0.in, H = P0.out;
+  const float* __restrict__ plan = a.plan;
+  float* xs = s_x[wid];
+  float* ks = s_k[wid];
+  float* p0 = s_p0[wid];
+  const bool hl = lane < H;  // this lane's hidden unit
+  float prev1 = 0.f;
+  if (FERRO && valid) {
+    if (lane < D) p0[lane] = a.state[b * D + lane];
+    if (hl) prev1 = a.state[a.B * D + b * H + lane];
+  }
+  bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
+  const float c0o = hl ? plan[P0.fconst + lane] : 0.f;
+  auto eval = [&](void) {  // xs -> ks (all lanes), hysteresis states updated
+    fn_wsync();
+    // layer 0: h_o
+    float h = 0.f;
+    if (hl) {
+      h = c0o;
+      for (int i = 0; i < D; ++i) {
+        const float x = xs[i];
+        const float sx = x * fn_sig_l2(-x * FETODE_LOG2E);
+        float w = 0.f;
+        if constexpr (FERRO) w = ffma(fn_sig_l2(-P0.gsl2e * (x - (re0 ? x : p0[i]))), -P0.wc, P0.wc);
+        int mfix;
+        float u;
+        fn_interval(plan, P0, i, x, mfix, u);
+        h += fn_edge<FERRO>(plan, P0, lane, i, x, sx, w, mfix, u);
+      }
+    }
+    fn_wsync();
+    if (FERRO && lane < D) p0[lane] = xs[lane];  // ferro_class.py:409
+    re0 = false;
+    // layer 1: lane o's contributions to every output, then the sum over the lanes
+    float w1 = 0.f, sh = 0.f, u1 = 0.f;
+    int m1 = 0;
+    if (hl) {
+      sh = h * fn_sig_l2(-h * FETODE_LOG2E);
+      if constexpr (FERRO) w1 = ffma(fn_sig_l2(-P1.gsl2e * (h - (re1 ? h : prev1))), -P1.wc, P1.wc);
+      fn_interval(plan, P1, lane, h, m1, u1);
+    }
+    if (FERRO) prev1 = h;
+    re1 = false;
+    for (int d = 0; d < D; ++d) {
+      float v = hl ? fn_edge<FERRO>(plan, P1, d, lane, h, sh, w1, m1, u1) : 0.f;
+#pragma unroll
+      for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s);
+      if (lane == 0) ks[d] = v + plan[P1.fconst + d];
+    }
+    fn_wsync();
+  };
+  // lane d < D carries state dim d
+  const bool dl = lane < D;
+  float y = (valid && dl) ? a.y0[b * D + lane] : 0.f;
+  if (a.single_eval) {
+    if (dl) xs[lane] = y;
+    eval();
+    if (valid && dl) a.eval_out[b * D + lane] = ks[lane];
+  } else {
+    if (valid && dl) a.solution[b * D + lane] = y;
+    const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4 : a.method == FETODE_MIDPOINT ? 2 : 1;
+    const float third = 1.0f / 3.0f;
+    int jj = 1;
+    for (int s = 0; s < a.n_steps; ++s) {
+      const float dt = a.step_coef[4 * s], hh = a.step_coef[4 * s + 1], h6 = a.step_coef[4 * s + 2];
+      float k1 = 0.f, k2 = 0.f, k3 = 0.f, k4 = 0.f;
+      for (int st = 0; st < ns; ++st) {  // fused4's generic path, same op order
+        float xin = y;
+        if (a.method == FETODE_RK4) {
+          if (st == 1) xin = y + (dt * k1) * third;
+          else if (st == 2) xin = y + dt * (k2 - k1 * third);
+          else if (st == 3) xin = y + dt * ((k1 - k2) + k3);
+        } else if (a.method == FETODE_RK4_CLASSIC) {
+          if (st == 1) xin = y + hh * k1;
+          else if (st == 2) xin = y + hh * k2;
+          else if (st == 3) xin = y + dt * k3;
+        } else if (a.method == FETODE_MIDPOINT) {
+          if (st == 1) xin = y + k1 * hh;
+        }
+        if (dl) xs[lane] = xin;
+        eval();
+        const float kk = dl ? ks[lane] : 0.f;
+        if (st == 0) k1 = kk;
+        else if (st == 1) k2 = kk;
+        else if (st == 2) k3 = kk;
+        else k4 = kk;
+      }
+      float y1;
+      if (a.method == FETODE_RK4) y1 = y + (((k1 + 3.0f * (k2 + k3)) + k4) * dt) * 0.125f;
+      else if (a.method == FETODE_RK4_CLASSIC) y1 = y + h6 * (((k1 + 2.0f * k2) + 2.0f * k3) + k4);
+      else if (a.method == FETODE_MIDPOINT) y1 = y + dt * k2;
+      else y1 = y + dt * k1;
+      for (; jj < a.T && a.out_step[jj] == s; ++jj) {
+        const int mode = a.out_mode[jj];
+        const float v = mode == 0 ? y : (mode == 1 ? y1 : y + a.out_slope[jj] * (y1 - y));
+        if (valid && dl) a.solution[((int64_t)jj * a.B + b) * D + lane] = v;
+      }
+      y = y1;
+    }
+  }
+  if (FERRO && valid) {
+    if (dl) a.state[b * D + lane] = p0[lane];
+    if (hl) a.state[a.B * D + b * H + lane] = prev1;
+  }
+}
+
+// the shapes fieldn serves (any other depth-2 [D, H, D] field of the fused kernels' basis shape)
+bool fieldn_supported(const fetode_field_t* f) {
+  if (f->n_layers != 2) return false;
+  const fetode_kanlinear_t &k0 = f->kan[0], &k1 = f->kan[1];
+  if (k0.in_features < 1 || k0.in_features > kFnMaxD || k1.out_features != k0.in_features ||
+      k1.in_features != k0.out_features || k0.out_features < 1 || k0.out_features > kFnMaxH)
+    return false;
+  if (k0.spline_order != 3 || k1.spline_order != 3 || k0.grid_size != k1.grid_size) return false;
+  if (f->ferro && (f->ferro[0].branch_sign || f->ferro[1].branch_sign)) return false;
+  return true;
+}
+
 int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
   const FusedEntry* e = find_fused(f);
-  if (!e) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
+  if (!e) {  // other widths: the generic single-launch kernel (inference and single evaluations)
+    if (!fieldn_supported(f) || a.tape) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
+    layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
+    layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
+    hipLaunchKernelGGL(f->ferro ? fieldn_kernel<true> : fieldn_kernel<false>, dim3(nblk(a.B, kFnWaves)),
+                       dim3(64 * kFnWaves), 0, (hipStream_t)stream, a);
+    LAUNCH_CHECK();
+    return FETODE_OK;
+  }
   layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
   layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
   static const float limit = [] {
@@ -1403,7 +1592,7 @@ int64_t fetode_fused_set_small_batch_max(int64_t b) {
 
 int fetode_fused_supported(const fetode_field_t* f) {
   if (validate_field(f) != FETODE_OK) return 0;
-  return find_fused(f) != nullptr;
+  return find_fused(f) != nullptr || fieldn_supported(f);
 }
 
 int fetode_field_forward(const fetode_field_t* f, const void* plan, const float* x, int64_t B,
