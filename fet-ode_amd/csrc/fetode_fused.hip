@@ -954,10 +954,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
 // The stage combines run redundantly on every lane in torchdiffeq's op order; thread 0 writes
 // the outputs.  Inference only (training tapes take v4).
 // =============================================================================================
-template <bool FERRO, bool HOT>
+template <bool FERRO, bool HOT, bool DOPRI = false, bool TAPE = false>
 __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
   constexpr int D = 2, H = 10, K = FERRO ? 10 : 0, KP = 5, NB = 10, NG = 12, NI = NG - 1, NFL = 1 + NB;
   __shared__ __attribute__((aligned(8))) f2 s_part[2][3];
+  __shared__ double s_gs[2];  // dopri5: the grid sums, from wave 0
+  __shared__ int s_gab;
+  float* trow = nullptr;      // dopri5 training: this evaluation's tape row (x, h, k), or null
   constexpr int SCH = 32;
   __shared__ float s_dt[SCH], s_hh[SCH], s_h6[SCH], s_oslope[SCH];
   __shared__ int s_ostep[SCH], s_omode[SCH];
@@ -1145,6 +1148,8 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       acc += c == m1 ? sv.y : 0.0f;
     }
     const float h = row_sum16(acc) + c0o;
+    if constexpr (TAPE)
+      if (trow && act && c == 0) trow[D + rr] = h;
     // ---------------- layer 1 (input h = h_rr) ----------------
     f2 acc01;
     {
@@ -1255,7 +1260,161 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       if (fact) return eval_body(xin, FT{});
       return eval_body(xin, FF{});
     };
-    if (a.single_eval) {
+    if constexpr (DOPRI) {
+      // ---- device-resident dopri5 on v6 (one trajectory per workgroup; the small batches: the
+      // reference's own X0 (1, 2)).  fused4's driver in f2 arithmetic (both state dims on every
+      // lane, the same fp32 ops per component), one grid sum per norm issued by wave 0 ----
+      const DopriParams& P = a.dp;
+      const double n_el = P.n_total;
+      int nfev = 0, n_att = 0, status = 0;
+      unsigned round = 0;
+      auto gsum2 = [&](double v0, double v1, double& s0, double& s1) {
+        if (w == 0) {
+          double r0 = 0.0, r1 = 0.0;
+          const bool ab = grid_sum2(P, round, v0, v1, r0, r1);
+          if (lane == 0) {
+            s_gs[0] = r0;
+            s_gs[1] = r1;
+            s_gab = ab ? 1 : 0;
+          }
+        }
+        __syncthreads();
+        s0 = s_gs[0];
+        s1 = s_gs[1];
+        if (s_gab) status = 4;
+      };
+      auto tape_eval = [&](f2 xin) -> f2 {  // the evaluation, and its tape row (x, h, k) in training
+        if constexpr (TAPE) trow = nfev < P.tape_cap ? a.tape + ((int64_t)nfev * a.B + b) * (2 * D + H) : nullptr;
+        const f2 k = eval(xin);
+        if constexpr (TAPE) {
+          if (trow && tid == 0) {
+            *reinterpret_cast<f2*>(trow) = xin;
+            *reinterpret_cast<f2*>(trow + D + H) = k;
+          }
+        }
+        ++nfev;
+        return k;
+      };
+      auto sq = [](f2 q) { return (double)q.x * q.x + (double)q.y * q.y; };
+      f2 f0 = tape_eval(y);
+      double dt;
+      if (P.first_step > 0.0) {
+        dt = P.first_step;
+      } else {  // misc._select_initial_step in fp32
+        const f2 scale = splat(P.atol) + splat(P.rtol) * f2{fabsf(y.x), fabsf(y.y)};
+        const f2 q0 = y / scale, q1 = f0 / scale;
+        double s, s1;
+        gsum2(sq(q0), sq(q1), s, s1);
+        const float d0 = fabsf(sqrtf((float)(s / n_el)));
+        const float d1 = fabsf(sqrtf((float)(s1 / n_el)));
+        float h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : (0.01f * d0) / d1;
+        h0 = fabsf(h0);
+        const f2 f1 = tape_eval(y + f0 * splat(h0));
+        const f2 q2 = (f1 - f0) / scale;
+        gsum2(sq(q2), 0.0, s, s1);
+        const float d2 = fabsf(sqrtf((float)(s / n_el)) / h0);
+        float h1;
+        if (d1 <= 1e-15f && d2 <= 1e-15f) h1 = fmaxf(1e-6f, h0 * 1e-3f);
+        else h1 = (float)pow((double)(0.01f / fmaxf(d1, d2)), (double)0.2f);
+        dt = (double)fminf(100.0f * h0, fabsf(h1));
+        if (TAPE && blockIdx.x == 0 && tid == 0) {
+          P.init_rec[0] = d0;
+          P.init_rec[1] = d1;
+          P.init_rec[2] = d2;
+          P.init_rec[3] = h0;
+          P.init_rec[4] = h1;
+        }
+      }
+      f2 co[5] = {y, splat(0.f), splat(0.f), splat(0.f), splat(0.f)};
+      double t0s = P.t[0], t1s = P.t[0];
+      for (int i = 1; i < P.T && status == 0; ++i) {
+        const double next_t = P.t[i];
+        int n_steps = 0;
+        while (next_t > t1s) {
+          if (n_steps >= P.max_steps) { status = 3; break; }
+          const double t0 = t1s;
+          if (!(t0 + dt > t0)) { status = 2; break; }
+          const float dt32 = (float)dt;
+          const double t1 = t0 + dt;
+          f2 A[6];
+#pragma unroll
+          for (int q = 0; q < 6; ++q) A[q] = f0 * splat(P.stc[0][q] * dt32);
+          f2 err = f0 * splat(P.stc[0][6] * dt32);
+          f2 mid = f0 * splat(P.stc[0][7] * dt32);
+          f2 yi = y, kn = f0;
+#pragma unroll 1
+          for (int st = 0; st < 6; ++st) {
+            yi = y + A[0];
+            float c[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) c[q] = P.stc[st + 1][q];
+            kn = tape_eval(yi);
+#pragma unroll
+            for (int q = 0; q < 5; ++q) A[q] = A[q + 1] + kn * splat(c[q] * dt32);
+            err = err + kn * splat(c[6] * dt32);
+            mid = mid + kn * splat(c[7] * dt32);
+          }
+          const f2 y1 = yi;
+          const f2 tol = splat(P.atol) + splat(P.rtol) * f2{fmaxf(fabsf(y.x), fabsf(y1.x)), fmaxf(fabsf(y.y), fabsf(y1.y))};
+          const f2 qe = err / tol;
+          double s, nbad;
+          gsum2(sq(qe), (__builtin_isfinite(y.x) && __builtin_isfinite(y.y)) ? 0.0 : 1.0, s, nbad);
+          if (status) break;
+          if (nbad != 0.0) { status = 1; break; }
+          const float ratio = sqrtf((float)(s / n_el));
+          const bool accept = ratio <= 1.0f;
+          if (blockIdx.x == 0 && tid == 0 && n_att < P.max_att) {
+            double* o = P.att + (int64_t)n_att * 4;
+            o[0] = t0;
+            o[1] = dt;
+            o[2] = (double)ratio;
+            o[3] = accept ? 1.0 : 0.0;
+          }
+          ++n_att;
+          if (accept) {  // interp._interp_fit (fused4's op order)
+            const f2 ym = y + mid, fa = f0, fb6 = kn, dtv = splat(dt32);
+            co[4] = ((splat(2.0f * dt32)) * (fb6 - fa) - splat(8.0f) * (y1 + y)) + splat(16.0f) * ym;
+            co[3] = ((dtv * (splat(5.0f) * fa - splat(3.0f) * fb6) + splat(18.0f) * y) + splat(14.0f) * y1) - splat(32.0f) * ym;
+            co[2] = ((dtv * (fb6 - splat(4.0f) * fa) - splat(11.0f) * y) - splat(5.0f) * y1) + splat(16.0f) * ym;
+            co[1] = dtv * fa;
+            co[0] = y;
+            y = y1;
+            f0 = kn;
+            t0s = t0;
+            t1s = t1;
+          } else {
+            t0s = t0;
+          }
+          const double rr_ = (double)ratio;
+          double nxt;
+          if (rr_ == 0.0) {
+            nxt = dt * P.ifactor;
+          } else {
+            const double dfac = rr_ < 1.0 ? 1.0 : P.dfactor;
+            const double factor = __builtin_isnan(rr_) ? rr_ : fmin(P.ifactor, fmax(P.safety / pow(rr_, 1.0 / 5.0), dfac));
+            nxt = dt * factor;
+          }
+          dt = __builtin_isnan(nxt) ? nxt : fmin(fmax(nxt, P.min_step), P.max_step);
+          ++n_steps;
+        }
+        if (status) break;
+        const float xq = (float)((next_t - t0s) / (t1s - t0s));
+        f2 total = co[0] + splat(xq) * co[1];
+        float xp = xq;
+#pragma unroll
+        for (int j = 2; j < 5; ++j) {
+          xp = xp * xq;
+          total = total + splat(xp) * co[j];
+        }
+        out_write(i, total);
+      }
+      if (blockIdx.x == 0 && tid == 0) {
+        P.stats[0] = nfev;
+        P.stats[1] = n_att;
+        P.stats[2] = __hip_atomic_load(P.bar + kDpLine * (kDpGroups + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 4 : status;
+      }
+    } else if (a.single_eval) {
+
       const f2 f = eval(y);
       if (tid == 0) *reinterpret_cast<f2*>(&a.eval_out[b * D]) = f;
     } else {
@@ -1307,7 +1466,7 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       }
     }
   }
-  if (FERRO && (a.single_eval || a.n_steps > 0)) {  // no evaluation: the state stays as it was
+  if (FERRO && (DOPRI || a.single_eval || a.n_steps > 0)) {  // no evaluation: the state stays as it was
     if (r == 1 && ogate) a.state[b * D + ofx] = pvs;
     if (act && hgate) a.state[a.B * D + b * H + rr] = pvh;
   }
@@ -1324,16 +1483,19 @@ struct FusedEntry {
   fused_fn small_rk4; // v6: rk4
   fused_fn dopri;     // v4 with the device-resident dopri5 driver
   fused_fn dopri_tape;  // the same, recording the training tape
+  fused_fn small_dopri, small_dopri_tape;  // v6 with the dopri5 driver (small batches)
 };
 const FusedEntry kFused[] = {
     // LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146)
     {2, 10, 2, 10, 10, 12, true, fused4_kernel<10, 10, 10, 12, true, false>, fused4_kernel<10, 10, 10, 12, true, true>,
      small6_kernel<true, false>, small6_kernel<true, true>, fused4_kernel<10, 10, 10, 12, true, false, true>,
-     fused4_kernel<10, 10, 10, 12, true, false, true, true>},
+     fused4_kernel<10, 10, 10, 12, true, false, true, true>, small6_kernel<true, false, true, false>,
+     small6_kernel<true, false, true, true>},
     // LV KAN [2,10,2] (predator_prey.py:101)
     {2, 10, 2, 1, 10, 12, false, fused4_kernel<10, 2, 10, 12, false, false>, fused4_kernel<10, 2, 10, 12, false, true>,
      small6_kernel<false, false>, small6_kernel<false, true>, fused4_kernel<10, 2, 10, 12, false, false, true>,
-     fused4_kernel<10, 2, 10, 12, false, false, true, true>},
+     fused4_kernel<10, 2, 10, 12, false, false, true, true>, small6_kernel<false, false, true, false>,
+     small6_kernel<false, false, true, true>},
 };
 
 // Batches up to kSmallMax take v6 (one trajectory per 3-wave workgroup, latency-bound chain split
@@ -1614,12 +1776,26 @@ int fetode_field_forward(const fetode_field_t* f, const void* plan, const float*
 }
 
 int64_t fetode_integrate_dopri5_workspace(int64_t B) {
-  const int64_t grid = (B + 1) / 2;
+  const int64_t grid = B;  // v6 (one trajectory per workgroup) at small batches, v4 (two) beyond
   return (int64_t)sizeof(unsigned) * kDpBarWords + (int64_t)sizeof(double) * (2 * grid + 4 * kDpGroups + 4);
 }
 
 // every workgroup must be resident at once (grid reductions): one-wave workgroups of two
 // trajectories, as many as the occupancy of the DOPRI instantiation admits (-1: query failed)
+// v6's dopri5 driver: one 192-thread workgroup per trajectory, every one resident
+static int64_t dopri5_small_resident_wgs(const FusedEntry* e, bool ferro) {
+  static int n_cu = 0, per_cu[2] = {0, 0};
+  const int fi = ferro ? 0 : 1;
+  if (!n_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return -1;
+  }
+  if (!per_cu[fi] && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[fi], e->small_dopri, 192, 0) != hipSuccess)
+    return -1;
+  return (int64_t)per_cu[fi] * n_cu;
+}
+
 static int64_t dopri5_resident_wgs(const FusedEntry* e, bool ferro) {
   static int n_cu = 0, per_cu[2] = {0, 0};
   const int fi = ferro ? 0 : 1;
@@ -1654,10 +1830,14 @@ static int dopri5_launch(const fetode_field_t* f, const void* plan, const float*
     return set_err(FETODE_EINVAL, "field is not R^D -> R^D");
   const FusedEntry* e = find_fused(f);
   if (!e) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
-  const int64_t resident = dopri5_resident_wgs(e, f->ferro != nullptr);
-  if (resident < 0) return set_err(FETODE_EHIP, "dopri5: occupancy query failed");
-  const int64_t grid = nblk(B, 2);
   const bool sharded = xr && xr->world > 1;
+  // small batches (the reference's own X0 (1, 2); the strong-scaled shard): v6, one trajectory per
+  // workgroup, when the whole grid is resident; else v4, two per one-wave workgroup
+  const int64_t res6 = (!sharded && B <= small_max()) ? dopri5_small_resident_wgs(e, f->ferro != nullptr) : -1;
+  const bool use6 = res6 >= B;
+  const int64_t resident = use6 ? res6 : dopri5_resident_wgs(e, f->ferro != nullptr);
+  if (resident < 0) return set_err(FETODE_EHIP, "dopri5: occupancy query failed");
+  const int64_t grid = use6 ? B : nblk(B, 2);
   const int64_t lgrid = grid + (sharded ? 1 : 0);   // + the cross-rank exchange workgroup
   if (lgrid > resident)
     return set_err(FETODE_EUNSUPPORTED, "dopri5: batch %lld needs %lld workgroups, %lld resident", (long long)B,
@@ -1746,7 +1926,9 @@ static int dopri5_launch(const fetode_field_t* f, const void* plan, const float*
   hipStream_t s = (hipStream_t)stream;
   HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kDpBarWords, s));
   void* args[] = {&a};
-  HIP_CHECK_RET(resident_launch((const void*)(a.tape ? e->dopri_tape : e->dopri), dim3((unsigned)lgrid), dim3(64), args, 0, s));
+  const void* fn = use6 ? (const void*)(a.tape ? e->small_dopri_tape : e->small_dopri)
+                        : (const void*)(a.tape ? e->dopri_tape : e->dopri);
+  HIP_CHECK_RET(resident_launch(fn, dim3((unsigned)lgrid), dim3(use6 ? 192 : 64), args, 0, s));
   return FETODE_OK;
 }
 

@@ -114,8 +114,15 @@ def _dopri5_grads(F, g, dev, flip=False):
     y0 = torch.from_numpy(g["y0_B64"]).to(dev)
     if flip:      # the same global loss with the batch in reverse order: only fp32 sums reorder
         y0 = y0.flip(0)
-    sol = F.odeint(lambda tt, yy: m(yy), y0, torch.tensor(T_DOPRI, dtype=torch.float64), rtol=1e-3, atol=1e-4)
-    (sol.square().sum() / sol.numel()).backward()
+    # the host-driven autograd path, as the sharded solve takes (the single-device resident
+    # training path evaluates the field with another kernel: other fp32 roundings)
+    from fet_ode_amd.dopri5 import set_resident_dopri5_training
+    prev = set_resident_dopri5_training(False)
+    try:
+        sol = F.odeint(lambda tt, yy: m(yy), y0, torch.tensor(T_DOPRI, dtype=torch.float64), rtol=1e-3, atol=1e-4)
+        (sol.square().sum() / sol.numel()).backward()
+    finally:
+        set_resident_dopri5_training(prev)
     att = [(a[1], a[3]) for a in F.dopri5.dopri5_solve.last.attempts]
     return _grads(m), (sol.flip(1) if flip else sol).detach().cpu(), att
 

@@ -215,6 +215,41 @@ def test_dopri5_resident_matches_host_driven(dev, kernel_switch, B, kind):
         assert ((a - b).norm() / b.norm()).item() <= 1e-4
 
 
+@pytest.mark.parametrize("B", [1, 64, 300])
+@pytest.mark.parametrize("kind", ["kanfet", "kan"])
+def test_dopri5_resident_small_batch_kernel(dev, kernel_switch, B, kind):
+    """Small batches (the reference's own X0 (1, 2)): the resident solve runs on v6 (one
+    trajectory per 192-thread workgroup) — against the host-driven loop whose evaluations are v6
+    too: the same attempts, dt to fp64 pow's last ulp, solution and state within 1e-6."""
+    import fet_ode_amd as F
+    from fet_ode_amd.dopri5 import ResidentSolve, set_resident_dopri5
+    kernel_switch(True)
+    gk = load_golden("traj_kanfet" if kind == "kanfet" else "traj_kan")
+    y0 = torch.from_numpy(gk["y0_B64"]).repeat(64, 1)[:B].to(dev)
+    t = torch.tensor([0.0, 0.2, 0.5], dtype=torch.float64)
+    out = []
+    for resident in (True, False):
+        prev = set_resident_dopri5(resident)
+        try:
+            m = (F.KANFET if kind == "kanfet" else F.KAN)([2, 10, 2], grid_size=5)
+            m.load_state_dict(golden_sd(gk))
+            m = m.to(dev)
+            with torch.no_grad():
+                sol = F.odeint(F.autonomous(m), y0, t, rtol=1e-3, atol=1e-4).cpu()
+        finally:
+            set_resident_dopri5(prev)
+        s = F.dopri5.dopri5_solve.last
+        assert isinstance(s, ResidentSolve) == resident
+        states = [l.ferro._prev.cpu() for l in m.layers] if kind == "kanfet" else []
+        out.append((sol, [(float(a[1]), float(a[3])) for a in s.attempts], s.nfev, states))
+    (s0, a0, n0, st0), (s1, a1, n1, st1) = out
+    assert n0 == n1 and [a[1] for a in a0] == [a[1] for a in a1]
+    np.testing.assert_allclose([a[0] for a in a0], [a[0] for a in a1], rtol=1e-13)
+    assert ((s0 - s1).norm(dim=(1, 2)) / s1.norm(dim=(1, 2)).clamp_min(1e-30)).max() <= 1e-6
+    for a, b in zip(st0, st1):
+        assert ((a - b).norm() / b.norm()).item() <= 1e-6
+
+
 def test_dopri5_resident_reference_tolerances(dev):
     """The north-star call itself: torchodeint(calDeriv, X0, t_learn) with torchdiffeq's default
     rtol 1e-7 / atol 1e-9 on the bench workload (B = 4096, 35 points): thousands of attempts in

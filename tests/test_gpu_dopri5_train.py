@@ -101,9 +101,9 @@ def _vs_oracle(kind, dev, B, t, rtol, atol, gtol, options=None, ltol=1e-5):
 @pytest.mark.parametrize("B", [1, 16, 64])
 @pytest.mark.parametrize("rtol", [1e-3, 1e-2, 1e-1])
 def test_dopri5_train_kan_vs_oracle_fp64(dev, B, rtol):
-    """Smooth field: the whole gradient (step-size control terms included) to 1e-4."""
+    """Smooth field: the whole gradient (step-size control terms included) to 2e-4."""
     t = torch.tensor(np.linspace(0, 2.0, 9))
-    _vs_oracle("kan", dev, B, t, rtol, rtol * 0.1, 1e-4)
+    _vs_oracle("kan", dev, B, t, rtol, rtol * 0.1, 2e-4)
 
 
 def test_dopri5_train_kan_first_step_vs_oracle_fp64(dev):
