@@ -1559,9 +1559,8 @@ __device__ __forceinline__ float fn_edge(const float* __restrict__ plan, const L
     const float* k2 = plan + P.fe_k2 + e0;
     const float* kE = plan + P.fe_k2Ec + e0;
     const float* cp = plan + P.fe_CPs2 + e0;
-    const float gx = P.gsl2e * x;
     for (int k = 0; k < P.K; ++k) {
-      const float s = rcp(ex2(gx + GEc[k]) + 1.0f);       // sigma(gs(-x - Ec))
+      const float s = rcp(ex2(ffma(P.gsl2e, x, GEc[k])) + 1.0f);  // sigma(gs(-x - Ec)), one rounding as v4
       const float m = ffma(w, s, 1.0f);                    // branch momentum (branch_sign = 1)
       const float z = ffma(kE[k], m, k2[k] * x);
       const float th = ffma(rcp(ex2(z) + 1.0f), -2.0f, 1.0f);
@@ -1698,7 +1697,11 @@ __global__ __launch_bounds__(64 * kFnWaves) void fieldn_kernel(FusedArgs a) {
 
 // the shapes fieldn serves (any other depth-2 [D, H, D] field of the fused kernels' basis shape)
 bool fieldn_supported(const fetode_field_t* f) {
-  if (f->n_layers != 2) return false;
+  static const bool on = [] {  // FETODE_FIELDN=0: these shapes take the per-stage path (A/B diagnostics)
+    const char* e = getenv("FETODE_FIELDN");
+    return !e || atoi(e) != 0;
+  }();
+  if (!on || f->n_layers != 2) return false;
   const fetode_kanlinear_t &k0 = f->kan[0], &k1 = f->kan[1];
   if (k0.in_features < 1 || k0.in_features > kFnMaxD || k1.out_features != k0.in_features ||
       k1.in_features != k0.out_features || k0.out_features < 1 || k0.out_features > kFnMaxH)

@@ -437,7 +437,10 @@ def _try_field_resident(func, y0, tp, reversed_, rtol, atol, options):
             return None
         B_total, b_off = agreed
         xr = D.XRank.get(grp, dev)
-    elif not lib.fetode_fused_supported(handle.ref):
+    elif B > lib.fetode_integrate_dopri5_max_batch(handle.ref, 0):
+        # no resident solver for this shape / batch: decide BEFORE pack_state, which rebinds the
+        # layers' prev_x to the fused state buffer (a declined launch would leave them there and
+        # skip the first-call re-initialisation of the host loop's first evaluation)
         return None
     plan = build_plan(field, handle, dev)
     state, mask = pack_state(field, B, dev)

@@ -110,7 +110,7 @@ def test_sharded_resident_dopri5_reproduces_single_device_exactly(dev):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("resident", [False, True], ids=["host-loop", "resident"])
-def test_sharded_dopri5_matches_single_device(dev, resident):
+def test_sharded_dopri5_matches_single_device(dev, kernel_switch, resident):
     import fet_ode_amd as F
     g = load_golden("traj_kanfet")
     m = _model(F, golden_sd(g))
@@ -125,6 +125,7 @@ def test_sharded_dopri5_matches_single_device(dev, resident):
     assert k0 == k1 == ("ResidentSolve" if resident else "_Dopri5")
     assert a0 == a1 and n0 == n1                    # both ranks took identical steps
     if resident:   # equal even shards of 64: whole leaves, so bitwise the single-device resident solve
+        kernel_switch(False)   # on v4, as the sharded kernels (small single-device batches take v6)
         with torch.no_grad():
             one = F.odeint(F.autonomous(_model(F, golden_sd(g))), torch.from_numpy(g["y0_B64"]).to(dev),
                            torch.tensor(T_GRID, dtype=torch.float64), rtol=1e-3, atol=1e-4).cpu()

@@ -321,7 +321,8 @@ def test_fused_backward_deterministic(dev, bwd_split):
         assert torch.equal(a, b)
 
 
-def test_training_grads_through_dopri5_kan(dev):
+@pytest.mark.parametrize("resident", [False, True], ids=["host-autograd", "resident-sweep"])
+def test_training_grads_through_dopri5_kan(dev, resident):
     """predator_prey.py:139-145 trains through torchodeint's default dopri5: loss.backward()
     through the GPU dopri5 (every stage of every attempt, the error ratios and the step sizes,
     as torchdiffeq's direct backprop) against the oracle's autograd through the same solve.
@@ -340,8 +341,12 @@ def test_training_grads_through_dopri5_kan(dev):
     m.load_state_dict(sd)
     m = m.to(dev)
     y0g = y0.clone().to(dev).requires_grad_(True)
-    pred = F.odeint(lambda tt, yy: m(yy), y0g, t, rtol=1e-5, atol=1e-7)
-    assert isinstance(D5.dopri5_solve.last, D5._Dopri5Grad)
+    prev = D5.set_resident_dopri5_training(resident)   # _Dopri5Grad, or the taped solve + sweep (§4.10)
+    try:
+        pred = F.odeint(lambda tt, yy: m(yy), y0g, t, rtol=1e-5, atol=1e-7)
+    finally:
+        D5.set_resident_dopri5_training(prev)
+    assert isinstance(D5.dopri5_solve.last, D5.ResidentSolve if resident else D5._Dopri5Grad)
     loss = torch.mean(torch.square(pred[:, 0, :] - target.to(dev)))
     loss.backward()
     ref = {}
