@@ -1669,6 +1669,8 @@ struct BwdEntry {
   bwd_fn adj, sum0, sum1;      // the split: adjoint sweep + per-layer parameter sums (or null)
   dopri_bwd_fn dopri;          // the reverse sweep of the resident dopri5 solve
   int dtpw;                    // its trajectories per wave (the whole batch is resident)
+  dopri_bwd_fn dopri1;         // the same, one trajectory per wave: half the VJP jobs per lane
+                               // (latency) where the batch leaves the grid room (small B)
 };
 const BwdEntry kBwd[] = {
     // LV KAN-FET [2,10,2]: one kernel, two trajectories per wave (measured: TPW 1 / 2 / 4 = 1034 / 897 /
@@ -1676,14 +1678,15 @@ const BwdEntry kBwd[] = {
 #ifdef FETODE_DIAG   // the split structure (measured slower) lives in the diagnostic build only
     {2, 10, 10, 10, 12, true, 2, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 2>,
      fixed_bwd_kernel<2, 10, 10, 10, 12, true, false, 1>, param_sum_kernel<2, 10, 10, 10, 12, 0>,
-     param_sum_kernel<2, 10, 10, 10, 12, 1>, dopri_bwd_kernel<2, 10, 10, 10, 12, true, 2>, 2},
+     param_sum_kernel<2, 10, 10, 10, 12, 1>, dopri_bwd_kernel<2, 10, 10, 10, 12, true, 2>, 2,
+     dopri_bwd_kernel<2, 10, 10, 10, 12, true, 1>},
 #else
     {2, 10, 10, 10, 12, true, 2, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 2>, nullptr, nullptr, nullptr,
-     dopri_bwd_kernel<2, 10, 10, 10, 12, true, 2>, 2},
+     dopri_bwd_kernel<2, 10, 10, 10, 12, true, 2>, 2, dopri_bwd_kernel<2, 10, 10, 10, 12, true, 1>},
 #endif
     // LV KAN [2,10,2] (126 VGPRs: four waves per SIMD already)
     {2, 10, 0, 10, 12, false, 1, fixed_bwd_kernel<2, 10, 1, 10, 12, false, true, 1>, nullptr, nullptr, nullptr,
-     dopri_bwd_kernel<2, 10, 1, 10, 12, false, 2>, 2},
+     dopri_bwd_kernel<2, 10, 1, 10, 12, false, 2>, 2, dopri_bwd_kernel<2, 10, 1, 10, 12, false, 1>},
 };
 // Which path the KAN-FET sweep takes (fetode_backward_set_split; env FETODE_BWD_SPLIT).  Default:
 // the one-kernel sweep — measured on MI355X at B = 4096, rk4, 34 steps: one kernel 1.06 ms vs the
@@ -1886,20 +1889,29 @@ int fetode_integrate_fixed_backward(const fetode_field_t* f, const void* plan, i
 
 // ---- reverse sweep of the resident dopri5 solve ----
 // every workgroup resident at once (one grid sum per attempt): the occupancy of the kernel
-static int64_t dopri_bwd_resident_wgs(const BwdEntry* e) {
+static int64_t dopri_bwd_resident_wgs(const BwdEntry* e, bool one = false) {
   static int n_cu = 0;
-  static int per_cu[2] = {0, 0};
-  const int fi = e->ferro ? 0 : 1;
+  static int per_cu[2][2] = {{0, 0}, {0, 0}};
+  const int fi = e->ferro ? 0 : 1, v = one ? 1 : 0;
   if (!n_cu) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return -1;
   }
-  if (!per_cu[fi] && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[fi], e->dopri, 64 * kTPB, 0) != hipSuccess)
+  if (!per_cu[fi][v] &&
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[fi][v], one ? e->dopri1 : e->dopri, 64 * kTPB, 0) != hipSuccess)
     return -1;
-  return (int64_t)per_cu[fi] * n_cu;
+  return (int64_t)per_cu[fi][v] * n_cu;
 }
-static int64_t dopri_bwd_grid(const BwdEntry* e, int64_t B) { return (B + kTPB * e->dtpw - 1) / (kTPB * e->dtpw); }
+// one trajectory per wave when that grid is resident (small batches), else e->dtpw
+static int dopri_bwd_tpw(const BwdEntry* e, int64_t B) {
+  if (e->dopri1 && (B + kTPB - 1) / kTPB <= dopri_bwd_resident_wgs(e, true)) return 1;
+  return e->dtpw;
+}
+static int64_t dopri_bwd_grid(const BwdEntry* e, int64_t B) {
+  const int tpw = dopri_bwd_tpw(e, B);
+  return (B + kTPB * tpw - 1) / (kTPB * tpw);
+}
 
 int64_t fetode_integrate_dopri5_backward_max_batch(const fetode_field_t* f) {
   if (validate_field(f) != FETODE_OK) return 0;
@@ -1939,7 +1951,8 @@ int fetode_integrate_dopri5_backward(const fetode_field_t* f, const void* plan, 
   const int base = opts[0] > 0.0 ? 1 : 2;
   if (n_att < 0 || n_ev != base + 6 * n_att)
     return set_err(FETODE_EINVAL, "dopri5 backward: %d evaluations do not match %d attempts", n_ev, n_att);
-  const int64_t resident = dopri_bwd_resident_wgs(e);
+  const bool one = dopri_bwd_tpw(e, B) == 1;
+  const int64_t resident = dopri_bwd_resident_wgs(e, one);
   if (resident < 0) return set_err(FETODE_EHIP, "dopri5 backward: occupancy query failed");
   const int64_t grid = dopri_bwd_grid(e, B);
   if (grid > resident)
@@ -2005,7 +2018,8 @@ int fetode_integrate_dopri5_backward(const fetode_field_t* f, const void* plan, 
   d.status = status;
   HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kDpBarWords, s));
   void* args[] = {&d};
-  HIP_CHECK_RET(resident_launch((const void*)e->dopri, dim3((unsigned)grid), dim3(64 * kTPB), args, 0, s));
+  HIP_CHECK_RET(resident_launch((const void*)(one ? e->dopri1 : e->dopri), dim3((unsigned)grid), dim3(64 * kTPB), args,
+                                0, s));
   const int64_t per = (nrow + nch - 1) / nch;
   hipLaunchKernelGGL(part_reduce_kernel, dim3(nblk(nacc, 64), (unsigned)nch), dim3(64), 0, s, part, nrow, nacc, per,
                      chunks);
