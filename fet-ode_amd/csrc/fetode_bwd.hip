@@ -1671,6 +1671,7 @@ struct BwdEntry {
   int dtpw;                    // its trajectories per wave (the whole batch is resident)
   dopri_bwd_fn dopri1;         // the same, one trajectory per wave: half the VJP jobs per lane
                                // (latency) where the batch leaves the grid room (small B)
+  bwd_fn fn1;                  // fn at one trajectory per wave (small B), or null
 };
 const BwdEntry kBwd[] = {
     // LV KAN-FET [2,10,2]: one kernel, two trajectories per wave (measured: TPW 1 / 2 / 4 = 1034 / 897 /
@@ -1679,14 +1680,15 @@ const BwdEntry kBwd[] = {
     {2, 10, 10, 10, 12, true, 2, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 2>,
      fixed_bwd_kernel<2, 10, 10, 10, 12, true, false, 1>, param_sum_kernel<2, 10, 10, 10, 12, 0>,
      param_sum_kernel<2, 10, 10, 10, 12, 1>, dopri_bwd_kernel<2, 10, 10, 10, 12, true, 2>, 2,
-     dopri_bwd_kernel<2, 10, 10, 10, 12, true, 1>},
+     dopri_bwd_kernel<2, 10, 10, 10, 12, true, 1>, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 1>},
 #else
     {2, 10, 10, 10, 12, true, 2, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 2>, nullptr, nullptr, nullptr,
-     dopri_bwd_kernel<2, 10, 10, 10, 12, true, 2>, 2, dopri_bwd_kernel<2, 10, 10, 10, 12, true, 1>},
+     dopri_bwd_kernel<2, 10, 10, 10, 12, true, 2>, 2, dopri_bwd_kernel<2, 10, 10, 10, 12, true, 1>,
+     fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 1>},
 #endif
     // LV KAN [2,10,2] (126 VGPRs: four waves per SIMD already)
     {2, 10, 0, 10, 12, false, 1, fixed_bwd_kernel<2, 10, 1, 10, 12, false, true, 1>, nullptr, nullptr, nullptr,
-     dopri_bwd_kernel<2, 10, 1, 10, 12, false, 2>, 2, dopri_bwd_kernel<2, 10, 1, 10, 12, false, 1>},
+     dopri_bwd_kernel<2, 10, 1, 10, 12, false, 2>, 2, dopri_bwd_kernel<2, 10, 1, 10, 12, false, 1>, nullptr},
 };
 // Which path the KAN-FET sweep takes (fetode_backward_set_split; env FETODE_BWD_SPLIT).  Default:
 // the one-kernel sweep — measured on MI355X at B = 4096, rk4, 34 steps: one kernel 1.06 ms vs the
@@ -1785,9 +1787,27 @@ int fetode_fused_backward_supported(const fetode_field_t* f) {
   return find_bwd(f) != nullptr;
 }
 
+// the one-kernel sweep at one trajectory per wave while those waves fit one resident round
+// (latency-bound small batches: half the VJP jobs per lane), else e->tpw
+int fixed_tpw(const BwdEntry* e, int64_t B) {
+  if (!e->fn1) return e->tpw;
+  static int64_t cap = -1;
+  if (cap < 0 && getenv("FETODE_BWD_TPW1") && atoi(getenv("FETODE_BWD_TPW1")) == 0) cap = 0;  // A/B knob
+  if (cap < 0) {
+    int dev = 0, n_cu = 0, per = 0;
+    cap = (hipGetDevice(&dev) == hipSuccess &&
+           hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+           hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, e->fn1, 64 * kTPB, 0) == hipSuccess)
+              ? (int64_t)per * n_cu * kTPB : 0;
+  }
+  // measured (tools/diag/bwd_small_time.py, rk4 iteration): B = 512 0.73 vs 0.93 ms, B = 2048 0.79 vs
+  // 0.75 ms — one trajectory per wave while at most half the resident waves are needed
+  return 2 * B <= cap ? 1 : e->tpw;
+}
+
 // partial rows of the chosen path: one per wave (one-kernel sweep) or per param_sum block (split)
 int64_t sum_rows(const BwdEntry* e, int64_t B, int64_t n_ev) {
-  if (!use_split(e)) return bwd_rows(B, e->tpw);
+  if (!use_split(e)) return bwd_rows(B, fixed_tpw(e, B));
   const int64_t tiles = (n_ev * B + kPsTS - 1) / kPsTS;
   return tiles < kSumBlocks ? (tiles > 0 ? tiles : 1) : kSumBlocks;
 }
@@ -1875,7 +1895,9 @@ int fetode_integrate_fixed_backward(const fetode_field_t* f, const void* plan, i
       HIP_CHECK_RET(hipMemsetAsync(part, 0, sizeof(float) * nrow * nacc, s));
     }
   } else {
-    hipLaunchKernelGGL(e->fn, dim3((unsigned)(nrow / kTPB)), dim3(64 * kTPB), 0, s, a);
+    // (an entry whose own sweep is one trajectory per wave has no fn1)
+    hipLaunchKernelGGL((e->fn1 && fixed_tpw(e, B) == 1) ? e->fn1 : e->fn, dim3((unsigned)(nrow / kTPB)), dim3(64 * kTPB),
+                       0, s, a);
     LAUNCH_CHECK();
   }
   const int64_t per = (nrow + nch - 1) / nch;
@@ -1905,7 +1927,8 @@ static int64_t dopri_bwd_resident_wgs(const BwdEntry* e, bool one = false) {
 }
 // one trajectory per wave when that grid is resident (small batches), else e->dtpw
 static int dopri_bwd_tpw(const BwdEntry* e, int64_t B) {
-  if (e->dopri1 && (B + kTPB - 1) / kTPB <= dopri_bwd_resident_wgs(e, true)) return 1;
+  // (as fixed_tpw: while the one-per-wave grid fills at most half of its resident capacity)
+  if (e->dopri1 && 2 * ((B + kTPB - 1) / kTPB) <= dopri_bwd_resident_wgs(e, true)) return 1;
   return e->dtpw;
 }
 static int64_t dopri_bwd_grid(const BwdEntry* e, int64_t B) {
