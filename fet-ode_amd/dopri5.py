@@ -503,7 +503,8 @@ def _t_device(tp, dev):
     return t_dev
 
 
-_TAPE_BYTES0 = 1 << 30   # first-call tape budget; later calls size the tape from the last solve
+_TAPE_BYTES0 = 1 << 30    # first-call tape budget; later calls size the tape from the last solve
+_TAPE_GUESS_MAX = 16 << 30  # a size learnt at another batch is capped here (a longer solve re-runs)
 
 
 class _FusedDopri5Fn(torch.autograd.Function):
@@ -530,6 +531,7 @@ class _FusedDopri5Fn(torch.autograd.Function):
         state0 = None if state is None else state.clone()
         per_ev = B * (2 * D + H) * 4
         cap, max_att = getattr(field, "_fetode_d5tape", (max(64, min(1 << 20, _TAPE_BYTES0 // per_ev)), 4096))
+        cap = max(64, min(cap, _TAPE_GUESS_MAX // per_ev))
         sol = torch.empty(T, B, D, device=dev, dtype=torch.float32)
         ws = torch.empty(max(1, lib.fetode_integrate_dopri5_workspace(B) // 4), device=dev, dtype=torch.float32)
         stats = torch.empty(3, device=dev, dtype=torch.int32)
@@ -605,7 +607,6 @@ class _FusedDopri5Fn(torch.autograd.Function):
             _lib.stream_handle(dev)), "fetode_integrate_dopri5_backward")
         _raise_status(int(status.item()), "fetode_integrate_dopri5_backward: a grid sum timed out (workgroups "
                                           "not co-resident); the gradients are invalid")
-        ctx.tape = None
         pgrads = [grads.get(id(p)) if w else None for p, w in zip(params, want)]
         return (None, None, gy0, None, None, None, None, *pgrads)
 
