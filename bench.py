@@ -379,6 +379,32 @@ def plain_closure_rate(model, y0d, t, reps=3):
                           "path": "closure_fusion(False): fetode_field_forward + fetode_rk_combine per stage"}}
 
 
+def synthetic_ecg(batch, T=96, seed=0):
+    """Synthetic ECG200-shaped series (the dataset is not in the image): a seeded sum of two
+    sinusoids + noise per row, z-normalised like the UCR files."""
+    g = torch.Generator().manual_seed(seed)
+    tt = torch.linspace(0, 1, T, dtype=torch.float64)
+    f = 1.0 + 3.0 * torch.rand(batch, 1, generator=g, dtype=torch.float64)
+    ph = 6.283185307179586 * torch.rand(batch, 1, generator=g, dtype=torch.float64)
+    x = torch.sin(6.283185307179586 * f * tt + ph) + 0.3 * torch.sin(18.84955592153876 * f * tt)
+    x = x + 0.1 * torch.randn(batch, T, generator=g, dtype=torch.float64)
+    x = (x - x.mean(dim=1, keepdim=True)) / x.std(dim=1, keepdim=True)
+    return x.to(torch.float32)
+
+
+def synthetic_mnist(batch, H=28, W=28, seed=0):
+    """Synthetic MNIST-shaped images in [0, 1] (the dataset is not in the image): a seeded ring per
+    image plus noise."""
+    g = torch.Generator().manual_seed(seed)
+    yy = torch.linspace(-1, 1, H, dtype=torch.float64).view(1, H, 1)
+    xx = torch.linspace(-1, 1, W, dtype=torch.float64).view(1, 1, W)
+    c = (torch.rand(batch, 2, 1, 1, generator=g, dtype=torch.float64) - 0.5)
+    r = 0.2 + 0.3 * torch.rand(batch, 1, 1, generator=g, dtype=torch.float64)
+    d = ((yy - c[:, 0]) ** 2 + (xx - c[:, 1]) ** 2).sqrt()
+    img = torch.exp(-((d - r) / 0.12) ** 2) + 0.05 * torch.rand(batch, H, W, generator=g, dtype=torch.float64)
+    return img.clamp(0, 1).to(torch.float32).unsqueeze(1)
+
+
 def ecg_rate(dev, reps=10, cpu_seconds=5.0, with_cpu=True, rtol=1e-3, atol=1e-4):
     """BASELINE configs[2] (train_ecg_kan_fet_nn_ode.py:512-572): KanFet_NODE.eval() forward on a
     batch of 200 synthetic ECG200-shaped series (T = 96; the dataset is not in the image), latent
@@ -387,12 +413,11 @@ def ecg_rate(dev, reps=10, cpu_seconds=5.0, with_cpu=True, rtol=1e-3, atol=1e-4)
     dopri5 solve is one device-resident launch (fetode_ecg_dopri5); the encoder / classifier are one
     launch each."""
     from fet_ode_amd import ecg
-    from oracle import ecg_ref as E
     torch.manual_seed(0)
     m = ecg.KanFet_NODE(T=96, num_classes=2, latent_dim=64, num_basis=10, rtol=rtol, atol=atol)
     sd = {k: v.clone() for k, v in m.state_dict().items()}
     m = m.to(dev).eval()
-    x = E.ecg_x(200, seed=1)
+    x = synthetic_ecg(200, seed=1)
     xd = x.to(dev)
     with torch.no_grad():
         for _ in range(2):
@@ -408,7 +433,8 @@ def ecg_rate(dev, reps=10, cpu_seconds=5.0, with_cpu=True, rtol=1e-3, atol=1e-4)
            "nfev": s.nfev, "attempts": len(s.attempts), "field_evals_per_s": s.nfev / el,
            "workload": f"KanFet_NODE(T=96, 2 classes, latent 64, nb 10), dopri5 rtol {rtol:g} atol {atol:g}, "
                        "t=[0,1], B=200 synthetic series, eval mode"}
-    if with_cpu:
+    if with_cpu:   # the oracle is the CPU leg only
+        from oracle import ecg_ref as E
         cores, _ = cpu_cores()
         torch.set_num_threads(cores)
         n, t0 = 0, time.perf_counter()
@@ -429,12 +455,11 @@ def mnist_rate(dev, batch=8192, reps=10, cpu_seconds=5.0, with_cpu=True):
     bases).  Forward images/s under no_grad and training images/s (forward + cross-entropy +
     backward of every parameter) on one GPU."""
     from fet_ode_amd import mnist
-    from oracle import mnist_ref as M
     torch.manual_seed(0)
     m = mnist.KuramotoKANClassifier()
     sd = {k: v.clone() for k, v in m.state_dict().items()}
     m = m.to(dev)
-    x = M.mnist_x(batch, seed=3)
+    x = synthetic_mnist(batch, seed=3)
     xd = x.to(dev)
     y = (torch.arange(batch) % 10).to(dev)
 
@@ -460,7 +485,8 @@ def mnist_rate(dev, batch=8192, reps=10, cpu_seconds=5.0, with_cpu=True):
            "ms_per_batch": fwd * 1e3, "train_images_per_s": batch / trn, "train_ms_per_batch": trn * 1e3,
            "workload": f"KuramotoKANClassifier(28x28, 10 Kuramoto steps, KANLinear 1568->10, nb 8), batch {batch}, "
                        "synthetic images"}
-    if with_cpu:
+    if with_cpu:   # the oracle is the CPU leg only
+        from oracle import mnist_ref as M
         cores, _ = cpu_cores()
         torch.set_num_threads(cores)
         ref = M.ClassifierRef(sd)
@@ -483,8 +509,6 @@ def ett_rate(dev, batch=8192, reps=2, substeps=4, cpu_seconds=5.0, with_cpu=True
     image), latent 64, KAN-FET latent field [64, 128, 64] (K=10), odeint_rk4 with the reference
     TrainConfig's rk4_substeps=4 over t_fut = 0..95.  Forward windows/s under no_grad on one GPU."""
     from fet_ode_amd import ett
-    from oracle import ett_ref as E
-    from oracle import torch_ref as O
     c = p = 96
     torch.manual_seed(0)
     m = ett.LatentNeuralODEForecaster(num_features=7, context_len=c, pred_len=p, latent_dim=64, solver="rk4")
@@ -509,6 +533,8 @@ def ett_rate(dev, batch=8192, reps=2, substeps=4, cpu_seconds=5.0, with_cpu=True
            "workload": f"LatentNeuralODEForecaster(7 features, 96->96, latent 64, KANFET[64,128,64] K=10), "
                        f"odeint_rk4 x{substeps} substeps ({steps} steps), batch {batch}, synthetic series"}
     if with_cpu:
+        from oracle import ett_ref as E
+        from oracle import torch_ref as O
         cores, _ = cpu_cores()
         torch.set_num_threads(cores)
         field = O.KANFETRef.from_state_dict({k[len("dynamics.net."):]: v for k, v in sd.items()
@@ -609,7 +635,6 @@ def ett_encoder_rate(dev, batch=8192, ctx=96, reps=20, with_cpu=True, cpu_second
     (the same launch with full = 1), and a training step (forward with tape + HIP VJP + the
     to_latent GEMMs)."""
     from fet_ode_amd import ett, _lib as L
-    from oracle import ett_ref as E
     torch.manual_seed(0)
     enc = ett.KANRNNEncoder(7, 64, 64, 10)
     sd = {k: v.clone() for k, v in enc.state_dict().items()}
@@ -680,6 +705,7 @@ def ett_encoder_rate(dev, batch=8192, ctx=96, reps=20, with_cpu=True, cpu_second
            "workload": f"KANRNNEncoder(7, hidden 64, latent 64, nb 10), context {ctx}, batch {batch}, synthetic series",
            "path": "fetode_kanrnn_forward (one launch, to_latent fused) / fetode_kanrnn_backward"}
     if with_cpu:
+        from oracle import ett_ref as E
         cores, _ = cpu_cores()
         torch.set_num_threads(cores)
         ref = E.KANRNNEncoderRef(sd)
