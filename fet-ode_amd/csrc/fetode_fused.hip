@@ -1217,6 +1217,13 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
   auto interp = [](int mode, f2 y0v, f2 y1v, float sl) -> f2 {
     return mode == 0 ? y0v : (mode == 1 ? y1v : y0v + splat(sl) * (y1v - y0v));
   };
+  // fixed-grid training tape (v6 at small batches): evaluation ev's row (x, h) of (n_evals, B, D + H)
+  auto tape_at = [&](int ev, f2 xin) __attribute__((always_inline)) {
+    if constexpr (TAPE && !DOPRI) {
+      trow = a.tape + ((int64_t)ev * a.B + b) * (D + H);
+      if (tid == 0) *reinterpret_cast<f2*>(trow) = xin;
+    }
+  };
   using FT = std::integral_constant<bool, true>;
   using FF = std::integral_constant<bool, false>;
 
@@ -1236,10 +1243,17 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
           load_outs(jj);
         }
         const f2 dt = splat(s_dt[s - sb]);
+        tape_at(4 * s, y);
         const f2 k1 = eval_body(y, fact_tag);
-        const f2 k2 = eval_body(y + (dt * k1) * third, fact_tag);
-        const f2 k3 = eval_body(y + dt * (k2 - k1 * third), fact_tag);
-        const f2 k4 = eval_body(y + dt * ((k1 - k2) + k3), fact_tag);
+        const f2 x2 = y + (dt * k1) * third;
+        tape_at(4 * s + 1, x2);
+        const f2 k2 = eval_body(x2, fact_tag);
+        const f2 x3 = y + dt * (k2 - k1 * third);
+        tape_at(4 * s + 2, x3);
+        const f2 k3 = eval_body(x3, fact_tag);
+        const f2 x4 = y + dt * ((k1 - k2) + k3);
+        tape_at(4 * s + 3, x4);
+        const f2 k4 = eval_body(x4, fact_tag);
         const f2 y1 = y + (((k1 + splat(3.0f) * (k2 + k3)) + k4) * dt) * splat(0.125f);
         while (jj < a.T) {
           if (jj - jb == SCH) {
@@ -1442,6 +1456,7 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
           } else if (a.method == FETODE_MIDPOINT) {
             if (st == 1) xin = y + k1 * hh;
           }
+          tape_at(s * ns + st, xin);
           const f2 kk = eval(xin);
           if (st == 0) k1 = kk;
           else if (st == 1) k2 = kk;
@@ -1484,18 +1499,21 @@ struct FusedEntry {
   fused_fn dopri;     // v4 with the device-resident dopri5 driver
   fused_fn dopri_tape;  // the same, recording the training tape
   fused_fn small_dopri, small_dopri_tape;  // v6 with the dopri5 driver (small batches)
+  fused_fn small_tape, small_rk4_tape;     // v6 recording the fixed-grid training tape
 };
 const FusedEntry kFused[] = {
     // LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146)
     {2, 10, 2, 10, 10, 12, true, fused4_kernel<10, 10, 10, 12, true, false>, fused4_kernel<10, 10, 10, 12, true, true>,
      small6_kernel<true, false>, small6_kernel<true, true>, fused4_kernel<10, 10, 10, 12, true, false, true>,
      fused4_kernel<10, 10, 10, 12, true, false, true, true>, small6_kernel<true, false, true, false>,
-     small6_kernel<true, false, true, true>},
+     small6_kernel<true, false, true, true>, small6_kernel<true, false, false, true>,
+     small6_kernel<true, true, false, true>},
     // LV KAN [2,10,2] (predator_prey.py:101)
     {2, 10, 2, 1, 10, 12, false, fused4_kernel<10, 2, 10, 12, false, false>, fused4_kernel<10, 2, 10, 12, false, true>,
      small6_kernel<false, false>, small6_kernel<false, true>, fused4_kernel<10, 2, 10, 12, false, false, true>,
      fused4_kernel<10, 2, 10, 12, false, false, true, true>, small6_kernel<false, false, true, false>,
-     small6_kernel<false, false, true, true>},
+     small6_kernel<false, false, true, true>, small6_kernel<false, false, false, true>,
+     small6_kernel<false, true, false, true>},
 };
 
 // Batches up to kSmallMax take v6 (one trajectory per 3-wave workgroup, latency-bound chain split
@@ -1730,8 +1748,9 @@ int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
   }();
   a.factor_limit = limit;
   const bool rk4 = !a.single_eval && a.method == FETODE_RK4;
-  if (!a.tape && a.B <= small_max()) {  // v6: one trajectory per 192-thread workgroup
-    hipLaunchKernelGGL(rk4 ? e->small_rk4 : e->small, dim3((unsigned)a.B), dim3(192), 0, (hipStream_t)stream, a);
+  if (a.B <= small_max()) {  // v6: one trajectory per 192-thread workgroup (training tapes too)
+    const fused_fn fn = a.tape ? (rk4 ? e->small_rk4_tape : e->small_tape) : (rk4 ? e->small_rk4 : e->small);
+    hipLaunchKernelGGL(fn, dim3((unsigned)a.B), dim3(192), 0, (hipStream_t)stream, a);
   } else {                              // v4: two trajectories per one-wave workgroup
     hipLaunchKernelGGL(rk4 ? e->fn_rk4 : e->fn, dim3(nblk(a.B, 2)), dim3(64), 0, (hipStream_t)stream, a);
   }
