@@ -952,7 +952,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
 //            over the wave's rows, and ONE workgroup barrier (per-wave partials in LDS, double-
 //            buffered by evaluation parity) give k on every lane.
 // The stage combines run redundantly on every lane in torchdiffeq's op order; thread 0 writes
-// the outputs.  Inference only (training tapes take v4).
+// the outputs.  TAPE = true also records the training tapes (fixed-grid rows (x, h) and the
+// dopri5 rows (x, h, k)) for B <= small_max(): the row owners write them
+// (tests/test_gpu_grad.py::test_small_batch_tape_matches_v4 checks v6 vs v4 tapes and gradients).
 // =============================================================================================
 template <bool FERRO, bool HOT, bool DOPRI = false, bool TAPE = false>
 __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {

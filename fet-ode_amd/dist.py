@@ -56,19 +56,6 @@ def shard(x: torch.Tensor, rank: Optional[int] = None, world_size: Optional[int]
     return x.narrow(dim, lo, hi - lo)
 
 
-def broadcast_parameters(module: torch.nn.Module, src: int = 0) -> None:
-    """Identical initial weights on every rank (one flat broadcast)."""
-    _, w = world()
-    if w == 1:
-        return
-    ps = list(module.parameters())
-    with torch.no_grad():
-        flat = torch._utils._flatten_dense_tensors([p.detach() for p in ps])
-        dist.broadcast(flat, src)
-        for p, f in zip(ps, torch._utils._unflatten_dense_tensors(flat, ps)):
-            p.copy_(f)   # through the Parameter: bumps its version, so cached plans rebuild
-
-
 def allreduce_gradients(params: Iterable[torch.nn.Parameter], average: bool = True,
                         weights: Optional[float] = None) -> None:
     """Sum (or average) the gradients of ``params`` over ranks in ONE flat all-reduce.
@@ -118,16 +105,26 @@ def _shared_flat(grads: List[torch.Tensor]) -> Optional[torch.Tensor]:
 
 
 def broadcast_parameters(module: torch.nn.Module, src: int = 0, group=None) -> None:
-    """Make every rank's parameters and buffers rank `src`'s, in place (what DDP does at
-    construction).  Needed before data-parallel training: the efficient_kan init the drop-ins
+    """Make every rank's parameters and persistent buffers rank `src`'s, in place (what DDP does
+    at construction).  Needed before data-parallel training: the efficient_kan init the drop-ins
     reproduce (curve2coeff's lstsq) is not bitwise reproducible across processes even with the
-    same seed, so ranks that each construct the model start from slightly different weights."""
+    same seed, so ranks that each construct the model start from slightly different weights.
+
+    Non-persistent buffers are per-rank state and are NOT broadcast: FerroelectricBasis' compact
+    hysteresis memory (`_prev`, `_bsign`, shape (B_local, in)) belongs to this rank's own
+    trajectories, and unequal shards would give the collective mismatched sizes.  Persistent
+    buffers a module lists in ``_rank_local_buffers`` are batch state too (the ECG hysteretic
+    LogisticBasis' prev_x / branch_state, rebound to (B, in, nb) per call) and stay local."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
         return
     nccl = dist.get_backend(group) == "nccl"
     dev = torch.device("cuda", torch.cuda.current_device()) if nccl else torch.device("cpu")
+    shared = list(module.parameters())
+    for mod in module.modules():
+        skip = set(mod._non_persistent_buffers_set) | set(getattr(mod, "_rank_local_buffers", ()))
+        shared += [b for n, b in mod.named_buffers(recurse=False) if n not in skip and b is not None]
     with torch.no_grad():
-        for t in list(module.parameters()) + list(module.buffers()):
+        for t in shared:
             buf = t.detach() if t.device == dev else t.detach().to(dev)
             dist.broadcast(buf, src=src, group=group)
             if buf is not t:

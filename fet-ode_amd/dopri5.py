@@ -57,12 +57,15 @@ _RMS_WS = {}
 atexit.register(_RMS_WS.clear)
 
 
-def _rms_workspace(dev):
-    """The norms' multi-workgroup workspace (zeroed once; the kernel leaves it zero), one per device."""
-    ws = _RMS_WS.get(dev)
+def _rms_workspace(dev, stream):
+    """The norms' multi-workgroup workspace (zeroed once; the kernel leaves it zero): its partials
+    and last-arriver counter are reused by every launch, so one per (device, stream) — two solves
+    on different streams of one device must not interleave on the same counter."""
+    key = (dev, int(stream or 0))
+    ws = _RMS_WS.get(key)
     if ws is None:
         n = _lib.load().fetode_scaled_rms_workspace(0)
-        ws = _RMS_WS[dev] = torch.zeros(max(1, n // 8), device=dev, dtype=torch.float64)
+        ws = _RMS_WS[key] = torch.zeros(max(1, n // 8), device=dev, dtype=torch.float64)
     return ws
 
 
@@ -91,7 +94,7 @@ class _Dopri5:
         self.max_num_steps = int(options.get("max_num_steps", 2 ** 31 - 1))
         self.k = torch.empty(7, self.n, device=self.dev, dtype=torch.float32)
         self.scal = torch.empty(2, device=self.dev, dtype=torch.float32)
-        self.rms_ws = _rms_workspace(self.dev)
+        self.rms_ws = _rms_workspace(self.dev, self.stream)
         self.n_global = self.n
         if self.group is not None:
             import torch.distributed as dist
@@ -246,7 +249,12 @@ _TABLEAU = np.concatenate([np.concatenate([b, np.zeros(6 - len(b), np.float32)])
 _RESIDENT_OPTS = {"first_step", "safety", "ifactor", "dfactor", "min_step", "max_step", "max_num_steps"}
 
 
-def _raise_status(status: int, timeout_msg: str):
+def _raise_status(status: int, timeout_msg: str, restore=None):
+    """torchdiffeq's assertions from a resident solver's status word.  Status 4 (a grid barrier
+    timed out: the workgroups were not co-resident) runs ``restore`` first, which puts the
+    hysteresis memory back to its pre-solve value, so the caller can retry on the host loop."""
+    if status == 4 and restore is not None:
+        restore()
     if status == 1:
         raise AssertionError("non-finite values in state `y`")
     if status == 2:
@@ -286,17 +294,30 @@ class deferred_status:
 def check_deferred():
     pending = list(_DEFERRED)
     _DEFERRED.clear()
-    for stats, msg in pending:
-        _raise_status(int(stats[2].item()), msg)
+    for stats, msg, restore in pending:
+        _raise_status(int(stats[2].item()), msg, restore)
 
 
-def _status_check(stats, timeout_msg):
+def _status_check(stats, timeout_msg, restore=None):
     """torchdiffeq's assertions from the kernel's status word (one read per solve), or queued
     for `check_deferred` inside `deferred_status`."""
     if _DEFER[0]:
-        _DEFERRED.append((stats, timeout_msg))
+        _DEFERRED.append((stats, timeout_msg, restore))
         return
-    _raise_status(int(stats[2].item()), timeout_msg)
+    _raise_status(int(stats[2].item()), timeout_msg, restore)
+
+
+def _restorer(pairs):
+    """restore() for _raise_status: copies pre-solve snapshots back into the live state tensors
+    (and rebinds module attributes) — [(target, snapshot)] or callables."""
+    def restore():
+        with torch.no_grad():
+            for item in pairs:
+                if callable(item):
+                    item()
+                else:
+                    item[0].copy_(item[1])
+    return restore
 _MAX_TRACE = 16384   # attempts logged per resident solve (the count itself is exact beyond it)
 
 
@@ -372,6 +393,7 @@ def _try_ecg_resident(func, y0, tp, reversed_, rtol, atol, options):
     wT = cached[1]
     bias = _lib.f32c(func.proj.bias) if func.proj.bias is not None else None
     prev = basis._prev_for(dev)
+    prev0 = prev.clone()   # the timeout path restores it (the kernel rewrites prev_x in place)
     yc = _lib.f32c(y0)
     tkey = (dev, tuple(tp.tolist()))   # tp is the host copy odeint made; uploads once per grid
     t_dev = _T_DEV.get(tkey)
@@ -399,10 +421,14 @@ def _try_ecg_resident(func, y0, tp, reversed_, rtol, atol, options):
     if rc == _lib.FETODE_EUNSUPPORTED:   # no resident grid for this batch / width: host-driven loop
         return None
     _lib.check(rc, "fetode_ecg_dopri5")   # prev_x was rewritten in place (read before, written after)
+    old_branch = basis.branch_state
     basis.branch_state = branch
     dopri5_solve.last = ResidentSolve(stats, att)
+
+    def back():
+        basis.branch_state = old_branch
     _status_check(stats, "fetode_ecg_dopri5: a grid barrier timed out (workgroups not co-resident); "
-                         "the solution is invalid")
+                         "the solution is invalid", _restorer([(prev, prev0), back]))
     return sol
 
 
@@ -444,6 +470,7 @@ def _try_field_resident(func, y0, tp, reversed_, rtol, atol, options):
         return None
     plan = build_plan(field, handle, dev)
     state, mask = pack_state(field, B, dev)
+    state0 = None if state is None else state.clone()   # for the timeout path
     yc = _lib.f32c(y0)
     tkey = (dev, tuple(tp.tolist()))
     t_dev = _T_DEV.get(tkey)
@@ -481,7 +508,7 @@ def _try_field_resident(func, y0, tp, reversed_, rtol, atol, options):
         unpack_state(field, state)
     dopri5_solve.last = ResidentSolve(stats, att)
     _status_check(stats, "fetode_integrate_dopri5: a grid reduction timed out (workgroups not co-resident); "
-                         "the solution is invalid")
+                         "the solution is invalid", None if state is None else _restorer([(state, state0)]))
     return sol
 
 
@@ -547,6 +574,9 @@ class _FusedDopri5Fn(torch.autograd.Function):
                 tape.data_ptr(), cap, init_rec.data_ptr(), _lib.stream_handle(dev)),
                 "fetode_integrate_dopri5_tape")
             nfev, n_att, status = stats.tolist()
+            if status != 0 and state is not None:   # every failure leaves the pre-solve memory
+                state.copy_(state0)
+                unpack_state(field, state)
             _raise_status(status, "fetode_integrate_dopri5_tape: a grid reduction timed out (workgroups not "
                                   "co-resident); the solution is invalid")
             if nfev <= cap and n_att <= max_att:
@@ -560,9 +590,11 @@ class _FusedDopri5Fn(torch.autograd.Function):
         dopri5_solve.last = ResidentSolve(stats, att)
         ctx.field, ctx.handle, ctx.B, ctx.mask = field, handle, B, mask
         ctx.plan = pin_plan(field, plan)
-        ctx.state0 = state0
         ctx.t_dev, ctx.rtol, ctx.atol, ctx.opts = t_dev, rtol, atol, opts
-        ctx.tape, ctx.att, ctx.init_rec = tape, att, init_rec
+        # through save_for_backward (not ctx attributes): autograd frees the tape — GBs at large B
+        # and tight rtol — after a non-retained backward, before the next iteration's forward
+        # allocates its own, and keeps it for retain_graph=True
+        ctx.save_for_backward(tape, att, init_rec, state0)
         ctx.n_ev, ctx.n_att = nfev, n_att
         return sol
 
@@ -571,6 +603,7 @@ class _FusedDopri5Fn(torch.autograd.Function):
         from .autograd_ops import FERRO_PARAM_NAMES, field_layers, kan_params
         lib = _lib.load()
         field, B = ctx.field, ctx.B
+        tape, att, init_rec, state0 = ctx.saved_tensors
         dev = grad.device
         g = _lib.f32c(grad)
         layers = field_layers(field)
@@ -601,9 +634,9 @@ class _FusedDopri5Fn(torch.autograd.Function):
         _lib.check(lib.fetode_integrate_dopri5_backward(
             ctx.handle.ref, ctx.plan.data_ptr(), B, ctx.t_dev.data_ptr(), ctx.t_dev.numel(), ctx.rtol, ctx.atol,
             ctx.opts.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_double)),
-            _TABLEAU.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_float)), g.data_ptr(), ctx.tape.data_ptr(),
-            ctx.n_ev, ctx.att.data_ptr(), ctx.n_att, ctx.init_rec.data_ptr(),
-            _lib.ptr(ctx.state0), ctx.mask, _lib.ptr(gy0), kg, fg, ws.data_ptr(), status.data_ptr(),
+            _TABLEAU.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_float)), g.data_ptr(), tape.data_ptr(),
+            ctx.n_ev, att.data_ptr(), ctx.n_att, init_rec.data_ptr(),
+            _lib.ptr(state0), ctx.mask, _lib.ptr(gy0), kg, fg, ws.data_ptr(), status.data_ptr(),
             _lib.stream_handle(dev)), "fetode_integrate_dopri5_backward")
         _raise_status(int(status.item()), "fetode_integrate_dopri5_backward: a grid sum timed out (workgroups "
                                           "not co-resident); the gradients are invalid")
@@ -685,12 +718,17 @@ def _try_wide_resident(func, y0, tp, reversed_, rtol, atol, options):
     yc = _lib.f32c(y0)
 
     def mem(f, width):
+        # the first-call rule of FerroelectricBasis._needs_reinit (ferro_class.py:373-378): batch,
+        # device, dtype; a matching but non-contiguous memory is the same state, made contiguous
         p = f._prev
-        fresh = p.shape != (B, width) or p.device != dev or p.dtype != torch.float32 or not p.is_contiguous()
+        fresh = p.shape != (B, width) or p.device != dev or p.dtype != torch.float32
+        if not fresh and not p.is_contiguous():
+            p = f._prev = p.contiguous()
         return fresh, p
 
     re0, p0 = mem(f0, D)
     re1, p1 = mem(f1, H)
+    snap = [(p, p.clone()) for re, p in ((re0, p0), (re1, p1)) if not re]   # for the timeout path
     st0 = torch.empty(B, D, device=dev, dtype=torch.float32) if re0 else p0   # prev_x after the solve
     st1 = torch.empty(B, H, device=dev, dtype=torch.float32) if re1 else p1
     tkey = (dev, tuple(tp.tolist()))
@@ -719,13 +757,17 @@ def _try_wide_resident(func, y0, tp, reversed_, rtol, atol, options):
     if rc == _lib.FETODE_EUNSUPPORTED:
         return None
     _lib.check(rc, "fetode_wide_dopri5")
+    old = (f0._prev, f1._prev)   # the memory before the solve (rebound back on a timeout)
+
+    def back():
+        f0._prev, f1._prev = old
     if re0:
         f0._prev = st0
     if re1:
         f1._prev = st1
     dopri5_solve.last = ResidentSolve(stats, att)
     _status_check(stats, "fetode_wide_dopri5: a grid barrier timed out (workgroups not co-resident); "
-                         "the solution is invalid")
+                         "the solution is invalid", _restorer(snap + [back]))
     return sol
 
 

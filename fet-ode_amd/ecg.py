@@ -111,6 +111,9 @@ def _mixer_apply(basis: "LogisticBasis", x, act_sigmoid: bool, w=None, b=None):
 class LogisticBasis(CacheFreeState, nn.Module):
     """Hysteretic logistic basis, train_ecg_kan_fet_nn_ode.py:54-133."""
 
+    # per-batch state (rebound to (B, in, nb) every call): never broadcast across ranks
+    _rank_local_buffers = ("prev_x", "branch_state")
+
     def __init__(self, in_dim: int, num_basis: int, gate_slope: float = 5.0, init_prev: float = 0.0,
                  eps: float = 1e-6, branch_breaking_point=0.5, use_noise=False, noise_std=0.05):
         super().__init__()

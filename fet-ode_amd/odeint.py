@@ -204,9 +204,10 @@ class _FusedFixedFn(torch.autograd.Function):
             # the backward needs the plan and the state of THIS solve: later solves overwrite the
             # state in place (a copy), and rebuild the plan into a new buffer once it is pinned
             ctx.plan = pin_plan(field, plan)
-            ctx.state0 = None if state is None else state.clone()
             ctx.mask, ctx.handle, ctx.method, ctx.sched, ctx.field = mask, handle, method, sched, field
-            ctx.tape, ctx.B = tape, B
+            ctx.B = B
+            # freed by autograd after a non-retained backward (kept for retain_graph=True)
+            ctx.save_for_backward(tape, None if state is None else state.clone())
         _lib.check(lib.fetode_integrate_fixed(
             handle.ref, plan.data_ptr(), method, y0.data_ptr(), B, coef.data_ptr(), sched.n_steps,
             ostep.data_ptr(), omode.data_ptr(), oslope.data_ptr(), sched.T, sol.data_ptr(),
@@ -219,6 +220,7 @@ class _FusedFixedFn(torch.autograd.Function):
     def backward(ctx, grad):
         lib = _lib.load()
         field, handle, sched, B = ctx.field, ctx.handle, ctx.sched, ctx.B
+        tape, state0 = ctx.saved_tensors
         dev = grad.device
         g = _lib.f32c(grad)
         _, coef, ostep, omode, oslope = sched.device_arrays(dev)
@@ -251,8 +253,8 @@ class _FusedFixedFn(torch.autograd.Function):
         ws = torch.empty(max(1, nbytes // 4), device=dev, dtype=torch.float32)
         _lib.check(lib.fetode_integrate_fixed_backward(
             handle.ref, ctx.plan.data_ptr(), ctx.method, B, coef.data_ptr(), sched.n_steps, ostep.data_ptr(),
-            omode.data_ptr(), oslope.data_ptr(), sched.T, g.data_ptr(), ctx.tape.data_ptr(),
-            _lib.ptr(ctx.state0), ctx.mask, _lib.ptr(gy0), kg, fg, ws.data_ptr(), _lib.stream_handle(dev)),
+            omode.data_ptr(), oslope.data_ptr(), sched.T, g.data_ptr(), tape.data_ptr(),
+            _lib.ptr(state0), ctx.mask, _lib.ptr(gy0), kg, fg, ws.data_ptr(), _lib.stream_handle(dev)),
             "fetode_integrate_fixed_backward")
         pgrads = [grads.get(id(p)) if w else None for p, w in zip(params, want)]
         return (None, None, None, gy0, None, None, *pgrads)

@@ -277,6 +277,38 @@ def test_fused_backward_first_call_rules(dev, bwd_split):
                 assert_grad_close(p.grad, ps[n].grad, f"B={B} call={call} {n}", rel=rel)
 
 
+@pytest.mark.parametrize("kind,npts,rel", [("kan", 35, 2e-5), ("kanfet", 6, 2e-4)])
+def test_small_batch_tape_matches_v4(dev, kernel_switch, kind, npts, rel):
+    """At B <= small_max the taped training forward runs on v6 (small6_kernel<..., TAPE>); forcing
+    the v4 kernel (fetode_fused_set_small_batch_max(0)) must give the same loss and gradients up
+    to the two kernels' rounding orders, for every fixed-grid method and for dopri5 (KAN field),
+    and both within the oracle-fp64 bars of the tests above."""
+    import fet_ode_amd as F
+    from oracle import torch_ref as O
+    g = load_golden("traj_kanfet" if kind == "kanfet" else "traj_kan")
+    sd = golden_sd(g)
+    t = torch.from_numpy(g["t35"])[:npts]
+    y0 = O.lv_y0(64, seed=9).to(dev)
+    w = torch.randn(npts, 64, 2, generator=torch.Generator().manual_seed(6)).to(dev)
+    methods = ["rk4", "rk4_classic", "midpoint", "euler"] + (["dopri5"] if kind == "kan" else [])
+    for method in methods:
+        res = []
+        for small in (True, False):
+            kernel_switch(small)
+            m = (F.KANFET if kind == "kanfet" else F.KAN)([2, 10, 2], grid_size=5)
+            m.load_state_dict(sd)
+            m = m.to(dev)
+            yg = y0.clone().requires_grad_(True)
+            kw = {"rtol": 1e-3, "atol": 1e-4} if method == "dopri5" else {"method": method}
+            loss = (F.odeint(F.autonomous(m), yg, t, **kw) * w).sum()
+            loss.backward()
+            res.append((loss.item(), {"y0": yg.grad.cpu(), **{n: p.grad.cpu() for n, p in m.named_parameters()}}))
+        (l6, g6), (l4, g4) = res
+        assert abs(l6 - l4) <= 1e-5 * abs(l4), (method, l6, l4)
+        for n in g4:
+            assert_grad_close(g6[n], g4[n], f"{method} {n}", rel=rel)
+
+
 def test_fused_backward_matches_per_stage_path_large_batch(dev):
     """B=4096, the bench horizon (34 rk4 steps), KAN field: the fused reverse sweep and the
     per-stage path (autograd through every stage, per-module HIP VJPs) agree within 1e-4."""

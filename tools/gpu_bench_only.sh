@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU call: default bench (the contract line) then the rocprofv3 kernel-trace stats of a short bench
 cd "$(dirname "$0")/.."
-R=${ROUND:-r03}
+R=${ROUND:-r04}
 O=gpurun_out; mkdir -p $O; export TMPDIR=/tmp
 step() { local name=$1; shift; "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; [ $rc -le 1 ] || exit $rc; return 0; }
 step bench timeout -k 10 600 python bench.py

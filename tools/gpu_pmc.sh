@@ -5,7 +5,7 @@
 #  (2) tools/pmc_kernels.sh over tools/diag/prof_targets.py (wide ETT layers, MNIST head, training
 #      step) -> a per-kernel summary.
 cd "$(dirname "$0")/.."
-R=${ROUND:-r03}
+R=${ROUND:-r04}
 O=gpurun_out
 mkdir -p $O profiles
 export TMPDIR=/tmp
@@ -17,5 +17,8 @@ step pmc_fetch timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d $O
 step pmc_write timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d $O/pmc_write_$R -o run --output-format csv -- $B
 FETODE_PMC_KERNEL="fused4_kernel<10, 10, 10, 12, true, true" python tools/pmc_traffic.py $O/pmc_fetch_$R $O/pmc_write_$R $O/pmc_a_$R $O/pmc_b_$R --out $O/${R}_v4_pmc_traffic.json > $O/pmc_traffic.log 2>&1 || exit 3
 cp $O/${R}_v4_pmc_traffic.json profiles/${R}_v4_pmc_traffic.json
-TAG=${R}_k bash tools/pmc_kernels.sh
-python tools/pmc_summary.py $O/pmc_${R}_k_a $O/pmc_${R}_k_b $O/pmc_${R}_k_c --json $O/${R}_kernels_pmc.json > $O/${R}_kernels_pmc.txt
+# issue / MFMA / wait accounting per kernel (tools/pmc_issue.py -> the bench line's `issue` and `mfma`)
+TAG=${R}_i ISSUE=1 ONLY_ISSUE=1 bash tools/pmc_kernels.sh
+python tools/pmc_summary.py $O/pmc_${R}_i_v $O/pmc_${R}_i_m $O/pmc_${R}_i_w --json $O/${R}_pmc_issue_raw.json > $O/${R}_pmc_issue_raw.txt || exit 3
+python tools/pmc_issue.py $O/${R}_pmc_issue_raw.json --out $O/${R}_pmc_issue.json > $O/${R}_pmc_issue.txt || exit 3
+cp $O/${R}_pmc_issue.json $O/${R}_pmc_issue_raw.json profiles/

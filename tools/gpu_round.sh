@@ -3,7 +3,7 @@
 # the rocprofv3 kernel-trace stats of a short bench.  Every step has its own time limit; a step
 # that crashes / times out (rc > 1) ends the call.
 cd "$(dirname "$0")/.."
-R=${ROUND:-r03}
+R=${ROUND:-r04}
 O=gpurun_out; mkdir -p $O
 export TMPDIR=/tmp
 step() { local name=$1; shift; "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; [ $rc -le 1 ] || exit $rc; return 0; }

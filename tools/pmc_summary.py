@@ -16,6 +16,12 @@ def load(dirs):
                 k = row["Kernel_Name"].replace("(anonymous namespace)::", "")
                 k = k.split("(")[0] if not k.startswith("void (") else k
                 acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+        # the kernel trace of the same pass: mean launch duration (profiled) per kernel
+        for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+            for row in csv.DictReader(open(f)):
+                k = row["Kernel_Name"].replace("(anonymous namespace)::", "")
+                k = k.split("(")[0] if not k.startswith("void (") else k
+                acc[k]["dur_ns"].append(float(row["End_Timestamp"]) - float(row["Start_Timestamp"]))
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
