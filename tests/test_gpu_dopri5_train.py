@@ -55,18 +55,19 @@ def _run(kind, dev, B, t, rtol, atol, resident, options=None, y0_grad=False, see
     return loss.item(), grads, (y0.grad.cpu() if y0_grad else None), att, s.nfev
 
 
-def _oracle(kind, B, t, rtol, atol, options=None, seed=0):
-    """fp64 autograd through the oracle: loss, param grads, y0 grad, nfev."""
+def _oracle(kind, B, t, rtol, atol, options=None, seed=0, dtype=torch.float64):
+    """autograd through the oracle (fp64 by default; fp32 = the reference's own arithmetic in its own
+    op order): loss, param grads, y0 grad, nfev."""
     from oracle import torch_ref as O
     g = load_golden("traj_kanfet" if kind == "kanfet" else "traj_kan")
     sd = golden_sd(g)
     import fet_ode_amd as F
     names = [n for n, _ in (F.KANFET if kind == "kanfet" else F.KAN)([2, 10, 2], grid_size=5).named_parameters()]
-    ps = {k: v.clone().double().requires_grad_(k in names) for k, v in sd.items()}
+    ps = {k: v.clone().to(dtype).requires_grad_(k in names) for k, v in sd.items()}
     ref = (O.KANFETRef.from_state_dict(ps, 2) if kind == "kanfet"
            else O.KANRef([O.KANLinearParams.from_state_dict(ps, f"layers.{l}.") for l in range(2)]))
-    y0 = torch.from_numpy(g["y0_B64"]).repeat((B + 63) // 64, 1)[:B].double().requires_grad_(True)
-    w = torch.randn(len(t), B, 2, generator=torch.Generator().manual_seed(seed)).double()
+    y0 = torch.from_numpy(g["y0_B64"]).repeat((B + 63) // 64, 1)[:B].to(dtype).requires_grad_(True)
+    w = torch.randn(len(t), B, 2, generator=torch.Generator().manual_seed(seed)).to(dtype)
     tr = O.Dopri5Trace()
     sol = O.odeint(lambda tt, yy: ref(yy), y0, t, rtol=rtol, atol=atol, trace=tr, options=options)
     loss = (w * sol).sum()
@@ -79,8 +80,13 @@ def _rel(a, b):
 
 
 def _vs_oracle(kind, dev, B, t, rtol, atol, gtol, options=None, ltol=1e-5):
-    """Per-tensor relative error against the fp64 oracle <= gtol, or (KAN) <= 2x the host autograd
-    path's own error where fp32 summation already costs more (small, cancelling gradients)."""
+    """Per-tensor relative error against the fp64 oracle <= gtol, or (KAN) <= 2x the error an fp32
+    implementation already makes there: the host autograd path's, or the reference's own fp32
+    autograd's (the oracle in fp32, reference op order).  The gradient through the step-size control
+    is a cancelling sum over the stages' VJPs (d err / d theta = dt * sum_i e_i dk_i / d theta), so at
+    rtol 1e-3 every fp32 implementation lands 2e-5 .. 1e-4 from fp64 on the spline scalers
+    (tools/diag/d5_prec.py, profiles/r04_d5_prec.log: reference fp32 6.8e-5 on layers.1.spline_scaler
+    at B = 1, host 4.1e-5, resident 1.0e-4)."""
     l0, g0, y0g0, _, n0 = _run(kind, dev, B, t, rtol, atol, True, options=options, y0_grad=True)
     l1, g1, y0g1, n1 = _oracle(kind, B, t, rtol, atol, options=options)
     assert n0 == n1, (n0, n1)
@@ -92,7 +98,10 @@ def _vs_oracle(kind, dev, B, t, rtol, atol, gtol, options=None, ltol=1e-5):
         assert nh == n1
         host = {n: _rel(gh[n], g1[n]) for n in g1}
         host["y0"] = _rel(y0gh, y0g1)
-        bad = {n: (e, host[n]) for n, e in worst.items() if e > max(gtol, 2 * host[n])}
+        _, g32, y0g32, n32 = _oracle(kind, B, t, rtol, atol, options=options, dtype=torch.float32)
+        ref32 = {n: _rel(g32[n], g1[n]) for n in g1}
+        ref32["y0"] = _rel(y0g32, y0g1)
+        bad = {n: (e, host[n], ref32[n]) for n, e in worst.items() if e > max(gtol, 2 * host[n], 2 * ref32[n])}
         assert not bad, bad
         return
     assert max(worst.values()) <= gtol, sorted(worst.items(), key=lambda kv: -kv[1])[:4]
@@ -101,9 +110,10 @@ def _vs_oracle(kind, dev, B, t, rtol, atol, gtol, options=None, ltol=1e-5):
 @pytest.mark.parametrize("B", [1, 16, 64])
 @pytest.mark.parametrize("rtol", [1e-3, 1e-2, 1e-1])
 def test_dopri5_train_kan_vs_oracle_fp64(dev, B, rtol):
-    """Smooth field: the whole gradient (step-size control terms included) to 2e-4."""
+    """Smooth field: the whole gradient (step-size control terms included) to 1e-4, or within 2x of
+    an fp32 implementation's own error where that is larger (_vs_oracle)."""
     t = torch.tensor(np.linspace(0, 2.0, 9))
-    _vs_oracle("kan", dev, B, t, rtol, rtol * 0.1, 2e-4)
+    _vs_oracle("kan", dev, B, t, rtol, rtol * 0.1, 1e-4)
 
 
 def test_dopri5_train_kan_first_step_vs_oracle_fp64(dev):

@@ -121,3 +121,23 @@ def test_classic_rk4_is_option_of_fixed_grid():
         z = z + (h / 6.0) * (k1 + 2 * k2 + 2 * k3 + k4)
         out.append(z)
     assert torch.allclose(a, torch.stack(out), atol=1e-14)
+
+
+def test_dopri5_replay_reproduces_solve_and_row_subsets():
+    """options['replay'] (test infrastructure for row-subset checks of large device solves): replaying
+    a solve's own attempt log gives the same solution bit for bit, and replaying the FULL batch's log
+    on a row subset gives those rows of the full solution (rows are independent given the steps)."""
+    W = torch.tensor([[0.3, -1.1], [0.9, 0.2]], dtype=torch.float64)
+    f = lambda t, y: torch.tanh(y @ W) - 0.1 * y
+    y0 = torch.linspace(-1.5, 2.0, 16, dtype=torch.float64).reshape(8, 2)
+    t = torch.tensor([0.0, 0.7, 2.0], dtype=torch.float64)
+    tr = O.Dopri5Trace()
+    sol = O.odeint(f, y0, t, rtol=1e-6, atol=1e-8, options={"first_step": 0.05}, trace=tr)
+    log = [(a[0], a[1], a[3]) for a in tr.attempts]
+    assert len(log) > 5
+    again = O.odeint(f, y0, t, rtol=1e-6, atol=1e-8, options={"first_step": 0.05, "replay": log})
+    assert torch.equal(again, sol)
+    sub = O.odeint(f, y0[2:5], t, rtol=1e-6, atol=1e-8, options={"first_step": 0.05, "replay": log})
+    assert torch.equal(sub, sol[:, 2:5])
+    with pytest.raises(AssertionError):
+        O.odeint(f, y0, t, options={"replay": log})      # the probe is a global norm: needs first_step

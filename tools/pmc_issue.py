@@ -51,7 +51,7 @@ def main():
             wc = c["SQ_WAVE_CYCLES"]
             r.update({"wait_any_share": c["SQ_WAIT_ANY"] / wc, "wait_inst_any_share": c.get("SQ_WAIT_INST_ANY", 0) / wc,
                       "active_inst_any_share": c.get("SQ_ACTIVE_INST_ANY", 0) / wc,
-                      "sq_busy_frac": c.get("SQ_BUSY_CYCLES", 0) / N_XCD / cyc})
+                      "sq_busy_cycles_per_xcd_over_elapsed": c.get("SQ_BUSY_CYCLES", 0) / N_XCD / cyc})
     for k, v in out.items():
         print(f"{k[:60]:60s} " + "  ".join(f"{n} {x:.3g}" for n, x in v.items() if n != "cycles"))
     if "--out" in sys.argv:
