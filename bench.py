@@ -5,10 +5,12 @@ vector field (train_kanfet_node_predprey.py:146), torch.manual_seed(0) weights, 
 2.5*U[0,1)^(4096x2), t = linspace(0, 3.5, 35) float64 (t_learn, :155), method='rk4' (torchdiffeq
 3/8 rule).  One bench "step" = one odeint solve = 34 RK4 steps of the batch, inputs resident in HBM.
 
-Scaling: --scaling strong (default, primary) splits the GLOBAL batch of 4096
-(seed 0) into contiguous per-rank blocks (fet_ode_amd.dist.shard_bounds): value = batch-4096 RK4
-steps/s of the whole job.  --scaling weak gives every rank its own 4096 trajectories (seed = rank):
-value = batch-4096 steps/s summed over ranks.  The forward path needs no collective either way.
+Scaling: the path partitions by trajectory with no data-path collective, so the contract line is
+WEAK scaling (--scaling weak, default): every rank solves its own batch of 4096 (seed = rank) and
+value = batch-4096 RK4 steps/s summed over the ranks.  At N > 1 the same run also times the STRONG
+split (the global seed-0 batch of 4096 cut into contiguous per-rank blocks,
+fet_ode_amd.dist.shard_bounds) and reports it as `strong_scaling`; --scaling strong makes that the
+contract value instead.
 
 Launch: python bench.py [--gpus N --steps K --warmup W]; N>1 via torch.distributed.run.
 Prints ONE JSON line on rank 0.
@@ -55,8 +57,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
-                    help="strong: global batch 4096 split over ranks (primary); weak: 4096 per rank")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="weak",
+                    help="weak: 4096 trajectories per rank (the contract line); strong: global batch 4096 split")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-dopri5", action="store_true", help="skip the LV dopri5 (torchdiffeq defaults) line")
     ap.add_argument("--no-ecg", action="store_true", help="skip the ECG dopri5 (configs[2]) line")
@@ -895,9 +897,32 @@ def main():
             el = tt.item()
         k_ms = kernel_time_ms(model, y0d, t)
     train = train_rate(model, y0d, t, args.train_iters, 5, world, strong) if args.train_iters > 0 else None
+    strong_line = None
+    if world > 1 and not strong:
+        # the other scaling mode from the same run: the global seed-0 batch of 4096 split over the ranks
+        import fet_ode_amd.dist as D
+        lo, hi = D.shard_bounds(B, rank, world)
+        y0s = lv_y0(B, 0)[lo:hi].to(dev)
+        with torch.no_grad():
+            for _ in range(args.warmup):
+                F.odeint(func, y0s, t, method="rk4")
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                F.odeint(func, y0s, t, method="rk4")
+            torch.cuda.synchronize(dev)
+            dist.barrier()
+            els = time.perf_counter() - t0
+        tt = torch.tensor([els], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        els = tt.item()
+        strong_line = {"value": args.steps * STEPS_PER_SOLVE / els, "ms_per_step": els / args.steps * 1e3,
+                       "batch_per_gpu": hi - lo, "unit": "RK4 steps/s of ONE batch-4096 job split over the GPUs",
+                       "scaling": "strong"}
     dp5_sharded = None
-    if world > 1 and strong and not args.no_dopri5:
-        dp5_sharded = lv_dopri5_sharded_rate(sd, y0d, t, world, B)
+    if world > 1 and not args.no_dopri5:
+        dp5_sharded = lv_dopri5_sharded_rate(sd, y0d, t, world, B if strong else B * world)
     ms_per_step = el / args.steps * 1e3
     # strong: every solve covers the global batch once; weak: each rank's solve is a batch of its own
     value = (1 if strong else world) * args.steps * STEPS_PER_SOLVE / el
@@ -949,6 +974,8 @@ def main():
                                    "solve_ms_b4096": solve_ms(model, y0d, t), "solve_ms_b512": solve_ms(model, y512, t),
                                    "note": "B=512 = the per-GPU block of the 8-GPU strong-scaled job; kernel by HIP "
                                            "events, solve = host wall of one odeint call (median)"}
+        if strong_line is not None:
+            out["strong_scaling"] = strong_line
         if train is not None:
             out["train"] = train
         if world == 1:

@@ -463,8 +463,17 @@ class _UncheckedAssign(torch.autograd.Function):
 
 
 def _dopri5(func, y0, t, rtol, atol, trace: Optional[Dopri5Trace], max_num_steps=2 ** 31 - 1,
-            first_step=None):
-    """RKAdaptiveStepsizeODESolver + Dopri5Solver (rk_common.py / dopri5.py)."""
+            first_step=None, replay=None):
+    """RKAdaptiveStepsizeODESolver + Dopri5Solver (rk_common.py / dopri5.py).
+
+    ``replay``: a list of (t0, dt, accepted) attempts recorded by another solve of the same batch
+    (test infrastructure): the attempts run with those step sizes and decisions instead of this
+    batch's own error ratios — so a row SUBSET of a large batch, whose RMS error norm couples every
+    row, can be checked against the large solve row by row.  Needs ``first_step`` (the initial-step
+    probe is a global norm too)."""
+    if replay is not None:
+        assert first_step is not None, "replay needs first_step"
+        replay = list(replay)
     sdt = y0.dtype
     tdt = torch.promote_types(torch.float64, sdt)
     rtol_t = torch.as_tensor(rtol, dtype=tdt)
@@ -502,6 +511,10 @@ def _dopri5(func, y0, t, rtol, atol, trace: Optional[Dopri5Trace], max_num_steps
             assert n_steps < max_num_steps, "max_num_steps exceeded"
             # _adaptive_step
             y0_, f0_, t0_, dt_ = st_y, st_f, st_t1, st_dt
+            if replay is not None:
+                r_t0, r_dt, r_acc = replay.pop(0)
+                assert abs(float(t0_) - r_t0) <= 1e-12 * max(1.0, abs(r_t0)), (float(t0_), r_t0)
+                dt_ = torch.as_tensor(r_dt, dtype=tdt)
             t1_ = t0_ + dt_
             assert t0_ + dt_ > t0_, "underflow in dt {}".format(dt_.item())
             assert torch.isfinite(y0_).all(), "non-finite values in state `y`"
@@ -519,7 +532,7 @@ def _dopri5(func, y0, t, rtol, atol, trace: Optional[Dopri5Trace], max_num_steps
             y1_error = k.matmul(dtc * c_err)
             error_tol = atol_t + rtol_t * torch.max(y0_.abs(), y1.abs())
             error_ratio = _rms_norm(y1_error / error_tol)
-            accept = bool(error_ratio <= 1)
+            accept = bool(error_ratio <= 1) if replay is None else bool(r_acc)
             if trace is not None:
                 trace.attempts.append((float(t0_.detach()), float(dt_.detach()), float(error_ratio.detach()), accept))
             if accept:
@@ -552,7 +565,8 @@ def odeint(func: Callable, y0: torch.Tensor, t, *, rtol=1e-7, atol=1e-9, method=
     options = dict(options or {})
     func, t, method, reversed_ = _check_inputs(func, y0, t, method)
     if method == "dopri5":
-        sol = _dopri5(func, y0, t, rtol, atol, trace, first_step=options.get("first_step"))
+        sol = _dopri5(func, y0, t, rtol, atol, trace, first_step=options.get("first_step"),
+                      replay=options.get("replay"))
     else:
         step = {"euler": euler_step, "midpoint": midpoint_step, "rk4_classic": rk4_classic_step,
                 "rk4": rk4_classic_step if classic_rk4 else rk4_alt_step}[method]

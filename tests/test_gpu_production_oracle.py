@@ -1,0 +1,113 @@
+"""MI355X: the ETT production sizes pinned to the oracle on row subsets (VERDICT r3 "next" 2).
+
+The other production-width tests compare the device paths with each other (resident dopri5 vs the
+host loop, the fused wide layer vs the per-module kernels); these compare them with the CPU oracle
+(oracle/torch_ref.py + oracle/ett_ref.py, the reference's op order) at the production batch itself,
+B = 8192 and KANFET[64, 128, 64] — so every tiling, input-slicing and grid-barrier case the kernels
+take at that size is on the checked path — on 256 rows: the first and last row tiles and 128 rows
+spread over the batch.
+
+* fetode_wide_dopri5 (train_kan_fet_ett.py:192, the forecaster's own solve): the error norm couples
+  all 8192 rows, so the oracle replays the device solve's attempt log (step sizes and accept
+  decisions; oracle.torch_ref `replay`) on the subset — the rows' arithmetic is then independent of
+  the other rows — with an explicit first_step (the initial-step probe is a global norm too; the
+  probe path itself is pinned against the host loop in test_gpu_wide_dopri5.py).
+* LatentNeuralODEForecaster forward with the KAN-FET latent field (train_kan_fet_ett.py:155-197) on
+  96 -> 8 windows, odeint_rk4: rows are independent, the oracle runs the subset directly.
+
+Bar: the fp32/fp64 envelope of tests/test_gpu_ett.py — |gpu - fp64| <= 4 |reference fp32 - fp64|
++ 1e-5 x scale, elementwise max over the subset (KAN-FET is ill-conditioned in fp32).
+Horizons are short so the untrained field stays bounded (|z| < 50)."""
+import pytest
+import torch
+
+import fet_ode_amd as F
+from fet_ode_amd import ett
+from fet_ode_amd.autograd_ops import field_layers
+from fet_ode_amd.dopri5 import ResidentSolve
+from oracle import ett_ref as E
+from oracle import torch_ref as O
+
+pytestmark = pytest.mark.gpu
+
+B = 8192
+
+
+def _rows():
+    g = torch.Generator().manual_seed(21)
+    mid = torch.randperm(B - 128, generator=g)[:128] + 64
+    return torch.cat([torch.arange(64), mid.sort().values, torch.arange(B - 64, B)])
+
+
+def _envelope(got, e32, e64, name, floor=1e-5, k=4.0):
+    got, e32, e64 = got.detach().double().cpu(), e32.detach().double().cpu(), e64.detach().double().cpu()
+    scale = e64.abs().max().item() + 1e-12
+    spread = (e32 - e64).abs().max().item()
+    err = (got - e64).abs().max().item()
+    assert err <= k * spread + floor * scale, f"{name}: |gpu-fp64|={err:.3e} fp32 spread={spread:.3e} scale={scale:.3e}"
+    return err / scale, spread / scale
+
+
+def test_wide_resident_dopri5_b8192_rows_vs_oracle(dev):
+    torch.manual_seed(0)
+    dyn = ett.KANFETDynamics(64, hidden=128, num_fet_basis=10)
+    sd = {k: v.clone() for k, v in dyn.net.state_dict().items()}
+    dyn = dyn.to(dev)
+    g = torch.Generator().manual_seed(3)
+    z0 = torch.randn(B, 64, generator=g) * 0.6
+    t = torch.linspace(0.0, 0.1, steps=3)
+    kw = dict(rtol=1e-1, atol=1e-2, options=dict(first_step=0.05))
+    prev = F.dopri5.set_wide_resident_dopri5(True, gap=(0, 0))
+    try:
+        with torch.no_grad():
+            sol = F.odeint(dyn, z0.to(dev), t.to(dev), method="dopri5", **kw)
+        s = F.dopri5.dopri5_solve.last
+        assert isinstance(s, ResidentSolve), "the wide resident path was not taken"
+    finally:
+        F.dopri5.set_wide_resident_dopri5(prev, gap=(512, 8192))
+    log = [(a[0], a[1], a[3]) for a in s.attempts]
+    assert len(log) >= 2 and torch.isfinite(sol).all()
+    mem = [f._prev.detach().cpu() for _, f in field_layers(dyn.net)]
+    rows = _rows()
+    outs = {}
+    for dt in (torch.float32, torch.float64):
+        ref = O.KANFETRef.from_state_dict({k: v.to(dt) for k, v in sd.items()}, 2)
+        tr = O.Dopri5Trace()
+        with torch.no_grad():
+            e = O.odeint(lambda tt, zz: ref(zz), z0[rows].to(dt), t.to(torch.float64), method="dopri5",
+                         rtol=kw["rtol"], atol=kw["atol"], options={**kw["options"], "replay": log}, trace=tr)
+        assert tr.nfev == s.nfev, (tr.nfev, s.nfev)
+        outs[dt] = (e, [st.prev_x[:, :, 0, 0].clone() for st in ref.states])
+    (e32, m32), (e64, m64) = outs[torch.float32], outs[torch.float64]
+    got = sol.cpu()[:, rows]
+    assert got.abs().max().item() < 50
+    _envelope(got, e32, e64, "wide dopri5 B=8192 solution rows")
+    for l in range(2):
+        _envelope(mem[l][rows], m32[l], m64[l], f"wide dopri5 B=8192 hysteresis memory layer {l}")
+
+
+def test_forecaster_latent64_b8192_rows_vs_oracle(dev):
+    c, p = 96, 8
+    torch.manual_seed(0)
+    m = ett.LatentNeuralODEForecaster(num_features=7, context_len=c, pred_len=p, latent_dim=64, solver="rk4")
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    g = torch.Generator().manual_seed(4)
+    series = torch.cumsum(torch.randn(B + c + p, 7, generator=g), 0) * 0.05
+    ds = ett.EnergyWindowDataset(series, series[:, -1], c, p, device=dev)
+    xb, _ = ds.batch(torch.arange(B, device=dev))
+    t_fut = torch.linspace(0.0, float(p - 1), steps=p)
+    with torch.no_grad():
+        got = m(xb, t_fut.to(dev), rk4_substeps=1)
+    assert got.shape == (B, p) and torch.isfinite(got).all()
+    rows = _rows()
+    xs = xb[rows.to(dev)].cpu()
+    outs = {}
+    for dt in (torch.float32, torch.float64):
+        sdd = {k: v.to(dt) for k, v in sd.items()}
+        field = O.KANFETRef.from_state_dict({k[len("dynamics.net."):]: v for k, v in sdd.items()
+                                             if k.startswith("dynamics.net.")}, 2)
+        ref = E.ForecasterRef(sdd, lambda tt, zz: field(zz))
+        with torch.no_grad():
+            outs[dt] = ref(xs.to(dt), t_fut.to(dt), rk4_substeps=1)
+    _envelope(got.cpu()[rows], outs[torch.float32], outs[torch.float64], "forecaster latent 64, B=8192 rows")
