@@ -146,6 +146,16 @@ SIGNATURES = {
                                           ctypes.POINTER(ctypes.c_float), _vp, _vp, _vp, _vp, _vp, _vp,
                                           ctypes.c_int32, _vp]),
     "fetode_wide_dopri5_workspace": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
+    "fetode_kuramoto_set_lds": (ctypes.c_int, [ctypes.c_int]),
+    "fetode_wide_dopri5_xrank": (ctypes.c_int, [ctypes.POINTER(KANLinearDesc), ctypes.POINTER(FerroDesc), _vp,
+                                                ctypes.POINTER(KANLinearDesc), ctypes.POINTER(FerroDesc), _vp, _vp,
+                                                ctypes.c_int64, ctypes.c_int64, _vp, _vp, ctypes.c_uint32, _vp,
+                                                ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+                                                ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_float), _vp,
+                                                _vp, _vp, _vp, _vp, _vp, ctypes.c_int32, ctypes.POINTER(XRankDesc),
+                                                _vp]),
+    "fetode_wide_dopri5_xrank_workspace": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                                            ctypes.c_int32, ctypes.c_int32]),
     "fetode_field_forward": (ctypes.c_int, [ctypes.POINTER(FieldDesc), _vp, _vp, ctypes.c_int64, _vp,
                                             ctypes.c_uint32, _vp, _vp]),
     "fetode_integrate_fixed": (ctypes.c_int, [ctypes.POINTER(FieldDesc), _vp, ctypes.c_int32, _vp,

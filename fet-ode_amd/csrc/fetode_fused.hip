@@ -62,30 +62,7 @@ namespace {
 
 #include "fetode_gridsum.h"
 
-// System-scope (sc0 sc1: write-through to memory / read past every cache) records for the
-// cross-rank exchange: the payload lands before the tag that publishes it (vmcnt(0) between).
-__device__ __forceinline__ void xr_st16(double* p, double v0, double v1) {
-  const unsigned long long a = __double_as_longlong(v0), b = __double_as_longlong(v1);
-  const dp_u32x4 v = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void xr_st_tag(double* p, unsigned long long tag) {
-  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-  const u32x2 v = {(unsigned)tag, (unsigned)(tag >> 32)};
-  asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ unsigned long long xr_ld_tag(const double* p) {
-  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-  u32x2 v;
-  asm volatile("global_load_dwordx2 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-  return ((unsigned long long)v.y << 32) | v.x;
-}
-__device__ __forceinline__ void xr_ld16(const double* p, double& v0, double& v1) {
-  dp_u32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-  v0 = __longlong_as_double(((unsigned long long)v.y << 32) | v.x);
-  v1 = __longlong_as_double(((unsigned long long)v.w << 32) | v.z);
-}
+#include "fetode_xrank.h"
 
 // Trajectory-sharded solve (xr_world > 1): the rank sum of every grid reduction is formed by ONE
 // extra workgroup (the last of the grid; the compute workgroups' path changes only in which counter
@@ -100,11 +77,6 @@ __device__ __forceinline__ void xr_ld16(const double* p, double& v0, double& v1)
 // ends when the compute workgroups post the solve's round count (dp_fin) or the abort word rises.
 // Bounded spins; a timeout raises the abort word (status 4) and the peers time out in turn.
 __device__ __forceinline__ unsigned* dp_fin(const DopriParams& P) { return P.bar + kDpLine * kDpGroups; }
-// inbox: (2 parity, 64 items) {v0, v1} records, then (2 parity, 64 ranks) tags (fetode_xrank_inbox_bytes)
-__device__ __forceinline__ double* xr_rec(double* inbox, unsigned par, int item) { return inbox + 2 * (64 * par + item); }
-__device__ __forceinline__ double* xr_tagp(double* inbox, unsigned par, int rank) {
-  return inbox + 2 * 2 * 64 + (64 * par + rank);
-}
 
 __device__ void xrank_comm(const DopriParams& P) {
   const int lane = threadIdx.x & 63;

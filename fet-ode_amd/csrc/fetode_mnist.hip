@@ -10,6 +10,8 @@
 // (written by the training forward), forming d theta_s from d theta_{s+1} with the stencil's
 // transpose; d omega and d K are per-image partial sums reduced over the batch in a fixed order
 // (no atomics: run-to-run identical).
+#include <cstdlib>
+
 #include "fetode_common.h"
 
 using namespace fetode;
@@ -85,6 +87,189 @@ __global__ __launch_bounds__(kKThreads) void kuramoto_fwd_kernel(const float* __
     phase_sincos(t, sv, cv);
     feat[b * 2 * HW + p] = cv;
     feat[b * 2 * HW + HW + p] = sv;
+  }
+}
+
+// ---- lane-per-column kernels (W <= 32, H = HM rows): no LDS, no barriers -------------------------
+// A wave holds two images: lanes 32 i + c (c < W) own column c of image 2 w + i, the column's H
+// phases (and omega) in registers.  Vertical neighbours are the neighbouring registers; horizontal
+// ones come from the neighbouring lanes by DPP wave shifts (wave_shr:1 = lane - 1, wave_shl:1 =
+// lane + 1; lanes c >= W hold zero sin / cos / g and bound_ctrl gives zero past the wave's ends, so
+// a missing tap adds +0 — the same sum as skipping it).  Rows are walked top to bottom with a
+// three-row window: row r's update needs rows r - 1 .. r + 1 of the step's OLD values, and row
+// r + 1's are formed before row r is overwritten.  Same tap order (up, left, right, down) and
+// per-pixel arithmetic as the LDS kernels (kuramoto_fwd_kernel / _bwd_kernel).
+constexpr int kLaneWaves = 4;  // waves per workgroup (2 images each)
+__device__ __forceinline__ float dpp_left(float v) {  // lane - 1's value (0 at lane 0)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float dpp_right(float v) {  // lane + 1's value (0 at lane 63)
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, true));
+}
+
+template <int H>
+__global__ __launch_bounds__(64 * kLaneWaves) void kuramoto_fwd_lanes_kernel(
+    const float* __restrict__ x, int64_t B, int W, int steps, float dt, const float* __restrict__ Kp,
+    const float* __restrict__ omega, float* __restrict__ feat, float* __restrict__ tape) {
+  const int lane = threadIdx.x & 63, c = lane & 31;
+  const int64_t b = ((int64_t)blockIdx.x * kLaneWaves + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const bool act = c < W && b < B;
+  const int HW = H * W;
+  const float K = *Kp;
+  const float pi = 3.14159265358979323846f;
+  const float* xb = x + (act ? b * HW + c : 0);
+  const float* ob = omega + (act ? c : 0);
+  float th[H], om[H];
+#pragma unroll
+  for (int r = 0; r < H; ++r) {
+    th[r] = pi * (2.0f * xb[r * W] - 1.0f);
+    om[r] = ob[r * W];
+  }
+  float* tpb = tape ? tape + (act ? b * (int64_t)(steps + 1) * HW + c : 0) : nullptr;
+  for (int st = 0; st < steps; ++st) {
+    if (tpb && act) {
+#pragma unroll
+      for (int r = 0; r < H; ++r) tpb[st * HW + r * W] = th[r];
+    }
+    float su = 0.f, cu = 0.f, sm, cm, sd = 0.f, cd = 0.f;  // rows r - 1 (up), r, r + 1 (down)
+    phase_sincos(th[0], sm, cm);
+    sm = act ? sm : 0.f;
+    cm = act ? cm : 0.f;
+#pragma unroll
+    for (int r = 0; r < H; ++r) {
+      if (r + 1 < H) {
+        phase_sincos(th[r + 1], sd, cd);
+        sd = act ? sd : 0.f;
+        cd = act ? cd : 0.f;
+      }
+      float sn_n = 0.f, cs_n = 0.f;
+      if (r > 0) {
+        sn_n += su;
+        cs_n += cu;
+      }
+      sn_n += dpp_left(sm);
+      cs_n += dpp_left(cm);
+      sn_n += dpp_right(sm);
+      cs_n += dpp_right(cm);
+      if (r + 1 < H) {
+        sn_n += sd;
+        cs_n += cd;
+      }
+      const float coupling = cm * sn_n - sm * cs_n;
+      th[r] = th[r] + dt * (om[r] + K * coupling);
+      su = sm;
+      cu = cm;
+      sm = sd;
+      cm = cd;
+    }
+  }
+  if (!act) return;
+  float* fb = feat + b * 2 * HW + c;
+#pragma unroll
+  for (int r = 0; r < H; ++r) {
+    if (tpb) tpb[steps * HW + r * W] = th[r];
+    float sv, cv;
+    phase_sincos(th[r], sv, cv);
+    fb[r * W] = cv;
+    fb[HW + r * W] = sv;
+  }
+}
+
+// The VJP on the same layout (kuramoto_bwd_kernel's per-pixel arithmetic and tap order): g, the
+// d omega accumulator and the step's tape phases in registers (each row's phase slot is refilled
+// with step st - 1's once its sin / cos are formed); per row a window of rows r - 1 .. r + 1 of the
+// step's sin / cos and OLD g (row r - 1's new g is written back after row r has read the old one).
+// d K: this lane's sum over its pixels and steps, then the image's 32 lanes by an xor tree.
+template <int H>
+__global__ __launch_bounds__(64 * kLaneWaves) void kuramoto_bwd_lanes_kernel(
+    int64_t B, int W, int steps, float dt, const float* __restrict__ Kp, const float* __restrict__ tape,
+    const float* __restrict__ gfeat, float* __restrict__ gx, float* __restrict__ gK_part,
+    float* __restrict__ gom_part) {
+  const int lane = threadIdx.x & 63, c = lane & 31;
+  const int64_t b = ((int64_t)blockIdx.x * kLaneWaves + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const bool act = c < W && b < B;
+  const int HW = H * W;
+  const float K = *Kp;
+  // inactive lanes read image 0 / column 0 (valid memory) and mask the values: no branches in the
+  // unrolled row loops (per-row branches made the register allocator copy the arrays at every join)
+  const float* tb = tape + (act ? b * (int64_t)(steps + 1) * HW + c : 0);
+  const float* gf = gfeat + (act ? b * 2 * HW + c : 0);
+  const int sp = steps > 0 ? steps - 1 : 0;
+  float g[H], go[H], th[H];
+  float gk = 0.f;
+#pragma unroll
+  for (int r = 0; r < H; ++r) {
+    go[r] = 0.f;
+    float sv, cv;
+    phase_sincos(tb[steps * HW + r * W], sv, cv);
+    const float gv = (-sv) * gf[r * W] + cv * gf[HW + r * W];
+    g[r] = act ? gv : 0.f;
+    th[r] = tb[sp * HW + r * W];
+  }
+  for (int st = steps - 1; st >= 0; --st) {
+    const float* tn = tb + (st > 0 ? st - 1 : 0) * HW;   // step st - 1 (step 0 again at the last: unused)
+    float su = 0.f, cu = 0.f, gu = 0.f, sm, cm, sd = 0.f, cd = 0.f;
+    float gnew_prev = 0.f;
+    phase_sincos(th[0], sm, cm);
+    sm = act ? sm : 0.f;
+    cm = act ? cm : 0.f;
+    th[0] = tn[0];
+#pragma unroll
+    for (int r = 0; r < H; ++r) {
+      if (r + 1 < H) {
+        phase_sincos(th[r + 1], sd, cd);
+        sd = act ? sd : 0.f;
+        cd = act ? cd : 0.f;
+        th[r + 1] = tn[(r + 1) * W];
+      }
+      const float gm = g[r], gd = (r + 1 < H) ? g[r + 1] : 0.f;
+      float S = 0.f, C = 0.f;  // tap order up, left, right, down
+      if (r > 0) {
+        S += su;
+        C += cu;
+      }
+      const float sl = dpp_left(sm), cl = dpp_left(cm), gl = dpp_left(gm);
+      const float sr = dpp_right(sm), cr = dpp_right(cm), gr = dpp_right(gm);
+      S += sl;
+      C += cl;
+      S += sr;
+      C += cr;
+      if (r + 1 < H) {
+        S += sd;
+        C += cd;
+      }
+      const float coupling = cm * S - sm * C;
+      gk += gm * coupling;
+      go[r] += gm;
+      float acc = gm * (-(sm * S + cm * C));
+      if (r > 0) acc += gu * (cu * cm + su * sm);
+      acc += gl * (cl * cm + sl * sm);   // a missing neighbour has g = sin = cos = 0: + 0
+      acc += gr * (cr * cm + sr * sm);
+      if (r + 1 < H) acc += gd * (cd * cm + sd * sm);
+      if (r > 0) g[r - 1] = gnew_prev;  // row r - 1's old g was last read above
+      gnew_prev = act ? gm + (dt * K) * acc : 0.f;
+      su = sm;
+      cu = cm;
+      gu = gm;
+      sm = sd;
+      cm = cd;
+    }
+    g[H - 1] = gnew_prev;
+  }
+  const float pi = 3.14159265358979323846f;
+  if (act && gx) {
+#pragma unroll
+    for (int r = 0; r < H; ++r) gx[b * HW + r * W + c] = (g[r] * pi) * 2.0f;  // theta_0 = pi (2 x - 1)
+  }
+  if (act && gom_part) {
+#pragma unroll
+    for (int r = 0; r < H; ++r) gom_part[b * HW + r * W + c] = dt * go[r];
+  }
+  if (gK_part) {  // the image's d K: xor tree over its 32 lanes (inactive lanes add 0)
+    float v = act ? gk : 0.f;
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (c == 0 && b < B) gK_part[b] = dt * v;
   }
 }
 
@@ -474,6 +659,14 @@ __global__ void wide_reduce_kernel(const float* __restrict__ part, int S, int64_
   out[t] = bias ? v + bias[o] : v;
 }
 
+// the LDS (workgroup-per-image) Kuramoto kernels for every shape: FETODE_KURA_LDS=1 (A/B and the
+// cross-check test), or fetode_kuramoto_set_lds(1)
+int g_kura_lds = [] {
+  const char* e = getenv("FETODE_KURA_LDS");
+  return e ? atoi(e) : 0;
+}();
+bool kura_lds_forced() { return g_kura_lds != 0; }
+
 int wide_supported(const fetode_kanlinear_t* kl) {
   return kl && kl->spline_order == 3 && kl->grid_size == 5 && (kl->num_logistic == 0 || kl->num_logistic == kWideNB) &&
          kl->out_features >= 1 && kl->out_features <= 16 && kl->in_features >= 4 && kl->in_features % 4 == 0 &&
@@ -499,11 +692,24 @@ int fetode_kuramoto_forward(const float* x, int64_t B, int32_t H, int32_t W, int
   if (!x || !K || !omega || !feat) return set_err(FETODE_EINVAL, "kuramoto: null pointer");
   if (H <= 0 || W <= 0 || H * W > kMaxPix || steps < 0)
     return set_err(FETODE_EINVAL, "kuramoto: H*W=%d (1..%d), steps=%d", H * W, kMaxPix, steps);
+  if (H == 28 && W <= 32 && !kura_lds_forced()) {  // lane per column (MNIST 28 x 28)
+    const unsigned grid = (unsigned)((B + 2 * kLaneWaves - 1) / (2 * kLaneWaves));
+    hipLaunchKernelGGL(kuramoto_fwd_lanes_kernel<28>, dim3(grid), dim3(64 * kLaneWaves), 0, (hipStream_t)stream, x, B,
+                       W, steps, dt, K, omega, feat, tape);
+    LAUNCH_CHECK();
+    return FETODE_OK;
+  }
   const size_t lds = sizeof(float) * 3 * H * W;
   hipLaunchKernelGGL(kuramoto_fwd_kernel, dim3((unsigned)B), dim3(kKThreads), lds, (hipStream_t)stream, x, H, W, steps,
                      dt, K, omega, feat, tape);
   LAUNCH_CHECK();
   return FETODE_OK;
+}
+
+int fetode_kuramoto_set_lds(int on) {
+  const int prev = g_kura_lds;
+  if (on >= 0) g_kura_lds = on;
+  return prev;
 }
 
 int64_t fetode_kuramoto_backward_workspace(int64_t B, int32_t H, int32_t W) {
@@ -523,9 +729,15 @@ int fetode_kuramoto_backward(int64_t B, int32_t H, int32_t W, int32_t steps, flo
   float* gom_part = gomega ? (float*)workspace : nullptr;
   float* gK_part = gK ? (float*)workspace + B * HW : nullptr;
   hipStream_t s = (hipStream_t)stream;
-  const size_t lds = sizeof(float) * 4 * HW;
-  hipLaunchKernelGGL(kuramoto_bwd_kernel, dim3((unsigned)B), dim3(kKThreads), lds, s, H, W, steps, dt, K, tape, gfeat,
-                     gx, gK_part, gom_part);
+  if (H == 28 && W <= 32 && !kura_lds_forced()) {
+    const unsigned grid = (unsigned)((B + 2 * kLaneWaves - 1) / (2 * kLaneWaves));
+    hipLaunchKernelGGL(kuramoto_bwd_lanes_kernel<28>, dim3(grid), dim3(64 * kLaneWaves), 0, s, B, W, steps, dt, K, tape,
+                       gfeat, gx, gK_part, gom_part);
+  } else {
+    const size_t lds = sizeof(float) * 4 * HW;
+    hipLaunchKernelGGL(kuramoto_bwd_kernel, dim3((unsigned)B), dim3(kKThreads), lds, s, H, W, steps, dt, K, tape, gfeat,
+                       gx, gK_part, gom_part);
+  }
   LAUNCH_CHECK();
   // fp64 slice sums, 8-byte aligned after the float partials
   const int64_t fl = B * ((int64_t)HW + 1);

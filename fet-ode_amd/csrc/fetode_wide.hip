@@ -35,6 +35,8 @@ using namespace fetode;
 
 namespace {
 
+#include "fetode_xrank.h"
+
 constexpr float kWideFactorLimit = 60.0f;  // |gs Ec| bound of the factored gate (header comment)
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -1102,17 +1104,26 @@ bool kan_bwd_wide_ok(const fetode_kanlinear_t* kl, const fetode_ferro_t* fl) {
 // Per-element solver state (y, f0, the running stage sums, err, mid, the interpolation
 // coefficients) lives in HBM and is touched only by the element's owner thread: layer-1 tile t
 // belongs to workgroup t % G, and its element (row, dim) to the epilogue thread that stores it —
-// so none of it crosses workgroups.  The one global quantity per attempt is the RMS error ratio:
-// per-workgroup fp64 partials, the barrier, and every workgroup sums all partials in the same
-// order (the same decisions everywhere).  Control arithmetic: the host-driven path's (fp32 stage
-// sums in fetode_lincomb's order, fp64 step control, fetode_interp_fit / _eval), so the solution
-// equals the host loop's bit for bit up to the norms' fp64 summation order.
+// so none of it crosses workgroups.  The one global quantity per attempt is the RMS error ratio,
+// summed in an order that depends on the batch alone (not on the grid): per layer-1 TILE an fp64
+// partial (its owner threads, fixed order), then leaves of `leafL` consecutive tiles summed tile by
+// tile, then an xor tree over the <= 64 leaves — every workgroup forms the same value, so all take
+// the same decisions.  Control arithmetic: the host-driven path's (fp32 stage sums in
+// fetode_lincomb's order, fp64 step control, fetode_interp_fit / _eval), so the solution equals the
+// host loop's bit for bit up to the norms' fp64 summation order.
+// Trajectory-sharded (fetode_wide_dopri5_xrank, SURVEY §8e caveat 2): each rank's grid owns the
+// tiles of its rows; the norms are exchanged between the ranks' kernels through IPC-mapped inboxes
+// (fetode_xrank.h).  When every rank's rows are whole leaves of the global tile sequence (and the
+// input slices are the global batch's), the ranks exchange the leaf sums themselves and every rank
+// forms the single device's xor tree: solution, steps and memory are bitwise the single device's on
+// the global batch; otherwise the ranks exchange their totals and sum them in rank order.
 // =============================================================================================
 constexpr int kEs = 17;  // per-element state rows: y, f0, A0..A5, err, mid, co0..co4, y1, k_last
 enum { kEY = 0, kEF0 = 1, kEA = 2, kEErr = 8, kEMid = 9, kECo = 10, kEY1 = 15, kEKl = 16 };
 constexpr int kWBarWords = 64 * 10;  // 8 XCD counters, top counter, generation | abort (256 B apart)
 constexpr unsigned kWSpinLimit = 1u << 22;
-constexpr int kWideDopriMaxGrid = 256 * 8;  // partial slots of the norm reduction
+constexpr int kWideDopriMaxGrid = 256 * 8;  // the persistent grid's cap (2 workgroups per CU)
+constexpr unsigned kXrSpinLimitW = 1u << 24;  // cross-rank polls: ranks may start seconds apart
 
 struct WideDopriArgs {
   WideArgs l0, l1;  // plan + layout of each layer; x / prev / nslice are set per phase
@@ -1135,10 +1146,17 @@ struct WideDopriArgs {
   int max_steps;
   float stc[7][8];  // tableau columns (DopriParams.stc)
   unsigned* bar;
-  double* slot;  // (grid, 2)
+  double* slot;  // (nT1, 2) per-tile norm partials
   int32_t* stats;
   double* att;
   int max_att;
+  // the norm's summation structure and the cross-rank exchange
+  double n_el;                 // element count of the norms: B_global * D
+  int leafL, n_leaf;           // tiles per leaf (power of two), leaves of the global tile sequence (<= 64)
+  int xr_rank, xr_world, xr_exact, leaf_lo, n_leaf_local;
+  unsigned xr_epoch;
+  double* const* xr_peers;     // (dev) every rank's inbox as mapped here (peers[rank] = own)
+  double* xr_inbox;
 };
 
 __device__ __forceinline__ void st_wt(float* p, float v) {  // write-through (sc1) store
@@ -1216,48 +1234,115 @@ __device__ __forceinline__ double wd_xor_sum(double v) {
   return v;
 }
 
-// Sum of two fp64 values over every thread of the grid, the same fixed order in every workgroup:
-// waves (xor tree), the workgroup's waves in index order, then the workgroups' partials (lane j sums
-// partials j, j + 64, .. in order, then an xor tree).  Contains a barrier.
-__device__ bool wide_sum2(unsigned* bar, double* slot, double v0, double v1, double& s0, double& s1) {
-  __shared__ double s_red[kWaves][2];
-  __shared__ double s_out[2];
+// The owner threads' two fp64 values of one layer-1 tile -> the tile's partial (xor tree per wave,
+// waves 0..3 in order), stored write-through at slot[t].  Every thread of the workgroup calls it.
+__device__ void wide_tile_partial(double* slot, int t, double v0, double v1) {
+  __shared__ double s_red[4][2];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   v0 = wd_xor_sum(v0);
   v1 = wd_xor_sum(v1);
-  if (lane == 0) {
+  if (lane == 0 && w < 4) {
     s_red[w][0] = v0;
     s_red[w][1] = v1;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double a0 = 0.0, a1 = 0.0;
-    for (int j = 0; j < kWaves; ++j) {
-      a0 += s_red[j][0];
-      a1 += s_red[j][1];
-    }
-    wd_st16(slot + 2 * blockIdx.x, a0, a1);
+  if (threadIdx.x == 0)
+    wd_st16(slot + 2 * t, ((s_red[0][0] + s_red[1][0]) + s_red[2][0]) + s_red[3][0],
+            ((s_red[0][1] + s_red[1][1]) + s_red[2][1]) + s_red[3][1]);
+  __syncthreads();
+}
+
+// leaf j's sum: its tiles [j L, (j + 1) L) of `nt` (read from slot, local tile numbering) in order
+__device__ __forceinline__ void wide_leaf(const double* slot, int j, int L, int nt, double& a0, double& a1) {
+  a0 = 0.0;
+  a1 = 0.0;
+  const int e = min((j + 1) * L, nt);
+  for (int t = j * L; t < e; ++t) {
+    double u0, u1;
+    wd_ld16(slot + 2 * t, u0, u1);
+    a0 += u0;
+    a1 += u1;
   }
-  if (wide_barrier(bar)) return true;
+}
+
+// The grid-wide (and, sharded, rank-wide) sum of the tile partials, returned to every workgroup in
+// the same fixed order.  Contains a grid barrier.  `round` counts the calls (the same in every
+// workgroup and on every rank: every rank takes the same decisions).
+__device__ bool wide_norm(const WideDopriArgs& a, unsigned& round, double& s0, double& s1) {
+  __shared__ double s_out[2];
+  __shared__ int s_ab;
+  if (wide_barrier(a.bar)) return true;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  unsigned* abw = a.bar + 64 * 9 + 1;
   if (w == 0) {
-    double a0 = 0.0, a1 = 0.0;
-    for (unsigned j = lane; j < gridDim.x; j += 64) {
-      double u0, u1;
-      wd_ld16(slot + 2 * j, u0, u1);
-      a0 += u0;
-      a1 += u1;
+    double g0 = 0.0, g1 = 0.0;
+    int ab = 0;
+    if (a.xr_world <= 1) {  // one device: every workgroup sums the leaves itself
+      double v0 = 0.0, v1 = 0.0;
+      if (lane < a.n_leaf) wide_leaf(a.slot, lane, a.leafL, a.nT1, v0, v1);
+      g0 = wd_xor_sum(v0);
+      g1 = wd_xor_sum(v1);
+    } else {
+      const unsigned r = round, par = r & 1u;
+      const int W = a.xr_world;
+      if (blockIdx.x == 0) {  // send: this rank's leaves at their global index (exact), or its total
+        double v0 = 0.0, v1 = 0.0;
+        if (lane < a.n_leaf_local) wide_leaf(a.slot, lane, a.leafL, a.nT1, v0, v1);
+        if (a.xr_exact) {
+          if (lane < a.n_leaf_local)
+            for (int q = 0; q < W; ++q) xr_st16(xr_rec(a.xr_peers[q], par, a.leaf_lo + lane), v0, v1);
+        } else {
+          const double t0 = wd_xor_sum(v0), t1 = wd_xor_sum(v1);
+          if (lane < W) xr_st16(xr_rec(a.xr_peers[lane], par, a.xr_rank), t0, t1);
+        }
+        const unsigned long long tag = ((unsigned long long)a.xr_epoch << 32) | (unsigned long long)(r + 1u);
+        if (lane < W) xr_st_tag(xr_tagp(a.xr_peers[lane], par, a.xr_rank), tag);
+      }
+      // receive: every rank's round-r tag in this device's inbox, then the records
+      const unsigned long long tag = ((unsigned long long)a.xr_epoch << 32) | (unsigned long long)(r + 1u);
+      if (lane < W) {
+        const double* tg = xr_tagp(a.xr_inbox, par, lane);
+        unsigned spins = 0;
+        while (xr_ld_tag(tg) != tag) {
+          __builtin_amdgcn_s_sleep(2);
+          if ((spins & 255u) == 255u && __hip_atomic_load(abw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+            ab = 1;
+            break;
+          }
+          if (++spins == kXrSpinLimitW) {
+            __hip_atomic_store(abw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ab = 1;
+            break;
+          }
+        }
+      }
+      ab = __any(ab) ? 1 : 0;
+      if (!ab) {
+        double v0 = 0.0, v1 = 0.0;
+        if (a.xr_exact) {  // the single device's xor tree over the global leaves
+          if (lane < a.n_leaf) xr_ld16(xr_rec(a.xr_inbox, par, lane), v0, v1);
+          g0 = wd_xor_sum(v0);
+          g1 = wd_xor_sum(v1);
+        } else {  // rank totals in rank order
+          if (lane < W) xr_ld16(xr_rec(a.xr_inbox, par, lane), v0, v1);
+          for (int j = 0; j < W; ++j) {
+            g0 += __shfl(v0, j);
+            g1 += __shfl(v1, j);
+          }
+        }
+      }
     }
-    a0 = wd_xor_sum(a0);
-    a1 = wd_xor_sum(a1);
     if (lane == 0) {
-      s_out[0] = a0;
-      s_out[1] = a1;
+      s_out[0] = g0;
+      s_out[1] = g1;
+      s_ab = ab;
     }
   }
+  ++round;
   __syncthreads();
   s0 = s_out[0];
   s1 = s_out[1];
-  return false;
+  return s_ab != 0;
 }
 
 enum { kCmbF0 = 0, kCmbF1 = 1, kCmbStage = 2 };
@@ -1281,7 +1366,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   const int G = (int)gridDim.x;
   const int64_t B = a.B, BD = B * a.D, BH = B * a.H;
   const int D = a.D, H = a.H;
-  const double n_el = (double)BD;
+  const double n_el = a.n_el;
   // element ownership: the layer-1 tile epilogue's storing threads (waves 0-3: row 16 (w % 4) +
   // 4 (lane / 16) + v, dim lane % 16), layer-1 tile t < nT1 on workgroup t % G
   const bool owner = w < 4;
@@ -1299,7 +1384,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     }
   };
   float* const es = a.es;
-  double acc0 = 0.0, acc1 = 0.0;  // this thread's partial norms
+  unsigned nround = 0;  // norm rounds (wide_norm)
 
   for_owned([&](int64_t i) {
     const float y = a.y0[i];
@@ -1369,7 +1454,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 #pragma unroll
       for (int q = 0; q < 8; ++q) c[q] = ctl.cc[q];
       const int S1 = a.S1;
-      for_owned([&](int64_t i) {
+      // norm terms: per layer-1 tile (wide_tile_partial) when this evaluation ends in a reduction
+      const bool red = (kind == kCmbF0 && !(a.first_step > 0.0)) || kind == kCmbF1 || (kind == kCmbStage && stg == 5);
+      double acc0 = 0.0, acc1 = 0.0;
+      auto elem = [&](int64_t i) {
         float k = a.ks[i];
         for (int s = 1; s < S1; ++s) k = k + a.ks[s * BD + i];  // slab 0 + slab 1 + ..: the launch path's order
         const float y = es[kEY * BD + i];
@@ -1407,17 +1495,31 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
             acc1 += __builtin_isfinite(y) ? 0.0 : 1.0;
           }
         }
-      });
+      };
+      for (int t = blockIdx.x; t < a.nT1; t += G) {
+        if (owner) {
+          const int64_t b0 = (int64_t)(t / a.nOT1) * kRows;
+          const int d = (t % a.nOT1) * kOuts + kr;
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int64_t b = b0 + 16 * rt + 4 * kq + v;
+            if (b < B) elem(b * D + d);
+          }
+        }
+        if (red) {
+          wide_tile_partial(a.slot, t, acc0, acc1);
+          acc0 = acc1 = 0.0;
+        }
+      }
     }
     // ---- the decision (thread 0) ----
     const int kind = ctl.kind, stg = ctl.stg;
     const bool reduce = !(kind == kCmbF0 && a.first_step > 0.0) && !(kind == kCmbStage && stg < 5);
     double s0 = 0.0, s1 = 0.0;
-    if (reduce && wide_sum2(a.bar, a.slot, acc0, acc1, s0, s1)) {
+    if (reduce && wide_norm(a, nround, s0, s1)) {
       status = 4;
       break;
     }
-    acc0 = acc1 = 0.0;  // (f0's norm terms are unused when first_step is given)
     __syncthreads();  // every wave has read this evaluation's control words before thread 0 rewrites them
     if (tid == 0) {
       ctl.nev = e + 1;
@@ -1603,21 +1705,23 @@ struct WideDopriShape {
   int64_t off_slot, off_xin, off_hs, off_ks, off_es, bytes;  // byte offsets in the workspace
 };
 
-// input slices per layer: the per-layer launch's rule (fetode_wide_layer_forward), so each layer's
-// sums are formed in the same order as the host-driven loop's
-WideDopriShape wide_dopri_shape(int64_t B, int D, int H) {
+// input slices per layer: the per-layer launch's rule (fetode_wide_layer_forward) over the batch
+// B_slices (the local batch: the host-driven loop's sums; a sharded solve that must be bitwise the
+// single device: the global batch)
+WideDopriShape wide_dopri_shape(int64_t B, int D, int H, int64_t B_slices = 0) {
   WideDopriShape s{};
   const int64_t rows = (B + kRows - 1) / kRows;
+  const int64_t rows_s = ((B_slices > 0 ? B_slices : B) + kRows - 1) / kRows;
   s.nOT0 = H / kOuts;
   s.nOT1 = D / kOuts;
   s.nT0 = (int)(rows * s.nOT0);
   s.nT1 = (int)(rows * s.nOT1);
-  s.S0 = wide_slices(s.nT0, D);
-  s.S1 = wide_slices(s.nT1, H);
+  s.S0 = wide_slices(rows_s * s.nOT0, D);
+  s.S1 = wide_slices(rows_s * s.nOT1, H);
   auto al = [](int64_t v) { return (v + 255) & ~int64_t(255); };
   int64_t o = al((int64_t)sizeof(unsigned) * kWBarWords);
   s.off_slot = o;
-  o = al(o + (int64_t)sizeof(double) * 2 * kWideDopriMaxGrid);
+  o = al(o + (int64_t)sizeof(double) * 2 * s.nT1);
   s.off_xin = o;
   o = al(o + (int64_t)sizeof(float) * 2 * B * D);
   s.off_hs = o;
@@ -1825,17 +1929,32 @@ int fetode_kanlinear_backward_wide(const fetode_kanlinear_t* kl, const fetode_fe
 }
 
 
-int64_t fetode_wide_dopri5_workspace(int64_t B, int32_t D, int32_t H) {
-  if (B <= 0 || D < 16 || H < 16) return -1;
-  return wide_dopri_shape(B, D, H).bytes;
+}  // extern "C"
+
+namespace {
+// the norm's leaves: L tiles each (the smallest power of two with <= 64 leaves over nt tiles)
+int wide_leaf_len(int64_t nt) {
+  int L = 1;
+  while ((nt + L - 1) / L > 64) L *= 2;
+  return L;
+}
+// a sharded solve is bitwise the single device's when this rank's rows are whole leaves of the
+// global tile sequence (tiles are 64-row blocks x output blocks, row-block-major)
+bool wide_xr_exact(int64_t B, int64_t B_total, int64_t b_off, int D) {
+  const int nOT1 = D / kOuts;
+  if (b_off % kRows) return false;
+  const int64_t nT1g = (B_total + kRows - 1) / kRows * nOT1, L = wide_leaf_len(nT1g);
+  const int64_t t_lo = b_off / kRows * nOT1, nT1 = (B + kRows - 1) / kRows * nOT1;
+  const bool last = b_off + B == B_total;
+  return t_lo % L == 0 && (nT1 % L == 0 || last) && (B % kRows == 0 || last);
 }
 
-int fetode_wide_dopri5(const fetode_kanlinear_t* kan0, const fetode_ferro_t* fer0, const void* plan0,
+int wide_dopri5_launch(const fetode_kanlinear_t* kan0, const fetode_ferro_t* fer0, const void* plan0,
                        const fetode_kanlinear_t* kan1, const fetode_ferro_t* fer1, const void* plan1, const float* y0,
                        int64_t B, const float* prev0, const float* prev1, uint32_t reinit_mask, const double* t,
                        int32_t T, double rtol, double atol, const double* opts, const float* tableau, float* solution,
                        float* state0, float* state1, void* workspace, int32_t* stats, double* attempts,
-                       int32_t max_attempts, void* stream) {
+                       int32_t max_attempts, const fetode_xrank_t* xr, int64_t B_total, void* stream) {
   if (!kan0 || !fer0 || !kan1 || !fer1) return set_err(FETODE_EUNSUPPORTED, "wide dopri5: needs two KAN-FET layers");
   if (!wide_supported(kan0, fer0) || !wide_supported(kan1, fer1))
     return set_err(FETODE_EUNSUPPORTED, "wide dopri5: a layer has no wide kernel");
@@ -1848,7 +1967,9 @@ int fetode_wide_dopri5(const fetode_kanlinear_t* kan0, const fetode_ferro_t* fer
     return set_err(FETODE_EINVAL, "wide dopri5: null pointer");
   if ((!(reinit_mask & 1u) && !prev0) || (!(reinit_mask & 2u) && !prev1))
     return set_err(FETODE_EINVAL, "wide dopri5: null hysteresis state");
-  const WideDopriShape sh = wide_dopri_shape(B, D, H);
+  const bool sharded = xr && xr->world > 1;
+  const bool exact = sharded && wide_xr_exact(B, B_total, xr->b_offset, D);
+  const WideDopriShape sh = wide_dopri_shape(B, D, H, exact ? B_total : 0);
   if ((int64_t)sh.nT0 * sh.S0 > 0x7fffffff / 2) return set_err(FETODE_EINVAL, "wide dopri5: batch too large");
   const int K = fer0->num_basis;
   const void* fn = K == 12 ? (const void*)wide_dopri5_kernel<12> : (const void*)wide_dopri5_kernel<10>;
@@ -1921,10 +2042,72 @@ int fetode_wide_dopri5(const fetode_kanlinear_t* kan0, const fetode_ferro_t* fer
   a.stats = stats;
   a.att = attempts;
   a.max_att = attempts ? max_attempts : 0;
+  a.n_el = (double)(sharded ? B_total : B) * D;
+  if (exact) {  // leaves of the global tile sequence; this rank's are [leaf_lo, leaf_lo + n_leaf_local)
+    const int64_t nT1g = (B_total + kRows - 1) / kRows * sh.nOT1;
+    a.leafL = wide_leaf_len(nT1g);
+    a.n_leaf = (int)((nT1g + a.leafL - 1) / a.leafL);
+    a.leaf_lo = (int)(xr->b_offset / kRows * sh.nOT1 / a.leafL);
+  } else {
+    a.leafL = wide_leaf_len(sh.nT1);
+    a.n_leaf = (sh.nT1 + a.leafL - 1) / a.leafL;
+    a.leaf_lo = 0;
+  }
+  a.n_leaf_local = (sh.nT1 + a.leafL - 1) / a.leafL;
+  a.xr_world = sharded ? xr->world : 1;
+  if (sharded) {
+    a.xr_rank = xr->rank;
+    a.xr_exact = exact ? 1 : 0;
+    a.xr_epoch = xr->epoch;
+    a.xr_peers = (double* const*)xr->peers;
+    a.xr_inbox = (double*)xr->inbox;
+  }
   hipStream_t s = (hipStream_t)stream;
   HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kWBarWords, s));
   void* args[] = {&a};
   HIP_CHECK_RET(resident_launch(fn, dim3((unsigned)grid), dim3(kThreads), args, 0, s));
   return FETODE_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int64_t fetode_wide_dopri5_workspace(int64_t B, int32_t D, int32_t H) {
+  if (B <= 0 || D < 16 || H < 16) return -1;
+  return wide_dopri_shape(B, D, H).bytes;
+}
+
+int64_t fetode_wide_dopri5_xrank_workspace(int64_t B, int64_t B_total, int64_t b_offset, int32_t D, int32_t H) {
+  if (B <= 0 || D < 16 || H < 16 || B_total < B || b_offset < 0 || b_offset + B > B_total) return -1;
+  return wide_dopri_shape(B, D, H, wide_xr_exact(B, B_total, b_offset, D) ? B_total : 0).bytes;
+}
+
+int fetode_wide_dopri5(const fetode_kanlinear_t* kan0, const fetode_ferro_t* fer0, const void* plan0,
+                       const fetode_kanlinear_t* kan1, const fetode_ferro_t* fer1, const void* plan1, const float* y0,
+                       int64_t B, const float* prev0, const float* prev1, uint32_t reinit_mask, const double* t,
+                       int32_t T, double rtol, double atol, const double* opts, const float* tableau, float* solution,
+                       float* state0, float* state1, void* workspace, int32_t* stats, double* attempts,
+                       int32_t max_attempts, void* stream) {
+  return wide_dopri5_launch(kan0, fer0, plan0, kan1, fer1, plan1, y0, B, prev0, prev1, reinit_mask, t, T, rtol, atol,
+                            opts, tableau, solution, state0, state1, workspace, stats, attempts, max_attempts, nullptr,
+                            B, stream);
+}
+
+int fetode_wide_dopri5_xrank(const fetode_kanlinear_t* kan0, const fetode_ferro_t* fer0, const void* plan0,
+                             const fetode_kanlinear_t* kan1, const fetode_ferro_t* fer1, const void* plan1,
+                             const float* y0, int64_t B, int64_t B_total, const float* prev0, const float* prev1,
+                             uint32_t reinit_mask, const double* t, int32_t T, double rtol, double atol,
+                             const double* opts, const float* tableau, float* solution, float* state0, float* state1,
+                             void* workspace, int32_t* stats, double* attempts, int32_t max_attempts,
+                             const fetode_xrank_t* xr, void* stream) {
+  if (!xr || xr->world < 1 || xr->rank < 0 || xr->rank >= xr->world || xr->world > 64)
+    return set_err(FETODE_EINVAL, "wide dopri5 xrank: bad rank / world");
+  if (xr->world > 1 && (!xr->peers || !xr->inbox)) return set_err(FETODE_EINVAL, "wide dopri5 xrank: null inbox / peers");
+  if (B_total < B || xr->b_offset < 0 || xr->b_offset + B > B_total)
+    return set_err(FETODE_EINVAL, "wide dopri5 xrank: shard [%lld, %lld) outside the global batch %lld",
+                   (long long)xr->b_offset, (long long)(xr->b_offset + B), (long long)B_total);
+  return wide_dopri5_launch(kan0, fer0, plan0, kan1, fer1, plan1, y0, B, prev0, prev1, reinit_mask, t, T, rtol, atol,
+                            opts, tableau, solution, state0, state1, workspace, stats, attempts, max_attempts, xr,
+                            B_total, stream);
 }
 }  // extern "C"

@@ -683,10 +683,15 @@ def _try_field_resident_train(func, y0, tp, reversed_, rtol, atol, options):
 def _try_wide_resident(func, y0, tp, reversed_, rtol, atol, options):
     """The whole solve in one launch (fetode_wide_dopri5) when `func` is a tagged two-layer wide
     KAN-FET field — the ETT forecaster's KANFETDynamics, KANFET([latent, hidden, latent]),
-    train_kan_fet_ett.py:192 — nothing needs gradients and the options are the scalar ones."""
+    train_kan_fet_ett.py:192 — nothing needs gradients and the options are the scalar ones.
+    Trajectory-sharded (options["norm_group"], dist.odeint_sharded): one launch per rank whose
+    norms are exchanged between the ranks' kernels (fetode_wide_dopri5_xrank) — every rank takes the
+    resident path or none."""
     from .autograd_ops import field_layers, wide_plan
     from .odeint import fused_field
     field = fused_field(func)
+    options = dict(options)
+    group = options.pop("norm_group", None)
     if field is None or reversed_ or y0.dim() != 2 or set(options) - _RESIDENT_OPTS:
         return None
     if not getattr(field, "has_ferro", False):
@@ -698,22 +703,40 @@ def _try_wide_resident(func, y0, tp, reversed_, rtol, atol, options):
         return None
     (k0, f0), (k1, f1) = layers
     B, D = y0.shape
-    if _WIDE_RESIDENT_GAP[0] < B < _WIDE_RESIDENT_GAP[1]:
+    H = k0.out_features
+    dev = y0.device
+    ok = True
+    if group is None and _WIDE_RESIDENT_GAP[0] < B < _WIDE_RESIDENT_GAP[1]:
         # measured crossover: between these batches the per-layer launches beat the
         # persistent grid's tiles plus its three grid barriers per evaluation
         return None
-    H = k0.out_features
     if D != k0.in_features or k1.in_features != H or k1.out_features != D or f0.num_basis != f1.num_basis:
-        return None
+        ok = False
     if torch.is_grad_enabled() and (y0.requires_grad or any(p.requires_grad for p in field.parameters())):
-        return None
-    dev = y0.device
-    e0, e1 = wide_plan(k0, f0, dev), wide_plan(k1, f1, dev)
-    if e0 is None or e1 is None:
-        return None
+        ok = False
+    e0 = e1 = None
+    if ok:
+        e0, e1 = wide_plan(k0, f0, dev), wide_plan(k1, f1, dev)
+        ok = e0 is not None and e1 is not None
     lib = _lib.load()
-    ws_bytes = lib.fetode_wide_dopri5_workspace(B, D, H)
+    xr = None
+    if group is not None:
+        # trajectory-sharded: all ranks take the resident path or none (their kernels exchange norms)
+        from . import dist as Dd
+        grp = None if group == "world" else group
+        agreed = Dd.resident_agreement(grp, dev, B, ok and Dd._RESIDENT_SHARDED[0])
+        if agreed is None:
+            return None
+        B_total, b_off = agreed
+        xr = Dd.XRank.get(grp, dev)
+        ws_bytes = lib.fetode_wide_dopri5_xrank_workspace(B, B_total, b_off, D, H)
+    elif not ok:
+        return None
+    else:
+        ws_bytes = lib.fetode_wide_dopri5_workspace(B, D, H)
     if ws_bytes < 0:
+        if xr is not None:
+            raise RuntimeError("sharded wide dopri5: no workspace for this shard after every rank agreed")
         return None
     yc = _lib.f32c(y0)
 
@@ -748,13 +771,26 @@ def _try_wide_resident(func, y0, tp, reversed_, rtol, atol, options):
                      float(options.get("min_step", 0.0)), float(options.get("max_step", math.inf)),
                      float(options.get("max_num_steps", 2 ** 31 - 1))], dtype=np.float64)
     by = _lib.ctypes.byref
-    rc = lib.fetode_wide_dopri5(
-        by(e0[1]), by(e0[2]), e0[0].data_ptr(), by(e1[1]), by(e1[2]), e1[0].data_ptr(), yc.data_ptr(), B,
-        None if re0 else p0.data_ptr(), None if re1 else p1.data_ptr(), (1 if re0 else 0) | (2 if re1 else 0),
-        t_dev.data_ptr(), T, float(rtol), float(atol), opts.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_double)),
-        _TABLEAU.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_float)), sol.data_ptr(), st0.data_ptr(),
-        st1.data_ptr(), ws.data_ptr(), stats.data_ptr(), att.data_ptr(), _MAX_TRACE, _lib.stream_handle(dev))
+    optp = opts.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_double))
+    tabp = _TABLEAU.ctypes.data_as(_lib.ctypes.POINTER(_lib.ctypes.c_float))
+    mask = (1 if re0 else 0) | (2 if re1 else 0)
+    if xr is not None:
+        xd = xr.desc(b_off)
+        rc = lib.fetode_wide_dopri5_xrank(
+            by(e0[1]), by(e0[2]), e0[0].data_ptr(), by(e1[1]), by(e1[2]), e1[0].data_ptr(), yc.data_ptr(), B, B_total,
+            None if re0 else p0.data_ptr(), None if re1 else p1.data_ptr(), mask, t_dev.data_ptr(), T, float(rtol),
+            float(atol), optp, tabp, sol.data_ptr(), st0.data_ptr(), st1.data_ptr(), ws.data_ptr(), stats.data_ptr(),
+            att.data_ptr(), _MAX_TRACE, by(xd), _lib.stream_handle(dev))
+    else:
+        rc = lib.fetode_wide_dopri5(
+            by(e0[1]), by(e0[2]), e0[0].data_ptr(), by(e1[1]), by(e1[2]), e1[0].data_ptr(), yc.data_ptr(), B,
+            None if re0 else p0.data_ptr(), None if re1 else p1.data_ptr(), mask, t_dev.data_ptr(), T, float(rtol),
+            float(atol), optp, tabp, sol.data_ptr(), st0.data_ptr(), st1.data_ptr(), ws.data_ptr(), stats.data_ptr(),
+            att.data_ptr(), _MAX_TRACE, _lib.stream_handle(dev))
     if rc == _lib.FETODE_EUNSUPPORTED:
+        if xr is not None:   # the peers' kernels are waiting for this rank's norms
+            raise RuntimeError("sharded wide dopri5: this rank's launch was refused after every rank agreed: "
+                               + _lib.load().fetode_last_error().decode(errors="replace"))
         return None
     _lib.check(rc, "fetode_wide_dopri5")
     old = (f0._prev, f1._prev)   # the memory before the solve (rebound back on a timeout)

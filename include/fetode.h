@@ -240,6 +240,22 @@ int fetode_integrate_dopri5_xrank(const fetode_field_t* field, const void* plan,
 /* inbox bytes for a world; allocate + export (handle: 64 bytes, hipIpcMemHandle_t), open a peer's
  * handle in this process, close / free.  Host calls (synchronous). */
 int64_t fetode_xrank_inbox_bytes(int32_t world);
+/* The wide KAN-FET field's resident dopri5 over this rank's shard [xr->b_offset, + B) of a
+ * trajectory-sharded global batch B_total (the ETT forecaster's solve, train_kan_fet_ett.py:192,
+ * sharded 8x: BASELINE configs[3]; dist.odeint_sharded).  Every error norm is the global batch's:
+ * the ranks' kernels exchange them through the inboxes (no host round trip); every rank takes the
+ * same attempts.  When the shard's rows are whole leaves of the global tile sequence the result is
+ * bitwise fetode_wide_dopri5 on the global batch.  Arguments as fetode_wide_dopri5; workspace:
+ * fetode_wide_dopri5_xrank_workspace(B, B_total, b_offset, D, H) bytes.  Replaces: the host loop's
+ * one all-reduce + read-back per attempt under dist.odeint_sharded. */
+int fetode_wide_dopri5_xrank(const fetode_kanlinear_t* kan0, const fetode_ferro_t* ferro0, const void* plan0,
+                             const fetode_kanlinear_t* kan1, const fetode_ferro_t* ferro1, const void* plan1,
+                             const float* y0, int64_t B, int64_t B_total, const float* prev0, const float* prev1,
+                             uint32_t reinit_mask, const double* t, int32_t T, double rtol, double atol,
+                             const double* opts, const float* tableau, float* solution, float* state0,
+                             float* state1, void* workspace, int32_t* stats, double* attempts,
+                             int32_t max_attempts, const fetode_xrank_t* xr, void* stream);
+int64_t fetode_wide_dopri5_xrank_workspace(int64_t B, int64_t B_total, int64_t b_offset, int32_t D, int32_t H);
 /* the largest batch one resident dopri5 launch takes on this device (sharded = 1: with the exchange
  * workgroup), 0 if the field has no resident kernel.  Host call (occupancy query, cached). */
 int64_t fetode_integrate_dopri5_max_batch(const fetode_field_t* field, int32_t sharded);
@@ -486,6 +502,9 @@ int fetode_nan_clamp_backward(int64_t n, float nan, float posinf, float neginf, 
 int fetode_kuramoto_forward(const float* x, int64_t B, int32_t H, int32_t W, int32_t steps, float dt, const float* K,
                             const float* omega, float* feat, float* tape, void* stream);
 int64_t fetode_kuramoto_backward_workspace(int64_t B, int32_t H, int32_t W);
+/* 1: the workgroup-per-image LDS kernels for every shape (else lane-per-column register kernels for
+ * W, H <= 32); -1 queries.  Returns the previous setting.  A/B and cross-check knob. */
+int fetode_kuramoto_set_lds(int on);
 int fetode_kuramoto_backward(int64_t B, int32_t H, int32_t W, int32_t steps, float dt, const float* K,
                              const float* tape, const float* gfeat, float* gx, float* gK, float* gomega,
                              void* workspace, void* stream);
