@@ -87,7 +87,7 @@ def _worker(rank, world, port, q, case, sd):
         opt = torch.optim.Adam(m.parameters(), lr=1e-3)
         opt.step()
         w = torch.cat([p.detach().double().cpu().reshape(-1) for p in m.parameters()])
-        q.put((rank, g, w))
+        q.put((rank, g.numpy(), w.numpy()))   # numpy: the worker may exit before the parent reads
     finally:
         dist.destroy_process_group()
 
@@ -112,7 +112,7 @@ def test_data_parallel_training_matches_single_device(dev, case):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (_, g0, w0), (_, g1, w1) = res
+    (_, g0, w0), (_, g1, w1) = [(r, torch.from_numpy(a), torch.from_numpy(b)) for r, a, b in res]
     assert torch.equal(g0, g1) and torch.equal(w0, w1)     # every rank: the same gradient and step
     rel = ((g0 - ref).norm() / ref.norm()).item()
     assert rel <= 1e-5, rel
