@@ -700,15 +700,30 @@ __global__ __launch_bounds__(256) void wide_ferro_bwd_kernel(WideFerroBwdArgs a)
 #pragma unroll
   for (int j = 0; j < kBwdOGW; ++j) anydir |= __builtin_amdgcn_ballot_w64(dir[j]) != 0;
   float* gxp = a.gxp + (int64_t)ogb * a.B * in;
+  // the next row group's U and g are loaded while this one computes (each row group's loads were
+  // a full global-memory round trip on the wave's chain); out-of-range rows read row r0 (valid)
+  auto ld = [&](int64_t b, float4& u, float* go) __attribute__((always_inline)) {
+    const int64_t bc = b < r1 ? b : r0;
+    u = a.U[bc * in + i];
+#pragma unroll
+    for (int j = 0; j < kBwdOGW; ++j) go[j] = a.g[bc * out + oo[j]];
+  };
+  float4 un;
+  float gn[kBwdOGW];
+  ld(r0 + q, un, gn);
   for (int64_t b0 = r0; b0 < r1; b0 += 4) {
     const int64_t b = b0 + q;
     const bool live = b < r1;
-    const float4 u = live ? a.U[b * in + i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 u = live ? un : make_float4(0.f, 0.f, 0.f, 0.f);
+    float gcur[kBwdOGW];
+#pragma unroll
+    for (int j = 0; j < kBwdOGW; ++j) gcur[j] = gn[j];
+    ld(b + 4, un, gn);
     const float xv = u.x, e = u.y, omu = u.z, dup = u.w;
     float dx = 0.f;
 #pragma unroll
     for (int j = 0; j < kBwdOGW; ++j) {
-      const float go = (live && ok[j]) ? a.g[b * out + oo[j]] : 0.f;
+      const float go = (live && ok[j]) ? gcur[j] : 0.f;
       f2 cn;
       if (anydir && dir[j]) cn = rcpx2(ex2x2(pfma(splat(gsl2e), splat(xv), gec[j])) + splat(1.0f));
       else cn = rcpx2(pfma(splat(e), Pf[j], splat(1.0f)));

@@ -205,9 +205,12 @@ def test_fused_backward_kan_vs_oracle_fp64(dev, method):
         assert_grad_close(got[n], exp[n], n, rel=1e-4)
 
 
+@pytest.mark.parametrize("small", [True, False], ids=["v6-tape", "v4-tape"])
 @pytest.mark.parametrize("method", ["rk4", "rk4_classic", "midpoint", "euler"])
-def test_fused_backward_kanfet_vs_oracle_fp64(dev, bwd_split, method):
-    """KAN-FET, 6 points (short enough to be well conditioned in fp32), B=16, every method."""
+def test_fused_backward_kanfet_vs_oracle_fp64(dev, bwd_split, kernel_switch, small, method):
+    """KAN-FET, 6 points (short enough to be well conditioned in fp32), B=16, every method; the
+    taped forward on v6 (the default at this batch) and on v4 (fetode_fused_set_small_batch_max(0))."""
+    kernel_switch(small)
     from oracle import torch_ref as O
     g = load_golden("traj_kanfet")
     t = torch.from_numpy(g["t35"])[:6]
@@ -277,7 +280,7 @@ def test_fused_backward_first_call_rules(dev, bwd_split):
                 assert_grad_close(p.grad, ps[n].grad, f"B={B} call={call} {n}", rel=rel)
 
 
-@pytest.mark.parametrize("kind,npts", [("kan", 35), ("kanfet", 6)])
+@pytest.mark.parametrize("kind,npts", [("kan", 35)])
 def test_small_batch_tape_matches_v4(dev, kernel_switch, kind, npts):
     """At B <= small_max the taped training forward runs on v6 (small6_kernel<..., TAPE>); forcing
     the v4 kernel (fetode_fused_set_small_batch_max(0)) gives the same tape up to the two kernels'
@@ -285,8 +288,10 @@ def test_small_batch_tape_matches_v4(dev, kernel_switch, kind, npts):
     trajectory and output time (sum(w * sol)) makes the gradient as ill-conditioned as the batch's
     worst trajectory (d loss / d y0 up to ~2e3 here), so both are held to the fp64 oracle's autograd
     with the reference's own fp32 autograd as the yardstick: |gpu - fp64| <= 4 |ref fp32 - fp64| +
-    1e-5 scale for the KAN field, every fixed-grid method, and the loss likewise; the KAN-FET field's
-    per-tensor errors scatter with the rounding (below)."""
+    1e-5 scale for the KAN field, every fixed-grid method, and the loss likewise.  (KAN-FET: an
+    all-trajectory loss only measures the hysteresis' fp32 chaos — tools/diag/tape_grad_check.py
+    finds v6, v4 and the reference's own fp32 each 1e-3 .. 5e-2 from fp64, tensor by tensor; both
+    kernels take the short-horizon oracle test below, test_fused_backward_kanfet_vs_oracle_fp64.)"""
     import fet_ode_amd as F
     from oracle import torch_ref as O
     g = load_golden("traj_kanfet" if kind == "kanfet" else "traj_kan")
@@ -327,13 +332,7 @@ def test_small_batch_tape_matches_v4(dev, kernel_switch, kind, npts):
                 ratios.append(err / spread)
                 if kind == "kan":
                     assert err <= 4 * spread, f"{tag} {n}: |gpu-fp64|={err:.3e} ref32 {spread:.3e}"
-            if kind == "kanfet":
-                # hysteresis: which fp32 rounding lands nearer fp64 is luck, tensor by tensor
-                # (tools/diag/tape_grad_check.py: v6 / v4 / reference fp32 each 1e-3 .. 5e-2 from fp64,
-                # either kernel up to ~11x the reference's error on single tensors): the typical error
-                # as the reference's, no tensor an order of magnitude beyond it
-                ratios.sort()
-                assert ratios[len(ratios) // 2] <= 2.0 and ratios[-1] <= 16.0, (tag, ratios)
+
 
 
 def test_fused_backward_matches_per_stage_path_large_batch(dev):
