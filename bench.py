@@ -644,6 +644,60 @@ def ett_dopri5_rate(dev, batch=8192, rtol=1e-3, atol=1e-4, small=256):
     return out
 
 
+def ett_dopri5_train_rate(dev, batch=2048, P=24, tscale=0.05, iters=2, rtol=1e-3, atol=1e-4):
+    """Training through the reference forecaster's own dopri5 call (train_kan_fet_ett.py:192, the
+    loop at :320-335: forward, MSE, loss.backward(), Adam) with the KAN-FET latent field [64, 128, 64].
+    torchdiffeq's direct backprop runs through every stage, the error ratios and the step sizes; here
+    the attempts are host-driven (dopri5._Dopri5Grad: one read-back per attempt) and every field
+    evaluation and VJP is the wide HIP kernels (_WideLayerFn: one launch forward, the Ferro and
+    KANLinear VJPs backward).  The untrained synthetic field is scaled by 0.1 (coef, KAN weights) and
+    the 24 outputs span 1.15 time units so the latent state stays where the reference's own logistic
+    basis has finite gradients (exp overflow x zero adjoint is NaN in its autograd beyond)."""
+    from fet_ode_amd import ett
+    import fet_ode_amd.dopri5  # noqa: F401
+    c = 96
+    torch.manual_seed(0)
+    m = ett.LatentNeuralODEForecaster(num_features=7, context_len=c, pred_len=P, latent_dim=64, solver="dopri5",
+                                      rtol=rtol, atol=atol)
+    with torch.no_grad():
+        for n, p_ in m.dynamics.net.named_parameters():
+            if n.endswith(("coef", "base_weight", "spline_weight", "logistic_weight")):
+                p_.mul_(0.1)
+    m = m.to(dev)
+    g = torch.Generator().manual_seed(4)
+    series = torch.cumsum(torch.randn(batch + c + P, 7, generator=g), 0) * 0.05
+    ds = ett.EnergyWindowDataset(series, series[:, -1], c, P, device=dev)
+    xb, yb = ds.batch(torch.arange(batch, device=dev))
+    t_fut = torch.linspace(0.0, float(P - 1) * tscale, steps=P, device=dev)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-4)
+    fwd, bwd, fin = [], [], True
+    for it in range(iters + 1):
+        opt.zero_grad(set_to_none=True)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        loss = torch.nn.functional.mse_loss(m(xb, t_fut), yb)
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        loss.backward()
+        opt.step()
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
+        fin = fin and bool(torch.isfinite(loss)) and all(bool(torch.isfinite(p_.grad).all())
+                                                         for p_ in m.parameters() if p_.grad is not None)
+        if it > 0:
+            fwd.append(t1 - t0)
+            bwd.append(t2 - t1)
+    s = F.dopri5.dopri5_solve.last
+    el = float(np.mean(fwd) + np.mean(bwd))
+    return {"value": batch / el, "unit": f"training windows/s (fwd + bwd + Adam, dopri5 rtol {rtol:g}, B={batch})",
+            "ms_per_iter": el * 1e3, "fwd_ms": float(np.mean(fwd)) * 1e3, "bwd_ms": float(np.mean(bwd)) * 1e3,
+            "attempts": s.n_attempts, "nfev": s.nfev, "finite": fin,
+            "workload": f"LatentNeuralODEForecaster(7 features, 96->{P}, latent 64, KANFET[64,128,64] K=10, field x0.1), "
+                        f"t_fut = linspace(0, {(P - 1) * tscale:g}, {P}), dopri5 rtol {rtol:g} atol {atol:g}, batch {batch}",
+            "path": "dopri5._Dopri5Grad: host-driven attempts (torchdiffeq's direct backprop incl. the step-size "
+                    "control), the wide HIP layer kernel per evaluation and the wide Ferro / KANLinear VJPs"}
+
+
 def ett_encoder_rate(dev, batch=8192, ctx=96, reps=20, with_cpu=True, cpu_seconds=5.0):
     """The encoder of the reference's KAN-FET ETT model (KAN_FET_LatentODE_DiffusionForecaster,
     train_kan_fet_ett.py:822-837): KANRNNEncoder(7 features, hidden 64, latent 64, 10 bases) over
@@ -1004,6 +1058,7 @@ def main():
             out["ett"] = ett_rate(dev, batch=args.ett_batch, with_cpu=not args.no_cpu_baseline)
             out["ett"]["encoder"] = ett_encoder_rate(dev, with_cpu=not args.no_cpu_baseline)
             out["ett"]["dopri5"] = ett_dopri5_rate(dev, batch=args.ett_batch)
+            out["ett"]["dopri5"]["train"] = ett_dopri5_train_rate(dev)
         if world == 1 and not args.no_cpu_baseline:
             cb, ref_sol = cpu_baseline(sd, y0, t, args.cpu_solves)
             out["cpu_baseline"] = cb
