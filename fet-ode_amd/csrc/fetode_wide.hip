@@ -669,12 +669,17 @@ __global__ __launch_bounds__(256) void wide_ferro_bwd_kernel(WideFerroBwdArgs a)
   const bool act = c < OPG * KP;
   const int ol = act ? c / KP : 0, kp = act ? c % KP : 0;
   const float gs = L.gs, wc = L.wc, gsl2e = L.gsl2e;
-  // this lane's element pairs in the kBwdOGW output groups of the block
-  f2 Pf[kBwdOGW], k2[kBwdOGW], kk[kBwdOGW], Ecv[kBwdOGW], Psv[kBwdOGW], cov[kBwdOGW], bsv[kBwdOGW];
-  f2 gec[kBwdOGW];
+  // this lane's element pairs in the kBwdOGW output groups of the block.  The parameter gradients are
+  // linear in three per-element sums and one per-output sum (as the LV sweep's):
+  //   A = sum g th,  C = sum g r (1 - r) sh,  E = sum gsh (m + Ec dm/dEc),  G = sum g
+  //   dPs = coef A, dbias = coef G, dcoef = Ps A + bias G, dk = 4 coef Ps C, dEc = E
+  // with gsh = g coef Ps 4 r (1 - r) k = g r (1 - r) cPk4 (1 - th^2 = 4 r (1 - r), th = 1 - 2 r:
+  // no cancellation where th saturates), so the row loop carries no coef / Ps / bias products.
+  f2 Pf[kBwdOGW], k2[kBwdOGW], Ecv[kBwdOGW], cPk4[kBwdOGW], gec[kBwdOGW];
   int oo[kBwdOGW];
   bool ok[kBwdOGW], dir[kBwdOGW];
-  f2 sk[kBwdOGW], sE[kBwdOGW], sPs[kBwdOGW], sb[kBwdOGW], sc[kBwdOGW];
+  f2 sA[kBwdOGW], sC[kBwdOGW], sE[kBwdOGW];
+  float sG[kBwdOGW];
 #pragma unroll
   for (int j = 0; j < kBwdOGW; ++j) {
     const int og = ogb * kBwdOGW + j;
@@ -687,14 +692,13 @@ __global__ __launch_bounds__(256) void wide_ferro_bwd_kernel(WideFerroBwdArgs a)
     const float4 a1 = ok[j] ? reinterpret_cast<const float4*>(a.plan + L.fe4)[p0 + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
     Pf[j] = f2{a0.x, a1.x};
     k2[j] = f2{a0.y, a1.y};
-    kk[j] = ok[j] ? f2{a.k[e0], a.k[e0 + 1]} : splat(0.f);
     Ecv[j] = ok[j] ? f2{a.Ec[e0], a.Ec[e0 + 1]} : splat(0.f);
-    Psv[j] = ok[j] ? f2{a.Ps[e0], a.Ps[e0 + 1]} : splat(0.f);
-    cov[j] = ok[j] ? f2{a.coef[e0], a.coef[e0 + 1]} : splat(0.f);
-    bsv[j] = ok[j] ? f2{a.bias[e0], a.bias[e0 + 1]} : splat(0.f);
+    cPk4[j] = ok[j] ? f2{4.0f * a.coef[e0] * a.Ps[e0] * a.k[e0], 4.0f * a.coef[e0 + 1] * a.Ps[e0 + 1] * a.k[e0 + 1]}
+                    : splat(0.f);
     gec[j] = ok[j] ? f2{a.plan[L.gec + p0], a.plan[L.gec + p0 + 1]} : splat(0.f);
     dir[j] = ok[j] && a.plan[L.dflag + (int64_t)oo[j] * in + i] != 0.f;
-    sk[j] = sE[j] = sPs[j] = sb[j] = sc[j] = splat(0.f);
+    sA[j] = sC[j] = sE[j] = splat(0.f);
+    sG[j] = 0.f;
   }
   bool anydir = false;
 #pragma unroll
@@ -720,49 +724,57 @@ __global__ __launch_bounds__(256) void wide_ferro_bwd_kernel(WideFerroBwdArgs a)
     for (int j = 0; j < kBwdOGW; ++j) gcur[j] = gn[j];
     ld(b + 4, un, gn);
     const float xv = u.x, e = u.y, omu = u.z, dup = u.w;
-    float dx = 0.f;
+    // per row: m = 1 + wco cn; dm/dx = a1 cn + a2 cn (1 - cn); dm/dEc = a2 cn (1 - cn)
+    const float wco = wc * omu, a1 = -wc * dup, a2 = -gs * wco;
+    f2 dxacc = splat(0.0f);
 #pragma unroll
     for (int j = 0; j < kBwdOGW; ++j) {
       const float go = (live && ok[j]) ? gcur[j] : 0.f;
       f2 cn;
       if (anydir && dir[j]) cn = rcpx2(ex2x2(pfma(splat(gsl2e), splat(xv), gec[j])) + splat(1.0f));
       else cn = rcpx2(pfma(splat(e), Pf[j], splat(1.0f)));
-      const f2 m = pfma(splat(wc * omu), cn, splat(1.0f));
+      const f2 m = pfma(splat(wco), cn, splat(1.0f));
       const f2 sh = pfma(Ecv[j], m, splat(xv));                     // x + Ec m
       const f2 r = rcpx2(ex2x2(k2[j] * sh) + splat(1.0f));          // 2^{2 log2e k sh}
       const f2 th = pfma(splat(-2.0f), r, splat(1.0f));             // tanh = 1 - 2 / (1 + e^{2 k sh})
-      const f2 gP = splat(go) * cov[j];
-      sc[j] = pfma(splat(go), pfma(Psv[j], th, bsv[j]), sc[j]);
-      sPs[j] = pfma(gP, th, sPs[j]);
-      sb[j] = sb[j] + gP;
-      const f2 gz = gP * Psv[j] * (splat(4.0f) * r * (splat(1.0f) - r));   // 1 - th^2 without cancellation
-      sk[j] = pfma(gz, sh, sk[j]);
-      const f2 gsh = gz * kk[j];
-      const f2 gm = gsh * Ecv[j];
-      const f2 dcn = splat(gs) * cn * (splat(1.0f) - cn);
-      const f2 t1 = splat(omu) * dcn;
-      sE[j] = pfma(gsh, m, sE[j]) - splat(wc) * gm * t1;
-      const f2 dxp = gsh - splat(wc) * gm * pfma(cn, splat(dup), t1);
-      dx += ok[j] ? dxp.x + dxp.y : 0.f;   // idle lanes: e = inf times P = 0 is NaN
+      sA[j] = pfma(splat(go), th, sA[j]);
+      sG[j] += go;
+      const f2 w = splat(go) * (r * (splat(1.0f) - r));             // g (1 - th^2) / 4
+      sC[j] = pfma(w, sh, sC[j]);
+      const f2 gsh = w * cPk4[j];
+      const f2 t = splat(a2) * (cn * (splat(1.0f) - cn));           // dm/dEc
+      sE[j] = pfma(gsh, pfma(Ecv[j], t, m), sE[j]);
+      const f2 dq = pfma(Ecv[j], pfma(splat(a1), cn, t), splat(1.0f));   // d sh/dx = 1 + Ec dm/dx
+      dxacc = ok[j] ? pfma(gsh, dq, dxacc) : dxacc;                 // idle lanes: e = inf times P = 0 is NaN
     }
-    const float row = row_sum16(dx);
+    const float row = row_sum16(dxacc.x + dxacc.y);
     if (c == 0 && live) gxp[b * in + i] = row;
   }
-  // the four row quarters hold the same elements: quarters (0 + 2) + (1 + 3) onto lanes 0..15
+  // the four row quarters hold the same elements: quarters (0 + 2) + (1 + 3) onto lanes 0..15, then
+  // the sums -> this row segment's parameter-gradient partials (reference layout)
   float* pp = a.pp + (int64_t)sgi * in * out * K * 5;
+  auto qsum = [&](float p) __attribute__((always_inline)) {
+    float qq = p;
+    permlane32_swap(p, qq);
+    float s2 = p + qq, s3 = s2;
+    permlane16_swap(s2, s3);
+    return s2 + s3;
+  };
 #pragma unroll
   for (int j = 0; j < kBwdOGW; ++j) {
-    f2 v[5] = {sk[j], sE[j], sPs[j], sb[j], sc[j]};
+    const float G = qsum(sG[j]);
 #pragma unroll
-    for (int t = 0; t < 5; ++t) {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        float p = h ? v[t].y : v[t].x, qq = p;
-        permlane32_swap(p, qq);
-        float s2 = p + qq, s3 = s2;
-        permlane16_swap(s2, s3);
-        const float tot = s2 + s3;
-        if (lane < 16 && ok[j]) pp[(((int64_t)i * out + oo[j]) * K + 2 * kp + h) * 5 + t] = tot;
+    for (int h = 0; h < 2; ++h) {
+      const float A = qsum(h ? sA[j].y : sA[j].x), C = qsum(h ? sC[j].y : sC[j].x), E = qsum(h ? sE[j].y : sE[j].x);
+      if (lane < 16 && ok[j]) {
+        const int64_t el = ((int64_t)i * out + oo[j]) * K + 2 * kp + h;
+        const float co = a.coef[el], ps = a.Ps[el], bi = a.bias[el];
+        float* d = pp + el * 5;
+        d[0] = 4.0f * co * ps * C;   // k
+        d[1] = E;                    // Ec
+        d[2] = co * A;               // Ps
+        d[3] = co * G;               // bias
+        d[4] = ps * A + bi * G;      // coef
       }
     }
   }
