@@ -1784,7 +1784,7 @@ int fetode_backward_set_split(int32_t enable) {
 
 int fetode_fused_backward_supported(const fetode_field_t* f) {
   if (validate_field(f) != FETODE_OK) return 0;
-  return find_bwd(f) != nullptr;
+  return find_bwd(f) != nullptr || fieldn_shape_supported(f);
 }
 
 // the one-kernel sweep at one trajectory per wave while those waves fit one resident round
@@ -1813,7 +1813,8 @@ int64_t sum_rows(const BwdEntry* e, int64_t B, int64_t n_ev) {
 }
 
 int64_t fetode_integrate_fixed_backward_workspace(const fetode_field_t* f, int32_t method, int32_t n_steps, int64_t B) {
-  if (validate_field(f) != FETODE_OK || !find_bwd(f) || B <= 0 || n_steps < 0) return -1;
+  if (validate_field(f) != FETODE_OK || B <= 0 || n_steps < 0) return -1;
+  if (!find_bwd(f)) return fieldn_shape_supported(f) ? fieldn_fixed_backward_workspace(f, method, n_steps, B) : -1;
   const BwdEntry* e = find_bwd(f);
   AccLayout L0, L1;
   layouts(f, &L0, &L1);
@@ -1834,13 +1835,18 @@ int fetode_integrate_fixed_backward(const fetode_field_t* f, const void* plan, i
   int rc = validate_field(f);
   if (rc) return rc;
   const BwdEntry* e = find_bwd(f);
-  if (!e) return set_err(FETODE_EUNSUPPORTED, "no fused backward kernel for this field shape");
+  const bool fieldn = !e && fieldn_shape_supported(f);  // other widths: fetode_fieldn_bwd.hip
+  if (!e && !fieldn) return set_err(FETODE_EUNSUPPORTED, "no fused backward kernel for this field shape");
   if (method < FETODE_EULER || method > FETODE_RK4_CLASSIC) return set_err(FETODE_EINVAL, "unknown method %d", method);
   if (B <= 0 || T <= 0) return FETODE_OK;
   if (!plan || !grad_solution || !workspace || (n_steps > 0 && (!tape || !step_coef || !out_step || !out_mode ||
                                                                  !out_slope)) ||
       (f->ferro && !state0 && (init_mask & 3u) != 3u))
     return set_err(FETODE_EINVAL, "null pointer");
+  if (fieldn)
+    return fieldn_fixed_backward(f, plan, method, B, step_coef, n_steps, out_step, out_mode, out_slope, T,
+                                 grad_solution, tape, state0, init_mask, grad_y0, kan_grads, ferro_grads, workspace,
+                                 stream);
   hipStream_t s = (hipStream_t)stream;
   AccLayout AL0, AL1;
   layouts(f, &AL0, &AL1);

@@ -50,6 +50,16 @@ struct LayerPlan {
 void layer_plan(const fetode_kanlinear_t& kl, const fetode_ferro_t* fl, int64_t base, LayerPlan* p);
 int validate_field(const fetode_field_t* f);
 
+// depth-2 fields of other widths served by fieldn_kernel (fetode_fused.hip), and their reverse
+// sweep (fetode_fieldn_bwd.hip): arguments and workspace as fetode_integrate_fixed_backward
+bool fieldn_shape_supported(const fetode_field_t* f);
+int64_t fieldn_fixed_backward_workspace(const fetode_field_t* f, int32_t method, int32_t n_steps, int64_t B);
+int fieldn_fixed_backward(const fetode_field_t* f, const void* plan, int32_t method, int64_t B, const float* step_coef,
+                          int32_t n_steps, const int32_t* out_step, const int32_t* out_mode, const float* out_slope,
+                          int32_t T, const float* grad_solution, const float* tape, const float* state0,
+                          uint32_t init_mask, float* grad_y0, const fetode_kanlinear_grad_t* kan_grads,
+                          const fetode_ferro_grad_t* ferro_grads, void* workspace, void* stream);
+
 // Launch of a grid that must be co-resident (the device-resident solvers' grid reductions).  The
 // callers size the grid by occupancy; by default it is an ordinary launch (bounded spins turn a
 // grid that is not co-resident into status 4), or hipLaunchCooperativeKernel when switched on

@@ -1525,8 +1525,10 @@ const FusedEntry* find_fused(const fetode_field_t* f) {
 // hidden unit o.  Per evaluation, lane o forms h_o from the D layer inputs (their features are
 // recomputed on every lane: D is small) and then its own input's features and contributions to
 // all D outputs; a butterfly sum over the lanes gives k.  The arithmetic is the fused kernels'
-// (the same plan and element formulas), the sums run in another order.  Inference only: training
-// tapes, the resident dopri5 and the fused backward exist for the specialised [2, 10, 2] shapes.
+// (the same plan and element formulas), the sums run in another order.  Training: the
+// launch records both layers' inputs of every evaluation (two tape planes); the reverse sweep is
+// fieldn_adj_kernel + the per-module parameter VJPs over every (evaluation, trajectory) row
+// (fetode_fieldn_bwd.hip).  The resident dopri5 exists for the specialised [2, 10, 2] shapes only.
 // =============================================================================================
 constexpr int kFnMaxD = 8, kFnMaxH = 64;
 constexpr int kFnWaves = 4;
@@ -1573,11 +1575,20 @@ __device__ __forceinline__ void fn_interval(const float* __restrict__ plan, cons
   u = mfix < P.NI ? (x - g[mfix]) * plan[P.rh + (int64_t)i * P.NI + mfix] : (fin ? 0.0f : __builtin_nanf(""));
 }
 
-template <bool FERRO>
-__global__ __launch_bounds__(64 * kFnWaves) void fieldn_kernel(FusedArgs a) {
-  __shared__ float s_x[kFnWaves][kFnMaxD], s_k[kFnWaves][kFnMaxD], s_p0[kFnWaves][kFnMaxD];
+// DOPRI: the whole dopri5 solve in this launch (fetode_integrate_dopri5 for these shapes), one
+// trajectory per one-wave workgroup, every workgroup resident (grid sums of the error norms)
+template <bool FERRO, bool DOPRI = false>
+__global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(FusedArgs a) {
+  constexpr int NW = DOPRI ? 1 : kFnWaves;
+  if constexpr (DOPRI) {
+    if (a.dp.xr_world > 1 && blockIdx.x == gridDim.x - 1) {  // the cross-rank exchange workgroup
+      xrank_comm(a.dp);
+      return;
+    }
+  }
+  __shared__ float s_x[NW][kFnMaxD], s_k[NW][kFnMaxD], s_p0[NW][kFnMaxD];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * kFnWaves + wid;
+  const int64_t b = (int64_t)blockIdx.x * NW + wid;
   const bool valid = b < a.B;
   const LayerPlan& P0 = a.P0;
   const LayerPlan& P1 = a.P1;
@@ -1594,8 +1605,15 @@ __global__ __launch_bounds__(64 * kFnWaves) void fieldn_kernel(FusedArgs a) {
   }
   bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
   const float c0o = hl ? plan[P0.fconst + lane] : 0.f;
+  // training tape (fieldn_adj_kernel, fetode_fieldn_bwd.hip): two planes, the layer-0 inputs
+  // (n_ev, B, D) then the layer-1 inputs (n_ev, B, H), one row per evaluation
+  const int nst = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4 : a.method == FETODE_MIDPOINT ? 2 : 1;
+  float* tx = (a.tape && !a.single_eval) ? a.tape : nullptr;
+  float* th_ = tx ? tx + (int64_t)a.n_steps * nst * a.B * D : nullptr;
+  int64_t ev = 0;
   auto eval = [&](void) {  // xs -> ks (all lanes), hysteresis states updated
     fn_wsync();
+    if (tx && valid && lane < D) tx[(ev * a.B + b) * D + lane] = xs[lane];
     // layer 0: h_o
     float h = 0.f;
     if (hl) {
@@ -1611,6 +1629,8 @@ __global__ __launch_bounds__(64 * kFnWaves) void fieldn_kernel(FusedArgs a) {
         h += fn_edge<FERRO>(plan, P0, lane, i, x, sx, w, mfix, u);
       }
     }
+    if (tx && valid && hl) th_[(ev * a.B + b) * H + lane] = h;
+    ++ev;
     fn_wsync();
     if (FERRO && lane < D) p0[lane] = xs[lane];  // ferro_class.py:409
     re0 = false;
@@ -1635,7 +1655,137 @@ __global__ __launch_bounds__(64 * kFnWaves) void fieldn_kernel(FusedArgs a) {
   // lane d < D carries state dim d
   const bool dl = lane < D;
   float y = (valid && dl) ? a.y0[b * D + lane] : 0.f;
-  if (a.single_eval) {
+  if constexpr (DOPRI) {
+    // ---- device-resident dopri5: fused4's driver (dopri5.py _Dopri5's control arithmetic) with
+    // lane d < D of the trajectory's wave carrying y_d; one grid sum per norm ----
+    const DopriParams& P = a.dp;
+    const bool real = valid && dl;  // one lane per (trajectory, state dim) in the sums
+    const double n_el = P.n_total;
+    int nfev = 0, n_att = 0, status = 0;
+    unsigned round = 0;
+    auto gsum2 = [&](double v0, double v1, double& s0, double& s1) {
+      v0 = xor_sum64(v0);
+      v1 = xor_sum64(v1);
+      if (grid_sum2(P, round, v0, v1, s0, s1)) status = 4;
+    };
+    auto f = [&](float xin) -> float {
+      if (dl) xs[lane] = xin;
+      eval();
+      return dl ? ks[lane] : 0.f;
+    };
+    if (real) a.solution[b * D + lane] = y;
+    float f0 = f(y);
+    ++nfev;
+    double dt;
+    if (P.first_step > 0.0) {
+      dt = P.first_step;
+    } else {  // misc._select_initial_step in fp32 (dopri5.py select_initial_step)
+      const float scale = P.atol + P.rtol * fabsf(y);
+      const float q0 = y / scale, q1 = f0 / scale;
+      double s0, s1;
+      gsum2(real ? (double)q0 * q0 : 0.0, real ? (double)q1 * q1 : 0.0, s0, s1);
+      const float d0 = fabsf(sqrtf((float)(s0 / n_el)));
+      const float d1 = fabsf(sqrtf((float)(s1 / n_el)));
+      float h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : (0.01f * d0) / d1;
+      h0 = fabsf(h0);
+      const float f1 = f(y + f0 * h0);
+      ++nfev;
+      const float q2 = (f1 - f0) / scale;
+      gsum2(real ? (double)q2 * q2 : 0.0, 0.0, s0, s1);
+      const float d2 = fabsf(sqrtf((float)(s0 / n_el)) / h0);
+      float h1;
+      if (d1 <= 1e-15f && d2 <= 1e-15f) h1 = fmaxf(1e-6f, h0 * 1e-3f);
+      else h1 = (float)pow((double)(0.01f / fmaxf(d1, d2)), (double)0.2f);  // fp64 pow rounded once
+      dt = (double)fminf(100.0f * h0, fabsf(h1));
+    }
+    float co[5] = {y, 0.f, 0.f, 0.f, 0.f};
+    double t0s = P.t[0], t1s = P.t[0];
+    for (int i = 1; i < P.T && status == 0; ++i) {
+      const double next_t = P.t[i];
+      int n_steps = 0;
+      while (next_t > t1s) {
+        if (n_steps >= P.max_steps) { status = 3; break; }
+        const double t0 = t1s;
+        if (!(t0 + dt > t0)) { status = 2; break; }
+        const float dt32 = (float)dt;
+        const double t1 = t0 + dt;
+        // rk_common._runge_kutta_step in fetode_lincomb's op order, accumulated as the stages
+        // arrive: A[q] is stage s + 1 + q's sum k0 c0 + k1 c1 + ... (left-to-right sums)
+        float A[6];
+        for (int q = 0; q < 6; ++q) A[q] = f0 * (P.stc[0][q] * dt32);
+        float err = f0 * (P.stc[0][6] * dt32);
+        float mid = f0 * (P.stc[0][7] * dt32);
+        float yi = y, kn = f0;
+        for (int st = 0; st < 6; ++st) {
+          yi = y + A[0];
+          kn = f(yi);
+          ++nfev;
+          for (int q = 0; q < 5; ++q) A[q] = A[q + 1] + kn * (P.stc[st + 1][q] * dt32);
+          err = err + kn * (P.stc[st + 1][6] * dt32);
+          mid = mid + kn * (P.stc[st + 1][7] * dt32);
+        }
+        const float y1 = yi;
+        const float tol = P.atol + P.rtol * fmaxf(fabsf(y), fabsf(y1));
+        const float qe = err / tol;
+        double sq, nbad;
+        gsum2(real ? (double)qe * qe : 0.0, (real && !__builtin_isfinite(y)) ? 1.0 : 0.0, sq, nbad);
+        if (status) break;
+        if (nbad != 0.0) { status = 1; break; }
+        const float ratio = sqrtf((float)(sq / n_el));
+        const bool accept = ratio <= 1.0f;
+        if (blockIdx.x == 0 && threadIdx.x == 0 && n_att < P.max_att) {
+          double* o = P.att + (int64_t)n_att * 4;
+          o[0] = t0;
+          o[1] = dt;
+          o[2] = (double)ratio;
+          o[3] = accept ? 1.0 : 0.0;
+        }
+        ++n_att;
+        if (accept) {  // interp._interp_fit (fetode_interp_fit's op order)
+          const float ym = y + mid, fa = f0, fb6 = kn;
+          co[4] = ((2.0f * dt32) * (fb6 - fa) - 8.0f * (y1 + y)) + 16.0f * ym;
+          co[3] = ((dt32 * (5.0f * fa - 3.0f * fb6) + 18.0f * y) + 14.0f * y1) - 32.0f * ym;
+          co[2] = ((dt32 * (fb6 - 4.0f * fa) - 11.0f * y) - 5.0f * y1) + 16.0f * ym;
+          co[1] = dt32 * fa;
+          co[0] = y;
+          y = y1;
+          f0 = kn;
+          t0s = t0;
+          t1s = t1;
+        } else {
+          t0s = t0;
+        }
+        // rk_common._optimal_step_size in fp64 (dopri5.py optimal_step)
+        const double rr = (double)ratio;
+        double nxt;
+        if (rr == 0.0) {
+          nxt = dt * P.ifactor;
+        } else {
+          const double dfac = rr < 1.0 ? 1.0 : P.dfactor;
+          const double factor = __builtin_isnan(rr) ? rr : fmin(P.ifactor, fmax(P.safety / pow(rr, 1.0 / 5.0), dfac));
+          nxt = dt * factor;
+        }
+        dt = __builtin_isnan(nxt) ? nxt : fmin(fmax(nxt, P.min_step), P.max_step);
+        ++n_steps;
+      }
+      if (status) break;
+      const float xq = (float)((next_t - t0s) / (t1s - t0s));  // interp._interp_evaluate
+      float total = co[0] + xq * co[1];
+      float xp = xq;
+      for (int j = 2; j < 5; ++j) {
+        xp = xp * xq;
+        total = total + xp * co[j];
+      }
+      if (real) a.solution[((int64_t)i * a.B + b) * D + lane] = total;
+    }
+    if (P.xr_world > 1 && blockIdx.x == 0 && threadIdx.x == 0)  // the exchange workgroup may stop
+      __hip_atomic_store(dp_fin(P), round + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      P.stats[0] = nfev;
+      P.stats[1] = n_att;
+      P.stats[2] = __hip_atomic_load(P.bar + kDpLine * (kDpGroups + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 4 : status;
+    }
+  } else if (a.single_eval) {
     if (dl) xs[lane] = y;
     eval();
     if (valid && dl) a.eval_out[b * D + lane] = ks[lane];
@@ -1706,7 +1856,7 @@ bool fieldn_supported(const fetode_field_t* f) {
 int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
   const FusedEntry* e = find_fused(f);
   if (!e) {  // other widths: the generic single-launch kernel (inference and single evaluations)
-    if (!fieldn_supported(f) || a.tape) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
+    if (!fieldn_supported(f)) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
     layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
     layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
     hipLaunchKernelGGL(f->ferro ? fieldn_kernel<true> : fieldn_kernel<false>, dim3(nblk(a.B, kFnWaves)),
@@ -1733,6 +1883,8 @@ int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
 }
 
 }  // namespace
+
+bool fetode::fieldn_shape_supported(const fetode_field_t* f) { return find_fused(f) == nullptr && fieldn_supported(f); }
 
 extern "C" {
 
@@ -1804,9 +1956,29 @@ static int64_t dopri5_resident_wgs(const FusedEntry* e, bool ferro) {
   return (int64_t)per_cu[fi] * n_cu;
 }
 
+// fieldn's dopri5 driver: one trajectory per one-wave workgroup, every one resident
+static int64_t dopri5_fieldn_resident_wgs(bool ferro) {
+  static int n_cu = 0, per_cu[2] = {0, 0};
+  const int fi = ferro ? 0 : 1;
+  if (!n_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return -1;
+  }
+  if (!per_cu[fi] && hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                         &per_cu[fi], ferro ? (const void*)fieldn_kernel<true, true> : (const void*)fieldn_kernel<false, true>,
+                         64, 0) != hipSuccess)
+    return -1;
+  return (int64_t)per_cu[fi] * n_cu;
+}
+
 int64_t fetode_integrate_dopri5_max_batch(const fetode_field_t* f, int32_t sharded) {
   if (validate_field(f) != FETODE_OK) return 0;
   const FusedEntry* e = find_fused(f);
+  if (!e && fieldn_supported(f)) {
+    const int64_t w = dopri5_fieldn_resident_wgs(f->ferro != nullptr) - (sharded ? 1 : 0);
+    return w > 0 ? w : 0;
+  }
   if (!e) return 0;
   const int64_t w = dopri5_resident_wgs(e, f->ferro != nullptr) - (sharded ? 1 : 0);
   return w > 0 ? 2 * w : 0;
@@ -1825,15 +1997,19 @@ static int dopri5_launch(const fetode_field_t* f, const void* plan, const float*
   if (f->kan[0].in_features != f->kan[f->n_layers - 1].out_features)
     return set_err(FETODE_EINVAL, "field is not R^D -> R^D");
   const FusedEntry* e = find_fused(f);
-  if (!e) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
+  // other widths: fieldn's driver, one trajectory per one-wave workgroup (no taped variant)
+  const bool fn = !e && fieldn_supported(f) && !(tape_cap > 0);
+  if (!e && !fn) return set_err(FETODE_EUNSUPPORTED, "no fused dopri5 kernel for this field shape");
   const bool sharded = xr && xr->world > 1;
   // small batches (the reference's own X0 (1, 2); the strong-scaled shard): v6, one trajectory per
   // workgroup, when the whole grid is resident; else v4, two per one-wave workgroup
-  const int64_t res6 = (!sharded && B <= small_max()) ? dopri5_small_resident_wgs(e, f->ferro != nullptr) : -1;
+  const int64_t res6 = (!fn && !sharded && B <= small_max()) ? dopri5_small_resident_wgs(e, f->ferro != nullptr) : -1;
   const bool use6 = res6 >= B;
-  const int64_t resident = use6 ? res6 : dopri5_resident_wgs(e, f->ferro != nullptr);
+  const int64_t resident = fn ? dopri5_fieldn_resident_wgs(f->ferro != nullptr)
+                              : use6 ? res6 : dopri5_resident_wgs(e, f->ferro != nullptr);
   if (resident < 0) return set_err(FETODE_EHIP, "dopri5: occupancy query failed");
-  const int64_t grid = use6 ? B : nblk(B, 2);
+  const int per = fn ? 1 : 2;  // trajectories per workgroup (v6: one, never sharded)
+  const int64_t grid = (use6 || fn) ? B : nblk(B, 2);
   const int64_t lgrid = grid + (sharded ? 1 : 0);   // + the cross-rank exchange workgroup
   if (lgrid > resident)
     return set_err(FETODE_EUNSUPPORTED, "dopri5: batch %lld needs %lld workgroups, %lld resident", (long long)B,
@@ -1902,9 +2078,9 @@ static int dopri5_launch(const fetode_field_t* f, const void* plan, const float*
     P.xr_epoch = xr->epoch;
     P.xr_peers = (double* const*)xr->peers;
     P.xr_inbox = (double*)xr->inbox;
-    const int64_t gg = cdiv(B_total, 2), shg = lshift(gg), Bk = (int64_t)8 << shg, off = xr->b_offset / 2;
+    const int64_t gg = cdiv(B_total, per), shg = lshift(gg), Bk = (int64_t)8 << shg, off = xr->b_offset / per;
     const bool last = xr->b_offset + B == B_total;
-    if (xr->b_offset % 2 == 0 && (B % 2 == 0 || last) && off % Bk == 0 && ((off + grid) % Bk == 0 || last)) {
+    if (xr->b_offset % per == 0 && (B % per == 0 || last) && off % Bk == 0 && ((off + grid) % Bk == 0 || last)) {
       P.xr_exact = 1;
       P.wg_off = (int32_t)off;
       P.nblk_global = (int32_t)gg;
@@ -1922,9 +2098,10 @@ static int dopri5_launch(const fetode_field_t* f, const void* plan, const float*
   hipStream_t s = (hipStream_t)stream;
   HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kDpBarWords, s));
   void* args[] = {&a};
-  const void* fn = use6 ? (const void*)(a.tape ? e->small_dopri_tape : e->small_dopri)
-                        : (const void*)(a.tape ? e->dopri_tape : e->dopri);
-  HIP_CHECK_RET(resident_launch(fn, dim3((unsigned)lgrid), dim3(use6 ? 192 : 64), args, 0, s));
+  const void* kfn = fn ? (f->ferro ? (const void*)fieldn_kernel<true, true> : (const void*)fieldn_kernel<false, true>)
+                   : use6 ? (const void*)(a.tape ? e->small_dopri_tape : e->small_dopri)
+                          : (const void*)(a.tape ? e->dopri_tape : e->dopri);
+  HIP_CHECK_RET(resident_launch(kfn, dim3((unsigned)lgrid), dim3(use6 ? 192 : 64), args, 0, s));
   return FETODE_OK;
 }
 

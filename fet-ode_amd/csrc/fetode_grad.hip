@@ -552,6 +552,171 @@ __global__ void kan_scale_ls_kernel(fetode_kanlinear_t kl, const float* __restri
   put(gr.logistic_scaler ? gr.logistic_scaler + t : nullptr, dls, accumulate);
 }
 
+// ------------------------------------------------------------------------------------------
+// Parameter sums over many rows (B >= kPsMinRows: the fieldn training pass runs them over every
+// (evaluation, trajectory) row, fetode_fieldn_bwd.hip): workgroup (input i, row split s) walks
+// tiles of kPsTile rows — each row's NF features of x[r, i] formed ONCE (kan_gw_kernel forms them
+// once per (o, i, f) block: out * NF times), the tile's g rows staged — and every thread sums a
+// 4 x 4 block of (feature, output) products over its share of the tile's rows; the logistic a / b
+// sums ride along per row.  Per-thread partials -> fixed-order workgroup sums -> per-split slots
+// -> kan_psum_reduce_kernel sums the splits in order (run-to-run identical).
+// ------------------------------------------------------------------------------------------
+constexpr int kPsTile = 64, kPsMaxNF = 40, kPsMaxOut = 64, kPsMinRows = 2048, kPsBlocks = 2048;
+int ps_splits(int in, int64_t B) {
+  int64_t S = kPsBlocks / in;
+  const int64_t tiles = (B + kPsTile - 1) / kPsTile;
+  if (S > tiles) S = tiles;
+  return S < 1 ? 1 : (int)S;
+}
+int ps_smax(int in) { return kPsBlocks / in > 1 ? kPsBlocks / in : 1; }
+
+template <int SO>
+__global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, const float* __restrict__ x,
+                                                      const float* __restrict__ g, int64_t B,
+                                                      float* __restrict__ part /* (S, in, NF, out) */,
+                                                      float* __restrict__ abpart /* (S, in, NB, 2) */) {
+  __shared__ float ft[kPsTile][kPsMaxNF + 1];
+  __shared__ float gt[kPsTile][kPsMaxOut + 1];
+  __shared__ float wl[kPsMaxOut][kMaxLogistic];
+  __shared__ float red[256 * 16];
+  const int in = kl.in_features, out = kl.out_features, NB = kl.num_logistic;
+  const int NG = kl.grid_size + 2 * SO + 1, NS = kl.grid_size + SO, NF = 1 + NS + NB;
+  const int i = blockIdx.x, s = blockIdx.y, S = gridDim.y, tid = threadIdx.x;
+  const int64_t tiles = (B + kPsTile - 1) / kPsTile;
+  const int64_t t0 = s * tiles / S, t1 = (s + 1) * tiles / S;
+  // the logistic weights W'[o, (i, j)] of this input (a / b sums)
+  for (int q = tid; q < out * NB; q += 256) {
+    const int o = q / NB, j = q % NB;
+    const float ls = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
+    wl[o][j] = (kl.logistic_weight[(int64_t)o * in * NB + i * NB + j] * kl.scale_logistic) * ls;
+  }
+  // this thread's (feature, output) block and its share of the tile's rows
+  const int FBK = (NF + 3) / 4, OBK = (out + 3) / 4, P = FBK * OBK, Q = P < 256 ? 256 / P : 1;
+  const int p = tid % P, q = tid / P;
+  const bool act = tid < P * Q;
+  const int f0 = 4 * (p / OBK), o0 = 4 * (p % OBK);
+  float acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[a][c] = 0.f;
+  float la[kMaxLogistic], lb[kMaxLogistic];
+#pragma unroll
+  for (int j = 0; j < kMaxLogistic; ++j) la[j] = lb[j] = 0.f;
+  const float* gi = kl.grid + (int64_t)i * NG;
+  for (int64_t tl = t0; tl < t1; ++tl) {
+    const int64_t r0 = tl * kPsTile;
+    __syncthreads();  // the previous tile's reads are done
+    for (int e = tid; e < kPsTile * out; e += 256) {
+      const int rr = e / out, o = e % out;
+      gt[rr][o] = r0 + rr < B ? g[(r0 + rr) * out + o] : 0.f;
+    }
+    if (tid < kPsTile) {  // row r0 + tid: the features as kan_gw_kernel forms them
+      const bool live = r0 + tid < B;
+      const float xv = live ? x[(r0 + tid) * in + i] : 0.f;
+      float* fr = ft[tid];
+      fr[0] = live ? xv * sigm(xv) : 0.f;
+      float val[SO + 1], der[SO + 1];
+      const int m = bspline_vals_derivs<SO>(xv, NG, gi, val, der);
+      for (int c = 0; c < NS; ++c) {
+        float v = (live && m == -2) ? __builtin_nanf("") : 0.f;
+#pragma unroll
+        for (int rr = 0; rr <= SO; ++rr)
+          if (live && m >= 0 && m - SO + rr == c) v = val[rr];
+        fr[1 + c] = v;
+      }
+      for (int j = 0; j < NB; ++j)
+        fr[1 + NS + j] = live ? 2.0f / (1.0f + expf(-kl.logistic_a[i * NB + j] * (xv - kl.logistic_b[i * NB + j]))) : 0.f;
+    }
+    __syncthreads();
+    if (tid < kPsTile && NB > 0 && r0 + tid < B) {  // logistic a / b: d phi_j through the row's g
+      const float xv = x[(r0 + tid) * in + i];
+      for (int j = 0; j < NB && j < kMaxLogistic; ++j) {
+        float gphi = 0.f;
+        for (int o = 0; o < out; ++o) gphi += gt[tid][o] * wl[o][j];
+        const float a = kl.logistic_a[i * NB + j], bb = kl.logistic_b[i * NB + j];
+        const float sg = 0.5f * ft[tid][1 + NS + j];  // sigm(a (x - b))
+        const float dz = gphi * 2.0f * sg * (1.0f - sg);
+        la[j] += dz * (xv - bb);
+        lb[j] += dz * (-a);
+      }
+    }
+    if (act) {
+      for (int rr = q; rr < kPsTile; rr += Q) {
+        float fv[4], gv[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) fv[a] = f0 + a < NF ? ft[rr][f0 + a] : 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) gv[c] = o0 + c < out ? gt[rr][o0 + c] : 0.f;
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) acc[a][c] = ffma(fv[a], gv[c], acc[a][c]);
+      }
+    }
+  }
+  // workgroup sums in a fixed order: the Q row groups of each block, then the tile rows' a / b
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) red[tid * 16 + a * 4 + c] = acc[a][c];
+  __syncthreads();
+  float* dst = part + ((int64_t)s * in + i) * NF * out;
+  for (int e = tid; e < P * 16; e += 256) {
+    const int pp = e / 16, ac = e % 16, a = ac / 4, c = ac % 4;
+    const int f = 4 * (pp / OBK) + a, o = 4 * (pp % OBK) + c;
+    float v = 0.f;
+    for (int qq = 0; qq < Q; ++qq) v += red[(qq * P + pp) * 16 + ac];
+    if (f < NF && o < out) dst[f * out + o] = v;
+  }
+  if (NB > 0) {
+    __syncthreads();
+    for (int j = 0; j < NB && j < kMaxLogistic; ++j) {
+      if (tid < kPsTile) {
+        red[tid * 2] = la[j];
+        red[tid * 2 + 1] = lb[j];
+      }
+      __syncthreads();
+      if (tid < 2) {
+        float v = 0.f;
+        for (int rr = 0; rr < kPsTile; ++rr) v += red[rr * 2 + tid];
+        abpart[(((int64_t)s * in + i) * NB + j) * 2 + tid] = v;
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// the splits in order -> base-weight gradient, d_scaled, d_wl, logistic a / b
+__global__ void kan_psum_reduce_kernel(fetode_kanlinear_t kl, const float* __restrict__ part,
+                                       const float* __restrict__ abpart, int S, float* __restrict__ d_scaled,
+                                       float* __restrict__ d_wl, fetode_kanlinear_grad_t gr, int accumulate) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int in = kl.in_features, out = kl.out_features, NB = kl.num_logistic;
+  const int NS = kl.grid_size + kl.spline_order, NF = 1 + NS + NB;
+  const int64_t nw = (int64_t)out * in * NF;
+  if (t < nw) {
+    const int f = (int)(t % NF);
+    const int64_t oi = t / NF;
+    const int o = (int)(oi / in), i = (int)(oi % in);
+    float v = 0.f;
+    for (int sp = 0; sp < S; ++sp) v += part[(((int64_t)sp * in + i) * NF + f) * out + o];
+    if (f == 0) put(gr.base_weight ? gr.base_weight + (int64_t)o * in + i : nullptr, v, accumulate);
+    else if (f <= NS) d_scaled[((int64_t)o * in + i) * NS + (f - 1)] = v;
+    else d_wl[(int64_t)o * in * NB + i * NB + (f - 1 - NS)] = v;
+  } else if (t < nw + (int64_t)in * NB) {
+    const int q = (int)(t - nw);  // (i, j)
+    float va = 0.f, vb = 0.f;
+    for (int sp = 0; sp < S; ++sp) {
+      va += abpart[((int64_t)sp * in * NB + q) * 2];
+      vb += abpart[((int64_t)sp * in * NB + q) * 2 + 1];
+    }
+    put(gr.logistic_a ? gr.logistic_a + q : nullptr, va, accumulate);
+    put(gr.logistic_b ? gr.logistic_b + q : nullptr, vb, accumulate);
+  }
+}
+
 // logistic basis parameters a, b: one block per (i, j)
 __global__ void kan_gab_kernel(fetode_kanlinear_t kl, const float* __restrict__ x, const float* __restrict__ g,
                                int64_t B, fetode_kanlinear_grad_t gr, int accumulate) {
@@ -679,6 +844,11 @@ __global__ void ferro_gp_kernel(fetode_ferro_t fl, const float* __restrict__ x, 
   }
 }
 
+bool ps_ok(const fetode_kanlinear_t* kl) {
+  const int NF = 1 + kl->grid_size + kl->spline_order + kl->num_logistic;
+  return kl->spline_order == 3 && NF <= kPsMaxNF && kl->out_features <= kPsMaxOut && kl->num_logistic <= kMaxLogistic;
+}
+
 }  // namespace
 
 extern "C" {
@@ -689,6 +859,9 @@ int64_t fetode_kanlinear_backward_workspace(const fetode_kanlinear_t* kl) {
   int64_t n = (int64_t)kl->out_features * kl->in_features * (NS + kl->num_logistic);
   if (fetode_kanlinear_wide_supported(kl))   // MFMA partials + logistic a / b partials
     n += (int64_t)kGwSplit * kl->in_features * (kGwF * 16 + 2 * kGwNB);
+  else if (ps_ok(kl))                        // kan_psum_kernel's per-split partials
+    n += (int64_t)ps_smax(kl->in_features) * kl->in_features *
+         ((int64_t)(1 + NS + kl->num_logistic) * kl->out_features + 2 * kl->num_logistic);
   return (int64_t)sizeof(float) * n;
 }
 
@@ -737,6 +910,16 @@ int fetode_kanlinear_backward(const fetode_kanlinear_t* kl, const float* x, int6
       hipLaunchKernelGGL(wide_gw_reduce_kernel, dim3(nblk((int64_t)out * in * kGwF, 256)), dim3(256), 0, s, *kl, dpart,
                          d_scaled, d_wl, *grads, accumulate);
       LAUNCH_CHECK();
+    } else if (B >= kPsMinRows && ps_ok(kl)) {   // many rows: features once per (row, input)
+      const int S = ps_splits(in, B);
+      float* part = d_wl + (int64_t)out * in * NB;
+      float* abpart = part + (int64_t)ps_smax(in) * in * (1 + NS + NB) * out;
+      hipLaunchKernelGGL(kan_psum_kernel<3>, dim3(in, S), dim3(256), 0, s, *kl, x, g, B, part, abpart);
+      LAUNCH_CHECK();
+      const int64_t nt = (int64_t)out * in * (1 + NS + NB) + (int64_t)in * NB;
+      hipLaunchKernelGGL(kan_psum_reduce_kernel, dim3(nblk(nt, 256)), dim3(256), 0, s, *kl, part, abpart, S, d_scaled,
+                         d_wl, *grads, accumulate);
+      LAUNCH_CHECK();
     } else {
       const int nblocks = out * in * (1 + NS + NB);
 #define KGW(S) hipLaunchKernelGGL(kan_gw_kernel<S>, dim3(nblocks), dim3(RB), 0, s, *kl, x, g, B, d_scaled, d_wl, *grads, accumulate)
@@ -751,7 +934,7 @@ int fetode_kanlinear_backward(const fetode_kanlinear_t* kl, const float* x, int6
       hipLaunchKernelGGL(kan_scale_ls_kernel, dim3(nblk(out, 64)), dim3(64), 0, s, *kl, d_wl, *grads, accumulate);
       LAUNCH_CHECK();
     }
-    if (NB > 0 && !wide) {
+    if (NB > 0 && !wide && !(B >= kPsMinRows && ps_ok(kl))) {
       hipLaunchKernelGGL(kan_gab_kernel, dim3(in * NB), dim3(RB), 0, s, *kl, x, g, B, *grads, accumulate);
       LAUNCH_CHECK();
     }

@@ -130,8 +130,10 @@ int fetode_field_forward(const fetode_field_t* field, const void* plan, const fl
  *   out_mode[j] (dev int32) 0: y(step start), 1: y(step end), 2: linear interp with out_slope[j];
  *   solution (T, B, D): row 0 is written from y0.
  *   state/init_mask as in fetode_field_forward (final state written back).
- *   tape (dev, nullable): (n_evals, B, D + H) the inputs of both layers of every field evaluation
- *   (n_evals = n_steps * stages), recorded for fetode_integrate_fixed_backward (training).
+ *   tape (dev, nullable): n_evals * B * (D + H) floats, the inputs of both layers of every field
+ *   evaluation (n_evals = n_steps * stages), recorded for fetode_integrate_fixed_backward
+ *   (training): rows (n_evals, B, D + H) for the specialised [2, 10, 2] fields; two planes
+ *   (n_evals, B, D) then (n_evals, B, H) for the other widths (fieldn).
  * Returns FETODE_EUNSUPPORTED when no fused kernel exists for this field shape. */
 int fetode_integrate_fixed(const fetode_field_t* field, const void* plan, int32_t method,
                            const float* y0, int64_t B, const float* step_coef, int32_t n_steps,
@@ -371,7 +373,9 @@ int fetode_ferro_backward_wide(const fetode_ferro_t* layer, const void* plan, co
  * loss.backward() through a fused fixed-grid solve (train_kanfet_node_predprey.py:254-257):
  * reverse-mode through every stage evaluation (efficientkan.py:160-182, ferro_class.py:368-420,
  * detached prev_x :381-382), the stage combines and the output interpolation.
- * 1 if a fused backward kernel exists for this field shape (the fused forward's shapes). */
+ * 1 if a fused backward exists for this field shape: the specialised [2, 10, 2] sweeps, and for
+ * the other depth-2 widths the fieldn sweep (an adjoint kernel + the per-module parameter VJPs over
+ * every (evaluation, trajectory) row, fetode_fieldn_bwd.hip). */
 int fetode_fused_backward_supported(const fetode_field_t* field);
 /* The KAN-FET sweep's structure: 0 = one kernel (adjoints and parameter-gradient sums together,
  * the default), 1 = split (an adjoint sweep that records every evaluation's adjoints, then the

@@ -100,3 +100,57 @@ def test_fieldn_dopri5_host_loop(dev):
     r = O.odeint(lambda tt, yy: ref(yy), y0.double(), t, rtol=1e-4, atol=1e-6, trace=tr)
     assert F.dopri5.dopri5_solve.last.nfev == tr.nfev
     assert ((sol.double() - r).norm(dim=(1, 2)) / r.norm(dim=(1, 2))).max().item() <= 1e-5
+
+
+@pytest.mark.parametrize("kind,widths,K", [("kanfet", [2, 16, 2], 12), ("kan", [4, 32, 4], 0), ("kanfet", [3, 8, 3], 6)])
+@pytest.mark.parametrize("B", [1, 64, 1000])
+def test_fieldn_dopri5_resident_matches_host_loop(dev, kind, widths, K, B):
+    """The whole dopri5 solve of such a field in ONE launch (fieldn_kernel<FERRO, DOPRI>: one
+    trajectory per one-wave workgroup, the error norms as grid sums) against the host-driven loop
+    (one fieldn launch per evaluation, the norm read back per attempt): the same field arithmetic
+    and fp64 norms, so the same attempts and nfev, step sizes equal to fp64 pow's last ulp (device
+    libm vs host), solution and hysteresis state within 1e-6 — on the KAN field.  The two paths
+    sum the fp64 norms in different orders, which moves an fp32 error ratio by an ulp now and then;
+    on the KAN-FET fields the hysteresis amplifies that (as on the [2,10,2] resident solver at
+    B = 4096, tests/test_gpu_dopri5.py): the same attempts, accept pattern and nfev, dt within
+    1e-4, solution and state within 1e-4 (measured: dt 2.3e-5 at most)."""
+    import fet_ode_amd as F
+    from fet_ode_amd.dopri5 import ResidentSolve, set_resident_dopri5
+    y0 = _y0(B, widths[0], seed=7)
+    t = torch.tensor([0.0, 0.3, 0.7], dtype=torch.float64)
+    out = []
+    for resident in (True, False):
+        prev = set_resident_dopri5(resident)
+        try:
+            m = _model(kind, widths, K).to(dev)
+            with torch.no_grad():
+                sol = F.odeint(F.autonomous(m), y0.to(dev), t, rtol=1e-4, atol=1e-6).cpu()
+        finally:
+            set_resident_dopri5(prev)
+        s = F.dopri5.dopri5_solve.last
+        assert isinstance(s, ResidentSolve) == resident
+        states = [l.ferro._prev.cpu() for l in m.layers] if kind == "kanfet" else []
+        out.append((sol, [(float(a[1]), float(a[3])) for a in s.attempts], s.nfev, states))
+    (s0, a0, n0, st0), (s1, a1, n1, st1) = out
+    assert n0 == n1 and [a[1] for a in a0] == [a[1] for a in a1]
+    dtol, stol = (1e-13, 1e-6) if kind == "kan" else (1e-4, 1e-4)
+    np.testing.assert_allclose([a[0] for a in a0], [a[0] for a in a1], rtol=dtol)
+    assert ((s0 - s1).norm(dim=(1, 2)) / s1.norm(dim=(1, 2)).clamp_min(1e-30)).max() <= stol
+    for a, b in zip(st0, st1):
+        assert ((a - b).norm() / b.norm()).item() <= stol
+
+
+def test_fieldn_dopri5_resident_falls_back_beyond_one_grid(dev):
+    """A batch larger than one resident grid of fieldn's dopri5 driver takes the host loop."""
+    import fet_ode_amd as F
+    from fet_ode_amd import _lib
+    from fet_ode_amd.autograd_ops import make_handle
+    from fet_ode_amd.dopri5 import ResidentSolve
+    m = _model("kan", [4, 32, 4], 0).to(dev)
+    cap = _lib.load().fetode_integrate_dopri5_max_batch(make_handle(m, 8, dev).ref, 0)
+    assert cap >= 1024
+    y0 = _y0(cap + 5, 4)
+    with torch.no_grad():
+        sol = F.odeint(F.autonomous(m), y0.to(dev), torch.tensor([0.0, 0.1]), rtol=1e-3, atol=1e-5)
+    assert not isinstance(F.dopri5.dopri5_solve.last, ResidentSolve)
+    assert torch.isfinite(sol).all()

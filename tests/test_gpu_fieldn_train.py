@@ -1,0 +1,175 @@
+"""Fused training of the depth-2 fields of other widths (VERDICT r3 missing #3: "fused training for
+any field except exactly [2,10,2]"): the fieldn forward records both layers' inputs of every
+evaluation and the backward is fieldn_adj_kernel + the per-module parameter VJPs over every
+(evaluation, trajectory) row (fet-ode_amd/csrc/fetode_fieldn_bwd.hip) — two launches plus the
+parameter sums instead of autograd through every stage.
+
+Checked against the fp64 oracle's autograd (the reference modules restated, oracle/torch_ref.py,
+through the restated torchdiffeq fixed-grid solver) and against the per-stage GPU path
+(F.set_fused_training(False)).  Reference: train_kanfet_node_predprey.py:254-257 (loss.backward()
+through odeint); the loss is a mean-square error against a target, as there.
+
+Tolerances (relative to each gradient's largest entry): the KAN field is well conditioned, 1e-4
+against fp64 as the [2,10,2] fused backward (tests/test_gpu_grad.py); KAN-FET fields 1e-3 (as the
+[2,10,2] KAN-FET tests: the Ferro gates amplify fp32 rounding) — or, where the field is so
+ill-conditioned that the reference's OWN fp32 autograd misses fp64 by more (its worst gradient of
+the case), four times that yardstick (the envelope rule of tests/test_gpu_ett.py).  Measured (tools/diag/fieldn_grad_check.py):
+KANFET([2, 16, 2], K = 12) from this random init is such a field — over 6 rk4 points the oracle's
+fp32 gradients are up to 0.76 (relative) from fp64, the fused GPU path's 0.03, the per-stage
+path's 0.22; on the KAN [4, 32, 4] and KANFET [3, 8, 3] fields all three agree to ~5e-7.  The
+per-stage GPU path is held to the same bar (both are fp32 paths with different summation orders)."""
+import numpy as np
+import pytest
+import torch
+
+from test_gpu_grad import assert_grad_close
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [("kanfet", [2, 16, 2], 12), ("kanfet", [3, 8, 3], 6), ("kan", [4, 32, 4], 0), ("kanfet", [1, 64, 1], 4)]
+SKIP = ("grid", "prev_x", "branch_sign")
+
+
+def _model(kind, widths, K, seed=0):
+    import fet_ode_amd as F
+    torch.manual_seed(seed)
+    if kind == "kan":
+        return F.KAN(widths, grid_size=5)
+    return F.KANFET(widths, grid_size=5, num_fet_basis=K)
+
+
+def _oracle(kind, ps, n_layers=2):
+    from oracle import torch_ref as O
+    if kind == "kan":
+        return O.KANRef([O.KANLinearParams.from_state_dict(ps, f"layers.{l}.") for l in range(n_layers)])
+    return O.KANFETRef.from_state_dict(ps, n_layers)
+
+
+def _y0(B, D, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    return 0.5 + 2.0 * torch.rand(B, D, generator=g)
+
+
+def _gpu_grads(m, y0, t, method, target, dev, opts=None):
+    import fet_ode_amd as F
+    m.zero_grad(set_to_none=True)
+    yg = y0.clone().to(dev).requires_grad_(True)
+    pred = F.odeint(F.autonomous(m), yg, t, method=method, options=opts)
+    loss = torch.mean(torch.square(pred - target.to(dev)))
+    loss.backward()
+    got = {"y0": yg.grad.cpu()}
+    got.update({n: p.grad.cpu() for n, p in m.named_parameters()})
+    return loss.item(), pred.grad_fn.name(), got
+
+
+def _oracle_grads(kind, sd, y0, t, method, target, opts=None, dtype=torch.float64):
+    from oracle import torch_ref as O
+    ps = {k: v.detach().cpu().to(dtype).clone().requires_grad_(k.split(".")[-1] not in SKIP) for k, v in sd.items()}
+    ref = _oracle(kind, ps)
+    yc = y0.clone().to(dtype).requires_grad_(True)
+    pr = O.odeint(lambda tt, yy: ref(yy), yc, t.to(dtype), method=method, options=opts)
+    loss = torch.mean(torch.square(pr - target.to(dtype)))
+    loss.backward()
+    exp = {"y0": yc.grad}
+    exp.update({n: ps[n].grad for n in ps if ps[n].grad is not None})
+    return loss.item(), exp
+
+
+def _rel(got, e64):
+    ex = e64.double().cpu()
+    return (got.double().cpu() - ex).abs().max().item() / (ex.abs().max().item() + 1e-12)
+
+
+def _envelope(got, e64, yard, name, rel):
+    """|got - fp64| <= max(rel, 4 yard) x max |fp64|, yard = the field's fp32 conditioning: the
+    largest relative error of the reference's own fp32 autograd over all the gradients of the case
+    (one parameter's fp32 error is a single sample of rounding noise, the field's worst is not)."""
+    err = _rel(got, e64)
+    assert err <= max(rel, 4.0 * yard), f"{name}: {err:.3e} (reference fp32 yardstick {yard:.3e})"
+
+
+@pytest.mark.parametrize("kind,widths,K", SHAPES)
+@pytest.mark.parametrize("method", ["rk4", "rk4_classic", "midpoint", "euler"])
+def test_fieldn_training_vs_oracle_and_per_stage(dev, kind, widths, K, method):
+    import fet_ode_amd as F
+    B, D = 48, widths[0]
+    t = torch.tensor(np.linspace(0, 0.5, 6))
+    y0 = _y0(B, D)
+    target = 0.3 * torch.ones(6, B, D)
+    m0 = _model(kind, widths, K)
+    sd = {k: v.clone() for k, v in m0.state_dict().items()}
+    res = {}
+    for fused in (True, False):
+        prev = F.set_fused_training(fused)
+        try:
+            m = _model(kind, widths, K).to(dev)
+            m.load_state_dict(sd)
+            res[fused] = _gpu_grads(m, y0, t, method, target, dev)
+        finally:
+            F.set_fused_training(prev)
+    assert "FusedFixed" in res[True][1], res[True][1]      # the fused launch pair ran
+    assert "FusedFixed" not in res[False][1]
+    lref, exp = _oracle_grads(kind, sd, y0, t, method, target)
+    _, e32 = _oracle_grads(kind, sd, y0, t, method, target, dtype=torch.float32)
+    rel = 1e-4 if kind == "kan" else 1e-3
+    loss, _, got = res[True]
+    assert abs(loss - lref) <= 1e-5 * abs(lref)
+    yard = max(_rel(e32[n], exp[n]) for n in got)
+    for n in got:
+        _envelope(got[n], exp[n], yard, f"fused {n}", rel)
+        _envelope(res[False][2][n], exp[n], yard, f"per-stage {n}", rel)
+
+
+def test_fieldn_training_carried_state_and_interpolated_outputs(dev):
+    """A second solve from the hysteresis state the first one left (evaluation 0's hysteresis
+    input = the stored state, not the reinit rule), B = 1 (the reference's first-call rule for a
+    batch of one), and a step_size grid whose outputs fall between grid points (the linear
+    interpolation's adjoint)."""
+    import fet_ode_amd as F
+    from oracle import torch_ref as O
+    kind, widths, K = "kanfet", [3, 8, 3], 6
+    t = torch.tensor([0.0, 0.13, 0.31, 0.45])
+    opts = {"step_size": 0.05}
+    for B in (1, 7):
+        m = _model(kind, widths, K)
+        sd = {k: v.clone() for k, v in m.state_dict().items()}
+        ps = {k: v.detach().double().clone().requires_grad_(k.split(".")[-1] not in SKIP) for k, v in sd.items()}
+        ref = _oracle(kind, ps)
+        m = m.to(dev)
+        y0 = _y0(B, 3, seed=11)
+        for call in range(2):
+            m.zero_grad(set_to_none=True)
+            for p in ps.values():
+                p.grad = None
+            yg = y0.clone().to(dev).requires_grad_(True)
+            pred = F.odeint(F.autonomous(m), yg, t, method="rk4", options=opts)
+            assert "FusedFixed" in pred.grad_fn.name()
+            pred.square().sum().backward()
+            yc = y0.clone().double().requires_grad_(True)
+            O.odeint(lambda tt, yy: ref(yy), yc, t, method="rk4", options=opts).square().sum().backward()
+            assert_grad_close(yg.grad, yc.grad, f"B={B} call={call} y0", rel=1e-3)
+            for n, p in m.named_parameters():
+                assert_grad_close(p.grad, ps[n].grad, f"B={B} call={call} {n}", rel=1e-3)
+
+
+def test_fieldn_training_large_batch_matches_per_stage(dev):
+    """B = 4096 (the LV bench batch) over 10 rk4 steps: fused vs per-stage GPU path (both fp32;
+    the well-conditioned KANFET [3, 8, 3] field)."""
+    import fet_ode_amd as F
+    kind, widths, K = "kanfet", [3, 8, 3], 6
+    B = 4096
+    t = torch.tensor(np.linspace(0, 0.5, 11))
+    y0 = _y0(B, 3, seed=5)
+    target = torch.zeros(11, B, 3)
+    sd = {k: v.clone() for k, v in _model(kind, widths, K).state_dict().items()}
+    res = {}
+    for fused in (True, False):
+        prev = F.set_fused_training(fused)
+        try:
+            m = _model(kind, widths, K).to(dev)
+            m.load_state_dict(sd)
+            res[fused] = _gpu_grads(m, y0, t, "rk4", target, dev)
+        finally:
+            F.set_fused_training(prev)
+    for n in res[True][2]:
+        assert_grad_close(res[True][2][n], res[False][2][n], n, rel=1e-3)
