@@ -1017,7 +1017,7 @@ def main():
             # north_star: "MFMA utilisation against chip peak" — the path's MFMA kernels (the LV field
             # itself has no GEMM-shaped work): the ETT wide KAN-FET layer and the MNIST
             # KANLinear head, from the committed PMC pass (tools/pmc_issue.py)
-            "mfma": {k: pmc_mfma(k) for k in ("wide_layer_kernel<10, true, true, 8>", "wide_fwd_kernel")},
+            "mfma": {k: pmc_mfma(k) for k in ("wide_layer_kernel<10, true, true, 8>", "wide_fwd4_kernel")},
         }
         if world == 1:
             # strong-scaling proxy on one GPU: the per-GPU block of an 8-GPU strong-scaled job

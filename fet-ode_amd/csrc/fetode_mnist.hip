@@ -648,6 +648,168 @@ __global__ __launch_bounds__(kWideThreads) void wide_fwd_kernel(fetode_kanlinear
   }
 }
 
+// wide_fwd4_kernel (the default): the same contraction, each wave on FOUR 16-row tiles (64 rows; a
+// 256-thread workgroup = 256 rows).  Per input group the lane's per-input data — its knots,
+// logistic (a, b) and the 17 B operands Wp[4 g + kq, f, r] — is read from LDS once and serves the
+// four tiles (per-(row, input) LDS operations 44 -> 23), the four tiles' features are formed first
+// and the MFMAs issued round-robin over four independent accumulators.  Same chunks, splits and
+// per-tile accumulation order as wide_fwd_kernel: bitwise the same partials.  Measured B = 8192
+// (tools/diag/mnist_head_time.py): 147.0 -> 140.6 us per head forward; PMC
+// (profiles/r04_h_pmc_issue.json): LDS-busy 0.59 -> 0.29, VALU-busy 0.36, MFMA-busy 0.32, 47 % of
+// wave cycles issue-stalled — the head is bound by its VALU feature work and MFMAs taking turns,
+// not by LDS; a software-pipelined variant (tile t + 1's features between tile t's MFMAs, branch-
+// free window) measured 142.7 us and was not kept.
+constexpr int kW4Rows = 256;
+__global__ __launch_bounds__(256) void wide_fwd4_kernel(fetode_kanlinear_t kl, const float* __restrict__ wp,
+                                                       const float* __restrict__ x, int64_t B, int nch,
+                                                       float* __restrict__ part) {
+  __shared__ float ws[kWideCh * kWideF * 16];
+  __shared__ float xs[kW4Rows][kWideCh + 1];
+  __shared__ float4 gk[kWideCh][kWideNG / 4];
+  __shared__ float4 tb[kWideCh * kWideTab];
+  __shared__ float2 lab[kWideCh][kWideNB];
+  __shared__ __attribute__((aligned(16))) float win[256 * kWinStride];
+  const int in = kl.in_features;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = lane & 15, kq = lane >> 4;
+  const int64_t row0 = (int64_t)blockIdx.x * kW4Rows;
+  const int S = gridDim.y, s = blockIdx.y;
+  const int c0 = s * nch / S, c1 = (s + 1) * nch / S;
+  const bool lg = kl.num_logistic != 0;
+  const float4* wtab = reinterpret_cast<const float4*>(wp + (int64_t)in * kWideF * 16);
+  float* mywin = win + tid * kWinStride;
+  for (int q = 0; q < kWinStride; ++q) mywin[q] = 0.f;
+  f32x4 acc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int PW = (kWideCh * kWideF * 16 + 255) / 256, PX = (kW4Rows * kWideCh + 255) / 256;
+  constexpr int PT = (kWideCh * kWideTab + 255) / 256, PG = (kWideCh * kWideNG + 255) / 256;
+  constexpr int PL = (kWideCh * kWideNB + 255) / 256;
+  float rw[PW], rx[PX], rg[PG], ra[PL], rb[PL];
+  float4 rt[PT];
+  auto fetch = [&](int c) __attribute__((always_inline)) {
+    const int i0 = c * kWideCh, ni = min(kWideCh, in - i0);
+#pragma unroll
+    for (int k = 0; k < PW; ++k) {
+      const int t = tid + 256 * k;
+      rw[k] = t < ni * kWideF * 16 ? wp[(int64_t)i0 * kWideF * 16 + t] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+      const int t = tid + 256 * k, rr = t / kWideCh, ii = t - rr * kWideCh;
+      rx[k] = (t < kW4Rows * kWideCh && row0 + rr < B && ii < ni) ? x[(row0 + rr) * in + i0 + ii] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < PT; ++k) {
+      const int t = tid + 256 * k;
+      rt[k] = t < ni * kWideTab ? wtab[(int64_t)i0 * kWideTab + t] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < PG; ++k) {
+      const int t = tid + 256 * k;
+      rg[k] = t < ni * kWideNG ? kl.grid[(int64_t)i0 * kWideNG + t] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+      const int t = tid + 256 * k;
+      const bool ok = lg && t < ni * kWideNB;
+      ra[k] = ok ? kl.logistic_a[(int64_t)i0 * kWideNB + t] : 0.f;
+      rb[k] = ok ? kl.logistic_b[(int64_t)i0 * kWideNB + t] : 0.f;
+    }
+  };
+  if (c0 < c1) fetch(c0);
+  for (int c = c0; c < c1; ++c) {
+    const int ni = min(kWideCh, in - c * kWideCh);
+    __syncthreads();  // the previous chunk's contraction is done with the LDS copies
+#pragma unroll
+    for (int k = 0; k < PW; ++k)
+      if (tid + 256 * k < kWideCh * kWideF * 16) ws[tid + 256 * k] = rw[k];
+#pragma unroll
+    for (int k = 0; k < PX; ++k) {
+      const int t = tid + 256 * k, rr = t / kWideCh, ii = t - rr * kWideCh;
+      if (t < kW4Rows * kWideCh) xs[rr][ii] = rx[k];
+    }
+#pragma unroll
+    for (int k = 0; k < PT; ++k)
+      if (tid + 256 * k < kWideCh * kWideTab) tb[tid + 256 * k] = rt[k];
+#pragma unroll
+    for (int k = 0; k < PG; ++k)
+      if (tid + 256 * k < kWideCh * kWideNG) reinterpret_cast<float*>(&gk[0][0])[tid + 256 * k] = rg[k];
+#pragma unroll
+    for (int k = 0; k < PL; ++k) {
+      const int t = tid + 256 * k;
+      if (t < kWideCh * kWideNB) lab[t / kWideNB][t % kWideNB] = make_float2(-ra[k] * FETODE_LOG2E, (ra[k] * rb[k]) * FETODE_LOG2E);
+    }
+    __syncthreads();
+    if (c + 1 < c1) fetch(c + 1);
+    for (int g = 0; g < ni / 4; ++g) {
+      const int il = 4 * g + kq;
+      // the lane's input: knots, logistic (a, b), B operands — once for the four row tiles
+      float4 gr4[kWideNG / 4];
+#pragma unroll
+      for (int j = 0; j < kWideNG / 4; ++j) gr4[j] = gk[il][j];
+      float2 ab[kWideNB];
+#pragma unroll
+      for (int j = 0; j < kWideNB; ++j) ab[j] = lab[il][j];
+      float wb[kWideF];
+      const float* wrow = ws + (il * kWideF) * 16 + r;  // lane (kq, o = r): Wp[i, f, o]
+#pragma unroll
+      for (int f = 0; f < kWideF; ++f) wb[f] = wrow[f * 16];
+      const float4* tbi = &tb[il * kWideTab];
+      // features of row tile t (lane row 16 t + r, input il) into feat[]
+      auto feats = [&](int t, float* feat) __attribute__((always_inline)) {
+        const float xi = xs[wv * 64 + 16 * t + r][il];
+        feat[0] = silu(xi);  // SiLU, efficientkan.py:166 / mnist :131
+        int m = -1;
+#pragma unroll
+        for (int j = 0; j < kWideNG / 4; ++j) {
+          const float4 v = gr4[j];
+          m += ((xi >= v.x) ? 1 : 0) + ((xi >= v.y) ? 1 : 0) + ((xi >= v.z) ? 1 : 0) + ((xi >= v.w) ? 1 : 0);
+        }
+        const bool fin = __builtin_isfinite(xi), ing = fin && m >= 0 && m < kWideNI;
+        const float4* tm = tbi + (ing ? m : 0) * 5;
+        const float4 gq = tm[4];
+        const float u = (xi - gq.x) * gq.y;
+        if (ing) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 p = tm[q];
+            mywin[m + q + 1] = ffma(ffma(ffma(p.w, u, p.z), u, p.y), u, p.x);
+          }
+        }
+        asm volatile("" ::: "memory");  // the window writes stay before the vector reads
+        const float4 d0 = *reinterpret_cast<const float4*>(mywin + 4), d1 = *reinterpret_cast<const float4*>(mywin + 8);
+        const float nf = fin ? 0.f : __builtin_nanf("");  // non-finite x: NaN bases, as (x - g) / d * 0
+        feat[1] = d0.x + nf; feat[2] = d0.y + nf; feat[3] = d0.z + nf; feat[4] = d0.w + nf;
+        feat[5] = d1.x + nf; feat[6] = d1.y + nf; feat[7] = d1.z + nf; feat[8] = d1.w + nf;
+        asm volatile("" ::: "memory");
+        if (ing) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) mywin[m + q + 1] = 0.f;
+        }
+#pragma unroll
+        for (int j = 0; j < kWideNB; ++j)  // 2 sigmoid(a (x - b)), mnist_kuramoto_kan.py:22 (2 in the weights)
+        feat[1 + kWideNS + j] = lg ? rcp(1.0f + ex2(ffma(ab[j].x, xi, ab[j].y))) : 0.f;
+      };
+      float ft[4][kWideF];  // the four tiles' features first: then 4 independent MFMA chains
+#pragma unroll
+      for (int t = 0; t < 4; ++t) feats(t, ft[t]);
+#pragma unroll
+      for (int f = 0; f < kWideF; ++f)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ft[t][f], wb[f], acc[t], 0, 0, 0);
+    }
+  }
+  // D of tile t: lane l holds rows 16 t + 4 (l >> 4) + v, column l & 15
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int64_t row = row0 + wv * 64 + 16 * t + 4 * kq + v;
+      if (row < B) part[((int64_t)s * B + row) * 16 + r] = acc[t][v];
+    }
+}
+
 __global__ void wide_reduce_kernel(const float* __restrict__ part, int S, int64_t B, int outf,
                                    const float* __restrict__ bias, float* __restrict__ out) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -792,8 +954,18 @@ int fetode_kanlinear_wide_forward(const fetode_kanlinear_t* kl, const float* wpa
   const int64_t tiles = (B + kWideRows - 1) / kWideRows;
   if (tiles > 0x7fffffff) return set_err(FETODE_EINVAL, "kanlinear wide: batch too large");
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(wide_fwd_kernel, dim3((unsigned)tiles, (unsigned)S), dim3(kWideThreads), 0, s, *kl, wpack, x, B, nch,
-                     (float*)workspace);
+  static const int v1 = [] {  // FETODE_WIDE_V=1: wide_fwd_kernel, one tile per wave (A/B, bitwise the same)
+    const char* e = getenv("FETODE_WIDE_V");
+    return e ? atoi(e) : 0;
+  }();
+  if (v1 == 1) {
+    hipLaunchKernelGGL(wide_fwd_kernel, dim3((unsigned)tiles, (unsigned)S), dim3(kWideThreads), 0, s, *kl, wpack, x, B,
+                       nch, (float*)workspace);
+  } else {
+    const int64_t t4 = (B + kW4Rows - 1) / kW4Rows;
+    hipLaunchKernelGGL(wide_fwd4_kernel, dim3((unsigned)t4, (unsigned)S),
+                       dim3(256), 0, s, *kl, wpack, x, B, nch, (float*)workspace);
+  }
   LAUNCH_CHECK();
   const int64_t n = B * kl->out_features;
   hipLaunchKernelGGL(wide_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, (const float*)workspace, S, B,
