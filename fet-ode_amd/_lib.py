@@ -122,6 +122,8 @@ SIGNATURES = {
                                                         ctypes.c_uint32, _vp, ctypes.POINTER(KANLinearGrad),
                                                         ctypes.POINTER(FerroGrad), _vp, _vp, _vp]),
     "fetode_integrate_dopri5_backward_workspace": (ctypes.c_int64, [ctypes.POINTER(FieldDesc), ctypes.c_int64]),
+    "fetode_integrate_dopri5_backward_workspace_ev": (ctypes.c_int64, [ctypes.POINTER(FieldDesc), ctypes.c_int64,
+                                                                       ctypes.c_int32]),
     "fetode_integrate_dopri5_backward_max_batch": (ctypes.c_int64, [ctypes.POINTER(FieldDesc)]),
     "fetode_integrate_dopri5_xrank": (ctypes.c_int, [ctypes.POINTER(FieldDesc), _vp, _vp, ctypes.c_int64,
                                                      ctypes.c_int64, _vp, ctypes.c_int32, ctypes.c_double,

@@ -1945,9 +1945,16 @@ static int64_t dopri_bwd_grid(const BwdEntry* e, int64_t B) {
 int64_t fetode_integrate_dopri5_backward_max_batch(const fetode_field_t* f) {
   if (validate_field(f) != FETODE_OK) return 0;
   const BwdEntry* e = find_bwd(f);
+  if (!e && fieldn_shape_supported(f)) return fieldn_dopri5_backward_max_batch(f);
   if (!e || !e->dopri) return 0;
   const int64_t w = dopri_bwd_resident_wgs(e);
   return w > 0 ? w * kTPB * e->dtpw : 0;
+}
+
+int64_t fetode_integrate_dopri5_backward_workspace_ev(const fetode_field_t* f, int64_t B, int32_t n_ev) {
+  if (validate_field(f) != FETODE_OK || B <= 0 || n_ev < 0) return -1;
+  if (!find_bwd(f) && fieldn_shape_supported(f)) return fieldn_dopri5_backward_workspace(f, B, n_ev);
+  return fetode_integrate_dopri5_backward_workspace(f, B);
 }
 
 int64_t fetode_integrate_dopri5_backward_workspace(const fetode_field_t* f, int64_t B) {
@@ -1972,7 +1979,8 @@ int fetode_integrate_dopri5_backward(const fetode_field_t* f, const void* plan, 
   int rc = validate_field(f);
   if (rc) return rc;
   const BwdEntry* e = find_bwd(f);
-  if (!e || !e->dopri) return set_err(FETODE_EUNSUPPORTED, "no dopri5 backward kernel for this field shape");
+  const bool fieldn = !e && fieldn_shape_supported(f);  // other widths: fetode_fieldn_bwd.hip
+  if (!fieldn && (!e || !e->dopri)) return set_err(FETODE_EUNSUPPORTED, "no dopri5 backward kernel for this field shape");
   if (B <= 0 || T <= 0) return FETODE_OK;
   if (!plan || !t || !opts || !tableau || !grad_solution || !tape || !attempts || !init_rec || !workspace ||
       !status || (f->ferro && !state0 && (init_mask & 3u) != 3u))
@@ -1980,6 +1988,10 @@ int fetode_integrate_dopri5_backward(const fetode_field_t* f, const void* plan, 
   const int base = opts[0] > 0.0 ? 1 : 2;
   if (n_att < 0 || n_ev != base + 6 * n_att)
     return set_err(FETODE_EINVAL, "dopri5 backward: %d evaluations do not match %d attempts", n_ev, n_att);
+  if (fieldn)
+    return fieldn_dopri5_backward(f, plan, B, t, T, rtol, atol, opts, tableau, grad_solution, tape, n_ev, attempts,
+                                  n_att, init_rec, state0, init_mask, grad_y0, kan_grads, ferro_grads, workspace, status,
+                                  stream);
   const bool one = dopri_bwd_tpw(e, B) == 1;
   const int64_t resident = dopri_bwd_resident_wgs(e, one);
   if (resident < 0) return set_err(FETODE_EHIP, "dopri5 backward: occupancy query failed");

@@ -59,6 +59,15 @@ int fieldn_fixed_backward(const fetode_field_t* f, const void* plan, int32_t met
                           int32_t T, const float* grad_solution, const float* tape, const float* state0,
                           uint32_t init_mask, float* grad_y0, const fetode_kanlinear_grad_t* kan_grads,
                           const fetode_ferro_grad_t* ferro_grads, void* workspace, void* stream);
+// the reverse sweep of fieldn's taped resident dopri5 solve (arguments as fetode_integrate_dopri5_backward)
+int64_t fieldn_dopri5_backward_max_batch(const fetode_field_t* f);
+int64_t fieldn_dopri5_backward_workspace(const fetode_field_t* f, int64_t B, int64_t n_ev);
+int fieldn_dopri5_backward(const fetode_field_t* f, const void* plan, int64_t B, const double* t, int32_t T, double rtol,
+                           double atol, const double* opts, const float* tableau, const float* grad_solution,
+                           const float* tape, int32_t n_ev, const double* attempts, int32_t n_att,
+                           const double* init_rec, const float* state0, uint32_t init_mask, float* grad_y0,
+                           const fetode_kanlinear_grad_t* kan_grads, const fetode_ferro_grad_t* ferro_grads,
+                           void* workspace, int32_t* status, void* stream);
 
 // Launch of a grid that must be co-resident (the device-resident solvers' grid reductions).  The
 // callers size the grid by occupancy; by default it is an ordinary launch (bounded spins turn a

@@ -1577,7 +1577,9 @@ __device__ __forceinline__ void fn_interval(const float* __restrict__ plan, cons
 
 // DOPRI: the whole dopri5 solve in this launch (fetode_integrate_dopri5 for these shapes), one
 // trajectory per one-wave workgroup, every workgroup resident (grid sums of the error norms)
-template <bool FERRO, bool DOPRI = false>
+// TAPE (with DOPRI): training — every evaluation's row (x, h, k) of (tape_cap, B, 2 D + H), the rows
+// fetode_integrate_dopri5_tape writes for the [2, 10, 2] fields too, and the initial-step scalars
+template <bool FERRO, bool DOPRI = false, bool TAPE = false>
 __global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(FusedArgs a) {
   constexpr int NW = DOPRI ? 1 : kFnWaves;
   if constexpr (DOPRI) {
@@ -1605,14 +1607,20 @@ __global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(Fuse
   }
   bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
   const float c0o = hl ? plan[P0.fconst + lane] : 0.f;
-  // training tape (fieldn_adj_kernel, fetode_fieldn_bwd.hip): two planes, the layer-0 inputs
-  // (n_ev, B, D) then the layer-1 inputs (n_ev, B, H), one row per evaluation
+  // training tapes.  Fixed grid (fieldn_adj_kernel, fetode_fieldn_bwd.hip): two planes, the layer-0
+  // inputs (n_ev, B, D) then the layer-1 inputs (n_ev, B, H).  dopri5 (TAPE): rows (x, h, k) of
+  // (tape_cap, B, 2 D + H) for the first tape_cap evaluations
   const int nst = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4 : a.method == FETODE_MIDPOINT ? 2 : 1;
-  float* tx = (a.tape && !a.single_eval) ? a.tape : nullptr;
+  float* tx = (!DOPRI && a.tape && !a.single_eval) ? a.tape : nullptr;
   float* th_ = tx ? tx + (int64_t)a.n_steps * nst * a.B * D : nullptr;
+  float* trow = nullptr;  // TAPE: this evaluation's row, or null past tape_cap
   int64_t ev = 0;
   auto eval = [&](void) {  // xs -> ks (all lanes), hysteresis states updated
     fn_wsync();
+    if constexpr (TAPE) {
+      trow = (ev < a.dp.tape_cap && valid) ? a.tape + (ev * a.B + b) * (2 * D + H) : nullptr;
+      if (trow && lane < D) trow[lane] = xs[lane];
+    }
     if (tx && valid && lane < D) tx[(ev * a.B + b) * D + lane] = xs[lane];
     // layer 0: h_o
     float h = 0.f;
@@ -1630,6 +1638,7 @@ __global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(Fuse
       }
     }
     if (tx && valid && hl) th_[(ev * a.B + b) * H + lane] = h;
+    if (TAPE && trow && hl) trow[D + lane] = h;
     ++ev;
     fn_wsync();
     if (FERRO && lane < D) p0[lane] = xs[lane];  // ferro_class.py:409
@@ -1671,7 +1680,9 @@ __global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(Fuse
     auto f = [&](float xin) -> float {
       if (dl) xs[lane] = xin;
       eval();
-      return dl ? ks[lane] : 0.f;
+      const float k = dl ? ks[lane] : 0.f;
+      if (TAPE && trow && dl) trow[D + H + lane] = k;
+      return k;
     };
     if (real) a.solution[b * D + lane] = y;
     float f0 = f(y);
@@ -1697,6 +1708,13 @@ __global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(Fuse
       if (d1 <= 1e-15f && d2 <= 1e-15f) h1 = fmaxf(1e-6f, h0 * 1e-3f);
       else h1 = (float)pow((double)(0.01f / fmaxf(d1, d2)), (double)0.2f);  // fp64 pow rounded once
       dt = (double)fminf(100.0f * h0, fabsf(h1));
+      if (TAPE && blockIdx.x == 0 && threadIdx.x == 0) {
+        P.init_rec[0] = d0;
+        P.init_rec[1] = d1;
+        P.init_rec[2] = d2;
+        P.init_rec[3] = h0;
+        P.init_rec[4] = h1;
+      }
     }
     float co[5] = {y, 0.f, 0.f, 0.f, 0.f};
     double t0s = P.t[0], t1s = P.t[0];
@@ -1957,26 +1975,30 @@ static int64_t dopri5_resident_wgs(const FusedEntry* e, bool ferro) {
 }
 
 // fieldn's dopri5 driver: one trajectory per one-wave workgroup, every one resident
-static int64_t dopri5_fieldn_resident_wgs(bool ferro) {
-  static int n_cu = 0, per_cu[2] = {0, 0};
-  const int fi = ferro ? 0 : 1;
+static const void* fieldn_dopri_fn(bool ferro, bool tape) {
+  return ferro ? (tape ? (const void*)fieldn_kernel<true, true, true> : (const void*)fieldn_kernel<true, true, false>)
+               : (tape ? (const void*)fieldn_kernel<false, true, true> : (const void*)fieldn_kernel<false, true, false>);
+}
+static int64_t dopri5_fieldn_resident_wgs(bool ferro, bool tape = false) {
+  static int n_cu = 0, per_cu[2][2] = {{0, 0}, {0, 0}};
+  const int fi = ferro ? 0 : 1, ti = tape ? 1 : 0;
   if (!n_cu) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       return -1;
   }
-  if (!per_cu[fi] && hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                         &per_cu[fi], ferro ? (const void*)fieldn_kernel<true, true> : (const void*)fieldn_kernel<false, true>,
-                         64, 0) != hipSuccess)
+  if (!per_cu[fi][ti] && hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu[fi][ti], fieldn_dopri_fn(ferro, tape), 64, 0) !=
+                             hipSuccess)
     return -1;
-  return (int64_t)per_cu[fi] * n_cu;
+  return (int64_t)per_cu[fi][ti] * n_cu;
 }
 
 int64_t fetode_integrate_dopri5_max_batch(const fetode_field_t* f, int32_t sharded) {
   if (validate_field(f) != FETODE_OK) return 0;
   const FusedEntry* e = find_fused(f);
-  if (!e && fieldn_supported(f)) {
-    const int64_t w = dopri5_fieldn_resident_wgs(f->ferro != nullptr) - (sharded ? 1 : 0);
+  if (!e && fieldn_supported(f)) {  // the taped variant's grid bounds training solves too
+    const int64_t w0 = dopri5_fieldn_resident_wgs(f->ferro != nullptr), w1 = dopri5_fieldn_resident_wgs(f->ferro != nullptr, true);
+    const int64_t w = (w0 < w1 ? w0 : w1) - (sharded ? 1 : 0);
     return w > 0 ? w : 0;
   }
   if (!e) return 0;
@@ -1997,15 +2019,15 @@ static int dopri5_launch(const fetode_field_t* f, const void* plan, const float*
   if (f->kan[0].in_features != f->kan[f->n_layers - 1].out_features)
     return set_err(FETODE_EINVAL, "field is not R^D -> R^D");
   const FusedEntry* e = find_fused(f);
-  // other widths: fieldn's driver, one trajectory per one-wave workgroup (no taped variant)
-  const bool fn = !e && fieldn_supported(f) && !(tape_cap > 0);
+  // other widths: fieldn's driver, one trajectory per one-wave workgroup
+  const bool fn = !e && fieldn_supported(f);
   if (!e && !fn) return set_err(FETODE_EUNSUPPORTED, "no fused dopri5 kernel for this field shape");
   const bool sharded = xr && xr->world > 1;
   // small batches (the reference's own X0 (1, 2); the strong-scaled shard): v6, one trajectory per
   // workgroup, when the whole grid is resident; else v4, two per one-wave workgroup
   const int64_t res6 = (!fn && !sharded && B <= small_max()) ? dopri5_small_resident_wgs(e, f->ferro != nullptr) : -1;
   const bool use6 = res6 >= B;
-  const int64_t resident = fn ? dopri5_fieldn_resident_wgs(f->ferro != nullptr)
+  const int64_t resident = fn ? dopri5_fieldn_resident_wgs(f->ferro != nullptr, tape_cap > 0)
                               : use6 ? res6 : dopri5_resident_wgs(e, f->ferro != nullptr);
   if (resident < 0) return set_err(FETODE_EHIP, "dopri5: occupancy query failed");
   const int per = fn ? 1 : 2;  // trajectories per workgroup (v6: one, never sharded)
@@ -2098,7 +2120,7 @@ static int dopri5_launch(const fetode_field_t* f, const void* plan, const float*
   hipStream_t s = (hipStream_t)stream;
   HIP_CHECK_RET(hipMemsetAsync(workspace, 0, sizeof(unsigned) * kDpBarWords, s));
   void* args[] = {&a};
-  const void* kfn = fn ? (f->ferro ? (const void*)fieldn_kernel<true, true> : (const void*)fieldn_kernel<false, true>)
+  const void* kfn = fn ? fieldn_dopri_fn(f->ferro != nullptr, a.tape != nullptr)
                    : use6 ? (const void*)(a.tape ? e->small_dopri_tape : e->small_dopri)
                           : (const void*)(a.tape ? e->dopri_tape : e->dopri);
   HIP_CHECK_RET(resident_launch(kfn, dim3((unsigned)lgrid), dim3(use6 ? 192 : 64), args, 0, s));

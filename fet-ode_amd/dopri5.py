@@ -626,9 +626,9 @@ class _FusedDopri5Fn(torch.autograd.Function):
             kg[l] = _lib.KANLinearGrad(*[_lib.ptr(gbuf(p)) for p in kan_params(kan)])
             if fg is not None:
                 fg[l] = _lib.FerroGrad(*[_lib.ptr(gbuf(getattr(fer, n))) for n in FERRO_PARAM_NAMES])
-        nbytes = lib.fetode_integrate_dopri5_backward_workspace(ctx.handle.ref, B)
+        nbytes = lib.fetode_integrate_dopri5_backward_workspace_ev(ctx.handle.ref, B, ctx.n_ev)
         if nbytes < 0:
-            _lib.check(_lib.FETODE_EUNSUPPORTED, "fetode_integrate_dopri5_backward_workspace")
+            _lib.check(_lib.FETODE_EUNSUPPORTED, "fetode_integrate_dopri5_backward_workspace_ev")
         ws = torch.empty(max(1, nbytes // 4), device=dev, dtype=torch.float32)
         status = torch.empty(1, device=dev, dtype=torch.int32)
         _lib.check(lib.fetode_integrate_dopri5_backward(
@@ -657,8 +657,8 @@ def set_resident_dopri5_training(enabled: bool) -> bool:
 
 def _try_field_resident_train(func, y0, tp, reversed_, rtol, atol, options):
     """The taped resident solve + reverse sweep when `func` is a fused-shape field (the LV [2,10,2]
-    KAN / KAN-FET), something needs gradients, the solve is single-device and forward in time, and
-    the options are the scalar ones."""
+    KAN / KAN-FET, or another depth-2 width on fieldn's driver and sweep), something needs
+    gradients, the solve is single-device and forward in time, and the options are the scalar ones."""
     from .autograd_ops import make_handle
     from .odeint import fused_field
     field = fused_field(func)

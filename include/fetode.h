@@ -420,6 +420,10 @@ int fetode_integrate_dopri5_backward(const fetode_field_t* field, const void* pl
                                      const fetode_kanlinear_grad_t* kan_grads, const fetode_ferro_grad_t* ferro_grads,
                                      void* workspace, int32_t* status, void* stream);
 int64_t fetode_integrate_dopri5_backward_workspace(const fetode_field_t* field, int64_t B);
+/* The workspace of a solve with n_ev evaluations: the other depth-2 widths' sweep (fieldn) records
+ * every evaluation's adjoints and layer inputs for its row-batched parameter VJPs, so its workspace
+ * grows with n_ev; for the [2, 10, 2] fields the same as fetode_integrate_dopri5_backward_workspace. */
+int64_t fetode_integrate_dopri5_backward_workspace_ev(const fetode_field_t* field, int64_t B, int32_t n_ev);
 int64_t fetode_integrate_dopri5_backward_max_batch(const fetode_field_t* field);
 
 /* ---- ECG KAN-FET NODE field (BASELINE configs[2]) -----------------------

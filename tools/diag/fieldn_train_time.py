@@ -73,3 +73,29 @@ for name, mk in (("KANFET[2,16,2] K=12", lambda: F.KANFET([2, 16, 2], grid_size=
             set_resident_dopri5(prev)
     print(f"{name} dopri5 B={B2}: resident {res[0]:.2f} ms, host loop {res[1]:.2f} ms "
           f"(nfev {F.dopri5.dopri5_solve.last.nfev})", flush=True)
+
+# dopri5 TRAINING (rtol 1e-3): the taped resident solve + fieldn_dopri_bwd_kernel vs _Dopri5Grad
+from fet_ode_amd.dopri5 import set_resident_dopri5_training  # noqa: E402
+B3 = int(os.environ.get("B3", "1024"))
+t3 = torch.tensor([0.0, 0.5, 1.0], dtype=torch.float64)
+for name, mk in (("KANFET[3,8,3] K=6", lambda: F.KANFET([3, 8, 3], grid_size=5, num_fet_basis=6)),
+                 ("KAN[4,32,4]", lambda: F.KAN([4, 32, 4], grid_size=5))):
+    torch.manual_seed(0)
+    m = mk().to(dev)
+    D = m.layers[0].kan.in_features if hasattr(m.layers[0], "kan") else m.layers[0].in_features
+    y0 = (0.5 + 2.0 * torch.rand(B3, D, device=dev))
+    func = F.autonomous(m)
+
+    def it3():
+        m.zero_grad(set_to_none=True)
+        F.odeint(func, y0, t3, rtol=1e-3, atol=1e-4).square().mean().backward()
+
+    res = []
+    for resident in (True, False):
+        prev = set_resident_dopri5_training(resident)
+        try:
+            res.append(ev_ms(it3, 3 if resident else 1))
+        finally:
+            set_resident_dopri5_training(prev)
+    print(f"{name} dopri5 training B={B3}: resident pair {res[0]:.2f} ms, host autograd {res[1]:.1f} ms "
+          f"({res[1] / res[0]:.1f}x, nfev {F.dopri5.dopri5_solve.last.nfev})", flush=True)

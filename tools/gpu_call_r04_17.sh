@@ -1,0 +1,5 @@
+cd $GRAFT_REPO_ROOT
+O=gpurun_out; mkdir -p $O
+export TMPDIR=/tmp
+step() { local name=$1; shift; "$@" > $O/$name.log 2>&1; local rc=$?; echo "$name rc=$rc"; tail -${TAILN:-15} $O/$name.log; [ $rc -le 1 ] || exit $rc; return 0; }
+TAILN=30 step fnd5t timeout -k 10 600 python -u -m pytest -q --timeout 300 --timeout-method thread tests/test_gpu_fieldn_train.py -k dopri5
