@@ -30,12 +30,7 @@ SHAPES = [("kanfet", [2, 16, 2], 12), ("kanfet", [3, 8, 3], 6), ("kan", [4, 32, 
 SKIP = ("grid", "prev_x", "branch_sign")
 
 
-def _model(kind, widths, K, seed=0):
-    import fet_ode_amd as F
-    torch.manual_seed(seed)
-    if kind == "kan":
-        return F.KAN(widths, grid_size=5)
-    return F.KANFET(widths, grid_size=5, num_fet_basis=K)
+from test_gpu_fieldn import _model  # noqa: E402  (one cached state dict per shape: efficient_kan's lstsq init is not reproducible)
 
 
 def _oracle(kind, ps, n_layers=2):
@@ -237,9 +232,10 @@ def test_fieldn_dopri5_training_vs_oracle_and_host(dev, kind, widths, K, B):
     l1, g1, a1, n1 = _d5_run(kind, widths, K, sd, y0, t, w, dev, False)
     assert n0 == n1 and [x[1] for x in a0] == [x[1] for x in a1]
     # the host path evaluates the field through the per-module kernels under autograd (another fp32
-    # rounding of the same field than fieldn's fused evaluation): on KAN the step sizes still agree
-    # to fp64 noise, on KAN-FET the hysteresis amplifies the ulp differences (§4.10)
-    np.testing.assert_allclose([x[0] for x in a0], [x[0] for x in a1], rtol=1e-12 if kind == "kan" else 1e-3)
+    # rounding of the same field than fieldn's fused evaluation): on KAN the step sizes agree to an
+    # fp32 ulp (the initial step is an fp32 value), on KAN-FET the hysteresis amplifies the ulp
+    # differences (§4.10)
+    np.testing.assert_allclose([x[0] for x in a0], [x[0] for x in a1], rtol=1e-6 if kind == "kan" else 1e-3)
     assert abs(l0 - l1) <= (1e-5 if kind == "kan" else 1e-3) * abs(l1) + 1e-6
     lo, go, no = _d5_oracle(kind, sd, y0, t, w)
     assert no == n0, (no, n0)
