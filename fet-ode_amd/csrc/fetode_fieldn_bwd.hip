@@ -22,6 +22,8 @@
 // the per-stage path to fp32 summation order.
 #include <string.h>
 
+#include <cstdlib>
+
 #include "fetode_common.h"
 
 using namespace fetode;
@@ -159,17 +161,26 @@ __device__ void fb_coefs(int method, float dt, float hh, float h6, float bc[4], 
   }
 }
 
-template <bool FERRO>
-__global__ __launch_bounds__(64 * kFbWaves) void fieldn_adj_kernel(FbArgs a) {
-  __shared__ float s_x[kFbWaves][kFbMaxD], s_p[kFbWaves][kFbMaxD], s_gk[kFbWaves][kFbMaxD];
-  __shared__ float s_ak[kFbWaves][4][kFbMaxD], s_ac[kFbWaves][4][3];
+// LDSP: the plan of both layers staged in LDS once per workgroup (as fieldn_kernel<.., LDSP>)
+constexpr int kFbWavesL = 8;
+constexpr int64_t kFbLdsMax = 78 * 1024;
+template <bool FERRO, bool LDSP = false>
+__global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_adj_kernel(FbArgs a) {
+  constexpr int NW = LDSP ? kFbWavesL : kFbWaves;
+  __shared__ float s_x[NW][kFbMaxD], s_p[NW][kFbMaxD], s_gk[NW][kFbMaxD];
+  __shared__ float s_ak[NW][4][kFbMaxD], s_ac[NW][4][3];
+  extern __shared__ float s_plan[];
+  if constexpr (LDSP) {
+    for (int64_t q = threadIdx.x; q < a.P1.end; q += blockDim.x) s_plan[q] = a.plan[q];
+    __syncthreads();
+  }
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * kFbWaves + wid;
+  const int64_t b = (int64_t)blockIdx.x * NW + wid;
   if (b >= a.B) return;  // whole waves only; no workgroup barriers below
   const LayerPlan& P0 = a.P0;
   const LayerPlan& P1 = a.P1;
   const int D = P0.in, H = P0.out;
-  const float* __restrict__ plan = a.plan;
+  const float* __restrict__ plan = LDSP ? s_plan : a.plan;
   const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4 : a.method == FETODE_MIDPOINT ? 2 : 1;
   const int64_t n_ev = (int64_t)a.n_steps * ns;
   const float* X = a.tape;
@@ -765,8 +776,23 @@ int fetode::fieldn_fixed_backward(const fetode_field_t* f, const void* plan, int
   a.init_mask = f->ferro ? init_mask : 3u;
   a.gy0 = grad_y0;
   a.gadj = gadj;
-  hipLaunchKernelGGL(f->ferro ? fieldn_adj_kernel<true> : fieldn_adj_kernel<false>, dim3(nblk(B, kFbWaves)),
-                     dim3(64 * kFbWaves), 0, s, a);
+  const int64_t pbytes = (int64_t)sizeof(float) * a.P1.end;
+  static const int lds_on = [] {  // FETODE_FIELDN_LDS=0: the plan read from global memory (A/B)
+    const char* e = getenv("FETODE_FIELDN_LDS");
+    return e ? atoi(e) : 1;
+  }();
+  if (lds_on && pbytes <= kFbLdsMax) {
+    auto* kfn = f->ferro ? fieldn_adj_kernel<true, true> : fieldn_adj_kernel<false, true>;
+    static bool attr[2] = {false, false};  // dynamic LDS beyond the 64 KB default
+    if (!attr[f->ferro ? 1 : 0]) {
+      HIP_CHECK_RET(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFbLdsMax));
+      attr[f->ferro ? 1 : 0] = true;
+    }
+    hipLaunchKernelGGL(kfn, dim3(nblk(B, kFbWavesL)), dim3(64 * kFbWavesL), (size_t)pbytes, s, a);
+  } else {
+    auto* kfn = f->ferro ? fieldn_adj_kernel<true, false> : fieldn_adj_kernel<false, false>;
+    hipLaunchKernelGGL(kfn, dim3(nblk(B, kFbWaves)), dim3(64 * kFbWaves), 0, s, a);
+  }
   LAUNCH_CHECK();
   if (n_ev == 0) return zero_grads(f, kan_grads, ferro_grads, s);
   // parameter gradients: the per-module VJPs over all n_ev * B rows (planes: tape = x then h,

@@ -1579,34 +1579,59 @@ __device__ __forceinline__ void fn_interval(const float* __restrict__ plan, cons
 // trajectory per one-wave workgroup, every workgroup resident (grid sums of the error norms)
 // TAPE (with DOPRI): training — every evaluation's row (x, h, k) of (tape_cap, B, 2 D + H), the rows
 // fetode_integrate_dopri5_tape writes for the [2, 10, 2] fields too, and the initial-step scalars
-template <bool FERRO, bool DOPRI = false, bool TAPE = false>
-__global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(FusedArgs a) {
-  constexpr int NW = DOPRI ? 1 : kFnWaves;
+// LDSP: the whole plan (both layers) is staged in LDS once per workgroup of kFnWavesL waves and read
+// from there (every element constant, edge weight, knot and spline cubic is read per evaluation:
+// from global memory each read is an L2 round trip on the evaluation's chain); plans up to
+// kFnLdsMax bytes (e.g. KANFET([2, 16, 2], K = 12): 31 KB, KAN([4, 32, 4]): 67 KB — two 8-wave
+// workgroups per CU still fit the 160 KB)
+constexpr int kFnWavesL = 8;
+constexpr int kFnMaxT = 8;  // trajectories per wave at most (H, D <= 8)
+// lanes per trajectory: the smallest power of two >= max(H, D, 64 / kFnMaxT) (host and device agree)
+__host__ __device__ inline int fn_lanes_per_traj(int D, int H) {
+  int hp = 64 / kFnMaxT;
+  while (hp < H || hp < D) hp <<= 1;
+  return hp < 64 ? hp : 64;
+}
+constexpr int64_t kFnLdsMax = 78 * 1024;
+template <bool FERRO, bool DOPRI = false, bool TAPE = false, bool LDSP = false>
+__global__ __launch_bounds__(DOPRI ? 64 : (LDSP ? 64 * kFnWavesL : 64 * kFnWaves)) void fieldn_kernel(FusedArgs a) {
+  constexpr int NW = DOPRI ? 1 : (LDSP ? kFnWavesL : kFnWaves);
+  extern __shared__ float s_plan[];
+  if constexpr (LDSP) {
+    const int64_t n = a.P1.end;  // the plan of both layers, from word 0
+    for (int64_t q = threadIdx.x; q < n; q += blockDim.x) s_plan[q] = a.plan[q];
+    __syncthreads();
+  }
   if constexpr (DOPRI) {
     if (a.dp.xr_world > 1 && blockIdx.x == gridDim.x - 1) {  // the cross-rank exchange workgroup
       xrank_comm(a.dp);
       return;
     }
   }
-  __shared__ float s_x[NW][kFnMaxD], s_k[NW][kFnMaxD], s_p0[NW][kFnMaxD];
+  // trajectories per wave: lane = (slot t, unit o) with HP = pow2 >= max(H, D) lanes per slot
+  // (KANFET([2, 16, 2]): four trajectories per wave); the resident dopri5 keeps one per wave
+  constexpr int MT = DOPRI ? 1 : kFnMaxT;
+  __shared__ float s_x[NW][MT][kFnMaxD], s_k[NW][MT][kFnMaxD], s_p0[NW][MT][kFnMaxD];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * NW + wid;
-  const bool valid = b < a.B;
   const LayerPlan& P0 = a.P0;
   const LayerPlan& P1 = a.P1;
   const int D = P0.in, H = P0.out;
-  const float* __restrict__ plan = a.plan;
-  float* xs = s_x[wid];
-  float* ks = s_k[wid];
-  float* p0 = s_p0[wid];
-  const bool hl = lane < H;  // this lane's hidden unit
+  const int HP = DOPRI ? 64 : fn_lanes_per_traj(D, H), TPW = 64 / HP;
+  const int t = lane / HP, o = lane & (HP - 1);
+  const int64_t b = ((int64_t)blockIdx.x * NW + wid) * TPW + t;
+  const bool valid = b < a.B;
+  const float* __restrict__ plan = LDSP ? s_plan : a.plan;
+  float* xs = s_x[wid][t];
+  float* ks = s_k[wid][t];
+  float* p0 = s_p0[wid][t];
+  const bool hl = o < H;  // this lane's hidden unit
   float prev1 = 0.f;
   if (FERRO && valid) {
-    if (lane < D) p0[lane] = a.state[b * D + lane];
-    if (hl) prev1 = a.state[a.B * D + b * H + lane];
+    if (o < D) p0[o] = a.state[b * D + o];
+    if (hl) prev1 = a.state[a.B * D + b * H + o];
   }
   bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
-  const float c0o = hl ? plan[P0.fconst + lane] : 0.f;
+  const float c0o = hl ? plan[P0.fconst + o] : 0.f;
   // training tapes.  Fixed grid (fieldn_adj_kernel, fetode_fieldn_bwd.hip): two planes, the layer-0
   // inputs (n_ev, B, D) then the layer-1 inputs (n_ev, B, H).  dopri5 (TAPE): rows (x, h, k) of
   // (tape_cap, B, 2 D + H) for the first tape_cap evaluations
@@ -1619,9 +1644,9 @@ __global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(Fuse
     fn_wsync();
     if constexpr (TAPE) {
       trow = (ev < a.dp.tape_cap && valid) ? a.tape + (ev * a.B + b) * (2 * D + H) : nullptr;
-      if (trow && lane < D) trow[lane] = xs[lane];
+      if (trow && o < D) trow[o] = xs[o];
     }
-    if (tx && valid && lane < D) tx[(ev * a.B + b) * D + lane] = xs[lane];
+    if (tx && valid && o < D) tx[(ev * a.B + b) * D + o] = xs[o];
     // layer 0: h_o
     float h = 0.f;
     if (hl) {
@@ -1634,14 +1659,14 @@ __global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(Fuse
         int mfix;
         float u;
         fn_interval(plan, P0, i, x, mfix, u);
-        h += fn_edge<FERRO>(plan, P0, lane, i, x, sx, w, mfix, u);
+        h += fn_edge<FERRO>(plan, P0, o, i, x, sx, w, mfix, u);
       }
     }
-    if (tx && valid && hl) th_[(ev * a.B + b) * H + lane] = h;
-    if (TAPE && trow && hl) trow[D + lane] = h;
+    if (tx && valid && hl) th_[(ev * a.B + b) * H + o] = h;
+    if (TAPE && trow && hl) trow[D + o] = h;
     ++ev;
     fn_wsync();
-    if (FERRO && lane < D) p0[lane] = xs[lane];  // ferro_class.py:409
+    if (FERRO && o < D) p0[o] = xs[o];  // ferro_class.py:409
     re0 = false;
     // layer 1: lane o's contributions to every output, then the sum over the lanes
     float w1 = 0.f, sh = 0.f, u1 = 0.f;
@@ -1649,21 +1674,20 @@ __global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(Fuse
     if (hl) {
       sh = h * fn_sig_l2(-h * FETODE_LOG2E);
       if constexpr (FERRO) w1 = ffma(fn_sig_l2(-P1.gsl2e * (h - (re1 ? h : prev1))), -P1.wc, P1.wc);
-      fn_interval(plan, P1, lane, h, m1, u1);
+      fn_interval(plan, P1, o, h, m1, u1);
     }
     if (FERRO) prev1 = h;
     re1 = false;
     for (int d = 0; d < D; ++d) {
-      float v = hl ? fn_edge<FERRO>(plan, P1, d, lane, h, sh, w1, m1, u1) : 0.f;
-#pragma unroll
-      for (int s = 32; s >= 1; s >>= 1) v += __shfl_xor(v, s);
-      if (lane == 0) ks[d] = v + plan[P1.fconst + d];
+      float v = hl ? fn_edge<FERRO>(plan, P1, d, o, h, sh, w1, m1, u1) : 0.f;
+      for (int s = HP >> 1; s >= 1; s >>= 1) v += __shfl_xor(v, s);  // within the slot's HP lanes
+      if (o == 0) ks[d] = v + plan[P1.fconst + d];
     }
     fn_wsync();
   };
   // lane d < D carries state dim d
-  const bool dl = lane < D;
-  float y = (valid && dl) ? a.y0[b * D + lane] : 0.f;
+  const bool dl = o < D;
+  float y = (valid && dl) ? a.y0[b * D + o] : 0.f;
   if constexpr (DOPRI) {
     // ---- device-resident dopri5: fused4's driver (dopri5.py _Dopri5's control arithmetic) with
     // lane d < D of the trajectory's wave carrying y_d; one grid sum per norm ----
@@ -1678,13 +1702,13 @@ __global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(Fuse
       if (grid_sum2(P, round, v0, v1, s0, s1)) status = 4;
     };
     auto f = [&](float xin) -> float {
-      if (dl) xs[lane] = xin;
+      if (dl) xs[o] = xin;
       eval();
-      const float k = dl ? ks[lane] : 0.f;
-      if (TAPE && trow && dl) trow[D + H + lane] = k;
+      const float k = dl ? ks[o] : 0.f;
+      if (TAPE && trow && dl) trow[D + H + o] = k;
       return k;
     };
-    if (real) a.solution[b * D + lane] = y;
+    if (real) a.solution[b * D + o] = y;
     float f0 = f(y);
     ++nfev;
     double dt;
@@ -1794,7 +1818,7 @@ __global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(Fuse
         xp = xp * xq;
         total = total + xp * co[j];
       }
-      if (real) a.solution[((int64_t)i * a.B + b) * D + lane] = total;
+      if (real) a.solution[((int64_t)i * a.B + b) * D + o] = total;
     }
     if (P.xr_world > 1 && blockIdx.x == 0 && threadIdx.x == 0)  // the exchange workgroup may stop
       __hip_atomic_store(dp_fin(P), round + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1804,11 +1828,11 @@ __global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(Fuse
       P.stats[2] = __hip_atomic_load(P.bar + kDpLine * (kDpGroups + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 4 : status;
     }
   } else if (a.single_eval) {
-    if (dl) xs[lane] = y;
+    if (dl) xs[o] = y;
     eval();
-    if (valid && dl) a.eval_out[b * D + lane] = ks[lane];
+    if (valid && dl) a.eval_out[b * D + o] = ks[o];
   } else {
-    if (valid && dl) a.solution[b * D + lane] = y;
+    if (valid && dl) a.solution[b * D + o] = y;
     const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4 : a.method == FETODE_MIDPOINT ? 2 : 1;
     const float third = 1.0f / 3.0f;
     int jj = 1;
@@ -1828,9 +1852,9 @@ __global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(Fuse
         } else if (a.method == FETODE_MIDPOINT) {
           if (st == 1) xin = y + k1 * hh;
         }
-        if (dl) xs[lane] = xin;
+        if (dl) xs[o] = xin;
         eval();
-        const float kk = dl ? ks[lane] : 0.f;
+        const float kk = dl ? ks[o] : 0.f;
         if (st == 0) k1 = kk;
         else if (st == 1) k2 = kk;
         else if (st == 2) k3 = kk;
@@ -1844,14 +1868,14 @@ __global__ __launch_bounds__(DOPRI ? 64 : 64 * kFnWaves) void fieldn_kernel(Fuse
       for (; jj < a.T && a.out_step[jj] == s; ++jj) {
         const int mode = a.out_mode[jj];
         const float v = mode == 0 ? y : (mode == 1 ? y1 : y + a.out_slope[jj] * (y1 - y));
-        if (valid && dl) a.solution[((int64_t)jj * a.B + b) * D + lane] = v;
+        if (valid && dl) a.solution[((int64_t)jj * a.B + b) * D + o] = v;
       }
       y = y1;
     }
   }
   if (FERRO && valid) {
-    if (dl) a.state[b * D + lane] = p0[lane];
-    if (hl) a.state[a.B * D + b * H + lane] = prev1;
+    if (dl) a.state[b * D + o] = p0[o];
+    if (hl) a.state[a.B * D + b * H + o] = prev1;
   }
 }
 
@@ -1877,8 +1901,24 @@ int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
     if (!fieldn_supported(f)) return set_err(FETODE_EUNSUPPORTED, "no fused kernel for this field shape");
     layer_plan(f->kan[0], f->ferro ? &f->ferro[0] : nullptr, 0, &a.P0);
     layer_plan(f->kan[1], f->ferro ? &f->ferro[1] : nullptr, a.P0.end, &a.P1);
-    hipLaunchKernelGGL(f->ferro ? fieldn_kernel<true> : fieldn_kernel<false>, dim3(nblk(a.B, kFnWaves)),
-                       dim3(64 * kFnWaves), 0, (hipStream_t)stream, a);
+    const int64_t pbytes = (int64_t)sizeof(float) * a.P1.end;
+    const int tpw = 64 / fn_lanes_per_traj(a.P0.in, a.P0.out);
+    static const int lds_on = [] {  // FETODE_FIELDN_LDS=0: the plan read from global memory (A/B)
+      const char* e = getenv("FETODE_FIELDN_LDS");
+      return e ? atoi(e) : 1;
+    }();
+    if (lds_on && pbytes <= kFnLdsMax) {
+      auto* kfn = f->ferro ? fieldn_kernel<true, false, false, true> : fieldn_kernel<false, false, false, true>;
+      static bool attr[2] = {false, false};  // dynamic LDS beyond the 64 KB default
+      if (!attr[f->ferro ? 1 : 0]) {
+        HIP_CHECK_RET(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFnLdsMax));
+        attr[f->ferro ? 1 : 0] = true;
+      }
+      hipLaunchKernelGGL(kfn, dim3(nblk(a.B, (int64_t)kFnWavesL * tpw)), dim3(64 * kFnWavesL), (size_t)pbytes,
+                         (hipStream_t)stream, a);
+    } else
+      hipLaunchKernelGGL(f->ferro ? fieldn_kernel<true> : fieldn_kernel<false>, dim3(nblk(a.B, (int64_t)kFnWaves * tpw)),
+                         dim3(64 * kFnWaves), 0, (hipStream_t)stream, a);
     LAUNCH_CHECK();
     return FETODE_OK;
   }
