@@ -53,6 +53,12 @@ int validate_field(const fetode_field_t* f);
 // depth-2 fields of other widths served by fieldn_kernel (fetode_fused.hip), and their reverse
 // sweep (fetode_fieldn_bwd.hip): arguments and workspace as fetode_integrate_fixed_backward
 bool fieldn_shape_supported(const fetode_field_t* f);
+// Ferro parameter sums over R rows split across workgroups (fetode_grad.hip; E * S <= 8192 partial
+// slots of the fixed-size workspace): the hysteresis input of row r is p0[r] (or x[r] when p0 is
+// null) for r < n0 and x[r - n0] after
+int64_t ferro_param_rows_workspace();
+int ferro_param_rows(const fetode_ferro_t* fl, const float* x, int64_t R, const float* p0, int64_t n0, const float* g,
+                     const fetode_ferro_grad_t* grads, void* workspace, int32_t accumulate, void* stream);
 int64_t fieldn_fixed_backward_workspace(const fetode_field_t* f, int32_t method, int32_t n_steps, int64_t B);
 int fieldn_fixed_backward(const fetode_field_t* f, const void* plan, int32_t method, int64_t B, const float* step_coef,
                           int32_t n_steps, const int32_t* out_step, const int32_t* out_mode, const float* out_slope,

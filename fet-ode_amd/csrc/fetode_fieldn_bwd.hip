@@ -163,23 +163,36 @@ __device__ void fb_coefs(int method, float dt, float hh, float h6, float bc[4], 
 
 // LDSP: the plan of both layers staged in LDS once per workgroup (as fieldn_kernel<.., LDSP>)
 constexpr int kFbWavesL = 8;
+constexpr int kFbMaxT = 8;  // trajectories per wave at most
+// lanes per trajectory: the smallest power of two >= max(H, D, 64 / kFbMaxT) (fieldn_kernel's rule)
+__host__ __device__ inline int fb_lanes_per_traj(int D, int H) {
+  int hp = 64 / kFbMaxT;
+  while (hp < H || hp < D) hp <<= 1;
+  return hp < 64 ? hp : 64;
+}
 constexpr int64_t kFbLdsMax = 78 * 1024;
 template <bool FERRO, bool LDSP = false>
 __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_adj_kernel(FbArgs a) {
   constexpr int NW = LDSP ? kFbWavesL : kFbWaves;
-  __shared__ float s_x[NW][kFbMaxD], s_p[NW][kFbMaxD], s_gk[NW][kFbMaxD];
-  __shared__ float s_ak[NW][4][kFbMaxD], s_ac[NW][4][3];
+  // several trajectories per wave, as fieldn_kernel: lane = (slot t, unit o), HP lanes per slot
+  __shared__ float s_x[NW][kFbMaxT][kFbMaxD], s_p[NW][kFbMaxT][kFbMaxD], s_gk[NW][kFbMaxT][kFbMaxD];
+  __shared__ float s_ak[NW][kFbMaxT][4][kFbMaxD], s_ac[NW][4][3];
   extern __shared__ float s_plan[];
   if constexpr (LDSP) {
     for (int64_t q = threadIdx.x; q < a.P1.end; q += blockDim.x) s_plan[q] = a.plan[q];
     __syncthreads();
   }
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t b = (int64_t)blockIdx.x * NW + wid;
-  if (b >= a.B) return;  // whole waves only; no workgroup barriers below
   const LayerPlan& P0 = a.P0;
   const LayerPlan& P1 = a.P1;
   const int D = P0.in, H = P0.out;
+  const int HP = fb_lanes_per_traj(D, H), TPW = 64 / HP;
+  const int t = lane / HP, o = lane & (HP - 1);
+  const int64_t bw = ((int64_t)blockIdx.x * NW + wid) * TPW;
+  if (bw >= a.B) return;  // whole waves only; no workgroup barriers below
+  const int64_t b = bw + t;
+  const bool live = b < a.B;  // a missing slot runs on zeros (its lanes still take part in the sums)
+  const int64_t bi = live ? b : bw;
   const float* __restrict__ plan = LDSP ? s_plan : a.plan;
   const int ns = a.method == FETODE_RK4 || a.method == FETODE_RK4_CLASSIC ? 4 : a.method == FETODE_MIDPOINT ? 2 : 1;
   const int64_t n_ev = (int64_t)a.n_steps * ns;
@@ -187,12 +200,12 @@ __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_
   const float* Hh = a.tape + n_ev * a.B * D;
   float* GK = a.gadj;
   float* GH = a.gadj + n_ev * a.B * D;
-  float* xs = s_x[wid];
-  float* ps = s_p[wid];
-  float* gk = s_gk[wid];
-  float(&ak)[4][kFbMaxD] = s_ak[wid];
+  float* xs = s_x[wid][t];
+  float* ps = s_p[wid][t];
+  float* gk = s_gk[wid][t];
+  float(&ak)[4][kFbMaxD] = s_ak[wid][t];
   float(&acs)[4][3] = s_ac[wid];
-  const bool dl = lane < D, hl = lane < H;
+  const bool dl = o < D, hl = o < H;
   float ay1 = 0.f, ay = 0.f;  // adjoint of y at the end of the current step (lanes < D)
   int jj = a.T - 1;
   for (int s = a.n_steps - 1; s >= 0; --s) {
@@ -201,7 +214,7 @@ __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_
     float ay0x = 0.f;  // outputs produced in this step (y at step start, end, or interpolated)
     for (; jj >= 1 && a.out_step[jj] == s; --jj) {
       if (dl) {
-        const float g = a.gsol[((int64_t)jj * a.B + b) * D + lane];
+        const float g = live ? a.gsol[((int64_t)jj * a.B + bi) * D + o] : 0.f;
         const int mode = a.out_mode[jj];
         if (mode == 0) {
           ay0x += g;
@@ -215,7 +228,7 @@ __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_
       }
     }
     if (dl) {
-      for (int j = 0; j < ns; ++j) ak[j][lane] = bc[j] * ay1;
+      for (int j = 0; j < ns; ++j) ak[j][o] = bc[j] * ay1;
       ay = ay1 + ay0x;
     }
     if (lane == 0)
@@ -224,40 +237,42 @@ __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_
     for (int st = ns - 1; st >= 0; --st) {
       const int64_t ev = (int64_t)s * ns + st;
       if (dl) {
-        const float x = X[(ev * a.B + b) * D + lane];
-        xs[lane] = x;
-        ps[lane] = ev > 0 ? X[((ev - 1) * a.B + b) * D + lane]
-                          : ((a.init_mask & 1u) ? x : (FERRO ? a.state0[b * D + lane] : 0.f));
-        gk[lane] = ak[st][lane];
+        const float x = live ? X[(ev * a.B + bi) * D + o] : 0.f;
+        xs[o] = x;
+        ps[o] = !live ? 0.f
+                : ev > 0 ? X[((ev - 1) * a.B + bi) * D + o]
+                         : ((a.init_mask & 1u) ? x : (FERRO ? a.state0[bi * D + o] : 0.f));
+        gk[o] = ak[st][o];
       }
       float h = 0.f, ph = 0.f;
-      if (hl) {
-        h = Hh[(ev * a.B + b) * H + lane];
-        ph = ev > 0 ? Hh[((ev - 1) * a.B + b) * H + lane]
-                    : ((a.init_mask & 2u) ? h : (FERRO ? a.state0[a.B * D + b * H + lane] : 0.f));
+      if (hl && live) {
+        h = Hh[(ev * a.B + bi) * H + o];
+        ph = ev > 0 ? Hh[((ev - 1) * a.B + bi) * H + o]
+                    : ((a.init_mask & 2u) ? h : (FERRO ? a.state0[a.B * D + bi * H + o] : 0.f));
       }
       fb_wsync();
       // layer 1 (h -> k): d loss / d h_o on lane o
-      const float gh = hl ? fb_vjp_input<FERRO>(plan, P1, lane, h, ph, gk, 0, D) : 0.f;
-      if (dl) GK[(ev * a.B + b) * D + lane] = gk[lane];
-      if (hl) GH[(ev * a.B + b) * H + lane] = gh;
+      const float gh = hl ? fb_vjp_input<FERRO>(plan, P1, o, h, ph, gk, 0, D) : 0.f;
+      if (live && dl) GK[(ev * a.B + b) * D + o] = gk[o];
+      if (live && hl) GH[(ev * a.B + b) * H + o] = gh;
       // layer 0 (x -> h): d loss / d x_i = sum over the lanes o of gh_o d edge(o, i) / d x_i
       float gx = 0.f;
       for (int i = 0; i < D; ++i) {
         const float one = 1.0f;
-        const float c = hl ? gh * fb_vjp_input<FERRO>(plan, P0, i, xs[i], ps[i], &one, lane, 1) : 0.f;
-        const float sum = fb_wave_sum(c);
-        if (lane == i) gx = sum;
+        const float c = hl ? gh * fb_vjp_input<FERRO>(plan, P0, i, xs[i], ps[i], &one, o, 1) : 0.f;
+        float sum = c;
+        for (int m = HP >> 1; m >= 1; m >>= 1) sum += __shfl_xor(sum, m);  // within the slot's lanes
+        if (o == i) gx = sum;
       }
       if (dl) {
         ay += gx;
-        for (int j = 0; j < st; ++j) ak[j][lane] = ffma(acs[st][j], gx, ak[j][lane]);
+        for (int j = 0; j < st; ++j) ak[j][o] = ffma(acs[st][j], gx, ak[j][o]);
       }
       fb_wsync();
     }
     ay1 = ay;
   }
-  if (dl && a.gy0) a.gy0[b * D + lane] = ay1 + a.gsol[b * D + lane];  // solution[0] = y0
+  if (live && dl && a.gy0) a.gy0[b * D + o] = ay1 + a.gsol[b * D + o];  // solution[0] = y0
 }
 
 // =============================================================================================
@@ -689,6 +704,12 @@ static int64_t fieldn_dopri_resident(bool ferro) {
 }
 
 // workspace: grid-sum words and slots | output / hidden adjoint planes | layer-input planes | KAN VJP scratch
+// the parameter-VJP scratch: the larger KANLinear workspace, or the Ferro row-split partials
+static int64_t param_ws(int64_t kw0, int64_t kw1) {
+  int64_t w = kw0 > kw1 ? kw0 : kw1;
+  return w > ferro_param_rows_workspace() ? w : ferro_param_rows_workspace();
+}
+
 struct FdWs {
   int64_t bar, slot, gadj, xc, hc, kws, total;
 };
@@ -702,7 +723,7 @@ static FdWs fieldn_dopri_ws(const fetode_field_t* f, int64_t B, int64_t n_ev) {
   w.xc = w.gadj + (int64_t)sizeof(float) * align16(n_ev * B * (D + H));
   w.hc = w.xc + (int64_t)sizeof(float) * align16(n_ev * B * D);
   w.kws = w.hc + (int64_t)sizeof(float) * align16(n_ev * B * H);
-  w.total = w.kws + (kw0 > kw1 ? kw0 : kw1);
+  w.total = w.kws + param_ws(kw0, kw1);
   return w;
 }
 
@@ -713,26 +734,22 @@ static int fieldn_param_vjps(const fetode_field_t* f, int64_t B, int64_t n_ev, c
                       const float* GKp, const float* GHp, const float* state0, uint32_t init_mask,
                       const fetode_kanlinear_grad_t* kan_grads, const fetode_ferro_grad_t* ferro_grads, void* kws,
                       void* stream) {
-  const int D = f->kan[0].in_features, H = f->kan[0].out_features;
+  const int D = f->kan[0].in_features;
   const int64_t R = n_ev * B;
   for (int l = 0; l < 2; ++l) {
     const float* x = l == 0 ? Xp : Hp;
     const float* g = l == 0 ? GHp : GKp;
-    const int in = l == 0 ? D : H;
     if (kan_grads && any_kan(kan_grads[l])) {
       const int rc = fetode_kanlinear_backward(&f->kan[l], x, R, g, nullptr, &kan_grads[l], kws, 0, stream);
       if (rc) return rc;
     }
     if (f->ferro && ferro_grads && any_ferro(ferro_grads[l])) {
+      // one row-split launch over both hysteresis rules (evaluation 0: the state before the solve or
+      // reinit; later evaluations: the previous one, B rows earlier)
       const bool re = (init_mask >> l) & 1u;
       const float* p0 = re ? nullptr : state0 + (l == 0 ? 0 : B * D);
-      int rc = fetode_ferro_backward(&f->ferro[l], x, B, p0, re ? 1 : 0, g, nullptr, &ferro_grads[l], 0, stream);
+      const int rc = ferro_param_rows(&f->ferro[l], x, R, p0, B, g, &ferro_grads[l], kws, 0, stream);
       if (rc) return rc;
-      if (n_ev > 1) {
-        rc = fetode_ferro_backward(&f->ferro[l], x + B * in, R - B, x, 0, g + B * (l == 0 ? H : D), nullptr,
-                                   &ferro_grads[l], 1, stream);
-        if (rc) return rc;
-      }
     }
   }
   return FETODE_OK;
@@ -742,7 +759,7 @@ int64_t fetode::fieldn_fixed_backward_workspace(const fetode_field_t* f, int32_t
   const int64_t D = f->kan[0].in_features, H = f->kan[0].out_features;
   const int64_t kw0 = fetode_kanlinear_backward_workspace(&f->kan[0]), kw1 = fetode_kanlinear_backward_workspace(&f->kan[1]);
   if (kw0 < 0 || kw1 < 0) return -1;
-  return (int64_t)sizeof(float) * align16(n_evals(method, n_steps) * B * (D + H)) + (kw0 > kw1 ? kw0 : kw1);
+  return (int64_t)sizeof(float) * align16(n_evals(method, n_steps) * B * (D + H)) + param_ws(kw0, kw1);
 }
 
 int fetode::fieldn_fixed_backward(const fetode_field_t* f, const void* plan, int32_t method, int64_t B,
@@ -777,6 +794,7 @@ int fetode::fieldn_fixed_backward(const fetode_field_t* f, const void* plan, int
   a.gy0 = grad_y0;
   a.gadj = gadj;
   const int64_t pbytes = (int64_t)sizeof(float) * a.P1.end;
+  const int tpw = 64 / fb_lanes_per_traj(D, H);
   static const int lds_on = [] {  // FETODE_FIELDN_LDS=0: the plan read from global memory (A/B)
     const char* e = getenv("FETODE_FIELDN_LDS");
     return e ? atoi(e) : 1;
@@ -788,10 +806,10 @@ int fetode::fieldn_fixed_backward(const fetode_field_t* f, const void* plan, int
       HIP_CHECK_RET(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kFbLdsMax));
       attr[f->ferro ? 1 : 0] = true;
     }
-    hipLaunchKernelGGL(kfn, dim3(nblk(B, kFbWavesL)), dim3(64 * kFbWavesL), (size_t)pbytes, s, a);
+    hipLaunchKernelGGL(kfn, dim3(nblk(B, kFbWavesL * tpw)), dim3(64 * kFbWavesL), (size_t)pbytes, s, a);
   } else {
     auto* kfn = f->ferro ? fieldn_adj_kernel<true, false> : fieldn_adj_kernel<false, false>;
-    hipLaunchKernelGGL(kfn, dim3(nblk(B, kFbWaves)), dim3(64 * kFbWaves), 0, s, a);
+    hipLaunchKernelGGL(kfn, dim3(nblk(B, kFbWaves * tpw)), dim3(64 * kFbWaves), 0, s, a);
   }
   LAUNCH_CHECK();
   if (n_ev == 0) return zero_grads(f, kan_grads, ferro_grads, s);

@@ -554,67 +554,109 @@ __global__ void kan_scale_ls_kernel(fetode_kanlinear_t kl, const float* __restri
 
 // ------------------------------------------------------------------------------------------
 // Parameter sums over many rows (B >= kPsMinRows: the fieldn training pass runs them over every
-// (evaluation, trajectory) row, fetode_fieldn_bwd.hip): workgroup (input i, row split s) walks
-// tiles of kPsTile rows — each row's NF features of x[r, i] formed ONCE (kan_gw_kernel forms them
-// once per (o, i, f) block: out * NF times), the tile's g rows staged — and every thread sums a
-// 4 x 4 block of (feature, output) products over its share of the tile's rows; the logistic a / b
-// sums ride along per row.  Per-thread partials -> fixed-order workgroup sums -> per-split slots
-// -> kan_psum_reduce_kernel sums the splits in order (run-to-run identical).
+// (evaluation, trajectory) row, fetode_fieldn_bwd.hip): workgroup (input group, row split s) walks
+// tiles of kPsTile rows.  Every thread forms the NF features of one (row, input) of the group ONCE
+// (kan_gw_kernel forms them once per (o, i, f) block: out * NF times) while the NEXT tile's x and
+// g are already in flight (the walk is latency-bound otherwise: two dependent global round trips
+// per tile); then every thread sums a 4 x 4 block of (feature, output) products of one input over
+// its share of the tile's rows; the logistic a / b sums ride along per (row, input).  Per-thread
+// partials -> fixed-order workgroup sums -> per-split slots -> kan_psum_reduce_kernel sums the
+// splits in order (run-to-run identical).
 // ------------------------------------------------------------------------------------------
-constexpr int kPsTile = 64, kPsMaxNF = 40, kPsMaxOut = 64, kPsMinRows = 2048, kPsBlocks = 2048;
-int ps_splits(int in, int64_t B) {
-  int64_t S = kPsBlocks / in;
+constexpr int kPsTile = 64, kPsMaxNF = 40, kPsMaxOut = 64, kPsMinRows = 2048, kPsBlocks = 2048, kPsMaxIG = 4;
+constexpr int kPsGReg = kPsTile / 4;  // g values a thread stages per tile (a column of every 4th row)
+// inputs per workgroup: up to 4, as long as the (input, feature block, output block) triples fit 256 threads
+__host__ __device__ inline int ps_ig(int in, int NF, int out) {
+  const int fo = ((NF + 3) / 4) * ((out + 3) / 4);
+  int ig = in < kPsMaxIG ? in : kPsMaxIG;
+  while (ig > 1 && ig * fo > 256) --ig;
+  return ig;
+}
+int ps_nf(const fetode_kanlinear_t* kl) { return 1 + kl->grid_size + kl->spline_order + kl->num_logistic; }
+int ps_groups(const fetode_kanlinear_t* kl) {
+  const int ig = ps_ig(kl->in_features, ps_nf(kl), kl->out_features);
+  return (kl->in_features + ig - 1) / ig;
+}
+int ps_smax(const fetode_kanlinear_t* kl) { return kPsBlocks / ps_groups(kl) > 1 ? kPsBlocks / ps_groups(kl) : 1; }
+int ps_splits(const fetode_kanlinear_t* kl, int64_t B) {
+  int64_t S = ps_smax(kl);
   const int64_t tiles = (B + kPsTile - 1) / kPsTile;
   if (S > tiles) S = tiles;
   return S < 1 ? 1 : (int)S;
 }
-int ps_smax(int in) { return kPsBlocks / in > 1 ? kPsBlocks / in : 1; }
+size_t ps_lds_bytes(const fetode_kanlinear_t* kl) {
+  const int NF = ps_nf(kl), out = kl->out_features, ig = ps_ig(kl->in_features, NF, out);
+  const int64_t n = (int64_t)ig * kPsTile * (NF | 1) + (int64_t)kPsTile * (out | 1) + (int64_t)ig * out * kl->num_logistic;
+  return sizeof(float) * (size_t)(n > 256 * 16 ? n : 256 * 16);
+}
 
-template <int SO>
+template <int SO, bool LOG>
 __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, const float* __restrict__ x,
                                                       const float* __restrict__ g, int64_t B,
                                                       float* __restrict__ part /* (S, in, NF, out) */,
                                                       float* __restrict__ abpart /* (S, in, NB, 2) */) {
-  __shared__ float ft[kPsTile][kPsMaxNF + 1];
-  __shared__ float gt[kPsTile][kPsMaxOut + 1];
-  __shared__ float wl[kPsMaxOut][kMaxLogistic];
-  __shared__ float red[256 * 16];
-  const int in = kl.in_features, out = kl.out_features, NB = kl.num_logistic;
+  extern __shared__ float ps_lds[];
+  const int in = kl.in_features, out = kl.out_features, NB = LOG ? kl.num_logistic : 0;
   const int NG = kl.grid_size + 2 * SO + 1, NS = kl.grid_size + SO, NF = 1 + NS + NB;
-  const int i = blockIdx.x, s = blockIdx.y, S = gridDim.y, tid = threadIdx.x;
+  const int IG = ps_ig(in, NF, out), i0 = blockIdx.x * IG, ni = in - i0 < IG ? in - i0 : IG;
+  const int s = blockIdx.y, S = gridDim.y, tid = threadIdx.x;
+  // odd row strides: a thread per row reads its row's g (logistic a / b) without bank conflicts
+  const int FS = NF | 1, GS = out | 1;
+  float* ft = ps_lds;                          // [IG * kPsTile][FS]: (input, row) features
+  float* gt = ft + IG * kPsTile * FS;          // [kPsTile][GS]
+  float* wl = gt + kPsTile * GS;               // [IG][out][NB]
+  float* red = ps_lds;                         // the workgroup sums, after the walk
   const int64_t tiles = (B + kPsTile - 1) / kPsTile;
   const int64_t t0 = s * tiles / S, t1 = (s + 1) * tiles / S;
-  // the logistic weights W'[o, (i, j)] of this input (a / b sums)
-  for (int q = tid; q < out * NB; q += 256) {
-    const int o = q / NB, j = q % NB;
+  // the logistic weights W'[o, (i, j)] of the group's inputs (a / b sums)
+  for (int q = tid; LOG && q < ni * out * NB; q += 256) {
+    const int ig = q / (out * NB), o = (q / NB) % out, j = q % NB;
     const float ls = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
-    wl[o][j] = (kl.logistic_weight[(int64_t)o * in * NB + i * NB + j] * kl.scale_logistic) * ls;
+    wl[q] = (kl.logistic_weight[(int64_t)o * in * NB + (i0 + ig) * NB + j] * kl.scale_logistic) * ls;
   }
-  // this thread's (feature, output) block and its share of the tile's rows
-  const int FBK = (NF + 3) / 4, OBK = (out + 3) / 4, P = FBK * OBK, Q = P < 256 ? 256 / P : 1;
+  // feature role: (input fig, row frr) of each tile
+  const int fig = tid / kPsTile, frr = tid % kPsTile;
+  const bool fe = fig < ni;
+  const int fin = i0 + (fe ? fig : 0);
+  const float* gi = kl.grid + (int64_t)fin * NG;
+  // sum role: a (input, feature block, output block) triple and a share of the tile's rows
+  const int FBK = (NF + 3) / 4, OBK = (out + 3) / 4, P = ni * FBK * OBK, Q = P < 256 ? 256 / P : 1;
   const int p = tid % P, q = tid / P;
   const bool act = tid < P * Q;
-  const int f0 = 4 * (p / OBK), o0 = 4 * (p % OBK);
+  const int pig = p / (FBK * OBK), f0 = 4 * ((p / OBK) % FBK), o0 = 4 * (p % OBK);
   float acc[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[a][c] = 0.f;
-  float la[kMaxLogistic], lb[kMaxLogistic];
+  constexpr int NL = LOG ? kMaxLogistic : 1;
+  float la[NL], lb[NL];
 #pragma unroll
-  for (int j = 0; j < kMaxLogistic; ++j) la[j] = lb[j] = 0.f;
-  const float* gi = kl.grid + (int64_t)i * NG;
+  for (int j = 0; j < NL; ++j) la[j] = lb[j] = 0.f;
+  // the next tile's x (this thread's row / input) and g (its share of the tile) in registers
+  float xn = 0.f, gn[kPsGReg];
+  const int gc = tid & 63, gr0 = tid >> 6;  // g staging: column gc of rows gr0, gr0 + 4, ...
+  auto fetch = [&](int64_t tl) {
+    const int64_t r0 = tl * kPsTile;
+    xn = (fe && r0 + frr < B) ? x[(r0 + frr) * in + fin] : 0.f;
+#pragma unroll
+    for (int k = 0; k < kPsGReg; ++k) {  // row gr0 + 4 k, column gc
+      const int64_t r = r0 + gr0 + 4 * k;
+      gn[k] = (gc < out && r < B) ? g[r * out + gc] : 0.f;
+    }
+  };
+  if (t0 < t1) fetch(t0);
   for (int64_t tl = t0; tl < t1; ++tl) {
     const int64_t r0 = tl * kPsTile;
+    const bool live = fe && r0 + frr < B;
+    const float xv = xn;
     __syncthreads();  // the previous tile's reads are done
-    for (int e = tid; e < kPsTile * out; e += 256) {
-      const int rr = e / out, o = e % out;
-      gt[rr][o] = r0 + rr < B ? g[(r0 + rr) * out + o] : 0.f;
-    }
-    if (tid < kPsTile) {  // row r0 + tid: the features as kan_gw_kernel forms them
-      const bool live = r0 + tid < B;
-      const float xv = live ? x[(r0 + tid) * in + i] : 0.f;
-      float* fr = ft[tid];
+#pragma unroll
+    for (int k = 0; k < kPsGReg; ++k)
+      if (gc < out) gt[(gr0 + 4 * k) * GS + gc] = gn[k];
+    if (tl + 1 < t1) fetch(tl + 1);
+    if (fe) {  // row r0 + frr, input fin: the features as kan_gw_kernel forms them
+      float* fr = ft + (fig * kPsTile + frr) * FS;
       fr[0] = live ? xv * sigm(xv) : 0.f;
       float val[SO + 1], der[SO + 1];
       const int m = bspline_vals_derivs<SO>(xv, NG, gi, val, der);
@@ -626,28 +668,40 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
         fr[1 + c] = v;
       }
       for (int j = 0; j < NB; ++j)
-        fr[1 + NS + j] = live ? 2.0f / (1.0f + expf(-kl.logistic_a[i * NB + j] * (xv - kl.logistic_b[i * NB + j]))) : 0.f;
+        fr[1 + NS + j] = live ? 2.0f / (1.0f + expf(-kl.logistic_a[fin * NB + j] * (xv - kl.logistic_b[fin * NB + j]))) : 0.f;
     }
     __syncthreads();
-    if (tid < kPsTile && NB > 0 && r0 + tid < B) {  // logistic a / b: d phi_j through the row's g
-      const float xv = x[(r0 + tid) * in + i];
-      for (int j = 0; j < NB && j < kMaxLogistic; ++j) {
-        float gphi = 0.f;
-        for (int o = 0; o < out; ++o) gphi += gt[tid][o] * wl[o][j];
-        const float a = kl.logistic_a[i * NB + j], bb = kl.logistic_b[i * NB + j];
-        const float sg = 0.5f * ft[tid][1 + NS + j];  // sigm(a (x - b))
+    if (LOG && live) {  // logistic a / b: d phi_j through the row's g
+      const float* fr = ft + (fig * kPsTile + frr) * FS;
+      float gph[NL];
+#pragma unroll
+      for (int j = 0; j < NL; ++j) gph[j] = 0.f;
+      for (int o = 0; o < out; ++o) {  // d loss / d phi_j = sum_o g[o] W'[o, (i, j)]
+        const float go = gt[frr * GS + o];
+        const float* wr = wl + (fig * out + o) * NB;
+#pragma unroll
+        for (int j = 0; j < NL; ++j)
+          if (j < NB) gph[j] += go * wr[j];
+      }
+#pragma unroll
+      for (int j = 0; j < NL; ++j) {
+        if (j >= NB) break;
+        const float gphi = gph[j];
+        const float a = kl.logistic_a[fin * NB + j], bb = kl.logistic_b[fin * NB + j];
+        const float sg = 0.5f * fr[1 + NS + j];  // sigm(a (x - b))
         const float dz = gphi * 2.0f * sg * (1.0f - sg);
         la[j] += dz * (xv - bb);
         lb[j] += dz * (-a);
       }
     }
     if (act) {
+      const float* fb = ft + pig * kPsTile * FS;
       for (int rr = q; rr < kPsTile; rr += Q) {
         float fv[4], gv[4];
 #pragma unroll
-        for (int a = 0; a < 4; ++a) fv[a] = f0 + a < NF ? ft[rr][f0 + a] : 0.f;
+        for (int a = 0; a < 4; ++a) fv[a] = f0 + a < NF ? fb[rr * FS + f0 + a] : 0.f;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) gv[c] = o0 + c < out ? gt[rr][o0 + c] : 0.f;
+        for (int c = 0; c < 4; ++c) gv[c] = o0 + c < out ? gt[rr * GS + o0 + c] : 0.f;
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -655,44 +709,55 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
       }
     }
   }
-  // workgroup sums in a fixed order: the Q row groups of each block, then the tile rows' a / b
+  // workgroup sums in a fixed order: the Q row groups of each triple, then the tile rows' a / b
   __syncthreads();
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int c = 0; c < 4; ++c) red[tid * 16 + a * 4 + c] = acc[a][c];
   __syncthreads();
-  float* dst = part + ((int64_t)s * in + i) * NF * out;
   for (int e = tid; e < P * 16; e += 256) {
     const int pp = e / 16, ac = e % 16, a = ac / 4, c = ac % 4;
-    const int f = 4 * (pp / OBK) + a, o = 4 * (pp % OBK) + c;
+    const int ig = pp / (FBK * OBK);
+    const int f = 4 * ((pp / OBK) % FBK) + a, o = 4 * (pp % OBK) + c;
     float v = 0.f;
     for (int qq = 0; qq < Q; ++qq) v += red[(qq * P + pp) * 16 + ac];
-    if (f < NF && o < out) dst[f * out + o] = v;
+    if (f < NF && o < out) part[(((int64_t)s * in + i0 + ig) * NF + f) * out + o] = v;
   }
-  if (NB > 0) {
-    __syncthreads();
-    for (int j = 0; j < NB && j < kMaxLogistic; ++j) {
-      if (tid < kPsTile) {
+  if (LOG) {
+    for (int j = 0; j < NB && j < NL; ++j) {
+      __syncthreads();
+      if (fe) {
         red[tid * 2] = la[j];
         red[tid * 2 + 1] = lb[j];
       }
       __syncthreads();
-      if (tid < 2) {
+      if (tid < 2 * ni) {
+        const int ig = tid / 2, c = tid % 2;
         float v = 0.f;
-        for (int rr = 0; rr < kPsTile; ++rr) v += red[rr * 2 + tid];
-        abpart[(((int64_t)s * in + i) * NB + j) * 2 + tid] = v;
+        for (int rr = 0; rr < kPsTile; ++rr) v += red[(ig * kPsTile + rr) * 2 + c];
+        abpart[(((int64_t)s * in + i0 + ig) * NB + j) * 2 + c] = v;
       }
-      __syncthreads();
     }
   }
 }
 
-// the splits in order -> base-weight gradient, d_scaled, d_wl, logistic a / b
-__global__ void kan_psum_reduce_kernel(fetode_kanlinear_t kl, const float* __restrict__ part,
-                                       const float* __restrict__ abpart, int S, float* __restrict__ d_scaled,
-                                       float* __restrict__ d_wl, fetode_kanlinear_grad_t gr, int accumulate) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// the splits in order -> base-weight gradient, d_scaled, d_wl, logistic a / b: one wave per output
+// (lane l sums splits l, l + 64, ...; then a fixed butterfly: run-to-run identical)
+__device__ __forceinline__ float split_sum64(const float* __restrict__ p, int S, int64_t stride, int lane) {
+  float v = 0.f;
+  for (int sp = lane; sp < S; sp += 64) v += p[(int64_t)sp * stride];
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
+
+__global__ __launch_bounds__(256) void kan_psum_reduce_kernel(fetode_kanlinear_t kl, const float* __restrict__ part,
+                                                             const float* __restrict__ abpart, int S,
+                                                             float* __restrict__ d_scaled, float* __restrict__ d_wl,
+                                                             fetode_kanlinear_grad_t gr, int accumulate) {
+  const int64_t t = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
   const int in = kl.in_features, out = kl.out_features, NB = kl.num_logistic;
   const int NS = kl.grid_size + kl.spline_order, NF = 1 + NS + NB;
   const int64_t nw = (int64_t)out * in * NF;
@@ -700,18 +765,16 @@ __global__ void kan_psum_reduce_kernel(fetode_kanlinear_t kl, const float* __res
     const int f = (int)(t % NF);
     const int64_t oi = t / NF;
     const int o = (int)(oi / in), i = (int)(oi % in);
-    float v = 0.f;
-    for (int sp = 0; sp < S; ++sp) v += part[(((int64_t)sp * in + i) * NF + f) * out + o];
+    const float v = split_sum64(part + ((int64_t)i * NF + f) * out + o, S, (int64_t)in * NF * out, lane);
+    if (lane) return;
     if (f == 0) put(gr.base_weight ? gr.base_weight + (int64_t)o * in + i : nullptr, v, accumulate);
     else if (f <= NS) d_scaled[((int64_t)o * in + i) * NS + (f - 1)] = v;
     else d_wl[(int64_t)o * in * NB + i * NB + (f - 1 - NS)] = v;
   } else if (t < nw + (int64_t)in * NB) {
     const int q = (int)(t - nw);  // (i, j)
-    float va = 0.f, vb = 0.f;
-    for (int sp = 0; sp < S; ++sp) {
-      va += abpart[((int64_t)sp * in * NB + q) * 2];
-      vb += abpart[((int64_t)sp * in * NB + q) * 2 + 1];
-    }
+    const float va = split_sum64(abpart + (int64_t)q * 2, S, (int64_t)in * NB * 2, lane);
+    const float vb = split_sum64(abpart + (int64_t)q * 2 + 1, S, (int64_t)in * NB * 2, lane);
+    if (lane) return;
     put(gr.logistic_a ? gr.logistic_a + q : nullptr, va, accumulate);
     put(gr.logistic_b ? gr.logistic_b + q : nullptr, vb, accumulate);
   }
@@ -844,6 +907,94 @@ __global__ void ferro_gp_kernel(fetode_ferro_t fl, const float* __restrict__ x, 
   }
 }
 
+// The Ferro parameter sums over many rows (the fieldn training pass: every (evaluation,
+// trajectory) row): ferro_gp_kernel gives each element ONE workgroup walking all rows (in * out * K
+// workgroups — 384 for [2, 16, 2] K=12 — each a serial chain of a few thousand rows); here element
+// e's rows are split S ways (~8 K workgroups), per-split sums land in the workspace and
+// ferro_gp_reduce_kernel adds the splits in order (run-to-run identical).  The hysteresis input of
+// row r: rows < n0 read p0 (or reinit: x itself), later rows the row n0 earlier (the previous
+// evaluation of the same trajectory, fieldn's tape layout (n_ev, B, in)).
+constexpr int kFgTarget = 8192, kFgChunk = 4;  // workgroups per launch; elements per workgroup
+int fg_units(const fetode_ferro_t* fl) {
+  return fl->in_dim * fl->out_dim * ((fl->num_basis + kFgChunk - 1) / kFgChunk);
+}
+int fg_splits(const fetode_ferro_t* fl, int64_t R) {
+  int64_t S = kFgTarget / fg_units(fl);
+  const int64_t rs = (R + 1023) / 1024;  // at least ~4 rows per thread
+  if (S > rs) S = rs;
+  return S < 1 ? 1 : (int)S;
+}
+
+// workgroup (i, o, chunk of kFgChunk elements k, split): per row the shared sigmoid of the
+// hysteresis gate once, then per element the forward's exp2 / rcp forms (fieldn's plan: branch
+// sign 1, so m = 1 + w s with w = -2 (1 - alpha)(1 - u), s = sigmoid(gs(-x - Ec)));
+// d P / d (k, Ec, Ps, bias, coef) as ferro_point_vjp with that m
+__global__ __launch_bounds__(RB) void ferro_gp_split_kernel(fetode_ferro_t fl, const float* __restrict__ x,
+                                                           int64_t R, const float* __restrict__ p0, int64_t n0,
+                                                           const float* __restrict__ g, float* __restrict__ part) {
+  __shared__ float red[5 * kFgChunk * RB];
+  const int in = fl.in_dim, out = fl.out_dim, K = fl.num_basis, NC = (K + kFgChunk - 1) / kFgChunk;
+  const int io = blockIdx.x / NC, kc = blockIdx.x % NC, sp = blockIdx.y, S = gridDim.y;
+  const int i = io / out, o = io % out;
+  const int e0 = io * K + kc * kFgChunk, ne = K - kc * kFgChunk < kFgChunk ? K - kc * kFgChunk : kFgChunk;
+  const int64_t r0 = sp * R / S, r1 = (sp + 1) * R / S;
+  const float gs = (float)fl.gate_slope, gs2 = gs * FETODE_LOG2E, wc = (float)(-2.0 * (1.0 - fl.alpha));
+  float Ec[kFgChunk], kk[kFgChunk], Ps[kFgChunk], bi[kFgChunk], co[kFgChunk], GE[kFgChunk], k2[kFgChunk];
+#pragma unroll
+  for (int j = 0; j < kFgChunk; ++j) {
+    const bool on = j < ne;
+    Ec[j] = on ? fl.Ec[e0 + j] : 0.f;
+    kk[j] = on ? fl.k[e0 + j] : 0.f;
+    Ps[j] = on ? fl.Ps[e0 + j] : 0.f;
+    bi[j] = on ? fl.bias[e0 + j] : 0.f;
+    co[j] = on ? fl.coef[e0 + j] : 0.f;
+    GE[j] = gs2 * Ec[j];
+    k2[j] = 2.0f * FETODE_LOG2E * kk[j];
+  }
+  float acc[5 * kFgChunk];
+#pragma unroll
+  for (int q = 0; q < 5 * kFgChunk; ++q) acc[q] = 0.f;
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += RB) {
+    const float xv = x[r * in + i];
+    const float pv = r >= n0 ? x[(r - n0) * in + i] : (p0 ? p0[r * in + i] : xv);
+    const float go = g[r * out + o];
+    const float u = rcp(1.0f + ex2(-gs2 * (xv - pv)));
+    const float w = wc * (1.0f - u);
+#pragma unroll
+    for (int j = 0; j < kFgChunk; ++j) {
+      const float sg = rcp(1.0f + ex2(ffma(gs2, xv, GE[j])));  // sigmoid(gs(-x - Ec))
+      const float m = ffma(w, sg, 1.0f);
+      const float sh = ffma(Ec[j], m, xv);
+      const float th = ffma(rcp(1.0f + ex2(k2[j] * sh)), -2.0f, 1.0f);  // tanh(k sh)
+      const float gP = go * co[j];
+      const float gz = gP * Ps[j] * ffma(-th, th, 1.0f);
+      acc[0 * kFgChunk + j] = ffma(gz, sh, acc[0 * kFgChunk + j]);                       // k
+      const float dmdE = -(w * gs) * (sg * (1.0f - sg));                                // d m / d Ec
+      acc[1 * kFgChunk + j] = ffma(gz * kk[j], ffma(Ec[j], dmdE, m), acc[1 * kFgChunk + j]);  // Ec
+      acc[2 * kFgChunk + j] = ffma(gP, th, acc[2 * kFgChunk + j]);                       // Ps
+      acc[3 * kFgChunk + j] += gP;                                                       // bias
+      acc[4 * kFgChunk + j] = ffma(go, ffma(Ps[j], th, bi[j]), acc[4 * kFgChunk + j]);   // coef
+    }
+  }
+  block_sum(acc, red);
+  if (threadIdx.x < 5 * ne) {
+    const int c = threadIdx.x / ne, j = threadIdx.x % ne;
+    part[((int64_t)sp * in * out * K + e0 + j) * 5 + c] = acc[c * kFgChunk + j];
+  }
+}
+
+__global__ __launch_bounds__(256) void ferro_gp_reduce_kernel(fetode_ferro_t fl, const float* __restrict__ part, int S,
+                                                             fetode_ferro_grad_t gr, int accumulate) {
+  const int E = fl.in_dim * fl.out_dim * fl.num_basis;
+  const int t = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  if (t >= E * 5) return;
+  const int e = t / 5, c = t % 5;
+  const float v = split_sum64(part + (int64_t)e * 5 + c, S, (int64_t)E * 5, lane);
+  if (lane) return;
+  float* dst = c == 0 ? gr.k : c == 1 ? gr.Ec : c == 2 ? gr.Ps : c == 3 ? gr.bias : gr.coef;
+  put(dst ? dst + e : nullptr, v, accumulate);
+}
+
 bool ps_ok(const fetode_kanlinear_t* kl) {
   const int NF = 1 + kl->grid_size + kl->spline_order + kl->num_logistic;
   return kl->spline_order == 3 && NF <= kPsMaxNF && kl->out_features <= kPsMaxOut && kl->num_logistic <= kMaxLogistic;
@@ -860,7 +1011,7 @@ int64_t fetode_kanlinear_backward_workspace(const fetode_kanlinear_t* kl) {
   if (fetode_kanlinear_wide_supported(kl))   // MFMA partials + logistic a / b partials
     n += (int64_t)kGwSplit * kl->in_features * (kGwF * 16 + 2 * kGwNB);
   else if (ps_ok(kl))                        // kan_psum_kernel's per-split partials
-    n += (int64_t)ps_smax(kl->in_features) * kl->in_features *
+    n += (int64_t)ps_smax(kl) * kl->in_features *
          ((int64_t)(1 + NS + kl->num_logistic) * kl->out_features + 2 * kl->num_logistic);
   return (int64_t)sizeof(float) * n;
 }
@@ -911,13 +1062,14 @@ int fetode_kanlinear_backward(const fetode_kanlinear_t* kl, const float* x, int6
                          d_scaled, d_wl, *grads, accumulate);
       LAUNCH_CHECK();
     } else if (B >= kPsMinRows && ps_ok(kl)) {   // many rows: features once per (row, input)
-      const int S = ps_splits(in, B);
+      const int S = ps_splits(kl, B);
       float* part = d_wl + (int64_t)out * in * NB;
-      float* abpart = part + (int64_t)ps_smax(in) * in * (1 + NS + NB) * out;
-      hipLaunchKernelGGL(kan_psum_kernel<3>, dim3(in, S), dim3(256), 0, s, *kl, x, g, B, part, abpart);
+      float* abpart = part + (int64_t)ps_smax(kl) * in * (1 + NS + NB) * out;
+      auto* kfn = NB > 0 ? kan_psum_kernel<3, true> : kan_psum_kernel<3, false>;
+      hipLaunchKernelGGL(kfn, dim3(ps_groups(kl), S), dim3(256), ps_lds_bytes(kl), s, *kl, x, g, B, part, abpart);
       LAUNCH_CHECK();
       const int64_t nt = (int64_t)out * in * (1 + NS + NB) + (int64_t)in * NB;
-      hipLaunchKernelGGL(kan_psum_reduce_kernel, dim3(nblk(nt, 256)), dim3(256), 0, s, *kl, part, abpart, S, d_scaled,
+      hipLaunchKernelGGL(kan_psum_reduce_kernel, dim3(nblk(nt, 4)), dim3(256), 0, s, *kl, part, abpart, S, d_scaled,
                          d_wl, *grads, accumulate);
       LAUNCH_CHECK();
     } else {
@@ -965,3 +1117,24 @@ int fetode_ferro_backward(const fetode_ferro_t* fl, const float* x, int64_t B, c
 }
 
 }  // extern "C"
+
+int64_t fetode::ferro_param_rows_workspace() { return (int64_t)sizeof(float) * kFgTarget * kFgChunk * 5; }
+
+int fetode::ferro_param_rows(const fetode_ferro_t* fl, const float* x, int64_t R, const float* p0, int64_t n0,
+                             const float* g, const fetode_ferro_grad_t* grads, void* workspace, int32_t accumulate,
+                             void* stream) {
+  if (!fl || fl->in_dim <= 0 || fl->out_dim <= 0 || fl->num_basis <= 0) return set_err(FETODE_EINVAL, "ferro: bad dims");
+  if (fl->branch_sign) return set_err(FETODE_EUNSUPPORTED, "ferro row sums: branch_sign");
+  if (R <= 0 || !grads) return FETODE_OK;
+  if (!x || !g || !workspace) return set_err(FETODE_EINVAL, "null pointer");
+  hipStream_t s = (hipStream_t)stream;
+  const int E = fl->in_dim * fl->out_dim * fl->num_basis;
+  const int S = fg_splits(fl, R);
+  float* part = (float*)workspace;
+  hipLaunchKernelGGL(ferro_gp_split_kernel, dim3(fg_units(fl), S), dim3(RB), 0, s, *fl, x, R, p0, n0, g, part);
+  LAUNCH_CHECK();
+  hipLaunchKernelGGL(ferro_gp_reduce_kernel, dim3(nblk((int64_t)E * 5, 4)), dim3(256), 0, s, *fl, part, S, *grads,
+                     accumulate);
+  LAUNCH_CHECK();
+  return FETODE_OK;
+}

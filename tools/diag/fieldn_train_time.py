@@ -1,7 +1,8 @@
 """Training iteration (odeint forward + loss.backward()) of a depth-2 field of another width —
 KANFET([2, 16, 2], K = 12) and KAN([4, 32, 4]) — at B = 4096 over the bench horizon (34 rk4 steps):
 the fused pair (fieldn forward with tape + fieldn_adj_kernel + per-module parameter VJPs) vs the
-per-stage path (F.set_fused_training(False)); HIP events, env B, N."""
+per-stage path (F.set_fused_training(False)); HIP events, env B, N.  SECT=1|2|3 runs one section;
+FUSED_ONLY=1 skips the per-stage / host-loop legs (for a rocprof kernel split)."""
 import os
 import sys
 
@@ -14,6 +15,8 @@ import fet_ode_amd as F  # noqa: E402
 dev = torch.device("cuda:0")
 B, N = int(os.environ.get("B", "4096")), int(os.environ.get("N", "5"))
 t = torch.tensor(np.linspace(0, 3.5, 35))
+SECT = os.environ.get("SECT", "123")
+FUSED_ONLY = os.environ.get("FUSED_ONLY", "0") == "1"
 
 
 def ev_ms(fn, n):
@@ -30,6 +33,8 @@ def ev_ms(fn, n):
 
 for name, mk in (("KANFET[2,16,2] K=12", lambda: F.KANFET([2, 16, 2], grid_size=5, num_fet_basis=12)),
                  ("KAN[4,32,4]", lambda: F.KAN([4, 32, 4], grid_size=5))):
+    if "1" not in SECT:
+        break
     torch.manual_seed(0)
     m = mk().to(dev)
     D = m.layers[0].kan.in_features if hasattr(m.layers[0], "kan") else m.layers[0].in_features
@@ -41,7 +46,7 @@ for name, mk in (("KANFET[2,16,2] K=12", lambda: F.KANFET([2, 16, 2], grid_size=
         F.odeint(func, y0, t, method="rk4").square().mean().backward()
 
     out = []
-    for fused in (True, False):
+    for fused in ((True,) if FUSED_ONLY else (True, False)):
         prev = F.set_fused_training(fused)
         try:
             out.append(ev_ms(it, N if fused else 1))
@@ -49,6 +54,9 @@ for name, mk in (("KANFET[2,16,2] K=12", lambda: F.KANFET([2, 16, 2], grid_size=
             F.set_fused_training(prev)
     with torch.no_grad():
         fwd = ev_ms(lambda: F.odeint(func, y0, t, method="rk4"), N)
+    if FUSED_ONLY:
+        print(f"{name} B={B}: inference solve {fwd:.2f} ms | training iteration fused {out[0]:.2f} ms", flush=True)
+        continue
     print(f"{name} B={B}: inference solve {fwd:.2f} ms | training iteration fused {out[0]:.2f} ms, "
           f"per-stage {out[1]:.1f} ms ({out[1] / out[0]:.1f}x)", flush=True)
 
@@ -58,6 +66,8 @@ B2 = int(os.environ.get("B2", "2048"))
 t2 = torch.tensor([0.0, 0.5, 1.0], dtype=torch.float64)
 for name, mk in (("KANFET[2,16,2] K=12", lambda: F.KANFET([2, 16, 2], grid_size=5, num_fet_basis=12)),
                  ("KAN[4,32,4]", lambda: F.KAN([4, 32, 4], grid_size=5))):
+    if "2" not in SECT:
+        break
     torch.manual_seed(0)
     m = mk().to(dev)
     D = m.layers[0].kan.in_features if hasattr(m.layers[0], "kan") else m.layers[0].in_features
@@ -80,6 +90,8 @@ B3 = int(os.environ.get("B3", "1024"))
 t3 = torch.tensor([0.0, 0.5, 1.0], dtype=torch.float64)
 for name, mk in (("KANFET[3,8,3] K=6", lambda: F.KANFET([3, 8, 3], grid_size=5, num_fet_basis=6)),
                  ("KAN[4,32,4]", lambda: F.KAN([4, 32, 4], grid_size=5))):
+    if "3" not in SECT:
+        break
     torch.manual_seed(0)
     m = mk().to(dev)
     D = m.layers[0].kan.in_features if hasattr(m.layers[0], "kan") else m.layers[0].in_features
