@@ -48,7 +48,7 @@ __device__ __forceinline__ float fb_wave_sum(float v) {
 // sum_{o in [o0, o0 + no)} go[o - o0] * d edge(o, i) / d x at x: the layer's edge (o, i) as the
 // forward evaluates it (fieldn fn_edge) — SiLU base, logistic branch, spline cubic per knot
 // interval, Ferro elements (o, i, k) with hysteresis input pv — differentiated in x
-template <bool FERRO>
+template <bool FERRO, int UNR = 1>
 __device__ float fb_vjp_input(const float* __restrict__ plan, const LayerPlan& P, int i, float x, float pv,
                               const float* go, int o0, int no) {
   const float sx = fb_sig(-x * FETODE_LOG2E);
@@ -71,6 +71,8 @@ __device__ float fb_vjp_input(const float* __restrict__ plan, const LayerPlan& P
   }
   // logistic branch: d/dx 1/(1 + 2^(a' x + b')) = -ln2 a' s (1 - s)
   const float* lg = plan + P.lg + 2 * (int64_t)i * P.NB;
+  // UNR: as fn_edge — overlap the independent exp2 / rcp chains of consecutive basis functions
+#pragma unroll UNR
   for (int j = 0; j < P.NB; ++j) {
     const float s = fb_sig(ffma(lg[2 * j], x, lg[2 * j + 1]));
     const float dj = (-kLn2 * lg[2 * j]) * (s * (1.0f - s));
@@ -93,6 +95,7 @@ __device__ float fb_vjp_input(const float* __restrict__ plan, const LayerPlan& P
       const float* kE = plan + P.fe_k2Ec + e0;
       const float* cp = plan + P.fe_CPs2 + e0;
       float d = 0.f;
+#pragma unroll UNR
       for (int k = 0; k < P.K; ++k) {
         const float s = rcp(ex2(ffma(P.gsl2e, x, GEc[k])) + 1.0f);
         const float mm = ffma(w, s, 1.0f);
@@ -164,12 +167,16 @@ __device__ void fb_coefs(int method, float dt, float hh, float h6, float bc[4], 
 // LDSP: the plan of both layers staged in LDS once per workgroup (as fieldn_kernel<.., LDSP>)
 constexpr int kFbWavesL = 8;
 constexpr int kFbMaxT = 8;  // trajectories per wave at most
-// lanes per trajectory: the smallest power of two >= max(H, D, 64 / kFbMaxT) (fieldn_kernel's rule)
-__host__ __device__ inline int fb_lanes_per_traj(int D, int H) {
+// unit lanes U = the smallest power of two >= max(H, D, 64 / kFbMaxT) and split factor SF as
+// fieldn_kernel (fn_unit_lanes / fn_split): split group sg takes half the layer-1 outputs (a
+// contiguous half) and the layer-0 inputs i = sg (mod 2)
+__host__ __device__ inline int fb_unit_lanes(int D, int H) {
   int hp = 64 / kFbMaxT;
   while (hp < H || hp < D) hp <<= 1;
   return hp < 64 ? hp : 64;
 }
+__host__ __device__ inline int fb_split(int D, int H) { return (fb_unit_lanes(D, H) <= 32 && D >= 2) ? 2 : 1; }
+__host__ __device__ inline int fb_lanes_per_traj(int D, int H) { return fb_unit_lanes(D, H) * fb_split(D, H); }
 constexpr int64_t kFbLdsMax = 78 * 1024;
 template <bool FERRO, bool LDSP = false>
 __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_adj_kernel(FbArgs a) {
@@ -186,8 +193,10 @@ __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_
   const LayerPlan& P0 = a.P0;
   const LayerPlan& P1 = a.P1;
   const int D = P0.in, H = P0.out;
-  const int HP = fb_lanes_per_traj(D, H), TPW = 64 / HP;
-  const int t = lane / HP, o = lane & (HP - 1);
+  const int U = fb_unit_lanes(D, H), SF = fb_split(D, H), HP = U * SF, TPW = 64 / HP;
+  const int t = lane / HP, sg = (lane & (HP - 1)) / U, o = lane & (U - 1);
+  const bool own = sg == 0;  // the group that owns the trajectory's adjoint state and writes
+  const int dlo = SF == 2 ? (sg ? (D + 1) / 2 : 0) : 0, dn = SF == 2 ? (sg ? D / 2 : (D + 1) / 2) : D;
   const int64_t bw = ((int64_t)blockIdx.x * NW + wid) * TPW;
   if (bw >= a.B) return;  // whole waves only; no workgroup barriers below
   const int64_t b = bw + t;
@@ -205,7 +214,7 @@ __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_
   float* gk = s_gk[wid][t];
   float(&ak)[4][kFbMaxD] = s_ak[wid][t];
   float(&acs)[4][3] = s_ac[wid];
-  const bool dl = o < D, hl = o < H;
+  const bool dl = own && o < D, hl = o < H;
   float ay1 = 0.f, ay = 0.f;  // adjoint of y at the end of the current step (lanes < D)
   int jj = a.T - 1;
   for (int s = a.n_steps - 1; s >= 0; --s) {
@@ -252,17 +261,23 @@ __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_
       }
       fb_wsync();
       // layer 1 (h -> k): d loss / d h_o on lane o
-      const float gh = hl ? fb_vjp_input<FERRO>(plan, P1, o, h, ph, gk, 0, D) : 0.f;
+      // (split: each group its half of the outputs, then the two halves' sum on both)
+      float gh = hl ? fb_vjp_input<FERRO, 4>(plan, P1, o, h, ph, gk + dlo, dlo, dn) : 0.f;
+      if (SF == 2) gh += __shfl_xor(gh, U);
       if (live && dl) GK[(ev * a.B + b) * D + o] = gk[o];
-      if (live && hl) GH[(ev * a.B + b) * H + o] = gh;
+      if (live && own && hl) GH[(ev * a.B + b) * H + o] = gh;
       // layer 0 (x -> h): d loss / d x_i = sum over the lanes o of gh_o d edge(o, i) / d x_i
       float gx = 0.f;
-      for (int i = 0; i < D; ++i) {
+      for (int i = sg; i < D; i += SF) {  // group sg: the inputs i = sg (mod SF)
         const float one = 1.0f;
-        const float c = hl ? gh * fb_vjp_input<FERRO>(plan, P0, i, xs[i], ps[i], &one, o, 1) : 0.f;
+        const float c = hl ? gh * fb_vjp_input<FERRO, 4>(plan, P0, i, xs[i], ps[i], &one, o, 1) : 0.f;
         float sum = c;
-        for (int m = HP >> 1; m >= 1; m >>= 1) sum += __shfl_xor(sum, m);  // within the slot's lanes
+        for (int m = U >> 1; m >= 1; m >>= 1) sum += __shfl_xor(sum, m);  // within the group's lanes
         if (o == i) gx = sum;
+        if (SF == 2) {  // the odd input's sum to its owner lane in group 0
+          const float oth = __shfl_xor(sum, U);
+          if (o == i + 1) gx = oth;
+        }
       }
       if (dl) {
         ay += gx;

@@ -1538,12 +1538,16 @@ __device__ __forceinline__ void fn_wsync() { asm volatile("s_waitcnt lgkmcnt(0)"
 __device__ __forceinline__ float fn_sig_l2(float zl) { return rcp(1.0f + ex2(zl)); }  // 1/(1+2^zl)
 
 // KAN edge (o, i) + the Ferro elements (o, i, k) of one layer at input x (gate weight w)
-template <bool FERRO>
+template <bool FERRO, int UNR = 1>
 __device__ __forceinline__ float fn_edge(const float* __restrict__ plan, const LayerPlan& P, int o, int i, float x,
                                          float sx, float w, int mfix, float u) {
   const float* kw = plan + P.kw + ((int64_t)o * P.in + i) * P.NFL;
   float v = kw[0] * sx;
   const float* lg = plan + P.lg + 2 * (int64_t)i * P.NB;
+  // UNR: the packed fixed-grid launch runs ~one wave per SIMD, so the independent exp2 / rcp chains
+  // of consecutive basis functions must overlap within the lane (the sums stay in order); the
+  // resident dopri5 keeps its register budget (occupancy = the batch one grid holds)
+#pragma unroll UNR
   for (int j = 0; j < P.NB; ++j) v = ffma(kw[1 + j], fn_sig_l2(ffma(lg[2 * j], x, lg[2 * j + 1])), v);
   const float4 cf = *reinterpret_cast<const float4*>(plan + P.sp + (((int64_t)o * P.in + i) * (P.NI + 1) + mfix) * 4);
   v += ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
@@ -1553,6 +1557,7 @@ __device__ __forceinline__ float fn_edge(const float* __restrict__ plan, const L
     const float* k2 = plan + P.fe_k2 + e0;
     const float* kE = plan + P.fe_k2Ec + e0;
     const float* cp = plan + P.fe_CPs2 + e0;
+#pragma unroll UNR
     for (int k = 0; k < P.K; ++k) {
       const float s = rcp(ex2(ffma(P.gsl2e, x, GEc[k])) + 1.0f);  // sigma(gs(-x - Ec)), one rounding as v4
       const float m = ffma(w, s, 1.0f);                    // branch momentum (branch_sign = 1)
@@ -1586,12 +1591,21 @@ __device__ __forceinline__ void fn_interval(const float* __restrict__ plan, cons
 // workgroups per CU still fit the 160 KB)
 constexpr int kFnWavesL = 8;
 constexpr int kFnMaxT = 8;  // trajectories per wave at most (H, D <= 8)
-// lanes per trajectory: the smallest power of two >= max(H, D, 64 / kFnMaxT) (host and device agree)
-__host__ __device__ inline int fn_lanes_per_traj(int D, int H) {
+// unit lanes of a trajectory: the smallest power of two U >= max(H, D, 64 / kFnMaxT); split factor
+// SF = 2 when a wave still holds two or more such groups and D >= 2: group sg of the trajectory's
+// U * SF lanes takes the layer-0 inputs i = sg (mod 2) and the layer-1 outputs d = sg (mod 2), so
+// each lane runs half the edges and the launch has twice the waves (the fixed-grid launch is
+// latency-bound at ~one wave per SIMD otherwise).  Host and device agree on both.
+__host__ __device__ inline int fn_unit_lanes(int D, int H) {
   int hp = 64 / kFnMaxT;
   while (hp < H || hp < D) hp <<= 1;
   return hp < 64 ? hp : 64;
 }
+__host__ __device__ inline int fn_split(int D, int H) {
+  static_assert(kFnMaxT >= 2, "");
+  return (fn_unit_lanes(D, H) <= 32 && D >= 2) ? 2 : 1;
+}
+__host__ __device__ inline int fn_lanes_per_traj(int D, int H) { return fn_unit_lanes(D, H) * fn_split(D, H); }
 constexpr int64_t kFnLdsMax = 78 * 1024;
 template <bool FERRO, bool DOPRI = false, bool TAPE = false, bool LDSP = false>
 __global__ __launch_bounds__(DOPRI ? 64 : (LDSP ? 64 * kFnWavesL : 64 * kFnWaves)) void fieldn_kernel(FusedArgs a) {
@@ -1608,16 +1622,18 @@ __global__ __launch_bounds__(DOPRI ? 64 : (LDSP ? 64 * kFnWavesL : 64 * kFnWaves
       return;
     }
   }
-  // trajectories per wave: lane = (slot t, unit o) with HP = pow2 >= max(H, D) lanes per slot
-  // (KANFET([2, 16, 2]): four trajectories per wave); the resident dopri5 keeps one per wave
+  // trajectories per wave: lane = (slot t, split group sg, unit o) with U = pow2 >= max(H, D) unit
+  // lanes and SF split groups per slot (KANFET([2, 16, 2]): two trajectories per wave, 2 x 16
+  // lanes each); the resident dopri5 keeps one trajectory per wave, unsplit
   constexpr int MT = DOPRI ? 1 : kFnMaxT;
   __shared__ float s_x[NW][MT][kFnMaxD], s_k[NW][MT][kFnMaxD], s_p0[NW][MT][kFnMaxD];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const LayerPlan& P0 = a.P0;
   const LayerPlan& P1 = a.P1;
   const int D = P0.in, H = P0.out;
-  const int HP = DOPRI ? 64 : fn_lanes_per_traj(D, H), TPW = 64 / HP;
-  const int t = lane / HP, o = lane & (HP - 1);
+  const int U = DOPRI ? 64 : fn_unit_lanes(D, H), SF = DOPRI ? 1 : fn_split(D, H), HP = U * SF, TPW = 64 / HP;
+  const int t = lane / HP, sg = (lane & (HP - 1)) / U, o = lane & (U - 1);
+  const bool own = sg == 0;  // the group that owns the trajectory's state and writes
   const int64_t b = ((int64_t)blockIdx.x * NW + wid) * TPW + t;
   const bool valid = b < a.B;
   const float* __restrict__ plan = LDSP ? s_plan : a.plan;
@@ -1627,7 +1643,7 @@ __global__ __launch_bounds__(DOPRI ? 64 : (LDSP ? 64 * kFnWavesL : 64 * kFnWaves
   const bool hl = o < H;  // this lane's hidden unit
   float prev1 = 0.f;
   if (FERRO && valid) {
-    if (o < D) p0[o] = a.state[b * D + o];
+    if (own && o < D) p0[o] = a.state[b * D + o];
     if (hl) prev1 = a.state[a.B * D + b * H + o];
   }
   bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
@@ -1644,14 +1660,15 @@ __global__ __launch_bounds__(DOPRI ? 64 : (LDSP ? 64 * kFnWavesL : 64 * kFnWaves
     fn_wsync();
     if constexpr (TAPE) {
       trow = (ev < a.dp.tape_cap && valid) ? a.tape + (ev * a.B + b) * (2 * D + H) : nullptr;
-      if (trow && o < D) trow[o] = xs[o];
+      if (trow && own && o < D) trow[o] = xs[o];
     }
-    if (tx && valid && o < D) tx[(ev * a.B + b) * D + o] = xs[o];
-    // layer 0: h_o
+    if (tx && valid && own && o < D) tx[(ev * a.B + b) * D + o] = xs[o];
+    // layer 0: h_o = c0 + (sum over the even inputs + sum over the odd inputs), each in input order
+    // (one order for every split: the split groups hold one parity each and swap their sums)
     float h = 0.f;
     if (hl) {
-      h = c0o;
-      for (int i = 0; i < D; ++i) {
+      float pe = 0.f, po = 0.f;
+      for (int i = sg; i < D; i += SF) {
         const float x = xs[i];
         const float sx = x * fn_sig_l2(-x * FETODE_LOG2E);
         float w = 0.f;
@@ -1659,14 +1676,22 @@ __global__ __launch_bounds__(DOPRI ? 64 : (LDSP ? 64 * kFnWavesL : 64 * kFnWaves
         int mfix;
         float u;
         fn_interval(plan, P0, i, x, mfix, u);
-        h += fn_edge<FERRO>(plan, P0, o, i, x, sx, w, mfix, u);
+        const float e = fn_edge<FERRO, DOPRI ? 1 : 4>(plan, P0, o, i, x, sx, w, mfix, u);
+        if (i & 1) po += e;
+        else pe += e;
       }
+      if (SF == 2) {
+        const float other = __shfl_xor(sg ? po : pe, U);  // each group sends its own parity's sum
+        if (sg) pe = other;
+        else po = other;
+      }
+      h = c0o + (pe + po);
     }
-    if (tx && valid && hl) th_[(ev * a.B + b) * H + o] = h;
+    if (tx && valid && own && hl) th_[(ev * a.B + b) * H + o] = h;
     if (TAPE && trow && hl) trow[D + o] = h;
     ++ev;
     fn_wsync();
-    if (FERRO && o < D) p0[o] = xs[o];  // ferro_class.py:409
+    if (FERRO && own && o < D) p0[o] = xs[o];  // ferro_class.py:409
     re0 = false;
     // layer 1: lane o's contributions to every output, then the sum over the lanes
     float w1 = 0.f, sh = 0.f, u1 = 0.f;
@@ -1678,15 +1703,15 @@ __global__ __launch_bounds__(DOPRI ? 64 : (LDSP ? 64 * kFnWavesL : 64 * kFnWaves
     }
     if (FERRO) prev1 = h;
     re1 = false;
-    for (int d = 0; d < D; ++d) {
-      float v = hl ? fn_edge<FERRO>(plan, P1, d, o, h, sh, w1, m1, u1) : 0.f;
-      for (int s = HP >> 1; s >= 1; s >>= 1) v += __shfl_xor(v, s);  // within the slot's HP lanes
+    for (int d = sg; d < D; d += SF) {  // group sg: the outputs d = sg (mod SF)
+      float v = hl ? fn_edge<FERRO, DOPRI ? 1 : 4>(plan, P1, d, o, h, sh, w1, m1, u1) : 0.f;
+      for (int s = U >> 1; s >= 1; s >>= 1) v += __shfl_xor(v, s);  // within the group's U lanes
       if (o == 0) ks[d] = v + plan[P1.fconst + d];
     }
     fn_wsync();
   };
   // lane d < D carries state dim d
-  const bool dl = o < D;
+  const bool dl = own && o < D;
   float y = (valid && dl) ? a.y0[b * D + o] : 0.f;
   if constexpr (DOPRI) {
     // ---- device-resident dopri5: fused4's driver (dopri5.py _Dopri5's control arithmetic) with
@@ -1875,7 +1900,7 @@ __global__ __launch_bounds__(DOPRI ? 64 : (LDSP ? 64 * kFnWavesL : 64 * kFnWaves
   }
   if (FERRO && valid) {
     if (dl) a.state[b * D + o] = p0[o];
-    if (hl) a.state[a.B * D + b * H + o] = prev1;
+    if (own && hl) a.state[a.B * D + b * H + o] = prev1;
   }
 }
 
