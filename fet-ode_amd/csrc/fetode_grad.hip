@@ -40,6 +40,10 @@ __device__ __forceinline__ void block_sum(float (&v)[N], float* red /* RB*N */) 
   for (int q = 0; q < N; ++q) v[q] = red[q * RB];
 }
 
+// a workgroup barrier over LDS only: __syncthreads() is also a workgroup-scope fence, which waits
+// for every outstanding global load (vmcnt(0)) — including a prefetch meant to cross the barrier
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ void put(float* dst, float v, int accumulate) {
   if (dst) *dst = accumulate ? *dst + v : v;
 }
@@ -586,7 +590,9 @@ int ps_splits(const fetode_kanlinear_t* kl, int64_t B) {
 }
 size_t ps_lds_bytes(const fetode_kanlinear_t* kl) {
   const int NF = ps_nf(kl), out = kl->out_features, ig = ps_ig(kl->in_features, NF, out);
-  const int64_t n = (int64_t)ig * kPsTile * (NF | 1) + (int64_t)kPsTile * (out | 1) + (int64_t)ig * out * kl->num_logistic;
+  const int NG = kl->grid_size + 2 * kl->spline_order + 1;
+  const int64_t n = (int64_t)ig * kPsTile * (NF | 1) + (int64_t)kPsTile * (out | 1) + (int64_t)ig * out * kl->num_logistic +
+                    (int64_t)ig * (NG + kl->spline_order * (NG - 1) + 3 * kl->num_logistic);
   return sizeof(float) * (size_t)(n > 256 * 16 ? n : 256 * 16);
 }
 
@@ -605,6 +611,9 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
   float* ft = ps_lds;                          // [IG * kPsTile][FS]: (input, row) features
   float* gt = ft + IG * kPsTile * FS;          // [kPsTile][GS]
   float* wl = gt + kPsTile * GS;               // [IG][out][NB]
+  float* kn = wl + IG * out * NB;              // [IG][NG] knots
+  float* rk = kn + IG * NG;                    // [IG][SO][NG - 1] reciprocal knot spans
+  float* lab = rk + IG * SO * (NG - 1);        // [IG][NB][3] logistic (-a log2e, b, a)
   float* red = ps_lds;                         // the workgroup sums, after the walk
   const int64_t tiles = (B + kPsTile - 1) / kPsTile;
   const int64_t t0 = s * tiles / S, t1 = (s + 1) * tiles / S;
@@ -614,11 +623,25 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
     const float ls = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
     wl[q] = (kl.logistic_weight[(int64_t)o * in * NB + (i0 + ig) * NB + j] * kl.scale_logistic) * ls;
   }
+  // the group's knots, reciprocal spans (bspline_vals_derivs_rk's layout) and logistic parameters
+  for (int q = tid; q < ni * NG; q += 256) kn[q] = kl.grid[(int64_t)(i0 + q / NG) * NG + q % NG];
+  for (int q = tid; q < ni * SO * (NG - 1); q += 256) {
+    const int ig = q / (SO * (NG - 1)), kj = q % (SO * (NG - 1)), k = kj / (NG - 1) + 1, j = kj % (NG - 1);
+    const float* gg = kl.grid + (int64_t)(i0 + ig) * NG;
+    rk[q] = j + k < NG ? 1.0f / (gg[j + k] - gg[j]) : 0.f;
+  }
+  for (int q = tid; LOG && q < ni * NB; q += 256) {
+    lab[3 * q] = -kl.logistic_a[i0 * NB + q] * FETODE_LOG2E;
+    lab[3 * q + 1] = kl.logistic_b[i0 * NB + q];
+    lab[3 * q + 2] = kl.logistic_a[i0 * NB + q];
+  }
   // feature role: (input fig, row frr) of each tile
   const int fig = tid / kPsTile, frr = tid % kPsTile;
   const bool fe = fig < ni;
   const int fin = i0 + (fe ? fig : 0);
-  const float* gi = kl.grid + (int64_t)fin * NG;
+  const float* gi = kn + (fe ? fig : 0) * NG;
+  const float* rki = rk + (fe ? fig : 0) * SO * (NG - 1);
+  const float* labi = lab + (fe ? fig : 0) * 3 * NB;
   // sum role: a (input, feature block, output block) triple and a share of the tile's rows
   const int FBK = (NF + 3) / 4, OBK = (out + 3) / 4, P = ni * FBK * OBK, Q = P < 256 ? 256 / P : 1;
   const int p = tid % P, q = tid / P;
@@ -650,16 +673,17 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
     const int64_t r0 = tl * kPsTile;
     const bool live = fe && r0 + frr < B;
     const float xv = xn;
-    __syncthreads();  // the previous tile's reads are done
+    lds_barrier();  // the previous tile's reads are done (the next tile's loads stay in flight)
 #pragma unroll
     for (int k = 0; k < kPsGReg; ++k)
       if (gc < out) gt[(gr0 + 4 * k) * GS + gc] = gn[k];
     if (tl + 1 < t1) fetch(tl + 1);
     if (fe) {  // row r0 + frr, input fin: the features as kan_gw_kernel forms them
       float* fr = ft + (fig * kPsTile + frr) * FS;
-      fr[0] = live ? xv * sigm(xv) : 0.f;
+      // the forward's exp2 / rcp forms (fn_edge): SiLU, logistic 2 / (1 + 2^(-a log2e (x - b)))
+      fr[0] = live ? xv * rcp(1.0f + ex2(-xv * FETODE_LOG2E)) : 0.f;
       float val[SO + 1], der[SO + 1];
-      const int m = bspline_vals_derivs<SO>(xv, NG, gi, val, der);
+      const int m = bspline_vals_derivs_rk<SO>(xv, NG, gi, rki, val, der);  // der unused: folded away
       for (int c = 0; c < NS; ++c) {
         float v = (live && m == -2) ? __builtin_nanf("") : 0.f;
 #pragma unroll
@@ -668,9 +692,9 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
         fr[1 + c] = v;
       }
       for (int j = 0; j < NB; ++j)
-        fr[1 + NS + j] = live ? 2.0f / (1.0f + expf(-kl.logistic_a[fin * NB + j] * (xv - kl.logistic_b[fin * NB + j]))) : 0.f;
+        fr[1 + NS + j] = live ? 2.0f * rcp(1.0f + ex2(labi[3 * j] * (xv - labi[3 * j + 1]))) : 0.f;
     }
-    __syncthreads();
+    lds_barrier();
     if (LOG && live) {  // logistic a / b: d phi_j through the row's g
       const float* fr = ft + (fig * kPsTile + frr) * FS;
       float gph[NL];
@@ -687,7 +711,7 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
       for (int j = 0; j < NL; ++j) {
         if (j >= NB) break;
         const float gphi = gph[j];
-        const float a = kl.logistic_a[fin * NB + j], bb = kl.logistic_b[fin * NB + j];
+        const float a = labi[3 * j + 2], bb = labi[3 * j + 1];
         const float sg = 0.5f * fr[1 + NS + j];  // sigm(a (x - b))
         const float dz = gphi * 2.0f * sg * (1.0f - sg);
         la[j] += dz * (xv - bb);
