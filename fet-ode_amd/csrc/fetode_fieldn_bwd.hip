@@ -25,6 +25,7 @@
 #include <cstdlib>
 
 #include "fetode_common.h"
+#include "fetode_fieldn_plan.h"
 
 using namespace fetode;
 
@@ -47,37 +48,42 @@ __device__ __forceinline__ float fb_wave_sum(float v) {
 
 // sum_{o in [o0, o0 + no)} go[o - o0] * d edge(o, i) / d x at x: the layer's edge (o, i) as the
 // forward evaluates it (fieldn fn_edge) — SiLU base, logistic branch, spline cubic per knot
-// interval, Ferro elements (o, i, k) with hysteresis input pv — differentiated in x
-template <bool FERRO, int UNR = 1>
+// interval, Ferro elements (o, i, k) with hysteresis input pv — differentiated in x.  IMG: the
+// plan's lane-contiguous LDS image (fetode_fieldn_plan.h), layer L (lanes: layer 0's outputs,
+// layer 1's inputs)
+template <bool FERRO, int UNR = 1, bool IMG = false, int L = 0>
 __device__ float fb_vjp_input(const float* __restrict__ plan, const LayerPlan& P, int i, float x, float pv,
                               const float* go, int o0, int no) {
+  using X = FnIdx<IMG, L>;
+  const int st = X::stride(P);
   const float sx = fb_sig(-x * FETODE_LOG2E);
   const float dsx = sx * ffma(x, 1.0f - sx, 1.0f);  // SiLU'
   // knot interval as fn_interval; off the grid: the plan's zero row, u = 0 (NaN for non-finite x)
-  const float* g = plan + P.knots + (int64_t)i * P.NG;
+  const float* g = plan + X::knot(P, i, 0);
+  const int gst = X::knot_stride(P);
   int m = -1;
-  for (int j = 0; j < P.NG; ++j) m += x >= g[j] ? 1 : 0;
+  for (int j = 0; j < P.NG; ++j) m += x >= g[j * gst] ? 1 : 0;
   const bool fin = __builtin_isfinite(x);
   const int mfix = ((unsigned)m < (unsigned)P.NI && fin) ? m : P.NI;
-  const float rhm = mfix < P.NI ? plan[P.rh + (int64_t)i * P.NI + mfix] : 0.f;
-  const float u = mfix < P.NI ? (x - g[mfix]) * rhm : (fin ? 0.0f : __builtin_nanf(""));
+  const float rhm = mfix < P.NI ? plan[X::rh(P, i, mfix)] : 0.f;
+  const float u = mfix < P.NI ? (x - g[mfix * gst]) * rhm : (fin ? 0.0f : __builtin_nanf(""));
   float acc = 0.f;
   for (int oo = 0; oo < no; ++oo) {
     const int o = o0 + oo;
-    const float* kw = plan + P.kw + ((int64_t)o * P.in + i) * P.NFL;
-    const float4 cf = *reinterpret_cast<const float4*>(plan + P.sp + (((int64_t)o * P.in + i) * (P.NI + 1) + mfix) * 4);
+    const float* kw = plan + X::row(P, P.kw, o, i, P.NFL);
+    const float4 cf = *reinterpret_cast<const float4*>(plan + X::sp(P, o, i, mfix));
     const float dsp = ffma(u, ffma(3.0f * u, cf.w, 2.0f * cf.z), cf.y) * rhm;
     acc = ffma(go[oo], ffma(kw[0], dsx, dsp), acc);
   }
   // logistic branch: d/dx 1/(1 + 2^(a' x + b')) = -ln2 a' s (1 - s)
-  const float* lg = plan + P.lg + 2 * (int64_t)i * P.NB;
   // UNR: as fn_edge — overlap the independent exp2 / rcp chains of consecutive basis functions
 #pragma unroll UNR
   for (int j = 0; j < P.NB; ++j) {
-    const float s = fb_sig(ffma(lg[2 * j], x, lg[2 * j + 1]));
-    const float dj = (-kLn2 * lg[2 * j]) * (s * (1.0f - s));
+    const float la = plan[X::lg(P, i, j, 0)];
+    const float s = fb_sig(ffma(la, x, plan[X::lg(P, i, j, 1)]));
+    const float dj = (-kLn2 * la) * (s * (1.0f - s));
     float wsum = 0.f;
-    for (int oo = 0; oo < no; ++oo) wsum = ffma(go[oo], plan[P.kw + ((int64_t)(o0 + oo) * P.in + i) * P.NFL + 1 + j], wsum);
+    for (int oo = 0; oo < no; ++oo) wsum = ffma(go[oo], plan[X::row(P, P.kw, o0 + oo, i, P.NFL) + (1 + j) * st], wsum);
     acc = ffma(dj, wsum, acc);
   }
   if constexpr (FERRO) {
@@ -89,7 +95,7 @@ __device__ float fb_vjp_input(const float* __restrict__ plan, const LayerPlan& P
     const float gw = (-kLn2 * P.gsl2e) * w;
     const float upp1 = 1.0f + up;
     for (int oo = 0; oo < no; ++oo) {
-      const int64_t e0 = (int64_t)(o0 + oo) * P.in * P.K + (int64_t)i * P.K;
+      const int64_t e0 = X::row(P, 0, o0 + oo, i, P.K);
       const float* GEc = plan + P.fe_GEc + e0;
       const float* k2 = plan + P.fe_k2 + e0;
       const float* kE = plan + P.fe_k2Ec + e0;
@@ -97,12 +103,12 @@ __device__ float fb_vjp_input(const float* __restrict__ plan, const LayerPlan& P
       float d = 0.f;
 #pragma unroll UNR
       for (int k = 0; k < P.K; ++k) {
-        const float s = rcp(ex2(ffma(P.gsl2e, x, GEc[k])) + 1.0f);
+        const float s = rcp(ex2(ffma(P.gsl2e, x, GEc[k * st])) + 1.0f);
         const float mm = ffma(w, s, 1.0f);
-        const float z = ffma(kE[k], mm, k2[k] * x);
+        const float z = ffma(kE[k * st], mm, k2[k * st] * x);
         const float th = ffma(rcp(ex2(z) + 1.0f), -2.0f, 1.0f);
         const float dm = gw * s * (upp1 - s);
-        d = ffma(cp[k] * ffma(-th, th, 1.0f), ffma(kE[k], dm, k2[k]), d);
+        d = ffma(cp[k * st] * ffma(-th, th, 1.0f), ffma(kE[k * st], dm, k2[k * st]), d);
       }
       acc = ffma(go[oo] * (0.5f * kLn2), d, acc);
     }
@@ -186,7 +192,7 @@ __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_
   __shared__ float s_ak[NW][kFbMaxT][4][kFbMaxD], s_ac[NW][4][3];
   extern __shared__ float s_plan[];
   if constexpr (LDSP) {
-    for (int64_t q = threadIdx.x; q < a.P1.end; q += blockDim.x) s_plan[q] = a.plan[q];
+    fn_stage_image(s_plan, a.plan, a.P0, a.P1);  // the lane-contiguous image (fetode_fieldn_plan.h)
     __syncthreads();
   }
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -262,7 +268,7 @@ __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_
       fb_wsync();
       // layer 1 (h -> k): d loss / d h_o on lane o
       // (split: each group its half of the outputs, then the two halves' sum on both)
-      float gh = hl ? fb_vjp_input<FERRO, 4>(plan, P1, o, h, ph, gk + dlo, dlo, dn) : 0.f;
+      float gh = hl ? fb_vjp_input<FERRO, 4, LDSP, 1>(plan, P1, o, h, ph, gk + dlo, dlo, dn) : 0.f;
       if (SF == 2) gh += __shfl_xor(gh, U);
       if (live && dl) GK[(ev * a.B + b) * D + o] = gk[o];
       if (live && own && hl) GH[(ev * a.B + b) * H + o] = gh;
@@ -270,7 +276,7 @@ __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_
       float gx = 0.f;
       for (int i = sg; i < D; i += SF) {  // group sg: the inputs i = sg (mod SF)
         const float one = 1.0f;
-        const float c = hl ? gh * fb_vjp_input<FERRO, 4>(plan, P0, i, xs[i], ps[i], &one, o, 1) : 0.f;
+        const float c = hl ? gh * fb_vjp_input<FERRO, 4, LDSP, 0>(plan, P0, i, xs[i], ps[i], &one, o, 1) : 0.f;
         float sum = c;
         for (int m = U >> 1; m >= 1; m >>= 1) sum += __shfl_xor(sum, m);  // within the group's lanes
         if (o == i) gx = sum;

@@ -14,6 +14,7 @@
 #include <type_traits>
 
 #include "fetode_common.h"
+#include "fetode_fieldn_plan.h"
 #if (defined(FETODE_EXP_NO_GRIDSUM) || defined(FETODE_EXP_NO_EVAL)) && !defined(FETODE_DIAG)
 #error "FETODE_EXP_NO_GRIDSUM / FETODE_EXP_NO_EVAL are diagnostic knobs: build them with make diag"
 #endif
@@ -1537,47 +1538,53 @@ __device__ __forceinline__ void fn_wsync() { asm volatile("s_waitcnt lgkmcnt(0)"
 
 __device__ __forceinline__ float fn_sig_l2(float zl) { return rcp(1.0f + ex2(zl)); }  // 1/(1+2^zl)
 
-// KAN edge (o, i) + the Ferro elements (o, i, k) of one layer at input x (gate weight w)
-template <bool FERRO, int UNR = 1>
+// KAN edge (o, i) + the Ferro elements (o, i, k) of one layer at input x (gate weight w); IMG: the
+// plan is read in its lane-contiguous LDS image (fetode_fieldn_plan.h), layer L
+template <bool FERRO, int UNR, bool IMG, int L>
 __device__ __forceinline__ float fn_edge(const float* __restrict__ plan, const LayerPlan& P, int o, int i, float x,
                                          float sx, float w, int mfix, float u) {
-  const float* kw = plan + P.kw + ((int64_t)o * P.in + i) * P.NFL;
+  using X = FnIdx<IMG, L>;
+  const int st = X::stride(P);
+  const float* kw = plan + X::row(P, P.kw, o, i, P.NFL);
   float v = kw[0] * sx;
-  const float* lg = plan + P.lg + 2 * (int64_t)i * P.NB;
   // UNR: the packed fixed-grid launch runs ~one wave per SIMD, so the independent exp2 / rcp chains
   // of consecutive basis functions must overlap within the lane (the sums stay in order); the
   // resident dopri5 keeps its register budget (occupancy = the batch one grid holds)
 #pragma unroll UNR
-  for (int j = 0; j < P.NB; ++j) v = ffma(kw[1 + j], fn_sig_l2(ffma(lg[2 * j], x, lg[2 * j + 1])), v);
-  const float4 cf = *reinterpret_cast<const float4*>(plan + P.sp + (((int64_t)o * P.in + i) * (P.NI + 1) + mfix) * 4);
+  for (int j = 0; j < P.NB; ++j)
+    v = ffma(kw[(1 + j) * st], fn_sig_l2(ffma(plan[X::lg(P, i, j, 0)], x, plan[X::lg(P, i, j, 1)])), v);
+  const float4 cf = *reinterpret_cast<const float4*>(plan + X::sp(P, o, i, mfix));
   v += ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
   if constexpr (FERRO) {
-    const int64_t e0 = (int64_t)o * P.in * P.K + (int64_t)i * P.K;
+    const int64_t e0 = X::row(P, 0, o, i, P.K);
     const float* GEc = plan + P.fe_GEc + e0;
     const float* k2 = plan + P.fe_k2 + e0;
     const float* kE = plan + P.fe_k2Ec + e0;
     const float* cp = plan + P.fe_CPs2 + e0;
 #pragma unroll UNR
     for (int k = 0; k < P.K; ++k) {
-      const float s = rcp(ex2(ffma(P.gsl2e, x, GEc[k])) + 1.0f);  // sigma(gs(-x - Ec)), one rounding as v4
+      const float s = rcp(ex2(ffma(P.gsl2e, x, GEc[k * st])) + 1.0f);  // sigma(gs(-x - Ec)), one rounding as v4
       const float m = ffma(w, s, 1.0f);                    // branch momentum (branch_sign = 1)
-      const float z = ffma(kE[k], m, k2[k] * x);
+      const float z = ffma(kE[k * st], m, k2[k * st] * x);
       const float th = ffma(rcp(ex2(z) + 1.0f), -2.0f, 1.0f);
-      v = ffma(cp[k], th, v);
+      v = ffma(cp[k * st], th, v);
     }
   }
   return v;
 }
 
 // knot interval of x on input i's grid (m = NI: off the grid, the zero row) and its coordinate u
+template <bool IMG, int L>
 __device__ __forceinline__ void fn_interval(const float* __restrict__ plan, const LayerPlan& P, int i, float x, int& mfix,
                                             float& u) {
-  const float* g = plan + P.knots + (int64_t)i * P.NG;
+  using X = FnIdx<IMG, L>;
+  const float* g = plan + X::knot(P, i, 0);
+  const int gs = X::knot_stride(P);
   int m = -1;
-  for (int j = 0; j < P.NG; ++j) m += x >= g[j] ? 1 : 0;
+  for (int j = 0; j < P.NG; ++j) m += x >= g[j * gs] ? 1 : 0;
   const bool fin = __builtin_isfinite(x);
   mfix = ((unsigned)m < (unsigned)P.NI && fin) ? m : P.NI;
-  u = mfix < P.NI ? (x - g[mfix]) * plan[P.rh + (int64_t)i * P.NI + mfix] : (fin ? 0.0f : __builtin_nanf(""));
+  u = mfix < P.NI ? (x - g[mfix * gs]) * plan[X::rh(P, i, mfix)] : (fin ? 0.0f : __builtin_nanf(""));
 }
 
 // DOPRI: the whole dopri5 solve in this launch (fetode_integrate_dopri5 for these shapes), one
@@ -1612,8 +1619,7 @@ __global__ __launch_bounds__(DOPRI ? 64 : (LDSP ? 64 * kFnWavesL : 64 * kFnWaves
   constexpr int NW = DOPRI ? 1 : (LDSP ? kFnWavesL : kFnWaves);
   extern __shared__ float s_plan[];
   if constexpr (LDSP) {
-    const int64_t n = a.P1.end;  // the plan of both layers, from word 0
-    for (int64_t q = threadIdx.x; q < n; q += blockDim.x) s_plan[q] = a.plan[q];
+    fn_stage_image(s_plan, a.plan, a.P0, a.P1);  // the lane-contiguous image of both layers' plans
     __syncthreads();
   }
   if constexpr (DOPRI) {
@@ -1675,8 +1681,8 @@ __global__ __launch_bounds__(DOPRI ? 64 : (LDSP ? 64 * kFnWavesL : 64 * kFnWaves
         if constexpr (FERRO) w = ffma(fn_sig_l2(-P0.gsl2e * (x - (re0 ? x : p0[i]))), -P0.wc, P0.wc);
         int mfix;
         float u;
-        fn_interval(plan, P0, i, x, mfix, u);
-        const float e = fn_edge<FERRO, DOPRI ? 1 : 4>(plan, P0, o, i, x, sx, w, mfix, u);
+        fn_interval<LDSP, 0>(plan, P0, i, x, mfix, u);
+        const float e = fn_edge<FERRO, DOPRI ? 1 : 4, LDSP, 0>(plan, P0, o, i, x, sx, w, mfix, u);
         if (i & 1) po += e;
         else pe += e;
       }
@@ -1699,12 +1705,12 @@ __global__ __launch_bounds__(DOPRI ? 64 : (LDSP ? 64 * kFnWavesL : 64 * kFnWaves
     if (hl) {
       sh = h * fn_sig_l2(-h * FETODE_LOG2E);
       if constexpr (FERRO) w1 = ffma(fn_sig_l2(-P1.gsl2e * (h - (re1 ? h : prev1))), -P1.wc, P1.wc);
-      fn_interval(plan, P1, o, h, m1, u1);
+      fn_interval<LDSP, 1>(plan, P1, o, h, m1, u1);
     }
     if (FERRO) prev1 = h;
     re1 = false;
     for (int d = sg; d < D; d += SF) {  // group sg: the outputs d = sg (mod SF)
-      float v = hl ? fn_edge<FERRO, DOPRI ? 1 : 4>(plan, P1, d, o, h, sh, w1, m1, u1) : 0.f;
+      float v = hl ? fn_edge<FERRO, DOPRI ? 1 : 4, LDSP, 1>(plan, P1, d, o, h, sh, w1, m1, u1) : 0.f;
       for (int s = U >> 1; s >= 1; s >>= 1) v += __shfl_xor(v, s);  // within the group's U lanes
       if (o == 0) ks[d] = v + plan[P1.fconst + d];
     }
