@@ -766,6 +766,174 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
   }
 }
 
+// Narrow layers (out <= 4: a field's last layer, in -> D): the tile kernel above stages features
+// and g rows in LDS for a handful of products per row.  Here a thread owns rows of ONE input and
+// keeps every (feature, output) sum in registers — (1 + NS + NB) x OUT of them — so a row is its x,
+// its g row (OUT floats, the next row's already in flight), the features in registers and
+// (1 + NS + NB) x OUT FMAs; the logistic a / b sums ride along.  The only LDS is the input's
+// tables (broadcast reads) and the final fixed-order sums (wave butterflies, then the 4 waves in
+// order), written in the tile kernel's per-split layout for kan_psum_reduce_kernel.
+constexpr int kPrNS = 8, kPrNB = 12, kPrMaxOut = 4;
+bool pr_ok(const fetode_kanlinear_t* kl) {
+  return kl->spline_order == 3 && kl->out_features <= kPrMaxOut && kl->grid_size + 3 <= kPrNS &&
+         kl->num_logistic <= kPrNB;
+}
+int pr_splits(const fetode_kanlinear_t* kl, int64_t B) {
+  int64_t S = kPsBlocks / kl->in_features;
+  const int64_t rs = (B + 1023) / 1024;  // at least ~4 rows per thread
+  if (S > rs) S = rs;
+  if (S > ps_smax(kl)) S = ps_smax(kl);
+  return S < 1 ? 1 : (int)S;
+}
+
+// NBM >= NB sizes the register sums: 10 (efficient_kan's default num_basis) or kPrNB
+template <int OUT, int NBM>
+__global__ __launch_bounds__(256) void kan_psum_rows_kernel(fetode_kanlinear_t kl, const float* __restrict__ x,
+                                                           const float* __restrict__ g, int64_t B,
+                                                           float* __restrict__ part /* (S, in, NF, out) */,
+                                                           float* __restrict__ abpart /* (S, in, NB, 2) */) {
+  constexpr int SO = 3, NV = (1 + kPrNS + NBM) * OUT + 2 * NBM;
+  __shared__ float wl[OUT * NBM], kn[kPrNS + SO + 1], rk[SO * (kPrNS + SO)], lab[3 * NBM];
+  __shared__ float red[4][NV];
+  const int in = kl.in_features, NB = kl.num_logistic;
+  const int NG = kl.grid_size + 2 * SO + 1, NS = kl.grid_size + SO, NF = 1 + NS + NB;
+  const int i = blockIdx.x, sp = blockIdx.y, S = gridDim.y, tid = threadIdx.x;
+  // input i's tables: W'[o, (i, j)], knots, reciprocal spans (bspline_vals_derivs_rk), logistic
+  for (int q = tid; q < OUT * NB; q += 256) {
+    const int o = q / NB, j = q % NB;
+    const float ls = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
+    wl[o * NBM + j] = (kl.logistic_weight[(int64_t)o * in * NB + i * NB + j] * kl.scale_logistic) * ls;
+  }
+  const float* gg = kl.grid + (int64_t)i * NG;
+  for (int q = tid; q < NG; q += 256) kn[q] = gg[q];
+  for (int q = tid; q < SO * (NG - 1); q += 256) {
+    const int k = q / (NG - 1) + 1, j = q % (NG - 1);
+    rk[q] = j + k < NG ? 1.0f / (gg[j + k] - gg[j]) : 0.f;
+  }
+  for (int j = tid; j < NB; j += 256) {
+    lab[3 * j] = -kl.logistic_a[i * NB + j] * FETODE_LOG2E;
+    lab[3 * j + 1] = kl.logistic_b[i * NB + j];
+    lab[3 * j + 2] = kl.logistic_a[i * NB + j];
+  }
+  __syncthreads();
+  float ab[OUT], spl[kPrNS][OUT], lw[NBM][OUT], la[NBM], lb[NBM];
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) {
+    ab[o] = 0.f;
+#pragma unroll
+    for (int c = 0; c < kPrNS; ++c) spl[c][o] = 0.f;
+#pragma unroll
+    for (int j = 0; j < NBM; ++j) lw[j][o] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < NBM; ++j) la[j] = lb[j] = 0.f;
+  const int64_t r0 = sp * B / S, r1 = (sp + 1) * B / S;
+  float xn = 0.f, gn[OUT];
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) gn[o] = 0.f;
+  if (r0 + tid < r1) {
+    xn = x[(r0 + tid) * in + i];
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) gn[o] = g[(r0 + tid) * OUT + o];
+  }
+  for (int64_t r = r0 + tid; r < r1; r += 256) {
+    const float xv = xn;
+    float gv[OUT];
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) gv[o] = gn[o];
+    if (r + 256 < r1) {  // the next row in flight while this one is summed
+      xn = x[(r + 256) * in + i];
+#pragma unroll
+      for (int o = 0; o < OUT; ++o) gn[o] = g[(r + 256) * OUT + o];
+    }
+    const float silu = xv * rcp(1.0f + ex2(-xv * FETODE_LOG2E));
+    float val[SO + 1], der[SO + 1];
+    const int m = bspline_vals_derivs_rk<SO>(xv, NG, kn, rk, val, der);  // der unused: folded away
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) ab[o] = ffma(gv[o], silu, ab[o]);
+#pragma unroll
+    for (int c = 0; c < kPrNS; ++c) {
+      float v = m == -2 ? __builtin_nanf("") : 0.f;  // non-finite x: NaN bases (the tile kernel's rule)
+#pragma unroll
+      for (int q = 0; q <= SO; ++q)
+        if (m >= 0 && m - SO + q == c) v = val[q];
+      if (c < NS)
+#pragma unroll
+        for (int o = 0; o < OUT; ++o) spl[c][o] = ffma(gv[o], v, spl[c][o]);
+    }
+#pragma unroll
+    for (int j = 0; j < NBM; ++j) {
+      if (j < NB) {
+        const float phi = 2.0f * rcp(1.0f + ex2(lab[3 * j] * (xv - lab[3 * j + 1])));
+        float gphi = 0.f;
+#pragma unroll
+        for (int o = 0; o < OUT; ++o) {
+          lw[j][o] = ffma(gv[o], phi, lw[j][o]);
+          gphi += gv[o] * wl[o * NBM + j];
+        }
+        const float sg = 0.5f * phi;  // sigm(a (x - b))
+        const float dz = gphi * 2.0f * sg * (1.0f - sg);
+        la[j] += dz * (xv - lab[3 * j + 1]);
+        lb[j] += dz * (-lab[3 * j + 2]);
+      }
+    }
+  }
+  // fixed-order sums: a butterfly per wave, then the four waves in order
+  const int wid = tid >> 6, lane = tid & 63;
+  auto wsum = [&](float v) {
+#pragma unroll
+    for (int mm = 32; mm >= 1; mm >>= 1) v += __shfl_xor(v, mm);
+    return v;
+  };
+  int q = 0;
+#pragma unroll
+  for (int o = 0; o < OUT; ++o) {
+    const float v = wsum(ab[o]);
+    if (lane == 0) red[wid][q] = v;
+    ++q;
+  }
+#pragma unroll
+  for (int c = 0; c < kPrNS; ++c)
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) {
+      const float v = c < NS ? wsum(spl[c][o]) : 0.f;
+      if (lane == 0) red[wid][q] = v;
+      ++q;
+    }
+#pragma unroll
+  for (int j = 0; j < NBM; ++j) {
+#pragma unroll
+    for (int o = 0; o < OUT; ++o) {
+      const float v = j < NB ? wsum(lw[j][o]) : 0.f;
+      if (lane == 0) red[wid][q] = v;
+      ++q;
+    }
+    const float va = j < NB ? wsum(la[j]) : 0.f, vb = j < NB ? wsum(lb[j]) : 0.f;
+    if (lane == 0) {
+      red[wid][q] = va;
+      red[wid][q + 1] = vb;
+    }
+    q += 2;
+  }
+  __syncthreads();
+  // slot order above: base (OUT), spline c-major (kPrNS x OUT), then per j: lw (OUT), a, b
+  for (int e = tid; e < NV; e += 256) {
+    const float v = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+    if (e < OUT) {
+      part[(((int64_t)sp * in + i) * NF + 0) * OUT + e] = v;
+    } else if (e < OUT + kPrNS * OUT) {
+      const int c = (e - OUT) / OUT, o = (e - OUT) % OUT;
+      if (c < NS) part[(((int64_t)sp * in + i) * NF + 1 + c) * OUT + o] = v;
+    } else {
+      const int t = e - OUT - kPrNS * OUT, j = t / (OUT + 2), k = t % (OUT + 2);
+      if (j < NB) {
+        if (k < OUT) part[(((int64_t)sp * in + i) * NF + 1 + NS + j) * OUT + k] = v;
+        else abpart[(((int64_t)sp * in + i) * NB + j) * 2 + (k - OUT)] = v;
+      }
+    }
+  }
+}
+
 // the splits in order -> base-weight gradient, d_scaled, d_wl, logistic a / b: one wave per output
 // (lane l sums splits l, l + 64, ...; then a fixed butterfly: run-to-run identical)
 __device__ __forceinline__ float split_sum64(const float* __restrict__ p, int S, int64_t stride, int lane) {
@@ -1086,11 +1254,20 @@ int fetode_kanlinear_backward(const fetode_kanlinear_t* kl, const float* x, int6
                          d_scaled, d_wl, *grads, accumulate);
       LAUNCH_CHECK();
     } else if (B >= kPsMinRows && ps_ok(kl)) {   // many rows: features once per (row, input)
-      const int S = ps_splits(kl, B);
+      const bool rows = pr_ok(kl);   // narrow layers: the row-owner form (sums in registers)
+      const int S = rows ? pr_splits(kl, B) : ps_splits(kl, B);
       float* part = d_wl + (int64_t)out * in * NB;
       float* abpart = part + (int64_t)ps_smax(kl) * in * (1 + NS + NB) * out;
-      auto* kfn = NB > 0 ? kan_psum_kernel<3, true> : kan_psum_kernel<3, false>;
-      hipLaunchKernelGGL(kfn, dim3(ps_groups(kl), S), dim3(256), ps_lds_bytes(kl), s, *kl, x, g, B, part, abpart);
+      if (rows) {
+        auto* kfn = NB <= 10 ? (out == 1 ? kan_psum_rows_kernel<1, 10> : out == 2 ? kan_psum_rows_kernel<2, 10>
+                               : out == 3 ? kan_psum_rows_kernel<3, 10> : kan_psum_rows_kernel<4, 10>)
+                             : (out == 1 ? kan_psum_rows_kernel<1, kPrNB> : out == 2 ? kan_psum_rows_kernel<2, kPrNB>
+                               : out == 3 ? kan_psum_rows_kernel<3, kPrNB> : kan_psum_rows_kernel<4, kPrNB>);
+        hipLaunchKernelGGL(kfn, dim3(in, S), dim3(256), 0, s, *kl, x, g, B, part, abpart);
+      } else {
+        auto* kfn = NB > 0 ? kan_psum_kernel<3, true> : kan_psum_kernel<3, false>;
+        hipLaunchKernelGGL(kfn, dim3(ps_groups(kl), S), dim3(256), ps_lds_bytes(kl), s, *kl, x, g, B, part, abpart);
+      }
       LAUNCH_CHECK();
       const int64_t nt = (int64_t)out * in * (1 + NS + NB) + (int64_t)in * NB;
       hipLaunchKernelGGL(kan_psum_reduce_kernel, dim3(nblk(nt, 4)), dim3(256), 0, s, *kl, part, abpart, S, d_scaled,

@@ -61,6 +61,33 @@ def test_kanlinear_grads_vs_oracle(dev, tag, dims):
         assert_grad_close(mp[n].grad, ps[k].grad, n)
 
 
+@pytest.mark.parametrize("dims,nb", [((2, 16), 10), ((33, 5), 10), ((4, 64), 3), ((3, 7), 0), ((1, 12), 10),
+                                     ((16, 2), 10), ((6, 4), 0), ((5, 3), 12), ((7, 1), 4)])
+def test_kanlinear_grads_many_rows_vs_oracle(dev, dims, nb):
+    """B = 4096 rows: the many-row parameter sums (fetode_grad.hip, B >= 2048) — the tile kernel
+    (input groups of 1..4 with a ragged last group at 33 inputs, 64 outputs, no logistic basis, one
+    input) and the row-owner kernel of narrow layers (out <= 4; NB 0, 4, 10, 12) — against the
+    oracle's fp64 autograd (some rows off the grid on either side)."""
+    import fet_ode_amd as F
+    from oracle import torch_ref as O
+    torch.manual_seed(3)
+    m = F.KANLinear(*dims, num_basis=max(nb, 1), enable_logistic_basis=nb > 0)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    gen = torch.Generator().manual_seed(4)
+    x = torch.rand(4096, dims[0], generator=gen) * 2.6 - 1.3
+    w = torch.randn(4096, dims[1], generator=gen)
+    xg = x.clone().to(dev).requires_grad_(True)
+    (m(xg) * w.to(dev)).sum().backward()
+    ps = {k: v.double().requires_grad_(k != "grid") for k, v in sd.items() if v.dtype.is_floating_point}
+    p = O.KANLinearParams.from_state_dict(ps)
+    xc = x.double().requires_grad_(True)
+    (O.kanlinear_forward(xc, p) * w.double()).sum().backward()
+    assert_grad_close(xg.grad, xc.grad, "x", rel=1e-4)
+    for n, q in m.named_parameters():
+        assert_grad_close(q.grad, ps[n].grad, n, rel=1e-4)
+
+
 @pytest.mark.parametrize("tag,dims", [("ferro_2x10x10", (2, 10, 10)), ("ferro_10x2x10", (10, 2, 10))])
 def test_ferro_grads_vs_oracle(dev, tag, dims):
     """Second call of a B=5 sequence (dx != 0, prev from the first call)."""
