@@ -556,6 +556,70 @@ __global__ void kan_scale_ls_kernel(fetode_kanlinear_t kl, const float* __restri
   put(gr.logistic_scaler ? gr.logistic_scaler + t : nullptr, dls, accumulate);
 }
 
+// The cubic B-spline bases of one input as per-interval polynomials in u = (x - g[m]) / (g[m+1] -
+// g[m]): bp[m * 4 + r] = the power-basis coefficients of B_{m-3+r} on interval m — Cox-de Boor
+// (efficientkan.py:117-131) restricted to interval m, evaluated in fp64 at u = 0, 1/3, 2/3, 1 and
+// converted (exact for cubics; fetode_bwd.hip BInTab builds the same tables).  A row's four
+// bases are then four float4 reads at its interval and a Horner each, instead of the recursion's
+// chain of knot reads.  Entry q of the NI x 4 table (one thread per entry).
+__device__ float4 bpoly_entry(const float* __restrict__ g, int NG, int q) {
+  constexpr int SO = 3;
+  const int m = q / 4, r = q % 4;
+  const double h = (double)g[m + 1] - g[m];
+  double v[4];
+  for (int s = 0; s < 4; ++s) {
+    const double x = g[m] + h * (s / 3.0);
+    double N[SO + 2];
+    for (int t = 0; t < SO + 2; ++t) N[t] = 0.0;
+    N[SO] = 1.0;
+    for (int k = 1; k <= SO; ++k) {
+      double M[SO + 2];
+      for (int t = 0; t < SO + 2; ++t) M[t] = 0.0;
+      for (int t = SO - k; t <= SO; ++t) {
+        const int j = m - SO + t;
+        if (j >= 0 && j <= NG - 2 - k)
+          M[t] = (x - g[j]) / ((double)g[j + k] - g[j]) * N[t] +
+                 ((double)g[j + k + 1] - x) / ((double)g[j + k + 1] - g[j + 1]) * N[t + 1];
+      }
+      for (int t = 0; t < SO + 2; ++t) N[t] = M[t];
+    }
+    v[s] = N[r];
+  }
+  return make_float4((float)v[0], (float)((-11.0 * v[0] + 18.0 * v[1] - 9.0 * v[2] + 2.0 * v[3]) / 2.0),
+                     (float)(9.0 * (2.0 * v[0] - 5.0 * v[1] + 4.0 * v[2] - v[3]) / 2.0),
+                     (float)(9.0 * (-v[0] + 3.0 * v[1] - 3.0 * v[2] + v[3]) / 2.0));
+}
+
+// every input's table once per launch (the many-row kernels stage their inputs' rows from it)
+__global__ void bpoly_build_kernel(fetode_kanlinear_t kl, float4* __restrict__ tab) {
+  const int NG = kl.grid_size + 2 * kl.spline_order + 1, per = (NG - 1) * 4;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < kl.in_features * per) tab[t] = bpoly_entry(kl.grid + (int64_t)(t / per) * NG, NG, t % per);
+}
+
+// a row's interval m (-1: off the grid, -2: not finite) and its four basis values from the tables
+__device__ __forceinline__ int bpoly_vals(float x, int NG, const float* __restrict__ kn, const float* __restrict__ rh,
+                                          const float4* __restrict__ bp, float* val) {
+  constexpr int SO = 3;
+#pragma unroll
+  for (int r = 0; r <= SO; ++r) val[r] = 0.f;
+  if (!__builtin_isfinite(x)) {
+#pragma unroll
+    for (int r = 0; r <= SO; ++r) val[r] = __builtin_nanf("");
+    return -2;
+  }
+  int m = -1;
+  for (int j = 0; j < NG; ++j) m += (x >= kn[j]) ? 1 : 0;
+  if (m < 0 || m > NG - 2) return -1;
+  const float u = (x - kn[m]) * rh[m];
+  float4 p[SO + 1];
+#pragma unroll
+  for (int r = 0; r <= SO; ++r) p[r] = bp[m * 4 + r];
+#pragma unroll
+  for (int r = 0; r <= SO; ++r) val[r] = ffma(ffma(ffma(p[r].w, u, p[r].z), u, p[r].y), u, p[r].x);
+  return m;
+}
+
 // ------------------------------------------------------------------------------------------
 // Parameter sums over many rows (B >= kPsMinRows: the fieldn training pass runs them over every
 // (evaluation, trajectory) row, fetode_fieldn_bwd.hip): workgroup (input group, row split s) walks
@@ -591,14 +655,15 @@ int ps_splits(const fetode_kanlinear_t* kl, int64_t B) {
 size_t ps_lds_bytes(const fetode_kanlinear_t* kl) {
   const int NF = ps_nf(kl), out = kl->out_features, ig = ps_ig(kl->in_features, NF, out);
   const int NG = kl->grid_size + 2 * kl->spline_order + 1;
-  const int64_t n = (int64_t)ig * kPsTile * (NF | 1) + (int64_t)kPsTile * (out | 1) + (int64_t)ig * out * kl->num_logistic +
-                    (int64_t)ig * (NG + kl->spline_order * (NG - 1) + 3 * kl->num_logistic);
+  const int64_t n = (int64_t)ig * (NG - 1) * 16 + (int64_t)ig * kPsTile * (NF | 1) + (int64_t)kPsTile * (out | 1) +
+                    (int64_t)ig * out * kl->num_logistic + (int64_t)ig * (NG + (NG - 1) + 3 * kl->num_logistic);
   return sizeof(float) * (size_t)(n > 256 * 16 ? n : 256 * 16);
 }
 
 template <int SO, bool LOG>
 __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, const float* __restrict__ x,
                                                       const float* __restrict__ g, int64_t B,
+                                                      const float4* __restrict__ bpt /* (in, NG - 1, 4) */,
                                                       float* __restrict__ part /* (S, in, NF, out) */,
                                                       float* __restrict__ abpart /* (S, in, NB, 2) */) {
   extern __shared__ float ps_lds[];
@@ -608,12 +673,13 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
   const int s = blockIdx.y, S = gridDim.y, tid = threadIdx.x;
   // odd row strides: a thread per row reads its row's g (logistic a / b) without bank conflicts
   const int FS = NF | 1, GS = out | 1;
-  float* ft = ps_lds;                          // [IG * kPsTile][FS]: (input, row) features
+  float4* bp = reinterpret_cast<float4*>(ps_lds);  // [IG][NG - 1][4] basis cubics (bpoly_entry)
+  float* ft = ps_lds + IG * (NG - 1) * 16;     // [IG * kPsTile][FS]: (input, row) features
   float* gt = ft + IG * kPsTile * FS;          // [kPsTile][GS]
   float* wl = gt + kPsTile * GS;               // [IG][out][NB]
   float* kn = wl + IG * out * NB;              // [IG][NG] knots
-  float* rk = kn + IG * NG;                    // [IG][SO][NG - 1] reciprocal knot spans
-  float* lab = rk + IG * SO * (NG - 1);        // [IG][NB][3] logistic (-a log2e, b, a)
+  float* rh = kn + IG * NG;                    // [IG][NG - 1] 1 / knot steps
+  float* lab = rh + IG * (NG - 1);             // [IG][NB][3] logistic (-a log2e, b, a)
   float* red = ps_lds;                         // the workgroup sums, after the walk
   const int64_t tiles = (B + kPsTile - 1) / kPsTile;
   const int64_t t0 = s * tiles / S, t1 = (s + 1) * tiles / S;
@@ -625,11 +691,11 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
   }
   // the group's knots, reciprocal spans (bspline_vals_derivs_rk's layout) and logistic parameters
   for (int q = tid; q < ni * NG; q += 256) kn[q] = kl.grid[(int64_t)(i0 + q / NG) * NG + q % NG];
-  for (int q = tid; q < ni * SO * (NG - 1); q += 256) {
-    const int ig = q / (SO * (NG - 1)), kj = q % (SO * (NG - 1)), k = kj / (NG - 1) + 1, j = kj % (NG - 1);
-    const float* gg = kl.grid + (int64_t)(i0 + ig) * NG;
-    rk[q] = j + k < NG ? 1.0f / (gg[j + k] - gg[j]) : 0.f;
+  for (int q = tid; q < ni * (NG - 1); q += 256) {
+    const float* gg = kl.grid + (int64_t)(i0 + q / (NG - 1)) * NG;
+    rh[q] = 1.0f / (gg[q % (NG - 1) + 1] - gg[q % (NG - 1)]);
   }
+  for (int q = tid; q < ni * (NG - 1) * 4; q += 256) bp[q] = bpt[(int64_t)i0 * (NG - 1) * 4 + q];
   for (int q = tid; LOG && q < ni * NB; q += 256) {
     lab[3 * q] = -kl.logistic_a[i0 * NB + q] * FETODE_LOG2E;
     lab[3 * q + 1] = kl.logistic_b[i0 * NB + q];
@@ -640,7 +706,8 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
   const bool fe = fig < ni;
   const int fin = i0 + (fe ? fig : 0);
   const float* gi = kn + (fe ? fig : 0) * NG;
-  const float* rki = rk + (fe ? fig : 0) * SO * (NG - 1);
+  const float* rhi = rh + (fe ? fig : 0) * (NG - 1);
+  const float4* bpi = bp + (fe ? fig : 0) * (NG - 1) * 4;
   const float* labi = lab + (fe ? fig : 0) * 3 * NB;
   // sum role: a (input, feature block, output block) triple and a share of the tile's rows
   const int FBK = (NF + 3) / 4, OBK = (out + 3) / 4, P = ni * FBK * OBK, Q = P < 256 ? 256 / P : 1;
@@ -682,8 +749,8 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
       float* fr = ft + (fig * kPsTile + frr) * FS;
       // the forward's exp2 / rcp forms (fn_edge): SiLU, logistic 2 / (1 + 2^(-a log2e (x - b)))
       fr[0] = live ? xv * rcp(1.0f + ex2(-xv * FETODE_LOG2E)) : 0.f;
-      float val[SO + 1], der[SO + 1];
-      const int m = bspline_vals_derivs_rk<SO>(xv, NG, gi, rki, val, der);  // der unused: folded away
+      float val[SO + 1];
+      const int m = bpoly_vals(xv, NG, gi, rhi, bpi, val);
       for (int c = 0; c < NS; ++c) {
         float v = (live && m == -2) ? __builtin_nanf("") : 0.f;
 #pragma unroll
@@ -790,10 +857,12 @@ int pr_splits(const fetode_kanlinear_t* kl, int64_t B) {
 template <int OUT, int NBM>
 __global__ __launch_bounds__(256) void kan_psum_rows_kernel(fetode_kanlinear_t kl, const float* __restrict__ x,
                                                            const float* __restrict__ g, int64_t B,
+                                                           const float4* __restrict__ bpt /* (in, NG - 1, 4) */,
                                                            float* __restrict__ part /* (S, in, NF, out) */,
                                                            float* __restrict__ abpart /* (S, in, NB, 2) */) {
   constexpr int SO = 3, NV = (1 + kPrNS + NBM) * OUT + 2 * NBM;
-  __shared__ float wl[OUT * NBM], kn[kPrNS + SO + 1], rk[SO * (kPrNS + SO)], lab[3 * NBM];
+  __shared__ float wl[OUT * NBM], kn[kPrNS + SO + 1], rh[kPrNS + SO], lab[3 * NBM];
+  __shared__ float4 bp[(kPrNS + SO) * 4];
   __shared__ float red[4][NV];
   const int in = kl.in_features, NB = kl.num_logistic;
   const int NG = kl.grid_size + 2 * SO + 1, NS = kl.grid_size + SO, NF = 1 + NS + NB;
@@ -806,10 +875,8 @@ __global__ __launch_bounds__(256) void kan_psum_rows_kernel(fetode_kanlinear_t k
   }
   const float* gg = kl.grid + (int64_t)i * NG;
   for (int q = tid; q < NG; q += 256) kn[q] = gg[q];
-  for (int q = tid; q < SO * (NG - 1); q += 256) {
-    const int k = q / (NG - 1) + 1, j = q % (NG - 1);
-    rk[q] = j + k < NG ? 1.0f / (gg[j + k] - gg[j]) : 0.f;
-  }
+  for (int q = tid; q < NG - 1; q += 256) rh[q] = 1.0f / (gg[q + 1] - gg[q]);
+  for (int q = tid; q < (NG - 1) * 4; q += 256) bp[q] = bpt[(int64_t)i * (NG - 1) * 4 + q];
   for (int j = tid; j < NB; j += 256) {
     lab[3 * j] = -kl.logistic_a[i * NB + j] * FETODE_LOG2E;
     lab[3 * j + 1] = kl.logistic_b[i * NB + j];
@@ -847,8 +914,8 @@ __global__ __launch_bounds__(256) void kan_psum_rows_kernel(fetode_kanlinear_t k
       for (int o = 0; o < OUT; ++o) gn[o] = g[(r + 256) * OUT + o];
     }
     const float silu = xv * rcp(1.0f + ex2(-xv * FETODE_LOG2E));
-    float val[SO + 1], der[SO + 1];
-    const int m = bspline_vals_derivs_rk<SO>(xv, NG, kn, rk, val, der);  // der unused: folded away
+    float val[SO + 1];
+    const int m = bpoly_vals(xv, NG, kn, rh, bp, val);
 #pragma unroll
     for (int o = 0; o < OUT; ++o) ab[o] = ffma(gv[o], silu, ab[o]);
 #pragma unroll
@@ -1202,9 +1269,10 @@ int64_t fetode_kanlinear_backward_workspace(const fetode_kanlinear_t* kl) {
   int64_t n = (int64_t)kl->out_features * kl->in_features * (NS + kl->num_logistic);
   if (fetode_kanlinear_wide_supported(kl))   // MFMA partials + logistic a / b partials
     n += (int64_t)kGwSplit * kl->in_features * (kGwF * 16 + 2 * kGwNB);
-  else if (ps_ok(kl))                        // kan_psum_kernel's per-split partials
+  else if (ps_ok(kl))                        // kan_psum_kernel's per-split partials + basis tables
     n += (int64_t)ps_smax(kl) * kl->in_features *
-         ((int64_t)(1 + NS + kl->num_logistic) * kl->out_features + 2 * kl->num_logistic);
+         ((int64_t)(1 + NS + kl->num_logistic) * kl->out_features + 2 * kl->num_logistic) +
+         4 + (int64_t)kl->in_features * (kl->grid_size + 2 * kl->spline_order) * 16;
   return (int64_t)sizeof(float) * n;
 }
 
@@ -1258,15 +1326,19 @@ int fetode_kanlinear_backward(const fetode_kanlinear_t* kl, const float* x, int6
       const int S = rows ? pr_splits(kl, B) : ps_splits(kl, B);
       float* part = d_wl + (int64_t)out * in * NB;
       float* abpart = part + (int64_t)ps_smax(kl) * in * (1 + NS + NB) * out;
+      float4* bpt = reinterpret_cast<float4*>(((uintptr_t)(abpart + (int64_t)ps_smax(kl) * in * NB * 2) + 15) & ~uintptr_t(15));
+      const int NG = kl->grid_size + 2 * SO + 1;
+      hipLaunchKernelGGL(bpoly_build_kernel, dim3(nblk((int64_t)in * (NG - 1) * 4, 64)), dim3(64), 0, s, *kl, bpt);
+      LAUNCH_CHECK();
       if (rows) {
         auto* kfn = NB <= 10 ? (out == 1 ? kan_psum_rows_kernel<1, 10> : out == 2 ? kan_psum_rows_kernel<2, 10>
                                : out == 3 ? kan_psum_rows_kernel<3, 10> : kan_psum_rows_kernel<4, 10>)
                              : (out == 1 ? kan_psum_rows_kernel<1, kPrNB> : out == 2 ? kan_psum_rows_kernel<2, kPrNB>
                                : out == 3 ? kan_psum_rows_kernel<3, kPrNB> : kan_psum_rows_kernel<4, kPrNB>);
-        hipLaunchKernelGGL(kfn, dim3(in, S), dim3(256), 0, s, *kl, x, g, B, part, abpart);
+        hipLaunchKernelGGL(kfn, dim3(in, S), dim3(256), 0, s, *kl, x, g, B, bpt, part, abpart);
       } else {
         auto* kfn = NB > 0 ? kan_psum_kernel<3, true> : kan_psum_kernel<3, false>;
-        hipLaunchKernelGGL(kfn, dim3(ps_groups(kl), S), dim3(256), ps_lds_bytes(kl), s, *kl, x, g, B, part, abpart);
+        hipLaunchKernelGGL(kfn, dim3(ps_groups(kl), S), dim3(256), ps_lds_bytes(kl), s, *kl, x, g, B, bpt, part, abpart);
       }
       LAUNCH_CHECK();
       const int64_t nt = (int64_t)out * in * (1 + NS + NB) + (int64_t)in * NB;
