@@ -656,7 +656,7 @@ size_t ps_lds_bytes(const fetode_kanlinear_t* kl) {
   const int NF = ps_nf(kl), out = kl->out_features, ig = ps_ig(kl->in_features, NF, out);
   const int NG = kl->grid_size + 2 * kl->spline_order + 1;
   const int64_t n = (int64_t)ig * (NG - 1) * 16 + (int64_t)ig * kPsTile * (NF | 1) + (int64_t)kPsTile * (out | 1) +
-                    (int64_t)ig * out * kl->num_logistic + (int64_t)ig * (NG + (NG - 1) + 3 * kl->num_logistic);
+                    (int64_t)ig * out * ((kl->num_logistic + 3) & ~3) + (int64_t)ig * (NG + (NG - 1) + 3 * kl->num_logistic);
   return sizeof(float) * (size_t)(n > 256 * 16 ? n : 256 * 16);
 }
 
@@ -673,21 +673,22 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
   const int s = blockIdx.y, S = gridDim.y, tid = threadIdx.x;
   // odd row strides: a thread per row reads its row's g (logistic a / b) without bank conflicts
   const int FS = NF | 1, GS = out | 1;
+  const int NBP = (NB + 3) & ~3;                   // W' rows padded to float4s
   float4* bp = reinterpret_cast<float4*>(ps_lds);  // [IG][NG - 1][4] basis cubics (bpoly_entry)
-  float* ft = ps_lds + IG * (NG - 1) * 16;     // [IG * kPsTile][FS]: (input, row) features
+  float* wl = ps_lds + IG * (NG - 1) * 16;     // [IG][out][NBP] (16-byte aligned rows)
+  float* ft = wl + IG * out * NBP;             // [IG * kPsTile][FS]: (input, row) features
   float* gt = ft + IG * kPsTile * FS;          // [kPsTile][GS]
-  float* wl = gt + kPsTile * GS;               // [IG][out][NB]
-  float* kn = wl + IG * out * NB;              // [IG][NG] knots
+  float* kn = gt + kPsTile * GS;               // [IG][NG] knots
   float* rh = kn + IG * NG;                    // [IG][NG - 1] 1 / knot steps
   float* lab = rh + IG * (NG - 1);             // [IG][NB][3] logistic (-a log2e, b, a)
   float* red = ps_lds;                         // the workgroup sums, after the walk
   const int64_t tiles = (B + kPsTile - 1) / kPsTile;
   const int64_t t0 = s * tiles / S, t1 = (s + 1) * tiles / S;
   // the logistic weights W'[o, (i, j)] of the group's inputs (a / b sums)
-  for (int q = tid; LOG && q < ni * out * NB; q += 256) {
-    const int ig = q / (out * NB), o = (q / NB) % out, j = q % NB;
+  for (int q = tid; LOG && q < ni * out * NBP; q += 256) {
+    const int ig = q / (out * NBP), o = (q / NBP) % out, j = q % NBP;
     const float ls = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
-    wl[q] = (kl.logistic_weight[(int64_t)o * in * NB + (i0 + ig) * NB + j] * kl.scale_logistic) * ls;
+    wl[q] = j < NB ? (kl.logistic_weight[(int64_t)o * in * NB + (i0 + ig) * NB + j] * kl.scale_logistic) * ls : 0.f;
   }
   // the group's knots, reciprocal spans (bspline_vals_derivs_rk's layout) and logistic parameters
   for (int q = tid; q < ni * NG; q += 256) kn[q] = kl.grid[(int64_t)(i0 + q / NG) * NG + q % NG];
@@ -767,12 +768,19 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
       float gph[NL];
 #pragma unroll
       for (int j = 0; j < NL; ++j) gph[j] = 0.f;
-      for (int o = 0; o < out; ++o) {  // d loss / d phi_j = sum_o g[o] W'[o, (i, j)]
+      for (int o = 0; o < out; ++o) {  // d loss / d phi_j = sum_o g[o] W'[o, (i, j)], W' row as float4s
         const float go = gt[frr * GS + o];
-        const float* wr = wl + (fig * out + o) * NB;
+        const float4* wr = reinterpret_cast<const float4*>(wl + (fig * out + o) * NBP);
 #pragma unroll
-        for (int j = 0; j < NL; ++j)
-          if (j < NB) gph[j] += go * wr[j];
+        for (int jq = 0; jq < NL / 4; ++jq) {
+          if (4 * jq < NB) {
+            const float4 w4 = wr[jq];
+            gph[4 * jq] += go * w4.x;
+            gph[4 * jq + 1] += go * w4.y;
+            gph[4 * jq + 2] += go * w4.z;
+            gph[4 * jq + 3] += go * w4.w;
+          }
+        }
       }
 #pragma unroll
       for (int j = 0; j < NL; ++j) {
