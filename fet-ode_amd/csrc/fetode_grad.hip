@@ -1181,7 +1181,7 @@ __global__ void ferro_gp_kernel(fetode_ferro_t fl, const float* __restrict__ x, 
 // ferro_gp_reduce_kernel adds the splits in order (run-to-run identical).  The hysteresis input of
 // row r: rows < n0 read p0 (or reinit: x itself), later rows the row n0 earlier (the previous
 // evaluation of the same trajectory, fieldn's tape layout (n_ev, B, in)).
-constexpr int kFgTarget = 8192, kFgChunk = 4;  // workgroups per launch; elements per workgroup
+constexpr int kFgTarget = 8192, kFgChunk = 6;  // workgroups per launch; elements per workgroup
 int fg_units(const fetode_ferro_t* fl) {
   return fl->in_dim * fl->out_dim * ((fl->num_basis + kFgChunk - 1) / kFgChunk);
 }
