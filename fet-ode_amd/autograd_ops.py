@@ -335,14 +335,27 @@ def _handle_key(model, B, device):
     only pointers and shapes, so it is reused while every tensor keeps its storage; the plan holds
     the parameter VALUES and is rebuilt when a version counter or the optimizer-step generation
     (_lib.param_generation: fused optimizers do not bump version counters) changes."""
+    ts = _field_tensors(model)
     key = [B, device]
     vkey = [_lib.param_generation()]
-    for t in _field_tensors(model):
-        if t.dtype != torch.float32 or not t.is_contiguous():
-            return None
-        key += [t.data_ptr(), t.shape[0]]
-        vkey.append(t._version)
-    return tuple(key), tuple(vkey)
+    kapp, vapp = key.append, vkey.append
+    for t in ts:
+        kapp(t.data_ptr())
+        kapp(t.shape[0])
+        vapp(t._version)
+    key = tuple(key)
+    # dtype / layout are checked when the key is new (a descriptor is built for it): a tensor that
+    # keeps its storage and leading size keeps its dtype, and parameters are not restrided in
+    # place (an in-place t_() of a square parameter would go unnoticed here)
+    cached = model.__dict__.get("_fetode_keyok")
+    if cached is None or cached[0] != key:
+        ok = all(t.dtype == torch.float32 and t.is_contiguous() for t in ts)
+        model.__dict__["_fetode_keyok"] = (key, ok)
+    elif not cached[1]:
+        ok = False
+    else:
+        ok = True
+    return (key, tuple(vkey)) if ok else None
 
 
 def make_handle(model, B: int, device) -> _lib.FieldHandle:

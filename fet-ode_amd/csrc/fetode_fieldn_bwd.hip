@@ -221,21 +221,6 @@ __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_
   float(&ak)[4][kFbMaxD] = s_ak[wid][t];
   float(&acs)[4][3] = s_ac[wid];
   const bool dl = own && o < D, hl = o < H;
-  // the layer inputs of evaluation e from the tape (e = -1: the hysteresis input of evaluation 0,
-  // the state before the solve or the reinit rule); lanes that do not own the value read nothing
-  auto ldx = [&](int64_t e) -> float {
-    if (!(dl && live) || e < -1) return 0.f;
-    if (e >= 0) return X[(e * a.B + bi) * D + o];
-    return (a.init_mask & 1u) ? X[bi * D + o] : (FERRO ? a.state0[bi * D + o] : 0.f);
-  };
-  auto ldh = [&](int64_t e) -> float {
-    if (!(hl && live) || e < -1) return 0.f;
-    if (e >= 0) return Hh[(e * a.B + bi) * H + o];
-    return (a.init_mask & 2u) ? Hh[bi * H + o] : (FERRO ? a.state0[a.B * D + bi * H + o] : 0.f);
-  };
-  // this evaluation's (x, prev x, h, prev h); evaluation ev - 1's inputs are ev's prev, so each
-  // evaluation loads only ev - 2's, one evaluation ahead (the tape's latency off the chain)
-  float cx = ldx(n_ev - 1), cpx = ldx(n_ev - 2), ch = ldh(n_ev - 1), cph = ldh(n_ev - 2);
   float ay1 = 0.f, ay = 0.f;  // adjoint of y at the end of the current step (lanes < D)
   int jj = a.T - 1;
   for (int s = a.n_steps - 1; s >= 0; --s) {
@@ -266,13 +251,20 @@ __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_
         for (int j = 0; j < 3; ++j) acs[i][j] = ac[i][j];
     for (int st = ns - 1; st >= 0; --st) {
       const int64_t ev = (int64_t)s * ns + st;
-      const float n2x = ldx(ev - 2), n2h = ldh(ev - 2);  // the next evaluation's prev, in flight
       if (dl) {
-        xs[o] = cx;
-        ps[o] = cpx;
+        const float x = live ? X[(ev * a.B + bi) * D + o] : 0.f;
+        xs[o] = x;
+        ps[o] = !live ? 0.f
+                : ev > 0 ? X[((ev - 1) * a.B + bi) * D + o]
+                         : ((a.init_mask & 1u) ? x : (FERRO ? a.state0[bi * D + o] : 0.f));
         gk[o] = ak[st][o];
       }
-      const float h = ch, ph = cph;
+      float h = 0.f, ph = 0.f;
+      if (hl && live) {
+        h = Hh[(ev * a.B + bi) * H + o];
+        ph = ev > 0 ? Hh[((ev - 1) * a.B + bi) * H + o]
+                    : ((a.init_mask & 2u) ? h : (FERRO ? a.state0[a.B * D + bi * H + o] : 0.f));
+      }
       fb_wsync();
       // layer 1 (h -> k): d loss / d h_o on lane o
       // (split: each group its half of the outputs, then the two halves' sum on both)
@@ -297,10 +289,6 @@ __global__ __launch_bounds__(LDSP ? 64 * kFbWavesL : 64 * kFbWaves) void fieldn_
         ay += gx;
         for (int j = 0; j < st; ++j) ak[j][o] = ffma(acs[st][j], gx, ak[j][o]);
       }
-      cx = cpx;  // evaluation ev - 1: its inputs are ev's prev, its prev the prefetched ev - 2
-      ch = cph;
-      cpx = n2x;
-      cph = n2h;
       fb_wsync();
     }
     ay1 = ay;
