@@ -1630,14 +1630,17 @@ __global__ __launch_bounds__(DOPRI ? 64 : (LDSP ? 64 * kFnWavesL : 64 * kFnWaves
   }
   // trajectories per wave: lane = (slot t, split group sg, unit o) with U = pow2 >= max(H, D) unit
   // lanes and SF split groups per slot (KANFET([2, 16, 2]): two trajectories per wave, 2 x 16
-  // lanes each); the resident dopri5 keeps one trajectory per wave, unsplit
+  // lanes each); the resident dopri5 keeps one trajectory per wave (SF groups of 64 / SF lanes)
   constexpr int MT = DOPRI ? 1 : kFnMaxT;
   __shared__ float s_x[NW][MT][kFnMaxD], s_k[NW][MT][kFnMaxD], s_p0[NW][MT][kFnMaxD];
   const int wid = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const LayerPlan& P0 = a.P0;
   const LayerPlan& P1 = a.P1;
   const int D = P0.in, H = P0.out;
-  const int U = DOPRI ? 64 : fn_unit_lanes(D, H), SF = DOPRI ? 1 : fn_split(D, H), HP = U * SF, TPW = 64 / HP;
+  // the resident dopri5 keeps one trajectory per wave but splits it as well: SF groups of 64 / SF
+  // lanes (lanes o >= H of a group add exact zeros to its butterfly, so the sums are the fixed-grid
+  // launch's bit for bit — the host-loop and resident solves stay comparable)
+  const int SF = fn_split(D, H), U = DOPRI ? 64 / SF : fn_unit_lanes(D, H), HP = U * SF, TPW = 64 / HP;
   const int t = lane / HP, sg = (lane & (HP - 1)) / U, o = lane & (U - 1);
   const bool own = sg == 0;  // the group that owns the trajectory's state and writes
   const int64_t b = ((int64_t)blockIdx.x * NW + wid) * TPW + t;
@@ -1694,7 +1697,7 @@ __global__ __launch_bounds__(DOPRI ? 64 : (LDSP ? 64 * kFnWavesL : 64 * kFnWaves
       h = c0o + (pe + po);
     }
     if (tx && valid && own && hl) th_[(ev * a.B + b) * H + o] = h;
-    if (TAPE && trow && hl) trow[D + o] = h;
+    if (TAPE && trow && own && hl) trow[D + o] = h;
     ++ev;
     fn_wsync();
     if (FERRO && own && o < D) p0[o] = xs[o];  // ferro_class.py:409
