@@ -690,7 +690,8 @@ __global__ __launch_bounds__(256) void kan_psum_kernel(fetode_kanlinear_t kl, co
     const float ls = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
     wl[q] = j < NB ? (kl.logistic_weight[(int64_t)o * in * NB + (i0 + ig) * NB + j] * kl.scale_logistic) * ls : 0.f;
   }
-  // the group's knots, reciprocal spans (bspline_vals_derivs_rk's layout) and logistic parameters
+  // the group's knots, 1 / knot steps, basis cubics (bpoly_entry, from the launch's table) and
+  // logistic parameters
   for (int q = tid; q < ni * NG; q += 256) kn[q] = kl.grid[(int64_t)(i0 + q / NG) * NG + q % NG];
   for (int q = tid; q < ni * (NG - 1); q += 256) {
     const float* gg = kl.grid + (int64_t)(i0 + q / (NG - 1)) * NG;
@@ -875,7 +876,7 @@ __global__ __launch_bounds__(256) void kan_psum_rows_kernel(fetode_kanlinear_t k
   const int in = kl.in_features, NB = kl.num_logistic;
   const int NG = kl.grid_size + 2 * SO + 1, NS = kl.grid_size + SO, NF = 1 + NS + NB;
   const int i = blockIdx.x, sp = blockIdx.y, S = gridDim.y, tid = threadIdx.x;
-  // input i's tables: W'[o, (i, j)], knots, reciprocal spans (bspline_vals_derivs_rk), logistic
+  // input i's tables: W'[o, (i, j)], knots, 1 / knot steps, basis cubics (bpoly_entry), logistic
   for (int q = tid; q < OUT * NB; q += 256) {
     const int o = q / NB, j = q % NB;
     const float ls = kl.logistic_scaler ? kl.logistic_scaler[o] : 1.0f;
