@@ -342,11 +342,12 @@ def _handle_key(model, B, device):
     for t in ts:
         kapp(t.data_ptr())
         kapp(t.shape[0])
+        kapp(t.dtype)
+        kapp(t.stride())
         vapp(t._version)
     key = tuple(key)
-    # dtype / layout are checked when the key is new (a descriptor is built for it): a tensor that
-    # keeps its storage and leading size keeps its dtype, and parameters are not restrided in
-    # place (an in-place t_() of a square parameter would go unnoticed here)
+    # dtype / layout are in the key (cheap attribute reads), so a restride (t_(), as_strided_) or a
+    # set_() onto another dtype at the same address makes a new key, which is checked here once
     cached = model.__dict__.get("_fetode_keyok")
     if cached is None or cached[0] != key:
         ok = all(t.dtype == torch.float32 and t.is_contiguous() for t in ts)

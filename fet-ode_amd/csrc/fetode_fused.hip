@@ -99,7 +99,7 @@ __device__ void xrank_comm(const DopriParams& P) {
           break;
         }
         __builtin_amdgcn_s_sleep(1);
-        if (++spins == kXrSpinLimit) {
+        if (++spins == (P.spin_limit ? P.spin_limit : kXrSpinLimit)) {
           __hip_atomic_store(abw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           stop = 1;
           break;
@@ -133,7 +133,7 @@ __device__ void xrank_comm(const DopriParams& P) {
           ab = 1;
           break;
         }
-        if (++spins == kXrSpinLimit) {
+        if (++spins == (P.spin_limit ? P.spin_limit : kXrSpinLimit)) {
           __hip_atomic_store(abw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           ab = 1;
           break;
@@ -1499,6 +1499,7 @@ int64_t g_small_max = [] {
   return e ? (int64_t)atoll(e) : (int64_t)512;  // measured switch point (tools/diag/batch_sweep.py)
 }();
 int64_t small_max() { return g_small_max; }
+uint32_t g_dp_spin_limit = 0;   // fetode_dopri5_set_spin_limit (0: the built-in limits)
 
 const FusedEntry* find_fused(const fetode_field_t* f) {
   if (f->n_layers != 2) return nullptr;
@@ -1986,6 +1987,12 @@ int fetode_debug_stamp_buffer(void* p) {
 }
 #endif
 
+uint32_t fetode_dopri5_set_spin_limit(uint32_t polls) {
+  const uint32_t prev = g_dp_spin_limit;
+  g_dp_spin_limit = polls;
+  return prev;
+}
+
 int64_t fetode_fused_set_small_batch_max(int64_t b) {
   const int64_t prev = g_small_max;
   if (b >= 0) g_small_max = b;
@@ -2123,6 +2130,7 @@ static int dopri5_launch(const fetode_field_t* f, const void* plan, const float*
   a.tape = tape_cap > 0 ? tape : nullptr;
   DopriParams& P = a.dp;
   P.on = 1;
+  P.spin_limit = g_dp_spin_limit;
   P.tape_cap = tape_cap;
   P.init_rec = init_rec;
   P.t = t;
@@ -2243,10 +2251,12 @@ int64_t fetode_xrank_inbox_bytes(int32_t world) {
 int fetode_xrank_alloc(int64_t bytes, void** dev_ptr, void* handle) {
   if (bytes <= 0 || !dev_ptr || !handle) return set_err(FETODE_EINVAL, "xrank alloc: bad argument");
   void* p = nullptr;
-  // fine-grained device memory: coherent for the system-scope stores / loads of the exchange
+  // fine-grained device memory: coherent for the system-scope stores / loads of the exchange.  No
+  // coarse-grained fallback: a peer spinning on coarse-grained IPC memory is not guaranteed to see
+  // remote stores, so without it the caller declines the resident sharded path on every rank
   if (hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocFinegrained) != hipSuccess || !p) {
-    (void)hipGetLastError();
-    HIP_CHECK_RET(hipMalloc(&p, (size_t)bytes));
+    const hipError_t e = hipGetLastError();
+    return set_err(FETODE_EUNSUPPORTED, "xrank alloc: no fine-grained device memory (%s)", hipGetErrorString(e));
   }
   HIP_CHECK_RET(hipMemset(p, 0, (size_t)bytes));
   hipIpcMemHandle_t h;

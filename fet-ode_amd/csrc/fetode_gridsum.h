@@ -37,6 +37,9 @@ struct DopriParams {
   // two layer inputs and the output of the first tape_cap evaluations; the initial-step scalars
   int64_t tape_cap;
   double* init_rec;    // {d0, d1, d2, h0, h1} of _select_initial_step, or null
+  // polls before a spin gives up (status 4); 0 = kDpSpinLimit / kXrSpinLimit.  A test knob
+  // (fetode_dopri5_set_spin_limit): a tiny limit forces the timeout path on a healthy grid
+  uint32_t spin_limit;
 };
 
 // the smallest power-of-two leaf length that needs <= kDpGroups leaves over nb workgroups
@@ -188,7 +191,7 @@ __device__ inline bool grid_sum2(const DopriParams& P, unsigned& round, double v
         ab = 1;
         break;
       }
-      if (++spins == (xr ? kXrSpinLimit : kDpSpinLimit)) {
+      if (++spins == (P.spin_limit ? P.spin_limit : (xr ? kXrSpinLimit : kDpSpinLimit))) {
         __hip_atomic_store(abw, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         ab = 1;
         break;

@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kKThreads) void kuramoto_fwd_kernel(const float* __
   }
 }
 
-// ---- lane-per-column kernels (W <= 32, H = HM rows): no LDS, no barriers -------------------------
+// ---- lane-per-column kernels (W < 32, H = HM rows): no LDS, no barriers ---------------------------
 // A wave holds two images: lanes 32 i + c (c < W) own column c of image 2 w + i, the column's H
 // phases (and omega) in registers.  Vertical neighbours are the neighbouring registers; horizontal
 // ones come from the neighbouring lanes by DPP wave shifts (wave_shr:1 = lane - 1, wave_shl:1 =
@@ -854,7 +854,7 @@ int fetode_kuramoto_forward(const float* x, int64_t B, int32_t H, int32_t W, int
   if (!x || !K || !omega || !feat) return set_err(FETODE_EINVAL, "kuramoto: null pointer");
   if (H <= 0 || W <= 0 || H * W > kMaxPix || steps < 0)
     return set_err(FETODE_EINVAL, "kuramoto: H*W=%d (1..%d), steps=%d", H * W, kMaxPix, steps);
-  if (H == 28 && W <= 32 && !kura_lds_forced()) {  // lane per column (MNIST 28 x 28)
+  if (H == 28 && W < 32 && !kura_lds_forced()) {  // lane per column (MNIST 28 x 28); lane 31 of each image stays empty
     const unsigned grid = (unsigned)((B + 2 * kLaneWaves - 1) / (2 * kLaneWaves));
     hipLaunchKernelGGL(kuramoto_fwd_lanes_kernel<28>, dim3(grid), dim3(64 * kLaneWaves), 0, (hipStream_t)stream, x, B,
                        W, steps, dt, K, omega, feat, tape);
@@ -891,7 +891,7 @@ int fetode_kuramoto_backward(int64_t B, int32_t H, int32_t W, int32_t steps, flo
   float* gom_part = gomega ? (float*)workspace : nullptr;
   float* gK_part = gK ? (float*)workspace + B * HW : nullptr;
   hipStream_t s = (hipStream_t)stream;
-  if (H == 28 && W <= 32 && !kura_lds_forced()) {
+  if (H == 28 && W < 32 && !kura_lds_forced()) {
     const unsigned grid = (unsigned)((B + 2 * kLaneWaves - 1) / (2 * kLaneWaves));
     hipLaunchKernelGGL(kuramoto_bwd_lanes_kernel<28>, dim3(grid), dim3(64 * kLaneWaves), 0, s, B, W, steps, dt, K, tape,
                        gfeat, gx, gK_part, gom_part);

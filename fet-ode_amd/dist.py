@@ -137,7 +137,12 @@ class XRank:
     peer's inbox mapped into this process, as a device array of pointers the kernel's exchange
     workgroup writes through (remote stores over xGMI).  One per (group, device); created
     collectively (all_gather of the 64-byte IPC handles) the first time a sharded resident solve
-    runs.  Mappings live until the process exits."""
+    runs.  Mappings live until the process exits.
+
+    Fail-safe: the inbox must be fine-grained device memory (fetode_xrank_alloc refuses a
+    coarse-grained fallback) and every peer's inbox must map.  Both outcomes are agreed over the
+    group, so ``ok`` is the same on every rank: when it is False every rank declines the resident
+    sharded path and takes the host-driven loop (one all-reduce per attempt) together."""
 
     _cache: dict = {}
 
@@ -159,22 +164,36 @@ class XRank:
             raise ValueError(f"sharded resident dopri5: world size {self.world} not supported")
         ptr = ctypes.c_void_p()
         handle = (ctypes.c_uint8 * 64)()
+        self.ok, self.reason = False, None
+        self.inbox, self.peers, self.epoch = None, None, 0
         with torch.cuda.device(device):
-            _lib.check(lib.fetode_xrank_alloc(nbytes, ctypes.byref(ptr), handle), "fetode_xrank_alloc")
+            rc = lib.fetode_xrank_alloc(nbytes, ctypes.byref(ptr), handle)
+            mine = bytes(handle) if rc == _lib.FETODE_OK else None
+            if mine is None:
+                self.reason = _lib.last_error()
             handles = [None] * self.world
-            dist.all_gather_object(handles, bytes(handle), group=group)
-            peers = []
-            for j, h in enumerate(handles):
-                if j == self.rank:
-                    peers.append(ptr.value)
-                    continue
-                hb = (ctypes.c_uint8 * 64).from_buffer_copy(h)
-                q = ctypes.c_void_p()
-                _lib.check(lib.fetode_xrank_open(hb, ctypes.byref(q)), "fetode_xrank_open")
-                peers.append(q.value)
+            dist.all_gather_object(handles, mine, group=group)   # reached by every rank, failed or not
+            opened, ok_open = [], mine is not None and all(h is not None for h in handles)
+            if ok_open:
+                for j, h in enumerate(handles):
+                    if j == self.rank:
+                        opened.append(ptr.value)
+                        continue
+                    hb = (ctypes.c_uint8 * 64).from_buffer_copy(h)
+                    q = ctypes.c_void_p()
+                    if lib.fetode_xrank_open(hb, ctypes.byref(q)) != _lib.FETODE_OK:
+                        self.reason = _lib.last_error()
+                        ok_open = False
+                        break
+                    opened.append(q.value)
+            flags = [None] * self.world
+            dist.all_gather_object(flags, bool(ok_open), group=group)
+        if not all(flags):
+            self.reason = self.reason or "a peer could not allocate or map its inbox"
+            return
+        self.ok = True
         self.inbox = ptr.value
-        self.peers = torch.tensor(peers, dtype=torch.int64, device=device)
-        self.epoch = 0
+        self.peers = torch.tensor(opened, dtype=torch.int64, device=device)
 
     def desc(self, b_offset: int):
         from . import _lib

@@ -457,12 +457,14 @@ def _try_field_resident(func, y0, tp, reversed_, rtol, atol, options):
         from . import dist as D
         grp = None if group == "world" else group
         ok = (D._RESIDENT_SHARDED[0] and bool(lib.fetode_fused_supported(handle.ref))
-              and B <= lib.fetode_integrate_dopri5_max_batch(handle.ref, 1))
+              and 0 < B <= lib.fetode_integrate_dopri5_max_batch(handle.ref, 1))
         agreed = D.resident_agreement(grp, dev, B, ok)
         if agreed is None:
             return None
         B_total, b_off = agreed
         xr = D.XRank.get(grp, dev)
+        if not xr.ok:   # agreed over the group: every rank takes the host loop
+            return None
     elif B > lib.fetode_integrate_dopri5_max_batch(handle.ref, 0):
         # no resident solver for this shape / batch: decide BEFORE pack_state, which rebinds the
         # layers' prev_x to the fused state buffer (a declined launch would leave them there and
@@ -574,8 +576,12 @@ class _FusedDopri5Fn(torch.autograd.Function):
                 tape.data_ptr(), cap, init_rec.data_ptr(), _lib.stream_handle(dev)),
                 "fetode_integrate_dopri5_tape")
             nfev, n_att, status = stats.tolist()
-            if status != 0 and state is not None:   # every failure leaves the pre-solve memory
+            if status == 4 and state is not None:
+                # a grid timeout leaves the pre-solve memory (the caller may rerun on the host loop);
+                # torchdiffeq's own assertions (1-3) keep the last evaluation's, as the reference's
+                # prev_x does when they fire — the same rule as _raise_status on the inference paths
                 state.copy_(state0)
+            if status != 0 and state is not None:
                 unpack_state(field, state)
             _raise_status(status, "fetode_integrate_dopri5_tape: a grid reduction timed out (workgroups not "
                                   "co-resident); the solution is invalid")
@@ -712,6 +718,8 @@ def _try_wide_resident(func, y0, tp, reversed_, rtol, atol, options):
         return None
     if D != k0.in_features or k1.in_features != H or k1.out_features != D or f0.num_basis != f1.num_basis:
         ok = False
+    if B <= 0:   # an empty shard votes no: every rank then falls back to the host loop together
+        ok = False
     if torch.is_grad_enabled() and (y0.requires_grad or any(p.requires_grad for p in field.parameters())):
         ok = False
     e0 = e1 = None
@@ -729,6 +737,8 @@ def _try_wide_resident(func, y0, tp, reversed_, rtol, atol, options):
             return None
         B_total, b_off = agreed
         xr = Dd.XRank.get(grp, dev)
+        if not xr.ok:   # agreed over the group: every rank takes the host loop
+            return None
         ws_bytes = lib.fetode_wide_dopri5_xrank_workspace(B, B_total, b_off, D, H)
     elif not ok:
         return None

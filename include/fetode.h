@@ -98,6 +98,12 @@ const char* fetode_last_error(void);
  * hipLaunchCooperativeKernel (env FETODE_COOPERATIVE=1).  A grid that is not co-resident ends
  * in status 4 (bounded spins), never a hang.  mode < 0 queries.  Returns the previous mode. */
 int32_t fetode_resident_launch_mode(int32_t mode);
+/* Test knob of the resident dopri5 solvers (fetode_integrate_dopri5[_xrank|_tape]): polls of one
+ * grid-reduction / cross-rank spin before it gives up with status 4 (0 = the built-in limits,
+ * ~1 s single device, ~16 s across ranks).  A tiny limit forces the timeout path on a healthy
+ * grid (tests/test_gpu_dopri5.py: the pre-solve hysteresis state is restored).  Returns the
+ * previous value.  Process-wide. */
+uint32_t fetode_dopri5_set_spin_limit(uint32_t polls);
 int fetode_abi_version(void);
 
 /* Size in bytes of the packed "plan" (pre-transformed parameters). */

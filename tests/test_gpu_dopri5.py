@@ -281,3 +281,54 @@ def test_dopri5_resident_falls_back_beyond_one_grid(dev):
     with torch.no_grad():
         sol = F.odeint(F.autonomous(m), y0, torch.tensor([0.0, 0.1], dtype=torch.float64), rtol=1e-3, atol=1e-4)
     assert torch.isfinite(sol).all() and not isinstance(F.dopri5.dopri5_solve.last, ResidentSolve)
+
+
+@pytest.mark.parametrize("B", [64, 4096])
+def test_dopri5_resident_timeout_restores_state(dev, B):
+    """The timeout path on a healthy grid (fetode_dopri5_set_spin_limit(1): the first poll that
+    does not find its reduction complete gives up): the resident solve raises RuntimeError
+    (status 4) and `_restorer` puts the hysteresis memory back to its pre-solve value, so the
+    caller can rerun — here on the host loop — and get exactly what the host loop gives from the
+    untouched state.  Then the limit is restored and the resident solve works again."""
+    import fet_ode_amd as F
+    from fet_ode_amd import _lib
+    from fet_ode_amd.dopri5 import ResidentSolve, set_resident_dopri5
+    lib = _lib.load()
+    g = load_golden("traj_kanfet")
+    y0 = torch.from_numpy(g["y0_B64"]).repeat(64, 1)[:B].to(dev)
+    t = torch.tensor([0.0, 0.2, 0.5], dtype=torch.float64)
+
+    def model():
+        m = F.KANFET([2, 10, 2], grid_size=5)
+        m.load_state_dict(golden_sd(g))
+        m = m.to(dev)
+        with torch.no_grad():   # a carried (non-fresh) hysteresis state before the solve under test
+            F.odeint(F.autonomous(m), y0, torch.tensor([0.0, 0.05], dtype=torch.float64), method="rk4")
+        return m
+
+    m = model()
+    before = [l.ferro._prev.clone() for l in m.layers]
+    prev = lib.fetode_dopri5_set_spin_limit(1)
+    try:
+        with torch.no_grad(), pytest.raises(RuntimeError, match="timed out"):
+            F.odeint(F.autonomous(m), y0, t, rtol=1e-3, atol=1e-4)
+            torch.cuda.synchronize(dev)
+    finally:
+        lib.fetode_dopri5_set_spin_limit(prev)
+    for a, b in zip(before, [l.ferro._prev for l in m.layers]):
+        assert torch.equal(a, b), "the pre-solve hysteresis state must survive a timed-out solve"
+    # the caller's retry on the host loop == the host loop on a fresh copy of the same state
+    pr = set_resident_dopri5(False)
+    try:
+        with torch.no_grad():
+            retry = F.odeint(F.autonomous(m), y0, t, rtol=1e-3, atol=1e-4).cpu()
+            m2 = model()
+            clean = F.odeint(F.autonomous(m2), y0, t, rtol=1e-3, atol=1e-4).cpu()
+    finally:
+        set_resident_dopri5(pr)
+    assert torch.equal(retry, clean)
+    for a, b in zip([l.ferro._prev for l in m.layers], [l.ferro._prev for l in m2.layers]):
+        assert torch.equal(a, b)
+    with torch.no_grad():
+        sol = F.odeint(F.autonomous(m2), y0, t, rtol=1e-3, atol=1e-4)
+    assert isinstance(F.dopri5.dopri5_solve.last, ResidentSolve) and torch.isfinite(sol).all()

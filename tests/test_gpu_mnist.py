@@ -87,37 +87,48 @@ def test_production_size_vs_oracle(dev):
         close(p.grad, ps[n].grad, 5e-4, "grad " + n)
 
 
-def test_kuramoto_lane_kernels_match_lds_kernels(dev):
+@pytest.mark.parametrize("W", [28, 31, 32])
+def test_kuramoto_lane_kernels_match_lds_kernels(dev, W):
     """The 28 x 28 production shape runs the lane-per-column Kuramoto kernels (registers + DPP wave
     shifts, no LDS); the workgroup-per-image LDS kernels (fetode_kuramoto_set_lds(1)) are the other
     implementation of the same per-pixel arithmetic and tap order: features, the tape, d/dx and
     d/domega bitwise equal, d/dK (a per-image sum in another order) to 1e-6.  An odd batch leaves
-    the last wave's second image empty."""
+    the last wave's second image empty.  W = 31 is the widest lane shape (lane 31 of each image
+    stays empty); W = 32 would put the two images of a wave next to each other across the DPP
+    shifts, so it takes the LDS kernels — checked here by images that do not couple: every image
+    of the batch equals the same image integrated alone."""
     from fet_ode_amd import _lib, mnist
     lib = _lib.load()
     torch.manual_seed(5)
-    m = mnist.Kuramoto2D(H=28, W=28, steps=10, dt=0.15)
+    m = mnist.Kuramoto2D(H=28, W=W, steps=10, dt=0.15)
     with torch.no_grad():
         m.omega.normal_(0, 0.3)
         m.K.fill_(0.8)
     sd = {k: v.clone() for k, v in m.state_dict().items()}
-    x = torch.rand(37, 1, 28, 28, generator=torch.Generator().manual_seed(6))
-    w = torch.randn(37, 2 * 784, generator=torch.Generator().manual_seed(7))
+    x = torch.rand(37, 1, 28, W, generator=torch.Generator().manual_seed(6))
+    w = torch.randn(37, 2 * 28 * W, generator=torch.Generator().manual_seed(7))
     out = []
     prev = lib.fetode_kuramoto_set_lds(-1)
     try:
         for lds in (0, 1):
             lib.fetode_kuramoto_set_lds(lds)
-            mm = mnist.Kuramoto2D(H=28, W=28, steps=10, dt=0.15)
+            mm = mnist.Kuramoto2D(H=28, W=W, steps=10, dt=0.15)
             mm.load_state_dict(sd)
             mm = mm.to(dev)
             xg = x.to(dev).requires_grad_(True)
             y = mm(xg)
             (y.reshape(37, -1) * w.to(dev)).sum().backward()
             out.append((y.detach().cpu(), xg.grad.cpu(), mm.omega.grad.cpu(), mm.K.grad.cpu()))
+        lib.fetode_kuramoto_set_lds(0)
+        mm = mnist.Kuramoto2D(H=28, W=W, steps=10, dt=0.15)
+        mm.load_state_dict(sd)
+        mm = mm.to(dev)
+        with torch.no_grad():
+            alone = torch.cat([mm(x[i:i + 1].to(dev)).cpu() for i in range(4)])
     finally:
         lib.fetode_kuramoto_set_lds(prev)
     (y0, gx0, go0, gk0), (y1, gx1, go1, gk1) = out
     assert torch.equal(y0, y1)
     assert torch.equal(gx0, gx1) and torch.equal(go0, go1)
     close(gk0, gk1, 1e-6, "grad K")
+    assert torch.equal(alone, y0[:4]), "images of one wave must not couple"

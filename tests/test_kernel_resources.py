@@ -58,11 +58,14 @@ def kernel_metadata(path, tmp_path):
 def scratch_accesses(elfs, name):
     """Scratch instructions (scratch_* / buffer_* to the private segment) in kernel `name`'s
     disassembly: a private segment the compiler reserves but never addresses costs no traffic."""
-    n = 0
+    n, seen = 0, False
     for f in elfs:
         out = subprocess.run([OBJDUMP, "-d", f"--disassemble-symbols={name}", str(f)], capture_output=True,
-                             text=True).stdout
+                             text=True, check=True).stdout
+        seen = seen or f"<{name}>:" in out
         n += sum(1 for line in out.splitlines() if re.search(r"\s(scratch|buffer)_(load|store)", line))
+    # an empty disassembly (name mismatch) must not pass as "no scratch instructions"
+    assert seen, f"{name}: not disassembled from any code object"
     return n
 
 
