@@ -217,40 +217,98 @@ __device__ __forceinline__ f2 rcpx2(f2 v) { return f2{rcp(v.x), rcp(v.y)}; }
 template <int IN, int FLEN>
 struct V4Lds {
   float F[FLEN];  // per input NFP floats: SiLU, logistic 0..NB-1 (2x folded into weights), zero pad
-  float4 G[IN];   // x, w = wc*(1-up), e = exp2(gs*log2e*x), u
+  // per input {e = exp2(gs*log2e*x), w = wc*(1-up)} and {x, pad}: each packed operand of a pair is
+  // the low or high half of a loaded register pair (op_sel broadcasts, no moves)
+  float4 G[IN];
   int M[IN];      // knot interval (NI = zero table row)
   float sink;     // target of idle feature jobs
 };
+// the two register pairs of input i ({e, w}, {x, pad}); the empty asm keeps each a loaded pair
+template <int IN, int FLEN>
+__device__ __forceinline__ void v4_g(const V4Lds<IN, FLEN>& L, int i, f2& ew, f2& xp) {
+  const f2* g2 = reinterpret_cast<const f2*>(&L.G[i]);
+  ew = g2[0];
+  xp = g2[1];
+  asm volatile("" : "+v"(ew), "+v"(xp));
+}
 
 // one Ferro element pair of one input: acc += cps * tanh(k (x - Ec m)) for both
 template <bool FACT>
-__device__ __forceinline__ f2 v4_pair(float4 g, f2 ep, f2 k2, f2 kE, f2 cp, f2 acc, float gsl2e) {
+__device__ __forceinline__ f2 v4_pair(f2 ew, f2 xp, f2 ep, f2 k2, f2 kE, f2 cp, f2 acc, float gsl2e) {
   f2 s;
   if constexpr (FACT) {
-    s = rcpx2(pfma(splat(g.z), ep, splat(1.0f)));               // sigma(gs(-x-Ec)), factored exp
+    s = rcpx2(pfma(splat(ew.x), ep, splat(1.0f)));              // sigma(gs(-x-Ec)), factored exp
   } else {
-    s = rcpx2(ex2x2(pfma(splat(gsl2e), splat(g.x), ep)) + splat(1.0f));
+    s = rcpx2(ex2x2(pfma(splat(gsl2e), splat(xp.x), ep)) + splat(1.0f));
   }
-  const f2 m = pfma(splat(g.y), s, splat(1.0f));                  // 1 - 2(1-a)(1-u) sigma
-  const f2 z = pfma(kE, m, k2 * splat(g.x));                      // 2 log2e k (x - Ec m)
+  const f2 m = pfma(splat(ew.y), s, splat(1.0f));                 // 1 - 2(1-a)(1-u) sigma
+  const f2 z = pfma(kE, m, k2 * splat(xp.x));                     // 2 log2e k (x - Ec m)
   const f2 th = pfma(rcpx2(ex2x2(z) + splat(1.0f)), splat(-2.0f), splat(1.0f));
   return pfma(cp, th, acc);
 }
 
-// the edge sum of one lane: NPL Ferro pairs, FPL feature weights, and (spl) the spline edge of
-// input `si` (sp_o = the layer's LDS cubic table at output o)
-template <int IN, int FLEN, int NI, int NPL, int FPL, bool FERRO, bool FACT>
-__device__ __forceinline__ float v4_edges(const V4Lds<IN, FLEN>& L, const float* sp_o, const int* gi, const f2* ep,
-                                          const f2* k2, const f2* kE, const f2* cp, const f2* fw, int fofs,
-                                          bool spl, int si, float gsl2e) {
-  // spline operands first (two dependent LDS reads), so their latency hides under the pairs
-  const float u = L.G[si].w;
-  const float4 cf = *reinterpret_cast<const float4*>(&sp_o[(si * (NI + 1) + L.M[si]) * 4]);
-  f2 acc = splat(0.0f);
-  if constexpr (FERRO) {
-#pragma unroll
-    for (int r = 0; r < NPL; ++r) acc = v4_pair<FACT>(L.G[gi[r]], ep[r], k2[r], kE[r], cp[r], acc, gsl2e);
+// one Ferro element (the single leftover of a layer's pair split): acc + cps * tanh(...)
+template <bool FACT>
+__device__ __forceinline__ float v4_single(f2 ew, f2 xp, float ep, float k2, float kE, float cp, float acc,
+                                           float gsl2e) {
+  float s;
+  if constexpr (FACT) {
+    s = rcp(ffma(ew.x, ep, 1.0f));
+  } else {
+    s = rcp(ex2(ffma(gsl2e, xp.x, ep)) + 1.0f);
   }
+  const float m = ffma(ew.y, s, 1.0f);
+  const float z = ffma(kE, m, k2 * xp.x);
+  const float th = ffma(rcp(ex2(z) + 1.0f), -2.0f, 1.0f);
+  return ffma(cp, th, acc);
+}
+
+// Ferro element split of one layer's output over a lane group: NPAIR element pairs (i, k), (i, k+1)
+// over `lanes` lanes.  When the remainder of pairs is at most half a round, the full rounds stay
+// pairs (NPL per lane) and the leftover pairs' elements go one per lane (NSL = 1: a single-element
+// round costs about half a pair round); otherwise one more pair round (NSL = 0).
+template <int NPAIR, int LANES>
+struct FerroSplit {
+  static constexpr int REM = NPAIR % LANES;
+  static constexpr bool SPLIT = REM > 0 && 2 * REM <= LANES;
+  static constexpr int NPL = SPLIT ? NPAIR / LANES : (NPAIR + LANES - 1) / LANES;
+  static constexpr int NSL = SPLIT ? 1 : 0;
+};
+
+// the edge sum of one lane: NPL Ferro pairs (+ NSL single elements), FPL feature weights, and
+// (spl) the spline edge of input `si` (sp_o = the layer's LDS cubic table at output o, kr = the
+// layer's (knot, 1/width) table by (input, interval): u = (x - knot) / width is formed here, from
+// the interval index the feature phase wrote; the zero row NI holds (0, 0): u = 0 for finite x and
+// NaN otherwise, as the reference's bases)
+template <int IN, int FLEN, int NI, int NPL, int NSL, int FPL, bool FERRO, bool FACT>
+__device__ __forceinline__ float v4_edges(const V4Lds<IN, FLEN>& L, const float* sp_o, const f2* kr,
+                                          const int* gi, const f2* ep, const f2* k2, const f2* kE, const f2* cp,
+                                          const f2* fw, int fofs, bool spl, int si, float gsl2e, int gis, float eps,
+                                          float k2s, float kEs, float cps) {
+  // spline operands first (dependent LDS reads), so their latency hides under the pairs
+  const int msi = L.M[si];
+  const float xsi = L.G[si].z;
+  const float4 cf = *reinterpret_cast<const float4*>(&sp_o[(si * (NI + 1) + msi) * 4]);
+  const f2 kw = kr[si * (NI + 1) + msi];
+  f2 acc = splat(0.0f);
+  float sgl = 0.0f;
+  if constexpr (FERRO) {
+    // the single element's dependent chain first: independent of the pairs, so its transcendental
+    // latencies interleave with theirs
+    if constexpr (NSL > 0) {
+      f2 ew, xp;
+      v4_g(L, gis, ew, xp);
+      sgl = v4_single<FACT>(ew, xp, eps, k2s, kEs, cps, 0.0f, gsl2e);
+    }
+#pragma unroll
+    for (int r = 0; r < NPL; ++r) {
+      f2 ew, xp;
+      v4_g(L, gi[r], ew, xp);
+      acc = v4_pair<FACT>(ew, xp, ep[r], k2[r], kE[r], cp[r], acc, gsl2e);
+    }
+  }
+  const float u = (xsi - kw.x) * kw.y;
+  // feature weights after the pairs (measured: 191 vs 201 us per B = 4096 solve with them first)
   if constexpr (FPL % 4 == 0) {  // chunk offsets are 16-byte aligned: ds_read_b128
     const float4* Fp = reinterpret_cast<const float4*>(&L.F[fofs]);
 #pragma unroll
@@ -266,7 +324,7 @@ __device__ __forceinline__ float v4_edges(const V4Lds<IN, FLEN>& L, const float*
     for (int f = 0; f < FPL / 2; ++f) acc = pfma(fw[f], Fp[f], acc);
   }
   const float sv = ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
-  return (acc.x + acc.y) + (spl ? sv : 0.0f);
+  return ((acc.x + acc.y) + sgl) + (spl ? sv : 0.0f);
 }
 
 // HOT = true: the rk4 (3/8) integrate path only, every stage inlined, outputs predicated;
@@ -282,9 +340,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   static_assert(H <= 10, "v4 layout: H <= 10 groups of 3 lanes");
   static_assert(!FERRO || K % 2 == 0, "v4 pairs Ferro elements (i, k), (i, k+1)");
   constexpr int KP = K / 2 > 0 ? K / 2 : 1;
-  // layer 0 (2 -> H): groups of 3 lanes; layer 1 (H -> 2): the 16 lanes of a row
-  constexpr int NPL0 = FERRO ? (D * KP + 2) / 3 : 0, NPL1 = FERRO ? (H * KP + 15) / 16 : 0;
-  constexpr int FPL0 = ((D * NFP + 2) / 3 + 3) & ~3, FPL1 = ((H * NFP + 15) / 16 + 3) & ~3;
+  // layer 0 (2 -> H): output o on a group of 3 lanes; layer 1 (H -> 2): hidden INPUT o on the
+  // same group (v7): its features, its Ferro elements of both outputs (pairs (o, 0, k), (o, 1, k):
+  // one packed pair feeds both output sums) and its two spline edges stay in the group's
+  // registers — no LDS exchange between layer 0 and layer 1
+  using FS0 = FerroSplit<D * KP, 3>;
+  static_assert(!FERRO || D == 2, "v7 layer 1 pairs the two outputs of an input");
+  constexpr int REM1 = K % 3;
+  constexpr bool SPLIT1 = REM1 == 1;                         // one k left: two singles (d = 0, 1)
+  constexpr int NPL0 = FERRO ? FS0::NPL : 0, NPL1 = FERRO ? (SPLIT1 ? K / 3 : (K + 2) / 3) : 0;
+  constexpr int NSL0 = FERRO ? FS0::NSL : 0, NSL1 = (FERRO && SPLIT1) ? 1 : 0;
+  constexpr int FPL0 = ((D * NFP + 2) / 3 + 3) & ~3;
+  constexpr int RF1 = (NFL + 2) / 3;                         // feature rounds of a hidden input (SiLU + NB)
   constexpr int FLEN0 = (3 * FPL0 > D * NFP ? 3 * FPL0 : D * NFP);
   if constexpr (DOPRI) {
     if (a.dp.xr_world > 1 && blockIdx.x == gridDim.x - 1) {   // the cross-rank exchange workgroup
@@ -292,32 +359,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
       return;
     }
   }
-  constexpr int FLEN1 = (16 * FPL1 > H * NFP ? 16 * FPL1 : H * NFP);
-  constexpr int NJH = FERRO ? NB + 3 : NB + 1;      // sigmoid-stream jobs per hidden input
-  constexpr int RH = (NJH + 2) / 3;                  // rounds over the 3 lanes of a group
   constexpr int KT = (NG + 2) / 3;                   // knots per group lane
   static_assert(3 * KT >= NG, "knots per group lane");
   constexpr int SPT0 = H * D * (NI + 1) * 4, SPT1 = D * H * (NI + 1) * 4;
 
   __shared__ __attribute__((aligned(16))) float s_sp0[SPT0];
   __shared__ __attribute__((aligned(16))) float s_sp1[SPT1];
+  __shared__ __attribute__((aligned(8))) f2 s_kr0[D * (NI + 1)], s_kr1[H * (NI + 1)];
   __shared__ float s_c0[H], s_c1[D];
   __shared__ __attribute__((aligned(16))) V4Lds<D, FLEN0> s_L0[2];
-  __shared__ __attribute__((aligned(16))) V4Lds<H, FLEN1> s_L1[2];
 
   const int tid = threadIdx.x;
   const int g = tid >> 5, lane = tid & 31, row = lane >> 4, c1 = lane & 15;
   const int64_t b = (int64_t)blockIdx.x * 2 + g;
   const bool valid = b < a.B;
   V4Lds<D, FLEN0>& L0 = s_L0[g];
-  V4Lds<H, FLEN1>& L1 = s_L1[g];
 
   for (int i = tid; i < SPT0; i += 64) s_sp0[i] = a.plan[a.P0.sp + i];
   for (int i = tid; i < SPT1; i += 64) s_sp1[i] = a.plan[a.P1.sp + i];
+  for (int i = tid; i < D * (NI + 1); i += 64) {
+    const int in = i / (NI + 1), m = i % (NI + 1);
+    s_kr0[i] = m < NI ? f2{a.plan[a.P0.knots + in * NG + m], a.plan[a.P0.rh + in * NI + m]} : f2{0.f, 0.f};
+  }
+  for (int i = tid; i < H * (NI + 1); i += 64) {
+    const int in = i / (NI + 1), m = i % (NI + 1);
+    s_kr1[i] = m < NI ? f2{a.plan[a.P1.knots + in * NG + m], a.plan[a.P1.rh + in * NI + m]} : f2{0.f, 0.f};
+  }
   for (int i = tid; i < H; i += 64) s_c0[i] = a.plan[a.P0.fconst + i];
   for (int i = tid; i < D; i += 64) s_c1[i] = a.plan[a.P1.fconst + i];
   for (int i = lane; i < FLEN0; i += 32) L0.F[i] = 0.f;  // pads stay zero (finite x zero weight)
-  for (int i = lane; i < FLEN1; i += 32) L1.F[i] = 0.f;
 
   const bool fact = FERRO && a.plan[a.P0.flag] <= a.factor_limit && a.plan[a.P1.flag] <= a.factor_limit;
   const float l2 = FETODE_LOG2E;
@@ -351,6 +421,22 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
     kE0[r] = f2{t[2][0], t[2][1]};
     cp0[r] = f2{t[3][0], t[3][1]};
   }
+  // layer-0 single: leftover element q = cc0 of pair NPL0 * 3 + q / 2
+  int gs0 = 0;
+  float es0 = 0.f, k2s0 = 0.f, kEs0 = 0.f, cps0 = 0.f;
+  if constexpr (NSL0 > 0) {
+    const int Pl = NPL0 * 3 + cc0 / 2;
+    const bool ok = act0 && cc0 < 2 * FS0::REM;
+    const int i = ok ? Pl / KP : 0;
+    const int64_t idx = (int64_t)o0c * (D * K) + i * K + (ok ? (Pl % KP) * 2 + cc0 % 2 : 0);
+    const float gec = ok ? a.plan[a.P0.fe_GEc + idx] : 0.f;
+    es0 = fact ? ex2(gec) : gec;
+    k2s0 = ok ? a.plan[a.P0.fe_k2 + idx] : 0.f;
+    kEs0 = ok ? a.plan[a.P0.fe_k2Ec + idx] : 0.f;
+    cps0 = ok ? a.plan[a.P0.fe_CPs2 + idx] : 0.f;
+    gs0 = i;
+    asm volatile("" : "+v"(gs0));
+  }
   f2 fw0[FPL0 / 2];
 #pragma unroll
   for (int f = 0; f < FPL0; f += 2) {
@@ -362,43 +448,61 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
     }
     fw0[f / 2] = f2{w[0], w[1]};
   }
-  // ---- layer-1 edge lane: output row, part c1 ----
+  // ---- layer-1 (v7): hidden input o0 on its group; lane cc0 owns k = cc0 + 3 r ----
+  // pair r: elements (o0, d = 0, k) and (o0, d = 1, k): .x feeds output 0, .y output 1
   f2 ep1[NPL1 > 0 ? NPL1 : 1], k21[NPL1 > 0 ? NPL1 : 1], kE1[NPL1 > 0 ? NPL1 : 1], cp1[NPL1 > 0 ? NPL1 : 1];
-  int gi1[NPL1 > 0 ? NPL1 : 1];
 #pragma unroll
   for (int r = 0; r < NPL1; ++r) {
-    const int P = c1 * NPL1 + r;
-    const bool ok = P < H * KP;
-    int i = ok ? P / KP : 0;
-    asm volatile("" : "+v"(i));
-    gi1[r] = i;
+    const int k = cc0 + 3 * r;
+    const bool ok = act0 && k < K;
     float t[4][2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int64_t idx = (int64_t)row * (H * K) + i * K + (ok ? (P % KP) * 2 + h : 0);
+    for (int d = 0; d < 2; ++d) {
+      const int64_t idx = (int64_t)d * (H * K) + o0c * K + (ok ? k : 0);
       const float gec = ok ? a.plan[a.P1.fe_GEc + idx] : 0.f;
-      t[0][h] = fact ? ex2(gec) : gec;
-      t[1][h] = ok ? a.plan[a.P1.fe_k2 + idx] : 0.f;
-      t[2][h] = ok ? a.plan[a.P1.fe_k2Ec + idx] : 0.f;
-      t[3][h] = ok ? a.plan[a.P1.fe_CPs2 + idx] : 0.f;
+      t[0][d] = fact ? ex2(gec) : gec;   // padding: ep = 1 (fact) / 0, k = 0: th = 0, cp = 0
+      t[1][d] = ok ? a.plan[a.P1.fe_k2 + idx] : 0.f;
+      t[2][d] = ok ? a.plan[a.P1.fe_k2Ec + idx] : 0.f;
+      t[3][d] = ok ? a.plan[a.P1.fe_CPs2 + idx] : 0.f;
     }
     ep1[r] = f2{t[0][0], t[0][1]};
     k21[r] = f2{t[1][0], t[1][1]};
     kE1[r] = f2{t[2][0], t[2][1]};
     cp1[r] = f2{t[3][0], t[3][1]};
   }
-  f2 fw1[FPL1 / 2];
-#pragma unroll
-  for (int f = 0; f < FPL1; f += 2) {
-    float w[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int qq = c1 * FPL1 + f + h, i = qq / NFP, ff = qq % NFP;
-      w[h] = (i < H && ff < NFL) ? a.plan[a.P1.kw + (int64_t)row * (H * NFL) + i * NFL + ff] : 0.f;
-    }
-    fw1[f / 2] = f2{w[0], w[1]};
+  // the single left over when K % 3 == 1: element (o0, d = cc0, K - 1) on lanes cc0 = 0, 1
+  float es1 = 0.f, k2s1 = 0.f, kEs1 = 0.f, cps1 = 0.f;
+  if constexpr (NSL1 > 0) {
+    const bool ok = act0 && cc0 < D;
+    const int64_t idx = (int64_t)(ok ? cc0 : 0) * (H * K) + o0c * K + (K - 1);
+    const float gec = ok ? a.plan[a.P1.fe_GEc + idx] : 0.f;
+    es1 = fact ? ex2(gec) : gec;
+    k2s1 = ok ? a.plan[a.P1.fe_k2 + idx] : 0.f;
+    kEs1 = ok ? a.plan[a.P1.fe_k2Ec + idx] : 0.f;
+    cps1 = ok ? a.plan[a.P1.fe_CPs2 + idx] : 0.f;
   }
-
+  // lane cc0 = d < 2 also owns the spline edge (o0 -> d): the single / spline value goes to output d
+  const f2 dsel1 = f2{(act0 && cc0 == 0) ? 1.f : 0.f, (act0 && cc0 == 1) ? 1.f : 0.f};
+  // feature rounds: job j = cc0 + 3 r (logistic j < NB, SiLU j == NB), its weights for both outputs
+  float fna1[RF1], fab1[RF1], fml1[RF1];
+  f2 fwt1[RF1];
+#pragma unroll
+  for (int r = 0; r < RF1; ++r) {
+    const int j = cc0 + 3 * r;
+    const bool ok = act0 && j < NFL;
+    fna1[r] = 0.f; fab1[r] = 0.f; fml1[r] = 0.f;
+    const int ff = j < NB ? 1 + j : 0;   // kw feature index: SiLU 0, logistic j at 1 + j
+    if (ok && j < NB) {
+      fna1[r] = a.plan[a.P1.lg + 2 * (o0 * NB + j)];
+      fab1[r] = a.plan[a.P1.lg + 2 * (o0 * NB + j) + 1];
+    } else if (ok) {
+      fna1[r] = -l2;
+      fml1[r] = 1.f;   // SiLU: h * sigmoid(h)
+    }
+    fwt1[r] = ok ? f2{a.plan[a.P1.kw + (int64_t)0 * (H * NFL) + o0 * NFL + ff],
+                      a.plan[a.P1.kw + (int64_t)1 * (H * NFL) + o0 * NFL + ff]}
+                 : f2{0.f, 0.f};
+  }
   // ---- layer-0 feature stream: input d = row, job c1 ----
   float xna, xab, xmul, xadd;
   float* xdst;
@@ -418,9 +522,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
       xdst = &L0.G[row].y;
     } else if (FERRO && j == J_EXP) {
       xna = a.P0.gsl2e;
-      xdst = &L0.G[row].z;
-    } else if (j == J_X) {
       xdst = &L0.G[row].x;
+    } else if (j == J_X) {
+      xdst = &L0.G[row].z;
     } else if (j == J_M) {
       xdst = reinterpret_cast<float*>(&L0.M[row]);
     }
@@ -430,50 +534,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   // knot interval: lane c1 holds knot c1 (and 1/(knot c1+1 - knot c1)); the lane whose knot
   // opens the interval writes u (no LDS round trip on the critical path)
   const float xknot = c1 < NG ? a.plan[a.P0.knots + row * NG + c1] : __builtin_inff();
-  const float xrh = c1 < NI ? a.plan[a.P0.rh + row * NI + c1] : 0.f;
 
-  // ---- layer-1 feature stream: hidden input o0, jobs cc0 + 3r ----
-  float hna[RH], hab[RH], hmul[RH], hadd[RH];
-  float* hdst[RH];
-#pragma unroll
-  for (int r = 0; r < RH; ++r) {
-    const int j = cc0 + 3 * r;
-    hna[r] = 0.f; hab[r] = 0.f; hmul[r] = 1.f; hadd[r] = 0.f;
-    hdst[r] = &L1.sink;
-    if (!act0) continue;
-    if (j < NB) {
-      hna[r] = a.plan[a.P1.lg + 2 * (o0 * NB + j)];
-      hab[r] = a.plan[a.P1.lg + 2 * (o0 * NB + j) + 1];
-      hdst[r] = &L1.F[o0 * NFP + 1 + j];
-    } else if (j == J_SILU) {
-      hna[r] = -l2;
-      hdst[r] = &L1.F[o0 * NFP];
-    } else if (FERRO && j == J_GATE) {
-      hna[r] = -a.P1.gsl2e; hmul[r] = -a.P1.wc; hadd[r] = a.P1.wc;
-      hdst[r] = &L1.G[o0].y;
-    } else if (FERRO && j == J_EXP) {
-      hna[r] = a.P1.gsl2e;
-      hdst[r] = &L1.G[o0].z;
-    }
-  }
-  // knots of hidden input o0: lane cc0 holds knots KT cc0 .. KT cc0 + KT-1 and their 1/width
-  float hknot[KT], hrh[KT];
+  // knots of hidden input o0: lane cc0 holds knots KT cc0 .. KT cc0 + KT-1
+  float hknot[KT];
 #pragma unroll
   for (int t = 0; t < KT; ++t) {
     const int kk = KT * cc0 + t;
     hknot[t] = (act0 && kk < NG) ? a.plan[a.P1.knots + o0 * NG + kk] : __builtin_inff();
-    hrh[t] = (act0 && kk < NI) ? a.plan[a.P1.rh + o0 * NI + kk] : 0.f;
   }
-  constexpr int RG = J_GATE / 3, CG = J_GATE % 3;  // round / lane of the layer-1 gate job
-  constexpr int RS = J_SILU / 3, RE = J_EXP / 3;
-  const bool h_silu = cc0 == J_SILU % 3, h_gate = FERRO && cc0 == CG, h_exp = FERRO && cc0 == J_EXP % 3;
-
-  // hysteresis state: prev_x of input `row` on the layer-0 gate lane, of input o0 on the
-  // layer-1 gate lane (ferro_class.py:409); per-layer contiguous blocks (include/fetode.h)
+  // hysteresis state: prev_x of input `row` on the layer-0 gate lane, of input o0 on every lane
+  // of its group (each forms the gate itself) (ferro_class.py:409); per-layer contiguous blocks
+  // (include/fetode.h)
   float prev0 = 0.f, prev1 = 0.f;
   if (FERRO && valid) {
     if (x_gate) prev0 = a.state[b * D + row];
-    if (act0 && h_gate) prev1 = a.state[a.B * D + b * H + o0];
+    if (act0) prev1 = a.state[a.B * D + b * H + o0];
   }
   bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
 
@@ -484,10 +559,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   STAMP_DECL
   const float c0o = s_c0[o0c], c1o = s_c1[row];  // per-output constants, held in registers
   const float* sp0_o = &s_sp0[o0c * D * (NI + 1) * 4];
-  const float* sp1_o = &s_sp1[row * H * (NI + 1) * 4];
-  const int fofs0 = cc0 * FPL0, fofs1 = c1 * FPL1;
-  const bool spl0 = act0 && cc0 < D, spl1 = c1 < H;  // lanes owning a spline edge (input si)
-  const int si0 = spl0 ? cc0 : 0, si1 = spl1 ? c1 : 0;
+  // layer 1: the cubic table of edge (o0 -> d = cc0) and the (knot, 1/width) rows of input o0
+  const float* sp1_e = &s_sp1[((cc0 < D ? cc0 : 0) * H + o0c) * (NI + 1) * 4];
+  const f2* kr1_o = &s_kr1[o0c * (NI + 1)];
+  const int fofs0 = cc0 * FPL0;
+  const bool spl0 = act0 && cc0 < D;  // lanes owning a layer-0 spline edge (input si)
+  const int si0 = spl0 ? cc0 : 0;
 
   // training tape: the two layer inputs of evaluation `ev` at tape[(ev B + b)(D + H) + c]
   // uniform: the inference path skips every tape op (the dopri5 driver has a taped instantiation
@@ -520,7 +597,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
       const int mfix = ((unsigned)mm < (unsigned)NI && fin) ? mm : NI;
       val = x_m ? __builtin_bit_cast(float, mfix) : val;
       *xdst = val;
-      if (c1 == mfix) L0.G[row].w = c1 < NI ? (xin - xknot) * xrh : (fin ? 0.0f : __builtin_nanf(""));
       if (FERRO) prev0 = xin;  // ferro_class.py:409 (meaningful on the gate lane)
       re0 = false;
     }
@@ -529,31 +605,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
     STAMP(0);
     FETODE_MARK("EDGES0");
     // (2) layer-0 edges -> h_o on the group of 3
-    float h = v4_edges<D, FLEN0, NI, NPL0, FPL0, FERRO, F_>(L0, sp0_o, gi0, ep0, k20, kE0, cp0, fw0, fofs0,
-                                                            spl0, si0, a.P0.gsl2e);
-    h = act0 ? h : 0.f;
-    h = group3_sum(h, cc0) + c0o;
+    float h = v4_edges<D, FLEN0, NI, NPL0, NSL0, FPL0, FERRO, F_>(L0, sp0_o, s_kr0, gi0, ep0, k20, kE0, cp0, fw0,
+                                                                  fofs0, spl0, si0, a.P0.gsl2e, gs0, es0, k2s0, kEs0,
+                                                                  cps0);
+    h = group3_sum(h, cc0) + c0o;   // lane 15 of a row (no group) is never read by a group
     STAMP(2);
     FETODE_MARK("H_FEAT");
+    // (3) layer 1 on the group of hidden input o0 (v7): partial sums of BOTH outputs in acc01
+    f2 acc01 = splat(0.0f);
     {
-      // layer-1 features of input o0: RH rounds of the sigmoid stream on the group's 3 lanes
-      const float pv = h_gate ? (re1 ? h : prev1) : 0.f;
-#pragma unroll
-      for (int r = 0; r < RH; ++r) {
-        const float hx = (FERRO && r == RG) ? h - pv : h;
-        const float e = ex2(ffma(hna[r], hx, hab[r]));
-        const float sg = rcp(1.0f + e);
-        float val;
-        if (r == RS || (FERRO && (r == RG || r == RE))) {
-          val = ffma(sg, (r == RS && h_silu) ? h : hmul[r], hadd[r]);
-          if (FERRO && r == RE) val = h_exp ? e : val;
-        } else {
-          val = sg;
-        }
-        *hdst[r] = val;
-      }
-      if (FERRO) prev1 = h;
-      re1 = false;
       // knot interval of h: KT compares per lane, summed over the group
       float cntf = 0.f;
 #pragma unroll
@@ -562,37 +622,48 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
       const int mm = (int)cntf - 1;
       const bool fin = __builtin_isfinite(h);
       const int mfix = ((unsigned)mm < (unsigned)NI && fin) ? mm : NI;
-      const int tq = mfix % KT;
-      // register select chain; the empty asm keeps the compiler from turning it into an
-      // indexed load of hknot/hrh (which would put both arrays in scratch memory)
-      float knm = hknot[0], rhm = hrh[0];
-      asm volatile("" : "+v"(knm), "+v"(rhm));
+      // spline operands by interval (the zero row NI holds (0, 0): u = 0 for finite h, NaN
+      // otherwise, as the reference's bases); their LDS latency hides under the pairs
+      const float4 cf = *reinterpret_cast<const float4*>(&sp1_e[mfix * 4]);
+      const f2 kw = kr1_o[mfix];
+      float sgl = 0.0f;
+      if constexpr (FERRO) {
+        // every lane of the group forms the gate and exp(gs h) of its input itself (three
+        // transcendentals: cheaper than broadcasting them across a group of 3 lanes)
+        const float pv = re1 ? h : prev1;
+        const float eg = ex2(ffma(-a.P1.gsl2e, h - pv, 0.0f));
+        const float w = ffma(rcp(1.0f + eg), -a.P1.wc, a.P1.wc);   // wc (1 - up)
+        const float e = F_ ? ex2(ffma(a.P1.gsl2e, h, 0.0f)) : 0.0f;
+        prev1 = h;   // ferro_class.py:409
+        re1 = false;
+        const f2 ew = f2{e, w}, xp = f2{h, 0.0f};
+        if constexpr (NSL1 > 0) sgl = v4_single<F_>(ew, xp, es1, k2s1, kEs1, cps1, 0.0f, a.P1.gsl2e);
 #pragma unroll
-      for (int t = 1; t < KT; ++t) {
-        knm = tq == t ? hknot[t] : knm;
-        rhm = tq == t ? hrh[t] : rhm;
-        asm volatile("" : "+v"(knm), "+v"(rhm));
+        for (int r = 0; r < NPL1; ++r) acc01 = v4_pair<F_>(ew, xp, ep1[r], k21[r], kE1[r], cp1[r], acc01, a.P1.gsl2e);
       }
-      if (act0 && cc0 == mfix / KT)
-        L1.G[o0].w = mfix < NI ? (h - knm) * rhm : (fin ? 0.0f : __builtin_nanf(""));
-      if (act0 && cc0 == 0) {
-        L1.G[o0].x = h;
-        L1.M[o0] = mfix;
-        if (taping && valid) tape_b[D + o0] = h;
+      // the group's features (SiLU + NB logistic), each weighted for both outputs
+#pragma unroll
+      for (int r = 0; r < RF1; ++r) {
+        const float e = ex2(ffma(fna1[r], h, fab1[r]));
+        const float sg = rcp(1.0f + e);
+        const float val = fml1[r] != 0.0f ? h * sg : sg;   // SiLU h sigma(h) / logistic sigma
+        acc01 = pfma(fwt1[r], splat(val), acc01);
       }
+      const float u = (h - kw.x) * kw.y;
+      const float sv = ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
+      acc01 = pfma(dsel1, splat(sgl + sv), acc01);   // lane d < 2: single + spline onto output d
+      if (taping && valid && act0 && cc0 == 0) tape_b[D + o0] = h;
     }
     if (taping) {
       tape_b += tape_stride;
       if constexpr (DOPRI) taping = --tape_left > 0;
     }
     STAMP(3);
-    __syncthreads();
-    STAMP(4);
-    FETODE_MARK("EDGES1");
-    // (3) layer-1 edges -> k_row on every lane of the row
-    const float v = v4_edges<H, FLEN1, NI, NPL1, FPL1, FERRO, F_>(L1, sp1_o, gi1, ep1, k21, kE1, cp1, fw1, fofs1,
-                                                                  spl1, si1, a.P1.gsl2e);
-    const float kr = row_sum16(v) + c1o;
+    // output sums over the half-wave: the permlane16 swap folds the two rows of each output into
+    // row d (rows 0 / 2: output 0, rows 1 / 3: output 1), a row sum finishes: k_row on row `row`
+    float p0 = acc01.x, p1 = acc01.y;
+    permlane16_swap(p0, p1);
+    const float kr = row_sum16(p0 + p1) + c1o;
     STAMP(5);
     FETODE_MARK("END");
     return kr;
@@ -902,7 +973,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   }
   if (FERRO && valid) {
     if (x_gate) a.state[b * D + row] = prev0;
-    if (act0 && h_gate) a.state[a.B * D + b * H + o0] = prev1;
+    if (act0 && cc0 == 0) a.state[a.B * D + b * H + o0] = prev1;
   }
   STAMP_FLUSH();
 }
@@ -1105,8 +1176,8 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       // gate_i / exp_i of the two inputs: slot 1, lanes 6..9 of every row (row_newbcast)
       const float g0 = dppm<0x156>(fv1), g1 = dppm<0x157>(fv1);
       const float e0 = dppm<0x158>(fv1), e1 = dppm<0x159>(fv1);
-      const float4 gi = i0 ? make_float4(x1, g1, e1, 0.f) : make_float4(x0, g0, e0, 0.f);
-      const f2 pr = v4_pair<F_>(gi, ep0, k20, kE0, cp0, splat(0.0f), a.P0.gsl2e);
+      const f2 ew = i0 ? f2{e1, g1} : f2{e0, g0}, xp = f2{i0 ? x1 : x0, 0.f};
+      const f2 pr = v4_pair<F_>(ew, xp, ep0, k20, kE0, cp0, splat(0.0f), a.P0.gsl2e);
       acc += pr.x + pr.y;
     }
     // spline edges (r, 0), (r, 1): the lane whose knot opens the interval (ballot count over a
@@ -1136,7 +1207,7 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       v = hexp ? e : v;
       if constexpr (FERRO) {
         const float gt = dppm<0x15B>(v), ee = dppm<0x15C>(v);  // row_newbcast:11 / :12
-        const f2 pr = v4_pair<F_>(make_float4(h, gt, ee, 0.f), ep1, k21, kE1, cp1, splat(0.0f), a.P1.gsl2e);
+        const f2 pr = v4_pair<F_>(f2{ee, gt}, f2{h, 0.f}, ep1, k21, kE1, cp1, splat(0.0f), a.P1.gsl2e);
         acc01 = pfma(psel, splat(pr.x + pr.y), acc01);  // 1 * ps onto output o1, 0 * ps (exact) onto the other
         pvh = hgate ? h : 0.f;
         re1 = false;
