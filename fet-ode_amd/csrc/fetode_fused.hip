@@ -184,6 +184,24 @@ struct FusedArgs {
   DopriParams dp;       // dp.on: the whole dopri5 solve in this launch (fetode_integrate_dopri5)
 };
 
+// integer version (knot counts)
+__device__ __forceinline__ int group3_sum_i(int v, int c) {
+  const int s0 = v + __builtin_amdgcn_update_dpp(0, v, 0x101, 0xF, 0xF, false) +
+                 __builtin_amdgcn_update_dpp(0, v, 0x102, 0xF, 0xF, false);
+  const int b1 = __builtin_amdgcn_mov_dpp(s0, 0x111, 0xF, 0xF, false);
+  const int b2 = __builtin_amdgcn_mov_dpp(s0, 0x112, 0xF, 0xF, false);
+  return c == 0 ? s0 : (c == 1 ? b1 : b2);
+}
+// knots <= x among this lane's N knots: one compare + one carry-in add per knot
+template <int N>
+__device__ __forceinline__ int knot_count(float x, const float* kn) {
+  int cnt = 0;
+#pragma unroll
+  for (int t = 0; t < N; ++t)
+    asm volatile("v_cmp_ge_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, 0, %0, vcc" : "+v"(cnt) : "v"(x), "v"(kn[t]) : "vcc");
+  return cnt;
+}
+
 // sum over lanes 3k, 3k+1, 3k+2 of a row (k < 5), result on all three
 __device__ __forceinline__ float group3_sum(float v, int c) {
   const float s0 = v + dpp<0x101>(v) + dpp<0x102>(v);  // row_shl:1, row_shl:2 -> valid at c == 0
@@ -615,11 +633,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
     f2 acc01 = splat(0.0f);
     {
       // knot interval of h: KT compares per lane, summed over the group
-      float cntf = 0.f;
-#pragma unroll
-      for (int t = 0; t < KT; ++t) cntf += h >= hknot[t] ? 1.0f : 0.0f;
-      cntf = group3_sum(cntf, cc0);
-      const int mm = (int)cntf - 1;
+      const int mm = group3_sum_i(knot_count<KT>(h, hknot), cc0) - 1;
       const bool fin = __builtin_isfinite(h);
       const int mfix = ((unsigned)mm < (unsigned)NI && fin) ? mm : NI;
       // spline operands by interval (the zero row NI holds (0, 0): u = 0 for finite h, NaN
@@ -733,7 +747,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
           int m0 = om0;
           float sl0 = osl0;
           asm volatile("" : "+v"(m0), "+v"(sl0));
-          out_write(jj, m0 == 0 ? y : (m0 == 1 ? y1 : y + sl0 * (y1 - y)));
+          const float oip = y + sl0 * (y1 - y);
+          const float o1 = m0 == 1 ? y1 : oip;
+          out_write(jj, m0 == 0 ? y : o1);
           ++jj;
           if (os1 == s) {  // several outputs inside one step (step_size grids)
             while (jj < a.T) {
