@@ -87,6 +87,41 @@ def test_production_size_vs_oracle(dev):
         close(p.grad, ps[n].grad, 5e-4, "grad " + n)
 
 
+def test_per_gpu_shard_b7500_rows_vs_oracle(dev):
+    """BASELINE configs[4]: MNIST B = 60000 sharded 8x = 7 500 images per GPU
+    (mnist_kuramoto_kan.py:207-283).  The whole 7 500-row batch runs on the device (every row tile
+    of the Kuramoto lane kernels and of the KANLinear head, the ragged last tile included); logits
+    and the parameter gradients of a loss over a 256-row subset (the first and last 64 rows and 128
+    spread between) are checked against the CPU oracle on those rows, at the bars of the batch-64
+    test above."""
+    from fet_ode_amd import mnist
+    from oracle import mnist_ref as M
+    B = 7500
+    torch.manual_seed(63)
+    m = mnist.KuramotoKANClassifier()
+    with torch.no_grad():
+        m.osc.omega.normal_(0, 0.3)
+        m.head.logistic_bias.normal_(0, 0.1)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    x = M.mnist_x(B, seed=64)
+    y = torch.arange(B) % 10
+    g = torch.Generator().manual_seed(65)
+    mid = torch.randperm(B - 128, generator=g)[:128] + 64
+    rows = torch.cat([torch.arange(64), mid.sort().values, torch.arange(B - 64, B)])
+    logits = m(x.to(dev))
+    assert logits.shape == (B, 10) and torch.isfinite(logits).all()
+    rd = rows.to(dev)
+    torch.nn.functional.cross_entropy(logits[rd], y[rows].to(dev)).backward()
+    ps = {k: v.clone().requires_grad_(k not in ("osc.neighbor_kernel", "head.grid")) for k, v in sd.items()}
+    ref = M.ClassifierRef(ps)
+    lr = ref(x[rows])
+    close(logits[rd], lr, 1e-5, "logits B=7500 rows")
+    torch.nn.functional.cross_entropy(lr, y[rows]).backward()
+    for n, p in m.named_parameters():
+        close(p.grad, ps[n].grad, 5e-4, "grad " + n + " (B=7500, 256-row loss)")
+
+
 @pytest.mark.parametrize("W", [28, 31, 32])
 def test_kuramoto_lane_kernels_match_lds_kernels(dev, W):
     """The 28 x 28 production shape runs the lane-per-column Kuramoto kernels (registers + DPP wave

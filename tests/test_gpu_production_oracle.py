@@ -86,6 +86,62 @@ def test_wide_resident_dopri5_b8192_rows_vs_oracle(dev):
         _envelope(mem[l][rows], m32[l], m64[l], f"wide dopri5 B=8192 hysteresis memory layer {l}")
 
 
+def test_wide_resident_dopri5_oracle_chooses_its_own_steps(dev):
+    """fetode_wide_dopri5 at KANFET[64, 128, 64] (train_kan_fet_ett.py:192) against the oracle's
+    OWN step-size control: no replay, no first_step — the oracle selects the initial step
+    (_select_initial_step) and accepts / rejects every attempt from its own fp32 error norms.  The
+    batch is one the CPU oracle can carry inside a test (B = 64: ~0.2 s per oracle evaluation at
+    these widths; B = 512 is ~2.4 s, ~4 min per solve); t in [0, 0.02] at rtol 1e-3 / atol 1e-4
+    gives 15 attempts (4 rejected while the probe's step shrinks, 11 accepted) whose error ratios
+    all stay >= 16 % away from 1, so the decisions are not at fp32 rounding level.  The device
+    solve must take the same attempts (accept pattern, nfev, dt to 1e-5 relative: the norms are
+    fp64 sums on the device and fp32 torch norms in the oracle); the solution and both layers'
+    hysteresis memory are checked against the fp32/fp64 envelope (the fp64 oracle's own control
+    takes the same decisions; a replay would need first_step and so skip the initial-step probe,
+    itself a stateful hysteresis call)."""
+    torch.manual_seed(0)
+    dyn = ett.KANFETDynamics(64, hidden=128, num_fet_basis=10)
+    sd = {k: v.clone() for k, v in dyn.net.state_dict().items()}
+    dyn = dyn.to(dev)
+    g = torch.Generator().manual_seed(3)
+    z0 = torch.randn(64, 64, generator=g) * 0.6
+    t = torch.linspace(0.0, 0.02, steps=3)
+    kw = dict(rtol=1e-3, atol=1e-4)
+    prev = F.dopri5.set_wide_resident_dopri5(True, gap=(0, 0))
+    try:
+        with torch.no_grad():
+            sol = F.odeint(dyn, z0.to(dev), t.to(dev), method="dopri5", **kw)
+        s = F.dopri5.dopri5_solve.last
+        assert isinstance(s, ResidentSolve), "the wide resident path was not taken"
+    finally:
+        F.dopri5.set_wide_resident_dopri5(prev, gap=(512, 8192))
+    mem = [f._prev.detach().cpu() for _, f in field_layers(dyn.net)]
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    ref32 = O.KANFETRef.from_state_dict(sd, 2)
+    tr = O.Dopri5Trace()
+    with torch.no_grad():
+        e32 = O.odeint(lambda tt, zz: ref32(zz), z0, t.to(torch.float64), method="dopri5", trace=tr, **kw)
+    m32 = [st.prev_x[:, :, 0, 0].clone() for st in ref32.states]
+    ours = [(a[1], a[3]) for a in s.attempts]
+    theirs = [(a[1], a[3]) for a in tr.attempts]
+    assert len(theirs) >= 10 and not all(acc for _, acc in theirs), theirs
+    assert [acc for _, acc in ours] == [acc for _, acc in theirs], (ours, theirs)
+    assert s.nfev == tr.nfev, (s.nfev, tr.nfev)
+    for (d0, _), (d1, _) in zip(ours, theirs):
+        assert abs(d0 - d1) <= 1e-5 * abs(d1), (ours, theirs)
+    assert min(abs(a[2] - 1.0) for a in tr.attempts) > 0.1   # decisions far from rounding level
+    sd64 = {k: v.to(torch.float64) for k, v in sd.items()}
+    ref64 = O.KANFETRef.from_state_dict(sd64, 2)
+    tr64 = O.Dopri5Trace()
+    with torch.no_grad():
+        e64 = O.odeint(lambda tt, zz: ref64(zz), z0.double(), t.to(torch.float64), method="dopri5", trace=tr64, **kw)
+    assert [a[3] for a in tr64.attempts] == [acc for _, acc in theirs]
+    m64 = [st.prev_x[:, :, 0, 0].clone() for st in ref64.states]
+    _envelope(sol.cpu(), e32, e64, "wide dopri5 B=64, oracle-chosen steps: solution")
+    for l in range(2):
+        _envelope(mem[l], m32[l], m64[l], f"wide dopri5 B=64, oracle-chosen steps: hysteresis memory layer {l}")
+
+
 def test_forecaster_latent64_b8192_rows_vs_oracle(dev):
     c, p = 96, 8
     torch.manual_seed(0)
