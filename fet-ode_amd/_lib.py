@@ -197,6 +197,7 @@ SIGNATURES = {
                                                   ctypes.c_int32, _vp, _vp]),
     "fetode_fused_backward_supported": (ctypes.c_int, [ctypes.POINTER(FieldDesc)]),
     "fetode_backward_set_split": (ctypes.c_int, [ctypes.c_int32]),
+    "fetode_backward_set_v7": (ctypes.c_int, [ctypes.c_int32]),
     "fetode_integrate_fixed_backward_workspace": (ctypes.c_int64, [ctypes.POINTER(FieldDesc), ctypes.c_int32,
                                                                   ctypes.c_int32, ctypes.c_int64]),
     "fetode_integrate_fixed_backward": (ctypes.c_int, [ctypes.POINTER(FieldDesc), _vp, ctypes.c_int32, ctypes.c_int64,

@@ -1337,8 +1337,11 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(FETOD
 // Jobs (256 threads): Ferro element e = tid (E = 200); edge q = tid - E (NE = 20; the i = 0 edge of
 // output o also sums G_o); logistic (i, j) jobs tid - E - NE and, if NL exceeds what is left, a
 // second one on threads 0.. (L1: 36 + 64 of 100).
+// FE = false (after sweep7_kernel, which keeps the Ferro sums itself): the KAN sums only — no
+// hysteresis inputs fetched, no Ferro jobs (edges on threads 0.., logistic jobs after them), the
+// Ferro slots of the block's row written as zeros.
 constexpr int kPsTS = 32;  // samples per tile
-template <int D, int H, int K, int NB, int NG, int LAYER>
+template <int D, int H, int K, int NB, int NG, int LAYER, bool FE = true>
 __global__ __launch_bounds__(256) void param_sum_kernel(BwdArgs a) {
   using LA = BL<D, H, K, NB, NG, true>;
   using LB = BL<H, D, K, NB, NG, true>;
@@ -1347,8 +1350,9 @@ __global__ __launch_bounds__(256) void param_sum_kernel(BwdArgs a) {
   constexpr int IN = L::IN, OUT = L::OUT, E = L::E, NE = L::NE, NL = L::NL;
   constexpr int TB = LAYER == 0 ? 0 : D;          // the layer's inputs in a tape row
   constexpr int GB = LAYER == 0 ? D : 0;          // its output adjoints in a gadj row (h | k)
-  constexpr int J1 = 256 - E - NE;                 // logistic jobs of the first round
-  static_assert(E + NE <= 256 && NL <= J1 + 64 && (NL <= J1 || NL - J1 <= E), "param_sum job map");
+  constexpr int EJ = FE ? E : 0;                   // Ferro jobs of this launch
+  constexpr int J1 = 256 - EJ - NE;                // logistic jobs of the first round
+  static_assert(EJ + NE <= 256 && NL <= J1 + 64 && (NL <= J1 || NL - J1 <= EJ), "param_sum job map");
   constexpr AccLayout AL = L::AL;
   __shared__ BInTab<W, NG, NB> TI;
   __shared__ BTab<L> Tb;
@@ -1367,13 +1371,13 @@ __global__ __launch_bounds__(256) void param_sum_kernel(BwdArgs a) {
   __syncthreads();
 
   // this thread's jobs and their constants
-  const bool fjob = tid < E;
+  const bool fjob = tid < EJ;
   const int e = fjob ? tid : 0, fi = e / (OUT * K), fo = (e % (OUT * K)) / K;
   const float4 fpa = Tb.fpa[e >> 1];
   const float fEc = (e & 1) ? fpa.y : fpa.x, fk2 = (e & 1) ? fpa.w : fpa.z;  // Ec, 2 log2e k
-  const bool ejob = tid >= E && tid < E + NE;
-  const int q = ejob ? tid - E : 0, eo = q / IN, ei = q % IN;
-  const int lq0 = tid - E - NE;
+  const bool ejob = tid >= EJ && tid < EJ + NE;
+  const int q = ejob ? tid - EJ : 0, eo = q / IN, ei = q % IN;
+  const int lq0 = tid - EJ - NE;
   const bool ljob0 = lq0 >= 0 && lq0 < NL;
   const bool ljob1 = NL > J1 && tid < NL - J1;
   const int l0 = ljob0 ? lq0 : 0, l1 = ljob1 ? J1 + tid : 0;
@@ -1411,6 +1415,7 @@ __global__ __launch_bounds__(256) void param_sum_kernel(BwdArgs a) {
       if (it < TS * IN && n < n1) {
         const int64_t ev = n / a.B;
         px[k] = a.tape[n * W + TB + i];
+        if (!FE) continue;  // no hysteresis input without the Ferro jobs
         if (ev > 0) pp[k] = a.tape[(n - a.B) * W + TB + i];
         else if (!imask) pp[k] = a.state0[(LAYER == 0 ? (n % a.B) * D : a.B * D + (n % a.B) * H) + i];
         else pp[k] = px[k];  // the tape_at(-1) rule: first call, dx = 0
@@ -1458,7 +1463,7 @@ __global__ __launch_bounds__(256) void param_sum_kernel(BwdArgs a) {
 #pragma unroll
       for (int c = 0; c < NS; ++c) sbd[s][i][c] = bd[c];
       sx[s][i] = x;
-      sup[s][i] = sigm_l2(-gsl * (x - pv));
+      if (FE) sup[s][i] = sigm_l2(-gsl * (x - pv));
     }
 #pragma unroll
     for (int k = 0; k < KO; ++k) {  // the layer's output adjoints
@@ -1515,6 +1520,9 @@ __global__ __launch_bounds__(256) void param_sum_kernel(BwdArgs a) {
   }
   // ---- this block's partial row (the layer's half; the other launch writes the other half) ----
   float* part = a.part + (int64_t)blockIdx.x * a.nacc + (LAYER == 0 ? 0 : LA::AL.n);
+  if (!FE) {
+    for (int i = tid; i < 3 * E; i += 256) part[AL.oA + i] = 0.f;  // (oA, oC, oE: contiguous)
+  }
   if (fjob) {
     part[AL.oA + e] = A;
     part[AL.oC + e] = C;
@@ -1659,6 +1667,8 @@ __global__ __launch_bounds__(64) void grad_apply_kernel(const double* __restrict
   }
 }
 
+#include "fetode_sweep7.h"
+
 typedef void (*bwd_fn)(BwdArgs);
 typedef void (*dopri_bwd_fn)(DopriBwdArgs);
 struct BwdEntry {
@@ -1672,6 +1682,7 @@ struct BwdEntry {
   dopri_bwd_fn dopri1;         // the same, one trajectory per wave: half the VJP jobs per lane
                                // (latency) where the batch leaves the grid room (small B)
   bwd_fn fn1;                  // fn at one trajectory per wave (small B), or null
+  bwd_fn v7;                   // the lane-group sweep (two trajectories per wave), or null
 };
 const BwdEntry kBwd[] = {
     // LV KAN-FET [2,10,2]: one kernel, two trajectories per wave (measured: TPW 1 / 2 / 4 = 1034 / 897 /
@@ -1680,15 +1691,17 @@ const BwdEntry kBwd[] = {
     {2, 10, 10, 10, 12, true, 2, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 2>,
      fixed_bwd_kernel<2, 10, 10, 10, 12, true, false, 1>, param_sum_kernel<2, 10, 10, 10, 12, 0>,
      param_sum_kernel<2, 10, 10, 10, 12, 1>, dopri_bwd_kernel<2, 10, 10, 10, 12, true, 2>, 2,
-     dopri_bwd_kernel<2, 10, 10, 10, 12, true, 1>, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 1>},
+     dopri_bwd_kernel<2, 10, 10, 10, 12, true, 1>, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 1>,
 #else
     {2, 10, 10, 10, 12, true, 2, fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 2>, nullptr, nullptr, nullptr,
      dopri_bwd_kernel<2, 10, 10, 10, 12, true, 2>, 2, dopri_bwd_kernel<2, 10, 10, 10, 12, true, 1>,
-     fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 1>},
+     fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 1>,
 #endif
+     sweep7_kernel},
     // LV KAN [2,10,2] (126 VGPRs: four waves per SIMD already)
     {2, 10, 0, 10, 12, false, 1, fixed_bwd_kernel<2, 10, 1, 10, 12, false, true, 1>, nullptr, nullptr, nullptr,
-     dopri_bwd_kernel<2, 10, 1, 10, 12, false, 2>, 2, dopri_bwd_kernel<2, 10, 1, 10, 12, false, 1>, nullptr},
+     dopri_bwd_kernel<2, 10, 1, 10, 12, false, 2>, 2, dopri_bwd_kernel<2, 10, 1, 10, 12, false, 1>, nullptr,
+     nullptr},
 };
 // Which path the KAN-FET sweep takes (fetode_backward_set_split; env FETODE_BWD_SPLIT).  Default:
 // the one-kernel sweep — measured on MI355X at B = 4096, rk4, 34 steps: one kernel 1.06 ms vs the
@@ -1702,6 +1715,17 @@ bool use_split(const BwdEntry* e) {
   return e->adj && g_bwd_split != 0;
 }
 constexpr int64_t kSumBlocks = 1024;  // param_sum_kernel blocks per layer (= partial rows)
+// The lane-group sweep (sweep7_kernel; fetode_backward_set_v7, env FETODE_BWD_V7):
+// 0 = off, 1 = where the one-kernel sweep would run two trajectories per wave (the default),
+// 2 = at every batch.
+int g_bwd_v7 = -1;
+int v7_mode() {
+  if (g_bwd_v7 < 0) {
+    const char* v = getenv("FETODE_BWD_V7");
+    g_bwd_v7 = v ? atoi(v) : 1;
+  }
+  return g_bwd_v7;
+}
 int64_t n_evals_of(int32_t method, int32_t n_steps) {
   return (int64_t)n_steps * (method == FETODE_RK4 || method == FETODE_RK4_CLASSIC ? 4 : method == FETODE_MIDPOINT ? 2 : 1);
 }
@@ -1782,6 +1806,12 @@ int fetode_backward_set_split(int32_t enable) {
 #endif
 }
 
+int fetode_backward_set_v7(int32_t mode) {
+  const int prev = v7_mode();
+  if (mode >= 0) g_bwd_v7 = mode;
+  return prev;
+}
+
 int fetode_fused_backward_supported(const fetode_field_t* f) {
   if (validate_field(f) != FETODE_OK) return 0;
   return find_bwd(f) != nullptr || fieldn_shape_supported(f);
@@ -1805,8 +1835,15 @@ int fixed_tpw(const BwdEntry* e, int64_t B) {
   return 2 * B <= cap ? 1 : e->tpw;
 }
 
-// partial rows of the chosen path: one per wave (one-kernel sweep) or per param_sum block (split)
+bool use_v7(const BwdEntry* e, int64_t B) {
+  if (!e->v7 || use_split(e)) return false;
+  const int m = v7_mode();
+  return m >= 2 || (m == 1 && fixed_tpw(e, B) == 2);
+}
+// partial rows of the chosen path: one per wave (the one-kernel and lane-group sweeps) or per
+// param_sum block (split)
 int64_t sum_rows(const BwdEntry* e, int64_t B, int64_t n_ev) {
+  if (use_v7(e, B)) return bwd_rows(B, 2);
   if (!use_split(e)) return bwd_rows(B, fixed_tpw(e, B));
   const int64_t tiles = (n_ev * B + kPsTS - 1) / kPsTS;
   return tiles < kSumBlocks ? (tiles > 0 ? tiles : 1) : kSumBlocks;
@@ -1887,7 +1924,10 @@ int fetode_integrate_fixed_backward(const fetode_field_t* f, const void* plan, i
   a.part = part;
   a.nacc = nacc;
   a.gadj = gadj;
-  if (split) {
+  if (use_v7(e, B)) {   // two trajectories per wave, one partial row per wave
+    hipLaunchKernelGGL(e->v7, dim3((unsigned)(nrow / kTPB)), dim3(64 * kTPB), 0, s, a);
+    LAUNCH_CHECK();
+  } else if (split) {
     // adjoint sweep: one wave per trajectory, every trajectory resident (grid-stride beyond)
     const int64_t blocks = (B + kTPB - 1) / kTPB;
     hipLaunchKernelGGL(e->adj, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(64 * kTPB), 0, s, a);

@@ -44,13 +44,18 @@ def kernel_switch():
     lib.fetode_fused_set_small_batch_max(prev)
 
 
-@pytest.fixture(params=[0, 1], ids=["one-kernel", "split"])
+@pytest.fixture(params=[0, 1, 2], ids=["one-kernel", "split", "lane-sweep"])
 def bwd_split(request):
-    """Run a fused-backward test through both sweep structures (fetode_backward_set_split)."""
+    """Run a fused-backward test through each sweep structure: the one-kernel sweep, the split
+    (fetode_backward_set_split, diagnostic build) and the lane-group sweep + KAN sums at every batch
+    (fetode_backward_set_v7(2))."""
     from fet_ode_amd import _lib
     lib = _lib.load()
-    prev = lib.fetode_backward_set_split(request.param)
+    prev_v7 = lib.fetode_backward_set_v7(2 if request.param == 2 else 0)
+    prev = lib.fetode_backward_set_split(1 if request.param == 1 else 0)
     if prev == -2:
+        lib.fetode_backward_set_v7(prev_v7)
         pytest.skip("the split backward is in the diagnostic build only (make diag)")
     yield request.param
     lib.fetode_backward_set_split(prev)
+    lib.fetode_backward_set_v7(prev_v7)

@@ -388,6 +388,35 @@ def test_fused_backward_matches_per_stage_path_large_batch(dev):
         assert_grad_close(res[0][n], res[1][n], n, rel=1e-4)
 
 
+@pytest.mark.parametrize("B", [4096, 777])
+def test_lane_sweep_matches_one_kernel_bench_horizon(dev, B):
+    """KAN-FET, the bench horizon (34 rk4 steps), the bench loss: the lane-group sweep + KAN sums
+    (fetode_backward_set_v7(2)) against the one-kernel sweep (mode 0) — the same VJP algebra in a
+    different lane map and summation order; B = 777 leaves the last wave half empty."""
+    import fet_ode_amd as F
+    from fet_ode_amd import _lib
+    from oracle import torch_ref as O
+    lib = _lib.load()
+    sd = golden_sd(load_golden("traj_kanfet"))
+    t = torch.from_numpy(load_golden("traj_kanfet")["t35"])
+    y0 = O.lv_y0(B, seed=1).to(dev)
+    res = []
+    prev = lib.fetode_backward_set_v7(-1)
+    try:
+        for mode in (0, 2):
+            lib.fetode_backward_set_v7(mode)
+            m = F.KANFET([2, 10, 2], grid_size=5)
+            m.load_state_dict(sd)
+            m = m.to(dev)
+            yg = y0.clone().requires_grad_(True)
+            F.odeint(F.autonomous(m), yg, t, method="rk4").square().mean().backward()
+            res.append({"y0": yg.grad.cpu(), **{n: p.grad.cpu() for n, p in m.named_parameters()}})
+    finally:
+        lib.fetode_backward_set_v7(prev)
+    for n in res[0]:
+        assert_grad_close(res[1][n], res[0][n], n, rel=1e-4)
+
+
 def test_fused_backward_deterministic(dev, bwd_split):
     """Two identical training solves give bitwise-identical gradients (fixed-order reductions)."""
     import fet_ode_amd as F
