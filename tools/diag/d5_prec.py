@@ -75,6 +75,7 @@ def rel(a, b):
 
 
 cases = os.environ.get("CASES", "1:1e-3,16:1e-3,64:1e-3,1:1e-2,16:1e-2,64:1e-2,1:1e-1,16:1e-1,64:1e-1")
+allerr = {}   # path -> list of (case, tensor, error)
 for c in cases.split(","):
     B, rtol = int(c.split(":")[0]), float(c.split(":")[1])
     o64, n64, s64 = oracle(B, rtol, torch.float64)
@@ -83,6 +84,20 @@ for c in cases.split(","):
                     ("host", lambda: gpu(B, rtol, False)), ("ref32", lambda: oracle(B, rtol, torch.float32))):
         gr, nf, sol = fn()
         errs = {n: rel(gr[n], o64[n]) for n in o64}
+        allerr.setdefault(lab, []).append(errs)
         worst = sorted(errs.items(), key=lambda kv: -kv[1])[:3]
         row[lab] = {"nfev": nf, "sol": rel(sol, s64), "worst": [(k, float("%.3g" % v)) for k, v in worst]}
     print(json.dumps(row), flush=True)
+
+# aggregates over the grid: geometric mean of every (case, tensor) error, and of each case's worst
+# tensor; ratios to the host path (the VERDICT r4 bar: res6 within 1.2x of host)
+gm = lambda v: float(np.exp(np.mean(np.log(np.maximum(v, 1e-30)))))
+summ = {}
+for lab, rows in allerr.items():
+    every = [e for r in rows for e in r.values()]
+    summ[lab] = {"geomean_all": gm(every), "geomean_worst": gm([max(r.values()) for r in rows]),
+                 "max": max(every)}
+for lab in summ:
+    summ[lab]["ratio_to_host_all"] = summ[lab]["geomean_all"] / summ["host"]["geomean_all"]
+    summ[lab]["ratio_to_host_worst"] = summ[lab]["geomean_worst"] / summ["host"]["geomean_worst"]
+print(json.dumps({"summary": summ}), flush=True)
