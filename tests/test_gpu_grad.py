@@ -417,6 +417,58 @@ def test_lane_sweep_matches_one_kernel_bench_horizon(dev, B):
         assert_grad_close(res[1][n], res[0][n], n, rel=1e-4)
 
 
+def test_lane_sweep_off_grid_inputs(dev):
+    """Initial states spread over [-4, 4] (the knots span [-2.2, 2.2]): both layers' inputs leave the
+    grid on many trajectories, so the lane sweep's out-of-grid branches (zero bases, the spline
+    table's zero row, the layer-0 interval from the wave ballot) run; held to the one-kernel sweep
+    within 1e-4 over 5 rk4 steps, and over one step (where the reference's own fp32 autograd is within
+    7.5e-4 of fp64; over 5 steps these wild states put it 26 % away) to the fp64 oracle with the
+    reference's fp32 error as the yardstick: |gpu - fp64| <= 4 |ref fp32 - fp64| + 1e-4 scale (both
+    sweeps measure the same errors here, at most 3.7x the reference's on layers.0.ferro.Ec —
+    tools/diag/offgrid_diag.py, profiles/r05_offgrid.log — the fp32 tape of the fused forward)."""
+    import fet_ode_amd as F
+    from fet_ode_amd import _lib
+    from oracle import torch_ref as O
+    lib = _lib.load()
+    g = load_golden("traj_kanfet")
+    sd = golden_sd(g)
+    y0 = (torch.rand(2048, 2, generator=torch.Generator().manual_seed(8), dtype=torch.float64) * 8 - 4).float()
+    skip = ("grid", "prev_x", "branch_sign")
+
+    def gpu(mode, t):
+        lib.fetode_backward_set_v7(mode)
+        m = F.KANFET([2, 10, 2], grid_size=5)
+        m.load_state_dict(sd)
+        m = m.to(dev)
+        yg = y0.clone().to(dev).requires_grad_(True)
+        F.odeint(F.autonomous(m), yg, t, method="rk4").square().mean().backward()
+        return {"y0": yg.grad.cpu(), **{n: p.grad.cpu() for n, p in m.named_parameters()}}
+
+    def oracle(dt, t):
+        ps = {k: v.clone().to(dt).requires_grad_(k.split(".")[-1] not in skip) for k, v in sd.items()}
+        ref = O.KANFETRef.from_state_dict(ps, 2)
+        yc = y0.clone().to(dt).requires_grad_(True)
+        O.odeint(lambda tt, yy: ref(yy), yc, t, method="rk4").square().mean().backward()
+        return {"y0": yc.grad.double(), **{n: ps[n].grad.double() for n in ps if ps[n].grad is not None}}
+
+    prev = lib.fetode_backward_set_v7(-1)
+    try:
+        t6 = torch.from_numpy(g["t35"])[:6]
+        one, lane = gpu(0, t6), gpu(2, t6)
+        t2 = torch.from_numpy(g["t35"])[:2]
+        lane2 = gpu(2, t2)
+    finally:
+        lib.fetode_backward_set_v7(prev)
+    for n in one:
+        assert_grad_close(lane[n], one[n], n, rel=1e-4)
+    e64, e32 = oracle(torch.float64, t2), oracle(torch.float32, t2)
+    for n in e64:
+        scale = e64[n].abs().max().item()
+        err = (lane2[n].double() - e64[n]).abs().max().item()
+        yard = (e32[n] - e64[n]).abs().max().item()
+        assert err <= 4 * yard + 1e-4 * scale, f"{n}: |gpu-fp64|={err:.3e} ref32 {yard:.3e} scale {scale:.3e}"
+
+
 def test_fused_backward_deterministic(dev, bwd_split):
     """Two identical training solves give bitwise-identical gradients (fixed-order reductions)."""
     import fet_ode_amd as F
