@@ -224,7 +224,9 @@ def train_rate(model, y0d, t, iters, warmup, world, strong=True):
         opt = torch.optim.Adam(m.parameters(), lr=1e-4, fused=True, capturable=capturable)
 
         def it():
-            opt.zero_grad(set_to_none=False)
+            # the reference's optimizer.zero_grad() (set_to_none=True, torch's default): autograd
+            # then keeps the fused backward's gradient views as .grad (no per-parameter add kernels)
+            opt.zero_grad(set_to_none=True)
             sol = F.odeint(func, y0d, t, method="rk4")
             loss = (sol - target).square().mean()
             loss.backward()

@@ -5,8 +5,12 @@ Adam.step) issues ~40 host calls per iteration; on a slow or contended host thei
 host issues one graph launch.
 
 The captured step must be shape-static and host-sync-free: inputs in fixed tensors (copy new data
-into them between replays), ``optimizer.zero_grad(set_to_none=False)``, an optimizer built with
-``capturable=True`` (torch.optim.Adam(..., fused=True, capturable=True)), no ``.item()``.  Every
+into them between replays), an optimizer built with ``capturable=True`` (torch.optim.Adam(...,
+fused=True, capturable=True)), no ``.item()``.  ``optimizer.zero_grad()`` may set the gradients to
+None (torch's default, the reference's call): the captured backward then allocates them once from
+the graph's pool and every replay writes the same buffers — and autograd keeps the fused backward's
+gradient views as ``.grad`` instead of adding them into zeroed tensors (one add kernel per
+parameter with ``set_to_none=False``: 24 of them per LV iteration, ≈ 10 % of it).  Every
 replay re-runs everything the eager iteration runs, in the same order — the parameter plan rebuild
 included (it is forced into the capture) — so replays are bitwise the eager iterations
 (tools/diag/train_graph2.py).

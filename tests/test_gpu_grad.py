@@ -567,7 +567,8 @@ def test_fused_solve_follows_fused_adam_steps(dev):
         assert torch.equal(a, b)
 
 
-def test_captured_training_step_matches_eager(dev):
+@pytest.mark.parametrize("set_to_none", [False, True])
+def test_captured_training_step_matches_eager(dev, set_to_none):
     """fet_ode_amd.training.CapturedStep: the whole iteration (fused solve with tape, MSE, the
     reverse sweep, the gradient reduction, fused capturable Adam) as one HIP graph; after the
     constructor's warm-up iterations and k replays the parameters are bitwise those of the same
@@ -589,7 +590,7 @@ def test_captured_training_step_matches_eager(dev):
         func = F.autonomous(m)
 
         def it():
-            opt.zero_grad(set_to_none=False)
+            opt.zero_grad(set_to_none=set_to_none)
             loss = (F.odeint(func, y0, t, method="rk4") - target).square().mean()
             loss.backward()
             opt.step()
