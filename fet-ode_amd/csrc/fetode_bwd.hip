@@ -1668,6 +1668,7 @@ __global__ __launch_bounds__(64) void grad_apply_kernel(const double* __restrict
 }
 
 #include "fetode_sweep7.h"
+#include "fetode_kansum.h"
 
 typedef void (*bwd_fn)(BwdArgs);
 typedef void (*dopri_bwd_fn)(DopriBwdArgs);
@@ -1682,7 +1683,9 @@ struct BwdEntry {
   dopri_bwd_fn dopri1;         // the same, one trajectory per wave: half the VJP jobs per lane
                                // (latency) where the batch leaves the grid room (small B)
   bwd_fn fn1;                  // fn at one trajectory per wave (small B), or null
-  bwd_fn v7;                   // the lane-group sweep (two trajectories per wave), or null
+  bwd_fn v7, v7s;              // the lane-group sweep (two trajectories per wave): Ferro sums + the
+                               // recorded adjoints (then ks), or every sum in the sweep; or null
+  bwd_fn ks;                   // the KAN sums over all samples after v7 (kansum_kernel)
 };
 const BwdEntry kBwd[] = {
     // LV KAN-FET [2,10,2]: one kernel, two trajectories per wave (measured: TPW 1 / 2 / 4 = 1034 / 897 /
@@ -1697,11 +1700,11 @@ const BwdEntry kBwd[] = {
      dopri_bwd_kernel<2, 10, 10, 10, 12, true, 2>, 2, dopri_bwd_kernel<2, 10, 10, 10, 12, true, 1>,
      fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 1>,
 #endif
-     sweep7_kernel},
+     sweep7_kernel<false>, sweep7_kernel<true>, kansum_kernel},
     // LV KAN [2,10,2] (126 VGPRs: four waves per SIMD already)
     {2, 10, 0, 10, 12, false, 1, fixed_bwd_kernel<2, 10, 1, 10, 12, false, true, 1>, nullptr, nullptr, nullptr,
      dopri_bwd_kernel<2, 10, 1, 10, 12, false, 2>, 2, dopri_bwd_kernel<2, 10, 1, 10, 12, false, 1>, nullptr,
-     nullptr},
+     nullptr, nullptr, nullptr},
 };
 // Which path the KAN-FET sweep takes (fetode_backward_set_split; env FETODE_BWD_SPLIT).  Default:
 // the one-kernel sweep — measured on MI355X at B = 4096, rk4, 34 steps: one kernel 1.06 ms vs the
@@ -1717,7 +1720,10 @@ bool use_split(const BwdEntry* e) {
 constexpr int64_t kSumBlocks = 1024;  // param_sum_kernel blocks per layer (= partial rows)
 // The lane-group sweep (sweep7_kernel; fetode_backward_set_v7, env FETODE_BWD_V7):
 // 0 = off, 1 = where the one-kernel sweep would run two trajectories per wave (the default),
-// 2 = at every batch.
+// 2 = at every batch; + 4: the sweep keeps the Ferro sums only and records each evaluation's
+// adjoints, kansum_kernel forms the KAN sums over all samples afterwards (measured at B = 4096:
+// 386 + 109 us vs 496 us with every sum in the sweep — kansum recomputes the features; kept as
+// the alternative).
 int g_bwd_v7 = -1;
 int v7_mode() {
   if (g_bwd_v7 < 0) {
@@ -1837,13 +1843,14 @@ int fixed_tpw(const BwdEntry* e, int64_t B) {
 
 bool use_v7(const BwdEntry* e, int64_t B) {
   if (!e->v7 || use_split(e)) return false;
-  const int m = v7_mode();
+  const int m = v7_mode() & 3;
   return m >= 2 || (m == 1 && fixed_tpw(e, B) == 2);
 }
+bool v7_offload(const BwdEntry* e, int64_t B) { return use_v7(e, B) && (v7_mode() & 4); }
 // partial rows of the chosen path: one per wave (the one-kernel and lane-group sweeps) or per
 // param_sum block (split)
 int64_t sum_rows(const BwdEntry* e, int64_t B, int64_t n_ev) {
-  if (use_v7(e, B)) return bwd_rows(B, 2);
+  if (use_v7(e, B)) return bwd_rows(B, 2) + (v7_offload(e, B) ? s7::kKsRows : 0);
   if (!use_split(e)) return bwd_rows(B, fixed_tpw(e, B));
   const int64_t tiles = (n_ev * B + kPsTS - 1) / kPsTS;
   return tiles < kSumBlocks ? (tiles > 0 ? tiles : 1) : kSumBlocks;
@@ -1859,7 +1866,7 @@ int64_t fetode_integrate_fixed_backward_workspace(const fetode_field_t* f, int32
   const int64_t n_ev = n_evals_of(method, n_steps);
   const int64_t nrow = sum_rows(e, B, n_ev);
   const int64_t nch = nrow < kChunks ? nrow : kChunks;
-  const int64_t adj = use_split(e) ? n_ev * B * (f->kan[0].in_features + f->kan[0].out_features) : 0;
+  const int64_t adj = use_split(e) || v7_offload(e, B) ? n_ev * B * (f->kan[0].in_features + f->kan[0].out_features) : 0;
   return (int64_t)sizeof(double) * nacc * (nch + 1) + (int64_t)sizeof(float) * (nrow * nacc + adj);
 }
 
@@ -1895,7 +1902,7 @@ int fetode_integrate_fixed_backward(const fetode_field_t* f, const void* plan, i
   double* S = (double*)workspace;
   double* chunks = S + nacc;
   float* part = (float*)(chunks + nch * nacc);
-  float* gadj = part + nrow * nacc;  // (n_ev, B, D + H), split path only
+  float* gadj = part + nrow * nacc;  // (n_ev, B, D + H): the split and lane-group (+ kansum) paths
 
   BwdArgs a;
   memset(&a, 0, sizeof(a));
@@ -1925,8 +1932,16 @@ int fetode_integrate_fixed_backward(const fetode_field_t* f, const void* plan, i
   a.nacc = nacc;
   a.gadj = gadj;
   if (use_v7(e, B)) {   // two trajectories per wave, one partial row per wave
-    hipLaunchKernelGGL(e->v7, dim3((unsigned)(nrow / kTPB)), dim3(64 * kTPB), 0, s, a);
+    const bool off = v7_offload(e, B);
+    const int64_t nw = bwd_rows(B, 2);
+    hipLaunchKernelGGL(off ? e->v7 : e->v7s, dim3((unsigned)(nw / kTPB)), dim3(64 * kTPB), 0, s, a);
     LAUNCH_CHECK();
+    if (off) {   // the KAN sums: kKsRows more partial rows (both layers' halves)
+      BwdArgs a2 = a;
+      a2.part = part + nw * nacc;
+      hipLaunchKernelGGL(e->ks, dim3((unsigned)s7::kKsRows, 2), dim3(64 * s7::kKsWaves), 0, s, a2);
+      LAUNCH_CHECK();
+    }
   } else if (split) {
     // adjoint sweep: one wave per trajectory, every trajectory resident (grid-stride beyond)
     const int64_t blocks = (B + kTPB - 1) / kTPB;

@@ -134,6 +134,9 @@ __device__ __forceinline__ float single_vjp(float Ec, float k2, float cPk, float
 }
 }  // namespace s7
 
+// KS = true: the KAN sums as well (per-wave LDS slots, above); KS = false: the Ferro sums only, each
+// evaluation's adjoints (g_0, g_1, d loss / d h) recorded in a.gadj for kansum_kernel
+template <bool KS>
 __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) void sweep7_kernel(BwdArgs a) {
   using namespace s7;
   using L0 = BL<D, H, K, NB, NG, true>;
@@ -337,7 +340,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
               const float wo = wc0 * (1.0f - sgx);
               V.gx[hh][xi] = make_float4(x, sgx, wo, F_ ? ex2(gl0 * x) : 0.f);
             }
-            if (q >= NB + 2) {   // base rb of the interval (the row's sums: only on in-grid x)
+            if (KS && q >= NB + 2) {   // base rb of the interval (the row's sums: only on in-grid x)
               const bool fin = __builtin_isfinite(x), in = fin && (unsigned)m < (unsigned)NI;
               const int mc = in ? m : 0;
               const float u = in ? (x - TI.knots[xi * NG + mc]) * TI.rh[xi * NI + mc] : 0.f;
@@ -360,7 +363,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
               const float der = sl ? sg * ffma(h, 1.0f - sg, 1.0f) : ffma(-sg, sg, sg);
               const float Tt = ffma(g01.x, jw.x, g01.y * jw.y) * der;
               // sums: logistic weights of both outputs (SiLU job: base weights), a, b
-              if (!(S7_SKIP & 1)) {
+              if (KS && !(S7_SKIP & 1)) {
               ks[64 * (S_LW1 + 2 * r)] = ffma(g01.x, val, ks[64 * (S_LW1 + 2 * r)]);
               ks[64 * (S_LW1 + 2 * r + 1)] = ffma(g01.y, val, ks[64 * (S_LW1 + 2 * r + 1)]);
               ks[64 * (S_LA1 + r)] = ffma(Tt, h - jf.w, ks[64 * (S_LA1 + r)]);
@@ -387,7 +390,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
             const float4 cf = sp1e[in ? m : NI];
             const float ge = sok ? (cc0 == 0 ? g01.x : g01.y) : 0.f;
             dh = ffma(ge, dcubic(cf, u) * rhm, dh);
-            if (!(S7_SKIP & 2)) {   // spline sums of edge (o -> cc0): the interval's four bases
+            if (KS && !(S7_SKIP & 2)) {   // spline sums of edge (o -> cc0): the interval's four bases
               const float4* bp = &TI.bp[TI.bpi(t1, mc)];
 #pragma unroll
               for (int r = 0; r < 4; ++r) {
@@ -409,9 +412,14 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
                                    c1 ? ee.y : ee.x, ge, h, up, wo, E, gl1, As1, Cs1, Es1);
             }
           }
-          G1 += g01;
+          if (KS) G1 += g01;
           const float g0o = act ? g3f(dh, cc0) : 0.f;   // d loss / d h_o on the group (lane 15: none)
           if (act && cc0 == 0) V.g0[hh][o] = g0o;
+          if (!KS && live) {   // this evaluation's adjoints for kansum_kernel
+            float* gr = a.gadj + ((int64_t)ev * a.B + b) * W;
+            if (q == 15) gr[row] = ak[st];
+            if (act && cc0 == 0) gr[D + o] = g0o;
+          }
           // ---- (3) layer 0 on the group of output o ----
           f2 dx01 = splat(0.f);
           {
@@ -438,7 +446,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
             const float4 fx = V.fx[hh][ie], bx = V.bx[hh][ie];
             const int mx = V.mx[hh][ie];
             const int mc = mx < NI ? mx : 0;
-            if (!(S7_SKIP & 16)) {
+            if (KS && !(S7_SKIP & 16)) {
             bs0 = ffma(ge, fx.x, bs0);
             acc0[mc + 0] = ffma(ge, bx.x, acc0[mc + 0]);
             acc0[mc + 1] = ffma(ge, bx.y, acc0[mc + 1]);
@@ -449,7 +457,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
             const float4 cf = sp0e[mx];
             const float dxe = ge * ffma(kbase0, fx.y, dcubic(cf, fx.z) * fx.w);
             dx01 = pfma(dsel, splat(dxe), dx01);   // lane 0: input 0, lane 1: input 1, lane 2: 0
-            G0 += sok && cc0 == 0 ? g0o : 0.f;
+            if (KS) G0 += sok && cc0 == 0 ? g0o : 0.f;
           }
           // ---- (4) layer-0 logistic (i = xi, j = q) for all ten outputs: sums, d / dx_i ----
           {
@@ -460,13 +468,13 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
               const f2 kv = *reinterpret_cast<const f2*>(&kwo[oo]);
               S = ffma(gv.x, kv.x, S);
               S = ffma(gv.y, kv.y, S);
-              if (!(S7_SKIP & 4)) {
+              if (KS && !(S7_SKIP & 4)) {
               ks[64 * (S_LW0 + oo)] = ffma(gv.x, sgx, ks[64 * (S_LW0 + oo)]);
               ks[64 * (S_LW0 + oo + 1)] = ffma(gv.y, sgx, ks[64 * (S_LW0 + oo + 1)]);
               }
             }
             const float Tt = (S * kwm) * ffma(-sgx, sgx, sgx);
-            if (!(S7_SKIP & 8)) {
+            if (KS && !(S7_SKIP & 8)) {
             ks[64 * S_LA0] = ffma(Tt, cx - pb0, ks[64 * S_LA0]);
             ks[64 * S_LB0] = ffma(-Tt, pa0, ks[64 * S_LB0]);
             }
@@ -526,6 +534,11 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
       part[A0L.oA + es0] = a0; part[A0L.oC + es0] = c0; part[A0L.oE + es0] = x0;
       part1[A1L.oA + es1] = a1; part1[A1L.oC + es1] = c1; part1[A1L.oE + es1] = x1;
     }
+  }
+  if constexpr (!KS) {   // the KAN slots of both layers: kansum_kernel's rows hold them
+    for (int i = 3 * A0L.E + lane; i < A0L.n; i += 64) part[i] = 0.f;
+    for (int i = 3 * A1L.E + lane; i < A1L.n; i += 64) part1[i] = 0.f;
+    return;
   }
   {
     const float g0t = G0 + partner(G0), g1x = G1.x + partner(G1.x), g1y = G1.y + partner(G1.y);

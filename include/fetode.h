@@ -388,11 +388,13 @@ int fetode_fused_backward_supported(const fetode_field_t* field);
  * parameter sums of each layer in parallel over the samples).  Same results up to fp32 summation
  * order.  Returns the previous setting; enable < 0 only queries.  Call before sizing workspaces. */
 int fetode_backward_set_split(int32_t enable);
-/* The [2, 10, 2] KAN-FET sweep on the forward's lane groups (sweep7_kernel: the Ferro sums and the
- * adjoints, each evaluation's adjoints recorded; then the KAN sums of each layer over all samples):
+/* The [2, 10, 2] KAN-FET sweep on the forward's lane groups (sweep7_kernel: the adjoints and every
+ * parameter-gradient sum in one launch):
  * 0 = off (the one-kernel sweep), 1 = where the one-kernel sweep would run two trajectories per wave
- * (the default), 2 = at every batch.  Same results up to fp32 summation order.  Returns the
- * previous setting; mode < 0 only queries.  Call before sizing workspaces. */
+ * (the default), 2 = at every batch; + 4 = the sweep keeps the Ferro sums only and a second launch
+ * forms the KAN sums over every recorded (evaluation, trajectory) sample.  Same results up to fp32
+ * summation order.  Returns the previous setting; mode < 0 only queries.  Call before sizing
+ * workspaces. */
 int fetode_backward_set_v7(int32_t mode);
 /* Workspace bytes for fetode_integrate_fixed_backward of a (method, n_steps) forward at batch B
  * (the split path records every evaluation's adjoints: n_evals * B * (D + H) floats of it). */

@@ -44,14 +44,14 @@ def kernel_switch():
     lib.fetode_fused_set_small_batch_max(prev)
 
 
-@pytest.fixture(params=[0, 1, 2], ids=["one-kernel", "split", "lane-sweep"])
+@pytest.fixture(params=[0, 1, 2, 6], ids=["one-kernel", "split", "lane-sweep", "lane-sweep-kansum"])
 def bwd_split(request):
     """Run a fused-backward test through each sweep structure: the one-kernel sweep, the split
-    (fetode_backward_set_split, diagnostic build) and the lane-group sweep + KAN sums at every batch
-    (fetode_backward_set_v7(2))."""
+    (fetode_backward_set_split, diagnostic build), the lane-group sweep at every batch
+    (fetode_backward_set_v7(2)) and the same with the KAN sums in kansum_kernel (mode 6)."""
     from fet_ode_amd import _lib
     lib = _lib.load()
-    prev_v7 = lib.fetode_backward_set_v7(2 if request.param == 2 else 0)
+    prev_v7 = lib.fetode_backward_set_v7(request.param if request.param in (2, 6) else 0)
     prev = lib.fetode_backward_set_split(1 if request.param == 1 else 0)
     if prev == -2:
         lib.fetode_backward_set_v7(prev_v7)

@@ -403,7 +403,7 @@ def test_lane_sweep_matches_one_kernel_bench_horizon(dev, B):
     res = []
     prev = lib.fetode_backward_set_v7(-1)
     try:
-        for mode in (0, 2):
+        for mode in (0, 2, 6):   # one kernel; the lane sweep; the lane sweep + kansum_kernel
             lib.fetode_backward_set_v7(mode)
             m = F.KANFET([2, 10, 2], grid_size=5)
             m.load_state_dict(sd)
@@ -415,6 +415,7 @@ def test_lane_sweep_matches_one_kernel_bench_horizon(dev, B):
         lib.fetode_backward_set_v7(prev)
     for n in res[0]:
         assert_grad_close(res[1][n], res[0][n], n, rel=1e-4)
+        assert_grad_close(res[2][n], res[0][n], n + " (kansum)", rel=1e-4)
 
 
 def test_lane_sweep_off_grid_inputs(dev):
