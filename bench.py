@@ -55,8 +55,11 @@ ALG_FLOPS_PER_TRAJ_STEP = 50_000   # ~50k flops (+5.8k transcendent
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
+    # defaults: the GPU's clocks settle within ~100 back-to-back solves (the first 100 average 181 us,
+    # every later block of 100 170.0-170.7 us: tools/diag/clock_ramp.py, profiles/r05_clock_ramp.log),
+    # so 200 untimed solves (~35 ms) precede 500 timed ones (~85 ms)
+    ap.add_argument("--steps", type=int, default=500)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
                     help="strong: global batch 4096 split over the ranks (the contract line); "
                          "weak: 4096 trajectories per rank")

@@ -8,5 +8,5 @@ step bench timeout -k 10 600 python bench.py
 tail -1 $O/bench.log > $O/bench_$R.json
 cat $O/bench_$R.json | head -c 600; echo
 [ -n "$NO_PROF" ] && exit 0
-step prof_stats timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$R -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --train-iters 5
+step prof_stats timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$R -o run --output-format csv -- python3 bench.py --steps 200 --warmup 100 --no-cpu-baseline --train-iters 20
 rm -f $O/prof_$R/run_kernel_trace.csv

@@ -16,7 +16,7 @@ step bench timeout -k 10 600 python bench.py
 tail -1 $O/bench.log > $O/bench_$R.json
 cat $O/bench_$R.json
 [ -n "$NO_PROF" ] && exit 0
-step prof_stats timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$R -o run --output-format csv -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --train-iters 5
+step prof_stats timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof_$R -o run --output-format csv -- python3 bench.py --steps 200 --warmup 100 --no-cpu-baseline --train-iters 20
 # keep gpurun_out small (it is merged back only below 64 MiB): the stats CSV, not the traces
 f=$(find $O/prof_$R -name '*kernel_stats.csv' | head -1); [ -n "$f" ] && cp "$f" $O/${R}_kernel_stats.csv
 rm -rf $O/prof_$R
