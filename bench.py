@@ -1076,16 +1076,20 @@ def main():
                        "parallelism": f"trajectory-sharded x{world} (no collective)"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": ("fused4_kernel<10,10,10,12,true,true,false,false> (v4 rk4 path)" if Bl > 512
-                                    else "small6_kernel<true,true,false,false> (v6 small-batch rk4 path)"),
+                         "kernel": ("fused4_kernel<10,10,10,12,true,true,false,false,2> (v7 rk4, two trajectories per wave)"
+                                    if Bl > 1024 else
+                                    "fused4_kernel<10,10,10,12,true,true,false,false,1> (v7 rk4, one trajectory per wave)"
+                                    if Bl > 320 else "small6_kernel<true,true,false,false> (v6 small-batch rk4 path)"),
                          "kernel_ms": k_ms, "alg_bytes_per_launch": bytes_launch,
                          "traffic_source": traffic_src,
                          "valu": {"achieved_tflops": tflops, "peak_tflops": FP32_PEAK_TFLOPS,
                                   "frac": tflops / FP32_PEAK_TFLOPS,
                                   "alg_flops_per_launch": flops_launch},
                          # the kernel's actual bound: the SIMDs' VALU issue (PMC, committed profile)
-                         "issue": pmc_issue("fused4_kernel<10, 10, 10, 12, true, true, false, false>" if Bl > 512
-                                            else "small6_kernel<true, true, false, false>")},
+                         "issue": (pmc_issue("fused4_kernel<10, 10, 10, 12, true, true, false, false, 2>")
+                                   or pmc_issue("fused4_kernel<10, 10, 10, 12, true, true, false, false>")) if Bl > 1024
+                                  else pmc_issue("fused4_kernel<10, 10, 10, 12, true, true, false, false, 1>") if Bl > 320
+                                  else pmc_issue("small6_kernel<true, true, false, false>")},
             # north_star: "MFMA utilisation against chip peak" — the path's MFMA kernels (the LV field
             # itself has no GEMM-shaped work): the ETT wide KAN-FET layer and the MNIST
             # KANLinear head, from the committed PMC pass (tools/pmc_issue.py)

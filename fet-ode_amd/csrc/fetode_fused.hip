@@ -348,7 +348,12 @@ __device__ __forceinline__ float v4_edges(const V4Lds<IN, FLEN>& L, const float*
 // HOT = true: the rk4 (3/8) integrate path only, every stage inlined, outputs predicated;
 // HOT = false: single evaluations and every other method.  At least 2 waves per SIMD in every
 // variant: the resident dopri5 grid (DOPRI) needs B / 2 co-resident waves.
-template <int H, int K_, int NB, int NG, bool FERRO, bool HOT, bool DOPRI = false, bool TAPE = false>
+// TPW = 1 (inference, mid batches): ONE trajectory per wave — each hidden unit's group is 6 lanes, the
+// 3 of the v7 map in each half-wave, and the halves split its Ferro pairs and feature rounds (per-lane
+// constants: no divergence); the halves' partial sums meet with one v_permlane32_swap each (the same
+// sum, in the same order, on both halves).  Half the pair rounds per lane: a shorter dependent chain
+// per evaluation where the waves do not fill the SIMDs.
+template <int H, int K_, int NB, int NG, bool FERRO, bool HOT, bool DOPRI = false, bool TAPE = false, int TPW = 2>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fused4_kernel(FusedArgs a) {
   constexpr int D = 2, NI = NG - 1, NFL = 1 + NB, NFP = (NFL + 1) & ~1, K = FERRO ? K_ : 0;
   // feature jobs: logistic 0..NB-1, SiLU, [gate, exp(gs x)], then x / u / m stores
@@ -358,19 +363,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   static_assert(H <= 10, "v4 layout: H <= 10 groups of 3 lanes");
   static_assert(!FERRO || K % 2 == 0, "v4 pairs Ferro elements (i, k), (i, k+1)");
   constexpr int KP = K / 2 > 0 ? K / 2 : 1;
+  static_assert(TPW == 2 || (TPW == 1 && HOT && !DOPRI && !TAPE), "one trajectory per wave: the rk4 inference path");
+  constexpr int NLG = TPW == 2 ? 3 : 6;                      // lanes per hidden unit
   // layer 0 (2 -> H): output o on a group of 3 lanes; layer 1 (H -> 2): hidden INPUT o on the
   // same group (v7): its features, its Ferro elements of both outputs (pairs (o, 0, k), (o, 1, k):
   // one packed pair feeds both output sums) and its two spline edges stay in the group's
   // registers — no LDS exchange between layer 0 and layer 1
-  using FS0 = FerroSplit<D * KP, 3>;
+  using FS0 = FerroSplit<D * KP, NLG>;
   static_assert(!FERRO || D == 2, "v7 layer 1 pairs the two outputs of an input");
-  constexpr int REM1 = K % 3;
-  constexpr bool SPLIT1 = REM1 == 1;                         // one k left: two singles (d = 0, 1)
-  constexpr int NPL0 = FERRO ? FS0::NPL : 0, NPL1 = FERRO ? (SPLIT1 ? K / 3 : (K + 2) / 3) : 0;
+  constexpr int REM1 = K % NLG;
+  constexpr bool SPLIT1 = TPW == 2 && REM1 == 1;             // one k left: two singles (d = 0, 1)
+  constexpr int NPL0 = FERRO ? FS0::NPL : 0, NPL1 = FERRO ? (SPLIT1 ? K / NLG : (K + NLG - 1) / NLG) : 0;
   constexpr int NSL0 = FERRO ? FS0::NSL : 0, NSL1 = (FERRO && SPLIT1) ? 1 : 0;
-  constexpr int FPL0 = ((D * NFP + 2) / 3 + 3) & ~3;
-  constexpr int RF1 = (NFL + 2) / 3;                         // feature rounds of a hidden input (SiLU + NB)
-  constexpr int FLEN0 = (3 * FPL0 > D * NFP ? 3 * FPL0 : D * NFP);
+  constexpr int FPL0 = ((D * NFP + NLG - 1) / NLG + 3) & ~3;
+  constexpr int RF1 = (NFL + NLG - 1) / NLG;                 // feature rounds of a hidden input (SiLU + NB)
+  constexpr int FLEN0 = (NLG * FPL0 > D * NFP ? NLG * FPL0 : D * NFP);
   if constexpr (DOPRI) {
     if (a.dp.xr_world > 1 && blockIdx.x == gridDim.x - 1) {   // the cross-rank exchange workgroup
       xrank_comm(a.dp);
@@ -385,11 +392,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   __shared__ __attribute__((aligned(16))) float s_sp1[SPT1];
   __shared__ __attribute__((aligned(8))) f2 s_kr0[D * (NI + 1)], s_kr1[H * (NI + 1)];
   __shared__ float s_c0[H], s_c1[D];
-  __shared__ __attribute__((aligned(16))) V4Lds<D, FLEN0> s_L0[2];
+  __shared__ __attribute__((aligned(16))) V4Lds<D, FLEN0> s_L0[TPW];
 
   const int tid = threadIdx.x;
-  const int g = tid >> 5, lane = tid & 31, row = lane >> 4, c1 = lane & 15;
-  const int64_t b = (int64_t)blockIdx.x * 2 + g;
+  const int hh = tid >> 5;                                   // half-wave
+  const int g = TPW == 2 ? hh : 0, lane = tid & 31, row = lane >> 4, c1 = lane & 15;
+  const int64_t b = (int64_t)blockIdx.x * TPW + g;
+  const bool own = TPW == 2 || hh == 0;                      // TPW 1: half 0 stores
   const bool valid = b < a.B;
   V4Lds<D, FLEN0>& L0 = s_L0[g];
 
@@ -415,11 +424,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   const int o0 = row * 5 + q / 3, cc0 = q % 3;
   const bool act0 = q < 15 && o0 < H;
   const int o0c = act0 ? o0 : 0;
+  const int gl = TPW == 2 ? cc0 : cc0 + 3 * hh;              // lane within the hidden unit's group
   f2 ep0[NPL0 > 0 ? NPL0 : 1], k20[NPL0 > 0 ? NPL0 : 1], kE0[NPL0 > 0 ? NPL0 : 1], cp0[NPL0 > 0 ? NPL0 : 1];
   int gi0[NPL0 > 0 ? NPL0 : 1];
 #pragma unroll
   for (int r = 0; r < NPL0; ++r) {
-    const int P = cc0 * NPL0 + r;
+    const int P = gl * NPL0 + r;
     const bool ok = act0 && P < D * KP;
     int i = ok ? P / KP : 0;
     asm volatile("" : "+v"(i));  // keep in a VGPR (no per-evaluation rematerialisation)
@@ -443,10 +453,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   int gs0 = 0;
   float es0 = 0.f, k2s0 = 0.f, kEs0 = 0.f, cps0 = 0.f;
   if constexpr (NSL0 > 0) {
-    const int Pl = NPL0 * 3 + cc0 / 2;
-    const bool ok = act0 && cc0 < 2 * FS0::REM;
+    const int Pl = NPL0 * NLG + gl / 2;
+    const bool ok = act0 && gl < 2 * FS0::REM;
     const int i = ok ? Pl / KP : 0;
-    const int64_t idx = (int64_t)o0c * (D * K) + i * K + (ok ? (Pl % KP) * 2 + cc0 % 2 : 0);
+    const int64_t idx = (int64_t)o0c * (D * K) + i * K + (ok ? (Pl % KP) * 2 + gl % 2 : 0);
     const float gec = ok ? a.plan[a.P0.fe_GEc + idx] : 0.f;
     es0 = fact ? ex2(gec) : gec;
     k2s0 = ok ? a.plan[a.P0.fe_k2 + idx] : 0.f;
@@ -461,17 +471,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
     float w[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int qq = cc0 * FPL0 + f + h, i = qq / NFP, ff = qq % NFP;
+      const int qq = gl * FPL0 + f + h, i = qq / NFP, ff = qq % NFP;
       w[h] = (act0 && i < D && ff < NFL) ? a.plan[a.P0.kw + (int64_t)o0c * (D * NFL) + i * NFL + ff] : 0.f;
     }
     fw0[f / 2] = f2{w[0], w[1]};
   }
-  // ---- layer-1 (v7): hidden input o0 on its group; lane cc0 owns k = cc0 + 3 r ----
+  // ---- layer-1 (v7): hidden input o0 on its group; lane gl owns k = gl + NLG r ----
   // pair r: elements (o0, d = 0, k) and (o0, d = 1, k): .x feeds output 0, .y output 1
   f2 ep1[NPL1 > 0 ? NPL1 : 1], k21[NPL1 > 0 ? NPL1 : 1], kE1[NPL1 > 0 ? NPL1 : 1], cp1[NPL1 > 0 ? NPL1 : 1];
 #pragma unroll
   for (int r = 0; r < NPL1; ++r) {
-    const int k = cc0 + 3 * r;
+    const int k = gl + NLG * r;
     const bool ok = act0 && k < K;
     float t[4][2];
 #pragma unroll
@@ -500,13 +510,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
     cps1 = ok ? a.plan[a.P1.fe_CPs2 + idx] : 0.f;
   }
   // lane cc0 = d < 2 also owns the spline edge (o0 -> d): the single / spline value goes to output d
-  const f2 dsel1 = f2{(act0 && cc0 == 0) ? 1.f : 0.f, (act0 && cc0 == 1) ? 1.f : 0.f};
+  const f2 dsel1 = f2{(act0 && gl == 0) ? 1.f : 0.f, (act0 && gl == 1) ? 1.f : 0.f};
   // feature rounds: job j = cc0 + 3 r (logistic j < NB, SiLU j == NB), its weights for both outputs
   float fna1[RF1], fab1[RF1], fml1[RF1];
   f2 fwt1[RF1];
 #pragma unroll
   for (int r = 0; r < RF1; ++r) {
-    const int j = cc0 + 3 * r;
+    const int j = gl + NLG * r;
     const bool ok = act0 && j < NFL;
     fna1[r] = 0.f; fab1[r] = 0.f; fml1[r] = 0.f;
     const int ff = j < NB ? 1 + j : 0;   // kw feature index: SiLU 0, logistic j at 1 + j
@@ -571,18 +581,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   bool re0 = FERRO && (a.init_mask & 1u), re1 = FERRO && (a.init_mask & 2u);
 
   float y = valid ? a.y0[b * D + row] : 0.f;   // state dim `row`, replicated over the row
-  if (!a.single_eval && valid && c1 == 0) a.solution[b * D + row] = y;
+  if (!a.single_eval && valid && own && c1 == 0) a.solution[b * D + row] = y;
   __syncthreads();  // tables staged
 
   STAMP_DECL
   const float c0o = s_c0[o0c], c1o = s_c1[row];  // per-output constants, held in registers
   const float* sp0_o = &s_sp0[o0c * D * (NI + 1) * 4];
   // layer 1: the cubic table of edge (o0 -> d = cc0) and the (knot, 1/width) rows of input o0
-  const float* sp1_e = &s_sp1[((cc0 < D ? cc0 : 0) * H + o0c) * (NI + 1) * 4];
+  const float* sp1_e = &s_sp1[((gl < D ? gl : 0) * H + o0c) * (NI + 1) * 4];
   const f2* kr1_o = &s_kr1[o0c * (NI + 1)];
-  const int fofs0 = cc0 * FPL0;
-  const bool spl0 = act0 && cc0 < D;  // lanes owning a layer-0 spline edge (input si)
-  const int si0 = spl0 ? cc0 : 0;
+  const int fofs0 = gl * FPL0;
+  const bool spl0 = act0 && gl < D;  // lanes owning a layer-0 spline edge (input si)
+  const int si0 = spl0 ? gl : 0;
 
   // training tape: the two layer inputs of evaluation `ev` at tape[(ev B + b)(D + H) + c]
   // uniform: the inference path skips every tape op (the dopri5 driver has a taped instantiation
@@ -626,6 +636,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
     float h = v4_edges<D, FLEN0, NI, NPL0, NSL0, FPL0, FERRO, F_>(L0, sp0_o, s_kr0, gi0, ep0, k20, kE0, cp0, fw0,
                                                                   fofs0, spl0, si0, a.P0.gsl2e, gs0, es0, k2s0, kEs0,
                                                                   cps0);
+    if constexpr (TPW == 1) {   // the two halves' partial edge sums (the same sum on both halves)
+      float p = h, q2 = h;
+      permlane32_swap(p, q2);
+      h = p + q2;
+    }
     h = group3_sum(h, cc0) + c0o;   // lane 15 of a row (no group) is never read by a group
     STAMP(2);
     FETODE_MARK("H_FEAT");
@@ -676,6 +691,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
     // output sums over the half-wave: the permlane16 swap folds the two rows of each output into
     // row d (rows 0 / 2: output 0, rows 1 / 3: output 1), a row sum finishes: k_row on row `row`
     float p0 = acc01.x, p1 = acc01.y;
+    if constexpr (TPW == 1) {   // the two halves' partials first (the same sums on both halves)
+      float p = p0, q2 = p0;
+      permlane32_swap(p, q2);
+      p0 = p + q2;
+      float r = p1, t = p1;
+      permlane32_swap(r, t);
+      p1 = r + t;
+    }
     permlane16_swap(p0, p1);
     const float kr = row_sum16(p0 + p1) + c1o;
     STAMP(5);
@@ -709,7 +732,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
 
   auto out_write = [&](int j, float v) __attribute__((always_inline)) {
 #ifndef FETODE_EXPERIMENT_NO_OUT
-    if (valid && c1 == 0) a.solution[((int64_t)j * a.B + b) * D + row] = v;
+    if (valid && own && c1 == 0) a.solution[((int64_t)j * a.B + b) * D + row] = v;
 #endif
   };
   using FT = std::integral_constant<bool, true>;
@@ -987,7 +1010,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
       }
     }
   }
-  if (FERRO && valid) {
+  if (FERRO && valid && own) {
     if (x_gate) a.state[b * D + row] = prev0;
     if (act0 && cc0 == 0) a.state[a.B * D + b * H + o0] = prev1;
   }
@@ -1562,6 +1585,7 @@ struct FusedEntry {
   fused_fn dopri_tape;  // the same, recording the training tape
   fused_fn small_dopri, small_dopri_tape;  // v6 with the dopri5 driver (small batches)
   fused_fn small_tape, small_rk4_tape;     // v6 recording the fixed-grid training tape
+  fused_fn fn_rk4_1;  // v7 rk4 at one trajectory per wave (inference, mid batches)
 };
 const FusedEntry kFused[] = {
     // LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146)
@@ -1569,13 +1593,13 @@ const FusedEntry kFused[] = {
      small6_kernel<true, false>, small6_kernel<true, true>, fused4_kernel<10, 10, 10, 12, true, false, true>,
      fused4_kernel<10, 10, 10, 12, true, false, true, true>, small6_kernel<true, false, true, false>,
      small6_kernel<true, false, true, true>, small6_kernel<true, false, false, true>,
-     small6_kernel<true, true, false, true>},
+     small6_kernel<true, true, false, true>, fused4_kernel<10, 10, 10, 12, true, true, false, false, 1>},
     // LV KAN [2,10,2] (predator_prey.py:101)
     {2, 10, 2, 1, 10, 12, false, fused4_kernel<10, 2, 10, 12, false, false>, fused4_kernel<10, 2, 10, 12, false, true>,
      small6_kernel<false, false>, small6_kernel<false, true>, fused4_kernel<10, 2, 10, 12, false, false, true>,
      fused4_kernel<10, 2, 10, 12, false, false, true, true>, small6_kernel<false, false, true, false>,
      small6_kernel<false, false, true, true>, small6_kernel<false, false, false, true>,
-     small6_kernel<false, true, false, true>},
+     small6_kernel<false, true, false, true>, fused4_kernel<10, 2, 10, 12, false, true, false, false, 1>},
 };
 
 // Batches up to kSmallMax take v6 (one trajectory per 3-wave workgroup, latency-bound chain split
@@ -1586,6 +1610,19 @@ int64_t g_small_max = [] {
   return e ? (int64_t)atoll(e) : (int64_t)512;  // measured switch point (tools/diag/batch_sweep.py)
 }();
 int64_t small_max() { return g_small_max; }
+// Inference rk4 batches in (g_tpw1_lo, g_tpw1_hi] take v7 at one trajectory per wave (before the
+// v6 / v4 choice; env FETODE_TPW1_LO / FETODE_TPW1_HI).  Measured (tools/diag/batch_sweep.py,
+// profiles/r05_t1w_sweep*.log, us per 34-step solve, v6 / one / two per wave): B = 256 77 / 93 / 114,
+// 384 98 / 97 / 114,
+// 512 101 / 97 / 113, 768 129 / 97 / 119, 1024 146 / 99 / 119, 1536 202 / 133 / 117.
+int64_t g_tpw1_lo = [] {
+  const char* e = getenv("FETODE_TPW1_LO");
+  return e ? (int64_t)atoll(e) : (int64_t)320;
+}();
+int64_t g_tpw1_hi = [] {
+  const char* e = getenv("FETODE_TPW1_HI");
+  return e ? (int64_t)atoll(e) : (int64_t)1024;
+}();
 uint32_t g_dp_spin_limit = 0;   // fetode_dopri5_set_spin_limit (0: the built-in limits)
 
 const FusedEntry* find_fused(const fetode_field_t* f) {
@@ -2052,7 +2089,9 @@ int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
   }();
   a.factor_limit = limit;
   const bool rk4 = !a.single_eval && a.method == FETODE_RK4;
-  if (a.B <= small_max()) {  // v6: one trajectory per 192-thread workgroup (training tapes too)
+  if (rk4 && !a.tape && a.B > g_tpw1_lo && a.B <= g_tpw1_hi) {   // v7, one trajectory per wave
+    hipLaunchKernelGGL(e->fn_rk4_1, dim3((unsigned)a.B), dim3(64), 0, (hipStream_t)stream, a);
+  } else if (a.B <= small_max()) {  // v6: one trajectory per 192-thread workgroup (training tapes too)
     const fused_fn fn = a.tape ? (rk4 ? e->small_rk4_tape : e->small_tape) : (rk4 ? e->small_rk4 : e->small);
     hipLaunchKernelGGL(fn, dim3((unsigned)a.B), dim3(192), 0, (hipStream_t)stream, a);
   } else {                              // v4: two trajectories per one-wave workgroup
@@ -2083,6 +2122,13 @@ uint32_t fetode_dopri5_set_spin_limit(uint32_t polls) {
 int64_t fetode_fused_set_small_batch_max(int64_t b) {
   const int64_t prev = g_small_max;
   if (b >= 0) g_small_max = b;
+  return prev;
+}
+
+int64_t fetode_fused_set_tpw1_range(int64_t lo, int64_t hi) {
+  const int64_t prev = g_tpw1_hi;
+  if (lo >= 0) g_tpw1_lo = lo;
+  if (hi >= 0) g_tpw1_hi = hi;
   return prev;
 }
 

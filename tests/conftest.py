@@ -33,15 +33,18 @@ def dev():
 
 @pytest.fixture
 def kernel_switch():
-    """Force the fused integrator's kernel: small(True) -> v6 at any batch, small(False) -> v4."""
+    """Force the fused integrator's kernel: small(True) -> v6 at any batch, small(False) -> v4 / v7 at
+    two trajectories per wave (the one-per-wave range is switched off meanwhile)."""
     from fet_ode_amd import _lib
     lib = _lib.load()
     prev = lib.fetode_fused_set_small_batch_max(-1)
+    prev_hi = lib.fetode_fused_set_tpw1_range(-1, 0)
 
     def small(on):
         lib.fetode_fused_set_small_batch_max(1 << 40 if on else 0)
     yield small
     lib.fetode_fused_set_small_batch_max(prev)
+    lib.fetode_fused_set_tpw1_range(-1, prev_hi)
 
 
 @pytest.fixture(params=[0, 1, 2, 6], ids=["one-kernel", "split", "lane-sweep", "lane-sweep-kansum"])

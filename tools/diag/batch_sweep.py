@@ -23,11 +23,13 @@ rows = []
 for B in [int(b) for b in os.environ.get("SWEEP_B", "1,64,256,512,1024,1536,2048,3072,4096,8192").split(",")]:
     y0 = bench.lv_y0(B, 0).to(dev)
     r = {"B": B}
-    for name, sm in (("v6", 1 << 40), ("v4", 0)):
+    for name, sm, t1 in (("v6", 1 << 40, 0), ("v7x1", 0, 1 << 40), ("v7x2", 0, 0)):
         lib.fetode_fused_set_small_batch_max(sm)
+        lib.fetode_fused_set_tpw1_range(0, t1)
         r[name + "_ms"] = bench.kernel_time_ms(m, y0, t)
     rows.append(r)
     print(json.dumps(r), flush=True)
-lib.fetode_fused_set_small_batch_max(2048)
+lib.fetode_fused_set_small_batch_max(512)
+lib.fetode_fused_set_tpw1_range(320, 1024)
 os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
 json.dump(rows, open(os.path.join(REPO, "gpurun_out", "batch_sweep.json"), "w"), indent=1)
