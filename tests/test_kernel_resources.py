@@ -100,6 +100,6 @@ CONTROL_SPILLS = {
     # dopri5 training: the taped forward and the KAN-FET reverse sweep sit at 255 /
     # 254 VGPRs; two or three per-lane 64-bit pointers live in scratch (checked in the ISA: <= 2
     # reloads per evaluation / per attempt, none in the Ferro VJP loops)
-    "_ZN12_GLOBAL__N_113fused4_kernelILi10ELi10ELi10ELi12ELb1ELb0ELb1ELb1EEEvNS_9FusedArgsE",
+    "_ZN12_GLOBAL__N_113fused4_kernelILi10ELi10ELi10ELi12ELb1ELb0ELb1ELb1ELi2EEEvNS_9FusedArgsE",
     "_ZN12_GLOBAL__N_116dopri_bwd_kernelILi2ELi10ELi10ELi10ELi12ELb1ELi2EEEvNS_12DopriBwdArgsE",
 }
