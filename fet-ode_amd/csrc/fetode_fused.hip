@@ -608,7 +608,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
     constexpr bool F_ = decltype(fact_tag)::value;
     STAMP(6);
     FETODE_MARK("X_FEAT");
-    if (taping && valid && c1 == 0) tape_b[row] = xin;
+    if (taping && valid && own && c1 == 0) tape_b[row] = xin;
     {
       // (1) layer-0 features of input `row`: one sigmoid-of-affine job per lane
       const float pv = x_gate ? (re0 ? xin : prev0) : 0.f;
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
       const float u = (h - kw.x) * kw.y;
       const float sv = ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
       acc01 = pfma(dsel1, splat(sgl + sv), acc01);   // lane d < 2: single + spline onto output d
-      if (taping && valid && act0 && cc0 == 0) tape_b[D + o0] = h;
+      if (taping && valid && own && act0 && cc0 == 0) tape_b[D + o0] = h;
     }
     if (taping) {
       tape_b += tape_stride;
@@ -2089,7 +2089,7 @@ int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
   }();
   a.factor_limit = limit;
   const bool rk4 = !a.single_eval && a.method == FETODE_RK4;
-  if (rk4 && !a.tape && a.B > g_tpw1_lo && a.B <= g_tpw1_hi) {   // v7, one trajectory per wave
+  if (rk4 && a.B > g_tpw1_lo && a.B <= g_tpw1_hi) {   // v7, one trajectory per wave (tapes too)
     hipLaunchKernelGGL(e->fn_rk4_1, dim3((unsigned)a.B), dim3(64), 0, (hipStream_t)stream, a);
   } else if (a.B <= small_max()) {  // v6: one trajectory per 192-thread workgroup (training tapes too)
     const fused_fn fn = a.tape ? (rk4 ? e->small_rk4_tape : e->small_tape) : (rk4 ? e->small_rk4 : e->small);

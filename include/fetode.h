@@ -124,7 +124,7 @@ int fetode_fused_supported(const fetode_field_t* field);
 int64_t fetode_fused_set_small_batch_max(int64_t b);
 /* Inference rk4 batches lo < B <= hi run the v7 kernel at ONE trajectory per wave (each hidden
  * unit's lane group split over both half-waves: half the Ferro rounds per lane — the latency-bound
- * batches of a strong-scaled shard), ahead of the small-batch switch above; training tapes never.
+ * batches of a strong-scaled shard), ahead of the small-batch switch above; training tapes too.
  * Defaults (320, 1024] (env FETODE_TPW1_LO / FETODE_TPW1_HI).  Sets lo / hi when >= 0; returns the
  * previous hi.  Process-wide tuning knob. */
 int64_t fetode_fused_set_tpw1_range(int64_t lo, int64_t hi);

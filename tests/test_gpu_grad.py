@@ -470,6 +470,50 @@ def test_lane_sweep_off_grid_inputs(dev):
         assert err <= 4 * yard + 1e-4 * scale, f"{n}: |gpu-fp64|={err:.3e} ref32 {yard:.3e} scale {scale:.3e}"
 
 
+def test_one_trajectory_per_wave_tape(dev):
+    """B = 777 (inside the one-trajectory-per-wave range, fetode_fused_set_tpw1_range): the taped
+    training forward on that kernel against the fp64 oracle's autograd with the reference's own
+    fp32 error as the yardstick (|gpu - fp64| <= 4 |ref fp32 - fp64| + 1e-4 scale), and the
+    two-per-wave kernel likewise, over one rk4 step (this batch's KAN-FET trajectories part from
+    fp64 within a few steps in any fp32 implementation: over 5 steps the two kernels' y0 gradients
+    are 21 % and 510 % from fp64, tools/diag/tape_cmp.py)."""
+    import fet_ode_amd as F
+    from fet_ode_amd import _lib
+    from oracle import torch_ref as O
+    lib = _lib.load()
+    g = load_golden("traj_kanfet")
+    sd = golden_sd(g)
+    t = torch.from_numpy(g["t35"])[:2]
+    y0 = O.lv_y0(777, seed=4)
+    skip = ("grid", "prev_x", "branch_sign")
+
+    def oracle(dt):
+        ps = {k: v.clone().to(dt).requires_grad_(k.split(".")[-1] not in skip) for k, v in sd.items()}
+        ref = O.KANFETRef.from_state_dict(ps, 2)
+        yc = y0.clone().to(dt).requires_grad_(True)
+        O.odeint(lambda tt, yy: ref(yy), yc, t, method="rk4").square().mean().backward()
+        return {"y0": yc.grad.double(), **{n: ps[n].grad.double() for n in ps if ps[n].grad is not None}}
+
+    e64, e32 = oracle(torch.float64), oracle(torch.float32)
+    prev = lib.fetode_fused_set_tpw1_range(-1, -1)
+    try:
+        for hi in (1 << 40, 0):
+            lib.fetode_fused_set_tpw1_range(0, hi)
+            m = F.KANFET([2, 10, 2], grid_size=5)
+            m.load_state_dict(sd)
+            m = m.to(dev)
+            yg = y0.clone().to(dev).requires_grad_(True)
+            F.odeint(F.autonomous(m), yg, t, method="rk4").square().mean().backward()
+            got = {"y0": yg.grad.cpu().double(), **{n: p.grad.cpu().double() for n, p in m.named_parameters()}}
+            for n in e64:
+                scale = e64[n].abs().max().item()
+                err = (got[n] - e64[n]).abs().max().item()
+                yard = (e32[n] - e64[n]).abs().max().item()
+                assert err <= 4 * yard + 1e-4 * scale, f"hi={hi} {n}: |gpu-fp64|={err:.3e} ref32 {yard:.3e}"
+    finally:
+        lib.fetode_fused_set_tpw1_range(320, prev)
+
+
 def test_fused_backward_deterministic(dev, bwd_split):
     """Two identical training solves give bitwise-identical gradients (fixed-order reductions)."""
     import fet_ode_amd as F
