@@ -799,162 +799,170 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
       return eval_body(xin, FF{});
     };
     if constexpr (DOPRI) {
-      // ---- device-resident dopri5 (dopri5.py _Dopri5, lane (traj, dim = row) carries y_row) ----
-      const DopriParams& P = a.dp;
-      const bool real = valid && c1 == 0;  // one lane per (trajectory, state dim) in the sums
-      const double n_el = P.n_total;   // B * D, or the global batch's in a sharded solve
-      int nfev = 0, n_att = 0, status = 0;
-      unsigned round = 0;
-#ifdef FETODE_EXP_NO_EVAL  // diagnostics only: a trivial field, the reductions and control as is
-      auto eval = [&](float xin) -> float { return -0.5f * xin; };
+      // the whole driver once per coercive-gate form (as the rk4 path): the evaluations inline
+      // one specialised field body, not a runtime choice between two per evaluation
+      auto drive = [&](auto fact_tag) __attribute__((always_inline)) {
+#ifndef FETODE_EXP_NO_EVAL
+        auto eval = [&](float xin) __attribute__((always_inline)) -> float { return eval_body(xin, fact_tag); };
+#else   // diagnostics only: a trivial field, the reductions and control as is
+        auto eval = [&](float xin) -> float { return -0.5f * xin; };
 #endif
-      auto gsum2 = [&](double v0, double v1, double& s0, double& s1) {
+        // ---- device-resident dopri5 (dopri5.py _Dopri5, lane (traj, dim = row) carries y_row) ----
+        const DopriParams& P = a.dp;
+        const bool real = valid && c1 == 0;  // one lane per (trajectory, state dim) in the sums
+        const double n_el = P.n_total;   // B * D, or the global batch's in a sharded solve
+        int nfev = 0, n_att = 0, status = 0;
+        unsigned round = 0;
+        auto gsum2 = [&](double v0, double v1, double& s0, double& s1) {
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          v0 += __shfl_xor(v0, o);
-          v1 += __shfl_xor(v1, o);
-        }
-        if (grid_sum2(P, round, v0, v1, s0, s1)) status = 4;
-      };
-      // training: the output of evaluation nfev (the first tape_cap of them) next to its layer
-      // inputs, in the row the evaluation just wrote (tape_b has moved past it)
-      auto ktape = [&](float k) {
-        if constexpr (TAPE)
-          if (nfev < P.tape_cap && valid && c1 == 0) tape_b[D + H + row - tape_stride] = k;
-      };
-      float f0 = eval(y);
-      ktape(f0);
-      ++nfev;
-      double dt;
-      if (P.first_step > 0.0) {
-        dt = P.first_step;
-      } else {  // misc._select_initial_step in fp32 (dopri5.py select_initial_step)
-        const float scale = P.atol + P.rtol * fabsf(y);
-        const float q0 = y / scale, q1 = f0 / scale;
-        double s, s1;
-        gsum2(real ? (double)q0 * q0 : 0.0, real ? (double)q1 * q1 : 0.0, s, s1);
-        const float d0 = fabsf(sqrtf((float)(s / n_el)));
-        const float d1 = fabsf(sqrtf((float)(s1 / n_el)));
-        float h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : (0.01f * d0) / d1;
-        h0 = fabsf(h0);
-        const float f1 = eval(y + f0 * h0);
-        ktape(f1);
+          for (int o = 32; o > 0; o >>= 1) {
+            v0 += __shfl_xor(v0, o);
+            v1 += __shfl_xor(v1, o);
+          }
+          if (grid_sum2(P, round, v0, v1, s0, s1)) status = 4;
+        };
+        // training: the output of evaluation nfev (the first tape_cap of them) next to its layer
+        // inputs, in the row the evaluation just wrote (tape_b has moved past it)
+        auto ktape = [&](float k) {
+          if constexpr (TAPE)
+            if (nfev < P.tape_cap && valid && c1 == 0) tape_b[D + H + row - tape_stride] = k;
+        };
+        float f0 = eval(y);
+        ktape(f0);
         ++nfev;
-        const float q2 = (f1 - f0) / scale;
-        gsum2(real ? (double)q2 * q2 : 0.0, 0.0, s, s1);
-        const float d2 = fabsf(sqrtf((float)(s / n_el)) / h0);
-        float h1;
-        if (d1 <= 1e-15f && d2 <= 1e-15f) h1 = fmaxf(1e-6f, h0 * 1e-3f);
-        else h1 = (float)pow((double)(0.01f / fmaxf(d1, d2)), (double)0.2f);  // fp64 pow rounded once: host == device
-        dt = (double)fminf(100.0f * h0, fabsf(h1));
-        if (TAPE && blockIdx.x == 0 && tid == 0) {
-          P.init_rec[0] = d0;
-          P.init_rec[1] = d1;
-          P.init_rec[2] = d2;
-          P.init_rec[3] = h0;
-          P.init_rec[4] = h1;
+        double dt;
+        if (P.first_step > 0.0) {
+          dt = P.first_step;
+        } else {  // misc._select_initial_step in fp32 (dopri5.py select_initial_step)
+          const float scale = P.atol + P.rtol * fabsf(y);
+          const float q0 = y / scale, q1 = f0 / scale;
+          double s, s1;
+          gsum2(real ? (double)q0 * q0 : 0.0, real ? (double)q1 * q1 : 0.0, s, s1);
+          const float d0 = fabsf(sqrtf((float)(s / n_el)));
+          const float d1 = fabsf(sqrtf((float)(s1 / n_el)));
+          float h0 = (d0 < 1e-5f || d1 < 1e-5f) ? 1e-6f : (0.01f * d0) / d1;
+          h0 = fabsf(h0);
+          const float f1 = eval(y + f0 * h0);
+          ktape(f1);
+          ++nfev;
+          const float q2 = (f1 - f0) / scale;
+          gsum2(real ? (double)q2 * q2 : 0.0, 0.0, s, s1);
+          const float d2 = fabsf(sqrtf((float)(s / n_el)) / h0);
+          float h1;
+          if (d1 <= 1e-15f && d2 <= 1e-15f) h1 = fmaxf(1e-6f, h0 * 1e-3f);
+          else h1 = (float)pow((double)(0.01f / fmaxf(d1, d2)), (double)0.2f);  // fp64 pow rounded once: host == device
+          dt = (double)fminf(100.0f * h0, fabsf(h1));
+          if (TAPE && blockIdx.x == 0 && tid == 0) {
+            P.init_rec[0] = d0;
+            P.init_rec[1] = d1;
+            P.init_rec[2] = d2;
+            P.init_rec[3] = h0;
+            P.init_rec[4] = h1;
+          }
         }
-      }
-      float co[5] = {y, 0.f, 0.f, 0.f, 0.f};
-      double t0s = P.t[0], t1s = P.t[0];
-      for (int i = 1; i < P.T && status == 0; ++i) {
-        const double next_t = P.t[i];
-        int n_steps = 0;
-        while (next_t > t1s) {
-          if (n_steps >= P.max_steps) { status = 3; break; }
-          const double t0 = t1s;
-          if (!(t0 + dt > t0)) { status = 2; break; }
-          const float dt32 = (float)dt;
-          const double t1 = t0 + dt;
-          // rk_common._runge_kutta_step in fetode_lincomb's op order, accumulated as the stages
-          // arrive: A[i] is stage s+1+i's sum k0 c0 + k1 c1 + ... (the same left-to-right sums)
-          float A[6];
+        float co[5] = {y, 0.f, 0.f, 0.f, 0.f};
+        double t0s = P.t[0], t1s = P.t[0];
+        for (int i = 1; i < P.T && status == 0; ++i) {
+          const double next_t = P.t[i];
+          int n_steps = 0;
+          while (next_t > t1s) {
+            if (n_steps >= P.max_steps) { status = 3; break; }
+            const double t0 = t1s;
+            if (!(t0 + dt > t0)) { status = 2; break; }
+            const float dt32 = (float)dt;
+            const double t1 = t0 + dt;
+            // rk_common._runge_kutta_step in fetode_lincomb's op order, accumulated as the stages
+            // arrive: A[i] is stage s+1+i's sum k0 c0 + k1 c1 + ... (the same left-to-right sums)
+            float A[6];
 #pragma unroll
-          for (int q = 0; q < 6; ++q) A[q] = f0 * (P.stc[0][q] * dt32);
-          float err = f0 * (P.stc[0][6] * dt32);
-          float mid = f0 * (P.stc[0][7] * dt32);
-          float yi = y, kn = f0;
+            for (int q = 0; q < 6; ++q) A[q] = f0 * (P.stc[0][q] * dt32);
+            float err = f0 * (P.stc[0][6] * dt32);
+            float mid = f0 * (P.stc[0][7] * dt32);
+            float yi = y, kn = f0;
 #pragma unroll 1
-          for (int st = 0; st < 6; ++st) {
-            yi = y + A[0];
-            // stage column st + 1 into SGPRs before the evaluation (the loads complete under it)
-            float c[8];
+            for (int st = 0; st < 6; ++st) {
+              yi = y + A[0];
+              // stage column st + 1 into SGPRs before the evaluation (the loads complete under it)
+              float c[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) c[q] = P.stc[st + 1][q];
-            kn = eval(yi);
-            ktape(kn);
-            ++nfev;
-            // entries past the tableau (coefficient 0) are never read again
+              for (int q = 0; q < 8; ++q) c[q] = P.stc[st + 1][q];
+              kn = eval(yi);
+              ktape(kn);
+              ++nfev;
+              // entries past the tableau (coefficient 0) are never read again
 #pragma unroll
-            for (int q = 0; q < 5; ++q) A[q] = A[q + 1] + kn * (c[q] * dt32);
-            err = err + kn * (c[6] * dt32);
-            mid = mid + kn * (c[7] * dt32);
-            STAMP(6);
+              for (int q = 0; q < 5; ++q) A[q] = A[q + 1] + kn * (c[q] * dt32);
+              err = err + kn * (c[6] * dt32);
+              mid = mid + kn * (c[7] * dt32);
+              STAMP(6);
+            }
+            const float y1 = yi;
+            const float tol = P.atol + P.rtol * fmaxf(fabsf(y), fabsf(y1));
+            const float qe = err / tol;
+            double s, nbad;
+            gsum2(real ? (double)qe * qe : 0.0, (real && !__builtin_isfinite(y)) ? 1.0 : 0.0, s, nbad);
+            STAMP(1);
+            if (status) break;
+            if (nbad != 0.0) { status = 1; break; }
+            const float ratio = sqrtf((float)(s / n_el));
+            const bool accept = ratio <= 1.0f;
+            if (blockIdx.x == 0 && tid == 0 && n_att < P.max_att) {
+              double* o = P.att + (int64_t)n_att * 4;
+              o[0] = t0;
+              o[1] = dt;
+              o[2] = (double)ratio;
+              o[3] = accept ? 1.0 : 0.0;
+            }
+            ++n_att;
+            if (accept) {  // interp._interp_fit (fetode_interp_fit's op order)
+              const float ym = y + mid, fa = f0, fb6 = kn;
+              co[4] = ((2.0f * dt32) * (fb6 - fa) - 8.0f * (y1 + y)) + 16.0f * ym;
+              co[3] = ((dt32 * (5.0f * fa - 3.0f * fb6) + 18.0f * y) + 14.0f * y1) - 32.0f * ym;
+              co[2] = ((dt32 * (fb6 - 4.0f * fa) - 11.0f * y) - 5.0f * y1) + 16.0f * ym;
+              co[1] = dt32 * fa;
+              co[0] = y;
+              y = y1;
+              f0 = kn;
+              t0s = t0;
+              t1s = t1;
+            } else {
+              t0s = t0;
+            }
+            // rk_common._optimal_step_size in fp64 (dopri5.py optimal_step)
+            const double rr = (double)ratio;
+            double nxt;
+            if (rr == 0.0) {
+              nxt = dt * P.ifactor;
+            } else {
+              const double dfac = rr < 1.0 ? 1.0 : P.dfactor;
+              const double factor = __builtin_isnan(rr) ? rr : fmin(P.ifactor, fmax(P.safety / pow(rr, 1.0 / 5.0), dfac));
+              nxt = dt * factor;
+            }
+            dt = __builtin_isnan(nxt) ? nxt : fmin(fmax(nxt, P.min_step), P.max_step);
+            ++n_steps;
+            STAMP(7);
           }
-          const float y1 = yi;
-          const float tol = P.atol + P.rtol * fmaxf(fabsf(y), fabsf(y1));
-          const float qe = err / tol;
-          double s, nbad;
-          gsum2(real ? (double)qe * qe : 0.0, (real && !__builtin_isfinite(y)) ? 1.0 : 0.0, s, nbad);
-          STAMP(1);
           if (status) break;
-          if (nbad != 0.0) { status = 1; break; }
-          const float ratio = sqrtf((float)(s / n_el));
-          const bool accept = ratio <= 1.0f;
-          if (blockIdx.x == 0 && tid == 0 && n_att < P.max_att) {
-            double* o = P.att + (int64_t)n_att * 4;
-            o[0] = t0;
-            o[1] = dt;
-            o[2] = (double)ratio;
-            o[3] = accept ? 1.0 : 0.0;
-          }
-          ++n_att;
-          if (accept) {  // interp._interp_fit (fetode_interp_fit's op order)
-            const float ym = y + mid, fa = f0, fb6 = kn;
-            co[4] = ((2.0f * dt32) * (fb6 - fa) - 8.0f * (y1 + y)) + 16.0f * ym;
-            co[3] = ((dt32 * (5.0f * fa - 3.0f * fb6) + 18.0f * y) + 14.0f * y1) - 32.0f * ym;
-            co[2] = ((dt32 * (fb6 - 4.0f * fa) - 11.0f * y) - 5.0f * y1) + 16.0f * ym;
-            co[1] = dt32 * fa;
-            co[0] = y;
-            y = y1;
-            f0 = kn;
-            t0s = t0;
-            t1s = t1;
-          } else {
-            t0s = t0;
-          }
-          // rk_common._optimal_step_size in fp64 (dopri5.py optimal_step)
-          const double rr = (double)ratio;
-          double nxt;
-          if (rr == 0.0) {
-            nxt = dt * P.ifactor;
-          } else {
-            const double dfac = rr < 1.0 ? 1.0 : P.dfactor;
-            const double factor = __builtin_isnan(rr) ? rr : fmin(P.ifactor, fmax(P.safety / pow(rr, 1.0 / 5.0), dfac));
-            nxt = dt * factor;
-          }
-          dt = __builtin_isnan(nxt) ? nxt : fmin(fmax(nxt, P.min_step), P.max_step);
-          ++n_steps;
-          STAMP(7);
-        }
-        if (status) break;
-        const float xq = (float)((next_t - t0s) / (t1s - t0s));  // interp._interp_evaluate
-        float total = co[0] + xq * co[1];
-        float xp = xq;
+          const float xq = (float)((next_t - t0s) / (t1s - t0s));  // interp._interp_evaluate
+          float total = co[0] + xq * co[1];
+          float xp = xq;
 #pragma unroll
-        for (int j = 2; j < 5; ++j) {
-          xp = xp * xq;
-          total = total + xp * co[j];
+          for (int j = 2; j < 5; ++j) {
+            xp = xp * xq;
+            total = total + xp * co[j];
+          }
+          out_write(i, total);
         }
-        out_write(i, total);
-      }
-      if (P.xr_world > 1 && blockIdx.x == 0 && tid == 0)   // the exchange workgroup may stop
-        __hip_atomic_store(dp_fin(P), round + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (blockIdx.x == 0 && tid == 0) {
-        P.stats[0] = nfev;
-        P.stats[1] = n_att;
-        P.stats[2] = __hip_atomic_load(P.bar + kDpLine * (kDpGroups + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 4 : status;
-      }
+        if (P.xr_world > 1 && blockIdx.x == 0 && tid == 0)   // the exchange workgroup may stop
+          __hip_atomic_store(dp_fin(P), round + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (blockIdx.x == 0 && tid == 0) {
+          P.stats[0] = nfev;
+          P.stats[1] = n_att;
+          P.stats[2] = __hip_atomic_load(P.bar + kDpLine * (kDpGroups + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? 4 : status;
+        }
+      };
+      if (fact) drive(FT{});
+      else drive(FF{});
     } else if (a.single_eval) {
       const float f = eval(y);
       if (valid && c1 == 0) a.eval_out[b * D + row] = f;
