@@ -760,12 +760,16 @@ __global__ __launch_bounds__(256) void wide_fwd4_kernel(fetode_kanlinear_t kl, c
       auto feats = [&](int t, float* feat) __attribute__((always_inline)) {
         const float xi = xs[wv * 64 + 16 * t + r][il];
         feat[0] = silu(xi);  // SiLU, efficientkan.py:166 / mnist :131
-        int m = -1;
+        // knot count: one v_cmp + one carry-in add per knot (no select + add)
+        int cnt = 0;
 #pragma unroll
         for (int j = 0; j < kWideNG / 4; ++j) {
-          const float4 v = gr4[j];
-          m += ((xi >= v.x) ? 1 : 0) + ((xi >= v.y) ? 1 : 0) + ((xi >= v.z) ? 1 : 0) + ((xi >= v.w) ? 1 : 0);
+          const float kv[4] = {gr4[j].x, gr4[j].y, gr4[j].z, gr4[j].w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            asm volatile("v_cmp_ge_f32 vcc, %1, %2\n\tv_addc_co_u32 %0, vcc, 0, %0, vcc" : "+v"(cnt) : "v"(xi), "v"(kv[q]) : "vcc");
         }
+        const int m = cnt - 1;
         const bool fin = __builtin_isfinite(xi), ing = fin && m >= 0 && m < kWideNI;
         const float4* tm = tbi + (ing ? m : 0) * 5;
         const float4 gq = tm[4];
@@ -777,27 +781,41 @@ __global__ __launch_bounds__(256) void wide_fwd4_kernel(fetode_kanlinear_t kl, c
             mywin[m + q + 1] = ffma(ffma(ffma(p.w, u, p.z), u, p.y), u, p.x);
           }
         }
+        if (!fin) {   // non-finite x (rare): NaN bases, as (x - g) / d * 0 in the reference
+#pragma unroll
+          for (int q = 4; q < 12; ++q) mywin[q] = __builtin_nanf("");
+        }
         asm volatile("" ::: "memory");  // the window writes stay before the vector reads
         const float4 d0 = *reinterpret_cast<const float4*>(mywin + 4), d1 = *reinterpret_cast<const float4*>(mywin + 8);
-        const float nf = fin ? 0.f : __builtin_nanf("");  // non-finite x: NaN bases, as (x - g) / d * 0
-        feat[1] = d0.x + nf; feat[2] = d0.y + nf; feat[3] = d0.z + nf; feat[4] = d0.w + nf;
-        feat[5] = d1.x + nf; feat[6] = d1.y + nf; feat[7] = d1.z + nf; feat[8] = d1.w + nf;
+        feat[1] = d0.x; feat[2] = d0.y; feat[3] = d0.z; feat[4] = d0.w;
+        feat[5] = d1.x; feat[6] = d1.y; feat[7] = d1.z; feat[8] = d1.w;
         asm volatile("" ::: "memory");
         if (ing) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) mywin[m + q + 1] = 0.f;
         }
+        if (!fin) {
+#pragma unroll
+          for (int q = 4; q < 12; ++q) mywin[q] = 0.f;
+        }
 #pragma unroll
         for (int j = 0; j < kWideNB; ++j)  // 2 sigmoid(a (x - b)), mnist_kuramoto_kan.py:22 (2 in the weights)
         feat[1 + kWideNS + j] = lg ? rcp(1.0f + ex2(ffma(ab[j].x, xi, ab[j].y))) : 0.f;
       };
-      float ft[4][kWideF];  // the four tiles' features first: then 4 independent MFMA chains
+      // tiles whose features are held at once (measured, tools/diag/mnist_head_time.py: 4 / 2 / 1 =
+      // 136 / 135 / 144 us; forcing 3 waves per SIMD spills 27-48 VGPRs: 167-202 us)
+      constexpr int TP = 4;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) feats(t, ft[t]);
+      for (int t0 = 0; t0 < 4; t0 += TP) {
+        float ft[TP][kWideF];   // TP tiles' features first: then TP independent MFMA chains
 #pragma unroll
-      for (int f = 0; f < kWideF; ++f)
+        for (int t = 0; t < TP; ++t) feats(t0 + t, ft[t]);
 #pragma unroll
-        for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ft[t][f], wb[f], acc[t], 0, 0, 0);
+        for (int f = 0; f < kWideF; ++f)
+#pragma unroll
+          for (int t = 0; t < TP; ++t)
+            acc[t0 + t] = __builtin_amdgcn_mfma_f32_16x16x4f32(ft[t][f], wb[f], acc[t0 + t], 0, 0, 0);
+      }
     }
   }
   // D of tile t: lane l holds rows 16 t + 4 (l >> 4) + v, column l & 15
