@@ -369,3 +369,50 @@ def test_wide_kanfet_field_autograd_two_calls(dev):
     for n in pr:
         err = (pa[n] - pr[n]).abs().max().item()
         assert err <= 1e-4 * pr[n].abs().max().item() + 1e-7, (n, err)
+
+
+def test_wide_field_flat_parameter_gradients(dev):
+    """The wide layers' parameter gradients through one flat tensor per layer (_WideLayerFlatFn)
+    against the per-parameter _WideLayerFn: two calls per graph; a second graph after an optimizer
+    step (the concatenation is rebuilt); two graphs recorded before either backward; a frozen
+    parameter (the per-parameter path)."""
+    from fet_ode_amd import autograd_ops as A
+    torch.manual_seed(23)
+    base = F.KANFET([64, 128, 64], grid_size=5, num_fet_basis=10)
+    xs = [_x(300, 64, seed=s).to(dev) * 0.5 for s in (4, 5, 6, 7)]
+    w = torch.randn(300, 64, generator=torch.Generator().manual_seed(8)).to(dev)
+
+    def run(flat, freeze=False):
+        A._FLAT_GRAD = flat
+        try:
+            m = F.KANFET([64, 128, 64], grid_size=5, num_fet_basis=10)
+            m.load_state_dict(base.state_dict())
+            m = m.to(dev)
+            if freeze:
+                A.field_layers(m)[0][0].base_weight.requires_grad_(False)
+            opt = torch.optim.SGD([p for p in m.parameters() if p.requires_grad], lr=1e-2)
+            out = []
+            ((m(xs[0]) * w).sum() + m(xs[1]).square().mean()).backward()
+            out.append({n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None})
+            if flat and not freeze:
+                kan = A.field_layers(m)[0][0]
+                assert not kan.__dict__["_fetode_flat"][3][0]   # the backward reached it
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+            l1 = (m(xs[2]) * w).sum()
+            l2 = m(xs[3]).square().mean()
+            l1.backward()
+            out.append({n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None})
+            l2.backward()
+            out.append({n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None})
+            return out
+        finally:
+            A._FLAT_GRAD = True
+
+    for freeze in (False, True):
+        got, exp = run(True, freeze), run(False, freeze)
+        for g, e in zip(got, exp):
+            assert g.keys() == e.keys() and len(e) >= (19 if freeze else 20)
+            for n in e:
+                err = (g[n] - e[n]).abs().max().item()
+                assert err <= 1e-6 * e[n].abs().max().item() + 1e-9, (freeze, n, err)
