@@ -177,6 +177,11 @@ SIGNATURES = {
     "fetode_scaled_rms": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_int64,
                                          _vp, _vp, _vp]),
     "fetode_scaled_rms_workspace": (ctypes.c_int64, [ctypes.c_int64]),
+    "fetode_comb_forward": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, _vp, _vp,
+                                           ctypes.c_int64, _vp]),
+    "fetode_comb_backward": (ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_void_p), ctypes.c_int32, _vp,
+                                            ctypes.POINTER(ctypes.c_void_p), _vp, _vp, ctypes.c_int64, _vp]),
+    "fetode_comb_workspace": (ctypes.c_int64, [ctypes.c_int64]),
     "fetode_scaled_sumsq": (ctypes.c_int, [_vp, _vp, _vp, _vp, ctypes.c_double, ctypes.c_double, ctypes.c_int64,
                                            _vp, _vp, _vp]),
     "fetode_interp_fit": (ctypes.c_int, [_vp, _vp, _vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_float),

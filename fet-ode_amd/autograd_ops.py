@@ -114,13 +114,13 @@ class _KANLinearFn(torch.autograd.Function):
         return (None, gx, *grads)
 
 
-def kan_backward(mod, xc, grad, want_x, want_params, gx_accum=None, out=None):
+def kan_backward(mod, xc, grad, want_x, want_params, gx_accum=None, out=None, entry=None):
     """HIP VJP of KANLinear: returns (gx, [grad per KAN_PARAM_NAMES or None]).  At the wide-layer
     widths with 64 / 128 outputs (ETT / ECG fields) the MFMA VJP (fetode_kanlinear_backward_wide);
     otherwise the generic kernels.  `out`: zero-filled tensors (per KAN_PARAM_NAMES) the parameter
     gradients are written into instead of fresh ones."""
     if mod.out_features in (64, 128) and mod.in_features >= 16 and (want_x or any(want_params)):
-        r = _kan_backward_wide(mod, xc, grad, want_x, want_params, gx_accum, out)
+        r = _kan_backward_wide(mod, xc, grad, want_x, want_params, gx_accum, out, entry)
         if r is not None:
             return r
     return _kan_backward_generic(mod, xc, grad, want_x, want_params, gx_accum, out)
@@ -132,8 +132,9 @@ def _grad_bufs(params, want, alloc, out):
             for k, (p, w) in enumerate(zip(params, want))]
 
 
-def _kan_backward_wide(mod, xc, grad, want_x, want_params, gx_accum=None, out=None):
-    entry = wide_plan(mod, None, xc.device)
+def _kan_backward_wide(mod, xc, grad, want_x, want_params, gx_accum=None, out=None, entry=None):
+    if entry is None:
+        entry = wide_plan(mod, None, xc.device)
     if entry is None:
         return None
     plan, kd, _, _ = entry
@@ -233,12 +234,12 @@ class _FerroFn(torch.autograd.Function):
         return (None, gx, None, None, None, gacc, *grads)
 
 
-def ferro_backward(mod, xc, prev, reinit, bsign, grad, want_x, want_params, gx_accum=None, out=None):
+def ferro_backward(mod, xc, prev, reinit, bsign, grad, want_x, want_params, gx_accum=None, out=None, entry=None):
     """HIP VJP of FerroelectricBasis: returns (gx, [grad per FERRO_PARAM_NAMES or None]).  At the
     wide-layer widths (ETT / ECG fields) with the constant branch sign, one pass over the element
     evaluations gives both (fetode_ferro_backward_wide); otherwise the generic two-kernel VJP."""
     if bsign is None and mod.in_dim >= 16 and mod.out_dim >= 16 and (want_x or any(want_params)):
-        r = _ferro_backward_wide(mod, xc, prev, reinit, grad, want_x, want_params, gx_accum, out)
+        r = _ferro_backward_wide(mod, xc, prev, reinit, grad, want_x, want_params, gx_accum, out, entry)
         if r is not None:
             return r
     return _ferro_backward_generic(mod, xc, prev, reinit, bsign, grad, want_x, want_params, gx_accum, out)
@@ -263,8 +264,9 @@ def _ferro_backward_generic(mod, xc, prev, reinit, bsign, grad, want_x, want_par
     return gx, grads
 
 
-def _ferro_backward_wide(mod, xc, prev, reinit, grad, want_x, want_params, gx_accum, out=None):
-    entry = wide_plan(None, mod, xc.device)
+def _ferro_backward_wide(mod, xc, prev, reinit, grad, want_x, want_params, gx_accum, out=None, entry=None):
+    if entry is None:
+        entry = wide_plan(None, mod, xc.device)
     if entry is None:
         return None
     plan, _, fd, _ = entry
@@ -480,7 +482,9 @@ def field_apply(model, x: torch.Tensor) -> torch.Tensor:
     x2 = x.reshape(-1, in0)
     _lib.require_gpu_tensor(x2, type(model).__name__ + ".forward")
     B = x2.shape[0]
-    grad = torch.is_grad_enabled() and grad_enabled_for(x2, *model.parameters())
+    # the stack's own tensors (module dict reads): model.parameters() walks the module tree, ~40 us
+    # per call — a dopri5 training solve evaluates the field ~200 times
+    grad = torch.is_grad_enabled() and (x2.requires_grad or any(t.requires_grad for t in _field_tensors(model)))
     if not grad:
         x2 = x2.contiguous()
         handle = make_handle(model, B, x2.device)
@@ -528,30 +532,58 @@ def field_apply(model, x: torch.Tensor) -> torch.Tensor:
 # the KAN contraction on MFMA (production widths: ETT 64/128, ECG FerroElectricNet 64/128)
 # ---------------------------------------------------------------------------------------------
 
-def _wide_key(kan, fer, device):
+def _wide_tensors(kan, fer):
     ts = []
     if kan is not None:
         ts += [kan.grid, *[p for p in kan_params(kan) if p is not None]]
     if fer is not None:
         ts += [getattr(fer, n) for n in FERRO_PARAM_NAMES]
-    key = [str(device), _lib.param_generation()]
-    for t in ts:
-        if t.dtype != torch.float32 or not t.is_contiguous() or t.device != device:
-            return None
-        key += [t.data_ptr(), t._version]
-    return tuple(key)
+    return ts
 
 
-def wide_plan(kan, fer, device):
+def _tkey(ts):
+    """Per-tensor (storage address, version counter, contiguity): a dtype or device change moves the
+    storage; the full check (fp32, contiguous, on the device) runs when a plan is (re)built."""
+    return tuple([(t.data_ptr(), t._version, t.is_contiguous()) for t in ts])
+
+
+def _wide_key(kan, fer, device, parts=None):
+    """The cache key of a wide-layer plan; `parts` = (KAN key, Ferro key) already computed by
+    wide_plans (one pass over the layer's tensors for its three plans)."""
+    if parts is None:
+        parts = (_tkey(_wide_tensors(kan, None)) if kan is not None else (),
+                 _tkey(_wide_tensors(None, fer)) if fer is not None else ())
+    return (str(device), _lib.param_generation(), parts[0] if kan is not None else (),
+            parts[1] if fer is not None else ())
+
+
+def _plan_tensors_ok(kan, fer, device):
+    return all(t.dtype == torch.float32 and t.is_contiguous() and t.device == device
+               for t in _wide_tensors(kan, fer))
+
+
+def wide_plans(kan, fer, device):
+    """(KANLinear + Ferro plan, KANLinear plan, Ferro plan) of a layer (wide_plan entries or None;
+    the Ferro one None when fer is None): the forward and the two VJPs' plans from one key pass."""
+    parts = (_tkey(_wide_tensors(kan, None)), _tkey(_wide_tensors(None, fer)) if fer is not None else ())
+    kf = wide_plan(kan, fer, device, parts)
+    if fer is None:
+        return kf, kf, None
+    return kf, wide_plan(kan, None, device, parts), wide_plan(None, fer, device, parts)
+
+
+def wide_plan(kan, fer, device, parts=None):
     """(plan, kan descriptor, ferro descriptor) of a wide layer, or None when the layer has no
     wide kernel.  Packed once per parameter version (the tensors' version counters, like the
     fused plan), cached on the KANLinear (or the Ferro module when alone)."""
     owner = kan if kan is not None else fer
     attr = "_fetode_wide_kf" if (kan is not None and fer is not None) else "_fetode_wide"
-    key = _wide_key(kan, fer, device)
+    key = _wide_key(kan, fer, device, parts)
     cached = owner.__dict__.get(attr)
-    if cached is not None and key is not None and cached[0] == key:
+    if cached is not None and cached[0] == key:
         return cached[1]
+    if not _plan_tensors_ok(kan, fer, device):
+        key = None   # never matched: rebuilt on every call
     lib = _lib.load()
     keep = []
     kd = kan.desc(keep) if kan is not None else None
@@ -581,11 +613,11 @@ class _WideLayerFn(torch.autograd.Function):
     non-None parameters (KAN_PARAM_NAMES order), then the Ferro module's (FERRO_PARAM_NAMES)."""
 
     @staticmethod
-    def forward(ctx, kan, fer, reinit, nk, x, *params):
+    def forward(ctx, kan, fer, reinit, ents, nk, x, *params):
         xc = _lib.f32c(x)
-        out = wide_apply(kan, fer, xc, reinit=reinit)
+        out = wide_apply(kan, fer, xc, reinit=reinit, entry=ents[0])
         prev = None if (fer is None or reinit) else fer._prev.detach().clone()   # overwritten after this call
-        ctx.kan, ctx.fer, ctx.reinit, ctx.nk = kan, fer, reinit, nk
+        ctx.kan, ctx.fer, ctx.reinit, ctx.nk, ctx.ents = kan, fer, reinit, nk, ents
         ctx.save_for_backward(xc, prev)
         return out
 
@@ -593,24 +625,24 @@ class _WideLayerFn(torch.autograd.Function):
     def backward(ctx, g):
         xc, prev = ctx.saved_tensors
         kan, fer, nk = ctx.kan, ctx.fer, ctx.nk
-        want_x = ctx.needs_input_grad[4]
-        pn = ctx.needs_input_grad[5:]
+        want_x = ctx.needs_input_grad[5]
+        pn = ctx.needs_input_grad[6:]
         kp = kan_params(kan)
         it = iter(pn[:nk])
         want_k = [next(it) if p is not None else False for p in kp]
-        gx, gk = kan_backward(kan, xc, g, want_x, want_k)
+        gx, gk = kan_backward(kan, xc, g, want_x, want_k, entry=ctx.ents[1])
         gf = []
         if fer is not None:
             want_f = list(pn[nk:])
             if want_x or any(want_f):
                 gxf, gf = ferro_backward(fer, xc, prev, ctx.reinit, None, g, want_x, want_f,
-                                         gx_accum=gx if want_x else None)
+                                         gx_accum=gx if want_x else None, entry=ctx.ents[2])
                 if want_x and gx is None:
                     gx = gxf
             else:
                 gf = [None] * len(want_f)
         grads_k = [t for t, p in zip(gk, kp) if p is not None]
-        return (None, None, None, None, gx, *grads_k, *gf)
+        return (None, None, None, None, None, gx, *grads_k, *gf)
 
 
 _FLAT_ALIGN = 64   # floats: every parameter's slice of the flat gradient starts 256-byte aligned
@@ -625,11 +657,11 @@ class _WideLayerFlatFn(torch.autograd.Function):
     once per graph."""
 
     @staticmethod
-    def forward(ctx, kan, fer, reinit, layout, x, flat):
+    def forward(ctx, kan, fer, reinit, ents, layout, x, flat):
         xc = _lib.f32c(x)
-        out = wide_apply(kan, fer, xc, reinit=reinit)
+        out = wide_apply(kan, fer, xc, reinit=reinit, entry=ents[0])
         prev = None if (fer is None or reinit) else fer._prev.detach().clone()   # overwritten after this call
-        ctx.kan, ctx.fer, ctx.reinit, ctx.layout = kan, fer, reinit, layout
+        ctx.kan, ctx.fer, ctx.reinit, ctx.layout, ctx.ents = kan, fer, reinit, layout, ents
         ctx.save_for_backward(xc, prev)
         return out
 
@@ -637,8 +669,8 @@ class _WideLayerFlatFn(torch.autograd.Function):
     def backward(ctx, g):
         xc, prev = ctx.saved_tensors
         kan, fer, (offs, total) = ctx.kan, ctx.fer, ctx.layout
-        want_x = ctx.needs_input_grad[4]
-        want_p = ctx.needs_input_grad[5]
+        want_x = ctx.needs_input_grad[5]
+        want_p = ctx.needs_input_grad[6]
         kp = kan_params(kan)
         fp = [getattr(fer, n) for n in FERRO_PARAM_NAMES] if fer is not None else []
         gflat = torch.zeros(total, device=xc.device, dtype=torch.float32) if want_p else None
@@ -647,13 +679,14 @@ class _WideLayerFlatFn(torch.autograd.Function):
         it = iter(views or [])
         kout = [None if p is None else next(it) for p in kp] if want_p else None
         fout = list(it) if want_p else None
-        gx, _ = kan_backward(kan, xc, g, want_x, [want_p and p is not None for p in kp], out=kout)
+        gx, _ = kan_backward(kan, xc, g, want_x, [want_p and p is not None for p in kp], out=kout,
+                             entry=ctx.ents[1])
         if fer is not None and (want_x or want_p):
             gxf, _ = ferro_backward(fer, xc, prev, ctx.reinit, None, g, want_x, [want_p] * len(fp),
-                                    gx_accum=gx if want_x else None, out=fout)
+                                    gx_accum=gx if want_x else None, out=fout, entry=ctx.ents[2])
             if want_x and gx is None:
                 gx = gxf
-        return (None, None, None, None, gx, gflat)
+        return (None, None, None, None, None, gx, gflat)
 
 
 def _flat_params(kan, fer, ps):
@@ -692,19 +725,19 @@ def wide_layer_grad(kan, fer, x, reinit: bool):
     """KANLinear(x) (+ Ferro(x)) with autograd through _WideLayerFlatFn (every parameter requires
     grad: the usual training case) or _WideLayerFn (some frozen), or None if the layer has no wide
     kernels (the caller then runs the per-module path)."""
-    if wide_plan(kan, fer, x.device) is None or (fer is not None and wide_plan(None, fer, x.device) is None):
-        return None
-    if wide_plan(kan, None, x.device) is None:
+    # the forward's plan and the two VJPs' (kept for the backward: the gradient at these parameters)
+    ents = wide_plans(kan, fer, x.device)
+    if ents[0] is None or ents[1] is None or (fer is not None and ents[2] is None):
         return None
     kp = [p for p in kan_params(kan) if p is not None]
     fp = [getattr(fer, n) for n in FERRO_PARAM_NAMES] if fer is not None else []
     if _FLAT_GRAD and all(p.requires_grad for p in kp + fp):
         flat, layout = _flat_params(kan, fer, kp + fp)
-        return _WideLayerFlatFn.apply(kan, fer, reinit, layout, x, flat)
-    return _WideLayerFn.apply(kan, fer, reinit, len(kp), x, *kp, *fp)
+        return _WideLayerFlatFn.apply(kan, fer, reinit, ents, layout, x, flat)
+    return _WideLayerFn.apply(kan, fer, reinit, ents, len(kp), x, *kp, *fp)
 
 
-def wide_apply(kan, fer, x, reinit: bool = False):
+def wide_apply(kan, fer, x, reinit: bool = False, entry=None):
     """out = KANLinear(x) + Ferro(x) (either may be None) through fetode_wide_layer_forward, or None
     if the layer has no wide kernel.  Reads the Ferro module's prev_x; the caller commits the new
     state (ferro_class.py:409).  The ABI takes a raw row-major pointer: x is made contiguous here
@@ -719,7 +752,8 @@ def wide_apply(kan, fer, x, reinit: bool = False):
         width, outf = kan.in_features, kan.out_features
     if width < 16 or outf < 16:
         return None
-    entry = wide_plan(kan, fer, dev)
+    if entry is None:
+        entry = wide_plan(kan, fer, dev)
     if entry is None:
         return None
     plan, kd, fd, _ = entry

@@ -2,6 +2,8 @@
 // rk_common._runge_kutta_step / interp._interp_fit / interp._interp_evaluate / misc._rms_norm).
 // Call sites in the reference: train_ecg_kan_fet_nn_ode.py:558-565, :1034-1041 and every
 // default-method odeint (train_kanfet_node_predprey.py:252).
+#include <algorithm>
+
 #include "fetode_common.h"
 
 using namespace fetode;
@@ -20,6 +22,92 @@ __global__ void lincomb_kernel(const float* __restrict__ y0, const float* __rest
   float acc = k[t] * c.c[0];
   for (int j = 1; j < m; ++j) acc = acc + k[j * kstride + t] * c.c[j];
   out[t] = y0 ? y0[t] + acc : acc;
+}
+
+// ---- the stage combine under autograd (dopri5._CombFn): coefficients on the device ----
+// _Dopri5Grad differentiates through dt (torchdiffeq's step-size control is a tensor expression), so
+// the coefficients c_j = beta_j dt are device values with a gradient.  Forward: out = y0 + sum_j k_j c_j
+// with every product rounded and the running sum in j order, then + y0 (the op order of the torch
+// expression it replaces: ks[0] * c[0] + ks[1] * c[1] + ..., then y0 + acc; no contraction).
+// Backward: d k_j = c_j g (rounded product, as torch's), d c_j = <g, k_j> (fp32 per-thread sums, then
+// fixed-order block and grid sums: deterministic for a given n).
+constexpr int kCombMax = 8;
+constexpr int kCombThreads = 256;
+constexpr int kCombMaxBlocks = 1024;
+
+struct CombPtrs {
+  const float* k[kCombMax];
+  float* gk[kCombMax];
+};
+
+__global__ __launch_bounds__(kCombThreads) void comb_fwd_kernel(const float* __restrict__ y0, CombPtrs p,
+                                                                const float* __restrict__ c, int m,
+                                                                float* __restrict__ out, int64_t n) {
+#pragma clang fp contract(off)
+  float cj[kCombMax];
+#pragma unroll
+  for (int j = 0; j < kCombMax; ++j) cj[j] = j < m ? c[j] : 0.f;
+  for (int64_t t = (int64_t)blockIdx.x * kCombThreads + threadIdx.x; t < n; t += (int64_t)gridDim.x * kCombThreads) {
+    float acc = p.k[0][t] * cj[0];
+#pragma unroll
+    for (int j = 1; j < kCombMax; ++j)
+      if (j < m) acc = acc + p.k[j][t] * cj[j];
+    out[t] = y0 ? y0[t] + acc : acc;
+  }
+}
+
+// part[block][j] = this block's share of <g, k_j> (when want_c)
+__global__ __launch_bounds__(kCombThreads) void comb_bwd_kernel(const float* __restrict__ g, CombPtrs p,
+                                                                const float* __restrict__ c, int m, int want_c,
+                                                                float* __restrict__ part, int64_t n) {
+#pragma clang fp contract(off)
+  __shared__ float red[kCombMax][kCombThreads];
+  float cj[kCombMax], dot[kCombMax];
+#pragma unroll
+  for (int j = 0; j < kCombMax; ++j) {
+    cj[j] = j < m ? c[j] : 0.f;
+    dot[j] = 0.f;
+  }
+  for (int64_t t = (int64_t)blockIdx.x * kCombThreads + threadIdx.x; t < n; t += (int64_t)gridDim.x * kCombThreads) {
+    const float gv = g[t];
+#pragma unroll
+    for (int j = 0; j < kCombMax; ++j) {
+      if (j < m) {
+        if (p.gk[j]) p.gk[j][t] = gv * cj[j];
+        if (want_c) dot[j] = dot[j] + gv * p.k[j][t];
+      }
+    }
+  }
+  if (!want_c) return;
+#pragma unroll
+  for (int j = 0; j < kCombMax; ++j) red[j][threadIdx.x] = dot[j];
+  __syncthreads();
+  for (int w = kCombThreads / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+#pragma unroll
+      for (int j = 0; j < kCombMax; ++j) red[j][threadIdx.x] += red[j][threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+  if ((int)threadIdx.x < kCombMax) part[(int64_t)blockIdx.x * kCombMax + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// gc[j] = sum over blocks of part[b][j]: wave j, lane l sums blocks l, l + 64, ... in order, then a
+// fixed tree over the lanes (a serial loop over 512 partials was 51 us of latency per call)
+__global__ __launch_bounds__(64 * kCombMax) void comb_dot_kernel(const float* __restrict__ part, int nb, int m,
+                                                                 float* __restrict__ gc) {
+  __shared__ float red[kCombMax][64];
+  const int j = threadIdx.x >> 6, l = threadIdx.x & 63;
+  float s = 0.f;
+  if (j < m)
+    for (int b = l; b < nb; b += 64) s += part[(int64_t)b * kCombMax + j];
+  red[j][l] = s;
+  __syncthreads();
+  for (int w = 32; w > 0; w >>= 1) {
+    if (l < w) red[j][l] += red[j][l + w];
+    __syncthreads();
+  }
+  if (l == 0 && j < m) gc[j] = red[j][0];
 }
 
 // sum(((a - sub) / (atol + rtol * max(|y0|, |y1|)))^2), one workgroup, fp64 accumulation;
@@ -198,6 +286,47 @@ int fetode_lincomb(const float* y0, const float* k, int64_t kstride, const float
   hipLaunchKernelGGL(lincomb_kernel, dim3(nblk(n, 256)), dim3(256), 0, (hipStream_t)stream, y0, k, kstride, cc, m,
                      out, n);
   LAUNCH_CHECK();
+  return FETODE_OK;
+}
+
+int64_t fetode_comb_workspace(int64_t n) {
+  return (int64_t)sizeof(float) * kCombMax * std::max(1, std::min(kCombMaxBlocks, nblk(n, kCombThreads)));
+}
+
+int fetode_comb_forward(const float* y0, const float* const* k, int32_t m, const float* c, float* out, int64_t n,
+                        void* stream) {
+  if (n <= 0) return FETODE_OK;
+  if (!k || !c || !out || m < 1 || m > kCombMax) return set_err(FETODE_EINVAL, "comb_forward: bad arguments (m=%d)", m);
+  CombPtrs p{};
+  for (int j = 0; j < m; ++j) {
+    if (!k[j]) return set_err(FETODE_EINVAL, "comb_forward: k[%d] is null", j);
+    p.k[j] = k[j];
+  }
+  const int nb = std::min(kCombMaxBlocks, nblk(n, kCombThreads));
+  hipLaunchKernelGGL(comb_fwd_kernel, dim3(nb), dim3(kCombThreads), 0, (hipStream_t)stream, y0, p, c, (int)m, out, n);
+  LAUNCH_CHECK();
+  return FETODE_OK;
+}
+
+int fetode_comb_backward(const float* g, const float* const* k, int32_t m, const float* c, float* const* gk,
+                         float* gc, void* workspace, int64_t n, void* stream) {
+  if (n <= 0 || !g || !k || !c || m < 1 || m > kCombMax || (gc && !workspace))
+    return set_err(FETODE_EINVAL, "comb_backward: bad arguments (m=%d)", m);
+  CombPtrs p{};
+  for (int j = 0; j < m; ++j) {
+    if (!k[j]) return set_err(FETODE_EINVAL, "comb_backward: k[%d] is null", j);
+    p.k[j] = k[j];
+    p.gk[j] = gk ? gk[j] : nullptr;
+  }
+  const int nb = std::min(kCombMaxBlocks, nblk(n, kCombThreads));
+  hipLaunchKernelGGL(comb_bwd_kernel, dim3(nb), dim3(kCombThreads), 0, (hipStream_t)stream, g, p, c, (int)m,
+                     gc ? 1 : 0, (float*)workspace, n);
+  LAUNCH_CHECK();
+  if (gc) {
+    hipLaunchKernelGGL(comb_dot_kernel, dim3(1), dim3(64 * kCombMax), 0, (hipStream_t)stream, (const float*)workspace, nb,
+                       (int)m, gc);
+    LAUNCH_CHECK();
+  }
   return FETODE_OK;
 }
 

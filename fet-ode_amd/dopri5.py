@@ -865,6 +865,50 @@ class _NormAllReduce(torch.autograd.Function):
         return t.to(g.device), None, None
 
 
+def _ptrs(ts):
+    return (_lib.ctypes.c_void_p * len(ts))(*[t.data_ptr() if t is not None else None for t in ts])
+
+
+class _CombFn(torch.autograd.Function):
+    """y0 + sum_j ks[j] * c[j] (y0 may be None) with c a device vector carrying a gradient (beta dt):
+    one fetode_comb_forward launch, and one fetode_comb_backward (+ its dot-product finish) for every
+    input's gradient — where the torch expression ran ~2 m kernels forward and ~5 m backward (a
+    select, its zero fill and copy, a product and a reduction per term), ≈ 20 % of the ETT dopri5
+    training iteration (profiles/r05_ett_train_flat_kernel_stats.csv).  Forward rounding is the torch
+    expression's (fetode.h); <g, k_j> is an fp32 sum in a fixed order instead of torch's."""
+
+    @staticmethod
+    def forward(ctx, y0, c, *ks):
+        lib = _lib.load()
+        n = ks[0].numel()
+        out = torch.empty_like(ks[0])
+        _lib.check(lib.fetode_comb_forward(_lib.ptr(y0), _ptrs(ks), len(ks), c.data_ptr(), out.data_ptr(), n,
+                                           _lib.stream_handle(out.device)), "fetode_comb_forward")
+        ctx.save_for_backward(c, *ks)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        c, *ks = ctx.saved_tensors
+        lib = _lib.load()
+        n = ks[0].numel()
+        g = g.contiguous()
+        want_y0, want_c, want_k = ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2:]
+        gks = [torch.empty_like(k) if w else None for k, w in zip(ks, want_k)]
+        gc = ws = None
+        if want_c:
+            gc = torch.empty_like(c)
+            ws = torch.empty(max(1, lib.fetode_comb_workspace(n) // 4), device=g.device, dtype=torch.float32)
+        if want_c or any(want_k):
+            _lib.check(lib.fetode_comb_backward(g.data_ptr(), _ptrs(ks), len(ks), c.data_ptr(), _ptrs(gks),
+                                                _lib.ptr(gc), _lib.ptr(ws), n, _lib.stream_handle(g.device)),
+                       "fetode_comb_backward")
+        return (g if want_y0 else None, gc, *gks)
+
+
+_FUSED_COMB = True   # tests flip it to compare with the torch expression
+
+
 class _Dopri5Grad:
     """dopri5 with torchdiffeq's direct backpropagation (no adjoint): the solve is recorded by
     autograd through every stage of every attempt, the RMS error ratios and the adaptive step
@@ -955,6 +999,18 @@ class _Dopri5Grad:
             h1 = (0.01 / max(d1, d2)) ** (1. / float(ORDER))
         return torch.min(100 * h0, h1.abs()).to(torch.float64)
 
+    def _stage(self, y0, ks, c):
+        """(y0 +) sum_j ks[j] c[j]: _CombFn for fp32 GPU states, the torch expression otherwise (the
+        CPU tests of the sharded norm drive this class in fp64 on the CPU)."""
+        k0 = ks[0]
+        if (_FUSED_COMB and k0.is_cuda and k0.dtype == torch.float32 and len(ks) <= 8 and c.is_contiguous()
+                and all(k.is_contiguous() and k.shape == k0.shape for k in ks)
+                and (y0 is None or (y0.is_contiguous() and y0.numel() == k0.numel()))):
+            out = _CombFn.apply(y0, c, *ks)
+            return out if y0 is None else out.view_as(y0)
+        acc = self._comb(ks, c)
+        return acc if y0 is None else y0 + acc.view_as(y0)
+
     @staticmethod
     def _comb(ks, c):
         """sum_j ks[j] * c[j] (torchdiffeq: torch.stack(ks, -1).matmul(c)).  As elementwise device ops,
@@ -974,14 +1030,17 @@ class _Dopri5Grad:
         yi = None
         for s in range(6):
             ti = t1c if self.alpha[s] == 1.0 else t0c + self.alpha_t[s] * dtc
-            yi = y0 + self._comb(ks, self.beta[s] * dtc).view_as(f0)
+            yi = self._stage(y0, ks, self.beta[s] * dtc)
             ks.append(self.f(ti, yi))
-        return yi, ks[-1], self._comb(ks, dtc * self.c_err), ks
+        return yi, ks[-1], self._stage(None, ks, dtc * self.c_err), ks
 
-    def optimal_step(self, dt, ratio):
-        if ratio == 0:
+    def optimal_step(self, dt, ratio, ratio_host=None):
+        """rk_common._optimal_step_size; ratio_host: the ratio's value already read back (the
+        single-device loop reads it once per attempt), for the two branch decisions."""
+        rv = ratio if ratio_host is None else ratio_host
+        if rv == 0:
             return dt * self.ifactor
-        dfactor = self.dfactor if ratio >= 1 else torch.ones((), dtype=torch.float64, device=self.dev)
+        dfactor = self.dfactor if rv >= 1 else torch.ones((), dtype=torch.float64, device=self.dev)
         er = ratio.type_as(dt)
         factor = torch.min(self.ifactor, torch.max(self.safety / er ** (1.0 / ORDER), dfactor))
         return dt * factor
@@ -995,32 +1054,57 @@ class _Dopri5Grad:
               if self.first_step is not None else self.select_initial_step(t[0], y, f0))
         t0s = t1s = t[0]
         coeff = [y] * 5
+        # single device: the control flow runs on host copies of t, t1 and dt (fp64, the same IEEE
+        # sums as the device tensors) and one read-back per attempt carries the ratio and y1's
+        # finiteness (asserted at the next attempt's top if y1 is accepted, where torchdiffeq asserts
+        # it); the tensors keep carrying the d/d dt terms.  Two syncs per attempt instead of nine.
+        host = not self.distributed
+        if host:
+            th = [float(v) for v in t.detach().cpu()]
+            t1h, dth = th[0], float(dt.detach())
+            yfin = bool(torch.isfinite(y).all())
         for i in range(1, len(t)):
             n_steps = 0
-            while t[i] > t1s:
+            while (th[i] > t1h) if host else bool(t[i] > t1s):
                 assert n_steps < self.max_num_steps, "max_num_steps exceeded"
                 t0 = t1s
-                assert t0 + dt > t0, "underflow in dt {}".format(dt.item())
-                if not self.distributed:
-                    assert torch.isfinite(y).all(), "non-finite values in state `y`"
+                if host:
+                    t0h = t1h
+                    assert t0h + dth > t0h, "underflow in dt {}".format(dth)
+                    assert yfin, "non-finite values in state `y`"
+                else:
+                    assert t0 + dt > t0, "underflow in dt {}".format(dt.item())
                 y1, f1, err, k = self.step(y, f0, t0, dt)
                 tol = self.atol + self.rtol * torch.max(y.abs(), y1.abs())
-                # sharded: the finiteness of y on every rank travels with this attempt's norm
-                ratio, finite = self.rms(err / tol, finite_of=y)
-                assert finite, "non-finite values in state `y`"
-                accept = bool(ratio <= 1)
-                self.attempts.append((float(t0.detach()), float(dt.detach()), float(ratio.detach()), accept))
+                if host:
+                    ratio = self.rms(err / tol)
+                    rv = torch.stack([ratio.detach().to(torch.float64),
+                                      torch.isfinite(y1.detach()).all().to(torch.float64)]).cpu()
+                    rh, y1fin = float(rv[0]), bool(rv[1] != 0)
+                    accept = rh <= 1
+                    self.attempts.append((t0h, dth, rh, accept))
+                else:
+                    # sharded: the finiteness of y on every rank travels with this attempt's norm
+                    ratio, finite = self.rms(err / tol, finite_of=y)
+                    assert finite, "non-finite values in state `y`"
+                    accept = bool(ratio <= 1)
+                    self.attempts.append((float(t0.detach()), float(dt.detach()), float(ratio.detach()), accept))
+                    rh = None
                 if accept:
                     dtm = dt.type_as(y)
-                    ym = y + self._comb(k, dtm * self.c_mid).view_as(y)
+                    ym = self._stage(y, k, dtm * self.c_mid)
                     fa, fb = k[0], k[-1]
                     coeff = [y, dtm * fa, dtm * (fb - 4 * fa) - 11 * y - 5 * y1 + 16 * ym,
                              dtm * (5 * fa - 3 * fb) + 18 * y + 14 * y1 - 32 * ym,
                              2 * dtm * (fb - fa) - 8 * (y1 + y) + 16 * ym]
                     y, f0, t0s, t1s = y1, f1, t0, t0 + dt
+                    if host:
+                        t1h, yfin = t0h + dth, y1fin
                 else:
                     t0s = t0
-                dt = self.optimal_step(dt, ratio).clamp(self.min_step, self.max_step)
+                dt = self.optimal_step(dt, ratio, rh).clamp(self.min_step, self.max_step)
+                if host:
+                    dth = float(dt.detach())
                 n_steps += 1
             x = ((t[i] - t0s) / (t1s - t0s)).to(self.sdt)   # interp._interp_evaluate
             total, xp = coeff[0] + x * coeff[1], x

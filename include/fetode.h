@@ -312,6 +312,18 @@ int fetode_axpby(int64_t n, float a, const float* x, float b, const float* y, fl
 /* out = (y0 ? y0 : 0) + sum_{j<m} k[j]*c[j]  — rk_common._runge_kutta_step stage inputs/error */
 int fetode_lincomb(const float* y0, const float* k, int64_t kstride, const float* c, int32_t m,
                    float* out, int64_t n, void* stream);
+/* The stage combine under autograd (dopri5._CombFn, _Dopri5Grad: rk_common._runge_kutta_step's
+ * torch.stack(k).matmul(beta * dt) with dt a differentiable device value).  k: host array of m <= 8
+ * device pointers (n floats each); c: m DEVICE fp32 coefficients.
+ * forward: out = (y0 ? y0 : 0) + ((k0*c0 + k1*c1) + ...), every product and sum rounded in that order.
+ * backward: gk[j] = c[j] * g (gk or gk[j] NULL: not written); gc (nullable, device, m floats) =
+ * <g, k_j> in fp32, summed in a fixed order (deterministic for a given n); workspace:
+ * fetode_comb_workspace(n) bytes when gc is given. */
+int fetode_comb_forward(const float* y0, const float* const* k, int32_t m, const float* c, float* out,
+                        int64_t n, void* stream);
+int fetode_comb_backward(const float* g, const float* const* k, int32_t m, const float* c, float* const* gk,
+                         float* gc, void* workspace, int64_t n, void* stream);
+int64_t fetode_comb_workspace(int64_t n);
 /* out[0] (dev) = sqrt(mean(((a - sub) / (atol + rtol*max(|y0|,|y1|)))^2)) — misc._rms_norm of the
  * scaled error (sub, y1 nullable: _select_initial_step's scale = atol + |y0|*rtol);
  * out[1] = 1 if y0 holds a non-finite value (torchdiffeq's per-step assertion), else 0. */

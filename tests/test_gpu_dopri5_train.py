@@ -203,3 +203,58 @@ def test_dopri5_train_bench_batch(dev):
     b = _run("kanfet", dev, 4096, t, 1e-3, 1e-4, True)
     assert a[0] == b[0] and all(torch.equal(a[1][n], b[1][n]) for n in a[1])
     assert all(torch.isfinite(v).all() for v in a[1].values())
+
+
+@pytest.mark.parametrize("n,m,with_y0", [(1, 1, True), (1000, 6, True), (131072, 7, False), (300_001, 8, True)])
+def test_stage_combine_fn_matches_torch_expression(dev, n, m, with_y0):
+    """_CombFn (fetode_comb_forward / _backward) against the torch expression it replaces in
+    _Dopri5Grad._comb: the forward and d k_j bitwise (same rounding order), d c_j = <g, k_j> within
+    fp32 summation-order error, d y0 = g; sizes below one block, above the grid's 1024 blocks."""
+    from fet_ode_amd.dopri5 import _CombFn, _Dopri5Grad
+    gen = torch.Generator().manual_seed(n + m)
+    ks = [torch.randn(n, generator=gen).to(dev).requires_grad_(True) for _ in range(m)]
+    y0 = torch.randn(n, generator=gen).to(dev).requires_grad_(True) if with_y0 else None
+    c = (torch.randn(m, generator=gen) * 0.3).to(dev).requires_grad_(True)
+    g = torch.randn(n, generator=gen).to(dev)
+    res = []
+    for fused in (True, False):
+        ins = [t.detach().clone().requires_grad_(True) for t in ks]
+        yy = y0.detach().clone().requires_grad_(True) if with_y0 else None
+        cc = c.detach().clone().requires_grad_(True)
+        if fused:
+            out = _CombFn.apply(yy, cc, *ins)
+        else:
+            out = _Dopri5Grad._comb(ins, cc)
+            out = out if yy is None else yy + out
+        out.backward(g)
+        res.append((out.detach(), [t.grad for t in ins], cc.grad, None if yy is None else yy.grad))
+    (o1, gk1, gc1, gy1), (o0, gk0, gc0, gy0) = res
+    assert torch.equal(o1, o0)
+    assert all(torch.equal(a, b) for a, b in zip(gk1, gk0))
+    if with_y0:
+        assert torch.equal(gy1, gy0)
+    scale = (g.abs() * torch.stack([k.detach().abs() for k in ks])).sum(1)
+    assert ((gc1 - gc0).abs() <= 1e-6 * scale + 1e-7).all(), (gc1, gc0)
+
+
+@pytest.mark.parametrize("kind", ["kan", "kanfet"])
+def test_host_autograd_fused_combine_matches_torch_expression(dev, kind):
+    """_Dopri5Grad with its stage combines in _CombFn against the torch expression: the same attempt
+    sequence and evaluations, the loss bitwise, the gradients to summation-order error (the d dt terms'
+    dot products are the only sums that change)."""
+    from fet_ode_amd import dopri5 as D
+    t = torch.tensor([0.0, 0.2, 0.5], dtype=torch.float64)
+    res = []
+    for fused in (True, False):
+        D._FUSED_COMB = fused
+        try:
+            res.append(_run(kind, dev, 64, t, 1e-3, 1e-4, False, y0_grad=True))
+        finally:
+            D._FUSED_COMB = True
+    (l1, g1, y1, a1, n1), (l0, g0, y0, a0, n0) = res
+    assert n1 == n0 and a1 == a0
+    assert l1 == l0
+    tol = 1e-5 if kind == "kan" else 1e-3   # KAN-FET: the dt chain amplifies (module docstring)
+    for n in g0:
+        assert _rel(g1[n], g0[n]) <= tol, (n, _rel(g1[n], g0[n]))
+    assert _rel(y1, y0) <= tol
