@@ -1011,23 +1011,33 @@ __device__ __forceinline__ void put_grad(float* p, float v, int accumulate) {
   if (p) *p = accumulate ? *p + v : v;
 }
 
-// thread per (input i, output o): the row segments in order, then the packing's chain rule
+// a block = 64 consecutive (input i, output o) pairs (o fastest); wave w sums the row segments of
+// features w, w + 4, ... in order (a thread per pair summing all 19 x rs partials ran 128 waves,
+// 48 us of load latency at B = 2048), then wave 0 applies the packing's chain rule from LDS
 // (wide_pack_kernel: base_weight; spline_weight * spline_scaler; 2 logistic_weight scale_logistic
-// logistic_scaler); the d/d(2 sigma) sums d_wl for the logistic_scaler pass
-__global__ void wide_kan_grad_kernel(fetode_kanlinear_t kl, const float* __restrict__ pw, int rs,
-                                     fetode_kanlinear_grad_t gr, float* __restrict__ d_wl, int accumulate) {
+// logistic_scaler) and writes the d/d(2 sigma) sums d_wl for the logistic_scaler pass
+__global__ __launch_bounds__(256) void wide_kan_grad_kernel(fetode_kanlinear_t kl, const float* __restrict__ pw, int rs,
+                                                            fetode_kanlinear_grad_t gr, float* __restrict__ d_wl,
+                                                            int accumulate) {
+  __shared__ float sv[kKF - 1][64];
   const int in = kl.in_features, out = kl.out_features;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= (int64_t)in * out) return;
-  const int o = (int)(t % out), i = (int)(t / out);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t t = (int64_t)blockIdx.x * 64 + lane;
+  const bool live = t < (int64_t)in * out;
+  const int o = live ? (int)(t % out) : 0, i = live ? (int)(t / out) : 0;
   const int64_t ncol = (int64_t)in * kKF, oi = (int64_t)o * in + i;
+  for (int f = wv; f < kKF - 1; f += 4) {
+    float s = 0.f;
+    const float* src = pw + (int64_t)i * kKF * out + (int64_t)f * out + o;
+#pragma unroll 4
+    for (int q = 0; q < rs; ++q) s += src[(int64_t)q * ncol * out];
+    sv[f][lane] = s;
+  }
+  __syncthreads();
+  if (wv != 0 || !live) return;
   float v[kKF - 1];
 #pragma unroll
-  for (int f = 0; f < kKF - 1; ++f) {
-    float s = 0.f;
-    for (int q = 0; q < rs; ++q) s += pw[((int64_t)q * ncol + (int64_t)i * kKF + f) * out + o];
-    v[f] = s;
-  }
+  for (int f = 0; f < kKF - 1; ++f) v[f] = sv[f][lane];
   put_grad(gr.base_weight ? gr.base_weight + oi : nullptr, v[0], accumulate);
   const float sc = kl.spline_scaler ? kl.spline_scaler[oi] : 1.0f;
   float dsc = 0.f;
@@ -1047,26 +1057,42 @@ __global__ void wide_kan_grad_kernel(fetode_kanlinear_t kl, const float* __restr
   }
 }
 
-// logistic a / b: the row groups in order; logistic_scaler: one wave per output, fixed-order sums
-__global__ void wide_kan_ab_ls_kernel(fetode_kanlinear_t kl, const float* __restrict__ abp, int n_rg,
-                                      const float* __restrict__ d_wl, fetode_kanlinear_grad_t gr, int accumulate) {
+// logistic a / b: a block = 64 (input, basis) sums, wave w adds row groups w, w + 16, ... in order,
+// then wave 0 the 16 wave sums in order (one thread per sum over all row groups ran 10 waves: 30 us
+// of load latency at B = 2048); logistic_scaler: one wave per output, fixed-order sums
+constexpr int kAbWaves = 16;
+__global__ __launch_bounds__(64 * kAbWaves) void wide_kan_ab_ls_kernel(fetode_kanlinear_t kl, const float* __restrict__ abp,
+                                                                       int n_rg, const float* __restrict__ d_wl,
+                                                                       fetode_kanlinear_grad_t gr, int accumulate) {
+  __shared__ float sab[kAbWaves][2][64];
   const int in = kl.in_features, out = kl.out_features;
   const int nab = in * kNB;
-  const int nabb = (nab + 255) / 256;
+  const int nabb = (nab + 63) / 64;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if ((int)blockIdx.x < nabb) {
-    const int t = blockIdx.x * 256 + threadIdx.x;
-    if (t >= nab) return;
+    const int t = blockIdx.x * 64 + lane;
     float sa = 0.f, sb = 0.f;
-    for (int q = 0; q < n_rg; ++q) {
-      sa += abp[((int64_t)q * nab + t) * 2];
-      sb += abp[((int64_t)q * nab + t) * 2 + 1];
+    if (t < nab)
+      for (int q = wv; q < n_rg; q += kAbWaves) {
+        const float2 v = *reinterpret_cast<const float2*>(&abp[((int64_t)q * nab + t) * 2]);
+        sa += v.x;
+        sb += v.y;
+      }
+    sab[wv][0][lane] = sa;
+    sab[wv][1][lane] = sb;
+    __syncthreads();
+    if (wv != 0 || t >= nab) return;
+    sa = sb = 0.f;
+    for (int u = 0; u < kAbWaves; ++u) {
+      sa += sab[u][0][lane];
+      sb += sab[u][1][lane];
     }
     put_grad(gr.logistic_a ? gr.logistic_a + t : nullptr, sa, accumulate);
     put_grad(gr.logistic_b ? gr.logistic_b + t : nullptr, sb, accumulate);
     return;
   }
   if (!kl.logistic_scaler) return;
-  const int o = ((int)blockIdx.x - nabb) * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int o = ((int)blockIdx.x - nabb) * kAbWaves + wv;
   if (o >= out) return;
   float s = 0.f;
   for (int q = lane; q < nab; q += 64)
@@ -1945,11 +1971,11 @@ int fetode_kanlinear_backward_wide(const fetode_kanlinear_t* kl, const fetode_fe
   hipLaunchKernelGGL(wide_kan_gw_kernel, dim3((unsigned)((p.tasks_gw + 3) / 4)), dim3(256), 0, s, (const float*)a.F, g, B,
                      ncol, out, p.rs, p.seg, ws + p.off_pw);
   LAUNCH_CHECK();
-  hipLaunchKernelGGL(wide_kan_grad_kernel, dim3((unsigned)(((int64_t)in * out + 255) / 256)), dim3(256), 0, s, *kl,
+  hipLaunchKernelGGL(wide_kan_grad_kernel, dim3((unsigned)(((int64_t)in * out + 63) / 64)), dim3(256), 0, s, *kl,
                      (const float*)(ws + p.off_pw), p.rs, *grads, ws + p.off_dwl, (int)accumulate);
   LAUNCH_CHECK();
-  const int nabb = (in * kNB + 255) / 256;
-  hipLaunchKernelGGL(wide_kan_ab_ls_kernel, dim3((unsigned)(nabb + (out + 3) / 4)), dim3(256), 0, s, *kl,
+  const int nabb = (in * kNB + 63) / 64;
+  hipLaunchKernelGGL(wide_kan_ab_ls_kernel, dim3((unsigned)(nabb + (out + kAbWaves - 1) / kAbWaves)), dim3(64 * kAbWaves), 0, s, *kl,
                      (const float*)a.abp, p.n_rg, (const float*)(ws + p.off_dwl), *grads, (int)accumulate);
   LAUNCH_CHECK();
   return FETODE_OK;
