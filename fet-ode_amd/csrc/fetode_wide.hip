@@ -808,17 +808,63 @@ struct FerroBwdPlan {
   int64_t tasks;
 };
 
+template <int K, int kBwdOGW>
+__global__ __launch_bounds__(256) void wide_ferro_bwd_kernel(WideFerroBwdArgs a);
+
+// resident waves of wide_ferro_bwd_kernel on the device (CUs x 4 waves x blocks per CU), 0 unknown
+int ferro_bwd_slots(int K) {
+  static int slots[2] = {-1, -1};
+  int& v = slots[K == 12 ? 1 : 0];
+  if (v < 0) {
+    v = 0;
+    int dev = 0, n_cu = 0, per = 0;
+    const int ogw = ferro_bwd_ogw();
+    const void* fn = K == 12 ? (ogw == 1 ? (const void*)wide_ferro_bwd_kernel<12, 1>
+                                : ogw == 4 ? (const void*)wide_ferro_bwd_kernel<12, 4> : (const void*)wide_ferro_bwd_kernel<12, 2>)
+                             : (ogw == 1 ? (const void*)wide_ferro_bwd_kernel<10, 1>
+                                : ogw == 4 ? (const void*)wide_ferro_bwd_kernel<10, 4> : (const void*)wide_ferro_bwd_kernel<10, 2>);
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, fn, 256, 0) == hipSuccess)
+      v = n_cu * per * 4;
+  }
+  return v;
+}
+
 FerroBwdPlan ferro_bwd_plan(int in, int out, int K, int64_t B) {
   FerroBwdPlan p{};
   const int kBwdOGW = ferro_bwd_ogw();
   const int OPG = 16 / (K / 2);
   p.n_og = (out + OPG - 1) / OPG;
   p.n_ogb = (p.n_og + kBwdOGW - 1) / kBwdOGW;
-  // row segments: enough waves to fill the chip (~8 per SIMD), each at least 256 rows
+  // row segments.  Every wave walks seg rows, so the kernel takes (waves / resident slots, rounded
+  // up) rounds of seg / 4 row steps: rs minimises rounds x (seg / 4 + a per-wave setup of ~16 steps)
+  // over segments of >= 64 rows (~8 waves per SIMD, >= 256 rows each, was 3 rounds of 342 rows at
+  // the ETT widths for 2.06 rounds of work: 8448 waves on 4096 slots).  FETODE_FERRO_BWD_RS = n
+  // fixes it (tuning knob).
   const int64_t base = (int64_t)p.n_ogb * in;
-  int64_t rs = (8 * 1024 + base - 1) / base;
-  const int64_t rmax = (B + 255) / 256;
-  rs = rs < rmax ? rs : rmax;
+  const int64_t rmax = std::max<int64_t>(1, std::min<int64_t>(64, (B + 63) / 64));
+  static const int rs_env = [] {
+    const char* e = getenv("FETODE_FERRO_BWD_RS");
+    return e ? atoi(e) : 0;
+  }();
+  int64_t rs = 1;
+  const int slots = ferro_bwd_slots(K);
+  if (rs_env > 0) {
+    rs = std::min<int64_t>(rs_env, (B + 3) / 4);
+  } else if (slots > 0) {
+    double best = 1e300;
+    for (int64_t r = 1; r <= rmax; ++r) {
+      const int64_t rounds = (base * r + slots - 1) / slots;
+      const double cost = (double)rounds * ((double)((B + r - 1) / r) / 4.0 + 16.0);
+      if (cost < best * 0.999) {
+        best = cost;
+        rs = r;
+      }
+    }
+  } else {
+    rs = std::min<int64_t>((8 * 1024 + base - 1) / base, (B + 255) / 256);
+  }
   p.rs = (int)(rs > 0 ? rs : 1);
   p.seg = (int)(((B + p.rs - 1) / p.rs + 3) / 4 * 4);
   p.rs = (int)((B + p.seg - 1) / p.seg);
