@@ -1054,10 +1054,15 @@ class _Dopri5Grad:
               if self.first_step is not None else self.select_initial_step(t[0], y, f0))
         t0s = t1s = t[0]
         coeff = [y] * 5
+        pending = None
         # single device: the control flow runs on host copies of t, t1 and dt (fp64, the same IEEE
-        # sums as the device tensors) and one read-back per attempt carries the ratio and y1's
-        # finiteness (asserted at the next attempt's top if y1 is accepted, where torchdiffeq asserts
-        # it); the tensors keep carrying the d/d dt terms.  Two syncs per attempt instead of nine.
+        # sums as the device tensors) and ONE read-back per attempt carries the ratio, the attempt's
+        # dt and y1's finiteness (asserted at the next attempt's top if y1 is accepted, where
+        # torchdiffeq asserts it; the dt-underflow check runs once the attempt's dt is read, i.e.
+        # after its evaluations); the tensors keep carrying the d/d dt terms.  One sync per attempt
+        # instead of nine.  The dense-output coefficients of an accepted step are formed only when
+        # an output time needs them (torchdiffeq forms them at every accept; the ones a later accept
+        # replaces before any output feed nothing: same solution, same gradient).
         host = not self.distributed
         if host:
             th = [float(v) for v in t.detach().cpu()]
@@ -1070,7 +1075,8 @@ class _Dopri5Grad:
                 t0 = t1s
                 if host:
                     t0h = t1h
-                    assert t0h + dth > t0h, "underflow in dt {}".format(dth)
+                    if dth is not None:
+                        assert t0h + dth > t0h, "underflow in dt {}".format(dth)
                     assert yfin, "non-finite values in state `y`"
                 else:
                     assert t0 + dt > t0, "underflow in dt {}".format(dt.item())
@@ -1078,9 +1084,12 @@ class _Dopri5Grad:
                 tol = self.atol + self.rtol * torch.max(y.abs(), y1.abs())
                 if host:
                     ratio = self.rms(err / tol)
-                    rv = torch.stack([ratio.detach().to(torch.float64),
+                    rv = torch.stack([ratio.detach().to(torch.float64), dt.detach(),
                                       torch.isfinite(y1.detach()).all().to(torch.float64)]).cpu()
-                    rh, y1fin = float(rv[0]), bool(rv[1] != 0)
+                    rh, y1fin = float(rv[0]), bool(rv[2] != 0)
+                    if dth is None:
+                        dth = float(rv[1])
+                        assert t0h + dth > t0h, "underflow in dt {}".format(dth)
                     accept = rh <= 1
                     self.attempts.append((t0h, dth, rh, accept))
                 else:
@@ -1091,12 +1100,7 @@ class _Dopri5Grad:
                     self.attempts.append((float(t0.detach()), float(dt.detach()), float(ratio.detach()), accept))
                     rh = None
                 if accept:
-                    dtm = dt.type_as(y)
-                    ym = self._stage(y, k, dtm * self.c_mid)
-                    fa, fb = k[0], k[-1]
-                    coeff = [y, dtm * fa, dtm * (fb - 4 * fa) - 11 * y - 5 * y1 + 16 * ym,
-                             dtm * (5 * fa - 3 * fb) + 18 * y + 14 * y1 - 32 * ym,
-                             2 * dtm * (fb - fa) - 8 * (y1 + y) + 16 * ym]
+                    pending = (y, y1, k, dt)
                     y, f0, t0s, t1s = y1, f1, t0, t0 + dt
                     if host:
                         t1h, yfin = t0h + dth, y1fin
@@ -1104,8 +1108,17 @@ class _Dopri5Grad:
                     t0s = t0
                 dt = self.optimal_step(dt, ratio, rh).clamp(self.min_step, self.max_step)
                 if host:
-                    dth = float(dt.detach())
+                    dth = None   # read with the next attempt's ratio
                 n_steps += 1
+            if pending is not None:   # interp._interp_fit of the last accepted step
+                yp, y1p, k, dtp = pending
+                dtm = dtp.type_as(yp)
+                ym = self._stage(yp, k, dtm * self.c_mid)
+                fa, fb = k[0], k[-1]
+                coeff = [yp, dtm * fa, dtm * (fb - 4 * fa) - 11 * yp - 5 * y1p + 16 * ym,
+                         dtm * (5 * fa - 3 * fb) + 18 * yp + 14 * y1p - 32 * ym,
+                         2 * dtm * (fb - fa) - 8 * (y1p + yp) + 16 * ym]
+                pending = None
             x = ((t[i] - t0s) / (t1s - t0s)).to(self.sdt)   # interp._interp_evaluate
             total, xp = coeff[0] + x * coeff[1], x
             for c in coeff[2:]:
