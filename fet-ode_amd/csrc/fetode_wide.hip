@@ -703,26 +703,35 @@ __global__ __launch_bounds__(256) void wide_ferro_bwd_kernel(WideFerroBwdArgs a)
   bool anydir = false;
 #pragma unroll
   for (int j = 0; j < kBwdOGW; ++j) anydir |= __builtin_amdgcn_ballot_w64(dir[j]) != 0;
-  float* gxp = a.gxp + (int64_t)ogb * a.B * in;
   // the next row group's U and g are loaded while this one computes (each row group's loads were
-  // a full global-memory round trip on the wave's chain); out-of-range rows read row r0 (valid)
-  auto ld = [&](int64_t b, float4& u, float* go) __attribute__((always_inline)) {
-    const int64_t bc = b < r1 ? b : r0;
-    u = a.U[bc * in + i];
+  // a full global-memory round trip on the wave's chain); out-of-range rows read row r0 (valid).
+  // Row pointers advance by 4 rows per step (the 64-bit row products per step were ~20 of the
+  // loop's ~150 instructions)
+  const float4* const u_r0 = a.U + r0 * in + i;
+  const float* const g_r0 = a.g + r0 * out;
+  const int64_t du = 4 * (int64_t)in, dg = 4 * (int64_t)out;
+  const float4* up = r0 + q < r1 ? u_r0 + q * (int64_t)in : u_r0;
+  const float* gp = r0 + q < r1 ? g_r0 + q * (int64_t)out : g_r0;
+  float* gxrow = a.gxp + (int64_t)ogb * a.B * in + (r0 + q) * in + i;
+  auto ld = [&](float4& u, float* go) __attribute__((always_inline)) {
+    u = *up;
 #pragma unroll
-    for (int j = 0; j < kBwdOGW; ++j) go[j] = a.g[bc * out + oo[j]];
+    for (int j = 0; j < kBwdOGW; ++j) go[j] = gp[oo[j]];
   };
   float4 un;
   float gn[kBwdOGW];
-  ld(r0 + q, un, gn);
-  for (int64_t b0 = r0; b0 < r1; b0 += 4) {
+  ld(un, gn);
+  for (int64_t b0 = r0; b0 < r1; b0 += 4, gxrow += du) {
     const int64_t b = b0 + q;
     const bool live = b < r1;
     const float4 u = live ? un : make_float4(0.f, 0.f, 0.f, 0.f);
     float gcur[kBwdOGW];
 #pragma unroll
     for (int j = 0; j < kBwdOGW; ++j) gcur[j] = gn[j];
-    ld(b + 4, un, gn);
+    const bool nx = b + 4 < r1;
+    up = nx ? up + du : u_r0;
+    gp = nx ? gp + dg : g_r0;
+    ld(un, gn);
     const float xv = u.x, e = u.y, omu = u.z, dup = u.w;
     // per row: m = 1 + wco cn; dm/dx = a1 cn + a2 cn (1 - cn); dm/dEc = a2 cn (1 - cn)
     const float wco = wc * omu, a1 = -wc * dup, a2 = -gs * wco;
@@ -748,7 +757,7 @@ __global__ __launch_bounds__(256) void wide_ferro_bwd_kernel(WideFerroBwdArgs a)
       dxacc = ok[j] ? pfma(gsh, dq, dxacc) : dxacc;                 // idle lanes: e = inf times P = 0 is NaN
     }
     const float row = row_sum16(dxacc.x + dxacc.y);
-    if (c == 0 && live) gxp[b * in + i] = row;
+    if (c == 0 && live) *gxrow = row;
   }
   // the four row quarters hold the same elements: quarters (0 + 2) + (1 + 3) onto lanes 0..15, then
   // the sums -> this row segment's parameter-gradient partials (reference layout)
