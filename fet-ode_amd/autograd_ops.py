@@ -692,11 +692,11 @@ class _WideLayerFlatFn(torch.autograd.Function):
 def _flat_params(kan, fer, ps):
     """(flat, layout) for _WideLayerFlatFn: the parameters' values concatenated (each slice padded
     to _FLAT_ALIGN floats), cached on the KANLinear and reused by every call of this graph.  A new
-    one is made when a parameter changed (version counter, identity) or once the graph's backward
+    one is made when a parameter changed (version counter, identity, storage) or once the graph's backward
     has reached it (its tensor hook), so a graph built after a backward never shares the old one.
     (A graph discarded unused leaves it cached; a later graph then routes through the same
     concatenation node, which saves no tensors and hands the same values to the parameters.)"""
-    key = tuple((id(p), p._version) for p in ps)
+    key = tuple([(id(p), p._version, p.data_ptr()) for p in ps])   # data_ptr: `.data` swaps (module.to)
     c = kan.__dict__.get("_fetode_flat")
     if c is not None and c[1] == key and c[3][0]:
         return c[0], c[2]
