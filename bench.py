@@ -467,7 +467,7 @@ def synthetic_mnist(batch, H=28, W=28, seed=0):
     return img.clamp(0, 1).to(torch.float32).unsqueeze(1)
 
 
-def ecg_rate(dev, reps=10, cpu_seconds=5.0, with_cpu=True, rtol=1e-3, atol=1e-4):
+def ecg_rate(dev, reps=50, cpu_seconds=5.0, with_cpu=True, rtol=1e-3, atol=1e-4):
     """BASELINE configs[2] (train_ecg_kan_fet_nn_ode.py:512-572): KanFet_NODE.eval() forward on a
     batch of 200 synthetic ECG200-shaped series (T = 96; the dataset is not in the image), latent
     64, 10 bases, dopri5 on [0, 1] at the class defaults rtol 1e-3 / atol 1e-4 (:512-530) or, for
@@ -482,7 +482,7 @@ def ecg_rate(dev, reps=10, cpu_seconds=5.0, with_cpu=True, rtol=1e-3, atol=1e-4)
     x = synthetic_ecg(200, seed=1)
     xd = x.to(dev)
     with torch.no_grad():
-        for _ in range(2):
+        for _ in range(20):   # clocks settle over the first back-to-back solves
             m(xd)
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
