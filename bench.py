@@ -634,7 +634,7 @@ def ett_rate(dev, batch=8192, reps=2, substeps=4, cpu_seconds=5.0, with_cpu=True
     return out
 
 
-def ett_dopri5_rate(dev, batch=8192, rtol=1e-3, atol=1e-4, small=256):
+def ett_dopri5_rate(dev, batch=8192, rtol=1e-3, atol=1e-4, small=(256, 1024)):
     """The reference forecaster's own solver call, odeint(dynamics, z0, t_fut, method="dopri5")
     (train_kan_fet_ett.py:192), with the KAN-FET latent field [64, 128, 64] (K = 10) on B = 8192
     96 -> 96 windows.  At torchdiffeq's default rtol 1e-7 / atol 1e-9 the fp32 KAN-FET field needs
@@ -642,7 +642,8 @@ def ett_dopri5_rate(dev, batch=8192, rtol=1e-3, atol=1e-4, small=256):
     on the host loop), so the line runs at rtol 1e-3 / atol 1e-4.  The forward's
     solve is ONE launch (fetode_wide_dopri5: persistent grid over the wide-layer tiles, DESIGN.md
     §4.8); `host_loop` times the host-driven loop on the same inputs (two wide-layer launches per
-    evaluation, one read-back per attempt; bitwise the same solution), `b256` both at B = 256."""
+    evaluation, one read-back per attempt; bitwise the same solution), `b256` / `b1024` both at
+    those batches (VERDICT r4 asked for B = 1024 beside 8192)."""
     from fet_ode_amd import dopri5 as D
     from fet_ode_amd import ett
     c = p = 96
@@ -698,11 +699,11 @@ def ett_dopri5_rate(dev, batch=8192, rtol=1e-3, atol=1e-4, small=256):
            "path": "fetode_wide_dopri5: the whole solve in one launch (persistent grid over the wide-layer tiles)",
            "host_loop": {**host, "same_solution": bool(torch.equal(yr, yh)),
                          "path": "dopri5 host loop: 2 fetode_wide_layer_forward per evaluation, a read-back per attempt"}}
-    if small:
-        rs, ys = run(small, True)
-        hs, yhs = run(small, False)
-        out[f"b{small}"] = {"resident": rs, "host_loop": hs, "same_solution": bool(torch.equal(ys, yhs)),
-                            "speedup": hs["ms_per_batch"] / rs["ms_per_batch"]}
+    for sb in small or ():
+        rs, ys = run(sb, True)
+        hs, yhs = run(sb, False)
+        out[f"b{sb}"] = {"resident": rs, "host_loop": hs, "same_solution": bool(torch.equal(ys, yhs)),
+                         "speedup": hs["ms_per_batch"] / rs["ms_per_batch"]}
     return out
 
 
