@@ -712,8 +712,9 @@ def ett_dopri5_train_rate(dev, batch=2048, P=24, tscale=0.05, iters=2, rtol=1e-3
     loop at :320-335: forward, MSE, loss.backward(), Adam) with the KAN-FET latent field [64, 128, 64].
     torchdiffeq's direct backprop runs through every stage, the error ratios and the step sizes; here
     the attempts are host-driven (dopri5._Dopri5Grad: one read-back per attempt) and every field
-    evaluation and VJP is the wide HIP kernels (_WideLayerFn: one launch forward, the Ferro and
-    KANLinear VJPs backward).  The untrained synthetic field is scaled by 0.1 (coef, KAN weights) and
+    evaluation and VJP is the wide HIP kernels (_WideLayerFlatFn: one launch forward, the Ferro and
+    KANLinear VJPs backward, the layer's parameters as one flat autograd input) and every stage
+    combine one HIP launch each way (_CombFn, d/d dt kept).  The untrained synthetic field is scaled by 0.1 (coef, KAN weights) and
     the 24 outputs span 1.15 time units so the latent state stays where the reference's own logistic
     basis has finite gradients (exp overflow x zero adjoint is NaN in its autograd beyond)."""
     from fet_ode_amd import ett
@@ -758,7 +759,8 @@ def ett_dopri5_train_rate(dev, batch=2048, P=24, tscale=0.05, iters=2, rtol=1e-3
             "workload": f"LatentNeuralODEForecaster(7 features, 96->{P}, latent 64, KANFET[64,128,64] K=10, field x0.1), "
                         f"t_fut = linspace(0, {(P - 1) * tscale:g}, {P}), dopri5 rtol {rtol:g} atol {atol:g}, batch {batch}",
             "path": "dopri5._Dopri5Grad: host-driven attempts (torchdiffeq's direct backprop incl. the step-size "
-                    "control), the wide HIP layer kernel per evaluation and the wide Ferro / KANLinear VJPs"}
+                    "control; one read-back per attempt), the wide HIP layer kernel per evaluation, the wide "
+                    "Ferro / KANLinear VJPs, stage combines as fetode_comb_forward / _backward"}
 
 
 def ett_encoder_rate(dev, batch=8192, ctx=96, reps=20, with_cpu=True, cpu_seconds=5.0):
