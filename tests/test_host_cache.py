@@ -64,3 +64,7 @@ def test_deepcopy_and_pickle_drop_hip_caches():
     f = ett.LatentNeuralODEForecaster(7, 96, 8)
     f.dynamics.net.__dict__["_fetode_wide_kf"] = (0, Desc())
     assert "_fetode_wide_kf" not in copy.deepcopy(f).dynamics.net.__dict__
+    # the wide layers' flat parameter tensor of a live graph (autograd_ops._flat_params) is a
+    # non-leaf tensor, which deepcopy refuses: it must not be copied either
+    kan.__dict__["_fetode_flat"] = (kan.base_weight * 1.0, (), ([], 0), [True])
+    assert "_fetode_flat" not in copy.deepcopy(m).layers[0].kan.__dict__
