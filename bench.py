@@ -707,7 +707,7 @@ def ett_dopri5_rate(dev, batch=8192, rtol=1e-3, atol=1e-4, small=(256, 1024)):
     return out
 
 
-def ett_dopri5_train_rate(dev, batch=2048, P=24, tscale=0.05, iters=2, rtol=1e-3, atol=1e-4):
+def ett_dopri5_train_rate(dev, batch=2048, P=24, tscale=0.05, iters=4, rtol=1e-3, atol=1e-4):
     """Training through the reference forecaster's own dopri5 call (train_kan_fet_ett.py:192, the
     loop at :320-335: forward, MSE, loss.backward(), Adam) with the KAN-FET latent field [64, 128, 64].
     torchdiffeq's direct backprop runs through every stage, the error ratios and the step sizes; here
