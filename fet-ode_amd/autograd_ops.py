@@ -542,9 +542,10 @@ def _wide_tensors(kan, fer):
 
 
 def _tkey(ts):
-    """Per-tensor (storage address, version counter, contiguity): a dtype or device change moves the
-    storage; the full check (fp32, contiguous, on the device) runs when a plan is (re)built."""
-    return tuple([(t.data_ptr(), t._version, t.is_contiguous()) for t in ts])
+    """Per-tensor (storage address, version counter, contiguity, dtype): a device change moves the
+    storage, set_() / restriding at the same address changes dtype or contiguity; the full check
+    (fp32, contiguous, on the device) runs when a plan is (re)built."""
+    return tuple([(t.data_ptr(), t._version, t.is_contiguous(), t.dtype) for t in ts])
 
 
 def _wide_key(kan, fer, device, parts=None):
