@@ -622,12 +622,24 @@ def ett_rate(dev, batch=8192, reps=2, substeps=4, cpu_seconds=5.0, with_cpu=True
                     ref8 = r.double()
                 n += 1
         cel = (time.perf_counter() - t0) / n
+        # the fp64 oracle on the same windows: the reference's own fp32 spread beside the GPU's
+        sd64 = {k: v.double() for k, v in sd.items()}
+        field64 = O.KANFETRef.from_state_dict({k[len("dynamics.net."):]: v for k, v in sd64.items()
+                                               if k.startswith("dynamics.net.")}, 2)
+        with torch.no_grad():
+            ref64 = E.ForecasterRef(sd64, lambda tt, zz: field64(zz))(xs.double(), tc.double(), rk4_substeps=substeps)
         d = (first8 - ref8).abs()
+        scale = float(ref64.abs().max())
+        err64, spread = float((first8 - ref64).abs().max()), float((ref8 - ref64).abs().max())
         out["parity"] = {"windows": 8, "max_abs_vs_oracle": float(d.max()),
                          "max_rel_vs_oracle": float(d.max() / ref8.abs().max().clamp_min(1e-30)),
                          "forecast_max_abs": float(ref8.abs().max()),
+                         "gpu_vs_fp64_max_rel": err64 / scale, "ref_fp32_vs_fp64_max_rel": spread / scale,
+                         "envelope_ok": err64 <= 4 * spread + 1e-5 * scale,
                          "note": "first call (fresh hysteresis state) of the GPU forecaster on the full batch, windows "
-                                 "0-7, vs oracle/ett_ref.py on those windows (torch CPU fp32)"}
+                                 "0-7, vs oracle/ett_ref.py on those windows (torch CPU fp32, and fp64: the "
+                                 "reference's own fp32 spread; envelope rule |gpu-fp64| <= 4 |ref32-fp64| + 1e-5 "
+                                 "scale, tests/test_gpu_production_oracle.py)"}
         out["cpu_baseline"] = {"value": 8 / cel, "unit": out["unit"].replace("1 GPU", "CPU"), "cores": cores,
                                "kind": "port", "sample": f"{n} forward(s) of 8 of the windows with oracle/ett_ref.py "
                                                          f"+ torch_ref.py (torch CPU fp32), {cel * n:.1f} s"}

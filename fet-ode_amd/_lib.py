@@ -106,6 +106,8 @@ SIGNATURES = {
     "fetode_fused_supported": (ctypes.c_int, [ctypes.POINTER(FieldDesc)]),
     "fetode_fused_set_small_batch_max": (ctypes.c_int64, [ctypes.c_int64]),
     "fetode_fused_set_tpw1_range": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int64]),
+    "fetode_fused_set_v8_range": (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int64]),
+    "fetode_fused_get_batch_ranges": (ctypes.c_int, [ctypes.c_void_p]),
     "fetode_dopri5_set_spin_limit": (ctypes.c_uint32, [ctypes.c_uint32]),
     "fetode_integrate_dopri5": (ctypes.c_int, [ctypes.POINTER(FieldDesc), _vp, _vp, ctypes.c_int64, _vp,
                                                ctypes.c_int32, ctypes.c_double, ctypes.c_double,

@@ -310,7 +310,12 @@ int fetode_comb_forward(const float* y0, const float* const* k, int32_t m, const
 
 int fetode_comb_backward(const float* g, const float* const* k, int32_t m, const float* c, float* const* gk,
                          float* gc, void* workspace, int64_t n, void* stream) {
-  if (n <= 0 || !g || !k || !c || m < 1 || m > kCombMax || (gc && !workspace))
+  if (n <= 0) {   // an empty state (as the forward accepts): d/d c = 0, nothing else to write
+    if (m < 1 || m > kCombMax) return set_err(FETODE_EINVAL, "comb_backward: bad arguments (m=%d)", m);
+    if (gc) HIP_CHECK_RET(hipMemsetAsync(gc, 0, sizeof(float) * (size_t)m, (hipStream_t)stream));
+    return FETODE_OK;
+  }
+  if (!g || !k || !c || m < 1 || m > kCombMax || (gc && !workspace))
     return set_err(FETODE_EINVAL, "comb_backward: bad arguments (m=%d)", m);
   CombPtrs p{};
   for (int j = 0; j < m; ++j) {

@@ -1201,9 +1201,11 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
   }
   if (!a.single_eval && tid == 0) *reinterpret_cast<f2*>(&a.solution[b * D]) = y;
   int par = 0;
+  STAMP_DECL
 
   auto eval_body = [&](f2 xin, auto fact_tag) __attribute__((always_inline)) -> f2 {
     constexpr bool F_ = decltype(fact_tag)::value;
+    STAMP(6);
     const float x0 = xin.x, x1 = xin.y;
     // ---------------- layer 0 ----------------
     float acc, fv1;
@@ -1219,6 +1221,7 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       acc = ffma(fw[1], fmac1 ? f1 : 0.f, acc);  // gate / exp jobs carry weight 0: never MAC e (inf * 0)
       fv1 = f1;
     }
+    STAMP(0);
     if constexpr (FERRO) {
       // gate_i / exp_i of the two inputs: slot 1, lanes 6..9 of every row (row_newbcast)
       const float g0 = dppm<0x156>(fv1), g1 = dppm<0x157>(fv1);
@@ -1240,7 +1243,9 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       acc += c == m0 ? sv.x : 0.0f;
       acc += c == m1 ? sv.y : 0.0f;
     }
+    STAMP(1);
     const float h = row_sum16(acc) + c0o;
+    STAMP(2);
     if constexpr (TAPE)
       if (trow && act && c == 0) trow[D + rr] = h;
     // ---------------- layer 1 (input h = h_rr) ----------------
@@ -1260,6 +1265,7 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
         re1 = false;
       }
     }
+    STAMP(3);
     {
       const uint64_t bal = __builtin_amdgcn_ballot_w64(h >= knh);
       int m = (int)__builtin_popcountll((bal >> (lane & 48)) & 0xFFFFull) - 1;
@@ -1279,9 +1285,11 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       const float sv = row_sum16(r + t);
       if ((lane & 31) == 0) reinterpret_cast<float*>(&s_part[par][w])[lane >> 5] = sv;
     }
+    STAMP(4);
     __syncthreads();
     const f2 p0 = s_part[par][0], p1 = s_part[par][1], p2 = s_part[par][2];
     par ^= 1;
+    STAMP(5);
     return f2{((p0.x + p1.x) + p2.x) + c1o0, ((p0.y + p1.y) + p2.y) + c1o1};
   };
 
@@ -1358,6 +1366,7 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
           ++jj;
         }
         y = y1;
+        STAMP(7);
       }
     };
     if (fact) run(FT{});
@@ -1574,9 +1583,322 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
       }
     }
   }
+  STAMP_FLUSH();
   if (FERRO && (DOPRI || a.single_eval || a.n_steps > 0)) {  // no evaluation: the state stays as it was
     if (r == 1 && ogate) a.state[b * D + ofx] = pvs;
     if (act && hgate) a.state[a.B * D + b * H + rr] = pvh;
+  }
+}
+
+// =============================================================================================
+// v8: one trajectory per TWO-wave workgroup — the strong-scaling shard kernel (rk4 inference).
+//
+// At B = 512 (the 8-way shard of the 4096 batch) v7 at one trajectory per wave leaves half the
+// SIMDs idle and each wave walks the whole evaluation (~1 500 cycles: ~170 VALU + 33
+// transcendentals issued by one wave, plus ~40 % of its cycles waiting on LDS round trips,
+// profiles/r06_shard_pmc.txt).  v8 gives each trajectory two waves (B = 512 -> 1 024 waves, one
+// per SIMD) and keeps LDS off the evaluation's chain except for ONE exchange of two partial sums:
+//   * wave w owns hidden units o = 5w .. 5w+4; unit u of the wave is 12 lanes, 3 in each of the
+//     4 rows (lanes 16r + 3u + j), lane index c = 3r + j in the unit;
+//   * layer 0: every lane knows x (both state dims, f2); lane c < 10 takes Ferro pair c of output o
+//     (input c / 5, elements 2(c % 5), +1) and forms its input's gate and exp(gs x) itself; lane c
+//     forms feature slots 2c, 2c+1 of the 24 (input c / 6: SiLU, 10 logistic, pad) and applies
+//     their weights; lane c holds knot interval c's spline cubics of edges (o, 0), (o, 1)
+//     (c = NI: the zero row) and the lane that owns x_i's interval adds edge (o, i) — interval
+//     from one wave ballot against the knots held one per unit lane; a group-of-3 DPP sum and two
+//     lane folds (permlane32 / permlane16 swaps) leave h_o on the unit's 12 lanes;
+//   * layer 1 (input h_o): lane c < 10 takes the element pair (o, d = 0 / 1, k = c), lane c < 11
+//     feature job c (logistic c, SiLU at c = NB) weighted for both outputs, the lane owning h_o's
+//     interval the two spline edges (o -> 0, 1), each lane the gate / exp(gs h_o) itself;
+//   * the wave's partial sums of both outputs (permlane32 swap, permlane16 fold, row sum) meet the
+//     other wave's through LDS and ONE workgroup barrier (double-buffered by evaluation parity);
+//     every lane of both waves forms k = (S_w0 + S_w1) + c in the same order, so both waves carry
+//     bitwise the same state and the stage combines run redundantly on every lane (torchdiffeq's
+//     op order, rk_common.rk4_alt_step_func).
+// Each butterfly / swap sum gives bitwise the same value on every lane it leaves it on (a + b and
+// b + a round alike), so no lane's copy of h_o or k drifts from another's.
+// =============================================================================================
+// TPB trajectories per workgroup (two waves each): TPB = 2 makes the workgroup four waves, which the
+// dispatcher spreads over a CU's four SIMDs — one wave per SIMD at B = 512 (with two-wave workgroups
+// two of them may share a SIMD pair).
+template <bool FERRO, int TPB>
+__global__ __launch_bounds__(128 * TPB) void v8_kernel(FusedArgs a) {
+  constexpr int D = 2, H = 10, K = FERRO ? 10 : 0, KP = 5, NB = 10, NG = 12, NI = NG - 1, NFL = 1 + NB;
+  constexpr int NFP = NFL + 1;  // feature slots per input: SiLU, NB logistic, pad
+  static_assert(D * NFP == 2 * 12 && NG == 12, "v8: 12 lanes per unit = 12 knots = 24 feature slots / 2");
+  __shared__ __attribute__((aligned(16))) float s_part[TPB][2][2][2];   // [traj][parity][wave][output]
+  constexpr int SCH = 32;
+  __shared__ float s_dt[SCH], s_oslope[SCH];
+  __shared__ int s_ostep[SCH], s_omode[SCH];
+
+  const int tid = threadIdx.x, tj = tid >> 7, w = (tid >> 6) & 1, lane = tid & 63, r = lane >> 4, q = lane & 15;
+  const bool act = q < 15;
+  const int u = act ? q / 3 : 0, c = 3 * r + (q % 3);   // unit in the wave, lane index in the unit
+  const int o = 5 * w + u;                              // hidden unit (layer-0 output, layer-1 input)
+  const int64_t b0 = (int64_t)blockIdx.x * TPB + tj;
+  const bool valid = b0 < a.B;          // an idle trajectory slot still takes part in the barriers
+  const int64_t b = valid ? b0 : 0;
+  const bool lead = valid && (tid & 127) == 0;
+  const float l2 = FETODE_LOG2E;
+  const bool fact = FERRO && a.plan[a.P0.flag] <= a.factor_limit && a.plan[a.P1.flag] <= a.factor_limit;
+  // the unit's 12 lanes (3 per row) as a ballot mask; layer 0's knots are the same on every unit:
+  // unit 0's lanes give its count as a uniform
+  const uint64_t umask = (0x0007000700070007ull << (3 * u));
+  constexpr uint64_t kMask0 = 0x0007000700070007ull;
+
+  // ---- layer 0, unit lane c: Ferro pair c (input ip, elements 2 kp, 2 kp + 1) ----
+  const bool pj = FERRO && act && c < 2 * KP;
+  const int ip = c >= KP ? 1 : 0;
+  f2 ep0 = splat(0.f), k20 = splat(0.f), kE0 = splat(0.f), cp0 = splat(0.f);
+  f2 ep1 = splat(0.f), k21 = splat(0.f), kE1 = splat(0.f), cp1 = splat(0.f);
+  if constexpr (FERRO) {
+    float t0[4][2], t1[4][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int64_t i0x = (int64_t)o * (D * K) + ip * K + (pj ? (c % KP) * 2 + h : 0);
+      const float g0 = pj ? a.plan[a.P0.fe_GEc + i0x] : 0.f;
+      t0[0][h] = fact ? ex2(g0) : g0;
+      t0[1][h] = pj ? a.plan[a.P0.fe_k2 + i0x] : 0.f;
+      t0[2][h] = pj ? a.plan[a.P0.fe_k2Ec + i0x] : 0.f;
+      t0[3][h] = pj ? a.plan[a.P0.fe_CPs2 + i0x] : 0.f;
+      // layer 1: element (o, d = h, k = c)
+      const int64_t i1x = (int64_t)h * (H * K) + o * K + (pj ? c : 0);
+      const float g1 = pj ? a.plan[a.P1.fe_GEc + i1x] : 0.f;
+      t1[0][h] = fact ? ex2(g1) : g1;
+      t1[1][h] = pj ? a.plan[a.P1.fe_k2 + i1x] : 0.f;
+      t1[2][h] = pj ? a.plan[a.P1.fe_k2Ec + i1x] : 0.f;
+      t1[3][h] = pj ? a.plan[a.P1.fe_CPs2 + i1x] : 0.f;
+    }
+    ep0 = f2{t0[0][0], t0[0][1]}; k20 = f2{t0[1][0], t0[1][1]}; kE0 = f2{t0[2][0], t0[2][1]}; cp0 = f2{t0[3][0], t0[3][1]};
+    ep1 = f2{t1[0][0], t1[0][1]}; k21 = f2{t1[1][0], t1[1][1]}; kE1 = f2{t1[2][0], t1[2][1]}; cp1 = f2{t1[3][0], t1[3][1]};
+  }
+  // ---- layer 0 feature slots 2c, 2c+1 of input fi = c / 6 (slot f: 0 SiLU, 1..NB logistic f-1, pad) ----
+  const int fi = c >= 6 ? 1 : 0;
+  float fna[2], fab[2], fml[2], fwv[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int f = (2 * c + s) % NFP;
+    fna[s] = 0.f; fab[s] = 0.f; fml[s] = 0.f; fwv[s] = 0.f;
+    if (act && f == 0) {
+      fna[s] = -l2;
+      fml[s] = 1.f;
+      fwv[s] = a.plan[a.P0.kw + (int64_t)o * (D * NFL) + fi * NFL];
+    } else if (act && f <= NB) {
+      fna[s] = a.plan[a.P0.lg + 2 * (fi * NB + f - 1)];
+      fab[s] = a.plan[a.P0.lg + 2 * (fi * NB + f - 1) + 1];
+      fwv[s] = a.plan[a.P0.kw + (int64_t)o * (D * NFL) + fi * NFL + f];
+    }
+  }
+  const f2 fw0 = f2{fwv[0], fwv[1]};
+  // ---- layer 0 splines: knot c of both inputs (the interval count), interval c's (knot, 1/width)
+  //      and cubics of edges (o, 0), (o, 1) (c = NI: the zero row: u = 0 for finite x, NaN otherwise)
+  const float kn0 = act ? a.plan[a.P0.knots + c] : __builtin_inff();
+  const float kn1 = act ? a.plan[a.P0.knots + NG + c] : __builtin_inff();
+  const bool ci = act && c < NI;
+  const f2 nukn0 = f2{ci ? -a.plan[a.P0.knots + c] : 0.f, ci ? -a.plan[a.P0.knots + NG + c] : 0.f};
+  const f2 urh0 = f2{ci ? a.plan[a.P0.rh + c] : 0.f, ci ? a.plan[a.P0.rh + NI + c] : 0.f};
+  float4 cs0[D], cs1[D];
+  {
+    const float4* sp0 = reinterpret_cast<const float4*>(a.plan + a.P0.sp);
+    const float4* sp1 = reinterpret_cast<const float4*>(a.plan + a.P1.sp);
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      cs0[i] = act ? sp0[(o * D + i) * (NI + 1) + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+      cs1[i] = act ? sp1[(i * H + o) * (NI + 1) + c] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  const f2 s0x = f2{cs0[0].x, cs0[1].x}, s0y = f2{cs0[0].y, cs0[1].y};
+  const f2 s0z = f2{cs0[0].z, cs0[1].z}, s0w = f2{cs0[0].w, cs0[1].w};
+  const f2 s1x = f2{cs1[0].x, cs1[1].x}, s1y = f2{cs1[0].y, cs1[1].y};
+  const f2 s1z = f2{cs1[0].z, cs1[1].z}, s1w = f2{cs1[0].w, cs1[1].w};
+  const float c0o = act ? a.plan[a.P0.fconst + o] : 0.f;
+  // ---- layer 1 (input h_o): feature job c (logistic c < NB, SiLU at NB), weights for both outputs
+  float hna = 0.f, hab = 0.f, hml = 0.f;
+  f2 hw = splat(0.f);
+  if (act && c < NB) {
+    hna = a.plan[a.P1.lg + 2 * (o * NB + c)];
+    hab = a.plan[a.P1.lg + 2 * (o * NB + c) + 1];
+    hw = f2{a.plan[a.P1.kw + (int64_t)0 * (H * NFL) + o * NFL + 1 + c], a.plan[a.P1.kw + (int64_t)1 * (H * NFL) + o * NFL + 1 + c]};
+  } else if (act && c == NB) {
+    hna = -l2;
+    hml = 1.f;
+    hw = f2{a.plan[a.P1.kw + (int64_t)0 * (H * NFL) + o * NFL], a.plan[a.P1.kw + (int64_t)1 * (H * NFL) + o * NFL]};
+  }
+  const float knh = act ? a.plan[a.P1.knots + o * NG + c] : __builtin_inff();
+  const float nukh = ci ? -a.plan[a.P1.knots + o * NG + c] : 0.f;
+  const float urhh = ci ? a.plan[a.P1.rh + o * NI + c] : 0.f;
+  const float c1o0 = a.plan[a.P1.fconst + 0], c1o1 = a.plan[a.P1.fconst + 1];
+
+  // hysteresis state (ferro_class.py:409): both layer-0 inputs on every lane, unit o's on its lanes
+  // the first evaluation is always at y0, so a fresh layer-0 state starts from y0 directly; layer 1's
+  // first input is only known inside it (re1)
+  bool re1 = FERRO && (a.init_mask & 2u);
+  f2 y = f2{a.y0[b * D + 0], a.y0[b * D + 1]};
+  f2 prev0 = splat(0.f);
+  float prev1 = 0.f;
+  if (FERRO) {
+    prev0 = (a.init_mask & 1u) ? y : f2{a.state[b * D + 0], a.state[b * D + 1]};
+    if (act) prev1 = a.state[a.B * D + b * H + o];
+  }
+  if (!a.single_eval && lead) *reinterpret_cast<f2*>(&a.solution[b * D]) = y;
+  int par = 0;
+  auto cubic2 = [](f2 x, f2 y_, f2 z, f2 w_, f2 uu) { return pfma(pfma(pfma(w_, uu, z), uu, y_), uu, x); };
+  auto interval = [](uint64_t bal, int cnt_extra, bool fin) {
+    constexpr int NI = NG - 1;
+    const int m = (int)__builtin_popcountll(bal) - 1 + cnt_extra;
+    return ((unsigned)m < (unsigned)NI && fin) ? m : NI;
+  };
+  STAMP_DECL
+
+  auto eval_body = [&](f2 xin, auto fact_tag) __attribute__((always_inline)) -> f2 {
+    constexpr bool F_ = decltype(fact_tag)::value;
+    STAMP(6);
+    // ---------------- layer 0 -> h_o on the unit's 12 lanes ----------------
+    float acc;
+    {
+      const float xf = fi ? xin.y : xin.x;   // this lane's feature input
+      float val[2];
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const float e = ex2(ffma(fna[s], xf, fab[s]));
+        const float sg = rcp(1.0f + e);
+        val[s] = fml[s] != 0.0f ? xf * sg : sg;
+      }
+      f2 pr = splat(0.0f);
+      if constexpr (FERRO) {
+        const float xg = ip ? xin.y : xin.x;
+        const float pv = ip ? prev0.y : prev0.x;
+        const float eg = ex2(ffma(-a.P0.gsl2e, xg - pv, 0.0f));
+        const float wg = ffma(rcp(1.0f + eg), -a.P0.wc, a.P0.wc);          // wc (1 - up)
+        const float e = F_ ? ex2(ffma(a.P0.gsl2e, xg, 0.0f)) : 0.0f;
+        pr = v4_pair<F_>(f2{e, wg}, f2{xg, 0.0f}, ep0, k20, kE0, cp0, splat(0.0f), a.P0.gsl2e);
+        prev0 = xin;   // ferro_class.py:409
+      }
+      STAMP(0);
+      pr = pfma(fw0, f2{val[0], val[1]}, pr);
+      // the two spline edges (o, 0), (o, 1): the lane owning x_i's knot interval
+      const int m0 = interval(__builtin_amdgcn_ballot_w64(xin.x >= kn0) & kMask0, 0, __builtin_isfinite(xin.x));
+      const int m1 = interval(__builtin_amdgcn_ballot_w64(xin.y >= kn1) & kMask0, 0, __builtin_isfinite(xin.y));
+      const f2 uu = (xin + nukn0) * urh0;
+      const f2 sv = cubic2(s0x, s0y, s0z, s0w, uu);
+      acc = (pr.x + pr.y) + ((c == m0 ? sv.x : 0.0f) + (c == m1 ? sv.y : 0.0f));
+    }
+    STAMP(1);
+    // unit sum: group of 3 in the row, then rows (0, 2), (1, 3) and (0, 1)
+    float hs = group3_sum(acc, q % 3);
+    {
+      float p = hs, t = hs;
+      permlane32_swap(p, t);
+      hs = p + t;
+      float p2 = hs, t2 = hs;
+      permlane16_swap(p2, t2);
+      hs = p2 + t2;
+    }
+    const float h = hs + c0o;
+    STAMP(2);
+    // ---------------- layer 1 (input h = h_o) ----------------
+    f2 acc01;
+    {
+      const int m = interval(__builtin_amdgcn_ballot_w64(h >= knh) & umask, 0, __builtin_isfinite(h));
+      const float e = ex2(ffma(hna, h, hab));
+      const float sg = rcp(1.0f + e);
+      const float v = hml != 0.0f ? h * sg : sg;
+      acc01 = splat(0.0f);
+      if constexpr (FERRO) {
+        const float pv = re1 ? h : prev1;
+        const float eg = ex2(ffma(-a.P1.gsl2e, h - pv, 0.0f));
+        const float wg = ffma(rcp(1.0f + eg), -a.P1.wc, a.P1.wc);
+        const float eh = F_ ? ex2(ffma(a.P1.gsl2e, h, 0.0f)) : 0.0f;
+        acc01 = v4_pair<F_>(f2{eh, wg}, f2{h, 0.0f}, ep1, k21, kE1, cp1, splat(0.0f), a.P1.gsl2e);
+        prev1 = h;   // ferro_class.py:409
+        re1 = false;
+      }
+      acc01 = pfma(hw, splat(v), acc01);
+      const float uh = (h + nukh) * urhh;
+      const f2 sab = cubic2(s1x, s1y, s1z, s1w, splat(uh));
+      acc01 += c == m ? sab : splat(0.0f);
+    }
+    STAMP(3);
+    // the wave's sums of both outputs: lanes 0-31 output 0, lanes 32-63 output 1
+    float sw;
+    {
+      float p = acc01.x, t = acc01.y;
+      permlane32_swap(p, t);
+      float s = p + t, s2 = s;
+      permlane16_swap(s, s2);
+      sw = row_sum16(s + s2);
+    }
+    STAMP(4);
+    if ((lane & 31) == 0) s_part[tj][par][w][lane >> 5] = sw;
+    __syncthreads();
+    const float4 pp = *reinterpret_cast<const float4*>(&s_part[tj][par][0][0]);
+    par ^= 1;
+    STAMP(5);
+    return f2{(pp.x + pp.z) + c1o0, (pp.y + pp.w) + c1o1};
+  };
+
+  auto load_steps = [&](int s0) {
+    __syncthreads();
+    for (int i = tid; i < SCH && s0 + i < a.n_steps; i += 128 * TPB) s_dt[i] = a.step_coef[4 * (s0 + i) + 0];
+    __syncthreads();
+  };
+  auto load_outs = [&](int j0) {
+    __syncthreads();
+    for (int i = tid; i < SCH; i += 128 * TPB) {
+      const bool in = j0 + i < a.T;
+      s_ostep[i] = in ? a.out_step[j0 + i] : -1;
+      s_omode[i] = in ? a.out_mode[j0 + i] : 1;
+      s_oslope[i] = in ? a.out_slope[j0 + i] : 0.f;
+    }
+    __syncthreads();
+  };
+  auto out_write = [&](int j, f2 v) __attribute__((always_inline)) {
+    if (lead) *reinterpret_cast<f2*>(&a.solution[((int64_t)j * a.B + b) * D]) = v;
+  };
+  auto interp = [](int mode, f2 y0v, f2 y1v, float sl) -> f2 {
+    return mode == 0 ? y0v : (mode == 1 ? y1v : y0v + splat(sl) * (y1v - y0v));
+  };
+  using FT = std::integral_constant<bool, true>;
+  using FF = std::integral_constant<bool, false>;
+  const f2 third = splat(1.0f / 3.0f);
+  int sb = 0, jb = 1, jj = 1;
+  load_steps(0);
+  load_outs(1);
+  auto run = [&](auto fact_tag) __attribute__((always_inline)) {
+    for (int s = 0; s < a.n_steps; ++s) {
+      if (s - sb == SCH) {
+        sb = s;
+        load_steps(s);
+      }
+      if (jj + 1 - jb >= SCH) {
+        jb = jj;
+        load_outs(jj);
+      }
+      const f2 dt = splat(s_dt[s - sb]);
+      const f2 k1 = eval_body(y, fact_tag);
+      const f2 k2 = eval_body(y + (dt * k1) * third, fact_tag);
+      const f2 k3 = eval_body(y + dt * (k2 - k1 * third), fact_tag);
+      const f2 k4 = eval_body(y + dt * ((k1 - k2) + k3), fact_tag);
+      const f2 y1 = y + (((k1 + splat(3.0f) * (k2 + k3)) + k4) * dt) * splat(0.125f);
+      while (jj < a.T) {
+        if (jj - jb == SCH) {
+          jb = jj;
+          load_outs(jj);
+        }
+        if (s_ostep[jj - jb] != s) break;
+        out_write(jj, interp(s_omode[jj - jb], y, y1, s_oslope[jj - jb]));
+        ++jj;
+      }
+      y = y1;
+      STAMP(7);
+    }
+  };
+  if (fact) run(FT{});
+  else run(FF{});
+  STAMP_FLUSH();
+  if (FERRO && valid && a.n_steps > 0) {  // no evaluation: the state stays as it was
+    if (lead) *reinterpret_cast<f2*>(&a.state[b * D]) = prev0;
+    if (act && c == 0) a.state[a.B * D + b * H + o] = prev1;   // each wave its own units
   }
 }
 
@@ -1594,6 +1916,8 @@ struct FusedEntry {
   fused_fn small_dopri, small_dopri_tape;  // v6 with the dopri5 driver (small batches)
   fused_fn small_tape, small_rk4_tape;     // v6 recording the fixed-grid training tape
   fused_fn fn_rk4_1;  // v7 rk4 at one trajectory per wave (inference, mid batches)
+  fused_fn rk4_v8;    // v8 rk4 at two waves per trajectory (inference, the strong-scaling shards)
+  fused_fn rk4_v8x2;  // the same, two trajectories per four-wave workgroup
 };
 const FusedEntry kFused[] = {
     // LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146)
@@ -1601,13 +1925,15 @@ const FusedEntry kFused[] = {
      small6_kernel<true, false>, small6_kernel<true, true>, fused4_kernel<10, 10, 10, 12, true, false, true>,
      fused4_kernel<10, 10, 10, 12, true, false, true, true>, small6_kernel<true, false, true, false>,
      small6_kernel<true, false, true, true>, small6_kernel<true, false, false, true>,
-     small6_kernel<true, true, false, true>, fused4_kernel<10, 10, 10, 12, true, true, false, false, 1>},
+     small6_kernel<true, true, false, true>, fused4_kernel<10, 10, 10, 12, true, true, false, false, 1>,
+     v8_kernel<true, 1>, v8_kernel<true, 2>},
     // LV KAN [2,10,2] (predator_prey.py:101)
     {2, 10, 2, 1, 10, 12, false, fused4_kernel<10, 2, 10, 12, false, false>, fused4_kernel<10, 2, 10, 12, false, true>,
      small6_kernel<false, false>, small6_kernel<false, true>, fused4_kernel<10, 2, 10, 12, false, false, true>,
      fused4_kernel<10, 2, 10, 12, false, false, true, true>, small6_kernel<false, false, true, false>,
      small6_kernel<false, false, true, true>, small6_kernel<false, false, false, true>,
-     small6_kernel<false, true, false, true>, fused4_kernel<10, 2, 10, 12, false, true, false, false, 1>},
+     small6_kernel<false, true, false, true>, fused4_kernel<10, 2, 10, 12, false, true, false, false, 1>,
+     v8_kernel<false, 1>, v8_kernel<false, 2>},
 };
 
 // Batches up to kSmallMax take v6 (one trajectory per 3-wave workgroup, latency-bound chain split
@@ -1630,6 +1956,20 @@ int64_t g_tpw1_lo = [] {
 int64_t g_tpw1_hi = [] {
   const char* e = getenv("FETODE_TPW1_HI");
   return e ? (int64_t)atoll(e) : (int64_t)1024;
+}();
+// Inference rk4 batches in (g_v8_lo, g_v8_hi] take v8 (two waves per trajectory), before every other
+// choice (env FETODE_V8_LO / FETODE_V8_HI).
+int64_t g_v8_lo = [] {
+  const char* e = getenv("FETODE_V8_LO");
+  return e ? (int64_t)atoll(e) : (int64_t)0;
+}();
+int64_t g_v8_hi = [] {
+  const char* e = getenv("FETODE_V8_HI");
+  return e ? (int64_t)atoll(e) : (int64_t)0;
+}();
+int g_v8_tpb = [] {   // trajectories per v8 workgroup (1: two waves, 2: four waves); env FETODE_V8_TPB
+  const char* e = getenv("FETODE_V8_TPB");
+  return e ? atoi(e) : 2;
 }();
 uint32_t g_dp_spin_limit = 0;   // fetode_dopri5_set_spin_limit (0: the built-in limits)
 
@@ -2097,7 +2437,12 @@ int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
   }();
   a.factor_limit = limit;
   const bool rk4 = !a.single_eval && a.method == FETODE_RK4;
-  if (rk4 && a.B > g_tpw1_lo && a.B <= g_tpw1_hi) {   // v7, one trajectory per wave (tapes too)
+  if (rk4 && !a.tape && a.B > g_v8_lo && a.B <= g_v8_hi) {   // v8, two waves per trajectory
+    if (g_v8_tpb == 2)
+      hipLaunchKernelGGL(e->rk4_v8x2, dim3(nblk(a.B, 2)), dim3(256), 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(e->rk4_v8, dim3((unsigned)a.B), dim3(128), 0, (hipStream_t)stream, a);
+  } else if (rk4 && a.B > g_tpw1_lo && a.B <= g_tpw1_hi) {   // v7, one trajectory per wave (tapes too)
     hipLaunchKernelGGL(e->fn_rk4_1, dim3((unsigned)a.B), dim3(64), 0, (hipStream_t)stream, a);
   } else if (a.B <= small_max()) {  // v6: one trajectory per 192-thread workgroup (training tapes too)
     const fused_fn fn = a.tape ? (rk4 ? e->small_rk4_tape : e->small_tape) : (rk4 ? e->small_rk4 : e->small);
@@ -2138,6 +2483,23 @@ int64_t fetode_fused_set_tpw1_range(int64_t lo, int64_t hi) {
   if (lo >= 0) g_tpw1_lo = lo;
   if (hi >= 0) g_tpw1_hi = hi;
   return prev;
+}
+
+int64_t fetode_fused_set_v8_range(int64_t lo, int64_t hi) {
+  const int64_t prev = g_v8_hi;
+  if (lo >= 0) g_v8_lo = lo;
+  if (hi >= 0) g_v8_hi = hi;
+  return prev;
+}
+
+int fetode_fused_get_batch_ranges(int64_t* out) {
+  if (!out) return set_err(FETODE_EINVAL, "fetode_fused_get_batch_ranges: null output");
+  out[0] = g_small_max;
+  out[1] = g_tpw1_lo;
+  out[2] = g_tpw1_hi;
+  out[3] = g_v8_lo;
+  out[4] = g_v8_hi;
+  return FETODE_OK;
 }
 
 int fetode_fused_supported(const fetode_field_t* f) {
@@ -2399,7 +2761,11 @@ int fetode_xrank_alloc(int64_t bytes, void** dev_ptr, void* handle) {
     const hipError_t e = hipGetLastError();
     return set_err(FETODE_EUNSUPPORTED, "xrank alloc: no fine-grained device memory (%s)", hipGetErrorString(e));
   }
-  HIP_CHECK_RET(hipMemset(p, 0, (size_t)bytes));
+  if (hipMemset(p, 0, (size_t)bytes) != hipSuccess) {
+    const hipError_t e = hipGetLastError();
+    (void)hipFree(p);
+    return set_err(FETODE_EHIP, "xrank alloc: hipMemset: %s", hipGetErrorString(e));
+  }
   hipIpcMemHandle_t h;
   const hipError_t e = hipIpcGetMemHandle(&h, p);
   if (e != hipSuccess) {

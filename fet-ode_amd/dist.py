@@ -188,6 +188,14 @@ class XRank:
                     opened.append(q.value)
             flags = [None] * self.world
             dist.all_gather_object(flags, bool(ok_open), group=group)
+            if not all(flags):
+                # release what this rank holds: the peer mappings opened so far and its own inbox
+                # (the failed XRank stays cached with ok = False for the life of the process)
+                for j, q in enumerate(opened):
+                    if j != self.rank and q:
+                        lib.fetode_xrank_close(ctypes.c_void_p(q))
+                if ptr.value:
+                    lib.fetode_xrank_free(ptr)
         if not all(flags):
             self.reason = self.reason or "a peer could not allocate or map its inbox"
             return

@@ -885,6 +885,7 @@ class _CombFn(torch.autograd.Function):
         _lib.check(lib.fetode_comb_forward(_lib.ptr(y0), _ptrs(ks), len(ks), c.data_ptr(), out.data_ptr(), n,
                                            _lib.stream_handle(out.device)), "fetode_comb_forward")
         ctx.save_for_backward(c, *ks)
+        ctx.y0_shape = None if y0 is None else y0.shape   # y0 may share k's size, not its shape
         return out
 
     @staticmethod
@@ -903,7 +904,7 @@ class _CombFn(torch.autograd.Function):
             _lib.check(lib.fetode_comb_backward(g.data_ptr(), _ptrs(ks), len(ks), c.data_ptr(), _ptrs(gks),
                                                 _lib.ptr(gc), _lib.ptr(ws), n, _lib.stream_handle(g.device)),
                        "fetode_comb_backward")
-        return (g if want_y0 else None, gc, *gks)
+        return (g.view(ctx.y0_shape) if want_y0 else None, gc, *gks)
 
 
 _FUSED_COMB = True   # tests flip it to compare with the torch expression
@@ -944,6 +945,9 @@ class _Dopri5Grad:
         self.safety = torch.as_tensor(options.get("safety", 0.9), **f64)
         self.ifactor = torch.as_tensor(options.get("ifactor", 10.0), **f64)
         self.dfactor = torch.as_tensor(options.get("dfactor", 0.2), **f64)
+        # host copies for _host_next_dt (no device read-back)
+        self._h = {k: np.float64(float(options.get(k, v))) for k, v in
+                   (("safety", 0.9), ("ifactor", 10.0), ("dfactor", 0.2))}
         self.min_step = float(options.get("min_step", 0.0))
         self.max_step = float(options.get("max_step", math.inf))
         self.max_num_steps = int(options.get("max_num_steps", 2 ** 31 - 1))
@@ -1045,6 +1049,23 @@ class _Dopri5Grad:
         factor = torch.min(self.ifactor, torch.max(self.safety / er ** (1.0 / ORDER), dfactor))
         return dt * factor
 
+    def _host_next_dt(self, dth, rh):
+        """optimal_step + clamp on host floats (numpy fp64, IEEE NaN / inf semantics): the next dt
+        up to the ulps of the device pow, NaN exactly when the device dt is NaN."""
+        h = self._h
+        with np.errstate(all="ignore"):
+            d, r = np.float64(dth), np.float64(rh)
+            if r == 0:
+                nxt = d * h["ifactor"]
+            else:
+                dfac = h["dfactor"] if r >= 1 else np.float64(1.0)
+                f = h["safety"] / r ** np.float64(1.0 / ORDER)
+                factor = f if np.isnan(f) else min(h["ifactor"], max(f, dfac))
+                nxt = d * factor
+            if not np.isnan(nxt):
+                nxt = min(max(nxt, np.float64(self.min_step)), np.float64(self.max_step))
+        return float(nxt)
+
     def integrate(self, tp):
         t = tp.to(device=self.dev, dtype=torch.float64)
         y = self.y0
@@ -1058,15 +1079,19 @@ class _Dopri5Grad:
         # single device: the control flow runs on host copies of t, t1 and dt (fp64, the same IEEE
         # sums as the device tensors) and ONE read-back per attempt carries the ratio, the attempt's
         # dt and y1's finiteness (asserted at the next attempt's top if y1 is accepted, where
-        # torchdiffeq asserts it; the dt-underflow check runs once the attempt's dt is read, i.e.
-        # after its evaluations); the tensors keep carrying the d/d dt terms.  One sync per attempt
-        # instead of nine.  The dense-output coefficients of an accepted step are formed only when
-        # an output time needs them (torchdiffeq forms them at every accept; the ones a later accept
+        # torchdiffeq asserts it); the tensors keep carrying the d/d dt terms.  One sync per attempt
+        # instead of nine.  The dt-underflow assert stays BEFORE the attempt's evaluations, as
+        # torchdiffeq's: the next dt is predicted on the host from the ratio just read
+        # (_host_next_dt, the same formula in fp64); only when the prediction is NaN or within a
+        # factor 2 of underflowing is the device dt read first (an extra sync in that rare case), so
+        # a failing check never advances a stateful field's hysteresis by six evaluations.  The
+        # dense-output coefficients of an accepted step are formed only when an output time needs them (torchdiffeq forms them at every accept; the ones a later accept
         # replaces before any output feed nothing: same solution, same gradient).
         host = not self.distributed
         if host:
             th = [float(v) for v in t.detach().cpu()]
             t1h, dth = th[0], float(dt.detach())
+            dt_est = dth
             yfin = bool(torch.isfinite(y).all())
         for i in range(1, len(t)):
             n_steps = 0
@@ -1075,6 +1100,8 @@ class _Dopri5Grad:
                 t0 = t1s
                 if host:
                     t0h = t1h
+                    if dth is None and not (dt_est == dt_est and t0h + 0.5 * dt_est > t0h):
+                        dth = float(dt.detach())   # near underflow / NaN: check the real dt first
                     if dth is not None:
                         assert t0h + dth > t0h, "underflow in dt {}".format(dth)
                     assert yfin, "non-finite values in state `y`"
@@ -1108,6 +1135,7 @@ class _Dopri5Grad:
                     t0s = t0
                 dt = self.optimal_step(dt, ratio, rh).clamp(self.min_step, self.max_step)
                 if host:
+                    dt_est = self._host_next_dt(dth, rh)
                     dth = None   # read with the next attempt's ratio
                 n_steps += 1
             if pending is not None:   # interp._interp_fit of the last accepted step

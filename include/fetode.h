@@ -128,6 +128,14 @@ int64_t fetode_fused_set_small_batch_max(int64_t b);
  * Defaults (320, 1024] (env FETODE_TPW1_LO / FETODE_TPW1_HI).  Sets lo / hi when >= 0; returns the
  * previous hi.  Process-wide tuning knob. */
 int64_t fetode_fused_set_tpw1_range(int64_t lo, int64_t hi);
+/* Inference rk4 batches lo < B <= hi run the v8 kernel: ONE trajectory per TWO-wave workgroup
+ * (each wave five hidden units, 12 lanes per unit; one LDS exchange of two partial sums per
+ * evaluation) — the 8- and 4-way strong-scaled shards, ahead of every other choice above.
+ * Env FETODE_V8_LO / FETODE_V8_HI.  Sets lo / hi when >= 0; returns the previous hi. */
+int64_t fetode_fused_set_v8_range(int64_t lo, int64_t hi);
+/* The current switch points, out[5] = {small_batch_max, tpw1_lo, tpw1_hi, v8_lo, v8_hi} (so a
+ * caller can save and restore every knob above). */
+int fetode_fused_get_batch_ranges(int64_t* out);
 
 /* One stateful field evaluation out = field(x) — KANFET.forward / KAN.forward.
  * x (B, in0), out (B, out_last), state (B*state_width, layout above) updated in place. */

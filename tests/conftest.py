@@ -31,20 +31,50 @@ def dev():
     return torch.device("cuda:0")
 
 
+class fused_ranges:
+    """Save every fused-integrator kernel switch (fetode_fused_get_batch_ranges: small-batch max,
+    one-trajectory-per-wave range, two-waves-per-trajectory range) and restore exactly those values
+    on exit — not literals, so a value set through the environment survives the test."""
+
+    def __init__(self):
+        import ctypes
+        from fet_ode_amd import _lib
+        self.lib = _lib.load()
+        self.saved = (ctypes.c_int64 * 5)()
+        _lib.check(self.lib.fetode_fused_get_batch_ranges(ctypes.addressof(self.saved)), "get_batch_ranges")
+        self.saved = list(self.saved)
+
+    def set(self, small=None, tpw1=None, v8=None):
+        if small is not None:
+            self.lib.fetode_fused_set_small_batch_max(small)
+        if tpw1 is not None:
+            self.lib.fetode_fused_set_tpw1_range(*tpw1)
+        if v8 is not None:
+            self.lib.fetode_fused_set_v8_range(*v8)
+        return self
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        sm, t_lo, t_hi, v_lo, v_hi = self.saved
+        self.lib.fetode_fused_set_small_batch_max(sm)
+        self.lib.fetode_fused_set_tpw1_range(t_lo, t_hi)
+        self.lib.fetode_fused_set_v8_range(v_lo, v_hi)
+        return False
+
+
 @pytest.fixture
 def kernel_switch():
     """Force the fused integrator's kernel: small(True) -> v6 at any batch, small(False) -> v4 / v7 at
-    two trajectories per wave (the one-per-wave range is switched off meanwhile)."""
-    from fet_ode_amd import _lib
-    lib = _lib.load()
-    prev = lib.fetode_fused_set_small_batch_max(-1)
-    prev_hi = lib.fetode_fused_set_tpw1_range(-1, 0)
+    two trajectories per wave (the one-per-wave and two-waves-per-trajectory ranges are switched off
+    meanwhile)."""
+    with fused_ranges() as fr:
+        fr.set(tpw1=(-1, 0), v8=(-1, 0))
 
-    def small(on):
-        lib.fetode_fused_set_small_batch_max(1 << 40 if on else 0)
-    yield small
-    lib.fetode_fused_set_small_batch_max(prev)
-    lib.fetode_fused_set_tpw1_range(-1, prev_hi)
+        def small(on):
+            fr.set(small=(1 << 40) if on else 0)
+        yield small
 
 
 @pytest.fixture(params=[0, 1, 2, 6], ids=["one-kernel", "split", "lane-sweep", "lane-sweep-kansum"])

@@ -1,26 +1,49 @@
 """Multi-process (world_size 2, gloo on CPU) tests of the trajectory-sharded DP logic.
-The GPU kernels cannot run here; the collective, sharding and gradient-bucket logic can."""
-import os
-import socket
+The GPU kernels cannot run here; the collective, sharding and gradient-bucket logic can.
 
+Harness (round 6): the ranks rendezvous through a file (``init_method="file://..."`` in pytest's
+tmp_path: no port to race for) and hand their results back as numpy arrays.  Round 5's harness put
+torch tensors on a torch.multiprocessing queue, which moves them through shared memory whose file
+descriptors the SENDING process serves; a worker that had already exited when the parent unpickled
+its result made ``q.get`` fail (one failure in 17 runs, after 8.4 s)."""
+import multiprocessing
+import os
+
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
-import torch.multiprocessing as mp
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+def _init(rank, world, init_file):
+    dist.init_process_group("gloo", init_method=f"file://{init_file}", rank=rank, world_size=world)
 
 
-def _worker(rank, world, port, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _spawn(target, world, tmp_path, *args):
+    """Run target(rank, world, init_file, q, *args) on `world` spawned ranks; returns their queue
+    items (plain Python / numpy objects) sorted by rank, after every rank exited with status 0."""
+    ctx = multiprocessing.get_context("spawn")
+    q = ctx.Queue()
+    init_file = str(tmp_path / f"rdzv_{target.__name__}")
+    procs = [ctx.Process(target=target, args=(r, world, init_file, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = [q.get(timeout=120) for _ in procs]
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    codes = [p.exitcode for p in procs]
+    assert codes == [0] * world, f"rank exit codes {codes}"
+    return sorted(res, key=lambda r: r[0])
+
+
+def _np(t):
+    return t.detach().cpu().clone().numpy()
+
+
+def _worker(rank, world, init_file, q):
+    _init(rank, world, init_file)
     import fet_ode_amd.dist as D
     torch.manual_seed(0)
     # reference-style linear model in plain torch (CPU): the shard/all-reduce logic is what's tested
@@ -38,28 +61,20 @@ def _worker(rank, world, port, q):
     loss = (x @ w.T).square().mean()
     loss.backward()
     D.allreduce_gradients([w], weights=(hi - lo) / 5)
-    q.put((rank, w.detach().clone(), w.grad.clone()))
+    q.put((rank, _np(w), _np(w.grad)))
     dist.destroy_process_group()
 
 
-def test_sharded_gradient_equals_global_gradient():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = sorted([q.get(timeout=120) for _ in procs], key=lambda r: r[0])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    (_, w0, g0), (_, w1, g1) = res
-    assert torch.equal(w0, w1)
+def test_sharded_gradient_equals_global_gradient(tmp_path):
+    (_, w0, g0), (_, w1, g1) = _spawn(_worker, 2, tmp_path)
+    assert np.array_equal(w0, w1), f"rank weights differ after broadcast: {w0} vs {w1}"
     torch.manual_seed(0)
     w = torch.randn(3, 2, requires_grad=True)
     xg = torch.arange(10, dtype=torch.float32).reshape(5, 2)
     (xg @ w.T).square().mean().backward()
-    assert torch.allclose(g0, w.grad, atol=1e-5) and torch.allclose(g1, w.grad, atol=1e-5)
+    ref = w.grad.numpy()
+    for r, g in ((0, g0), (1, g1)):
+        assert np.allclose(g, ref, atol=1e-5), f"rank {r} all-reduced gradient {g} vs global {ref}"
 
 
 def test_shard_bounds_rules():
@@ -102,49 +117,42 @@ def _sharded_grad(rank, world, sizes, group_opt):
     return sol.detach(), [p.grad.clone() for p in ps], [(a[1], a[3]) for a in s.attempts]
 
 
-def _dopri_worker(rank, world, port, q, sizes):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _dopri_worker(rank, world, init_file, q, sizes):
+    torch.set_num_threads(1)            # one fixed reduction order per rank
+    _init(rank, world, init_file)
     try:
         sol, grads, att = _sharded_grad(rank, world, sizes, "world")
         flat = torch.cat([g.reshape(-1) for g in grads])
         dist.all_reduce(flat)           # == allreduce_gradients(average=False)
-        q.put((rank, sol, flat, att))
+        q.put((rank, _np(sol), _np(flat), att))
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("sizes", [(3, 3), (4, 2)])
-def test_sharded_dopri5_gradient_through_step_control_fp64(sizes):
+def test_sharded_dopri5_gradient_through_step_control_fp64(sizes, tmp_path):
     """fp64 on CPU (no rounding noise): 2 ranks with the global-batch RMS norm take the single
     process's steps, and the summed gradients equal the single-process gradient — including the
     d loss / d dt terms that cross ranks (the all-reduced norm adjoint), with unequal shards too."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_dopri_worker, args=(r, 2, port, q, sizes)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = sorted([q.get(timeout=120) for _ in procs], key=lambda r: r[0])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    (_, s0, g0, a0), (_, s1, g1, a1) = res
+    (_, s0, g0, a0), (_, s1, g1, a1) = _spawn(_dopri_worker, 2, tmp_path, sizes)
     sol, grads, att = _sharded_grad(0, 1, (6,), None)
-    ref = torch.cat([g.reshape(-1) for g in grads])
-    assert a0 == a1 and [a[1] for a in a0] == [a[1] for a in att] and len(att) > 3
-    for (d0, _), (dr, _) in zip(a0, att):
-        assert abs(d0 - dr) <= 1e-12 * abs(dr)
-    assert torch.allclose(torch.cat([s0, s1], dim=1), sol, rtol=1e-12, atol=1e-14)
-    assert torch.equal(g0, g1)
-    assert ((g0 - ref).norm() / ref.norm()).item() <= 1e-10, ((g0 - ref).norm() / ref.norm()).item()
+    ref = torch.cat([g.reshape(-1) for g in grads]).numpy()
+    assert a0 == a1, f"the ranks took different attempts: {a0} vs {a1}"
+    assert [a[1] for a in a0] == [a[1] for a in att], \
+        f"accept pattern sharded {[a[1] for a in a0]} vs single process {[a[1] for a in att]}"
+    assert len(att) > 3, f"only {len(att)} attempts"
+    for j, ((d0, _), (dr, _)) in enumerate(zip(a0, att)):
+        assert abs(d0 - dr) <= 1e-12 * abs(dr), f"attempt {j}: dt sharded {d0!r} vs single process {dr!r}"
+    sol_sh = np.concatenate([s0, s1], axis=1)
+    assert np.allclose(sol_sh, sol.detach().numpy(), rtol=1e-12, atol=1e-14), \
+        f"solution max abs diff {np.abs(sol_sh - sol.detach().numpy()).max()}"
+    assert np.array_equal(g0, g1), f"all-reduced gradients differ between ranks: max {np.abs(g0 - g1).max()}"
+    rel = np.linalg.norm(g0 - ref) / np.linalg.norm(ref)
+    assert rel <= 1e-10, f"summed sharded gradient vs single process: relative {rel}"
 
 
-def _views_worker(rank, world, port, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _views_worker(rank, world, init_file, q):
+    _init(rank, world, init_file)
     import fet_ode_amd.dist as D
     # gradients that are views of one flat buffer (what the fused backward hands autograd):
     # reduced in place, no copies; a mixed set falls back to the flatten path
@@ -158,32 +166,20 @@ def _views_worker(rank, world, port, q):
     assert D._shared_flat([ps[1].grad, ps[0].grad]) is None
     assert D._shared_flat([flat[:4], flat[6:]]) is None
     D.allreduce_gradients(ps)
-    q.put((rank, flat.clone(), ps[0].grad.data_ptr() == flat.data_ptr()))
+    q.put((rank, _np(flat), ps[0].grad.data_ptr() == flat.data_ptr()))
     dist.destroy_process_group()
 
 
-def test_allreduce_in_place_on_shared_gradient_buffer():
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_views_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = sorted([q.get(timeout=120) for _ in procs], key=lambda r: r[0])
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
-    exp = torch.arange(10, dtype=torch.float32) * 1.5   # mean of rank 0 (x1) and rank 1 (x2)
-    for _, flat, still_view in res:
-        assert still_view and torch.equal(flat, exp)
+def test_allreduce_in_place_on_shared_gradient_buffer(tmp_path):
+    res = _spawn(_views_worker, 2, tmp_path)
+    exp = np.arange(10, dtype=np.float32) * 1.5   # mean of rank 0 (x1) and rank 1 (x2)
+    for r, flat, still_view in res:
+        assert still_view, f"rank {r}: the gradient is no longer a view of the flat buffer"
+        assert np.array_equal(flat, exp), f"rank {r}: {flat} vs {exp}"
 
 
-def _bcast_worker(rank, world, port, q):
-    import os
-    import torch.distributed as dist
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _bcast_worker(rank, world, init_file, q):
+    _init(rank, world, init_file)
     import fet_ode_amd as F
     import fet_ode_amd.dist as D
     torch.manual_seed(rank)          # deliberately different weights per rank
@@ -198,29 +194,14 @@ def _bcast_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_broadcast_parameters_gives_every_rank_rank0_weights():
+def test_broadcast_parameters_gives_every_rank_rank0_weights(tmp_path):
     """dist.broadcast_parameters (the efficient_kan init is not bitwise reproducible across
     processes, so DP ranks take rank 0's weights and persistent buffers); each rank's hysteresis
     memory — unequal shard sizes — is left alone (no mismatched collective, no overwrite)."""
-    import socket
-    import numpy as np
-    import torch.multiprocessing as mp
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    ps = [ctx.Process(target=_bcast_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in ps:
-        p.start()
-    res = dict(q.get(timeout=120) for _ in ps)
-    for p in ps:
-        p.join(60)
-        assert p.exitcode == 0
-    assert res[0][1] and res[1][1]
+    res = dict(_spawn(_bcast_worker, 2, tmp_path))
+    assert res[0][1] and res[1][1], "a rank's hysteresis memory was overwritten by the broadcast"
     for k in res[0][0]:
-        assert np.array_equal(res[0][0][k], res[1][0][k]), k
+        assert np.array_equal(res[0][0][k], res[1][0][k]), f"parameter {k} differs between ranks"
 
 
 def test_host_dopri5_grad_matches_oracle_fp64():
@@ -250,3 +231,32 @@ def test_host_dopri5_grad_matches_oracle_fp64():
     assert torch.allclose(s0, s1, rtol=1e-12, atol=1e-14)
     for a, b in zip(g0, g1):
         assert torch.allclose(a, b, rtol=1e-9, atol=1e-12), (a, b)
+
+
+@pytest.mark.parametrize("nan_at", [3, 9, 15])
+def test_host_dopri5_grad_dt_underflow_checked_before_evaluating(nan_at):
+    """the single-device _Dopri5Grad loop reads each attempt's dt back together with its
+    ratio, so its dt-underflow assert could only run after the attempt's six evaluations — six
+    evaluations more than torchdiffeq makes, which on a stateful (hysteretic) field leaves a later
+    prev_x.  A field that turns NaN after `nan_at` calls makes the ratio NaN, the next dt NaN, and
+    the next attempt's top assert fire: the host loop must fail with the oracle's message after
+    exactly the oracle's number of field evaluations."""
+    from fet_ode_amd.dopri5 import _Dopri5Grad
+    from oracle import torch_ref as O
+    t = torch.tensor([0.0, 0.5, 1.0], dtype=torch.float64)
+    calls = {}
+    for impl in ("host", "oracle"):
+        n = [0]
+
+        def f(tt, y):
+            n[0] += 1
+            return -y * (float("nan") if n[0] > nan_at else 1.0)
+
+        y0 = _y0_64()
+        with pytest.raises(AssertionError, match="underflow in dt"):
+            if impl == "host":
+                _Dopri5Grad(f, y0, 1e-6, 1e-8, {}, False, check_device=False).integrate(t)
+            else:
+                O.odeint(f, y0, t, rtol=1e-6, atol=1e-8)
+        calls[impl] = n[0]
+    assert calls["host"] == calls["oracle"], f"field evaluations before the assert: {calls}"

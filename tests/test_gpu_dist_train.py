@@ -72,7 +72,9 @@ def _worker(rank, world, port, q, case):
             D.allreduce_gradients(list(m.parameters()), average=False)
             s = F.dopri5.dopri5_solve.last
             extra = [(a[1], a[3]) for a in s.attempts]
-        q.put((rank, sol.detach().cpu(), _grads(m), extra))
+        # numpy: a tensor in the queue is a shared-memory handle served by this process, which may
+        # have exited when the parent unpickles it (ConnectionRefusedError)
+        q.put((rank, sol.detach().cpu().numpy(), _grads(m).numpy(), extra))
     finally:
         dist.destroy_process_group()
 
@@ -88,7 +90,7 @@ def _run(case):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    return res
+    return [(r, torch.from_numpy(s), torch.from_numpy(g), extra) for r, s, g, extra in res]
 
 
 def _rel(a, b):

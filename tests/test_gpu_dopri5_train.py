@@ -14,8 +14,8 @@ the next step size — a steep function of the parameters, the dt chain compound
 attempts, and central differences of the loss do not converge as eps shrinks.  With identical
 attempt sequences the fp32 paths and the fp64 oracle agree to ~0.5 % on short horizons, and at the
 reference's rtol 1e-7 over 35 points the gradient norm reaches ~1e17 in every implementation.  The
-KAN-FET checks are therefore: the fp64 oracle at 2e-2 where the sequences coincide, the loss, and
-bitwise run-to-run determinism."""
+KAN-FET checks are therefore: the fp64 oracle where the sequences coincide, with the reference's own
+fp32 autograd error as the yardstick (4x), the loss, and bitwise run-to-run determinism."""
 import numpy as np
 import pytest
 import torch
@@ -93,7 +93,7 @@ def _vs_oracle(kind, dev, B, t, rtol, atol, gtol, options=None, ltol=1e-5):
     assert abs(l0 - l1) <= ltol * abs(l1) + 1e-5, (l0, l1)
     worst = {n: _rel(g0[n], g1[n]) for n in g1}
     worst["y0"] = _rel(y0g0, y0g1)
-    if kind == "kan" and max(worst.values()) > gtol:
+    if max(worst.values()) > gtol:
         _, gh, y0gh, _, nh = _run(kind, dev, B, t, rtol, atol, False, options=options, y0_grad=True)
         assert nh == n1
         host = {n: _rel(gh[n], g1[n]) for n in g1}
@@ -101,10 +101,11 @@ def _vs_oracle(kind, dev, B, t, rtol, atol, gtol, options=None, ltol=1e-5):
         _, g32, y0g32, n32 = _oracle(kind, B, t, rtol, atol, options=options, dtype=torch.float32)
         ref32 = {n: _rel(g32[n], g1[n]) for n in g1}
         ref32["y0"] = _rel(y0g32, y0g1)
-        bad = {n: (e, host[n], ref32[n]) for n, e in worst.items() if e > max(gtol, 2 * host[n], 2 * ref32[n])}
-        assert not bad, bad
-        return
-    assert max(worst.values()) <= gtol, sorted(worst.items(), key=lambda kv: -kv[1])[:4]
+        k = 2 if kind == "kan" else 4
+        bad = {n: (e, host[n], ref32[n]) for n, e in worst.items() if e > max(gtol, 2 * host[n], k * ref32[n])}
+        print(f"{kind} B={B}: worst {max(worst.values()):.2e}, host {max(host.values()):.2e}, "
+              f"oracle fp32 {max(ref32.values()):.2e}")
+        assert not bad, f"(resident, host, oracle fp32) errors vs the fp64 oracle beyond the bar: {bad}"
 
 
 @pytest.mark.parametrize("B", [1, 16, 64])
@@ -123,9 +124,11 @@ def test_dopri5_train_kan_first_step_vs_oracle_fp64(dev):
 
 @pytest.mark.parametrize("B,rtol,T", [(1, 1e-1, 0.5), (64, 1e-2, 0.1)])
 def test_dopri5_train_kanfet_vs_oracle_fp64(dev, B, rtol, T):
-    """KAN-FET where the attempt sequences coincide: 2e-2 (ill-conditioned, module docstring)."""
+    """KAN-FET where the attempt sequences coincide: 1e-4 per tensor, or 2x the host path's error, or
+    4x the reference's own fp32 autograd error (ill-conditioned, module docstring) — the fixed 2e-2
+    bar of rounds 3-5 is gone."""
     t = torch.tensor(np.linspace(0, T, 3))
-    _vs_oracle("kanfet", dev, B, t, rtol, rtol * 0.1, 2e-2, ltol=1e-3)
+    _vs_oracle("kanfet", dev, B, t, rtol, rtol * 0.1, 1e-4, ltol=1e-3)
 
 
 @pytest.mark.parametrize("B", [1, 64, 300])

@@ -175,9 +175,10 @@ def test_fieldn_training_large_batch_matches_per_stage(dev):
 # [2,10,2] sweep's step-size-control adjoint, fieldn's per-evaluation VJP) + the row-batched
 # parameter VJPs — against the fp64 oracle's autograd (torchdiffeq detaches nothing: d loss / d dt
 # through the error ratio and the initial step is part of the gradient) and against autograd
-# through the host-driven solver (dopri5.py _Dopri5Grad).  Bars as tests/test_gpu_dopri5_train.py:
-# KAN 1e-4 per tensor (relative norm) or 2x what the host path / the reference's own fp32 autograd
-# already miss; KAN-FET 2e-2 (the hysteresis makes dopri5 gradients ill-conditioned, §4.10).
+# through the host-driven solver (dopri5.py _Dopri5Grad).  Bars (round 6): per tensor (relative
+# norm) 1e-4, or 2x what the host path misses, or k x what the reference's own fp32 autograd misses
+# (k = 2 KAN, 4 KAN-FET: the hysteresis makes dopri5 gradients ill-conditioned, §4.10); the dt
+# sequence within 4x the fp32 oracle's own dt spread (KAN 1e-5).
 # ---------------------------------------------------------------------------------------------
 
 def _d5_run(kind, widths, K, sd, y0, t, w, dev, resident, rtol=1e-3, atol=1e-4):
@@ -243,16 +244,23 @@ def test_fieldn_dopri5_training_vs_oracle_and_host(dev, kind, widths, K, B):
     # same accept pattern, every dt within fp32-vs-fp64 rounding of the error ratios (KAN-FET: the
     # hysteresis amplifies it, §4.10)
     assert [x[3] for x in ao] == [x[1] for x in a0]
-    np.testing.assert_allclose([x[1] for x in ao], [x[0] for x in a0], rtol=1e-5 if kind == "kan" else 1e-2)
+    # the yardstick: the oracle's OWN fp32 solve (its own step control) against its fp64 one — the
+    # dt sequence's spread and each gradient's (no fixed 1e-2 bar)
+    _, g32, n32, a32 = _d5_oracle(kind, sd, y0, t, w, dtype=torch.float32)
+    assert [x[3] for x in a32] == [x[3] for x in ao], "the fp32 oracle takes other step decisions"
+    dt64 = np.array([x[1] for x in ao])
+    spread = float(np.max(np.abs(np.array([x[1] for x in a32]) - dt64) / dt64))
+    dt_err = float(np.max(np.abs(np.array([x[0] for x in a0]) - dt64) / dt64))
+    assert dt_err <= (1e-5 if kind == "kan" else 4 * spread + 1e-6), \
+        f"dt vs the fp64 oracle: {dt_err:.3e} (oracle fp32 spread {spread:.3e})"
     err = {n: _nrel(g0[n], go[n]) for n in go}
     host = {n: _nrel(g1[n], go[n]) for n in go}
-    if kind == "kan":
-        _, g32, _, _ = _d5_oracle(kind, sd, y0, t, w, dtype=torch.float32)
-        ref32 = {n: _nrel(g32[n], go[n]) for n in go}
-        bad = {n: (e, host[n], ref32[n]) for n, e in err.items() if e > max(1e-4, 2 * host[n], 2 * ref32[n])}
-    else:
-        bad = {n: (e, host[n]) for n, e in err.items() if e > 2e-2}
-    assert not bad, bad
+    ref32 = {n: _nrel(g32[n], go[n]) for n in go}
+    k = 2 if kind == "kan" else 4
+    bad = {n: (e, host[n], ref32[n]) for n, e in err.items() if e > max(1e-4, 2 * host[n], k * ref32[n])}
+    assert not bad, f"gradients beyond the fp32 yardstick (resident, host, oracle fp32 vs fp64): {bad}"
+    print(f"{kind}{widths} B={B}: dt {dt_err:.2e} (spread {spread:.2e}); grad max rel "
+          f"{max(err.values()):.2e} (oracle fp32 {max(ref32.values()):.2e})")
 
 
 def test_fieldn_dopri5_training_is_the_resident_pair_and_deterministic(dev):

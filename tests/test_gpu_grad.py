@@ -495,10 +495,10 @@ def test_one_trajectory_per_wave_tape(dev):
         return {"y0": yc.grad.double(), **{n: ps[n].grad.double() for n in ps if ps[n].grad is not None}}
 
     e64, e32 = oracle(torch.float64), oracle(torch.float32)
-    prev = lib.fetode_fused_set_tpw1_range(-1, -1)
-    try:
+    from conftest import fused_ranges
+    with fused_ranges() as fr:
         for hi in (1 << 40, 0):
-            lib.fetode_fused_set_tpw1_range(0, hi)
+            fr.set(tpw1=(0, hi))
             m = F.KANFET([2, 10, 2], grid_size=5)
             m.load_state_dict(sd)
             m = m.to(dev)
@@ -510,8 +510,6 @@ def test_one_trajectory_per_wave_tape(dev):
                 err = (got[n] - e64[n]).abs().max().item()
                 yard = (e32[n] - e64[n]).abs().max().item()
                 assert err <= 4 * yard + 1e-4 * scale, f"hi={hi} {n}: |gpu-fp64|={err:.3e} ref32 {yard:.3e}"
-    finally:
-        lib.fetode_fused_set_tpw1_range(320, prev)
 
 
 def test_fused_backward_deterministic(dev, bwd_split):

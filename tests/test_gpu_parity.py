@@ -467,55 +467,68 @@ def test_small_batch_kernel_nonfinite_and_offgrid_inputs(dev, kernel_switch):
         assert ok, (k, md)
 
 
-@pytest.mark.parametrize("B", [1, 7, 512, 1000, 2048])
-def test_one_trajectory_per_wave_matches_two(dev, B):
-    """The rk4 inference kernel at one trajectory per wave (fetode_fused_set_tpw1_range: each hidden
-    unit's lane group split over both half-waves, the halves' partial sums met by a permlane32 swap;
-    forced at every batch by fetode_fused_set_tpw1_range(0, ...))
-    against the two-trajectories-per-wave kernel: KAN-FET 3 steps within 1e-5 per slice and the
-    same hysteresis state (1e-4 normwise, as the v6 comparison above), KAN over the 35-point grid
-    within the fixture bar, and rows with NaN / +-inf / off-grid / on-knot states giving the same
-    NaN pattern and finite values (1e-5)."""
+def _forced_kernel_vs_two_per_wave(dev, B, force):
+    """KAN-FET 3 rk4 steps with odd rows (NaN / +-inf / off-grid / on-knot states) under the kernel
+    `force` selects (a fused_ranges.set(...) argument dict) against the two-trajectories-per-wave
+    kernel, and KAN over the 35-point grid against the fixture under the forced kernel."""
     import fet_ode_amd as F
-    from fet_ode_amd import _lib
-    lib = _lib.load()
+    from conftest import fused_ranges
     g = load_golden("traj_kanfet")
     y0 = torch.from_numpy(g["y0_B64"]).repeat((B + 63) // 64, 1)[:B].clone()
     odd = torch.tensor([[float("nan"), 0.5], [0.5, float("inf")], [-float("inf"), 1.0], [12.0, -12.0],
                         [0.6, 2.2], [-2.2, -0.2], [2.19, -2.19]], dtype=torch.float32)
     y0[:min(B, 7)] = odd[:min(B, 7)]
     t = torch.from_numpy(g["t35"])[:4]
-    prev_s = lib.fetode_fused_set_small_batch_max(0)
-    prev_t = lib.fetode_fused_set_tpw1_range(-1, -1)
-    lo = 320   # the default lower bound (the knob returns only the previous upper bound)
+    off = dict(small=0, tpw1=(0, 0), v8=(0, 0))
     outs, states = [], []
-    try:
-        for t1 in (1 << 40, 0):
-            lib.fetode_fused_set_tpw1_range(0, t1)
+    with fused_ranges() as fr:
+        for forced in (True, False):
+            fr.set(**off)
+            if forced:
+                fr.set(**force)
             m = _kanfet_from(g, dev)
             with torch.no_grad():
                 outs.append(F.odeint(F.autonomous(m), y0.to(dev), t, method="rk4").cpu())
             states.append([l.ferro._prev.cpu() for l in m.layers])
         a, b = outs
-        assert torch.equal(torch.isnan(a), torch.isnan(b))
+        assert torch.equal(torch.isnan(a), torch.isnan(b)), "NaN pattern differs from the two-per-wave kernel"
         fin = torch.isfinite(b).all(-1).all(0)          # trajectories that stay finite
         if fin.any():
-            assert slice_rel_err(a[:, fin], b[:, fin]) <= 1e-5
-        for sa, sb in zip(*states):
-            assert torch.equal(torch.isnan(sa), torch.isnan(sb))
+            err = slice_rel_err(a[:, fin], b[:, fin])
+            assert err <= 1e-5, f"KAN-FET slices vs the two-per-wave kernel: {err}"
+        for li, (sa, sb) in enumerate(zip(*states)):
+            assert torch.equal(torch.isnan(sa), torch.isnan(sb)), f"layer {li} hysteresis NaN pattern"
             ok = torch.isfinite(sb).all(-1)
             if ok.any():
-                assert ((sa[ok] - sb[ok]).norm() / sb[ok].norm()).item() <= 1e-4
+                rel = ((sa[ok] - sb[ok]).norm() / sb[ok].norm()).item()
+                assert rel <= 1e-4, f"layer {li} hysteresis state vs the two-per-wave kernel: {rel}"
         gk = load_golden("traj_kan")
         yk = torch.from_numpy(gk["y0_B64"]).repeat((B + 63) // 64, 1)[:B]
         exp = torch.from_numpy(gk["sol_B64_t35"])[:, torch.arange(B) % 64]
-        lib.fetode_fused_set_tpw1_range(0, 1 << 40)
+        fr.set(**off).set(**force)
         m = F.KAN([2, 10, 2], grid_size=5)
         m.load_state_dict(golden_sd(gk))
         m = m.to(dev)
         with torch.no_grad():
             sol = F.odeint(F.autonomous(m), yk.to(dev), torch.from_numpy(gk["t35"]), method="rk4").cpu()
-        assert slice_rel_err(sol, exp) <= REL
-    finally:
-        lib.fetode_fused_set_small_batch_max(prev_s)
-        lib.fetode_fused_set_tpw1_range(lo, prev_t)
+        err = slice_rel_err(sol, exp)
+        assert err <= REL, f"KAN trajectories vs the reference fixture: {err}"
+
+
+@pytest.mark.parametrize("B", [1, 7, 512, 1000, 2048])
+def test_one_trajectory_per_wave_matches_two(dev, B):
+    """The rk4 inference kernel at one trajectory per wave (fetode_fused_set_tpw1_range: each hidden
+    unit's lane group split over both half-waves, the halves' partial sums met by a permlane32 swap;
+    forced at every batch) against the two-trajectories-per-wave kernel: KAN-FET 3 steps within 1e-5
+    per slice and the same hysteresis state (1e-4 normwise, as the v6 comparison above), KAN over the
+    35-point grid within the fixture bar, and rows with NaN / +-inf / off-grid / on-knot states giving
+    the same NaN pattern and finite values (1e-5)."""
+    _forced_kernel_vs_two_per_wave(dev, B, dict(tpw1=(0, 1 << 40)))
+
+
+@pytest.mark.parametrize("B", [1, 7, 512, 1000, 2048])
+def test_two_waves_per_trajectory_matches_two_per_wave(dev, B):
+    """v8 (fetode_fused_set_v8_range: one trajectory per two-wave workgroup, 12 lanes per hidden unit,
+    spline cubics in registers, one LDS exchange of the two waves' output partials per evaluation;
+    forced at every batch) under the same bars as the one-per-wave kernel above."""
+    _forced_kernel_vs_two_per_wave(dev, B, dict(v8=(0, 1 << 40)))

@@ -167,3 +167,46 @@ def test_forecaster_latent64_b8192_rows_vs_oracle(dev):
         with torch.no_grad():
             outs[dt] = ref(xs.to(dt), t_fut.to(dt), rk4_substeps=1)
     _envelope(got.cpu()[rows], outs[torch.float32], outs[torch.float64], "forecaster latent 64, B=8192 rows")
+
+
+def test_forecaster_bench_workload_96_horizon_vs_oracle(dev):
+    """BASELINE config 4 at its own horizon: the bench's ETT workload exactly —
+    LatentNeuralODEForecaster 96 -> 96, latent 64, KAN-FET field [64, 128, 64] scaled x 0.1,
+    odeint_rk4 with the reference TrainConfig's 4 substeps over t_fut = 0..95 (380 rk4 steps),
+    B = 8192, first call on fresh hysteresis state (train_kan_fet_ett.py:51-83, 155-197) — against
+    oracle/ett_ref.py in fp32 and fp64 on 16 windows spread over the batch (both row-tile edges and
+    12 seeded random rows).  Bar: the envelope rule above, |gpu - fp64| <= 4 |ref fp32 - fp64|
+    + 1e-5 x scale over the 16 x 96 forecasts."""
+    c = p = 96
+    torch.manual_seed(0)
+    m = ett.LatentNeuralODEForecaster(num_features=7, context_len=c, pred_len=p, latent_dim=64, solver="rk4")
+    with torch.no_grad():   # bench.ett_rate's scaling of the untrained field
+        for n, p_ in m.dynamics.net.named_parameters():
+            if n.endswith(("coef", "base_weight", "spline_weight", "logistic_weight")):
+                p_.mul_(0.1)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    m = m.to(dev)
+    g = torch.Generator().manual_seed(4)
+    series = torch.cumsum(torch.randn(B + c + p, 7, generator=g), 0) * 0.05
+    ds = ett.EnergyWindowDataset(series, series[:, -1], c, p, device=dev)
+    xb, _ = ds.batch(torch.arange(B, device=dev))
+    t_fut = torch.linspace(0.0, float(p - 1), steps=p)
+    with torch.no_grad():
+        got = m(xb, t_fut.to(dev), rk4_substeps=4)
+    assert got.shape == (B, p) and torch.isfinite(got).all()
+    gr = torch.Generator().manual_seed(22)
+    rows = torch.cat([torch.tensor([0, 1, B - 2, B - 1]),
+                      (torch.randperm(B - 4, generator=gr)[:12] + 2).sort().values])
+    xs = xb[rows.to(dev)].cpu()
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    outs = {}
+    for dt in (torch.float32, torch.float64):
+        sdd = {k: v.to(dt) for k, v in sd.items()}
+        field = O.KANFETRef.from_state_dict({k[len("dynamics.net."):]: v for k, v in sdd.items()
+                                             if k.startswith("dynamics.net.")}, 2)
+        ref = E.ForecasterRef(sdd, lambda tt, zz: field(zz))
+        with torch.no_grad():
+            outs[dt] = ref(xs.to(dt), t_fut.to(dt), rk4_substeps=4)
+    rel, spread = _envelope(got.cpu()[rows], outs[torch.float32], outs[torch.float64],
+                            "forecaster 96->96 x4 substeps, B=8192, 16 windows")
+    print(f"config-4 horizon: |gpu-fp64|/scale {rel:.3e}, |ref fp32-fp64|/scale {spread:.3e}")

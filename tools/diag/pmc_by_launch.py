@@ -30,6 +30,8 @@ for key, cs in sorted(acc.items(), key=lambda kv: -sum(kv[1].get("SQ_WAVE_CYCLES
         line += f" lds {c['SQ_INSTS_LDS']:.3g} salu {c.get('SQ_INSTS_SALU', 0):.3g} trans {c.get('SQ_INSTS_VALU_TRANS_F32', 0):.3g}"
         line += f" conflict/idx {c.get('SQ_LDS_BANK_CONFLICT', 0) / max(c.get('SQ_LDS_IDX_ACTIVE', 1), 1):.2f}"
         line += f" waitinstlds {c.get('SQ_WAIT_INST_LDS', 0):.3g} activelds {c.get('SQ_ACTIVE_INST_LDS', 0):.3g}"
+    if cyc and "SQ_ACTIVE_INST_VALU" in c:
+        line += f" | valu_busy {4 * c['SQ_ACTIVE_INST_VALU'] / (N_SIMD * cyc):.2f} waves {c.get('SQ_WAVES', 0):.0f}"
     if cyc:
         line += f" | cycles/xcd {cyc:.3g}"
     print(line)

@@ -43,6 +43,25 @@ if which in ("all", "small"):   # the strong-scaling shard (v6, B = 512) next to
             for _ in range(4):
                 F.odeint(F.autonomous(m), y0, t, method="rk4")
     torch.cuda.synchronize()
+if which == "shard":   # the 8-way strong shard B = 512: v7 one trajectory per wave (default) then v6 forced
+    import numpy as np
+    import bench
+    from fet_ode_amd import _lib
+    lib = _lib.load()
+    torch.manual_seed(0)
+    m = F.KANFET([2, 10, 2], grid_size=5).to(dev)
+    t = torch.tensor(np.linspace(0, 3.5, 35))
+    y0 = bench.lv_y0(512, 0).to(dev)
+    with torch.no_grad():
+        for _ in range(4):
+            F.odeint(F.autonomous(m), y0, t, method="rk4")
+        lo = lib.fetode_fused_set_tpw1_range(-1, 0)
+        prev = lib.fetode_fused_set_small_batch_max(1 << 40)
+        for _ in range(4):
+            F.odeint(F.autonomous(m), y0, t, method="rk4")
+        lib.fetode_fused_set_small_batch_max(prev)
+        lib.fetode_fused_set_tpw1_range(-1, lo)
+    torch.cuda.synchronize()
 if which in ("all", "train"):
     import numpy as np
     import bench
