@@ -60,6 +60,9 @@ def parse():
     # so 200 untimed solves (~35 ms) precede 500 timed ones (~85 ms)
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--settle-s", type=float, default=0.25,
+                    help="before the W warm-up solves: back-to-back solves for this many seconds so the GPU's "
+                         "clocks reach their loaded state (DESIGN.md §3; 0 disables)")
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
                     help="strong: global batch 4096 split over the ranks (the contract line); "
                          "weak: 4096 trajectories per rank")
@@ -775,6 +778,54 @@ def ett_dopri5_train_rate(dev, batch=2048, P=24, tscale=0.05, iters=4, rtol=1e-3
                     "Ferro / KANLinear VJPs, stage combines as fetode_comb_forward / _backward"}
 
 
+def ett_reference_iteration_rate(dev, batch=64, ctx=32, P=8, iters=2, rtol=1e-7, atol=1e-9, field_scale=0.1):
+    """The reference's OWN training iteration (train_kan_fet_ett.py:258-260 TrainConfig, :312-335
+    run_epoch): batch_size 64, context 32 -> pred 8, t_fut = linspace(0, 7, 8), the forecaster's
+    odeint(..., method="dopri5") at torchdiffeq's defaults (rtol 1e-7 / atol 1e-9), MSE, backward,
+    clip_grad_norm_(1.0), AdamW(lr 1e-3, weight_decay 1e-4) — with the KAN-FET latent field
+    [64, 128, 64] (config 4's substitution) scaled by `field_scale` (untrained weights,
+    synthetic 7-column series: the dataset is not in the image).  Host-driven dopri5 under autograd
+    (dopri5._Dopri5Grad), the wide HIP layer / VJP kernels."""
+    from fet_ode_amd import ett
+    import fet_ode_amd.dopri5  # noqa: F401
+    torch.manual_seed(0)
+    m = ett.LatentNeuralODEForecaster(num_features=7, context_len=ctx, pred_len=P, latent_dim=64, solver="dopri5",
+                                      rtol=rtol, atol=atol)
+    with torch.no_grad():
+        for n, p_ in m.dynamics.net.named_parameters():
+            if n.endswith(("coef", "base_weight", "spline_weight", "logistic_weight")):
+                p_.mul_(field_scale)
+    m = m.to(dev)
+    g = torch.Generator().manual_seed(4)
+    series = torch.cumsum(torch.randn(batch + ctx + P, 7, generator=g), 0) * 0.05
+    ds = ett.EnergyWindowDataset(series, series[:, -1], ctx, P, device=dev)
+    xb, yb = ds.batch(torch.arange(batch, device=dev))
+    t_fut = torch.linspace(0.0, float(P - 1), steps=P, device=dev)
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-4)
+    its, fin, att, nfev = [], True, [], []
+    for it in range(iters):
+        opt.zero_grad(set_to_none=True)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        loss = torch.nn.functional.mse_loss(m(xb, t_fut), yb)
+        s = F.dopri5.dopri5_solve.last
+        loss.backward()
+        torch.nn.utils.clip_grad_norm_(m.parameters(), 1.0)
+        opt.step()
+        torch.cuda.synchronize(dev)
+        its.append(time.perf_counter() - t0)
+        att.append(s.n_attempts)
+        nfev.append(s.nfev)
+        fin = fin and bool(torch.isfinite(loss))
+    el = float(np.mean(its))
+    return {"value": batch / el, "unit": f"training windows/s (the reference's iteration, B={batch})",
+            "ms_per_iter": el * 1e3, "attempts": att, "nfev": nfev, "finite": fin,
+            "workload": f"LatentNeuralODEForecaster(7 features, {ctx}->{P}, latent 64, KANFET[64,128,64] K=10, field "
+                        f"x{field_scale:g}), t_fut = linspace(0, {P - 1}, {P}), dopri5 rtol {rtol:g} atol {atol:g}, "
+                        f"MSE, clip_grad_norm 1.0, AdamW(1e-3, wd 1e-4), batch {batch}",
+            "path": "dopri5._Dopri5Grad (host-driven attempts under autograd), wide HIP layer + VJP kernels"}
+
+
 def ett_encoder_rate(dev, batch=8192, ctx=96, reps=20, with_cpu=True, cpu_seconds=5.0):
     """The encoder of the reference's KAN-FET ETT model (KAN_FET_LatentODE_DiffusionForecaster,
     train_kan_fet_ett.py:822-837): KANRNNEncoder(7 features, hidden 64, latent 64, 10 bases) over
@@ -1013,6 +1064,16 @@ def main():
         return F.odeint(func, y0d, t, method="rk4")
 
     with torch.no_grad():
+        # clock settle: the GPU raises its clocks over the first ~100 back-to-back solves (~20 ms:
+        # 181 -> 170 us per solve, profiles/r05_clock_ramp.log); a fixed wall time of untimed solves
+        # first, so a short warm-up (the driver's W = 5) times the loaded clock like a long one
+        settle_n, ts = 0, time.perf_counter()
+        while time.perf_counter() - ts < args.settle_s:
+            for _ in range(10):
+                solve()
+            settle_n += 10
+            torch.cuda.synchronize(dev)
+        settle_s = time.perf_counter() - ts
         for _ in range(args.warmup):
             solve()
         torch.cuda.synchronize(dev)
@@ -1079,6 +1140,8 @@ def main():
             "unit": "RK4 steps/s of the batch-4096 job" + (" (global batch split over GPUs)" if strong
                                                           else " (4096 per GPU, summed over GPUs)"),
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+            "clock_settle": {"solves": settle_n, "s": settle_s,
+                             "note": "untimed back-to-back solves before the warm-up (GPU clock ramp, DESIGN.md §3)"},
             # a bench "step" is one 34-step odeint solve; per RK4 step of the batch:
             "ms_per_rk4_step": ms_per_step / STEPS_PER_SOLVE,
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "fp32",
@@ -1094,7 +1157,9 @@ def main():
                          "kernel": ("fused4_kernel<10,10,10,12,true,true,false,false,2> (v7 rk4, two trajectories per wave)"
                                     if Bl > 1024 else
                                     "fused4_kernel<10,10,10,12,true,true,false,false,1> (v7 rk4, one trajectory per wave)"
-                                    if Bl > 320 else "small6_kernel<true,true,false,false> (v6 small-batch rk4 path)"),
+                                    if Bl > 512 else
+                                    "v8_kernel<true,2> (v8 rk4, one trajectory per two waves, two per workgroup)"
+                                    if Bl > 256 else "small6_kernel<true,true,false,false> (v6 small-batch rk4 path)"),
                          "kernel_ms": k_ms, "alg_bytes_per_launch": bytes_launch,
                          "traffic_source": traffic_src,
                          "valu": {"achieved_tflops": tflops, "peak_tflops": FP32_PEAK_TFLOPS,
@@ -1103,7 +1168,8 @@ def main():
                          # the kernel's actual bound: the SIMDs' VALU issue (PMC, committed profile)
                          "issue": (pmc_issue("fused4_kernel<10, 10, 10, 12, true, true, false, false, 2>")
                                    or pmc_issue("fused4_kernel<10, 10, 10, 12, true, true, false, false>")) if Bl > 1024
-                                  else pmc_issue("fused4_kernel<10, 10, 10, 12, true, true, false, false, 1>") if Bl > 320
+                                  else pmc_issue("fused4_kernel<10, 10, 10, 12, true, true, false, false, 1>") if Bl > 512
+                                  else pmc_issue("v8_kernel<true, 2>") if Bl > 256
                                   else pmc_issue("small6_kernel<true, true, false, false>")},
             # north_star: "MFMA utilisation against chip peak" — the path's MFMA kernels (the LV field
             # itself has no GEMM-shaped work): the ETT wide KAN-FET layer and the MNIST
@@ -1154,6 +1220,7 @@ def main():
             out["ett"]["encoder"] = ett_encoder_rate(dev, with_cpu=not args.no_cpu_baseline)
             out["ett"]["dopri5"] = ett_dopri5_rate(dev, batch=args.ett_batch)
             out["ett"]["dopri5"]["train"] = ett_dopri5_train_rate(dev)
+            out["ett"]["dopri5"]["train"]["reference_iteration"] = ett_reference_iteration_rate(dev)
         if world == 1 and not args.no_cpu_baseline:
             cb, ref_sol = cpu_baseline(sd, y0, t, args.cpu_solves)
             out["cpu_baseline"] = cb

@@ -363,7 +363,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   static_assert(H <= 10, "v4 layout: H <= 10 groups of 3 lanes");
   static_assert(!FERRO || K % 2 == 0, "v4 pairs Ferro elements (i, k), (i, k+1)");
   constexpr int KP = K / 2 > 0 ? K / 2 : 1;
-  static_assert(TPW == 2 || (TPW == 1 && HOT && !DOPRI && !TAPE), "one trajectory per wave: the rk4 inference path");
+  static_assert(TPW == 2 || (TPW == 1 && HOT && !DOPRI), "one trajectory per wave: the rk4 path");
   constexpr int NLG = TPW == 2 ? 3 : 6;                      // lanes per hidden unit
   // layer 0 (2 -> H): output o on a group of 3 lanes; layer 1 (H -> 2): hidden INPUT o on the
   // same group (v7): its features, its Ferro elements of both outputs (pairs (o, 0, k), (o, 1, k):
@@ -595,9 +595,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   const int si0 = spl0 ? gl : 0;
 
   // training tape: the two layer inputs of evaluation `ev` at tape[(ev B + b)(D + H) + c]
-  // uniform: the inference path skips every tape op (the dopri5 driver has a taped instantiation
-  // of its own: the inference one carries no tape code, its registers are full)
-  bool taping = (!DOPRI || TAPE) && a.tape != nullptr;
+  // TAPE = false (every inference instantiation) carries no tape code at all: the fixed-grid
+  // training forward and the dopri5 driver have taped instantiations of their own
+  bool taping = TAPE && a.tape != nullptr;
   // the dopri5 tape holds the first tape_cap evaluations (the host re-runs a longer solve)
   int64_t tape_left = DOPRI ? a.dp.tape_cap : 0;
   // dopri5 training rows also hold the evaluation's output k after the two layer inputs
@@ -1918,6 +1918,7 @@ struct FusedEntry {
   fused_fn fn_rk4_1;  // v7 rk4 at one trajectory per wave (inference, mid batches)
   fused_fn rk4_v8;    // v8 rk4 at two waves per trajectory (inference, the strong-scaling shards)
   fused_fn rk4_v8x2;  // the same, two trajectories per four-wave workgroup
+  fused_fn fn_tape, fn_rk4_tape, fn_rk4_1_tape;  // v4 / v7 recording the fixed-grid training tape
 };
 const FusedEntry kFused[] = {
     // LV KAN-FET [2,10,2], K=10 (train_kanfet_node_predprey.py:146)
@@ -1926,14 +1927,16 @@ const FusedEntry kFused[] = {
      fused4_kernel<10, 10, 10, 12, true, false, true, true>, small6_kernel<true, false, true, false>,
      small6_kernel<true, false, true, true>, small6_kernel<true, false, false, true>,
      small6_kernel<true, true, false, true>, fused4_kernel<10, 10, 10, 12, true, true, false, false, 1>,
-     v8_kernel<true, 1>, v8_kernel<true, 2>},
+     v8_kernel<true, 1>, v8_kernel<true, 2>, fused4_kernel<10, 10, 10, 12, true, false, false, true>,
+     fused4_kernel<10, 10, 10, 12, true, true, false, true>, fused4_kernel<10, 10, 10, 12, true, true, false, true, 1>},
     // LV KAN [2,10,2] (predator_prey.py:101)
     {2, 10, 2, 1, 10, 12, false, fused4_kernel<10, 2, 10, 12, false, false>, fused4_kernel<10, 2, 10, 12, false, true>,
      small6_kernel<false, false>, small6_kernel<false, true>, fused4_kernel<10, 2, 10, 12, false, false, true>,
      fused4_kernel<10, 2, 10, 12, false, false, true, true>, small6_kernel<false, false, true, false>,
      small6_kernel<false, false, true, true>, small6_kernel<false, false, false, true>,
      small6_kernel<false, true, false, true>, fused4_kernel<10, 2, 10, 12, false, true, false, false, 1>,
-     v8_kernel<false, 1>, v8_kernel<false, 2>},
+     v8_kernel<false, 1>, v8_kernel<false, 2>, fused4_kernel<10, 2, 10, 12, false, false, false, true>,
+     fused4_kernel<10, 2, 10, 12, false, true, false, true>, fused4_kernel<10, 2, 10, 12, false, true, false, true, 1>},
 };
 
 // Batches up to kSmallMax take v6 (one trajectory per 3-wave workgroup, latency-bound chain split
@@ -1959,13 +1962,16 @@ int64_t g_tpw1_hi = [] {
 }();
 // Inference rk4 batches in (g_v8_lo, g_v8_hi] take v8 (two waves per trajectory), before every other
 // choice (env FETODE_V8_LO / FETODE_V8_HI).
+// Measured (tools/diag/batch_sweep.py, profiles/r06_v8_sweep.log, us per 34-step solve, v6 / v7 one
+// per wave / v8 at two trajectories per four-wave workgroup): B = 256 77 / 93 / 84, 320 94 / 92 / 84,
+// 448 96 / 93 / 84, 512 97 / 93 / 85, 576 124 / 93 / 112 (v8 past one wave per SIMD), 1024 140 / 98 / 112.
 int64_t g_v8_lo = [] {
   const char* e = getenv("FETODE_V8_LO");
-  return e ? (int64_t)atoll(e) : (int64_t)0;
+  return e ? (int64_t)atoll(e) : (int64_t)256;
 }();
 int64_t g_v8_hi = [] {
   const char* e = getenv("FETODE_V8_HI");
-  return e ? (int64_t)atoll(e) : (int64_t)0;
+  return e ? (int64_t)atoll(e) : (int64_t)512;
 }();
 int g_v8_tpb = [] {   // trajectories per v8 workgroup (1: two waves, 2: four waves); env FETODE_V8_TPB
   const char* e = getenv("FETODE_V8_TPB");
@@ -2443,12 +2449,13 @@ int launch_fused(const fetode_field_t* f, FusedArgs& a, void* stream) {
     else
       hipLaunchKernelGGL(e->rk4_v8, dim3((unsigned)a.B), dim3(128), 0, (hipStream_t)stream, a);
   } else if (rk4 && a.B > g_tpw1_lo && a.B <= g_tpw1_hi) {   // v7, one trajectory per wave (tapes too)
-    hipLaunchKernelGGL(e->fn_rk4_1, dim3((unsigned)a.B), dim3(64), 0, (hipStream_t)stream, a);
+    hipLaunchKernelGGL(a.tape ? e->fn_rk4_1_tape : e->fn_rk4_1, dim3((unsigned)a.B), dim3(64), 0, (hipStream_t)stream, a);
   } else if (a.B <= small_max()) {  // v6: one trajectory per 192-thread workgroup (training tapes too)
     const fused_fn fn = a.tape ? (rk4 ? e->small_rk4_tape : e->small_tape) : (rk4 ? e->small_rk4 : e->small);
     hipLaunchKernelGGL(fn, dim3((unsigned)a.B), dim3(192), 0, (hipStream_t)stream, a);
   } else {                              // v4: two trajectories per one-wave workgroup
-    hipLaunchKernelGGL(rk4 ? e->fn_rk4 : e->fn, dim3(nblk(a.B, 2)), dim3(64), 0, (hipStream_t)stream, a);
+    const fused_fn fn = a.tape ? (rk4 ? e->fn_rk4_tape : e->fn_tape) : (rk4 ? e->fn_rk4 : e->fn);
+    hipLaunchKernelGGL(fn, dim3(nblk(a.B, 2)), dim3(64), 0, (hipStream_t)stream, a);
   }
   LAUNCH_CHECK();
   return FETODE_OK;

@@ -125,13 +125,14 @@ int64_t fetode_fused_set_small_batch_max(int64_t b);
 /* Inference rk4 batches lo < B <= hi run the v7 kernel at ONE trajectory per wave (each hidden
  * unit's lane group split over both half-waves: half the Ferro rounds per lane — the latency-bound
  * batches of a strong-scaled shard), ahead of the small-batch switch above; training tapes too.
- * Defaults (320, 1024] (env FETODE_TPW1_LO / FETODE_TPW1_HI).  Sets lo / hi when >= 0; returns the
+ * Defaults (320, 1024], below the v8 range (env FETODE_TPW1_LO / FETODE_TPW1_HI).  Sets lo / hi when >= 0; returns the
  * previous hi.  Process-wide tuning knob. */
 int64_t fetode_fused_set_tpw1_range(int64_t lo, int64_t hi);
 /* Inference rk4 batches lo < B <= hi run the v8 kernel: ONE trajectory per TWO-wave workgroup
  * (each wave five hidden units, 12 lanes per unit; one LDS exchange of two partial sums per
- * evaluation) — the 8- and 4-way strong-scaled shards, ahead of every other choice above.
- * Env FETODE_V8_LO / FETODE_V8_HI.  Sets lo / hi when >= 0; returns the previous hi. */
+ * evaluation; two trajectories per four-wave workgroup) — the 8-way strong-scaled shard, ahead of
+ * every other choice above.  Default (256, 512] (env FETODE_V8_LO / FETODE_V8_HI).  Sets lo / hi
+ * when >= 0; returns the previous hi. */
 int64_t fetode_fused_set_v8_range(int64_t lo, int64_t hi);
 /* The current switch points, out[5] = {small_batch_max, tpw1_lo, tpw1_hi, v8_lo, v8_hi} (so a
  * caller can save and restore every knob above). */

@@ -15,7 +15,8 @@ attempts, and central differences of the loss do not converge as eps shrinks.  W
 attempt sequences the fp32 paths and the fp64 oracle agree to ~0.5 % on short horizons, and at the
 reference's rtol 1e-7 over 35 points the gradient norm reaches ~1e17 in every implementation.  The
 KAN-FET checks are therefore: the fp64 oracle where the sequences coincide, with the reference's own
-fp32 autograd error as the yardstick (4x), the loss, and bitwise run-to-run determinism."""
+fp32 autograd error (over re-roundings of its parameters) as the yardstick, the loss, and bitwise
+run-to-run determinism."""
 import numpy as np
 import pytest
 import torch
@@ -55,14 +56,19 @@ def _run(kind, dev, B, t, rtol, atol, resident, options=None, y0_grad=False, see
     return loss.item(), grads, (y0.grad.cpu() if y0_grad else None), att, s.nfev
 
 
-def _oracle(kind, B, t, rtol, atol, options=None, seed=0, dtype=torch.float64):
+def _oracle(kind, B, t, rtol, atol, options=None, seed=0, dtype=torch.float64, perturb=None):
     """autograd through the oracle (fp64 by default; fp32 = the reference's own arithmetic in its own
-    op order): loss, param grads, y0 grad, nfev."""
+    op order): loss, param grads, y0 grad, nfev.  perturb=j: every parameter scaled by
+    (1 + 6e-8 N(0, 1)) from generator seed j — an equally valid fp32 rounding of the same model (the
+    controls of oracle/parity.py)."""
     from oracle import torch_ref as O
     g = load_golden("traj_kanfet" if kind == "kanfet" else "traj_kan")
     sd = golden_sd(g)
     import fet_ode_amd as F
     names = [n for n, _ in (F.KANFET if kind == "kanfet" else F.KAN)([2, 10, 2], grid_size=5).named_parameters()]
+    if perturb is not None:
+        gen = torch.Generator().manual_seed(perturb)
+        sd = {k: (v * (1 + 6e-8 * torch.randn(v.shape, generator=gen)) if k in names else v) for k, v in sd.items()}
     ps = {k: v.clone().to(dtype).requires_grad_(k in names) for k, v in sd.items()}
     ref = (O.KANFETRef.from_state_dict(ps, 2) if kind == "kanfet"
            else O.KANRef([O.KANLinearParams.from_state_dict(ps, f"layers.{l}.") for l in range(2)]))
@@ -98,11 +104,18 @@ def _vs_oracle(kind, dev, B, t, rtol, atol, gtol, options=None, ltol=1e-5):
         assert nh == n1
         host = {n: _rel(gh[n], g1[n]) for n in g1}
         host["y0"] = _rel(y0gh, y0g1)
-        _, g32, y0g32, n32 = _oracle(kind, B, t, rtol, atol, options=options, dtype=torch.float32)
-        ref32 = {n: _rel(g32[n], g1[n]) for n in g1}
-        ref32["y0"] = _rel(y0g32, y0g1)
-        k = 2 if kind == "kan" else 4
-        bad = {n: (e, host[n], ref32[n]) for n, e in worst.items() if e > max(gtol, 2 * host[n], k * ref32[n])}
+        # the reference's own fp32 error — KAN-FET: the worst of it and of three equally valid fp32
+        # re-roundings of the parameters (the gradient through the hysteresis-coupled step control
+        # is ill-conditioned, so one fp32 rounding is one draw of that error)
+        ref32 = {}
+        for pert in ([None] if kind == "kan" else [None, 1, 2, 3]):
+            _, g32, y0g32, n32 = _oracle(kind, B, t, rtol, atol, options=options, dtype=torch.float32, perturb=pert)
+            if n32 != n1:
+                continue   # a re-rounding that takes other attempts is no yardstick for this path
+            for n in g1:
+                ref32[n] = max(ref32.get(n, 0.0), _rel(g32[n], g1[n]))
+            ref32["y0"] = max(ref32.get("y0", 0.0), _rel(y0g32, y0g1))
+        bad = {n: (e, host[n], ref32[n]) for n, e in worst.items() if e > max(gtol, 2 * host[n], 2 * ref32[n])}
         print(f"{kind} B={B}: worst {max(worst.values()):.2e}, host {max(host.values()):.2e}, "
               f"oracle fp32 {max(ref32.values()):.2e}")
         assert not bad, f"(resident, host, oracle fp32) errors vs the fp64 oracle beyond the bar: {bad}"
@@ -125,8 +138,9 @@ def test_dopri5_train_kan_first_step_vs_oracle_fp64(dev):
 @pytest.mark.parametrize("B,rtol,T", [(1, 1e-1, 0.5), (64, 1e-2, 0.1)])
 def test_dopri5_train_kanfet_vs_oracle_fp64(dev, B, rtol, T):
     """KAN-FET where the attempt sequences coincide: 1e-4 per tensor, or 2x the host path's error, or
-    4x the reference's own fp32 autograd error (ill-conditioned, module docstring) — the fixed 2e-2
-    bar of rounds 3-5 is gone."""
+    2x the worst fp32 error of the reference itself over its own rounding and three equally valid
+    re-roundings of the parameters (ill-conditioned, module docstring) — the fixed 2e-2 bar of rounds
+    3-5 is gone."""
     t = torch.tensor(np.linspace(0, T, 3))
     _vs_oracle("kanfet", dev, B, t, rtol, rtol * 0.1, 1e-4, ltol=1e-3)
 

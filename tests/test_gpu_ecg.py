@@ -104,7 +104,13 @@ def test_node_dopri5_vs_reference(dev, name):
 
 def test_node_dopri5_batch200_vs_oracle(dev):
     """BASELINE configs[2] shape: batch 200 (ECG200 train + test rows), latent 64, rtol 1e-3 /
-    atol 1e-4, against the CPU oracle run here on the same seeded weights and series."""
+    atol 1e-4, against the CPU oracle run here on the same seeded weights and series, in fp32 and
+    fp64.  Bar (round 6): the reference-fp32 envelope of the ETT tests,
+    |gpu - fp64| <= 4 |ref fp32 - fp64| + 1e-5 x scale over every logit — no row allowance.
+    (The branch gate is a hard switch on x - prev_x decided close to fp32 resolution on this
+    workload: the fp64 oracle's smallest gate margin is 9.1e-8, row 129, evaluation 24.  The resident
+    solve the default path takes stays within 2.5e-7 of fp64 on every row; the host-driven loop of
+    per-module kernels flips a basis on ~4 rows)"""
     from fet_ode_amd import ecg
     from oracle import ecg_ref as E
     torch.manual_seed(0)
@@ -113,22 +119,20 @@ def test_node_dopri5_batch200_vs_oracle(dev):
     m = m.to(dev).eval()
     x = E.ecg_x(200, seed=1)
     ref = E.ECGNodeRef(sd, rtol=1e-3, atol=1e-4)
+    ref64 = E.ECGNodeRef({k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()},
+                         rtol=1e-3, atol=1e-4)
     with torch.no_grad():
         lo = m(x.to(dev))
         le = ref(x)
+        l64 = ref64(x.double())
     s = m.last_solve
     assert s.nfev == ref.trace.nfev and len(s.attempts) == len(ref.trace.attempts)
-    # The branch gate is a hard switch on x - prev_x, and on this workload it is decided below fp32
-    # resolution: the fp64 oracle's smallest gate margin is 9.1e-8 (row 129, evaluation 24), and
-    # the shadow row 199 (whose input is every row's prev_x) comes within 1e-5, so where a flip
-    # happens depends on each implementation's rounding order.  Rows: 1e-5 relative for at least
-    # 98 %, 1e-3 relative for all (a flipped basis moves a logit by ~1e-4 relative here).
+    assert ref64.trace.nfev == ref.trace.nfev
     lo, le = lo.cpu().double(), le.double()
-    scale = le.abs().max().item()
-    dev_rows = (lo - le).abs().max(dim=1).values / scale
-    off = (dev_rows > 1e-5).nonzero().flatten().tolist()
-    assert len(off) <= 200 // 50, f"logits B=200: {len(off)} rows beyond 1e-5: {off}"
-    assert dev_rows.max().item() <= 1e-3, f"logits B=200: max rel {dev_rows.max().item():.3e}"
+    scale = l64.abs().max().item()
+    err, spread = (lo - l64).abs().max().item(), (le - l64).abs().max().item()
+    assert err <= 4 * spread + 1e-5 * scale, \
+        f"logits B=200: |gpu-fp64| {err:.3e}, ref fp32 spread {spread:.3e}, scale {scale:.3e}"
 
 
 def test_training_through_fixed_grid(dev):

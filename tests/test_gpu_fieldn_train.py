@@ -176,9 +176,10 @@ def test_fieldn_training_large_batch_matches_per_stage(dev):
 # parameter VJPs — against the fp64 oracle's autograd (torchdiffeq detaches nothing: d loss / d dt
 # through the error ratio and the initial step is part of the gradient) and against autograd
 # through the host-driven solver (dopri5.py _Dopri5Grad).  Bars (round 6): per tensor (relative
-# norm) 1e-4, or 2x what the host path misses, or k x what the reference's own fp32 autograd misses
-# (k = 2 KAN, 4 KAN-FET: the hysteresis makes dopri5 gradients ill-conditioned, §4.10); the dt
-# sequence within 4x the fp32 oracle's own dt spread (KAN 1e-5).
+# norm) 1e-4, or 2x what the host path misses, or 2x what the reference's own fp32 autograd misses
+# (KAN-FET: the worst over its rounding and three equally valid re-roundings of the parameters — the
+# hysteresis makes dopri5 gradients ill-conditioned, §4.10); the dt sequence within 4x the fp32
+# oracle's own dt spread (KAN 1e-5).
 # ---------------------------------------------------------------------------------------------
 
 def _d5_run(kind, widths, K, sd, y0, t, w, dev, resident, rtol=1e-3, atol=1e-4):
@@ -201,8 +202,13 @@ def _d5_run(kind, widths, K, sd, y0, t, w, dev, resident, rtol=1e-3, atol=1e-4):
     return loss.item(), g, [(float(a[1]), bool(a[3])) for a in s.attempts], s.nfev
 
 
-def _d5_oracle(kind, sd, y0, t, w, rtol=1e-3, atol=1e-4, dtype=torch.float64):
+def _d5_oracle(kind, sd, y0, t, w, rtol=1e-3, atol=1e-4, dtype=torch.float64, perturb=None):
+    """perturb=j: parameters scaled by (1 + 6e-8 N(0, 1)) (seed j), an equally valid fp32 rounding."""
     from oracle import torch_ref as O
+    if perturb is not None:
+        gen = torch.Generator().manual_seed(perturb)
+        sd = {k: (v * (1 + 6e-8 * torch.randn(v.shape, generator=gen)) if k.split(".")[-1] not in SKIP
+                  and v.is_floating_point() else v) for k, v in sd.items()}
     ps = {k: v.detach().cpu().to(dtype).clone().requires_grad_(k.split(".")[-1] not in SKIP) for k, v in sd.items()}
     ref = _oracle(kind, ps)
     yc = y0.clone().to(dtype).requires_grad_(True)
@@ -256,8 +262,12 @@ def test_fieldn_dopri5_training_vs_oracle_and_host(dev, kind, widths, K, B):
     err = {n: _nrel(g0[n], go[n]) for n in go}
     host = {n: _nrel(g1[n], go[n]) for n in go}
     ref32 = {n: _nrel(g32[n], go[n]) for n in go}
-    k = 2 if kind == "kan" else 4
-    bad = {n: (e, host[n], ref32[n]) for n, e in err.items() if e > max(1e-4, 2 * host[n], k * ref32[n])}
+    if kind != "kan":   # KAN-FET: the worst over three re-roundings too (one fp32 rounding = one draw)
+        for pert in (1, 2, 3):
+            _, gp, npf, _ = _d5_oracle(kind, sd, y0, t, w, dtype=torch.float32, perturb=pert)
+            if npf == no:
+                ref32 = {n: max(ref32[n], _nrel(gp[n], go[n])) for n in go}
+    bad = {n: (e, host[n], ref32[n]) for n, e in err.items() if e > max(1e-4, 2 * host[n], 2 * ref32[n])}
     assert not bad, f"gradients beyond the fp32 yardstick (resident, host, oracle fp32 vs fp64): {bad}"
     print(f"{kind}{widths} B={B}: dt {dt_err:.2e} (spread {spread:.2e}); grad max rel "
           f"{max(err.values()):.2e} (oracle fp32 {max(ref32.values()):.2e})")

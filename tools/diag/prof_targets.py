@@ -38,7 +38,7 @@ if which in ("all", "small"):   # the strong-scaling shard (v6, B = 512) next to
     m = F.KANFET([2, 10, 2], grid_size=5).to(dev)
     t = torch.tensor(np.linspace(0, 3.5, 35))
     with torch.no_grad():
-        for B in (512, 4096):
+        for B in (512, 1024, 4096):
             y0 = bench.lv_y0(B, 0).to(dev)
             for _ in range(4):
                 F.odeint(F.autonomous(m), y0, t, method="rk4")

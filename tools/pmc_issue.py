@@ -17,6 +17,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: dense fp32 (MFMA = vector
 MFMA_FLOPS = 2 * 16 * 16 * 4    # v_mfma_f32_16x16x4_f32
 KEYS = ["fused4_kernel<10, 10, 10, 12, true, true, false, false, 2>", "fused4_kernel<10, 10, 10, 12, true, true, false, false, 1>",
         "fused4_kernel<10, 10, 10, 12, true, true, false, false>", "small6_kernel<true, true, false, false>",
+        "v8_kernel<true, 2>",
         "fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 2>", "fixed_bwd_kernel<2, 10, 10, 10, 12, true, true, 1>",
         "sweep7_kernel<true>", "sweep7_kernel<false>", "kansum_kernel",
         "wide_layer_kernel<10, true, true, 8>", "wide_fwd4_kernel", "wide_fwd_kernel", "kuramoto_fwd_kernel",
