@@ -43,6 +43,15 @@ PARAM_FLOATS = 3052 + 144      # trainable params + grid buffers of KANFET [2,10
 STATE_IN = 2 + 10              # sum of Ferro in_l
 
 
+_T_START = time.perf_counter()
+
+
+def progress(msg):
+    """One line per bench leg on stderr (the JSON line stays the only stdout line): a long leg is
+    visibly alive (the GPU harness kills a command that writes nothing for minutes)."""
+    print(f"[bench +{time.perf_counter() - _T_START:6.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
 def alg_bytes_per_step(b):
     """y read+write (16 B) + compact prev_x r/w per Ferro layer (8*sum in_l) per
     trajectory, + parameters once:  112*B + 12784."""
@@ -72,6 +81,8 @@ def parse():
     ap.add_argument("--no-mnist", action="store_true", help="skip the MNIST Kuramoto + KANLinear line")
     ap.add_argument("--no-ett", action="store_true", help="skip the ETT KAN-FET latent-ODE forecaster line")
     ap.add_argument("--ett-batch", type=int, default=8192)
+    ap.add_argument("--ett-ref-iters", type=int, default=1,
+                    help="iterations of the reference's own ETT training step (rtol 1e-7, ~1 min each); 0 skips")
     ap.add_argument("--cpu-solves", type=int, default=5, help="CPU baseline: median over this many solves")
     ap.add_argument("--train-iters", type=int, default=50, help="0 skips the training-rate line")
     return ap.parse_args()
@@ -1063,6 +1074,7 @@ def main():
     def solve():
         return F.odeint(func, y0d, t, method="rk4")
 
+    progress(f"headline: rk4 B={Bl} x {args.steps} solves (warm-up {args.warmup})")
     with torch.no_grad():
         # clock settle: the GPU raises its clocks over the first ~100 back-to-back solves (~20 ms:
         # 181 -> 170 us per solve, profiles/r05_clock_ramp.log); a fixed wall time of untimed solves
@@ -1092,6 +1104,7 @@ def main():
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
             el = tt.item()
         k_ms = kernel_time_ms(model, y0d, t)
+    progress("train")
     train = train_rate(model, y0d, t, args.train_iters, 5, world, strong) if args.train_iters > 0 else None
     other_line = None
     if world > 1:
@@ -1194,10 +1207,13 @@ def main():
         if train is not None:
             out["train"] = train
         if world == 1:
+            progress("plain closure")
             out["lv_plain_closure"] = plain_closure_rate(model, y0d, t)
         if world == 1 and not args.no_dopri5:
+            progress("lv dopri5")
             out["lv_dopri5"] = lv_dopri5_rate(sd, y0d, t)
             out["lv_dopri5"]["rtol_1e-3"] = lv_dopri5_rate(sd, y0d, t, reps=5, rtol=1e-3, atol=1e-4)
+            progress("lv dopri5 training")
             tr = lv_dopri5_train_rate(sd, y0d, t)
             tr["host_autograd"] = lv_dopri5_train_rate(sd, y0d, t, iters=1, resident=False)
             tr["speedup_vs_host_autograd"] = tr["value"] / tr["host_autograd"]["value"]
@@ -1211,17 +1227,27 @@ def main():
         if dp5_sharded is not None:
             out["lv_dopri5"] = dp5_sharded
         if world == 1 and not args.no_ecg:
+            progress("ecg")
             out["ecg"] = ecg_rate(dev, with_cpu=not args.no_cpu_baseline)
             out["ecg"]["rtol_1e-2"] = ecg_rate(dev, with_cpu=False, rtol=1e-2, atol=1e-3)
         if world == 1 and not args.no_mnist:
+            progress("mnist")
             out["mnist"] = mnist_rate(dev, with_cpu=not args.no_cpu_baseline)
         if world == 1 and not args.no_ett:
+            progress("ett rk4 forecaster")
             out["ett"] = ett_rate(dev, batch=args.ett_batch, with_cpu=not args.no_cpu_baseline)
+            progress("ett encoder")
             out["ett"]["encoder"] = ett_encoder_rate(dev, with_cpu=not args.no_cpu_baseline)
+            progress("ett dopri5")
             out["ett"]["dopri5"] = ett_dopri5_rate(dev, batch=args.ett_batch)
+            progress("ett dopri5 training")
             out["ett"]["dopri5"]["train"] = ett_dopri5_train_rate(dev)
-            out["ett"]["dopri5"]["train"]["reference_iteration"] = ett_reference_iteration_rate(dev)
+            if args.ett_ref_iters > 0:
+                progress("ett reference iteration (dopri5 rtol 1e-7, ~1 min)")
+                out["ett"]["dopri5"]["train"]["reference_iteration"] = ett_reference_iteration_rate(
+                    dev, iters=args.ett_ref_iters)
         if world == 1 and not args.no_cpu_baseline:
+            progress("cpu baseline + parity")
             cb, ref_sol = cpu_baseline(sd, y0, t, args.cpu_solves)
             out["cpu_baseline"] = cb
             if "lv_dopri5" in out:

@@ -298,13 +298,19 @@ struct FerroSplit {
 // layer's (knot, 1/width) table by (input, interval): u = (x - knot) / width is formed here, from
 // the interval index the feature phase wrote; the zero row NI holds (0, 0): u = 0 for finite x and
 // NaN otherwise, as the reference's bases)
+// (round 6) x_si's knot interval comes from the feature phase's wave ballot `bal` (the trajectory's
+// 16-bit row of input si starts at bit `bbase` + 16 si): every lane forms it in registers, so the
+// spline table reads issue straight after the exchange instead of behind an LDS read of the interval.
+// A non-finite x counts 0 or all knots (lanes >= NG hold +inf): the zero row, whose (x - 0) * 0 is the
+// reference's NaN — no separate finiteness test.
 template <int IN, int FLEN, int NI, int NPL, int NSL, int FPL, bool FERRO, bool FACT>
 __device__ __forceinline__ float v4_edges(const V4Lds<IN, FLEN>& L, const float* sp_o, const f2* kr,
                                           const int* gi, const f2* ep, const f2* k2, const f2* kE, const f2* cp,
                                           const f2* fw, int fofs, bool spl, int si, float gsl2e, int gis, float eps,
-                                          float k2s, float kEs, float cps) {
-  // spline operands first (dependent LDS reads), so their latency hides under the pairs
-  const int msi = L.M[si];
+                                          float k2s, float kEs, float cps, uint64_t bal, int bbase) {
+  // spline operands first (table reads by interval), so their latency hides under the pairs
+  const int mraw = (int)__builtin_popcountll((bal >> (bbase + 16 * si)) & 0xFFFFull) - 1;
+  const int msi = (unsigned)mraw < (unsigned)NI ? mraw : NI;
   const float xsi = L.G[si].z;
   const float4 cf = *reinterpret_cast<const float4*>(&sp_o[(si * (NI + 1) + msi) * 4]);
   const f2 kw = kr[si * (NI + 1) + msi];
@@ -553,12 +559,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
       xdst = &L0.G[row].x;
     } else if (j == J_X) {
       xdst = &L0.G[row].z;
-    } else if (j == J_M) {
-      xdst = reinterpret_cast<float*>(&L0.M[row]);
     }
   }
   const bool x_silu = c1 == J_SILU, x_gate = FERRO && c1 == J_GATE, x_exp = FERRO && c1 == J_EXP;
-  const bool x_x = c1 == J_X, x_m = c1 == J_M;
+  const bool x_x = c1 == J_X;
   // knot interval: lane c1 holds knot c1 (and 1/(knot c1+1 - knot c1)); the lane whose knot
   // opens the interval writes u (no LDS round trip on the critical path)
   const float xknot = c1 < NG ? a.plan[a.P0.knots + row * NG + c1] : __builtin_inff();
@@ -604,6 +608,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   constexpr int TW = DOPRI ? 2 * D + H : D + H;
   float* tape_b = taping ? a.tape + (valid ? b : 0) * TW : nullptr;
   const int64_t tape_stride = a.B * TW;
+  uint64_t bal0 = 0;   // the feature phase's knot ballot (both trajectories' rows of both inputs)
   auto eval_body = [&](float xin, auto fact_tag) __attribute__((always_inline)) -> float {
     constexpr bool F_ = decltype(fact_tag)::value;
     STAMP(6);
@@ -617,25 +622,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
       float val = ffma(sg, x_silu ? xin : xmul, xadd);
       val = x_exp ? e : val;
       val = x_x ? xin : val;
-      // knot interval: lanes c1 < NG compare against their knot (the rest hold +inf), the row's
-      // count from the wave ballot
-      const int cnt = (int)__builtin_popcountll((__builtin_amdgcn_ballot_w64(xin >= xknot) >> (tid & 48)) & 0xFFFFull);
-      const int mm = cnt - 1;
-      const bool fin = __builtin_isfinite(xin);
-      const int mfix = ((unsigned)mm < (unsigned)NI && fin) ? mm : NI;
-      val = x_m ? __builtin_bit_cast(float, mfix) : val;
+      // knot intervals: lanes c1 < NG compare against their knot (the rest hold +inf); the edge
+      // lanes count their input's row of this ballot themselves (v4_edges)
+      bal0 = __builtin_amdgcn_ballot_w64(xin >= xknot);
       *xdst = val;
       if (FERRO) prev0 = xin;  // ferro_class.py:409 (meaningful on the gate lane)
       re0 = false;
     }
     STAMP(0);
-    __syncthreads();
+    // the workgroup is this one wave: its LDS operations execute in order, so the edge reads see the
+    // feature writes with no wait on them (a wave barrier only keeps the compiler from reordering)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     STAMP(0);
     FETODE_MARK("EDGES0");
     // (2) layer-0 edges -> h_o on the group of 3
     float h = v4_edges<D, FLEN0, NI, NPL0, NSL0, FPL0, FERRO, F_>(L0, sp0_o, s_kr0, gi0, ep0, k20, kE0, cp0, fw0,
                                                                   fofs0, spl0, si0, a.P0.gsl2e, gs0, es0, k2s0, kEs0,
-                                                                  cps0);
+                                                                  cps0, bal0, TPW == 2 ? 32 * g : 0);
     if constexpr (TPW == 1) {   // the two halves' partial edge sums (the same sum on both halves)
       float p = h, q2 = h;
       permlane32_swap(p, q2);
@@ -648,9 +653,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
     f2 acc01 = splat(0.0f);
     {
       // knot interval of h: KT compares per lane, summed over the group
+      // (a non-finite h counts 0 or all 12 knots: the zero row, no finiteness test needed)
       const int mm = group3_sum_i(knot_count<KT>(h, hknot), cc0) - 1;
-      const bool fin = __builtin_isfinite(h);
-      const int mfix = ((unsigned)mm < (unsigned)NI && fin) ? mm : NI;
+      const int mfix = (unsigned)mm < (unsigned)NI ? mm : NI;
       // spline operands by interval (the zero row NI holds (0, 0): u = 0 for finite h, NaN
       // otherwise, as the reference's bases); their LDS latency hides under the pairs
       const float4 cf = *reinterpret_cast<const float4*>(&sp1_e[mfix * 4]);
