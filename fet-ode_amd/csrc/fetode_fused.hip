@@ -53,6 +53,22 @@ __device__ __forceinline__ unsigned long long stamp_now() {
 #define STAMP_FLUSH()
 #endif
 
+// Wave priority around an evaluation's serial phases (round 6).  At two trajectories per wave two
+// waves share each SIMD and run the same instruction stream; the SIMD arbitrates their VALU issue by
+// priority, then age.  The wave in a serial phase (the DPP / permlane reductions, the stage combine,
+// the feature exchange) raises its priority so it gets through the dependent chain, and drops it for
+// the Ferro pair rounds, whose independent instructions then fill the other wave's latency.
+// Measured B = 4096: 159.9 -> 152.6 us per solve (tools/diag/fwd_ab.py, profiles/r06_prio_ab.log);
+// at one wave per SIMD (TPW = 1, v8) there is no partner to yield to and it costs 2 %: TPW = 2 only.
+#define PRIO_HI() \
+  do {            \
+    if constexpr (TPW == 2) __builtin_amdgcn_s_setprio(1); \
+  } while (0)
+#define PRIO_LO() \
+  do {            \
+    if constexpr (TPW == 2) __builtin_amdgcn_s_setprio(0); \
+  } while (0)
+
 #ifdef FETODE_ISA_MARKERS
 #define FETODE_MARK(s) asm volatile("; MARK " s ::: "memory")
 #else
@@ -637,6 +653,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     STAMP(0);
     FETODE_MARK("EDGES0");
+    PRIO_LO();
     // (2) layer-0 edges -> h_o on the group of 3
     float h = v4_edges<D, FLEN0, NI, NPL0, NSL0, FPL0, FERRO, F_>(L0, sp0_o, s_kr0, gi0, ep0, k20, kE0, cp0, fw0,
                                                                   fofs0, spl0, si0, a.P0.gsl2e, gs0, es0, k2s0, kEs0,
@@ -646,6 +663,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
       permlane32_swap(p, q2);
       h = p + q2;
     }
+    PRIO_HI();
     h = group3_sum(h, cc0) + c0o;   // lane 15 of a row (no group) is never read by a group
     STAMP(2);
     FETODE_MARK("H_FEAT");
@@ -671,6 +689,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
         prev1 = h;   // ferro_class.py:409
         re1 = false;
         const f2 ew = f2{e, w}, xp = f2{h, 0.0f};
+        PRIO_LO();
         if constexpr (NSL1 > 0) sgl = v4_single<F_>(ew, xp, es1, k2s1, kEs1, cps1, 0.0f, a.P1.gsl2e);
 #pragma unroll
         for (int r = 0; r < NPL1; ++r) acc01 = v4_pair<F_>(ew, xp, ep1[r], k21[r], kE1[r], cp1[r], acc01, a.P1.gsl2e);
@@ -695,6 +714,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
     STAMP(3);
     // output sums over the half-wave: the permlane16 swap folds the two rows of each output into
     // row d (rows 0 / 2: output 0, rows 1 / 3: output 1), a row sum finishes: k_row on row `row`
+    PRIO_HI();
     float p0 = acc01.x, p1 = acc01.y;
     if constexpr (TPW == 1) {   // the two halves' partials first (the same sums on both halves)
       float p = p0, q2 = p0;
