@@ -26,6 +26,17 @@
 #define S7_SKIP 0   // diagnostic: bit 1 layer-1 logistic sums, 2 layer-1 spline, 4 layer-0 lw, 8 layer-0 a/b, 16 layer-0 spline/base
 #endif
 
+#ifndef S7_PRIO
+#define S7_PRIO 0   // wave priority over the serial phases (fetode_fused.hip PRIO_HI / PRIO_LO): A/B knob
+#endif
+#if S7_PRIO
+#define S7_HI() __builtin_amdgcn_s_setprio(1)
+#define S7_LO() __builtin_amdgcn_s_setprio(0)
+#else
+#define S7_HI()
+#define S7_LO()
+#endif
+
 namespace s7 {
 constexpr int D = 2, H = 10, K = 10, NB = 10, NG = 12, NI = NG - 1, NS = NG - 1 - kSO, NFL = 1 + NB, KP = K / 2;
 constexpr int W = D + H;
@@ -401,6 +412,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
               nan1 |= fin ? 0 : 1;
             }
             // Ferro elements (o, d, k): pairs over both outputs, then the single (o, cc0, K - 1)
+            S7_LO();
 #pragma unroll
             for (int r = 0; r < NPL1; ++r)
               dh += pair_vjp<F_>(T.fa1[p1[r]], T.fb1[p1[r]], T.ee1[p1[r]], g01, h, up, wo, E, gl1, A1[r], C1[r], E1[r]);
@@ -413,6 +425,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
             }
           }
           if (KS) G1 += g01;
+          S7_HI();
           const float g0o = act ? g3f(dh, cc0) : 0.f;   // d loss / d h_o on the group (lane 15: none)
           if (act && cc0 == 0) V.g0[hh][o] = g0o;
           if (!KS && live) {   // this evaluation's adjoints for kansum_kernel
@@ -424,6 +437,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
           f2 dx01 = splat(0.f);
           {
             const f2 g2 = splat(g0o);
+            S7_LO();
 #pragma unroll
             for (int r = 0; r < NPL0; ++r) {
               const bool i1 = p0[r] >= H * KP;   // the pair's input
@@ -481,6 +495,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
             dx01 = pfma(mrow, splat(Tt * pa0), dx01);
           }
           // ---- (5) d loss / d x: rows fold, row sum -> dx of state dim `row` on row `row` ----
+          S7_HI();
           float r0 = dx01.x, r1 = dx01.y;
           pl16(r0, r1);
           const float dx = rs16(r0 + r1);
