@@ -1356,6 +1356,23 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
   const f2 third = splat(1.0f / 3.0f);
   if constexpr (HOT) {
     int sb = 0, jb = 1, jj = 1;
+    // the step's outputs from the schedule entries read at its start (os1: a second output inside
+    // the same step, step_size grids: the rest from LDS)
+    auto out_step = [&](int s, int os0, int os1, int om0, float osl0, f2 y, f2 y1) __attribute__((always_inline)) {
+      if (os0 != s) return;
+      out_write(jj, interp(om0, y, y1, osl0));
+      ++jj;
+      if (os1 != s) return;
+      while (jj < a.T) {
+        if (jj - jb == SCH) {
+          jb = jj;
+          load_outs(jj);
+        }
+        if (s_ostep[jj - jb] != s) break;
+        out_write(jj, interp(s_omode[jj - jb], y, y1, s_oslope[jj - jb]));
+        ++jj;
+      }
+    };
     load_steps(0);
     load_outs(1);
     auto run = [&](auto fact_tag) __attribute__((always_inline)) {
@@ -1369,6 +1386,11 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
           load_outs(jj);
         }
         const f2 dt = splat(s_dt[s - sb]);
+        // this step's output schedule read up front (as small6): its LDS round trips overlap the
+        // four evaluations instead of following them on the wave's chain
+        const int jr = jj - jb;
+        const int os0 = s_ostep[jr], os1 = s_ostep[jr + 1], om0 = s_omode[jr];
+        const float osl0 = s_oslope[jr];
         tape_at(4 * s, y);
         const f2 k1 = eval_body(y, fact_tag);
         const f2 x2 = y + (dt * k1) * third;
@@ -1381,15 +1403,7 @@ __global__ __launch_bounds__(192) void small6_kernel(FusedArgs a) {
         tape_at(4 * s + 3, x4);
         const f2 k4 = eval_body(x4, fact_tag);
         const f2 y1 = y + (((k1 + splat(3.0f) * (k2 + k3)) + k4) * dt) * splat(0.125f);
-        while (jj < a.T) {
-          if (jj - jb == SCH) {
-            jb = jj;
-            load_outs(jj);
-          }
-          if (s_ostep[jj - jb] != s) break;
-          out_write(jj, interp(s_omode[jj - jb], y, y1, s_oslope[jj - jb]));
-          ++jj;
-        }
+        out_step(s, os0, os1, om0, osl0, y, y1);
         y = y1;
         STAMP(7);
       }
@@ -1900,19 +1914,29 @@ __global__ __launch_bounds__(128 * TPB) void v8_kernel(FusedArgs a) {
         load_outs(jj);
       }
       const f2 dt = splat(s_dt[s - sb]);
+      // the step's output schedule read up front (as small6 / fused4): off the evaluation chain
+      const int jr = jj - jb;
+      const int os0 = s_ostep[jr], os1 = s_ostep[jr + 1], om0 = s_omode[jr];
+      const float osl0 = s_oslope[jr];
       const f2 k1 = eval_body(y, fact_tag);
       const f2 k2 = eval_body(y + (dt * k1) * third, fact_tag);
       const f2 k3 = eval_body(y + dt * (k2 - k1 * third), fact_tag);
       const f2 k4 = eval_body(y + dt * ((k1 - k2) + k3), fact_tag);
       const f2 y1 = y + (((k1 + splat(3.0f) * (k2 + k3)) + k4) * dt) * splat(0.125f);
-      while (jj < a.T) {
-        if (jj - jb == SCH) {
-          jb = jj;
-          load_outs(jj);
-        }
-        if (s_ostep[jj - jb] != s) break;
-        out_write(jj, interp(s_omode[jj - jb], y, y1, s_oslope[jj - jb]));
+      if (os0 == s) {
+        out_write(jj, interp(om0, y, y1, osl0));
         ++jj;
+        if (os1 == s) {  // several outputs inside one step (step_size grids)
+          while (jj < a.T) {
+            if (jj - jb == SCH) {
+              jb = jj;
+              load_outs(jj);
+            }
+            if (s_ostep[jj - jb] != s) break;
+            out_write(jj, interp(s_omode[jj - jb], y, y1, s_oslope[jj - jb]));
+            ++jj;
+          }
+        }
       }
       y = y1;
       STAMP(7);

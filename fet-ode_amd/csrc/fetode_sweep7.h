@@ -27,7 +27,9 @@
 #endif
 
 #ifndef S7_PRIO
-#define S7_PRIO 0   // wave priority over the serial phases (fetode_fused.hip PRIO_HI / PRIO_LO): A/B knob
+// wave priority over the serial phases (as fetode_fused.hip PRIO_HI / PRIO_LO): the sweep runs two
+// waves per SIMD; measured 0.558 -> 0.546 ms per B = 4096 backward (profiles/r06_s7prio_ab.log)
+#define S7_PRIO 1
 #endif
 #if S7_PRIO
 #define S7_HI() __builtin_amdgcn_s_setprio(1)

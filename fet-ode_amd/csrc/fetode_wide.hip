@@ -38,6 +38,9 @@ namespace {
 #include "fetode_xrank.h"
 
 constexpr float kWideFactorLimit = 60.0f;  // |gs Ec| bound of the factored gate (header comment)
+#ifndef WIDE_FOLD
+#define WIDE_FOLD 0   // 1: the folded tanh (rounds 3-5; diagnostics / A-B)
+#endif
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f2 __attribute__((ext_vector_type(2)));
@@ -57,10 +60,10 @@ constexpr int pitch_of(int ch) { return ((ch * kWF + 29) / 32) * 32 + 2; }
 struct WideLayout {
   int in, out, K;
   bool kan, ferro;
-  int64_t fe4;     // (out, in, K) float4 {P = 2^{gs log2e Ec}, 2 log2e k, 2 log2e k Ec, -2 coef Ps}
+  int64_t fe4;     // (out, in, K) float4 {P = 2^{gs log2e Ec}, 2 log2e k, 2 log2e k Ec, coef Ps}
   int64_t gec;     // (out, in, K) gs log2e Ec (direct form)
   int64_t dflag;   // (out, in) 1 if some |gs Ec| > kWideFactorLimit for (o, i)
-  int64_t fconst;  // (out) sum_{i,k} coef (bias + Ps): coef Ps tanh = coef Ps - 2 coef Ps / (1 + e^{2z})
+  int64_t fconst;  // (out) sum_{i,k} coef bias (WIDE_FOLD: + coef Ps, the folded tanh's constant part)
   int64_t wp;      // (in, 20, out) packed KAN weights
   int64_t lg;      // (in, NB, 2) (-a log2e, a b log2e)
   int64_t knots;   // (in, 12) knot grid (efficientkan.py:55-61 buffer)
@@ -152,7 +155,11 @@ __global__ void wide_pack_kernel(fetode_kanlinear_t kl, fetode_ferro_t fl, WideL
     d[0] = ex2(gec);
     d[1] = k2;
     d[2] = k2 * Ec;
+#if WIDE_FOLD
     d[3] = -2.0f * (co * Ps);
+#else
+    d[3] = co * Ps;
+#endif
     plan[L.gec + t] = gec;
   }
   if (L.ferro && t < (int64_t)out * in) {
@@ -244,7 +251,11 @@ __global__ void wide_const_kernel(fetode_ferro_t fl, WideLayout L, float* __rest
     for (int p = lane; p < L.in * L.K; p += 64) {
       const int i = p / L.K, k = p % L.K;
       const int src = (i * L.out + o) * L.K + k;
+#if WIDE_FOLD
       s += fl.coef[src] * fl.bias[src] + fl.coef[src] * fl.Ps[src];
+#else
+      s += fl.coef[src] * fl.bias[src];
+#endif
     }
   for (int m = 32; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
   if (lane == 0) plan[L.fconst + o] = s;
@@ -514,8 +525,16 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
               const f2 sg = rcpx2(pfma(splat(e), f2{p0.x, p1.x}, splat(1.0f)));
               const f2 mm = pfma(splat(wg), sg, splat(1.0f));
               const f2 z = pfma(f2{p0.z, p1.z}, mm, f2{p0.y, p1.y} * splat(xv));
+#if WIDE_FOLD
               // coef Ps tanh z = coef Ps - 2 coef Ps / (1 + 2^z): the constant part lives in fconst
               acc2 = pfma(f2{p0.w, p1.w}, rcpx2(ex2x2(z) + splat(1.0f)), acc2);
+#else
+              // coef Ps tanh z, tanh z = 1 - 2 / (1 + 2^z): the terms keep the size of the
+              // reference's (round 6: the fold above summed terms of size coef Ps whatever tanh was,
+              // and over the 380 stateful steps of the ETT forecast its cancellation cost ~4x the
+              // reference's own fp32 error)
+              acc2 = pfma(f2{p0.w, p1.w}, pfma(rcpx2(ex2x2(z) + splat(1.0f)), splat(-2.0f), splat(1.0f)), acc2);
+#endif
             }
             acc = acc2.x + acc2.y;
           } else {
@@ -526,7 +545,11 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
               const float sg = rcp(1.0f + ex2(ffma(gsl2e, xv, gec[k])));
               const float mm = ffma(wg, sg, 1.0f);
               const float z = ffma(p.z, mm, p.y * xv);
+#if WIDE_FOLD
               acc = ffma(p.w, rcp(ex2(z) + 1.0f), acc);
+#else
+              acc = ffma(p.w, ffma(rcp(ex2(z) + 1.0f), -2.0f, 1.0f), acc);
+#endif
             }
           }
           facc[j] += acc;  // K bases of one input first, then inputs (the reference's two-level sum)
