@@ -629,7 +629,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
     constexpr bool F_ = decltype(fact_tag)::value;
     STAMP(6);
     FETODE_MARK("X_FEAT");
+#ifndef FETODE_EXPERIMENT_NO_TAPE_STORE
     if (taping && valid && own && c1 == 0) tape_b[row] = xin;
+#endif
     {
       // (1) layer-0 features of input `row`: one sigmoid-of-affine job per lane
       const float pv = x_gate ? (re0 ? xin : prev0) : 0.f;
@@ -705,7 +707,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
       const float u = (h - kw.x) * kw.y;
       const float sv = ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
       acc01 = pfma(dsel1, splat(sgl + sv), acc01);   // lane d < 2: single + spline onto output d
+#ifndef FETODE_EXPERIMENT_NO_TAPE_STORE
       if (taping && valid && own && act0 && cc0 == 0) tape_b[D + o0] = h;
+#endif
     }
     if (taping) {
       tape_b += tape_stride;
