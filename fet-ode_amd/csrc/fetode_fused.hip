@@ -629,9 +629,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
     constexpr bool F_ = decltype(fact_tag)::value;
     STAMP(6);
     FETODE_MARK("X_FEAT");
-#ifndef FETODE_EXPERIMENT_NO_TAPE_STORE
-    if (taping && valid && own && c1 == 0) tape_b[row] = xin;
-#endif
     {
       // (1) layer-0 features of input `row`: one sigmoid-of-affine job per lane
       const float pv = x_gate ? (re0 ? xin : prev0) : 0.f;
@@ -708,7 +705,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
       const float sv = ffma(ffma(ffma(cf.w, u, cf.z), u, cf.y), u, cf.x);
       acc01 = pfma(dsel1, splat(sgl + sv), acc01);   // lane d < 2: single + spline onto output d
 #ifndef FETODE_EXPERIMENT_NO_TAPE_STORE
-      if (taping && valid && own && act0 && cc0 == 0) tape_b[D + o0] = h;
+      // the evaluation's tape row in ONE non-temporal store: h_o from the group's first lane, x_row
+      // from the row's idle lane 15 (two plain stores cost the B = 4096 taped solve 23 us over none,
+      // this one 15: profiles/r06_tape_store_ab.log; the sweep reads the rows long after)
+      if (taping && valid && own && ((act0 && cc0 == 0) || q == 15))
+        __builtin_nontemporal_store(q == 15 ? xin : h, tape_b + (q == 15 ? row : D + o0));
 #endif
     }
     if (taping) {

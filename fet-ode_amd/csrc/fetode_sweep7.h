@@ -51,16 +51,34 @@ constexpr int AR = NS + 2 * kSO;                    // spline-sum row: kSO guard
 constexpr int S_LW0 = 0, S_LA0 = H, S_LB0 = H + 1, S_LW1 = H + 2, S_LA1 = S_LW1 + 2 * RF1, S_LB1 = S_LA1 + RF1,
               NKS = S_LB1 + RF1;
 constexpr int NSR = 2 * (H * D) + 1;                // spline rows per layer: (half, o, i) + a dummy row
+// The element constants a lane reads are tabled per ROUND and LANE ([r][lane & 31]: both halves
+// hold the same parameters): a round's reads are 32 consecutive entries, free of the bank conflicts
+// the element-indexed tables had (lanes of different units on one 16-B slot: 2-way on most reads,
+// 140 of the ~260 conflict cycles per evaluation, profiles/r06_sweep_pmc.txt), and the lanes keep
+// no element indices in VGPRs.  Round NPL is the lane's single.
 struct Tab {
-  float4 fa0[D * H * KP], fb0[D * H * KP];  // layer-0 pairs p = e / 2: (Ec, Ec', k2, k2'), (cPk, cPk', Eg2, Eg2')
-  f2 ee0[D * H * KP];                        // 2^(gs log2e Ec) (the factored coercive gate)
-  float4 fa1[H * K], fb1[H * K];             // layer-1 pairs p = o K + k: elements (o, 0, k), (o, 1, k)
-  f2 ee1[H * K];
+  float4 fa0[NPL0 + 1][32], fb0[NPL0 + 1][32];  // layer-0 pairs: (Ec, Ec', k2, k2'), (cPk, cPk', Eg2, Eg2')
+  f2 ee0[NPL0 + 1][32];                          // 2^(gs log2e Ec) (the factored coercive gate)
+  float4 fa1[NPL1 + 1][32], fb1[NPL1 + 1][32];  // layer-1 pairs: elements (o, 0, k), (o, 1, k)
+  f2 ee1[NPL1 + 1][32];
   float4 sp0[H * D * (NI + 1)], sp1[D * H * (NI + 1)];  // edge cubics by interval (plan layout)
   float kw0[H * D * NFL];                               // SiLU weight, 2 * scaled logistic weights
   float kwT[D * NB * H];                                // layer-0 logistic weights by (i, j): the ten outputs
-  float4 jf[H * 12];    // layer-1 job (o, j): (-a log2e, a b log2e, a, b); SiLU (j = NB): (-log2e, 0, 1, 0)
-  f2 jw[H * 12];        // its weights for outputs 0, 1 (SiLU: the base weights)
+  float4 jf[RF1][32];   // layer-1 job (o, j = cc0 + 3 r): (-a log2e, a b log2e, a, b); SiLU (j = NB): (-log2e, 0, 1, 0)
+  f2 jw[RF1][32];       // its weights for outputs 0, 1 (SiLU: the base weights)
+};
+// the lane map of sweep7_kernel (lane & 31): hidden unit o (idle lane 15: unit 0's constants, never
+// used) and part cc0 of its group of 3; its element pair P = cc0 NPL + r of the unit
+struct LaneMap {
+  int row, q, o, cc0;
+  __device__ explicit LaneMap(int l) : row(l >> 4), q(l & 15), o(q < 15 ? row * 5 + q / 3 : 0), cc0(q % 3) {}
+  __device__ int p0(int r) const {   // layer-0 pair (i, o, 2 kp .. 2 kp + 1) as e / 2
+    const int P = cc0 * NPL0 + r, i = P / KP, kp = P % KP;
+    return (i * H + o) * KP + kp;
+  }
+  __device__ int ps0() const { return ((D - 1) * H + o) * KP + (KP - 1); }   // layer-0 single: (1, o, 8 + cc0)
+  __device__ int p1(int r) const { return o * K + (cc0 + 3 * r); }         // layer-1 pair (o, k), both outputs
+  __device__ int ps1() const { return o * K + (K - 1); }                     // layer-1 single: (o, cc0, 9)
 };
 struct Wv {
   float4 gx[2][D];   // per half, layer-0 input i: x, up, wo, 2^(gs log2e x)
@@ -167,21 +185,26 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
   const float gl0 = a.P0.gsl2e, gl1 = a.P1.gsl2e, wc0 = a.P0.wc, wc1 = a.P1.wc;
   // ---- tables (once per workgroup) ----
   TI.stage(a.plan, a.P0, a.P1, D, tid, 64 * kTPB);
-  for (int p = tid; p < D * H * KP; p += 64 * kTPB) {   // layer 0: e = 2p, 2p + 1
-    const int e = 2 * p;
+  for (int t = tid; t < (NPL0 + 1) * 32; t += 64 * kTPB) {   // layer 0: elements e = 2p, 2p + 1
+    const int r = t / 32;
+    const LaneMap lm(t % 32);
+    const int e = 2 * (r < NPL0 ? lm.p0(r) : lm.ps0());
     const fetode_ferro_t& f = a.f0;
-    T.fa0[p] = make_float4(f.Ec[e], f.Ec[e + 1], k2c * f.k[e], k2c * f.k[e + 1]);
-    T.fb0[p] = make_float4((f.coef[e] * f.Ps[e]) * f.k[e], (f.coef[e + 1] * f.Ps[e + 1]) * f.k[e + 1], gl0 * f.Ec[e],
-                           gl0 * f.Ec[e + 1]);
-    T.ee0[p] = f2{ex2(gl0 * f.Ec[e]), ex2(gl0 * f.Ec[e + 1])};
+    T.fa0[r][t % 32] = make_float4(f.Ec[e], f.Ec[e + 1], k2c * f.k[e], k2c * f.k[e + 1]);
+    T.fb0[r][t % 32] = make_float4((f.coef[e] * f.Ps[e]) * f.k[e], (f.coef[e + 1] * f.Ps[e + 1]) * f.k[e + 1],
+                                   gl0 * f.Ec[e], gl0 * f.Ec[e + 1]);
+    T.ee0[r][t % 32] = f2{ex2(gl0 * f.Ec[e]), ex2(gl0 * f.Ec[e + 1])};
   }
-  for (int p = tid; p < H * K; p += 64 * kTPB) {   // layer 1: (o, 0, k), (o, 1, k)
+  for (int t = tid; t < (NPL1 + 1) * 32; t += 64 * kTPB) {   // layer 1: (o, 0, k), (o, 1, k)
+    const int r = t / 32;
+    const LaneMap lm(t % 32);
+    const int p = r < NPL1 ? lm.p1(r) : lm.ps1();
     const int oo = p / K, k = p % K, e0 = (oo * D + 0) * K + k, e1 = (oo * D + 1) * K + k;
     const fetode_ferro_t& f = a.f1;
-    T.fa1[p] = make_float4(f.Ec[e0], f.Ec[e1], k2c * f.k[e0], k2c * f.k[e1]);
-    T.fb1[p] = make_float4((f.coef[e0] * f.Ps[e0]) * f.k[e0], (f.coef[e1] * f.Ps[e1]) * f.k[e1], gl1 * f.Ec[e0],
-                           gl1 * f.Ec[e1]);
-    T.ee1[p] = f2{ex2(gl1 * f.Ec[e0]), ex2(gl1 * f.Ec[e1])};
+    T.fa1[r][t % 32] = make_float4(f.Ec[e0], f.Ec[e1], k2c * f.k[e0], k2c * f.k[e1]);
+    T.fb1[r][t % 32] = make_float4((f.coef[e0] * f.Ps[e0]) * f.k[e0], (f.coef[e1] * f.Ps[e1]) * f.k[e1],
+                                   gl1 * f.Ec[e0], gl1 * f.Ec[e1]);
+    T.ee1[r][t % 32] = f2{ex2(gl1 * f.Ec[e0]), ex2(gl1 * f.Ec[e1])};
   }
   {
     const float4* s0 = reinterpret_cast<const float4*>(a.plan + a.P0.sp);
@@ -195,8 +218,9 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
       const int ij = i / H, oo = i % H, ii = ij / NB, j = ij % NB;
       T.kwT[i] = a.plan[a.P0.kw + (oo * D + ii) * NFL + 1 + j];
     }
-    for (int i = tid; i < H * 12; i += 64 * kTPB) {
-      const int oo = i / 12, j = i % 12;
+    for (int t = tid; t < RF1 * 32; t += 64 * kTPB) {
+      const LaneMap lm(t % 32);
+      const int oo = lm.o, j = lm.cc0 + 3 * (t / 32);
       float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
       f2 w = f2{0.f, 0.f};
       if (j < NB) {
@@ -209,8 +233,8 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
         const int ff = j < NB ? 1 + j : 0;
         w = f2{a.plan[a.P1.kw + (0 * H + oo) * NFL + ff], a.plan[a.P1.kw + (1 * H + oo) * NFL + ff]};
       }
-      T.jf[i] = v;
-      T.jw[i] = w;
+      T.jf[t / 32][t % 32] = v;
+      T.jw[t / 32][t % 32] = w;
     }
   }
   for (int i = lane; i < NKS * 64; i += 64) (&V.ks[0][0])[i] = 0.f;
@@ -237,27 +261,11 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
   const int rb = q >= NB + 2 ? q - (NB + 2) : 0;   // base lanes
   const float xknot = q < NG ? a.plan[a.P0.knots + xi * NG + q] : __builtin_inff();
   const f2 mrow = xi == 0 ? f2{1.f, 0.f} : f2{0.f, 1.f};   // this row's component of (dx_0, dx_1)
-  // layer-1 feature rounds of the group: job j = cc0 + 3 r, its constants in T.jf / T.jw (idle
-  // lane 15 reads group 0's, its results are never used)
-  const int jb = o * 12 + cc0;
+  // layer-1 feature rounds of the group: job j = cc0 + 3 r, its constants in T.jf / T.jw [r][l]
+  // (idle lane 15 reads group 0's, its results are never used)
   static_assert(NB % 3 == 1 && NFL <= 3 * RF1, "SiLU = job NB in the last round");
   const float4* hk4 = reinterpret_cast<const float4*>(&TI.knots[(D + o) * NG + KT * cc0]);   // 4 knots
-  // pair / single slots
-  int p0[NPL0], p1[NPL1];
-#pragma unroll
-  for (int r = 0; r < NPL0; ++r) {
-    const int P = cc0 * NPL0 + r, i = P / KP, kp = P % KP;
-    p0[r] = (i * H + o) * KP + kp;
-    asm volatile("" : "+v"(p0[r]));
-  }
-#pragma unroll
-  for (int r = 0; r < NPL1; ++r) {
-    p1[r] = o * K + (cc0 + 3 * r);
-    asm volatile("" : "+v"(p1[r]));
-  }
   const bool sok = act && cc0 < 2;                 // single / edge lanes
-  const int ps0 = ((D - 1) * H + o) * KP + (KP - 1);   // layer-0 single: (1, o, 8 + cc0)
-  const int ps1 = o * K + (K - 1);                     // layer-1 single: (o, cc0, 9)
   const f2 dsel = f2{(sok && cc0 == 0) ? 1.f : 0.f, (sok && cc0 == 1) ? 1.f : 0.f};
   const int ie = sok ? cc0 : 0;                        // edge input (layer 0) / output (layer 1)
   const int t1 = D + o;                                // combined input index of h_o
@@ -302,22 +310,44 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
       float px = tape_at(n_ev - 2, xi), ph = tape_at(n_ev - 2, D + o);
       float ay1 = 0.f;   // adjoint of y (state dim `row`) at the end of the current step
       int jj = a.T - 1;
+      // the next output's schedule entry and adjoint, and the next step's coefficients, fetched one
+      // step ahead: their global round trips overlap the step's evaluations instead of heading its
+      // chain (as the forward's output schedule, fetode_fused.hip)
+      int pst = -1, pmd = 1;
+      float psl = 0.f, pg = 0.f;
+      auto fetch_out = [&]() __attribute__((always_inline)) {
+        pst = jj >= 1 ? a.out_step[jj] : -1;
+        if (jj >= 1) {
+          pmd = a.out_mode[jj];
+          psl = a.out_slope[jj];
+          pg = live ? a.gsol[((int64_t)jj * a.B + b) * D + row] : 0.f;
+        }
+      };
+      fetch_out();
+      int sn = a.n_steps - 1;
+      float sc0 = sn >= 0 ? a.step_coef[4 * sn] : 0.f, sc1 = sn >= 0 ? a.step_coef[4 * sn + 1] : 0.f;
+      float sc2 = sn >= 0 ? a.step_coef[4 * sn + 2] : 0.f;
       for (int s = a.n_steps - 1; s >= 0; --s) {
         float bc[4], ac[4][3];
-        step_coefs(a.method, a.step_coef[4 * s], a.step_coef[4 * s + 1], a.step_coef[4 * s + 2], bc, ac);
+        step_coefs(a.method, sc0, sc1, sc2, bc, ac);
+        if (s > 0) {
+          sc0 = a.step_coef[4 * (s - 1)];
+          sc1 = a.step_coef[4 * (s - 1) + 1];
+          sc2 = a.step_coef[4 * (s - 1) + 2];
+        }
         float ay0x = 0.f;
-        for (; jj >= 1 && a.out_step[jj] == s; --jj) {
-          const float g = live ? a.gsol[((int64_t)jj * a.B + b) * D + row] : 0.f;
-          const int mode = a.out_mode[jj];
-          if (mode == 0) {
+        while (pst == s) {
+          const float g = pg;
+          if (pmd == 0) {
             ay0x += g;
-          } else if (mode == 1) {
+          } else if (pmd == 1) {
             ay1 += g;
           } else {
-            const float slo = a.out_slope[jj];
-            ay1 = ffma(slo, g, ay1);
-            ay0x = ffma(1.0f - slo, g, ay0x);
+            ay1 = ffma(psl, g, ay1);
+            ay0x = ffma(1.0f - psl, g, ay0x);
           }
+          --jj;
+          fetch_out();
         }
         float ak[4];
 #pragma unroll
@@ -368,8 +398,8 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
             // features: logistic j / SiLU, d out / d h through both outputs
 #pragma unroll
             for (int r = 0; r < RF1; ++r) {
-              const float4 jf = T.jf[jb + 3 * r];
-              const f2 jw = T.jw[jb + 3 * r];
+              const float4 jf = T.jf[r][l];
+              const f2 jw = T.jw[r][l];
               const bool sl = r == RF1 - 1 && cc0 == 1;   // the SiLU job (NB = cc0 + 3 (RF1 - 1))
               const float sg = rcp(1.0f + ex2(ffma(jf.x, h, jf.y)));
               const float val = sl ? h * sg : sg;
@@ -417,10 +447,10 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
             S7_LO();
 #pragma unroll
             for (int r = 0; r < NPL1; ++r)
-              dh += pair_vjp<F_>(T.fa1[p1[r]], T.fb1[p1[r]], T.ee1[p1[r]], g01, h, up, wo, E, gl1, A1[r], C1[r], E1[r]);
+              dh += pair_vjp<F_>(T.fa1[r][l], T.fb1[r][l], T.ee1[r][l], g01, h, up, wo, E, gl1, A1[r], C1[r], E1[r]);
             {
-              const float4 fa = T.fa1[ps1], fb = T.fb1[ps1];
-              const f2 ee = T.ee1[ps1];
+              const float4 fa = T.fa1[NPL1][l], fb = T.fb1[NPL1][l];
+              const f2 ee = T.ee1[NPL1][l];
               const bool c1 = cc0 == 1;
               dh += single_vjp<F_>(c1 ? fa.y : fa.x, c1 ? fa.w : fa.z, c1 ? fb.y : fb.x, c1 ? fb.w : fb.z,
                                    c1 ? ee.y : ee.x, ge, h, up, wo, E, gl1, As1, Cs1, Es1);
@@ -442,17 +472,17 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
             S7_LO();
 #pragma unroll
             for (int r = 0; r < NPL0; ++r) {
-              const bool i1 = p0[r] >= H * KP;   // the pair's input
+              const bool i1 = cc0 * NPL0 + r >= KP;   // the pair's input (LaneMap::p0)
               const float4 gx = V.gx[hh][i1 ? 1 : 0];
-              const float d = pair_vjp<F_>(T.fa0[p0[r]], T.fb0[p0[r]], T.ee0[p0[r]], g2, gx.x, gx.y, gx.z, gx.w, gl0,
+              const float d = pair_vjp<F_>(T.fa0[r][l], T.fb0[r][l], T.ee0[r][l], g2, gx.x, gx.y, gx.z, gx.w, gl0,
                                            A0[r], C0[r], E0[r]);
               dx01 = pfma(f2{i1 ? 0.f : 1.f, i1 ? 1.f : 0.f}, splat(d), dx01);
             }
             const float ge = sok ? g0o : 0.f;
             {
               const float4 gx = V.gx[hh][D - 1];
-              const float4 fa = T.fa0[ps0], fb = T.fb0[ps0];
-              const f2 ee = T.ee0[ps0];
+              const float4 fa = T.fa0[NPL0][l], fb = T.fb0[NPL0][l];
+              const f2 ee = T.ee0[NPL0][l];
               const bool c1 = cc0 == 1;
               const float d = single_vjp<F_>(c1 ? fa.y : fa.x, c1 ? fa.w : fa.z, c1 ? fb.y : fb.x, c1 ? fb.w : fb.z,
                                              c1 ? ee.y : ee.x, ge, gx.x, gx.y, gx.z, gx.w, gl0, As0, Cs0, Es0);
@@ -529,22 +559,23 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
     if (lo && act) base[idx] = t;
   };
   // Ferro sums
+  const LaneMap lm(l);
 #pragma unroll
   for (int r = 0; r < NPL0; ++r) {
-    const int e = 2 * p0[r];
+    const int e = 2 * lm.p0(r);
     put(part, A0L.oA + e, A0[r].x); put(part, A0L.oA + e + 1, A0[r].y);
     put(part, A0L.oC + e, C0[r].x); put(part, A0L.oC + e + 1, C0[r].y);
     put(part, A0L.oE + e, E0[r].x); put(part, A0L.oE + e + 1, E0[r].y);
   }
 #pragma unroll
   for (int r = 0; r < NPL1; ++r) {
-    const int oo = p1[r] / K, k = p1[r] % K, e0 = (oo * D + 0) * K + k, e1 = (oo * D + 1) * K + k;
+    const int oo = lm.p1(r) / K, k = lm.p1(r) % K, e0 = (oo * D + 0) * K + k, e1 = (oo * D + 1) * K + k;
     put(part1, A1L.oA + e0, A1[r].x); put(part1, A1L.oA + e1, A1[r].y);
     put(part1, A1L.oC + e0, C1[r].x); put(part1, A1L.oC + e1, C1[r].y);
     put(part1, A1L.oE + e0, E1[r].x); put(part1, A1L.oE + e1, E1[r].y);
   }
   {
-    const int es0 = 2 * ps0 + cc0, es1 = (o * D + cc0) * K + (K - 1);
+    const int es0 = 2 * lm.ps0() + cc0, es1 = (o * D + cc0) * K + (K - 1);
     const float a0 = As0 + partner(As0), c0 = Cs0 + partner(Cs0), x0 = Es0 + partner(Es0);
     const float a1 = As1 + partner(As1), c1 = Cs1 + partner(Cs1), x1 = Es1 + partner(Es1);
     if (lo && sok) {
