@@ -46,7 +46,8 @@ constexpr int NPL0 = (D * KP) / 3, NPL1 = K / 3;   // pair rounds per layer; the
 static_assert(D * KP - 3 * NPL0 == 1 && K - 3 * NPL1 == 1, "one leftover pair (layer 0) / k (layer 1)");
 constexpr int RF1 = (NFL + 2) / 3;                  // layer-1 feature rounds (SiLU + NB logistic)
 constexpr int KT = (NG + 2) / 3;                    // knots per group lane
-constexpr int AR = NS + 2 * kSO;                    // spline-sum row: kSO guards, NS bases, kSO guards
+constexpr int AR = NS + 2 * kSO;
+constexpr int SPR = NI + 2;                         // spline-table row stride (float4)                    // spline-sum row: kSO guards, NS bases, kSO guards
 // KAN-sum LDS slots per lane
 constexpr int S_LW0 = 0, S_LA0 = H, S_LB0 = H + 1, S_LW1 = H + 2, S_LA1 = S_LW1 + 2 * RF1, S_LB1 = S_LA1 + RF1,
               NKS = S_LB1 + RF1;
@@ -61,8 +62,9 @@ struct Tab {
   f2 ee0[NPL0 + 1][32];                          // 2^(gs log2e Ec) (the factored coercive gate)
   float4 fa1[NPL1 + 1][32], fb1[NPL1 + 1][32];  // layer-1 pairs: elements (o, 0, k), (o, 1, k)
   f2 ee1[NPL1 + 1][32];
-  float4 sp0[H * D * (NI + 1)], sp1[D * H * (NI + 1)];  // edge cubics by interval (plan layout)
-  float kw0[H * D * NFL];                               // SiLU weight, 2 * scaled logistic weights
+  // edge cubics by interval, one row of NI + 1 per edge padded to SPR float4: rows of different
+  // edges start on different 16-B slots of the bank row (12: units 4 apart collide)
+  float4 sp0[H * D * SPR], sp1[D * H * SPR];
   float kwT[D * NB * H];                                // layer-0 logistic weights by (i, j): the ten outputs
   float4 jf[RF1][32];   // layer-1 job (o, j = cc0 + 3 r): (-a log2e, a b log2e, a, b); SiLU (j = NB): (-log2e, 0, 1, 0)
   f2 jw[RF1][32];       // its weights for outputs 0, 1 (SiLU: the base weights)
@@ -210,10 +212,9 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
     const float4* s0 = reinterpret_cast<const float4*>(a.plan + a.P0.sp);
     const float4* s1 = reinterpret_cast<const float4*>(a.plan + a.P1.sp);
     for (int i = tid; i < H * D * (NI + 1); i += 64 * kTPB) {
-      T.sp0[i] = s0[i];
-      T.sp1[i] = s1[i];
+      T.sp0[(i / (NI + 1)) * SPR + i % (NI + 1)] = s0[i];
+      T.sp1[(i / (NI + 1)) * SPR + i % (NI + 1)] = s1[i];
     }
-    for (int i = tid; i < H * D * NFL; i += 64 * kTPB) T.kw0[i] = a.plan[a.P0.kw + i];
     for (int i = tid; i < D * NB * H; i += 64 * kTPB) {
       const int ij = i / H, oo = i % H, ii = ij / NB, j = ij % NB;
       T.kwT[i] = a.plan[a.P0.kw + (oo * D + ii) * NFL + 1 + j];
@@ -269,8 +270,8 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
   const f2 dsel = f2{(sok && cc0 == 0) ? 1.f : 0.f, (sok && cc0 == 1) ? 1.f : 0.f};
   const int ie = sok ? cc0 : 0;                        // edge input (layer 0) / output (layer 1)
   const int t1 = D + o;                                // combined input index of h_o
-  const float4* sp1e = &T.sp1[(ie * H + o) * (NI + 1)];
-  const float4* sp0e = &T.sp0[(o * D + ie) * (NI + 1)];
+  const float4* sp1e = &T.sp1[(ie * H + o) * SPR];
+  const float4* sp0e = &T.sp0[(o * D + ie) * SPR];
   const int srow = sok ? hh * (H * D) + o * D + ie : NSR - 1;   // this lane's spline-sum rows
   float* acc0 = &V.spl[0][srow][0];
   float* acc1 = &V.spl[1][srow][0];
@@ -293,7 +294,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
   const int n_ev = a.n_steps * ns;
   auto run = [&](auto fact_tag) __attribute__((always_inline)) {
     constexpr bool F_ = decltype(fact_tag)::value;
-    const float kbase0 = T.kw0[(o * D + ie) * NFL];
+    const float kbase0 = a.plan[a.P0.kw + (o * D + ie) * NFL];   // the edge's SiLU weight
     for (int64_t b0 = ((int64_t)blockIdx.x * kTPB + wid) * 2; b0 < a.B; b0 += (int64_t)gridDim.x * kTPB * 2) {
       const int64_t b = b0 + hh;
       const bool live = b < a.B;
