@@ -46,8 +46,10 @@ constexpr int NPL0 = (D * KP) / 3, NPL1 = K / 3;   // pair rounds per layer; the
 static_assert(D * KP - 3 * NPL0 == 1 && K - 3 * NPL1 == 1, "one leftover pair (layer 0) / k (layer 1)");
 constexpr int RF1 = (NFL + 2) / 3;                  // layer-1 feature rounds (SiLU + NB logistic)
 constexpr int KT = (NG + 2) / 3;                    // knots per group lane
-constexpr int AR = NS + 2 * kSO;
-constexpr int SPR = NI + 2;                         // spline-table row stride (float4)                    // spline-sum row: kSO guards, NS bases, kSO guards
+// spline-sum row: kSO guards, NS bases, kSO guards, one pad: an odd row stride puts the 20 edge rows
+// of a half-wave on 20 different banks (an even one folds them onto 16)
+constexpr int AR = NS + 2 * kSO + 1;
+constexpr int SPR = NI + 2;                         // spline-table row stride (float4)
 // KAN-sum LDS slots per lane
 constexpr int S_LW0 = 0, S_LA0 = H, S_LB0 = H + 1, S_LW1 = H + 2, S_LA1 = S_LW1 + 2 * RF1, S_LB1 = S_LA1 + RF1,
               NKS = S_LB1 + RF1;
@@ -175,7 +177,9 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
   using L0 = BL<D, H, K, NB, NG, true>;
   using L1 = BL<H, D, K, NB, NG, true>;
   constexpr AccLayout A0L = L0::AL, A1L = L1::AL;
-  __shared__ BInTab<W, NG, NB> TI;   // knots, 1 / widths, basis cubics [t][m][r] of all 12 inputs
+  // knots, 1 / widths, basis cubics [t][m][r] of all 12 inputs (no logistic table: the lanes hold
+  // their logistic constants in registers / T.jf)
+  __shared__ BInTab<W, NG, 0> TI;
   __shared__ Tab T;
   __shared__ Wv WV[kTPB];
   const int tid = threadIdx.x, wid = tid >> 6, lane = tid & 63;
