@@ -51,8 +51,10 @@ constexpr int KT = (NG + 2) / 3;                    // knots per group lane
 constexpr int AR = NS + 2 * kSO + 1;
 constexpr int SPR = NI + 2;                         // spline-table row stride (float4)
 // KAN-sum LDS slots per lane
-constexpr int S_LW0 = 0, S_LA0 = H, S_LB0 = H + 1, S_LW1 = H + 2, S_LA1 = S_LW1 + 2 * RF1, S_LB1 = S_LA1 + RF1,
-              NKS = S_LB1 + RF1;
+// KAN-sum LDS slot PAIRS per lane (both components of a pair are updated together, one
+// ds_read_b64 / ds_write_b64 each): layer-0 logistic weights of outputs (2p, 2p + 1), layer-0
+// (a, b), layer-1 round r's logistic weights of outputs (0, 1), layer-1 round r's (a, b)
+constexpr int P_LW0 = 0, P_AB0 = H / 2, P_LW1 = P_AB0 + 1, P_AB1 = P_LW1 + RF1, NKP = P_AB1 + RF1;
 constexpr int NSR = 2 * (H * D) + 1;                // spline rows per layer: (half, o, i) + a dummy row
 // The element constants a lane reads are tabled per ROUND and LANE ([r][lane & 31]: both halves
 // hold the same parameters): a round's reads are 32 consecutive entries, free of the bank conflicts
@@ -90,7 +92,7 @@ struct Wv {
   float4 bx[2][D];   // the interval's four bases B_{m-3 .. m}(x_i)
   int mx[2][D];      // interval (NI: outside the grid / non-finite)
   float g0[2][H];    // d loss / d h of the evaluation
-  float ks[NKS][64];                // KAN sums, [slot][lane]
+  f2 ks[NKP][64];                   // KAN sums, [pair][lane]
   float spl[2][NSR][AR];            // spline sums per layer and edge row
 };
 __device__ __forceinline__ float dcubic(float4 c, float u) { return ffma(u, ffma(3.0f * u, c.w, 2.0f * c.z), c.y); }
@@ -242,7 +244,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
       T.jw[t / 32][t % 32] = w;
     }
   }
-  for (int i = lane; i < NKS * 64; i += 64) (&V.ks[0][0])[i] = 0.f;
+  for (int i = lane; i < NKP * 64; i += 64) (&V.ks[0][0])[i] = splat(0.f);
   for (int i = lane; i < 2 * NSR * AR; i += 64) (&V.spl[0][0][0])[i] = 0.f;
   const bool fact = a.plan[a.P0.flag] <= kFactorLimit && a.plan[a.P1.flag] <= kFactorLimit;
 
@@ -279,7 +281,7 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
   const int srow = sok ? hh * (H * D) + o * D + ie : NSR - 1;   // this lane's spline-sum rows
   float* acc0 = &V.spl[0][srow][0];
   float* acc1 = &V.spl[1][srow][0];
-  float* ks = &V.ks[0][lane];                                 // slot k at ks[64 k]
+  f2* ks = &V.ks[0][lane];                                    // pair k at ks[64 k]
 
   // ---- Ferro accumulators ----
   f2 A0[NPL0], C0[NPL0], E0[NPL0], A1[NPL1], C1[NPL1], E1[NPL1];
@@ -412,10 +414,8 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
               const float Tt = ffma(g01.x, jw.x, g01.y * jw.y) * der;
               // sums: logistic weights of both outputs (SiLU job: base weights), a, b
               if (KS && !(S7_SKIP & 1)) {
-              ks[64 * (S_LW1 + 2 * r)] = ffma(g01.x, val, ks[64 * (S_LW1 + 2 * r)]);
-              ks[64 * (S_LW1 + 2 * r + 1)] = ffma(g01.y, val, ks[64 * (S_LW1 + 2 * r + 1)]);
-              ks[64 * (S_LA1 + r)] = ffma(Tt, h - jf.w, ks[64 * (S_LA1 + r)]);
-              ks[64 * (S_LB1 + r)] = ffma(-Tt, jf.z, ks[64 * (S_LB1 + r)]);
+              ks[64 * (P_LW1 + r)] = pfma(g01, splat(val), ks[64 * (P_LW1 + r)]);
+              ks[64 * (P_AB1 + r)] = pfma(f2{Tt, -Tt}, f2{h - jf.w, jf.z}, ks[64 * (P_AB1 + r)]);
               }
               dh = ffma(Tt, jf.z, dh);
             }
@@ -520,14 +520,12 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
               S = ffma(gv.x, kv.x, S);
               S = ffma(gv.y, kv.y, S);
               if (KS && !(S7_SKIP & 4)) {
-              ks[64 * (S_LW0 + oo)] = ffma(gv.x, sgx, ks[64 * (S_LW0 + oo)]);
-              ks[64 * (S_LW0 + oo + 1)] = ffma(gv.y, sgx, ks[64 * (S_LW0 + oo + 1)]);
+              ks[64 * (P_LW0 + oo / 2)] = pfma(gv, splat(sgx), ks[64 * (P_LW0 + oo / 2)]);
               }
             }
             const float Tt = (S * kwm) * ffma(-sgx, sgx, sgx);
             if (KS && !(S7_SKIP & 8)) {
-            ks[64 * S_LA0] = ffma(Tt, cx - pb0, ks[64 * S_LA0]);
-            ks[64 * S_LB0] = ffma(-Tt, pa0, ks[64 * S_LB0]);
+            ks[64 * P_AB0] = pfma(f2{Tt, -Tt}, f2{cx - pb0, pa0}, ks[64 * P_AB0]);
             }
             dx01 = pfma(mrow, splat(Tt * pa0), dx01);
           }
@@ -622,8 +620,8 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
 #pragma unroll
   for (int r = 0; r < RF1; ++r) {
     const int j = cc0 + 3 * r;
-    const float vx = ks[64 * (S_LW1 + 2 * r)], vy = ks[64 * (S_LW1 + 2 * r + 1)];
-    const float va = ks[64 * (S_LA1 + r)], vb = ks[64 * (S_LB1 + r)];
+    const float vx = ks[64 * (P_LW1 + r)].x, vy = ks[64 * (P_LW1 + r)].y;
+    const float va = ks[64 * (P_AB1 + r)].x, vb = ks[64 * (P_AB1 + r)].y;
     const float wx = vx + partner(vx), wy = vy + partner(vy), xa = va + partner(va), xb = vb + partner(vb);
     if (lo && act && j < NB) {
       part1[A1L.oLw + 0 * A1L.NL + o * NB + j] = wx;
@@ -637,12 +635,12 @@ __global__ __launch_bounds__(64 * kTPB) __attribute__((amdgpu_waves_per_eu(2))) 
   }
 #pragma unroll
   for (int oo = 0; oo < H; ++oo) {
-    const float v = ks[64 * (S_LW0 + oo)];
+    const float v = oo % 2 ? ks[64 * (P_LW0 + oo / 2)].y : ks[64 * (P_LW0 + oo / 2)].x;
     const float w = v + partner(v);
     if (lo && q < NB) part[A0L.oLw + oo * A0L.NL + xi * NB + q] = w;
   }
   {
-    const float va = ks[64 * S_LA0], vb = ks[64 * S_LB0];
+    const float va = ks[64 * P_AB0].x, vb = ks[64 * P_AB0].y;
     const float xa = va + partner(va), xb = vb + partner(vb);
     if (lo && q < NB) {
       part[A0L.oLa + xi * NB + q] = xa;
