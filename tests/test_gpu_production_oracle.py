@@ -169,14 +169,15 @@ def test_forecaster_latent64_b8192_rows_vs_oracle(dev):
     _envelope(got.cpu()[rows], outs[torch.float32], outs[torch.float64], "forecaster latent 64, B=8192 rows")
 
 
+@pytest.mark.timeout(900)   # the CPU oracle: 5 x 380 steps of the [64, 128, 64] field on 8 rows
 def test_forecaster_bench_workload_96_horizon_vs_oracle(dev):
     """BASELINE config 4 at its own horizon: the bench's ETT workload exactly —
     LatentNeuralODEForecaster 96 -> 96, latent 64, KAN-FET field [64, 128, 64] scaled x 0.1,
     odeint_rk4 with the reference TrainConfig's 4 substeps over t_fut = 0..95 (380 rk4 steps),
     B = 8192, first call on fresh hysteresis state (train_kan_fet_ett.py:51-83, 155-197) — against
-    oracle/ett_ref.py in fp32 and fp64 on 16 windows spread over the batch (both row-tile edges and
-    12 seeded random rows).  Bar: the envelope rule above, |gpu - fp64| <= 4 |ref fp32 - fp64|
-    + 1e-5 x scale over the 16 x 96 forecasts, the fp32 term the worst of the reference's own
+    oracle/ett_ref.py in fp32 and fp64 on 8 windows spread over the batch (both row-tile edges and
+    4 seeded random rows).  Bar: the envelope rule above, |gpu - fp64| <= 4 |ref fp32 - fp64|
+    + 1e-5 x scale over the 8 x 96 forecasts, the fp32 term the worst of the reference's own
     rounding and three re-roundings of its parameters."""
     c = p = 96
     torch.manual_seed(0)
@@ -197,7 +198,7 @@ def test_forecaster_bench_workload_96_horizon_vs_oracle(dev):
     assert got.shape == (B, p) and torch.isfinite(got).all()
     gr = torch.Generator().manual_seed(22)
     rows = torch.cat([torch.tensor([0, 1, B - 2, B - 1]),
-                      (torch.randperm(B - 4, generator=gr)[:12] + 2).sort().values])
+                      (torch.randperm(B - 4, generator=gr)[:4] + 2).sort().values])
     xs = xb[rows.to(dev)].cpu()
     torch.set_num_threads(min(16, torch.get_num_threads()))
     outs = {}
@@ -224,5 +225,5 @@ def test_forecaster_bench_workload_96_horizon_vs_oracle(dev):
             c32 = E.ForecasterRef(sdp, lambda tt, zz: fp(zz))(xs, t_fut, rk4_substeps=4).double()
         if (c32 - e64).abs().max() > (worst32 - e64).abs().max():
             worst32 = c32
-    rel, spread = _envelope(got.cpu()[rows], worst32, e64, "forecaster 96->96 x4 substeps, B=8192, 16 windows")
+    rel, spread = _envelope(got.cpu()[rows], worst32, e64, "forecaster 96->96 x4 substeps, B=8192, 8 windows")
     print(f"config-4 horizon: |gpu-fp64|/scale {rel:.3e}, worst fp32 rounding vs fp64 /scale {spread:.3e}")
