@@ -340,14 +340,20 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
   constexpr int kPitch = pitch_of(kCh);
   static_assert(kCh * kRows <= kThreads && (kCh & 1) == 0, "one staging item per thread, even chunks");
   static_assert(!FERRO || K % 2 == 0, "Ferro elements in (k, k+1) pairs");
-  __shared__ float s_x[kCh * kRows], s_w[kCh * kRows], s_e[kCh * kRows];
+  // staged per (input, row) at si * kRP + sr: the pitch kRows + 4 puts a half-wave's 8 inputs x 4 rows
+  // on 32 different banks (at kRows the 8 inputs of a row shared one: 8-way, round 6)
+  constexpr int kRP = kRows + 4;
+  __shared__ float s_x[kCh * kRP], s_w[kCh * kRP], s_e[kCh * kRP];
   __shared__ float s_dfl[kOuts * kCh];
   // the chunk's per-input KAN parameters (knots | 1 / spans | logistic (-a log2e, a b log2e)), staged
   // one chunk ahead and double-buffered by chunk parity: the staging items read them from LDS instead
   // of a dependent L2 round trip per item before the basis-table gather (the KANLinear part of the
   // layer 98 -> 52 us with the loads taken away entirely)
-  constexpr int kPar = 64, kPK = 0, kPR = 12, kPL = 24, kP2 = 44, kP3 = 54;
-  __shared__ __attribute__((aligned(16))) float s_par[KAN ? 2 : 1][KAN ? kCh * kPar : 1];
+  // In LDS each input's block sits at a pitch of kParL = 68 floats: at 64 (one 256-byte bank row) the
+  // 8 inputs a half-wave reads at once all hit the same bank — the layer's LDS was 65 % conflict
+  // cycles (SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE, profiles/r06_lds_wide.txt)
+  constexpr int kPar = 64, kParL = 68, kPK = 0, kPR = 12, kPL = 24, kP2 = 44, kP3 = 54;
+  __shared__ __attribute__((aligned(16))) float s_par[KAN ? 2 : 1][KAN ? kCh * kParL : 1];
   // KAN features of the chunk (MFMA A operand); the epilogue reuses the space for the Ferro sums
   // and the second K-half of the MFMA tile
   constexpr int kPhi = KAN ? kRows * kPitch : 0, kFer = 2 * kRows * (kOuts + 1);
@@ -400,7 +406,7 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
   };
   if constexpr (KAN) {
     const float p0 = ld_par(ibeg);
-    if (pld) s_par[0][tid] = p0;  // read after the first chunk's barrier
+    if (pld) s_par[0][(tid / kPar) * kParL + tid % kPar] = p0;  // read after the first chunk's barrier
   }
   int pbuf = 0;
   for (int i0 = ibeg; i0 < iend; i0 += kCh) {
@@ -419,9 +425,9 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
       if (stager) {
       // is_moving_up = sigmoid(gate_slope (x - prev_x)) (ferro_class.py:387), w = wc (1 - up)
       const float up = rcp(1.0f + ex2(-gsl2e * (x - pv)));
-      s_x[si * kRows + sr] = x;
-      s_w[si * kRows + sr] = wc * (1.0f - up);
-      s_e[si * kRows + sr] = ex2(gsl2e * x);
+      s_x[si * kRP + sr] = x;
+      s_w[si * kRP + sr] = wc * (1.0f - up);
+      s_e[si * kRP + sr] = ex2(gsl2e * x);
       }
       if (tid < kOuts * kCh) s_dfl[tid] = plan[L.dflag + (int64_t)(o0 + tid / kCh) * in + i0 + tid % kCh];
     }
@@ -431,7 +437,7 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
       // indicator, then the Cox-de Boor recursion restricted to the interval's triangle (the four
       // bases B_{m-3..m} that can be non-zero) on the staged knots and reciprocal spans, all from LDS
       // (no per-item gather of fitted tables: the layer's staging waited on those L2 round trips)
-      const float* P = &s_par[KAN ? pbuf : 0][si * kPar];
+      const float* P = &s_par[KAN ? pbuf : 0][si * kParL];
       const float* g = P + kPK;
       int m = -1;
 #pragma unroll
@@ -477,7 +483,7 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
       }
     }
     if constexpr (KAN) {
-      if (pld) s_par[pbuf ^ 1][tid] = parn;
+      if (pld) s_par[pbuf ^ 1][(tid / kPar) * kParL + tid % kPar] = parn;
     }
     __syncthreads();
     if constexpr (KAN) pbuf ^= 1;
@@ -496,7 +502,7 @@ __device__ __forceinline__ void wide_tile(const WideArgs& a, const int bx, const
 #pragma unroll kIU
       for (int ii = 0; ii < kCh; ++ii) {
         const int i = i0 + ii;
-        const float xv = s_x[ii * kRows + lane], wg = s_w[ii * kRows + lane], e = s_e[ii * kRows + lane];
+        const float xv = s_x[ii * kRP + lane], wg = s_w[ii * kRP + lane], e = s_e[ii * kRP + lane];
 #pragma unroll
         for (int j = 0; j < kJ; ++j) {
           const int jo = kJ * w + j;
