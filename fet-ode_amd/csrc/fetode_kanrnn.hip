@@ -27,7 +27,7 @@ constexpr int kWaves = 4;         // waves (rows in flight) per workgroup
 constexpr int kMaxH = 256;        // hidden columns (4 per lane)
 constexpr int kMaxF = 64;         // input features
 constexpr int kMaxQ = 2048;       // combined basis columns (F + H) * nb, 32 per lane
-constexpr int kMaxW = 16384;      // latent * H floats of W^T in LDS (64 KiB)
+constexpr int kMaxW = 16384;      // (latent + 1) * H floats of W^T in LDS (64 KiB)
 constexpr int kBwdWaves = 4096;   // waves of the backward (rows are strided over them)
 constexpr int kFwdGroups = 1024;  // forward workgroups (4 waves each)
 constexpr int kRedChunks = 32;    // first-pass chunks of the fixed-order partial reduction
@@ -77,7 +77,10 @@ __device__ __forceinline__ void col_params(const RnnArgs& a, int c, float& na, f
 
 template <int MC>
 __global__ __launch_bounds__(256) void kanrnn_fwd_kernel(RnnArgs a) {
-  extern __shared__ float s_w[];                 // W^T (H, latent) when projecting
+  // W^T (H, latent) when projecting, rows at a pitch of latent + 1: the staging writes of 32
+  // consecutive j (one row each) land on 32 banks instead of one (37 % of the kernel's LDS cycles
+  // were conflicts at pitch latent = 64, profiles/r06_lds_enc.txt)
+  extern __shared__ float s_w[];
   __shared__ float s_x[kWaves][kMaxF];
   __shared__ float s_h[kWaves][2][kMaxH];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -85,7 +88,7 @@ __global__ __launch_bounds__(256) void kanrnn_fwd_kernel(RnnArgs a) {
   if (proj) {
     for (int e = threadIdx.x; e < a.latent * a.H; e += blockDim.x) {
       const int o = e / a.H, j = e - o * a.H;
-      s_w[j * a.latent + o] = a.w[e];
+      s_w[j * (a.latent + 1) + o] = a.w[e];
     }
     __syncthreads();
   }
@@ -137,7 +140,7 @@ __global__ __launch_bounds__(256) void kanrnn_fwd_kernel(RnnArgs a) {
   if (proj) {
     for (int o = lane; o < a.latent; o += 64) {
       float acc = 0.0f;
-      for (int j = 0; j < a.H; ++j) acc = __builtin_fmaf(h[j], s_w[j * a.latent + o], acc);
+      for (int j = 0; j < a.H; ++j) acc = __builtin_fmaf(h[j], s_w[j * (a.latent + 1) + o], acc);
       a.z0[row * a.latent + o] = acc + a.bias[o];
     }
   }
@@ -411,8 +414,9 @@ int fetode_kanrnn_forward(const fetode_kanrnn_t* m, const float* x, int64_t B, i
   if (T > 0 && !x) return set_err(FETODE_EINVAL, "kanrnn: null x");
   if (T == 0) return set_err(FETODE_EINVAL, "kanrnn: T = 0 (h_T = h0; nothing to run)");
   if (z0 && (m->latent < 1 || !m->w || !m->bias)) return set_err(FETODE_EINVAL, "kanrnn: z0 needs latent, w, bias");
-  if (z0 && (int64_t)m->latent * m->hidden > kMaxW)
-    return set_err(FETODE_EUNSUPPORTED, "kanrnn: latent * H = %d > %d (project outside)", m->latent * m->hidden, kMaxW);
+  if (z0 && (int64_t)(m->latent + 1) * m->hidden > kMaxW)
+    return set_err(FETODE_EUNSUPPORTED, "kanrnn: (latent + 1) * H = %d > %d (project outside)",
+                   (m->latent + 1) * m->hidden, kMaxW);
   if (z0 && m->latent > 256) return set_err(FETODE_EUNSUPPORTED, "kanrnn: latent > 256");
   if (B > (int64_t)0x7fffffff * kWaves) return set_err(FETODE_EINVAL, "kanrnn: batch too large");
   RnnArgs a = rnn_args(m);
@@ -422,7 +426,7 @@ int fetode_kanrnn_forward(const fetode_kanrnn_t* m, const float* x, int64_t B, i
   // enough workgroups to fill the chip; rows are strided over the waves (W^T is staged once per workgroup)
   const int64_t nwg = (B + kWaves - 1) / kWaves;
   const unsigned grid = (unsigned)(nwg < kFwdGroups ? nwg : kFwdGroups);
-  const size_t lds = z0 ? sizeof(float) * (size_t)m->latent * m->hidden : 0;
+  const size_t lds = z0 ? sizeof(float) * (size_t)(m->latent + 1) * m->hidden : 0;
   hipStream_t s = (hipStream_t)stream;
   if (a.H <= 64)
     hipLaunchKernelGGL(kanrnn_fwd_kernel<1>, dim3(grid), dim3(64 * kWaves), lds, s, a);

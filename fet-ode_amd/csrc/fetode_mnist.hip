@@ -668,7 +668,11 @@ __global__ __launch_bounds__(256) void wide_fwd4_kernel(fetode_kanlinear_t kl, c
   __shared__ float4 gk[kWideCh][kWideNG / 4];
   __shared__ float4 tb[kWideCh * kWideTab];
   __shared__ float2 lab[kWideCh][kWideNB];
-  __shared__ __attribute__((aligned(16))) float win[256 * kWinStride];
+  // per-lane dense-basis window, position-major ([pos][tid]): a lane's writes at its interval's
+  // positions m + 1 .. m + 4 hit bank tid % 32 whatever m is (lane-major at a 20-float stride they
+  // collided: 45 % of the head's LDS cycles were conflicts, profiles/r06_lds_mnist.txt)
+  constexpr int kWinPos = 16;   // positions 0 .. 15: slot m + r + 1 holds B_{m-3+r}; dense c at 4 + c
+  __shared__ float win[kWinPos * 256];
   const int in = kl.in_features;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = lane & 15, kq = lane >> 4;
@@ -677,8 +681,8 @@ __global__ __launch_bounds__(256) void wide_fwd4_kernel(fetode_kanlinear_t kl, c
   const int c0 = s * nch / S, c1 = (s + 1) * nch / S;
   const bool lg = kl.num_logistic != 0;
   const float4* wtab = reinterpret_cast<const float4*>(wp + (int64_t)in * kWideF * 16);
-  float* mywin = win + tid * kWinStride;
-  for (int q = 0; q < kWinStride; ++q) mywin[q] = 0.f;
+  float* mywin = win + tid;   // position q at mywin[256 q]
+  for (int q = 0; q < kWinPos; ++q) mywin[256 * q] = 0.f;
   f32x4 acc[4];
 #pragma unroll
   for (int t = 0; t < 4; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -778,25 +782,24 @@ __global__ __launch_bounds__(256) void wide_fwd4_kernel(fetode_kanlinear_t kl, c
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const float4 p = tm[q];
-            mywin[m + q + 1] = ffma(ffma(ffma(p.w, u, p.z), u, p.y), u, p.x);
+            mywin[256 * (m + q + 1)] = ffma(ffma(ffma(p.w, u, p.z), u, p.y), u, p.x);
           }
         }
         if (!fin) {   // non-finite x (rare): NaN bases, as (x - g) / d * 0 in the reference
 #pragma unroll
-          for (int q = 4; q < 12; ++q) mywin[q] = __builtin_nanf("");
+          for (int q = 4; q < 12; ++q) mywin[256 * q] = __builtin_nanf("");
         }
         asm volatile("" ::: "memory");  // the window writes stay before the vector reads
-        const float4 d0 = *reinterpret_cast<const float4*>(mywin + 4), d1 = *reinterpret_cast<const float4*>(mywin + 8);
-        feat[1] = d0.x; feat[2] = d0.y; feat[3] = d0.z; feat[4] = d0.w;
-        feat[5] = d1.x; feat[6] = d1.y; feat[7] = d1.z; feat[8] = d1.w;
+#pragma unroll
+        for (int c = 0; c < kWideNS; ++c) feat[1 + c] = mywin[256 * (4 + c)];
         asm volatile("" ::: "memory");
         if (ing) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) mywin[m + q + 1] = 0.f;
+          for (int q = 0; q < 4; ++q) mywin[256 * (m + q + 1)] = 0.f;
         }
         if (!fin) {
 #pragma unroll
-          for (int q = 4; q < 12; ++q) mywin[q] = 0.f;
+          for (int q = 4; q < 12; ++q) mywin[256 * q] = 0.f;
         }
 #pragma unroll
         for (int j = 0; j < kWideNB; ++j)  // 2 sigmoid(a (x - b)), mnist_kuramoto_kan.py:22 (2 in the weights)

@@ -241,8 +241,8 @@ def _rnn_desc(cell, lin, keep):
 
 
 def _fused_projection(lin, H) -> bool:
-    """to_latent inside the recurrence launch (W^T in LDS) when it fits."""
-    return lin is not None and lin.weight.shape[0] <= 256 and lin.weight.shape[0] * H <= 16384
+    """to_latent inside the recurrence launch (W^T in LDS, rows padded to latent + 1) when it fits."""
+    return lin is not None and lin.weight.shape[0] <= 256 and (lin.weight.shape[0] + 1) * H <= 16384
 
 
 class _KANRNNFn(torch.autograd.Function):
