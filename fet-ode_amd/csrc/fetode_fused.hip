@@ -328,7 +328,8 @@ __device__ __forceinline__ float v4_edges(const V4Lds<IN, FLEN>& L, const float*
   const int mraw = (int)__builtin_popcountll((bal >> (bbase + 16 * si)) & 0xFFFFull) - 1;
   const int msi = (unsigned)mraw < (unsigned)NI ? mraw : NI;
   const float xsi = L.G[si].z;
-  const float4 cf = *reinterpret_cast<const float4*>(&sp_o[(si * (NI + 1) + msi) * 4]);
+  // the cubic tables' rows are NI + 2 float4 apart (NI + 1 entries and a pad, fused4_kernel)
+  const float4 cf = *reinterpret_cast<const float4*>(&sp_o[(si * (NI + 2) + msi) * 4]);
   const f2 kw = kr[si * (NI + 1) + msi];
   f2 acc = splat(0.0f);
   float sgl = 0.0f;
@@ -408,11 +409,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   }
   constexpr int KT = (NG + 2) / 3;                   // knots per group lane
   static_assert(3 * KT >= NG, "knots per group lane");
-  constexpr int SPT0 = H * D * (NI + 1) * 4, SPT1 = D * H * (NI + 1) * 4;
+  // edge cubic tables by interval, one row of NI + 1 float4 per edge padded to SPR: at a pitch of 12
+  // float4 the rows of units 4 apart (layer 1) / of the same parity (layer 0) start on the same
+  // 16-byte slot of the bank row and the lanes' interval reads collide (35 % of the kernel's LDS
+  // cycles were conflicts, profiles/r06_lds_bench_nores.txt)
+  constexpr int SPR = NI + 2, SPE = (NI + 1) * 4;
+  constexpr int SPT0 = H * D * SPR * 4, SPT1 = D * H * SPR * 4;
 
   __shared__ __attribute__((aligned(16))) float s_sp0[SPT0];
   __shared__ __attribute__((aligned(16))) float s_sp1[SPT1];
-  __shared__ __attribute__((aligned(8))) f2 s_kr0[D * (NI + 1)], s_kr1[H * (NI + 1)];
+  __shared__ __attribute__((aligned(8))) f2 s_kr0[D * (NI + 1)], s_kr1[H * SPR];
   __shared__ float s_c0[H], s_c1[D];
   __shared__ __attribute__((aligned(16))) V4Lds<D, FLEN0> s_L0[TPW];
 
@@ -424,15 +430,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
   const bool valid = b < a.B;
   V4Lds<D, FLEN0>& L0 = s_L0[g];
 
-  for (int i = tid; i < SPT0; i += 64) s_sp0[i] = a.plan[a.P0.sp + i];
-  for (int i = tid; i < SPT1; i += 64) s_sp1[i] = a.plan[a.P1.sp + i];
+  for (int i = tid; i < H * D * SPE; i += 64) s_sp0[(i / SPE) * SPR * 4 + i % SPE] = a.plan[a.P0.sp + i];
+  for (int i = tid; i < D * H * SPE; i += 64) s_sp1[(i / SPE) * SPR * 4 + i % SPE] = a.plan[a.P1.sp + i];
   for (int i = tid; i < D * (NI + 1); i += 64) {
     const int in = i / (NI + 1), m = i % (NI + 1);
     s_kr0[i] = m < NI ? f2{a.plan[a.P0.knots + in * NG + m], a.plan[a.P0.rh + in * NI + m]} : f2{0.f, 0.f};
   }
   for (int i = tid; i < H * (NI + 1); i += 64) {
     const int in = i / (NI + 1), m = i % (NI + 1);
-    s_kr1[i] = m < NI ? f2{a.plan[a.P1.knots + in * NG + m], a.plan[a.P1.rh + in * NI + m]} : f2{0.f, 0.f};
+    s_kr1[in * SPR + m] = m < NI ? f2{a.plan[a.P1.knots + in * NG + m], a.plan[a.P1.rh + in * NI + m]} : f2{0.f, 0.f};
   }
   for (int i = tid; i < H; i += 64) s_c0[i] = a.plan[a.P0.fconst + i];
   for (int i = tid; i < D; i += 64) s_c1[i] = a.plan[a.P1.fconst + i];
@@ -606,10 +612,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void fu
 
   STAMP_DECL
   const float c0o = s_c0[o0c], c1o = s_c1[row];  // per-output constants, held in registers
-  const float* sp0_o = &s_sp0[o0c * D * (NI + 1) * 4];
+  const float* sp0_o = &s_sp0[o0c * D * SPR * 4];
   // layer 1: the cubic table of edge (o0 -> d = cc0) and the (knot, 1/width) rows of input o0
-  const float* sp1_e = &s_sp1[((gl < D ? gl : 0) * H + o0c) * (NI + 1) * 4];
-  const f2* kr1_o = &s_kr1[o0c * (NI + 1)];
+  const float* sp1_e = &s_sp1[((gl < D ? gl : 0) * H + o0c) * SPR * 4];
+  const f2* kr1_o = &s_kr1[o0c * SPR];
   const int fofs0 = gl * FPL0;
   const bool spl0 = act0 && gl < D;  // lanes owning a layer-0 spline edge (input si)
   const int si0 = spl0 ? gl : 0;
