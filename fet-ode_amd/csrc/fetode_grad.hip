@@ -267,7 +267,10 @@ typedef float gw_f32x4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void wide_gw_kernel(fetode_kanlinear_t kl, const float* __restrict__ x,
                                                      const float* __restrict__ g, int64_t B,
                                                      float* __restrict__ dpart) {
-  __shared__ float Fs[4][kGwF][64];
+  // feature rows at a pitch of 66: the MFMA A operand reads Fs[wv][m][col] for the 16 features m of
+  // a half-wave at once — at a pitch of 64 all 16 hit one bank (16-way; 64 % of the kernel's LDS
+  // cycles were conflicts, profiles/r06_lds_bench_nores.txt); at 66, 2 m + col covers 32 banks
+  __shared__ float Fs[4][kGwF][66];
   __shared__ float gs[64][16];
   __shared__ float gk[4][kGwNG];
   __shared__ float rk[4][3 * (kGwNG - 1)];  // 1 / (g[j+k] - g[j]) (bspline_local)
