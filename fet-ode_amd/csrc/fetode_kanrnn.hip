@@ -165,6 +165,7 @@ __global__ __launch_bounds__(256) void kanrnn_bwd_kernel(BwdArgs A) {
   __shared__ float s_cg[kWaves][kMaxH + 16];      // d loss / d (v - b) of the live columns (+ read padding)
   __shared__ float s_gn[kWaves][kMaxH];           // d loss / d h_{t-1}
   __shared__ int s_bad[kWaves][kIn];              // a dropped column reading this input gave NaN
+  __shared__ float s_thr[kIn];                    // per input slot: |v| below it keeps every dropped column finite
   extern __shared__ float4 s_par[];               // per combined column {-a, b, input slot, 0}
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int gw = blockIdx.x * kWaves + wv;
@@ -175,11 +176,37 @@ __global__ __launch_bounds__(256) void kanrnn_bwd_kernel(BwdArgs A) {
     col_params(a, c, na, b, src, isx);
     s_par[c] = make_float4(na, b, __int_as_float(isx ? src : kMaxF + src), 0.0f);
   }
+  // The dropped columns (c >= H) only ever contribute a NaN, when exp(na (v - b)) overflows.  With
+  // |na (v - b)| <= |na| (|v| + |b|) (1 + 2 eps), |v| < kExpFinite / |na| (1 - 1e-5) - |b| (1 + 1e-5)
+  // keeps every dropped column of the input finite: a step whose staged inputs all pass skips their
+  // checks (bitwise the same sums: they add nothing then).  A NaN bound (an infinite b) is -inf.
+  const int NU = a.F + a.H;   // inputs: x_t (F) and h_{t-1} (H)
+  for (int u = threadIdx.x; u < NU; u += blockDim.x) {
+    const bool ux = u < a.F;
+    const int c0 = ux ? u * a.nb : a.Fnb + (u - a.F) * a.nb;
+    float T = __builtin_inff();
+    for (int c = c0; c < c0 + a.nb; ++c) {
+      if (c < a.H || c >= a.Q) continue;   // live, or no column
+      float na, b;
+      int src;
+      bool isx;
+      col_params(a, c, na, b, src, isx);
+      const float t = kExpFinite / fabsf(na) * (1.0f - 1e-5f) - fabsf(b) * (1.0f + 1e-5f);
+      T = (t != t) ? -__builtin_inff() : (t < T ? t : T);
+    }
+    s_thr[ux ? u : kMaxF + u - a.F] = T;
+  }
   __syncthreads();
+  const float thr_x = lane < a.F ? s_thr[lane] : __builtin_inff();
+  float thr_h[MCL];
+#pragma unroll
+  for (int m = 0; m < MCL; ++m) {
+    const int c = lane + 64 * m;
+    thr_h[m] = c < a.H ? s_thr[kMaxF + c] : __builtin_inff();
+  }
   float ga[MQ], gb[MQ];
 #pragma unroll
   for (int m = 0; m < MQ; ++m) ga[m] = 0.f, gb[m] = 0.f;
-  const int NU = a.F + a.H;   // inputs: x_t (F) and h_{t-1} (H)
   for (int64_t row = gw; row < a.B; row += A.n_waves) {
     const float* xr = a.x + row * (int64_t)a.T * a.F;
     const float* tr = A.f.tape + row * (int64_t)a.T * a.H;
@@ -215,15 +242,22 @@ __global__ __launch_bounds__(256) void kanrnn_bwd_kernel(BwdArgs A) {
         load_hp(t - 1, hpn);
         if (lane < a.F) xn = xr[(int64_t)(t - 1) * a.F + lane];
       }
+      // every staged input inside its dropped columns' finite range: the step skips their checks
+      bool risky = lane < a.F && !(fabsf(xv) < thr_x);
+#pragma unroll
+      for (int m = 0; m < MCL; ++m) risky |= !(fabsf(hp[m]) < thr_h[m]);
+      const bool check_dropped = __builtin_amdgcn_ballot_w64(risky) != 0;
       wsync();
 #pragma unroll
       for (int m = 0; m < MQ; ++m) {
         const int c = lane + 64 * m;
         if (c >= a.Q) continue;
+        const bool live = m < MCL && c < a.H;
+        if (!live && !check_dropped) continue;
         const float4 pc = s_par[c];
         const int u = __float_as_int(pc.z);
         const float v = s_in[wv][u];
-        if (m < MCL && c < a.H) {
+        if (live) {
           // live column: torch's autograd of sigmoid(reciprocal(1 + exp(na * (v - b))) * 2)
           float e, r, d1;
           basis_col(v, pc.x, pc.y, e, r, d1);
