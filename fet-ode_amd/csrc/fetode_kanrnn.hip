@@ -207,6 +207,7 @@ __global__ __launch_bounds__(256) void kanrnn_bwd_kernel(BwdArgs A) {
   float ga[MQ], gb[MQ];
 #pragma unroll
   for (int m = 0; m < MQ; ++m) ga[m] = 0.f, gb[m] = 0.f;
+  bool bad_dirty = true;   // s_bad may hold flags (a step that checked its dropped columns, or LDS garbage)
   for (int64_t row = gw; row < a.B; row += A.n_waves) {
     const float* xr = a.x + row * (int64_t)a.T * a.F;
     const float* tr = A.f.tape + row * (int64_t)a.T * a.H;
@@ -236,7 +237,8 @@ __global__ __launch_bounds__(256) void kanrnn_bwd_kernel(BwdArgs A) {
         if (c < a.H) s_in[wv][kMaxF + c] = hp[m];
       }
       if (lane < a.F) s_in[wv][lane] = xv;
-      for (int u = lane; u < NU; u += 64) s_bad[wv][u < a.F ? u : kMaxF + u - a.F] = 0;
+      if (bad_dirty)
+        for (int u = lane; u < NU; u += 64) s_bad[wv][u < a.F ? u : kMaxF + u - a.F] = 0;
       float hpn[MCL], xn = 0.0f;
       if (t > 0) {
         load_hp(t - 1, hpn);
@@ -247,6 +249,7 @@ __global__ __launch_bounds__(256) void kanrnn_bwd_kernel(BwdArgs A) {
 #pragma unroll
       for (int m = 0; m < MCL; ++m) risky |= !(fabsf(hp[m]) < thr_h[m]);
       const bool check_dropped = __builtin_amdgcn_ballot_w64(risky) != 0;
+      bad_dirty = check_dropped;   // only a checking step writes flags
       wsync();
 #pragma unroll
       for (int m = 0; m < MQ; ++m) {
@@ -303,7 +306,7 @@ __global__ __launch_bounds__(256) void kanrnn_bwd_kernel(BwdArgs A) {
             for (int k = 0; k < cnt; ++k) sum += s_cg[wv][c0 + k];
           }
         }
-        if (s_bad[wv][ux ? u : kMaxF + i]) sum += __builtin_nanf("");
+        if (check_dropped && s_bad[wv][ux ? u : kMaxF + i]) sum += __builtin_nanf("");
         if (ux) {
           if (A.g_x) A.g_x[(row * a.T + t) * a.F + i] = sum;
         } else {
